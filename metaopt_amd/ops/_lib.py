@@ -1,0 +1,107 @@
+"""ctypes binding of ``libmopt_kernels.so`` (the gfx950 HIP kernels).
+
+The library is loaded after ``torch`` so that its ``libamdhip64.so.7`` dependency resolves to the
+HIP runtime torch already mapped (same SONAME): kernels then launch on torch's streams and are
+captured by torch's HIP graphs like any other work.
+
+``get_lib()`` raises loudly when the library is missing or fails to load while a GPU is present:
+GPU code paths never fall back silently to the PyTorch reference.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must be imported before the HIP library is dlopen'ed)
+
+from . import build as _build
+
+_LOCK = threading.Lock()
+_LIB = None
+ABI_VERSION = 3
+
+c_void_p = ctypes.c_void_p
+c_int = ctypes.c_int
+c_uint = ctypes.c_uint
+c_float = ctypes.c_float
+
+_SIGNATURES = {
+    "mopt_abi_version": ([], c_int),
+    "mopt_mlp_fwd": ([c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                      c_void_p, c_uint, c_int, c_int, c_void_p], c_int),
+    "mopt_mlp_fwd_ce": ([c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                         c_void_p, c_void_p, c_void_p, c_float, c_int, c_void_p], c_int),
+    "mopt_mlp_bwd": ([c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                      c_void_p, c_void_p, c_int, c_int, c_void_p], c_int),
+}
+
+_OPTIONAL_SIGNATURES: dict = {}
+
+
+def register_signatures(sigs: dict) -> None:
+    """Other op modules declare the C symbols they use (bound lazily on first load)."""
+    _OPTIONAL_SIGNATURES.update(sigs)
+    if _LIB is not None:
+        _bind(_LIB, sigs)
+
+
+def _bind(lib, sigs):
+    for name, (args, res) in sigs.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+
+
+class KernelLibraryError(RuntimeError):
+    pass
+
+
+def get_lib(build_if_missing: bool = True):
+    """Return the loaded kernel library (building it in-tree first if needed)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    with _LOCK:
+        if _LIB is not None:
+            return _LIB
+        path = _build.lib_path()
+        if build_if_missing and (os.environ.get("MOPT_REBUILD") or not path.exists()):
+            try:
+                _build.build()
+            except Exception as exc:  # pragma: no cover - exercised on hosts without hipcc
+                raise KernelLibraryError(f"cannot build {path}: {exc}") from exc
+        if not path.exists():
+            raise KernelLibraryError(f"HIP kernel library not found at {path}; run "
+                                     "`python -m metaopt_amd.ops.build`")
+        try:
+            lib = ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL)
+        except OSError as exc:
+            raise KernelLibraryError(f"failed to load {path}: {exc}") from exc
+        _bind(lib, _SIGNATURES)
+        _bind(lib, _OPTIONAL_SIGNATURES)
+        ver = lib.mopt_abi_version()
+        if ver != ABI_VERSION:
+            raise KernelLibraryError(f"{path} has ABI {ver}, expected {ABI_VERSION}; rebuild it")
+        _LIB = lib
+        return lib
+
+
+def check(err: int, what: str) -> None:
+    if err != 0:
+        raise RuntimeError(f"HIP launch of {what} failed with hipError_t {err}")
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def available() -> bool:
+    """True when a GPU is visible and the kernel library loads."""
+    if not torch.cuda.is_available():
+        return False
+    try:
+        get_lib()
+        return True
+    except KernelLibraryError:
+        return False

@@ -1,0 +1,116 @@
+"""In-tree build of the gfx950 HIP kernels into one shared library.
+
+The kernels are plain HIP C++ (no hipify, no CUDA shims) compiled by ``hipcc --offload-arch=gfx950``
+into ``metaopt_amd/ops/lib/libmopt_kernels.so``.  The library exposes a C ABI that
+:mod:`metaopt_amd.ops._lib` binds with ctypes, so the build needs neither torch headers nor a JIT
+cache: the ``.so`` lives in the source tree and travels with the repository snapshot to the GPU box.
+
+Each ``csrc/*.hip`` file is compiled to its own object (incremental: only stale objects rebuild) and
+the objects are linked once.  ``python -m metaopt_amd.ops.build [--force]`` rebuilds by hand.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+CSRC = HERE / "csrc"
+OUT_DIR = HERE / "lib"
+LIB_NAME = "libmopt_kernels.so"
+ARCH = os.environ.get("MOPT_OFFLOAD_ARCH", "gfx950")
+
+COMMON_FLAGS = [
+    f"--offload-arch={ARCH}",
+    "-O3",
+    "-std=c++17",
+    "-fPIC",
+    "-munsafe-fp-atomics",
+    "-Wno-unused-result",
+]
+
+
+def hipcc_path() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and Path(cand).exists():
+            return cand
+    raise RuntimeError("hipcc not found: the HIP kernels cannot be built")
+
+
+def lib_path() -> Path:
+    return OUT_DIR / LIB_NAME
+
+
+def _sources():
+    return sorted(CSRC.glob("*.hip"))
+
+
+def _headers():
+    return sorted(CSRC.glob("*.h"))
+
+
+def _needs(obj: Path, deps) -> bool:
+    if not obj.exists():
+        return True
+    t = obj.stat().st_mtime
+    return any(d.stat().st_mtime > t for d in deps)
+
+
+def _compile(src: Path, obj: Path, hipcc: str, extra) -> None:
+    cmd = [hipcc, *COMMON_FLAGS, *extra, "-c", str(src), "-o", str(obj)]
+    proc = subprocess.run(cmd, capture_output=True, text=True)
+    if proc.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src.name}:\n{proc.stderr}")
+
+
+def build(force: bool = False, verbose: bool = False, extra_flags=None) -> Path:
+    """Compile every ``csrc/*.hip`` for gfx950 and link ``libmopt_kernels.so``; returns its path."""
+    hipcc = hipcc_path()
+    OUT_DIR.mkdir(parents=True, exist_ok=True)
+    obj_dir = OUT_DIR / "obj"
+    obj_dir.mkdir(exist_ok=True)
+    extra = list(extra_flags or [])
+    headers = _headers()
+    jobs = []
+    objs = []
+    for src in _sources():
+        obj = obj_dir / (src.stem + ".o")
+        objs.append(obj)
+        if force or _needs(obj, [src, *headers, Path(__file__)]):
+            jobs.append((src, obj))
+    workers = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", "8"))))
+    if jobs:
+        with cf.ThreadPoolExecutor(workers) as ex:
+            futs = [ex.submit(_compile, s, o, hipcc, extra) for s, o in jobs]
+            for f in futs:
+                f.result()
+        if verbose:
+            print(f"[mopt build] compiled {[s.name for s, _ in jobs]}")
+    lib = lib_path()
+    if force or jobs or _needs(lib, objs):
+        tmp = lib.with_suffix(".so.tmp")
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp)]
+        proc = subprocess.run(cmd, capture_output=True, text=True)
+        if proc.returncode != 0:
+            raise RuntimeError(f"link failed:\n{proc.stderr}")
+        os.replace(tmp, lib)
+        if verbose:
+            print(f"[mopt build] linked {lib}")
+    return lib
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--force", action="store_true")
+    args = ap.parse_args(argv)
+    path = build(force=args.force, verbose=True)
+    print(path)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,92 @@
+// Shared device helpers for the metaopt_amd gfx950 (CDNA4) kernels.
+//
+// Conventions used by every kernel in this directory:
+//   * wave = 64 lanes, workgroups of 256 threads (4 waves), one wave per 16x16 MFMA fragment set;
+//   * bf16 tensors are stored as raw 16-bit words and moved 16 bytes per lane;
+//   * MFMA = v_mfma_f32_16x16x32_bf16.  Lane l holds A[row l&15][k 8(l>>4)..+7],
+//     B[k 8(l>>4)..+7][col l&15]; the f32 result C[row 4(l>>4)+r][col l&15] is register r.
+//   * LDS tiles are [rows][64 + 8] bf16 (144-byte rows): 16-byte row reads at a fixed column are
+//     conflict-free over 16 consecutive rows, and the rows stay 16-byte aligned for ds_read_b128
+//     and 8-byte aligned for ds_read_b64_tr_b16.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mopt {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint16_t bf16_t;  // storage type of a bf16 element
+
+constexpr int kLdsStride = 72;  // bf16 elements per LDS tile row (64 + 8 pad)
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+__device__ __forceinline__ float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;  // hipcc emits v_cvt_pk_bf16_f32 (RNE, NaN-preserving)
+  return __builtin_bit_cast(bf16_t, b);
+}
+
+__device__ __forceinline__ uint32_t pack2bf(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// ds_read_b64_tr_b16: the 16 lanes of a group each supply the address of row q = i>>2, columns
+// 4(i&3)..+3 of a 4x16 block; lane i receives column i of the 4 rows.
+__device__ __forceinline__ s16x4 lds_tr4(const bf16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
+}
+
+__device__ __forceinline__ bf16x8 cat_frag(s16x4 lo, s16x4 hi) {
+  s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ __forceinline__ bf16x8 lds_frag(const bf16_t* p) {
+  return __builtin_bit_cast(bf16x8, *(const uint4*)p);
+}
+
+// Bijective XCD-aware remap: consecutive work items land on the same XCD (blocks b, b+8, ... share
+// one L2 under round-robin dispatch), so the k-strips / n-tiles of one trial share its operands in
+// L2.  Speed only, never correctness.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  if (nwg <= 8) return bid;
+  const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
+
+// murmur3 finaliser: the counter-based RNG behind per-trial dropout.  Mirrored bit-for-bit by
+// metaopt_amd/ops/reference.py so the HIP path and the PyTorch reference draw identical masks.
+__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+
+__device__ __forceinline__ uint32_t rng_key(uint32_t seed, uint32_t layer, uint32_t step) {
+  return fmix32(seed ^ fmix32(layer * 0x9E3779B9u + step * 0x7FEB352Du + 0x632BE5ABu));
+}
+
+__device__ __forceinline__ float rng_uniform(uint32_t key, uint32_t idx) {
+  return (float)(fmix32(key ^ (idx * 0x9E3779B9u)) >> 8) * (1.0f / 16777216.0f);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+}  // namespace mopt

@@ -1,0 +1,535 @@
+// Population-batched MLP training kernels for MI355X (gfx950 / CDNA4).
+//
+// A "population" is P independent trials (hyper-parameter configurations) trained side by side.
+// Every trial owns its own weights, optimizer state, hyper-parameters and RNG stream; the widths
+// are ragged (per-trial), so every launch walks a work list of (trial-layer, tile) items built on
+// the host (metaopt_amd/ops/population.py) instead of a dense [P, ...] grid.  Dims are padded to
+// multiples of 64 with zero weights, which is exact: a zero-padded unit never receives gradient.
+//
+// Kernels (north-star inventory K1/K2/K4/K5/K6/K7):
+//   mlp_fwd_kernel     Y = dropout(relu(X W^T + b))            K1 + K7, bf16 MFMA, f32 accumulate
+//   mlp_fwd_ce_kernel  logits = X W^T + b; fused softmax-CE      K1 + K4 (loss, #correct, dLogits)
+//   mlp_bwd_opt_kernel one pass over W per step that computes    K2 + K5/K6
+//                        dX = dZ W      (-> masked dZ of the layer below),
+//                        dW = dZ^T X, db = colsum(dZ)
+//                      and applies the per-trial SGD-momentum / AdamW update in the epilogue, so
+//                      dW never touches HBM.  W is read once (f32 master) for both dX and the update.
+//
+// Memory-bound by design: per parameter and step the population moves 2 B (forward) + 18 B (fused
+// backward + SGD) through HBM; the MFMA work (6 * B FLOP per parameter) is a small fraction of the
+// chip's bf16 rate at B = 128.  See profiles/ for measured bandwidth.
+#include "common.h"
+
+using namespace mopt;
+
+extern "C" {
+
+// One (trial, layer) of the population; 64 bytes, mirrored by metaopt_amd/ops/population.py.
+struct MlpTL {
+  int32_t K;       // padded input features (multiple of 64)
+  int32_t N;       // padded output features (multiple of 64)
+  int32_t trial;   // population slot (index into the hyper-parameter table)
+  int32_t n_real;  // real outputs (classes of the CE layer)
+  int64_t w_off;   // W [N][K] row-major: offset into the f32 master / bf16 / optimizer buffers
+  int64_t b_off;   // bias [N]: offset into the f32 master / optimizer buffers
+  int64_t x_off;   // layer input  [rows][K] bf16: offset into the x buffer of the launch
+  int64_t y_off;   // layer output [rows][N] bf16: offset into act (forward) / grad (backward)
+  int64_t gx_off;  // dZ of the layer below [rows][K] bf16 in grad (backward), -1 if none
+  int64_t pad;
+};
+
+// Per-trial hyper-parameters; 32 bytes.  SGD: b1 = momentum.  AdamW: b1, b2, eps, t = step count.
+struct TrialHP {
+  float lr, b1, wd, drop, b2, eps;
+  uint32_t seed, t;
+};
+
+}  // extern "C"
+
+namespace {
+
+constexpr int BM = 128;  // rows (batch) per workgroup
+constexpr int BN = 64;   // output features per forward tile / per backward chunk
+constexpr int BK = 64;   // reduction step of the forward, width of a backward k-strip
+constexpr int LS = kLdsStride;
+
+enum FwdFlags { kRelu = 1, kDropout = 2, kWriteGrad = 4 };
+enum BwdFlags { kHasDx = 1, kInDropout = 2, kUpdateBias = 4 };
+enum Opt { kSGD = 0, kAdamW = 1 };
+
+// ----------------------------------------------------------------------------------------------
+// Forward GEMM core: acc[i][j] = X[row0 + 32*wave + 16i .., :] . W[n0 + 16j .., :]^T over all K.
+// Register-staged double buffering: the next K-step's global loads are issued before the current
+// step's MFMAs (T14), the LDS tile is written after the barrier.
+// ----------------------------------------------------------------------------------------------
+__device__ __forceinline__ void fwd_gemm(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
+                                         int K, bf16_t* As, bf16_t* Bs, f32x4 (&acc)[2][4]) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  uint4 ra[4], rb[2];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
+      ra[i] = *(const uint4*)(X + (size_t)r * K + k0 + ch * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
+      rb[i] = *(const uint4*)(W + (size_t)r * K + k0 + ch * 8);
+    }
+  };
+  gload(0);
+  for (int k0 = 0; k0 < K; k0 += BK) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
+      *(uint4*)(As + r * LS + ch * 8) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
+      *(uint4*)(Bs + r * LS + ch * 8) = rb[i];
+    }
+    __syncthreads();
+    if (k0 + BK < K) gload(k0 + BK);
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf16x8 a[2], b[4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = lds_frag(As + (wave * 32 + i * 16 + li) * LS + ks * 32 + g * 8);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = lds_frag(Bs + (j * 16 + li) * LS + ks * 32 + g * 8);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+}
+
+// Y[rows, n0:n0+64] = dropout(relu(X W^T + b)) for one (trial-layer, n-tile, 128-row block).
+__global__ __launch_bounds__(256) void mlp_fwd_kernel(const MlpTL* __restrict__ tls,
+                                                      const int2* __restrict__ work, int n_work,
+                                                      const bf16_t* __restrict__ xb,
+                                                      const float* __restrict__ p32,
+                                                      const bf16_t* __restrict__ p16,
+                                                      bf16_t* __restrict__ act,
+                                                      const TrialHP* __restrict__ hp,
+                                                      uint32_t step, int layer, int flags) {
+  __shared__ __attribute__((aligned(16))) bf16_t smem[(BM + BN) * LS];
+  bf16_t* As = smem;
+  bf16_t* Bs = smem + BM * LS;
+  const int2 wi = work[xcd_remap(blockIdx.x, n_work)];
+  const MlpTL tl = tls[wi.x];
+  const int K = tl.K, N = tl.N, n0 = wi.y * BN, row0 = blockIdx.y * BM;
+  const bf16_t* X = xb + tl.x_off + (size_t)row0 * K;
+  const bf16_t* W = p16 + tl.w_off + (size_t)n0 * K;
+
+  f32x4 acc[2][4];
+  fwd_gemm(X, W, K, As, Bs, acc);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, g = lane >> 4;
+  const float* bias = p32 + tl.b_off + n0;
+  const TrialHP h = hp[tl.trial];
+  const bool drop = (flags & kDropout) && h.drop > 0.f;
+  const float inv_keep = drop ? 1.f / (1.f - h.drop) : 1.f;
+  // The dropout stream is keyed by the trial's own step count (h.t), so a trial draws the same
+  // masks whichever slot it occupies and whenever it joined the population.
+  const uint32_t key = rng_key(h.seed, (uint32_t)layer, h.t + step);
+  bf16_t* Cs = smem;  // reuse As (the last K-step ended with a barrier)
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = j * 16 + li;
+    const float bj = bias[col];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wave * 32 + i * 16 + g * 4 + r;
+        float v = acc[i][j][r] + bj;
+        if (flags & kRelu) v = fmaxf(v, 0.f);
+        if (drop) {
+          const uint32_t idx = (uint32_t)((row0 + row) * N + n0 + col);
+          v = rng_uniform(key, idx) >= h.drop ? v * inv_keep : 0.f;
+        }
+        Cs[row * LS + col] = f2bf(v);
+      }
+  }
+  __syncthreads();
+  bf16_t* Y = act + tl.y_off + (size_t)row0 * N + n0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
+    *(uint4*)(Y + (size_t)r * N + ch * 8) = *(const uint4*)(Cs + r * LS + ch * 8);
+  }
+}
+
+// Output layer: logits = X W^T + b (N padded to 64 >= classes), fused softmax cross-entropy.
+// Writes dLogits = (softmax - onehot) * inv_b as bf16 (training) and accumulates the per-trial
+// loss sum and #correct (atomic, one add per wave).
+__global__ __launch_bounds__(256) void mlp_fwd_ce_kernel(const MlpTL* __restrict__ tls,
+                                                         const int2* __restrict__ work, int n_work,
+                                                         const bf16_t* __restrict__ xb,
+                                                         const float* __restrict__ p32,
+                                                         const bf16_t* __restrict__ p16,
+                                                         const int32_t* __restrict__ labels,
+                                                         bf16_t* __restrict__ grad,
+                                                         float* __restrict__ loss_out,
+                                                         float* __restrict__ correct_out,
+                                                         float inv_b, int flags) {
+  constexpr int CS = BN + 1;  // f32 logits row stride
+  constexpr int kSmemBytes = BM * CS * 4 > (BM + BN) * LS * 2 ? BM * CS * 4 : (BM + BN) * LS * 2;
+  __shared__ __attribute__((aligned(16))) char smem_raw[kSmemBytes];
+  bf16_t* As = (bf16_t*)smem_raw;
+  bf16_t* Bs = As + BM * LS;
+  float* Ls = (float*)smem_raw;
+
+  const int2 wi = work[xcd_remap(blockIdx.x, n_work)];
+  const MlpTL tl = tls[wi.x];
+  const int K = tl.K, N = tl.N, row0 = blockIdx.y * BM, C = tl.n_real;
+  const bf16_t* X = xb + tl.x_off + (size_t)row0 * K;
+  const bf16_t* W = p16 + tl.w_off;
+
+  f32x4 acc[2][4];
+  fwd_gemm(X, W, K, As, Bs, acc);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, g = lane >> 4;
+  const float* bias = p32 + tl.b_off;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = j * 16 + li;
+    const float bj = bias[col];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Ls[(wave * 32 + i * 16 + g * 4 + r) * CS + col] = acc[i][j][r] + bj;
+  }
+  __syncthreads();
+
+  float loss = 0.f, corr = 0.f;
+  if (tid < BM) {
+    const float* z = Ls + tid * CS;
+    const int y = labels[row0 + tid];
+    float m = -INFINITY;
+    int am = 0;
+    for (int c = 0; c < C; ++c)
+      if (z[c] > m) { m = z[c]; am = c; }
+    float s = 0.f;
+    for (int c = 0; c < C; ++c) s += __expf(z[c] - m);
+    const float lse = m + __logf(s);
+    loss = lse - z[y];
+    corr = (am == y) ? 1.f : 0.f;
+    if (flags & kWriteGrad) {
+      const float rs = 1.f / s;
+      bf16_t* dz = grad + tl.y_off + (size_t)(row0 + tid) * N;
+#pragma unroll
+      for (int ch = 0; ch < BN / 8; ++ch) {
+        uint32_t w4[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c0 = ch * 8 + 2 * e, c1 = c0 + 1;
+          const float g0 = c0 < C ? (__expf(z[c0] - m) * rs - (c0 == y ? 1.f : 0.f)) * inv_b : 0.f;
+          const float g1 = c1 < C ? (__expf(z[c1] - m) * rs - (c1 == y ? 1.f : 0.f)) * inv_b : 0.f;
+          w4[e] = pack2bf(g0, g1);
+        }
+        *(uint4*)(dz + ch * 8) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+      }
+    }
+  }
+  loss = wave_sum(loss);
+  corr = wave_sum(corr);
+  if (lane == 0 && wave < 2) {
+    atomicAdd(loss_out + tl.trial, loss);
+    atomicAdd(correct_out + tl.trial, corr);
+  }
+}
+
+// ----------------------------------------------------------------------------------------------
+// Fused backward + optimizer for one (trial-layer, 64-wide k-strip of W).  The workgroup holds the
+// X strip X[:, k0:k0+64] in LDS for the whole pass and walks W[:, k0:k0+64] in 64-row chunks:
+//   dX[:, strip] += dZ[:, chunk] . W[chunk, strip]        (A: dZ row reads, B: W^T by tr-reads)
+//   dW^T[strip, chunk] = X[:, strip]^T . dZ[:, chunk]     (A: X tr-reads held in VGPRs, B: dZ tr)
+//   W, M (, V) <- optimizer(W, M, dW)                       (dW^T C-layout = 4 consecutive k/lane)
+// One LDS image per operand serves both row reads and ds_read_b64_tr_b16 transposed reads.
+// ----------------------------------------------------------------------------------------------
+template <int OPT>
+__global__ __launch_bounds__(256) void mlp_bwd_opt_kernel(const MlpTL* __restrict__ tls,
+                                                          const int2* __restrict__ work, int n_work,
+                                                          const bf16_t* __restrict__ xb,
+                                                          bf16_t* __restrict__ grad,
+                                                          float* __restrict__ p32,
+                                                          bf16_t* __restrict__ p16,
+                                                          float* __restrict__ m32,
+                                                          float* __restrict__ v32,
+                                                          const TrialHP* __restrict__ hp, int flags) {
+  __shared__ __attribute__((aligned(16))) bf16_t smem[(2 * BM + BN) * LS + 2 * 4 * BN];
+  bf16_t* Xs = smem;
+  bf16_t* Zs = smem + BM * LS;
+  bf16_t* Ws = smem + 2 * BM * LS;
+  float* red = (float*)(smem + (2 * BM + BN) * LS);  // [4][64] bias partial sums
+
+  const int2 wi = work[xcd_remap(blockIdx.x, n_work)];
+  const MlpTL tl = tls[wi.x];
+  const int K = tl.K, N = tl.N, k0 = wi.y * BK;
+  const bf16_t* X = xb + tl.x_off;
+  const bf16_t* dZ = grad + tl.y_off;
+  float* W32 = p32 + tl.w_off;
+  float* M32 = m32 + tl.w_off;
+  bf16_t* W16 = p16 + tl.w_off;
+  const TrialHP h = hp[tl.trial];
+  const bool has_dx = flags & kHasDx;
+  const bool do_bias = (flags & kUpdateBias) && wi.y == 0;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, g = lane >> 4, q = li >> 2, pp = li & 3;
+  const int wk = wave >> 1, wn = wave & 1;
+
+  // Optimizer constants (uniform per workgroup).
+  float c1 = 1.f, c2 = 1.f;
+  if (OPT == kAdamW) {
+    const float t = (float)h.t;
+    c1 = h.lr / (1.f - __powf(h.b1, t));           // lr / bias_correction1
+    c2 = 1.f / sqrtf(1.f - __powf(h.b2, t));        // 1 / sqrt(bias_correction2)
+  }
+
+  // Stage X[:, k0:k0+64] (128 x 64 bf16).
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
+    *(uint4*)(Xs + r * LS + ch * 8) = *(const uint4*)(X + (size_t)r * K + k0 + ch * 8);
+  }
+  __syncthreads();
+
+  // A fragments of dW^T = X^T dZ for this wave's 32 k-rows, all 128 batch rows (kept in VGPRs).
+  bf16x8 xa[2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int c0 = 32 * wk + 16 * t + 4 * pp;
+      const s16x4 lo = lds_tr4(Xs + (32 * s + 8 * g + q) * LS + c0);
+      const s16x4 hi = lds_tr4(Xs + (32 * s + 8 * g + 4 + q) * LS + c0);
+      xa[t][s] = cat_frag(lo, hi);
+    }
+
+  f32x4 dx[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dx[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int nc = 0; nc < N; nc += BN) {
+    // ---- global loads: dZ chunk (row-major), master W and optimizer state in dW^T C-layout ----
+    uint4 zr[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
+      zr[i] = *(const uint4*)(dZ + (size_t)r * N + nc + ch * 8);
+    }
+    f32x4 w[2][2], m[2][2], v[2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const size_t o = (size_t)(nc + 32 * wn + 16 * u + li) * K + k0 + 32 * wk + 16 * t + 4 * g;
+        w[t][u] = *(const f32x4*)(W32 + o);
+        m[t][u] = *(const f32x4*)(M32 + o);
+        if (OPT == kAdamW) v[t][u] = *(const f32x4*)(v32 + tl.w_off + o);
+      }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
+      *(uint4*)(Zs + r * LS + ch * 8) = zr[i];
+    }
+    if (has_dx) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const f32x4 o = w[t][u];
+          *(uint2*)(Ws + (32 * wn + 16 * u + li) * LS + 32 * wk + 16 * t + 4 * g) =
+              make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
+        }
+    }
+    __syncthreads();
+
+    // ---- dX[:, strip] += dZ[:, chunk] . W[chunk, strip] ----
+    if (has_dx) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 a[2], b[4];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) a[i] = lds_frag(Zs + (32 * wave + 16 * i + li) * LS + 32 * s + 8 * g);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const s16x4 lo = lds_tr4(Ws + (32 * s + 8 * g + q) * LS + 16 * j + 4 * pp);
+          const s16x4 hi = lds_tr4(Ws + (32 * s + 8 * g + 4 + q) * LS + 16 * j + 4 * pp);
+          b[j] = cat_frag(lo, hi);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) dx[i][j] = mfma16(a[i], b[j], dx[i][j]);
+      }
+    }
+
+    // ---- dW^T[strip, chunk] = X^T dZ ----
+    f32x4 dw[2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) dw[t][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      bf16x8 bz[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int c0 = 32 * wn + 16 * u + 4 * pp;
+        const s16x4 lo = lds_tr4(Zs + (32 * s + 8 * g + q) * LS + c0);
+        const s16x4 hi = lds_tr4(Zs + (32 * s + 8 * g + 4 + q) * LS + c0);
+        bz[u] = cat_frag(lo, hi);
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) dw[t][u] = mfma16(xa[t][s], bz[u], dw[t][u]);
+    }
+
+    // ---- optimizer epilogue: register r of dw[t][u] is dW[n][k + r] ----
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const size_t o = (size_t)(nc + 32 * wn + 16 * u + li) * K + k0 + 32 * wk + 16 * t + 4 * g;
+        f32x4 wv = w[t][u], mv = m[t][u], vv;
+        if (OPT == kAdamW) vv = v[t][u];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float gr = dw[t][u][r];
+          if (OPT == kSGD) {
+            const float gg = gr + h.wd * wv[r];
+            mv[r] = h.b1 * mv[r] + gg;
+            wv[r] = wv[r] - h.lr * mv[r];
+          } else {
+            wv[r] = wv[r] * (1.f - h.lr * h.wd);
+            mv[r] = h.b1 * mv[r] + (1.f - h.b1) * gr;
+            vv[r] = h.b2 * vv[r] + (1.f - h.b2) * gr * gr;
+            wv[r] = wv[r] - c1 * mv[r] / (sqrtf(vv[r]) * c2 + h.eps);
+          }
+        }
+        *(f32x4*)(W32 + o) = wv;
+        *(f32x4*)(M32 + o) = mv;
+        if (OPT == kAdamW) *(f32x4*)(v32 + tl.w_off + o) = vv;
+        *(uint2*)(W16 + o) = make_uint2(pack2bf(wv[0], wv[1]), pack2bf(wv[2], wv[3]));
+      }
+
+    // ---- bias: db[n] = sum_b dZ[b][n]; only the k-strip-0 workgroup owns the bias ----
+    if (do_bias) {
+      const int col = tid & 63, part = tid >> 6;
+      float s = 0.f;
+      for (int r = part * 32; r < part * 32 + 32; ++r) s += bf2f(Zs[r * LS + col]);
+      red[part * 64 + col] = s;
+      __syncthreads();
+      if (tid < 64) {
+        const float gb = red[tid] + red[64 + tid] + red[128 + tid] + red[192 + tid];
+        float* bp = p32 + tl.b_off + nc + tid;
+        float* bm = m32 + tl.b_off + nc + tid;
+        float bw = *bp, mb = *bm;
+        if (OPT == kSGD) {
+          mb = h.b1 * mb + gb;
+          bw = bw - h.lr * mb;
+        } else {
+          float* bv = v32 + tl.b_off + nc + tid;
+          float vb = *bv;
+          mb = h.b1 * mb + (1.f - h.b1) * gb;
+          vb = h.b2 * vb + (1.f - h.b2) * gb * gb;
+          bw = bw - c1 * mb / (sqrtf(vb) * c2 + h.eps);
+          *bv = vb;
+        }
+        *bp = bw;
+        *bm = mb;
+      }
+    }
+    __syncthreads();
+  }
+
+  if (!has_dx) return;
+  // ---- dZ of the layer below: dX * relu'(.) * dropout mask, both read off X (X > 0) ----
+  const float inv_keep = ((flags & kInDropout) && h.drop > 0.f) ? 1.f / (1.f - h.drop) : 1.f;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 32 * wave + 16 * i + 4 * g + r, col = 16 * j + li;
+        const float xv = bf2f(Xs[row * LS + col]);
+        Zs[row * LS + col] = f2bf(xv > 0.f ? dx[i][j][r] * inv_keep : 0.f);
+      }
+  __syncthreads();
+  bf16_t* GX = grad + tl.gx_off + k0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
+    *(uint4*)(GX + (size_t)r * K + ch * 8) = *(const uint4*)(Zs + r * LS + ch * 8);
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+// C ABI (loaded with ctypes by metaopt_amd/ops/_lib.py).  Every launcher returns a hipError_t.
+// ------------------------------------------------------------------------------------------------
+extern "C" {
+
+int mopt_abi_version() { return 3; }
+
+int mopt_mlp_fwd(const void* tls, const void* work, int n_work, int n_rowblocks, const void* xb,
+                 const void* p32, const void* p16, void* act, const void* hp, unsigned step,
+                 int layer, int flags, void* stream) {
+  if (n_work <= 0) return 0;
+  hipLaunchKernelGGL(mlp_fwd_kernel, dim3(n_work, n_rowblocks), dim3(256), 0, (hipStream_t)stream,
+                     (const MlpTL*)tls, (const int2*)work, n_work, (const bf16_t*)xb,
+                     (const float*)p32, (const bf16_t*)p16, (bf16_t*)act, (const TrialHP*)hp, step,
+                     layer, flags);
+  return (int)hipGetLastError();
+}
+
+int mopt_mlp_fwd_ce(const void* tls, const void* work, int n_work, int n_rowblocks, const void* xb,
+                    const void* p32, const void* p16, const void* labels, void* grad, void* loss,
+                    void* correct, float inv_b, int flags, void* stream) {
+  if (n_work <= 0) return 0;
+  hipLaunchKernelGGL(mlp_fwd_ce_kernel, dim3(n_work, n_rowblocks), dim3(256), 0,
+                     (hipStream_t)stream, (const MlpTL*)tls, (const int2*)work, n_work,
+                     (const bf16_t*)xb, (const float*)p32, (const bf16_t*)p16,
+                     (const int32_t*)labels, (bf16_t*)grad, (float*)loss, (float*)correct, inv_b,
+                     flags);
+  return (int)hipGetLastError();
+}
+
+int mopt_mlp_bwd(const void* tls, const void* work, int n_work, const void* xb, void* grad,
+                 void* p32, void* p16, void* m32, void* v32, const void* hp, int opt, int flags,
+                 void* stream) {
+  if (n_work <= 0) return 0;
+  if (opt == kAdamW) {
+    hipLaunchKernelGGL(mlp_bwd_opt_kernel<kAdamW>, dim3(n_work), dim3(256), 0, (hipStream_t)stream,
+                       (const MlpTL*)tls, (const int2*)work, n_work, (const bf16_t*)xb,
+                       (bf16_t*)grad, (float*)p32, (bf16_t*)p16, (float*)m32, (float*)v32,
+                       (const TrialHP*)hp, flags);
+  } else {
+    hipLaunchKernelGGL(mlp_bwd_opt_kernel<kSGD>, dim3(n_work), dim3(256), 0, (hipStream_t)stream,
+                       (const MlpTL*)tls, (const int2*)work, n_work, (const bf16_t*)xb,
+                       (bf16_t*)grad, (float*)p32, (bf16_t*)p16, (float*)m32, (float*)v32,
+                       (const TrialHP*)hp, flags);
+  }
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

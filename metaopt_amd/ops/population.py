@@ -1,0 +1,493 @@
+"""Device-resident population of MLP trials trained side by side (north-star configs 1 and 2).
+
+:class:`PopulationMLP` owns flat device buffers for ``capacity`` trial *slots*:
+
+* ``p32`` f32 master weights, ``p16`` their bf16 copy (forward operand), ``m32``/``v32`` optimizer
+  state -- every slot a fixed-size region sized for ``max_width`` (288 GB of HBM makes the
+  per-slot worst case cheap, and fixed regions make slot replacement, ASHA resume and PBT exploit
+  plain region copies);
+* ``act``/``grad`` bf16 activations and their gradients ([rows][N_l] per slot and layer);
+* a hyper-parameter table (per-slot lr / momentum / weight decay / dropout / seed / step).
+
+A trial with hidden width ``w`` uses padded dims (multiples of 64) inside its region; padding is
+zero and stays zero (a zero-padded unit never receives gradient), so ragged widths cost only their
+own padded FLOPs.  Each layer is one launch over a work list of (trial-layer, tile) items: the
+forward (K1, K7), fused softmax-CE (K4) and the fused backward + SGD/AdamW update (K2, K5, K6)
+kernels of ``csrc/pop_mlp.hip``.
+
+Backends: ``"hip"`` (gfx950 kernels, the only GPU path; never falls back silently) and
+``"torch"`` (the fp32 reference of :mod:`metaopt_amd.ops.reference`, used on CPU-only hosts).
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from . import reference as ref
+
+TL_DTYPE = np.dtype([("K", "<i4"), ("N", "<i4"), ("trial", "<i4"), ("n_real", "<i4"),
+                     ("w_off", "<i8"), ("b_off", "<i8"), ("x_off", "<i8"), ("y_off", "<i8"),
+                     ("gx_off", "<i8"), ("pad", "<i8")])
+HP_DTYPE = np.dtype([("lr", "<f4"), ("b1", "<f4"), ("wd", "<f4"), ("drop", "<f4"),
+                     ("b2", "<f4"), ("eps", "<f4"), ("seed", "<u4"), ("t", "<u4")])
+assert TL_DTYPE.itemsize == 64 and HP_DTYPE.itemsize == 32
+
+TILE = 64
+FWD_RELU, FWD_DROPOUT, FWD_WRITE_GRAD = 1, 2, 4
+BWD_HAS_DX, BWD_IN_DROPOUT, BWD_UPDATE_BIAS = 1, 2, 4
+OPTIMIZERS = {"sgd": 0, "adamw": 1}
+
+
+def pad64(n: int) -> int:
+    return (int(n) + TILE - 1) // TILE * TILE
+
+
+@dataclass
+class MemberConfig:
+    """Hyper-parameters of one population member (one trial)."""
+
+    width: int
+    lr: float
+    momentum: float = 0.9          # SGD momentum, or AdamW beta1
+    weight_decay: float = 0.0
+    dropout: float = 0.0
+    seed: int = 0
+    beta2: float = 0.999
+    eps: float = 1e-8
+
+    def to_dict(self) -> dict:
+        return dataclasses.asdict(self)
+
+
+class PopulationMLP:
+    """``capacity`` MLP trials (``n_hidden`` ReLU layers of per-trial width) on one device."""
+
+    def __init__(self, capacity: int, in_features: int = 784, num_classes: int = 10,
+                 max_width: int = 1024, n_hidden: int = 3, batch_size: int = 128,
+                 eval_batch: int = 1024, optimizer: str = "sgd", device=None,
+                 backend: Optional[str] = None, emulate_bf16: bool = True):
+        if optimizer not in OPTIMIZERS:
+            raise ValueError(f"optimizer must be one of {sorted(OPTIMIZERS)}")
+        if num_classes > TILE:
+            raise ValueError("the fused CE epilogue supports at most 64 classes")
+        self.device = torch.device(device) if device is not None else (
+            torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
+        if backend is None:
+            backend = "hip" if self.device.type == "cuda" else "torch"
+        if backend == "hip":
+            if self.device.type != "cuda":
+                raise ValueError("the hip backend needs a GPU device")
+            from . import _lib
+            self._lib = _lib.get_lib()  # raises loudly: no silent fallback on a GPU box
+        self.backend = backend
+        if backend == "hip" and batch_size != 128:
+            raise ValueError("the fused backward kernel is tiled for 128-row batches")
+        if batch_size % 128 or eval_batch % 128:
+            raise ValueError("batch sizes must be multiples of 128")
+        self.capacity = int(capacity)
+        self.in_features = int(in_features)
+        self.num_classes = int(num_classes)
+        self.max_width = int(max_width)
+        self.n_hidden = int(n_hidden)
+        self.L = self.n_hidden + 1
+        self.batch_size = int(batch_size)
+        self.eval_batch = int(eval_batch)
+        self.optimizer = optimizer
+        self.emulate_bf16 = emulate_bf16
+        self.K0 = pad64(in_features)
+
+        dims_max = self.layer_dims(self.max_width)
+        self.slot_params = sum(pad64(k * n) + pad64(n) for k, n in dims_max)
+        self.nmax = [n for _, n in dims_max]
+        self.act_row = sum(self.nmax)
+        dev = self.device
+        total = self.capacity * self.slot_params
+        self.p32 = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.p16 = torch.zeros(total, dtype=torch.bfloat16, device=dev)
+        self.m32 = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.v32 = (torch.zeros(total, dtype=torch.float32, device=dev) if optimizer == "adamw"
+                    else torch.zeros(1, dtype=torch.float32, device=dev))
+        self.act = torch.zeros(self.capacity * self.batch_size * self.act_row,
+                               dtype=torch.bfloat16, device=dev)
+        self.grad = torch.zeros_like(self.act)
+        self.act_eval = torch.zeros(self.capacity * self.eval_batch * self.act_row,
+                                    dtype=torch.bfloat16, device=dev)
+        self.loss = torch.zeros(self.capacity, dtype=torch.float32, device=dev)
+        self.correct = torch.zeros(self.capacity, dtype=torch.float32, device=dev)
+        self.hp = np.zeros(self.capacity, dtype=HP_DTYPE)
+        self.hp_dev = torch.zeros(self.capacity * HP_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+        self.members: List[Optional[MemberConfig]] = [None] * self.capacity
+        self._dirty = True
+        self._tables: Dict[str, dict] = {}
+
+    # ------------------------------------------------------------------ layout
+    def layer_dims(self, width: int):
+        """Padded (K, N) per layer for a trial of hidden width ``width``."""
+        wp = pad64(width)
+        if self.n_hidden == 0:
+            return [(self.K0, TILE)]
+        dims = [(self.K0, wp)]
+        dims += [(wp, wp)] * (self.n_hidden - 1)
+        dims.append((wp, TILE))
+        return dims
+
+    def real_dims(self, width: int):
+        if self.n_hidden == 0:
+            return [(self.in_features, self.num_classes)]
+        dims = [(self.in_features, width)]
+        dims += [(width, width)] * (self.n_hidden - 1)
+        dims.append((width, self.num_classes))
+        return dims
+
+    def param_offsets(self, width: int):
+        """[(w_off, b_off)] per layer, relative to the slot base."""
+        offs, o = [], 0
+        for k, n in self.layer_dims(width):
+            offs.append((o, o + pad64(k * n)))
+            o += pad64(k * n) + pad64(n)
+        return offs
+
+    def slot_base(self, slot: int) -> int:
+        return slot * self.slot_params
+
+    def n_params(self, slot: int) -> int:
+        """Real (unpadded) parameter count of the member in ``slot``."""
+        cfg = self.members[slot]
+        return sum(k * n + n for k, n in self.real_dims(cfg.width))
+
+    def padded_params(self, slot: int) -> int:
+        cfg = self.members[slot]
+        return sum(k * n + n for k, n in self.layer_dims(cfg.width))
+
+    def flops_per_step(self, slot: int) -> int:
+        """Padded MFMA FLOPs of one train step (fwd + dX + dW) of the member in ``slot``."""
+        cfg = self.members[slot]
+        f = 0
+        for l, (k, n) in enumerate(self.layer_dims(cfg.width)):
+            f += 2 * self.batch_size * k * n * (3 if l > 0 else 2)
+        return f
+
+    def bytes_per_step(self, slot: int) -> int:
+        """HBM bytes per step for parameters/state of ``slot`` (fwd bf16 + fused bwd/update)."""
+        per = 2 + (18 if self.optimizer == "sgd" else 26)
+        return per * self.padded_params(slot)
+
+    # ------------------------------------------------------------------ members
+    def active_slots(self) -> List[int]:
+        return [i for i, m in enumerate(self.members) if m is not None]
+
+    def free_slots(self) -> List[int]:
+        return [i for i, m in enumerate(self.members) if m is None]
+
+    def _write_hp(self, slot: int, cfg: MemberConfig, t: int) -> None:
+        self.hp[slot] = (cfg.lr, cfg.momentum, cfg.weight_decay, cfg.dropout, cfg.beta2, cfg.eps,
+                         cfg.seed & 0xFFFFFFFF, t)
+
+    def _upload_hp(self) -> None:
+        host = torch.from_numpy(self.hp.view(np.uint8).copy())
+        self.hp_dev.copy_(host, non_blocking=False)
+
+    def set_member(self, slot: int, cfg: MemberConfig, init: bool = True) -> None:
+        """Place ``cfg`` in ``slot``; with ``init`` draw fresh weights (torch.nn.Linear init)."""
+        if cfg.width > self.max_width or cfg.width < 1:
+            raise ValueError(f"width {cfg.width} outside [1, {self.max_width}]")
+        if not (0.0 <= cfg.dropout < 1.0):
+            raise ValueError("dropout must be in [0, 1)")
+        self.members[slot] = cfg
+        self._write_hp(slot, cfg, 0)
+        if init:
+            self._init_slot(slot)
+        self._dirty = True
+
+    def update_hparams(self, slot: int, **changes) -> None:
+        """Change hyper-parameters of a live member without touching its weights (PBT explore)."""
+        cfg = dataclasses.replace(self.members[slot], **changes)
+        if cfg.width != self.members[slot].width:
+            raise ValueError("width cannot change in place")
+        t = int(self.hp[slot]["t"])
+        self.members[slot] = cfg
+        self._write_hp(slot, cfg, t)
+        self._dirty = True
+
+    def remove_member(self, slot: int) -> None:
+        self.members[slot] = None
+        self.hp[slot] = np.zeros((), dtype=HP_DTYPE)
+        self._dirty = True
+
+    def steps_done(self, slot: int) -> int:
+        return int(self.hp[slot]["t"])
+
+    def _region(self, slot: int):
+        b = self.slot_base(slot)
+        return slice(b, b + self.slot_params)
+
+    def _init_slot(self, slot: int) -> None:
+        cfg = self.members[slot]
+        reg = self._region(slot)
+        self.p32[reg].zero_()
+        self.m32[reg].zero_()
+        if self.optimizer == "adamw":
+            self.v32[reg].zero_()
+        gen = torch.Generator(device=self.device)
+        gen.manual_seed(int(cfg.seed) & 0x7FFFFFFFFFFFFFFF)
+        base = self.slot_base(slot)
+        for (k, n), (kr, nr), (wo, bo) in zip(self.layer_dims(cfg.width), self.real_dims(cfg.width),
+                                              self.param_offsets(cfg.width)):
+            bound = 1.0 / math.sqrt(kr)
+            w = self.p32[base + wo: base + wo + n * k].view(n, k)
+            w[:nr, :kr] = (torch.rand(nr, kr, generator=gen, device=self.device) * 2 - 1) * bound
+            b = self.p32[base + bo: base + bo + n]
+            b[:nr] = (torch.rand(nr, generator=gen, device=self.device) * 2 - 1) * bound
+        self.p16[reg] = self.p32[reg].to(torch.bfloat16)
+
+    def layer_views(self, slot: int, buf: torch.Tensor = None):
+        """[(W [N,K], b [N])] views of ``buf`` (default: f32 master) for the member in ``slot``."""
+        buf = self.p32 if buf is None else buf
+        cfg = self.members[slot]
+        base = self.slot_base(slot)
+        out = []
+        for (k, n), (wo, bo) in zip(self.layer_dims(cfg.width), self.param_offsets(cfg.width)):
+            out.append((buf[base + wo: base + wo + n * k].view(n, k), buf[base + bo: base + bo + n]))
+        return out
+
+    # ------------------------------------------------------------------ checkpoints (device)
+    def slot_state(self, slot: int, to_cpu: bool = False) -> dict:
+        """Device checkpoint of a member: config, step count, weights and optimizer state."""
+        reg = self._region(slot)
+        mv = (lambda t: t.detach().cpu().clone()) if to_cpu else (lambda t: t.detach().clone())
+        st = {"config": self.members[slot].to_dict(), "t": int(self.hp[slot]["t"]),
+              "p32": mv(self.p32[reg]), "m32": mv(self.m32[reg]), "optimizer": self.optimizer}
+        if self.optimizer == "adamw":
+            st["v32"] = mv(self.v32[reg])
+        return st
+
+    def load_slot_state(self, slot: int, state: dict) -> None:
+        cfg = MemberConfig(**state["config"])
+        self.members[slot] = cfg
+        self._write_hp(slot, cfg, int(state["t"]))
+        reg = self._region(slot)
+        self.p32[reg].copy_(state["p32"])
+        self.m32[reg].copy_(state["m32"])
+        if self.optimizer == "adamw":
+            self.v32[reg].copy_(state["v32"])
+        self.p16[reg] = self.p32[reg].to(torch.bfloat16)
+        self._dirty = True
+
+    def copy_member(self, src: int, dst: int, **hp_changes) -> None:
+        """PBT exploit inside one device: dst <- src (weights, optimizer state, step count)."""
+        rs, rd = self._region(src), self._region(dst)
+        self.p32[rd].copy_(self.p32[rs])
+        self.p16[rd].copy_(self.p16[rs])
+        self.m32[rd].copy_(self.m32[rs])
+        if self.optimizer == "adamw":
+            self.v32[rd].copy_(self.v32[rs])
+        cfg = dataclasses.replace(self.members[src], **hp_changes)
+        self.members[dst] = cfg
+        self._write_hp(dst, cfg, int(self.hp[src]["t"]))
+        self._dirty = True
+
+    # ------------------------------------------------------------------ tables
+    def _build_tables(self, rows: int) -> dict:
+        L = self.L
+        tl = np.zeros(self.capacity * L, dtype=TL_DTYPE)
+        fwd: List[list] = [[] for _ in range(L)]
+        bwd: List[list] = [[] for _ in range(L)]
+        act_slot = rows * self.act_row
+        layer_base = np.concatenate([[0], np.cumsum(self.nmax)]) * rows
+        for s in self.active_slots():
+            cfg = self.members[s]
+            base = self.slot_base(s)
+            for l, ((k, n), (wo, bo)) in enumerate(zip(self.layer_dims(cfg.width),
+                                                       self.param_offsets(cfg.width))):
+                i = s * L + l
+                y_off = s * act_slot + int(layer_base[l])
+                prev = s * act_slot + int(layer_base[l - 1]) if l > 0 else 0
+                n_real = self.num_classes if l == L - 1 else n
+                tl[i] = (k, n, s, n_real, base + wo, base + bo, prev, y_off,
+                         prev if l > 0 else -1, 0)
+                fwd[l].extend((i, t) for t in range(n // TILE))
+                bwd[l].extend((i, t) for t in range(k // TILE))
+        out = {"tl_np": tl, "rows": rows}
+        if self.device.type == "cuda":
+            out["tl"] = torch.from_numpy(tl.view(np.uint8).copy()).to(self.device)
+            out["fwd"] = [torch.tensor(w, dtype=torch.int32).reshape(-1, 2).to(self.device)
+                          for w in fwd]
+            out["bwd"] = [torch.tensor(w, dtype=torch.int32).reshape(-1, 2).to(self.device)
+                          for w in bwd]
+        out["n_fwd"] = [len(w) for w in fwd]
+        out["n_bwd"] = [len(w) for w in bwd]
+        return out
+
+    def _refresh(self) -> None:
+        if not self._dirty:
+            return
+        self._tables = {"train": self._build_tables(self.batch_size),
+                        "eval": self._build_tables(self.eval_batch)}
+        if self.device.type == "cuda":
+            self._upload_hp()
+        self._active_t = torch.tensor(
+            [1 if m is not None else 0 for m in self.members], dtype=torch.int32, device=self.device)
+        self._dirty = False
+
+    # ------------------------------------------------------------------ training
+    def train_step(self, x: torch.Tensor, y: torch.Tensor) -> None:
+        """One SGD/AdamW step of every active member on the shared minibatch (x [B,K0] bf16, y [B])."""
+        self._refresh()
+        if x.shape != (self.batch_size, self.K0):
+            raise ValueError(f"x must be [{self.batch_size}, {self.K0}] (padded), got {tuple(x.shape)}")
+        act_mask = np.array([m is not None for m in self.members])
+        self.hp["t"][act_mask] += 1
+        if self.backend == "hip":
+            self._hp_increment()
+            self._train_step_hip(x, y)
+        else:
+            self._train_step_torch(x, y)
+
+    def _hp_increment(self) -> None:
+        # device copy of the step counters: hp_dev viewed as int32 [capacity, 8], column 7 = t
+        self.hp_dev.view(torch.int32).view(self.capacity, 8)[:, 7].add_(self._active_t)
+
+    def _train_step_hip(self, x, y) -> None:
+        from ._lib import check, stream_ptr
+        lib, tb, L = self._lib, self._tables["train"], self.L
+        stream = stream_ptr(self.device)
+        self.loss.zero_()
+        self.correct.zero_()
+        drop = any(m is not None and m.dropout > 0 for m in self.members)
+        xb = x.contiguous()
+        for l in range(L - 1):
+            src = xb if l == 0 else self.act
+            check(lib.mopt_mlp_fwd(tb["tl"].data_ptr(), tb["fwd"][l].data_ptr(), tb["n_fwd"][l], 1,
+                                   src.data_ptr(), self.p32.data_ptr(), self.p16.data_ptr(),
+                                   self.act.data_ptr(), self.hp_dev.data_ptr(), 0, l,
+                                   FWD_RELU | (FWD_DROPOUT if drop else 0), stream), "mlp_fwd")
+        src = xb if L == 1 else self.act
+        check(lib.mopt_mlp_fwd_ce(tb["tl"].data_ptr(), tb["fwd"][L - 1].data_ptr(),
+                                  tb["n_fwd"][L - 1], 1, src.data_ptr(), self.p32.data_ptr(),
+                                  self.p16.data_ptr(), y.data_ptr(), self.grad.data_ptr(),
+                                  self.loss.data_ptr(), self.correct.data_ptr(),
+                                  1.0 / self.batch_size, FWD_WRITE_GRAD, stream), "mlp_fwd_ce")
+        opt = OPTIMIZERS[self.optimizer]
+        for l in range(L - 1, -1, -1):
+            src = xb if l == 0 else self.act
+            flags = BWD_UPDATE_BIAS
+            if l > 0:
+                flags |= BWD_HAS_DX | (BWD_IN_DROPOUT if drop else 0)
+            check(lib.mopt_mlp_bwd(tb["tl"].data_ptr(), tb["bwd"][l].data_ptr(), tb["n_bwd"][l],
+                                   src.data_ptr(), self.grad.data_ptr(), self.p32.data_ptr(),
+                                   self.p16.data_ptr(), self.m32.data_ptr(), self.v32.data_ptr(),
+                                   self.hp_dev.data_ptr(), opt, flags, stream), "mlp_bwd")
+
+    def _train_step_torch(self, x, y) -> None:
+        self.loss.zero_()
+        self.correct.zero_()
+        em = self.emulate_bf16
+        xf = x.float()
+        for s in self.active_slots():
+            cfg = self.members[s]
+            t = int(self.hp[s]["t"])
+            layers = self.layer_views(s)
+            mom = self.layer_views(s, self.m32)
+            acts = [xf]
+            a = xf
+            for l in range(self.L - 1):
+                w, b = layers[l]
+                a = ref.hidden_fwd(a, w, b, cfg.dropout, cfg.seed, l, t, emulate_bf16=em)
+                acts.append(a)
+            w, b = layers[-1]
+            wq = ref.bf16_round(w) if em else w
+            logits = a @ wq.t() + b
+            ls, cs, dz = ref.softmax_ce(logits, y, self.num_classes, 1.0 / self.batch_size, em)
+            self.loss[s] = ls
+            self.correct[s] = cs
+            inv_keep = ref._inv_keep(cfg.dropout) if cfg.dropout > 0 else 1.0
+            for l in range(self.L - 1, -1, -1):
+                w, b = layers[l]
+                a_in = acts[l]
+                dw = dz.t() @ a_in
+                db = dz.sum(0)
+                if l > 0:
+                    wq = ref.bf16_round(w) if em else w
+                    dx = dz @ wq
+                    dz_prev = torch.where(a_in > 0, dx * inv_keep, torch.zeros_like(dx))
+                    dz_prev = ref.bf16_round(dz_prev) if em else dz_prev
+                mw, mb = mom[l]
+                if self.optimizer == "sgd":
+                    ref.sgd_update(w, mw, dw, cfg.lr, cfg.momentum, cfg.weight_decay)
+                    ref.sgd_update(b, mb, db, cfg.lr, cfg.momentum, 0.0)
+                else:
+                    vw, vb = self.layer_views(s, self.v32)[l]
+                    ref.adamw_update(w, mw, vw, dw, cfg.lr, cfg.momentum, cfg.beta2, cfg.eps,
+                                     cfg.weight_decay, t)
+                    ref.adamw_update(b, mb, vb, db, cfg.lr, cfg.momentum, cfg.beta2, cfg.eps, 0.0, t)
+                if l > 0:
+                    dz = dz_prev
+            reg = self._region(s)
+            self.p16[reg] = self.p32[reg].to(torch.bfloat16)
+
+    # ------------------------------------------------------------------ evaluation
+    @torch.no_grad()
+    def evaluate(self, x: torch.Tensor, y: torch.Tensor):
+        """Mean loss and accuracy per slot (numpy [capacity]; NaN for empty slots)."""
+        self._refresh()
+        rows = x.shape[0]
+        if rows % 128 or rows > self.eval_batch:
+            raise ValueError(f"eval rows must be a multiple of 128 and <= {self.eval_batch}")
+        if self.backend == "hip":
+            from ._lib import check, stream_ptr
+            lib, tb, L = self._lib, self._tables["eval"], self.L
+            stream = stream_ptr(self.device)
+            self.loss.zero_()
+            self.correct.zero_()
+            xb = x.contiguous()
+            rb = rows // 128
+            for l in range(L - 1):
+                src = xb if l == 0 else self.act_eval
+                check(lib.mopt_mlp_fwd(tb["tl"].data_ptr(), tb["fwd"][l].data_ptr(), tb["n_fwd"][l],
+                                       rb, src.data_ptr(), self.p32.data_ptr(), self.p16.data_ptr(),
+                                       self.act_eval.data_ptr(), self.hp_dev.data_ptr(), 0, l,
+                                       FWD_RELU, stream), "mlp_fwd(eval)")
+            src = xb if L == 1 else self.act_eval
+            check(lib.mopt_mlp_fwd_ce(tb["tl"].data_ptr(), tb["fwd"][L - 1].data_ptr(),
+                                      tb["n_fwd"][L - 1], rb, src.data_ptr(), self.p32.data_ptr(),
+                                      self.p16.data_ptr(), y.data_ptr(), self.grad.data_ptr(),
+                                      self.loss.data_ptr(), self.correct.data_ptr(), 1.0, 0, stream),
+                  "mlp_fwd_ce(eval)")
+            loss = self.loss.float().cpu().numpy() / rows
+            acc = self.correct.float().cpu().numpy() / rows
+        else:
+            loss = np.zeros(self.capacity, dtype=np.float32)
+            acc = np.zeros(self.capacity, dtype=np.float32)
+            xf = x.float()
+            em = self.emulate_bf16
+            for s in self.active_slots():
+                cfg = self.members[s]
+                layers = self.layer_views(s)
+                a = xf
+                for l in range(self.L - 1):
+                    w, b = layers[l]
+                    a = ref.hidden_fwd(a, w, b, cfg.dropout, cfg.seed, l, 0, emulate_bf16=em,
+                                       train=False)
+                w, b = layers[-1]
+                wq = ref.bf16_round(w) if em else w
+                ls, cs, _ = ref.softmax_ce(a @ wq.t() + b, y, self.num_classes, 1.0, em)
+                loss[s] = float(ls) / rows
+                acc[s] = float(cs) / rows
+        for s in range(self.capacity):
+            if self.members[s] is None:
+                loss[s] = np.nan
+                acc[s] = np.nan
+        return loss, acc
+
+    def train_loss(self) -> np.ndarray:
+        """Mean training loss of the last step per slot."""
+        out = self.loss.float().cpu().numpy() / self.batch_size
+        for s in range(self.capacity):
+            if self.members[s] is None:
+                out[s] = np.nan
+        return out
