@@ -1,0 +1,209 @@
+"""Asynchronous Successive Halving (reference: ``src/orion/algo/asha.py:36-365``).
+
+Li et al., "A System for Massively Parallel Hyperparameter Tuning" (arXiv:1810.05934).
+
+Same rung/bracket logic as the reference -- budgets ``logspace(log_b(min), log_b(max), n_rungs,
+base=b)``, promotion of the top ``len(rung) // b`` completed points of the highest promotable rung,
+softmax-of-size bracket choice for new samples, opt-out (``None``) once every bracket is filled --
+with three changes made for device populations:
+
+* ``suggest(num)`` supports ``num > 1`` (the reference raises): a population asks for hundreds
+  of points at once.  Each suggested point is registered immediately as *pending* (objective
+  None) in its rung, so one call never promotes the same point twice and fills count pending
+  work exactly like the reference counts lies;
+* ``Bracket.is_done`` returns a bool (the reference returns ``len(rung)``, quirk 4);
+* the full rung state round-trips through ``state_dict``/``set_state`` when ``full=True`` is
+  requested (device checkpoints resume the search without replaying trials).
+"""
+from __future__ import annotations
+
+import copy
+import hashlib
+import logging
+
+import numpy
+
+from ..space.dims import Fidelity
+from .base import ALGORITHMS, BaseAlgorithm
+
+log = logging.getLogger(__name__)
+
+SPACE_ERROR = ("ASHA cannot be used if space does not contain a fidelity dimension.")
+
+
+def _is_fidelity(dim) -> bool:
+    return isinstance(dim, Fidelity) or isinstance(getattr(dim, "original_dimension", None),
+                                                   Fidelity)
+
+
+@ALGORITHMS.register()
+class ASHA(BaseAlgorithm):
+    """Asynchronous Successive Halving over the space's single ``fidelity`` dimension."""
+
+    def __init__(self, space, seed=None, grace_period=None, max_resources=None,
+                 reduction_factor=None, num_rungs=None, num_brackets=1):
+        super().__init__(space, seed=seed, max_resources=max_resources,
+                         grace_period=grace_period, reduction_factor=reduction_factor,
+                         num_rungs=num_rungs, num_brackets=num_brackets)
+        self.trial_info = {}  # id (non-fidelity params) -> Bracket
+        try:
+            fid = self.space.values()[self.fidelity_index]
+        except IndexError as exc:
+            raise RuntimeError(SPACE_ERROR) from exc
+        min_r = grace_period if grace_period is not None else fid.low
+        max_r = max_resources if max_resources is not None else fid.high
+        eta = reduction_factor if reduction_factor is not None else fid.base
+        if eta < 2:
+            raise AttributeError("Reduction factor for ASHA needs to be at least 2.")
+        if num_rungs is None:
+            num_rungs = int(numpy.log(max_r / min_r) / numpy.log(eta) + 1)
+        self.num_rungs = num_rungs
+        budgets = numpy.logspace(numpy.log(min_r) / numpy.log(eta), numpy.log(max_r) / numpy.log(eta),
+                                 num_rungs, base=eta).astype(int)
+        self.budgets = [int(b) for b in budgets]
+        self.brackets = [Bracket(self, eta, self.budgets[i:]) for i in range(num_brackets)]
+
+    def seed_rng(self, seed):
+        self.rng = numpy.random.RandomState(seed)
+
+    @property
+    def state_dict(self):
+        return {"rng_state": self.rng.get_state()}
+
+    def set_state(self, state_dict):
+        self.seed_rng(0)
+        self.rng.set_state(state_dict["rng_state"])
+        if "rungs" in state_dict:
+            for bracket, rungs in zip(self.brackets, state_dict["rungs"]):
+                bracket.rungs = [(b, {k: (o, tuple(p)) for k, (o, p) in r.items()})
+                                 for b, r in rungs]
+            self.trial_info = {k: self.brackets[i] for k, i in state_dict["trial_info"].items()}
+
+    def full_state(self) -> dict:
+        """RNG + rungs (for persisting the search itself, not only its RNG)."""
+        st = self.state_dict
+        st["rungs"] = [[(b, {k: (o, list(p)) for k, (o, p) in r.items()}) for b, r in br.rungs]
+                       for br in self.brackets]
+        st["trial_info"] = {k: self.brackets.index(b) for k, b in self.trial_info.items()}
+        return copy.deepcopy(st)
+
+    def suggest(self, num=1):
+        out = []
+        for _ in range(num):
+            p = self._suggest_one()
+            if p is None:
+                break
+            out.append(p)
+        return out or None
+
+    def _suggest_one(self):
+        for bracket in self.brackets:
+            cand = bracket.update_rungs()
+            if cand is not None:
+                bracket.register(cand, None, overwrite=False)
+                return cand
+        if all(b.is_filled for b in self.brackets):
+            log.debug("All brackets are filled.")
+            return None
+        for _ in range(100):
+            point = list(self.space.sample(1, seed=tuple(self.rng.randint(0, 1000000, size=3)))[0])
+            if self.get_id(point) not in self.trial_info:
+                break
+        else:
+            raise RuntimeError("ASHA keeps sampling already existing points.")
+        sizes = numpy.array([len(b.rungs) for b in self.brackets])
+        probs = numpy.e ** (sizes - sizes.max())
+        probs = numpy.array([p * int(not b.is_filled) for p, b in zip(probs, self.brackets)])
+        idx = self.rng.choice(len(self.brackets), p=probs / probs.sum())
+        point[self.fidelity_index] = self.brackets[idx].rungs[0][0]
+        point = tuple(point)
+        self.trial_info[self.get_id(point)] = self.brackets[idx]
+        self.brackets[idx].register(point, None, overwrite=False)
+        return point
+
+    def get_id(self, point) -> str:
+        p = list(point)
+        non_fid = p[:self.fidelity_index] + p[self.fidelity_index + 1:]
+        return hashlib.md5(str(non_fid).encode("utf-8")).hexdigest()
+
+    def observe(self, points, results):
+        for point, result in zip(points, results):
+            _id = self.get_id(point)
+            bracket = self.trial_info.get(_id)
+            if bracket is None:
+                fid = point[self.fidelity_index]
+                cands = [b for b in self.brackets if b.rungs[0][0] == fid]
+                if not cands:
+                    raise ValueError(f"No bracket found for point {_id} with fidelity {fid}")
+                bracket = cands[0]
+            try:
+                bracket.register(point, result["objective"])
+            except IndexError:
+                log.warning("Point registered to wrong bracket (corrupted timestamps?).")
+                continue
+            self.trial_info.setdefault(_id, bracket)
+
+    @property
+    def is_done(self):
+        return all(b.is_done for b in self.brackets)
+
+    @property
+    def fidelity_index(self) -> int:
+        return [i for i, d in enumerate(self.space.values()) if _is_fidelity(d)][0]
+
+
+class Bracket:
+    """Rungs ``[(budget, {id: (objective, point)})]`` of one ASHA bracket."""
+
+    def __init__(self, asha, reduction_factor, budgets):
+        self.asha = asha
+        self.reduction_factor = reduction_factor
+        self.rungs = [(int(b), dict()) for b in budgets]
+
+    def register(self, point, objective, overwrite=True):
+        fid = point[self.asha.fidelity_index]
+        rungs = [r for b, r in self.rungs if b == fid]
+        if not rungs:
+            raise IndexError(f"Bad fidelity level {fid}. Should be in "
+                             f"{[b for b, _ in self.rungs]}. Params: {point}")
+        _id = self.asha.get_id(point)
+        if overwrite or _id not in rungs[0]:
+            rungs[0][_id] = (objective, tuple(point))
+
+    def get_candidate(self, rung_id):
+        _, rung = self.rungs[rung_id]
+        nxt = self.rungs[rung_id + 1][1]
+        done = sorted(((o, p) for o, p in rung.values() if o is not None), key=lambda x: x[0])
+        k = min(len(rung) // self.reduction_factor, len(done))
+        for i in range(k):
+            point = done[i][1]
+            if self.asha.get_id(point) not in nxt:
+                return point
+        return None
+
+    @property
+    def is_done(self) -> bool:
+        """A point has COMPLETED at the top budget (the reference counts pending ones too)."""
+        return any(o is not None for o, _ in self.rungs[-1][1].values())
+
+    @property
+    def is_filled(self) -> bool:
+        return self.has_rung_filled(len(self.rungs) - 2)
+
+    def has_rung_filled(self, rung_id) -> bool:
+        n = len(self.rungs)
+        return len(self.rungs[rung_id][1]) >= self.reduction_factor ** (n - rung_id - 1)
+
+    def update_rungs(self):
+        if self.rungs[-1][1]:  # the top rung is taken (pending or completed): no more promotions
+            return None
+        for rung_id in range(len(self.rungs) - 2, -1, -1):
+            cand = self.get_candidate(rung_id)
+            if cand is not None:
+                cand = list(copy.deepcopy(cand))
+                cand[self.asha.fidelity_index] = self.rungs[rung_id + 1][0]
+                return tuple(cand)
+        return None
+
+    def __repr__(self):
+        return f"Bracket({[b for b, _ in self.rungs]})"

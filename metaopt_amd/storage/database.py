@@ -1,0 +1,679 @@
+"""Document databases: the control plane shared by every worker of an experiment.
+
+Same contract as the reference's ``src/orion/core/io/database/`` (``AbstractDB`` :23-264,
+``EphemeralDB`` ephemeraldb.py:18-480, ``PickledDB`` pickleddb.py:29-207, ``MongoDB``
+mongodb.py:30-295): ``write`` (insert, or ``$set`` update with a query), ``read`` (query +
+projection), ``read_and_write`` (atomic find-and-modify of the first match), ``count``,
+``remove``, ``ensure_index`` (unique indexes raise :class:`DuplicateKeyError`),
+``index_information`` and ``drop_index``.
+
+Backends:
+  * :class:`EphemeralDB` -- in-process, for ``--debug`` and tests.  Documents are stored nested
+    with an ``_id`` hash index, so ``read_and_write`` by id and unique checks are O(1) instead of
+    the reference's flattened linear scans.
+  * :class:`PickledDB` -- an EphemeralDB persisted in one file, every operation under a
+    ``FileLock`` with an atomic tmp-file + rename write, for workers on a shared filesystem.
+  * :class:`MongoDB` -- pymongo, ``find_one_and_update`` for the atomic reserve.
+
+Query operators: equality on dotted keys, ``$ne $in $nin $gt $gte $lt $lte $exists``.
+"""
+from __future__ import annotations
+
+import copy
+import datetime
+import logging
+import os
+import pickle
+from contextlib import contextmanager
+from typing import Any, Dict, Iterable, List, Optional
+
+from ..utils.registry import Registry
+
+log = logging.getLogger(__name__)
+logging.getLogger("filelock").setLevel("ERROR")
+
+
+class DatabaseError(RuntimeError):
+    """Backend-independent database failure."""
+
+
+class DuplicateKeyError(DatabaseError):
+    """A write would duplicate a unique index value."""
+
+
+class OutdatedDatabaseError(DatabaseError):
+    """The database schema is older than this version of the framework (run ``db upgrade``)."""
+
+
+class DatabaseTimeout(DatabaseError):
+    """The database lock or server could not be acquired in time."""
+
+
+DATABASES = Registry("Database")
+
+
+# ----------------------------------------------------------------------------------------------
+# Query / projection engine on nested documents
+# ----------------------------------------------------------------------------------------------
+_MISSING = object()
+
+
+def _get_path(doc, key: str):
+    cur = doc
+    for part in key.split("."):
+        if isinstance(cur, dict) and part in cur:
+            cur = cur[part]
+        elif isinstance(cur, list) and part.isdigit() and int(part) < len(cur):
+            cur = cur[int(part)]
+        else:
+            return _MISSING
+    return cur
+
+
+def _cmp(op, a, b):
+    try:
+        return op(a, b)
+    except TypeError:
+        return False
+
+
+_OPS = {
+    "$ne": lambda a, b: a is _MISSING or a != b,
+    "$in": lambda a, b: a is not _MISSING and a in b,
+    "$nin": lambda a, b: a is _MISSING or a not in b,
+    "$gt": lambda a, b: a is not _MISSING and a is not None and _cmp(lambda x, y: x > y, a, b),
+    "$gte": lambda a, b: a is not _MISSING and a is not None and _cmp(lambda x, y: x >= y, a, b),
+    "$lt": lambda a, b: a is not _MISSING and a is not None and _cmp(lambda x, y: x < y, a, b),
+    "$lte": lambda a, b: a is not _MISSING and a is not None and _cmp(lambda x, y: x <= y, a, b),
+    "$exists": lambda a, b: (a is not _MISSING) == bool(b),
+}
+
+
+def _flatten_query(query: dict, prefix: str = "") -> List[tuple]:
+    """-> [(dotted_key, op, value)]; nested non-operator dicts become dotted keys."""
+    out = []
+    for k, v in query.items():
+        key = f"{prefix}.{k}" if prefix else k
+        if isinstance(v, dict) and v and all(str(x).startswith("$") for x in v):
+            for op, val in v.items():
+                if op not in _OPS:
+                    raise ValueError(f"Operator '{op}' is not supported")
+                out.append((key, op, val))
+        elif isinstance(v, dict) and v:
+            out.extend(_flatten_query(v, key))
+        elif k.split(".")[-1].startswith("$"):
+            parts = key.split(".")
+            op = parts[-1]
+            if op not in _OPS:
+                raise ValueError(f"Operator '{op}' is not supported")
+            out.append((".".join(parts[:-1]), op, v))
+        else:
+            out.append((key, "$eq", v))
+    return out
+
+
+def match(doc: dict, query: Optional[dict]) -> bool:
+    if not query:
+        return True
+    for key, op, val in _flatten_query(query):
+        cur = _get_path(doc, key)
+        if op == "$eq":
+            if cur is _MISSING or cur != val:
+                return False
+        elif not _OPS[op](cur, val):
+            return False
+    return True
+
+
+def _set_path(doc, key: str, value):
+    parts = key.split(".")
+    cur = doc
+    for p in parts[:-1]:
+        nxt = cur.get(p)
+        if not isinstance(nxt, dict):
+            nxt = {}
+            cur[p] = nxt
+        cur = nxt
+    cur[parts[-1]] = value
+
+
+def apply_update(doc: dict, data: dict) -> None:
+    """``$set`` (default when no operator is given), ``$inc``, ``$unset``, ``$push``."""
+    if any(k.startswith("$") for k in data):
+        for op, fields in data.items():
+            for key, value in _flatten_set(fields).items():
+                if op == "$set":
+                    _set_path(doc, key, copy.deepcopy(value))
+                elif op == "$inc":
+                    cur = _get_path(doc, key)
+                    _set_path(doc, key, (0 if cur is _MISSING or cur is None else cur) + value)
+                elif op == "$unset":
+                    parts = key.split(".")
+                    parent = _get_path(doc, ".".join(parts[:-1])) if len(parts) > 1 else doc
+                    if isinstance(parent, dict):
+                        parent.pop(parts[-1], None)
+                elif op == "$push":
+                    cur = _get_path(doc, key)
+                    _set_path(doc, key, ([] if cur is _MISSING or cur is None else list(cur))
+                              + [copy.deepcopy(value)])
+                else:
+                    raise ValueError(f"Update operator '{op}' is not supported")
+    else:
+        for key, value in _flatten_set(data).items():
+            _set_path(doc, key, copy.deepcopy(value))
+
+
+def _flatten_set(fields: dict) -> dict:
+    """Dotted keys for nested dicts given to $set, but keep dict *values* of dotted keys whole."""
+    out = {}
+    for k, v in fields.items():
+        out[k] = v
+    return out
+
+
+def project(doc: dict, selection: Optional[dict]) -> dict:
+    """Mongo-style projection: all-1 (include) or all-0 (exclude); ``_id`` shown unless 0."""
+    if not selection:
+        return copy.deepcopy(doc)
+    sel = dict(selection)
+    id_flag = sel.pop("_id", 1)
+    if sel:
+        flags = set(bool(v) for v in sel.values())
+        if len(flags) > 1:
+            raise ValueError(f"Cannot mix selection with 1 and 0s except for _id: {selection}")
+        include = flags.pop()
+    else:
+        include = bool(id_flag)
+        if include:
+            return {"_id": copy.deepcopy(doc.get("_id"))} if "_id" in doc else {}
+        out = copy.deepcopy(doc)
+        out.pop("_id", None)
+        return out
+    if include:
+        out: Dict[str, Any] = {}
+        for key in sel:
+            val = _get_path(doc, key)
+            _set_path(out, key, None if val is _MISSING else copy.deepcopy(val))
+        if id_flag and "_id" in doc:
+            out["_id"] = copy.deepcopy(doc["_id"])
+        return out
+    out = copy.deepcopy(doc)
+    for key in sel:
+        parts = key.split(".")
+        parent = _get_path(out, ".".join(parts[:-1])) if len(parts) > 1 else out
+        if isinstance(parent, dict):
+            parent.pop(parts[-1], None)
+    if not id_flag:
+        out.pop("_id", None)
+    return out
+
+
+def index_name(keys) -> str:
+    """Mongo-style index names: ``_id_`` or ``name_1_version_1``."""
+    if not isinstance(keys, (list, tuple)):
+        keys = [(keys, 1)]
+    names = [k if isinstance(k, str) else k[0] for k in keys]
+    if names == ["_id"]:
+        return "_id_"
+    orders = [1 if isinstance(k, str) else (1 if k[1] in (1, AbstractDB.ASCENDING) else -1)
+              for k in keys]
+    return "_".join(f"{n}_{o}" for n, o in zip(names, orders))
+
+
+def _hashable(v):
+    if isinstance(v, dict):
+        return tuple(sorted((k, _hashable(x)) for k, x in v.items()))
+    if isinstance(v, (list, tuple)):
+        return tuple(_hashable(x) for x in v)
+    return v
+
+
+# ----------------------------------------------------------------------------------------------
+# Interfaces
+# ----------------------------------------------------------------------------------------------
+class AbstractDB:
+    ASCENDING = 0
+    DESCENDING = 1
+
+    def __init__(self, host="localhost", name=None, port=None, username=None, password=None,
+                 **kwargs):
+        self.host = host
+        self.name = name
+        self.port = port
+        self.username = username
+        self.password = password
+        self.options = kwargs
+        self._db = None
+        self._conn = None
+        self.initiate_connection()
+
+    @property
+    def is_connected(self) -> bool:
+        raise NotImplementedError
+
+    def initiate_connection(self):
+        raise NotImplementedError
+
+    def close_connection(self):
+        raise NotImplementedError
+
+    def ensure_index(self, collection_name, keys, unique=False):
+        raise NotImplementedError
+
+    def index_information(self, collection_name) -> dict:
+        raise NotImplementedError
+
+    def drop_index(self, collection_name, name):
+        raise NotImplementedError
+
+    def write(self, collection_name, data, query=None) -> int:
+        raise NotImplementedError
+
+    def read(self, collection_name, query=None, selection=None) -> List[dict]:
+        raise NotImplementedError
+
+    def read_and_write(self, collection_name, query, data, selection=None) -> Optional[dict]:
+        raise NotImplementedError
+
+    def count(self, collection_name, query=None) -> int:
+        raise NotImplementedError
+
+    def remove(self, collection_name, query) -> int:
+        raise NotImplementedError
+
+    @property
+    def configuration(self) -> dict:
+        return {"type": type(self).__name__.lower(), "host": self.host, "name": self.name}
+
+
+class ReadOnlyDB:
+    """Read-only view (``read``/``count`` only) handed to experiment views."""
+
+    __slots__ = ("_database",)
+    valid_attributes = ["host", "name", "port", "username", "password", "is_connected",
+                        "initiate_connection", "close_connection", "read", "count"]
+
+    def __init__(self, database):
+        self._database = database
+
+    def __getattr__(self, attr):
+        if attr not in self.valid_attributes:
+            raise AttributeError(f"Cannot access attribute {attr} on view-only experiments.")
+        return getattr(self._database, attr)
+
+
+# ----------------------------------------------------------------------------------------------
+# In-memory backend
+# ----------------------------------------------------------------------------------------------
+class _Collection:
+    def __init__(self):
+        self.docs: Dict[Any, dict] = {}  # _id -> doc (insertion-ordered)
+        self.indexes: Dict[str, tuple] = {}  # name -> (keys, unique, set of values)
+        self._next_id = 1
+        self.create_index("_id", unique=True)
+
+    def create_index(self, keys, unique=False):
+        if not isinstance(keys, (list, tuple)):
+            keys = [(keys, AbstractDB.ASCENDING)]
+        keys = [(k, AbstractDB.ASCENDING) if isinstance(k, str) else tuple(k) for k in keys]
+        name = index_name(keys)
+        if name in self.indexes:
+            return name
+        fields = tuple(k for k, _ in keys)
+        values = set()
+        if unique:
+            for d in self.docs.values():
+                v = self._key(d, fields)
+                if v in values:
+                    raise DuplicateKeyError(f"Duplicate key error: index={name} value={v}")
+                values.add(v)
+        self.indexes[name] = (fields, unique, values)
+        return name
+
+    @staticmethod
+    def _key(doc, fields):
+        return tuple(_hashable(None if (v := _get_path(doc, f)) is _MISSING else v) for f in fields)
+
+    def _check_unique(self, doc, exclude_id=_MISSING):
+        for name, (fields, unique, values) in self.indexes.items():
+            if not unique:
+                continue
+            v = self._key(doc, fields)
+            if v in values:
+                if exclude_id is not _MISSING:
+                    old = self.docs.get(exclude_id)
+                    if old is not None and self._key(old, fields) == v:
+                        continue
+                raise DuplicateKeyError(f"Duplicate key error: index={name} value={v}")
+
+    def _register(self, doc):
+        for fields, unique, values in self.indexes.values():
+            if unique:
+                values.add(self._key(doc, fields))
+
+    def _unregister(self, doc):
+        for fields, unique, values in self.indexes.values():
+            if unique:
+                values.discard(self._key(doc, fields))
+
+    def insert(self, doc: dict):
+        if "_id" not in doc:
+            while self._next_id in self.docs:
+                self._next_id += 1
+            doc["_id"] = self._next_id
+            self._next_id += 1
+        stored = copy.deepcopy(doc)
+        self._check_unique(stored)
+        self.docs[_hashable(stored["_id"])] = stored
+        self._register(stored)
+
+    def find_iter(self, query):
+        if query and set(query) == {"_id"} and not isinstance(query["_id"], dict):
+            d = self.docs.get(_hashable(query["_id"]))
+            return [d] if d is not None else []
+        return [d for d in self.docs.values() if match(d, query)]
+
+    def update(self, doc: dict, data: dict):
+        new = copy.deepcopy(doc)
+        apply_update(new, data)
+        if new.get("_id") != doc.get("_id"):
+            raise DatabaseError("cannot change _id")
+        self._unregister(doc)
+        try:
+            self._check_unique(new)
+        except DuplicateKeyError:
+            self._register(doc)
+            raise
+        doc.clear()
+        doc.update(new)
+        self._register(doc)
+
+    def delete(self, doc):
+        self._unregister(doc)
+        del self.docs[_hashable(doc["_id"])]
+
+
+@DATABASES.register("ephemeraldb")
+class EphemeralDB(AbstractDB):
+    """Non-persistent in-process database (``--debug``; tests)."""
+
+    @property
+    def is_connected(self):
+        return self._db is not None
+
+    def initiate_connection(self):
+        if self._db is None:
+            self._db = {}
+
+    def close_connection(self):
+        pass
+
+    def _col(self, name) -> _Collection:
+        col = self._db.get(name)
+        if col is None:
+            col = self._db[name] = _Collection()
+        return col
+
+    def ensure_index(self, collection_name, keys, unique=False):
+        self._col(collection_name).create_index(keys, unique=unique)
+
+    def index_information(self, collection_name):
+        return {name: unique for name, (_, unique, _) in self._col(collection_name).indexes.items()}
+
+    def drop_index(self, collection_name, name):
+        col = self._col(collection_name)
+        if name not in col.indexes:
+            raise DatabaseError(f"index not found with name {name}")
+        del col.indexes[name]
+
+    def write(self, collection_name, data, query=None):
+        col = self._col(collection_name)
+        if query is None:
+            docs = data if isinstance(data, (list, tuple)) else [data]
+            for d in docs:
+                col.insert(d)
+            return len(docs)
+        n = 0
+        for d in list(col.find_iter(query)):
+            col.update(d, data)
+            n += 1
+        return n
+
+    def read(self, collection_name, query=None, selection=None):
+        return [project(d, selection) for d in self._col(collection_name).find_iter(query)]
+
+    def read_and_write(self, collection_name, query, data, selection=None):
+        col = self._col(collection_name)
+        found = col.find_iter(query)
+        if not found:
+            return None
+        doc = found[0]
+        col.update(doc, data)
+        return project(doc, selection)
+
+    def count(self, collection_name, query=None):
+        col = self._col(collection_name)
+        if not query:
+            return len(col.docs)
+        return len(col.find_iter(query))
+
+    def remove(self, collection_name, query):
+        col = self._col(collection_name)
+        found = list(col.find_iter(query))
+        for d in found:
+            col.delete(d)
+        return len(found)
+
+    def drop(self, collection_name):
+        self._db.pop(collection_name, None)
+
+    def collection_names(self):
+        return sorted(self._db)
+
+
+# ----------------------------------------------------------------------------------------------
+# File backend
+# ----------------------------------------------------------------------------------------------
+def default_pickled_path() -> str:
+    base = os.environ.get("XDG_DATA_HOME") or os.path.join(os.path.expanduser("~"), ".local",
+                                                           "share")
+    return os.path.join(base, "mopt", "mopt_db.pkl")
+
+
+@DATABASES.register("pickleddb")
+class PickledDB(AbstractDB):
+    """An :class:`EphemeralDB` pickled to ``host`` (a file path), every op under a file lock."""
+
+    LOCK_TIMEOUT = 60
+
+    def __init__(self, host=None, name=None, *args, timeout=None, **kwargs):
+        host = host or default_pickled_path()
+        if host in ("localhost", ""):
+            host = default_pickled_path()
+        self.timeout = timeout if timeout is not None else self.LOCK_TIMEOUT
+        super().__init__(host, name=name)
+        d = os.path.dirname(os.path.abspath(host))
+        os.makedirs(d, exist_ok=True)
+
+    @property
+    def is_connected(self):
+        return True
+
+    def initiate_connection(self):
+        pass
+
+    def close_connection(self):
+        pass
+
+    def _load(self) -> EphemeralDB:
+        if not os.path.exists(self.host):
+            return EphemeralDB()
+        with open(self.host, "rb") as f:
+            data = f.read()
+        if not data:
+            return EphemeralDB()
+        return pickle.loads(data)  # our own file format, written by _dump below
+
+    def _dump(self, db: EphemeralDB) -> None:
+        tmp = f"{self.host}.{os.getpid()}.tmp"
+        with open(tmp, "wb") as f:
+            pickle.dump(db, f, protocol=pickle.HIGHEST_PROTOCOL)
+        os.replace(tmp, self.host)
+
+    @contextmanager
+    def locked_database(self, write=True):
+        from filelock import FileLock, Timeout
+        lock = FileLock(self.host + ".lock")
+        try:
+            with lock.acquire(timeout=self.timeout):
+                db = self._load()
+                yield db
+                if write:
+                    self._dump(db)
+        except Timeout as exc:
+            raise DatabaseTimeout(f"could not acquire lock for PickledDB after {self.timeout} "
+                                  "seconds") from exc
+
+    def ensure_index(self, collection_name, keys, unique=False):
+        with self.locked_database() as db:
+            db.ensure_index(collection_name, keys, unique=unique)
+
+    def index_information(self, collection_name):
+        with self.locked_database(write=False) as db:
+            return db.index_information(collection_name)
+
+    def drop_index(self, collection_name, name):
+        with self.locked_database() as db:
+            return db.drop_index(collection_name, name)
+
+    def write(self, collection_name, data, query=None):
+        with self.locked_database() as db:
+            return db.write(collection_name, data, query=query)
+
+    def read(self, collection_name, query=None, selection=None):
+        with self.locked_database(write=False) as db:
+            return db.read(collection_name, query=query, selection=selection)
+
+    def read_and_write(self, collection_name, query, data, selection=None):
+        with self.locked_database() as db:
+            return db.read_and_write(collection_name, query, data, selection=selection)
+
+    def count(self, collection_name, query=None):
+        with self.locked_database(write=False) as db:
+            return db.count(collection_name, query=query)
+
+    def remove(self, collection_name, query):
+        with self.locked_database() as db:
+            return db.remove(collection_name, query)
+
+
+# ----------------------------------------------------------------------------------------------
+# MongoDB backend
+# ----------------------------------------------------------------------------------------------
+@DATABASES.register("mongodb")
+class MongoDB(AbstractDB):
+    """pymongo backend; ``host`` may be a ``mongodb://`` URI (user, password, db name parsed)."""
+
+    def __init__(self, host="localhost", name=None, port=None, username=None, password=None,
+                 serverSelectionTimeoutMS=5000, **kwargs):
+        self._timeout_ms = serverSelectionTimeoutMS
+        if host and str(host).startswith("mongodb://"):
+            from pymongo.uri_parser import parse_uri
+            info = parse_uri(host)
+            username = username or info.get("username")
+            password = password or info.get("password")
+            name = name or info.get("database")
+            port = port or (info["nodelist"][0][1] if info.get("nodelist") else None)
+        super().__init__(host, name, port or 27017, username, password, **kwargs)
+
+    @property
+    def is_connected(self):
+        return self._conn is not None
+
+    def initiate_connection(self):
+        if self._conn is not None:
+            return
+        import pymongo
+        from pymongo.errors import ConnectionFailure, OperationFailure
+        try:
+            self._conn = pymongo.MongoClient(
+                host=self.host, port=int(self.port) if self.port else None,
+                username=self.username, password=self.password,
+                serverSelectionTimeoutMS=self._timeout_ms)
+            self._db = self._conn[self.name or "mopt"]
+            self._conn.admin.command("ping")
+        except (ConnectionFailure, OperationFailure) as exc:
+            self._conn = None
+            raise DatabaseError(str(exc)) from exc
+
+    def close_connection(self):
+        if self._conn is not None:
+            self._conn.close()
+            self._conn = None
+
+    @contextmanager
+    def _errors(self):
+        from pymongo import errors
+        try:
+            yield
+        except errors.DuplicateKeyError as exc:
+            raise DuplicateKeyError(str(exc)) from exc
+        except errors.BulkWriteError as exc:
+            raise DuplicateKeyError(str(exc)) from exc
+        except (errors.ConnectionFailure, errors.OperationFailure) as exc:
+            raise DatabaseError(str(exc)) from exc
+
+    def ensure_index(self, collection_name, keys, unique=False):
+        import pymongo
+        if not isinstance(keys, (list, tuple)):
+            keys = [(keys, self.ASCENDING)]
+        keys = [(k, pymongo.ASCENDING if o == self.ASCENDING else pymongo.DESCENDING)
+                for k, o in keys]
+        with self._errors():
+            self._db[collection_name].create_index(keys, unique=unique, background=True)
+
+    def index_information(self, collection_name):
+        with self._errors():
+            info = self._db[collection_name].index_information()
+        return {name: info[name].get("unique", name == "_id_") for name in info}
+
+    def drop_index(self, collection_name, name):
+        with self._errors():
+            self._db[collection_name].drop_index(name)
+
+    def write(self, collection_name, data, query=None):
+        col = self._db[collection_name]
+        with self._errors():
+            if query is None:
+                docs = data if isinstance(data, (list, tuple)) else [data]
+                res = col.insert_many(docs)
+                return len(res.inserted_ids)
+            update = data if any(k.startswith("$") for k in data) else {"$set": data}
+            return col.update_many(query, update).modified_count
+
+    def read(self, collection_name, query=None, selection=None):
+        with self._errors():
+            return list(self._db[collection_name].find(query or {}, selection))
+
+    def read_and_write(self, collection_name, query, data, selection=None):
+        import pymongo
+        update = data if any(k.startswith("$") for k in data) else {"$set": data}
+        with self._errors():
+            return self._db[collection_name].find_one_and_update(
+                query, update, projection=selection,
+                return_document=pymongo.ReturnDocument.AFTER)
+
+    def count(self, collection_name, query=None):
+        with self._errors():
+            return self._db[collection_name].count_documents(query or {})
+
+    def remove(self, collection_name, query):
+        with self._errors():
+            return self._db[collection_name].delete_many(query).deleted_count
+
+
+def create_database(of_type: str = "ephemeraldb", **config) -> AbstractDB:
+    """Instantiate a backend by (case-insensitive) name."""
+    cls = DATABASES.get(of_type)
+    config = {k: v for k, v in config.items() if v is not None}
+    return cls(**config)
