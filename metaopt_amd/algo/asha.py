@@ -41,10 +41,10 @@ class ASHA(BaseAlgorithm):
     """Asynchronous Successive Halving over the space's single ``fidelity`` dimension."""
 
     def __init__(self, space, seed=None, grace_period=None, max_resources=None,
-                 reduction_factor=None, num_rungs=None, num_brackets=1):
+                 reduction_factor=None, num_rungs=None, num_brackets=1, repetitions=1):
         super().__init__(space, seed=seed, max_resources=max_resources,
                          grace_period=grace_period, reduction_factor=reduction_factor,
-                         num_rungs=num_rungs, num_brackets=num_brackets)
+                         num_rungs=num_rungs, num_brackets=num_brackets, repetitions=repetitions)
         self.trial_info = {}  # id (non-fidelity params) -> Bracket
         try:
             fid = self.space.values()[self.fidelity_index]
@@ -61,7 +61,9 @@ class ASHA(BaseAlgorithm):
         budgets = numpy.logspace(numpy.log(min_r) / numpy.log(eta), numpy.log(max_r) / numpy.log(eta),
                                  num_rungs, base=eta).astype(int)
         self.budgets = [int(b) for b in budgets]
+        self.eta = eta
         self.brackets = [Bracket(self, eta, self.budgets[i:]) for i in range(num_brackets)]
+        self._repetition = 1
 
     def seed_rng(self, seed):
         self.rng = numpy.random.RandomState(seed)
@@ -74,6 +76,9 @@ class ASHA(BaseAlgorithm):
         self.seed_rng(0)
         self.rng.set_state(state_dict["rng_state"])
         if "rungs" in state_dict:
+            while len(self.brackets) < len(state_dict["rungs"]):
+                self.brackets.append(Bracket(self, self.eta, self.budgets[:1]))
+            self._repetition = state_dict.get("repetition", 1)
             for bracket, rungs in zip(self.brackets, state_dict["rungs"]):
                 bracket.rungs = [(b, {k: (o, tuple(p)) for k, (o, p) in r.items()})
                                  for b, r in rungs]
@@ -85,6 +90,7 @@ class ASHA(BaseAlgorithm):
         st["rungs"] = [[(b, {k: (o, list(p)) for k, (o, p) in r.items()}) for b, r in br.rungs]
                        for br in self.brackets]
         st["trial_info"] = {k: self.brackets.index(b) for k, b in self.trial_info.items()}
+        st["repetition"] = self._repetition
         return copy.deepcopy(st)
 
     def suggest(self, num=1):
@@ -102,23 +108,31 @@ class ASHA(BaseAlgorithm):
             if cand is not None:
                 bracket.register(cand, None, overwrite=False)
                 return cand
-        if all(b.is_filled for b in self.brackets):
-            log.debug("All brackets are filled.")
-            return None
+        current = self.brackets[-self.num_brackets:]
+        if all(b.is_filled for b in current):
+            if self._repetition >= (self.repetitions if self.repetitions is not None else 1):
+                log.debug("All brackets are filled.")
+                return None
+            # ``repetitions > 1``: run another set of brackets (the population keeps sampling
+            # instead of idling, as in the original ASHA which never stops adding configs)
+            self._repetition += 1
+            self.brackets += [Bracket(self, self.eta, self.budgets[i:])
+                              for i in range(self.num_brackets)]
+            current = self.brackets[-self.num_brackets:]
         for _ in range(100):
             point = list(self.space.sample(1, seed=tuple(self.rng.randint(0, 1000000, size=3)))[0])
             if self.get_id(point) not in self.trial_info:
                 break
         else:
             raise RuntimeError("ASHA keeps sampling already existing points.")
-        sizes = numpy.array([len(b.rungs) for b in self.brackets])
+        sizes = numpy.array([len(b.rungs) for b in current])
         probs = numpy.e ** (sizes - sizes.max())
-        probs = numpy.array([p * int(not b.is_filled) for p, b in zip(probs, self.brackets)])
-        idx = self.rng.choice(len(self.brackets), p=probs / probs.sum())
-        point[self.fidelity_index] = self.brackets[idx].rungs[0][0]
+        probs = numpy.array([p * int(not b.is_filled) for p, b in zip(probs, current)])
+        idx = self.rng.choice(len(current), p=probs / probs.sum())
+        point[self.fidelity_index] = current[idx].rungs[0][0]
         point = tuple(point)
-        self.trial_info[self.get_id(point)] = self.brackets[idx]
-        self.brackets[idx].register(point, None, overwrite=False)
+        self.trial_info[self.get_id(point)] = current[idx]
+        current[idx].register(point, None, overwrite=False)
         return point
 
     def get_id(self, point) -> str:
@@ -145,7 +159,8 @@ class ASHA(BaseAlgorithm):
 
     @property
     def is_done(self):
-        return all(b.is_done for b in self.brackets)
+        reps = self.repetitions if self.repetitions is not None else 1
+        return self._repetition >= reps and all(b.is_done for b in self.brackets)
 
     @property
     def fidelity_index(self) -> int:

@@ -1,0 +1,74 @@
+"""The 4-layer MLP sweep task (BASELINE.json configs 1 and 2).
+
+Maps a trial's parameters to a :class:`~metaopt_amd.ops.population.MemberConfig` of the device
+population, and names the search space the benchmark sweeps:
+
+* ``/lr ~ loguniform(1e-3, 1.0)`` -- SGD learning rate (momentum 0.9, weight decay 5e-4 fixed);
+* ``/width ~ loguniform(64, 1024, discrete=True)`` -- hidden width of the 3 ReLU layers;
+* ``/dropout ~ uniform(0, 0.5)`` -- dropout after each hidden layer;
+* ``/steps ~ fidelity(32, 2048, 4)`` -- training budget in optimizer steps (ASHA rungs 32, 128, 512,
+  2048).
+
+Config 1 (logistic regression, CPU) is the same task with ``n_hidden=0`` and a 2-HP space
+(``/lr``, ``/weight_decay``).
+"""
+from __future__ import annotations
+
+import hashlib
+from dataclasses import dataclass, field
+from typing import Dict, Optional
+
+from ..ops.population import MemberConfig
+
+MLP_PRIORS = {
+    "/lr": "loguniform(1e-3, 1.0)",
+    "/width": "loguniform(64, 1024, discrete=True)",
+    "/dropout": "uniform(0, 0.5)",
+    "/steps": "fidelity(32, 2048, 4)",
+}
+
+LOGREG_PRIORS = {
+    "/lr": "loguniform(1e-3, 1.0)",
+    "/weight_decay": "loguniform(1e-6, 1e-1)",
+    "/steps": "fidelity(64, 256, 2)",
+}
+
+
+def param_key(params: Dict, fidelity_name: str) -> str:
+    """Identity of a configuration regardless of its budget (the ASHA promotion key)."""
+    items = sorted((k, v) for k, v in params.items() if k != fidelity_name)
+    return hashlib.md5(repr(items).encode("utf-8")).hexdigest()
+
+
+@dataclass
+class MLPSweepTask:
+    priors: Dict[str, str] = field(default_factory=lambda: dict(MLP_PRIORS))
+    fidelity: str = "/steps"
+    momentum: float = 0.9
+    weight_decay: float = 5e-4
+    width: int = 256          # used when the space has no /width
+    n_hidden: int = 3
+    in_features: int = 784
+    num_classes: int = 10
+    max_width: int = 1024
+
+    def member_config(self, params: Dict, seed: int) -> MemberConfig:
+        return MemberConfig(
+            width=int(params.get("/width", self.width)),
+            lr=float(params["/lr"]),
+            momentum=float(params.get("/momentum", self.momentum)),
+            weight_decay=float(params.get("/weight_decay", self.weight_decay)),
+            dropout=float(params.get("/dropout", 0.0)) if self.n_hidden > 0 else 0.0,
+            seed=int(seed) & 0x7FFFFFFF,
+        )
+
+    def budget(self, params: Dict) -> int:
+        return int(params[self.fidelity])
+
+    def key(self, params: Dict) -> str:
+        return param_key(params, self.fidelity)
+
+    @staticmethod
+    def seed_of(key: str) -> int:
+        """Deterministic per-configuration seed (same weights init when a trial is re-run)."""
+        return int(key[:8], 16)

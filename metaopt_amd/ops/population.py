@@ -47,6 +47,16 @@ def pad64(n: int) -> int:
     return (int(n) + TILE - 1) // TILE * TILE
 
 
+def _ranges(counts: np.ndarray) -> np.ndarray:
+    """concatenate(arange(c) for c in counts), vectorised."""
+    counts = np.asarray(counts, dtype=np.int64)
+    total = int(counts.sum())
+    if total == 0:
+        return np.zeros(0, np.int64)
+    starts = np.repeat(np.cumsum(counts) - counts, counts)
+    return np.arange(total, dtype=np.int64) - starts
+
+
 @dataclass
 class MemberConfig:
     """Hyper-parameters of one population member (one trial)."""
@@ -256,9 +266,16 @@ class PopulationMLP:
         return out
 
     # ------------------------------------------------------------------ checkpoints (device)
+    def used_params(self, slot: int) -> int:
+        """Length of the prefix of the slot region the member actually uses."""
+        cfg = self.members[slot]
+        return sum(pad64(k * n) + pad64(n) for k, n in self.layer_dims(cfg.width))
+
     def slot_state(self, slot: int, to_cpu: bool = False) -> dict:
-        """Device checkpoint of a member: config, step count, weights and optimizer state."""
-        reg = self._region(slot)
+        """Device checkpoint of a member: config, step count, weights and optimizer state
+        (only the used prefix of the slot region is copied)."""
+        b = self.slot_base(slot)
+        reg = slice(b, b + self.used_params(slot))
         mv = (lambda t: t.detach().cpu().clone()) if to_cpu else (lambda t: t.detach().clone())
         st = {"config": self.members[slot].to_dict(), "t": int(self.hp[slot]["t"]),
               "p32": mv(self.p32[reg]), "m32": mv(self.m32[reg]), "optimizer": self.optimizer}
@@ -270,7 +287,8 @@ class PopulationMLP:
         cfg = MemberConfig(**state["config"])
         self.members[slot] = cfg
         self._write_hp(slot, cfg, int(state["t"]))
-        reg = self._region(slot)
+        b = self.slot_base(slot)
+        reg = slice(b, b + state["p32"].numel())
         self.p32[reg].copy_(state["p32"])
         self.m32[reg].copy_(state["m32"])
         if self.optimizer == "adamw":
@@ -293,32 +311,53 @@ class PopulationMLP:
 
     # ------------------------------------------------------------------ tables
     def _build_tables(self, rows: int) -> dict:
+        """Trial-layer descriptors + per-layer work lists, built with numpy (no per-item loops)."""
         L = self.L
         tl = np.zeros(self.capacity * L, dtype=TL_DTYPE)
-        fwd: List[list] = [[] for _ in range(L)]
-        bwd: List[list] = [[] for _ in range(L)]
         act_slot = rows * self.act_row
-        layer_base = np.concatenate([[0], np.cumsum(self.nmax)]) * rows
-        for s in self.active_slots():
-            cfg = self.members[s]
-            base = self.slot_base(s)
-            for l, ((k, n), (wo, bo)) in enumerate(zip(self.layer_dims(cfg.width),
-                                                       self.param_offsets(cfg.width))):
-                i = s * L + l
-                y_off = s * act_slot + int(layer_base[l])
-                prev = s * act_slot + int(layer_base[l - 1]) if l > 0 else 0
-                n_real = self.num_classes if l == L - 1 else n
-                tl[i] = (k, n, s, n_real, base + wo, base + bo, prev, y_off,
-                         prev if l > 0 else -1, 0)
-                fwd[l].extend((i, t) for t in range(n // TILE))
-                bwd[l].extend((i, t) for t in range(k // TILE))
-        out = {"tl_np": tl, "rows": rows}
+        layer_base = (np.concatenate([[0], np.cumsum(self.nmax)]) * rows).astype(np.int64)
+        slots = np.array(self.active_slots(), dtype=np.int64)
+        fwd: List[np.ndarray] = []
+        bwd: List[np.ndarray] = []
+        if len(slots):
+            widths = np.array([self.members[s].width for s in slots])
+            # per-slot layer dims / offsets (vectorised over slots, looped over the few layers)
+            wp = (widths + TILE - 1) // TILE * TILE
+            Ks, Ns = [], []
+            for l in range(L):
+                K = np.full_like(wp, self.K0) if l == 0 else wp
+                N = np.full_like(wp, TILE) if l == L - 1 else wp
+                Ks.append(K)
+                Ns.append(N)
+            off = np.zeros_like(wp)
+            for l in range(L):
+                K, N = Ks[l], Ns[l]
+                i = slots * L + l
+                w_off = slots * self.slot_params + off
+                b_off = w_off + (K * N + TILE - 1) // TILE * TILE
+                off = off + (K * N + TILE - 1) // TILE * TILE + (N + TILE - 1) // TILE * TILE
+                y_off = slots * act_slot + layer_base[l]
+                prev = slots * act_slot + layer_base[l - 1] if l > 0 else np.zeros_like(slots)
+                tl["K"][i] = K
+                tl["N"][i] = N
+                tl["trial"][i] = slots
+                tl["n_real"][i] = self.num_classes if l == L - 1 else N
+                tl["w_off"][i] = w_off
+                tl["b_off"][i] = b_off
+                tl["x_off"][i] = prev
+                tl["y_off"][i] = y_off
+                tl["gx_off"][i] = prev if l > 0 else -1
+                nt, nk = N // TILE, K // TILE
+                fwd.append(np.stack([np.repeat(i, nt), _ranges(nt)], 1).astype(np.int32))
+                bwd.append(np.stack([np.repeat(i, nk), _ranges(nk)], 1).astype(np.int32))
+        else:
+            fwd = [np.zeros((0, 2), np.int32) for _ in range(L)]
+            bwd = [np.zeros((0, 2), np.int32) for _ in range(L)]
+        out = {"tl_np": tl, "rows": rows, "fwd_np": fwd, "bwd_np": bwd}
         if self.device.type == "cuda":
             out["tl"] = torch.from_numpy(tl.view(np.uint8).copy()).to(self.device)
-            out["fwd"] = [torch.tensor(w, dtype=torch.int32).reshape(-1, 2).to(self.device)
-                          for w in fwd]
-            out["bwd"] = [torch.tensor(w, dtype=torch.int32).reshape(-1, 2).to(self.device)
-                          for w in bwd]
+            out["fwd"] = [torch.from_numpy(np.ascontiguousarray(w)).to(self.device) for w in fwd]
+            out["bwd"] = [torch.from_numpy(np.ascontiguousarray(w)).to(self.device) for w in bwd]
         out["n_fwd"] = [len(w) for w in fwd]
         out["n_bwd"] = [len(w) for w in bwd]
         return out
@@ -432,15 +471,19 @@ class PopulationMLP:
 
     # ------------------------------------------------------------------ evaluation
     @torch.no_grad()
-    def evaluate(self, x: torch.Tensor, y: torch.Tensor):
-        """Mean loss and accuracy per slot (numpy [capacity]; NaN for empty slots)."""
+    def evaluate(self, x: torch.Tensor, y: torch.Tensor, slots=None):
+        """Mean loss and accuracy per slot (numpy [capacity]; NaN for empty slots and for slots
+        outside ``slots`` when a subset is given)."""
         self._refresh()
         rows = x.shape[0]
+        subset = None if slots is None else set(int(s) for s in slots)
         if rows % 128 or rows > self.eval_batch:
             raise ValueError(f"eval rows must be a multiple of 128 and <= {self.eval_batch}")
         if self.backend == "hip":
             from ._lib import check, stream_ptr
             lib, tb, L = self._lib, self._tables["eval"], self.L
+            if subset is not None:
+                tb = self._subset_table(tb, subset)
             stream = stream_ptr(self.device)
             self.loss.zero_()
             self.correct.zero_()
@@ -466,6 +509,8 @@ class PopulationMLP:
             xf = x.float()
             em = self.emulate_bf16
             for s in self.active_slots():
+                if subset is not None and s not in subset:
+                    continue
                 cfg = self.members[s]
                 layers = self.layer_views(s)
                 a = xf
@@ -479,10 +524,20 @@ class PopulationMLP:
                 loss[s] = float(ls) / rows
                 acc[s] = float(cs) / rows
         for s in range(self.capacity):
-            if self.members[s] is None:
+            if self.members[s] is None or (subset is not None and s not in subset):
                 loss[s] = np.nan
                 acc[s] = np.nan
         return loss, acc
+
+    def _subset_table(self, tb: dict, subset) -> dict:
+        L = self.L
+        keep = np.zeros(self.capacity, dtype=bool)
+        keep[list(subset)] = True
+        out = dict(tb)
+        fwd = [w[keep[w[:, 0] // L]] for w in tb["fwd_np"]]
+        out["fwd"] = [torch.from_numpy(np.ascontiguousarray(w)).to(self.device) for w in fwd]
+        out["n_fwd"] = [len(w) for w in fwd]
+        return out
 
     def train_loss(self) -> np.ndarray:
         """Mean training loss of the last step per slot."""

@@ -306,9 +306,13 @@ class ReadOnlyDB:
 # In-memory backend
 # ----------------------------------------------------------------------------------------------
 class _Collection:
+    """Documents by ``_id`` plus indexes: unique ones reject duplicates, every single-field index
+    is also a hash index (value -> ids) that equality / ``$in`` queries use to avoid full scans."""
+
     def __init__(self):
-        self.docs: Dict[Any, dict] = {}  # _id -> doc (insertion-ordered)
-        self.indexes: Dict[str, tuple] = {}  # name -> (keys, unique, set of values)
+        self.docs: Dict[Any, dict] = {}  # hashable _id -> doc (insertion-ordered)
+        self.indexes: Dict[str, tuple] = {}  # name -> (fields, unique, set of values)
+        self.hash_index: Dict[str, Dict[Any, set]] = {}  # field -> value -> set(hashable _id)
         self._next_id = 1
         self.create_index("_id", unique=True)
 
@@ -328,33 +332,54 @@ class _Collection:
                     raise DuplicateKeyError(f"Duplicate key error: index={name} value={v}")
                 values.add(v)
         self.indexes[name] = (fields, unique, values)
+        if len(fields) == 1 and fields[0] != "_id" and fields[0] not in self.hash_index:
+            hidx: Dict[Any, set] = {}
+            for hid, d in self.docs.items():
+                hidx.setdefault(self._hval(d, fields[0]), set()).add(hid)
+            self.hash_index[fields[0]] = hidx
         return name
+
+    def drop_index(self, name):
+        fields, _, _ = self.indexes.pop(name)
+        if len(fields) == 1 and not any(f == fields for f, _, _ in self.indexes.values()):
+            self.hash_index.pop(fields[0], None)
+
+    @staticmethod
+    def _hval(doc, field):
+        v = _get_path(doc, field)
+        try:
+            return _hashable(None if v is _MISSING else v)
+        except TypeError:  # pragma: no cover - unhashable leaf
+            return repr(v)
 
     @staticmethod
     def _key(doc, fields):
-        return tuple(_hashable(None if (v := _get_path(doc, f)) is _MISSING else v) for f in fields)
+        return tuple(_hashable(None if (v := _get_path(doc, f)) is _MISSING else v)
+                     for f in fields)
 
-    def _check_unique(self, doc, exclude_id=_MISSING):
+    def _check_unique(self, doc):
         for name, (fields, unique, values) in self.indexes.items():
-            if not unique:
-                continue
-            v = self._key(doc, fields)
-            if v in values:
-                if exclude_id is not _MISSING:
-                    old = self.docs.get(exclude_id)
-                    if old is not None and self._key(old, fields) == v:
-                        continue
-                raise DuplicateKeyError(f"Duplicate key error: index={name} value={v}")
+            if unique and self._key(doc, fields) in values:
+                raise DuplicateKeyError(f"Duplicate key error: index={name} "
+                                        f"value={self._key(doc, fields)}")
 
     def _register(self, doc):
+        hid = _hashable(doc["_id"])
         for fields, unique, values in self.indexes.values():
             if unique:
                 values.add(self._key(doc, fields))
+        for field, hidx in self.hash_index.items():
+            hidx.setdefault(self._hval(doc, field), set()).add(hid)
 
     def _unregister(self, doc):
+        hid = _hashable(doc["_id"])
         for fields, unique, values in self.indexes.values():
             if unique:
                 values.discard(self._key(doc, fields))
+        for field, hidx in self.hash_index.items():
+            s = hidx.get(self._hval(doc, field))
+            if s is not None:
+                s.discard(hid)
 
     def insert(self, doc: dict):
         if "_id" not in doc:
@@ -367,11 +392,49 @@ class _Collection:
         self.docs[_hashable(stored["_id"])] = stored
         self._register(stored)
 
+    def _candidates(self, query):
+        """Ids narrowed by the most selective hash-indexed equality / $in clause, or None."""
+        best = None
+        for key, val in query.items():
+            if key not in self.hash_index:
+                continue
+            hidx = self.hash_index[key]
+            if isinstance(val, dict):
+                if set(val) == {"$in"}:
+                    ids = set()
+                    for v in val["$in"]:
+                        ids |= hidx.get(_hashable(v), set())
+                else:
+                    continue
+            else:
+                try:
+                    ids = hidx.get(_hashable(val), set())
+                except TypeError:  # pragma: no cover
+                    continue
+            if best is None or len(ids) < len(best):
+                best = ids
+        return best
+
     def find_iter(self, query):
         if query and set(query) == {"_id"} and not isinstance(query["_id"], dict):
             d = self.docs.get(_hashable(query["_id"]))
             return [d] if d is not None else []
+        if query:
+            cands = self._candidates(query)
+            if cands is not None:
+                # keep insertion order for deterministic "first match" semantics
+                if len(cands) * 8 < len(self.docs):
+                    docs = sorted((self.docs[i] for i in cands if i in self.docs),
+                                  key=lambda d: self._order(d))
+                else:
+                    docs = [d for i, d in self.docs.items() if i in cands]
+                return [d for d in docs if match(d, query)]
         return [d for d in self.docs.values() if match(d, query)]
+
+    def _order(self, doc):
+        if not hasattr(self, "_pos") or len(self._pos) != len(self.docs):
+            self._pos = {k: i for i, k in enumerate(self.docs)}
+        return self._pos.get(_hashable(doc["_id"]), 0)
 
     def update(self, doc: dict, data: dict):
         new = copy.deepcopy(doc)
@@ -424,7 +487,7 @@ class EphemeralDB(AbstractDB):
         col = self._col(collection_name)
         if name not in col.indexes:
             raise DatabaseError(f"index not found with name {name}")
-        del col.indexes[name]
+        col.drop_index(name)
 
     def write(self, collection_name, data, query=None):
         col = self._col(collection_name)

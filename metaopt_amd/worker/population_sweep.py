@@ -1,0 +1,332 @@
+"""Device population sweep: an experiment's trials trained as populations, one process per GPU.
+
+This is the device-side worker (north-star configs 1-3): instead of one subprocess per trial, each
+rank keeps ``capacity`` trials resident on its GPU (:class:`~metaopt_amd.ops.population.
+PopulationMLP`) and trains all of them with one set of kernel launches per step.
+
+Control flow (every ``sync_every`` steps -- trial budgets are multiples of it, so trials start and
+finish exactly on sync boundaries and no slot idles):
+
+1. each rank evaluates the members that reached their budget (validation loss/accuracy) and
+   keeps a device checkpoint of those that ASHA may promote;
+2. **C1**: one ``all_gather`` of a [capacity, 7] f64 status block per rank (trial key, steps,
+   budget, train loss, val loss, val acc, NaN flag) -- a few KB, latency-bound over xGMI;
+3. rank 0 (the only process touching the experiment storage) records completed/broken trials,
+   feeds them to the algorithm, asks it for as many points as there are free slots, registers
+   them (already ``reserved``), and places them: promotions on the rank holding the checkpoint,
+   new points on the least-loaded ranks;
+4. **C5**: one ``broadcast`` of a [world * capacity, 10] f64 assignment block; every rank
+   initialises new members, resumes promoted ones from their checkpoints, and continues.
+
+Fault tolerance: a member whose loss turns NaN/Inf is marked ``broken`` without stopping the
+population; in-flight trials get their storage heartbeat refreshed periodically, so if the job
+dies they become *lost* and other workers re-run them.
+"""
+from __future__ import annotations
+
+import collections
+import datetime
+import logging
+import math
+import time
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from ..core.trial import Trial
+from ..ops.population import MemberConfig, PopulationMLP
+from ..parallel.comm import Comm
+from ..storage.database import DuplicateKeyError
+from ..utils import format_trials
+
+log = logging.getLogger(__name__)
+
+NONE, NEW, RESUME, CLEAR = 0, 1, 2, 3
+ST_COLS = 7     # key, steps, budget, train_loss, val_loss, val_acc, bad
+AS_COLS = 10    # action, key, width, lr, momentum, wd, dropout, seed, budget, resume_key
+
+
+class PopulationSweep:
+    def __init__(self, pop: PopulationMLP, task, data, comm: Optional[Comm] = None,
+                 experiment=None, sync_every: int = 16, ckpt_capacity: int = 512,
+                 heartbeat_every: float = 30.0, max_trials: Optional[float] = None):
+        self.pop = pop
+        self.task = task
+        self.data = data
+        self.comm = comm or Comm(device=pop.device)
+        self.experiment = experiment
+        if self.comm.is_root and experiment is None:
+            raise ValueError("rank 0 needs the experiment")
+        self.sync_every = int(sync_every)
+        self.ckpt_capacity = int(ckpt_capacity)
+        self.heartbeat_every = heartbeat_every
+        P = pop.capacity
+        self.slot_key = np.full(P, -1, dtype=np.int64)
+        self.slot_budget = np.zeros(P, dtype=np.int64)
+        self.ckpts: "collections.OrderedDict[int, dict]" = collections.OrderedDict()
+        self.global_step = 0
+        self.samples = 0
+        self.done = False
+        # rank-0 bookkeeping
+        self.trials: Dict[int, Trial] = {}            # key -> reserved trial
+        self.key_params: Dict[int, dict] = {}
+        self.ckpt_index: Dict[str, tuple] = {}        # param key -> (rank, trial key, steps)
+        self.ckpt_fifo = [collections.deque() for _ in range(self.comm.world_size)]
+        self.next_key = 1
+        self.completed = 0
+        self.broken = 0
+        self.best = (math.inf, None)
+        self.history: List[tuple] = []                # (time, key, val_loss, budget)
+        self._last_hb = time.time()
+        self.max_trials = (max_trials if max_trials is not None else
+                           (experiment.max_trials if experiment is not None else math.inf))
+        if self.comm.is_root:
+            self.algorithm = experiment.algorithms
+            self.space = experiment.space
+
+    # ------------------------------------------------------------------ main loop
+    def start(self) -> None:
+        """Fill every slot of every rank (first sync with nothing running)."""
+        self._sync(evaluate=False)
+
+    def step(self) -> None:
+        x, y = self.data.batch(self.global_step)
+        self.pop.train_step(x, y)
+        self.global_step += 1
+        self.samples += self.pop.batch_size * int((self.slot_key >= 0).sum())
+        if self.global_step % self.sync_every == 0:
+            self._sync()
+
+    def run(self, max_steps: int) -> dict:
+        if self.global_step == 0 and (self.slot_key < 0).all():
+            self.start()
+        for _ in range(max_steps):
+            if self.done:
+                break
+            self.step()
+        return self.summary()
+
+    # ------------------------------------------------------------------ sync
+    def _local_status(self, evaluate=True) -> torch.Tensor:
+        pop = self.pop
+        P = pop.capacity
+        st = np.zeros((P, ST_COLS), dtype=np.float64)
+        st[:, 0] = self.slot_key
+        steps = np.array([pop.steps_done(s) for s in range(P)], dtype=np.float64)
+        st[:, 1] = steps
+        st[:, 2] = self.slot_budget
+        active = self.slot_key >= 0
+        if active.any() and self.global_step > 0:
+            tl = pop.train_loss()
+            st[:, 3] = np.where(active, tl, np.nan)
+            bad = active & ~np.isfinite(tl)
+            st[:, 6] = bad
+        finished = [s for s in range(P) if active[s] and steps[s] >= self.slot_budget[s]
+                    and not st[s, 6]]
+        if evaluate and finished:
+            vx, vy = self.data.validation()
+            vl, va = pop.evaluate(vx, vy, slots=finished)
+            st[finished, 4] = vl[finished]
+            st[finished, 5] = va[finished]
+            for s in finished:
+                if not math.isfinite(vl[s]):
+                    st[s, 6] = 1
+        return torch.from_numpy(st).to(self.comm._coll_device())
+
+    def _sync(self, evaluate=True) -> None:
+        P = self.pop.capacity
+        status = self._local_status(evaluate)
+        gathered = self.comm.all_gather_rows(status).cpu().numpy()          # C1
+        # one extra row carries the sweep-level "done" flag
+        assign = np.zeros((self.comm.world_size * P + 1, AS_COLS), dtype=np.float64)
+        if self.comm.is_root:
+            assign = self._decide(gathered)
+            assign[-1, 0] = float(self.done)
+        assign_t = torch.from_numpy(assign).to(self.comm._coll_device())
+        self.comm.broadcast_(assign_t, src=0)                               # C5
+        self._apply(gathered, assign_t.cpu().numpy())
+
+    # ------------------------------------------------------------------ rank 0
+    def _decide(self, gathered: np.ndarray) -> np.ndarray:
+        W, P = self.comm.world_size, self.pop.capacity
+        assign = np.zeros((W * P + 1, AS_COLS), dtype=np.float64)
+        free = []
+        done_pts, done_res = [], []
+        now = datetime.datetime.utcnow()
+        for row in range(W * P):
+            key = int(gathered[row, 0])
+            rank, slot = divmod(row, P)
+            if key < 0:
+                free.append(row)
+                continue
+            steps, budget = int(gathered[row, 1]), int(gathered[row, 2])
+            bad = gathered[row, 6] > 0
+            if not bad and steps < budget:
+                continue
+            trial = self.trials.pop(key, None)
+            params = self.key_params.pop(key, None)
+            free.append(row)
+            assign[row, 0] = CLEAR
+            if trial is None:
+                continue
+            if bad:
+                self.broken += 1
+                self._set_status(trial, "broken")
+                continue
+            vl, va, tl = float(gathered[row, 4]), float(gathered[row, 5]), float(gathered[row, 3])
+            trial.results = [Trial.Result(name="val_loss", type="objective", value=vl),
+                             Trial.Result(name="val_acc", type="statistic", value=va),
+                             Trial.Result(name="train_loss", type="statistic", value=tl)]
+            trial.status = "completed"
+            trial.end_time = now
+            self.experiment.storage.push_trial_results(trial)
+            self.completed += 1
+            self.history.append((time.time(), key, vl, budget))
+            if vl < self.best[0]:
+                self.best = (vl, dict(params))
+            done_pts.append(format_trials.trial_to_tuple(trial, self.space))
+            done_res.append({"objective": vl, "constraint": [], "gradient": None})
+            if budget < self._max_budget():
+                self._record_ckpt(self.task.key(params), rank, key, steps)
+        if done_pts:
+            self.algorithm.observe(done_pts, done_res)
+        self._heartbeat()
+        self._fill(free, assign)
+        return assign
+
+    def _max_budget(self) -> int:
+        dim = self.space[self.task.fidelity] if self.task.fidelity in self.space else None
+        return int(dim.high) if dim is not None else 0
+
+    def _record_ckpt(self, pkey, rank, key, steps):
+        fifo = self.ckpt_fifo[rank]
+        fifo.append(key)
+        self.ckpt_index[pkey] = (rank, key, steps)
+        while len(fifo) > self.ckpt_capacity:   # mirrors the owner's FIFO eviction exactly
+            old = fifo.popleft()
+            for pk, (r, k, _) in list(self.ckpt_index.items()):
+                if r == rank and k == old:
+                    del self.ckpt_index[pk]
+
+    def _fill(self, free_rows: List[int], assign: np.ndarray) -> None:
+        W, P = self.comm.world_size, self.pop.capacity
+        if self.done or not free_rows:
+            return
+        n_done = self.completed + self.broken
+        in_flight = len(self.trials)
+        budget_left = self.max_trials - n_done - in_flight
+        n = int(min(len(free_rows), budget_left)) if math.isfinite(budget_left) else len(free_rows)
+        if self.algorithm.is_done or n <= 0:
+            if in_flight == 0:
+                self.done = True
+            return
+        points = self.algorithm.suggest(n) or []
+        if not points and in_flight == 0:
+            self.done = True
+            return
+        free_by_rank = {r: [row for row in free_rows if row // P == r] for r in range(W)}
+        stamp = datetime.datetime.utcnow()
+        for point in points:
+            params = dict(zip(self.space.keys(), point))
+            pkey = self.task.key(params)
+            owner = self.ckpt_index.get(pkey)
+            if owner is not None and free_by_rank[owner[0]]:
+                row = free_by_rank[owner[0]].pop(0)
+                action, resume = RESUME, owner[1]
+                del self.ckpt_index[pkey]
+                try:  # the owner drops the checkpoint when it resumes it: mirror that
+                    self.ckpt_fifo[owner[0]].remove(owner[1])
+                except ValueError:
+                    pass
+            else:
+                rank = max(free_by_rank, key=lambda r: len(free_by_rank[r]))
+                if not free_by_rank[rank]:
+                    break
+                row = free_by_rank[rank].pop(0)
+                action, resume = NEW, -1
+            trial = format_trials.tuple_to_trial(point, self.space)
+            trial.experiment = self.experiment.id
+            trial.status = "reserved"
+            trial.submit_time = trial.start_time = trial.heartbeat = stamp
+            try:
+                self.experiment.storage.register_trial(trial)
+            except DuplicateKeyError:
+                log.debug("duplicate point %s skipped", point)
+                free_by_rank[row // P].insert(0, row)
+                continue
+            key = self.next_key
+            self.next_key += 1
+            self.trials[key] = trial
+            self.key_params[key] = params
+            cfg = self.task.member_config(params, self.task.seed_of(pkey))
+            assign[row] = (action, key, cfg.width, cfg.lr, cfg.momentum, cfg.weight_decay,
+                           cfg.dropout, cfg.seed, self.task.budget(params), resume)
+
+    def _set_status(self, trial, status):
+        try:
+            self.experiment.storage.set_trial_status(trial, status, was="reserved")
+        except Exception as exc:  # pragma: no cover - storage hiccup must not kill the sweep
+            log.warning("could not mark trial %s %s: %s", trial.id, status, exc)
+
+    def _heartbeat(self):
+        if time.time() - self._last_hb < self.heartbeat_every:
+            return
+        self._last_hb = time.time()
+        for t in self.trials.values():
+            self.experiment.storage.update_heartbeat(t)
+
+    # ------------------------------------------------------------------ every rank
+    def _apply(self, gathered: np.ndarray, assign: np.ndarray) -> None:
+        P = self.pop.capacity
+        r0 = self.comm.rank * P
+        pop = self.pop
+        mine = assign[r0:r0 + P]
+        g = gathered[r0:r0 + P]
+        max_b = None
+        # checkpoint every member that completed below the top budget (rank 0 mirrors the rule)
+        for s in range(P):
+            if mine[s, 0] == CLEAR and self.slot_key[s] >= 0:
+                finished_ok = g[s, 6] == 0 and g[s, 1] >= g[s, 2]
+                if max_b is None:
+                    max_b = self._max_budget_local()
+                if finished_ok and self.slot_budget[s] < max_b:
+                    self.ckpts[int(self.slot_key[s])] = pop.slot_state(s)
+                    while len(self.ckpts) > self.ckpt_capacity:
+                        self.ckpts.popitem(last=False)
+                pop.remove_member(s)
+                self.slot_key[s] = -1
+                self.slot_budget[s] = 0
+        for s in range(P):
+            a = mine[s]
+            act = int(a[0])
+            if act not in (NEW, RESUME):
+                continue
+            cfg = MemberConfig(width=int(a[2]), lr=float(a[3]), momentum=float(a[4]),
+                               weight_decay=float(a[5]), dropout=float(a[6]), seed=int(a[7]))
+            st = self.ckpts.pop(int(a[9]), None) if act == RESUME else None
+            if st is not None:
+                pop.load_slot_state(s, st)
+                pop.update_hparams(s, lr=cfg.lr, momentum=cfg.momentum,
+                                   weight_decay=cfg.weight_decay, dropout=cfg.dropout)
+            else:
+                pop.set_member(s, cfg, init=True)
+            self.slot_key[s] = int(a[1])
+            self.slot_budget[s] = int(a[8])
+        self.done = bool(assign[-1, 0])
+
+    def _max_budget_local(self) -> int:
+        return getattr(self, "_mb", None) or self._compute_mb()
+
+    def _compute_mb(self):
+        from ..space.builder import build_space
+        dim = build_space(self.task.priors)[self.task.fidelity]
+        self._mb = int(dim.high)
+        return self._mb
+
+    # ------------------------------------------------------------------ reporting
+    def summary(self) -> dict:
+        return {"global_step": self.global_step, "samples": self.samples,
+                "completed": self.completed, "broken": self.broken,
+                "best_val_loss": self.best[0], "best_params": self.best[1],
+                "active": int((self.slot_key >= 0).sum())}
