@@ -17,6 +17,7 @@ with three changes made for device populations:
 """
 from __future__ import annotations
 
+import bisect
 import copy
 import hashlib
 import logging
@@ -82,6 +83,8 @@ class ASHA(BaseAlgorithm):
             for bracket, rungs in zip(self.brackets, state_dict["rungs"]):
                 bracket.rungs = [(b, {k: (o, tuple(p)) for k, (o, p) in r.items()})
                                  for b, r in rungs]
+                bracket._sorted = [sorted((o, k) for k, (o, _) in r.items() if o is not None)
+                                   for _, r in bracket.rungs]
             self.trial_info = {k: self.brackets[i] for k, i in state_dict["trial_info"].items()}
 
     def full_state(self) -> dict:
@@ -94,20 +97,29 @@ class ASHA(BaseAlgorithm):
         return copy.deepcopy(st)
 
     def suggest(self, num=1):
+        """Promotions first (one at a time, each registered as pending), then all remaining new
+        points drawn in ONE vectorised ``space.sample`` call and spread over the brackets."""
         out = []
-        for _ in range(num):
-            p = self._suggest_one()
-            if p is None:
+        while len(out) < num:
+            cand = None
+            for bracket in self.brackets:
+                cand = bracket.update_rungs()
+                if cand is not None:
+                    bracket.register(cand, None, overwrite=False)
+                    break
+            if cand is None:
                 break
-            out.append(p)
+            out.append(cand)
+        remaining = num - len(out)
+        if remaining > 0:
+            out.extend(self._sample_new(remaining))
         return out or None
 
     def _suggest_one(self):
-        for bracket in self.brackets:
-            cand = bracket.update_rungs()
-            if cand is not None:
-                bracket.register(cand, None, overwrite=False)
-                return cand
+        pts = self.suggest(1)
+        return pts[0] if pts else None
+
+    def _current_brackets(self):
         current = self.brackets[-self.num_brackets:]
         if all(b.is_filled for b in current):
             if self._repetition >= (self.repetitions if self.repetitions is not None else 1):
@@ -119,21 +131,39 @@ class ASHA(BaseAlgorithm):
             self.brackets += [Bracket(self, self.eta, self.budgets[i:])
                               for i in range(self.num_brackets)]
             current = self.brackets[-self.num_brackets:]
-        for _ in range(100):
-            point = list(self.space.sample(1, seed=tuple(self.rng.randint(0, 1000000, size=3)))[0])
-            if self.get_id(point) not in self.trial_info:
+        return current
+
+    def _sample_new(self, n):
+        current = self._current_brackets()
+        if current is None:
+            return []
+        fi = self.fidelity_index
+        out = []
+        for _attempt in range(100):
+            need = n - len(out)
+            if need <= 0:
                 break
+            pts = self.space.sample(need, seed=tuple(self.rng.randint(0, 1000000, size=3)))
+            sizes = numpy.array([len(b.rungs) for b in current])
+            probs = numpy.e ** (sizes - sizes.max())
+            probs = numpy.array([p * int(not b.is_filled) for p, b in zip(probs, current)])
+            if probs.sum() <= 0:
+                break
+            picks = self.rng.choice(len(current), size=len(pts), p=probs / probs.sum())
+            for point, idx in zip(pts, picks):
+                point = list(point)
+                point[fi] = current[idx].rungs[0][0]
+                point = tuple(point)
+                _id = self.get_id(point)
+                if _id in self.trial_info:
+                    continue
+                self.trial_info[_id] = current[idx]
+                current[idx].register(point, None, overwrite=False)
+                out.append(point)
         else:
-            raise RuntimeError("ASHA keeps sampling already existing points.")
-        sizes = numpy.array([len(b.rungs) for b in current])
-        probs = numpy.e ** (sizes - sizes.max())
-        probs = numpy.array([p * int(not b.is_filled) for p, b in zip(probs, current)])
-        idx = self.rng.choice(len(current), p=probs / probs.sum())
-        point[self.fidelity_index] = current[idx].rungs[0][0]
-        point = tuple(point)
-        self.trial_info[self.get_id(point)] = current[idx]
-        current[idx].register(point, None, overwrite=False)
-        return point
+            if len(out) < n:
+                raise RuntimeError("ASHA keeps sampling already existing points.")
+        return out
 
     def get_id(self, point) -> str:
         p = list(point)
@@ -164,36 +194,57 @@ class ASHA(BaseAlgorithm):
 
     @property
     def fidelity_index(self) -> int:
-        return [i for i, d in enumerate(self.space.values()) if _is_fidelity(d)][0]
+        cached = self.__dict__.get("_fidelity_index")
+        if cached is not None and cached[0] is self.space:
+            return cached[1]
+        idx = [i for i, d in enumerate(self.space.values()) if _is_fidelity(d)][0]
+        self.__dict__["_fidelity_index"] = (self.space, idx)
+        return idx
 
 
 class Bracket:
-    """Rungs ``[(budget, {id: (objective, point)})]`` of one ASHA bracket."""
+    """Rungs ``[(budget, {id: (objective, point)})]`` of one ASHA bracket.
+
+    Each rung also keeps its completed entries sorted by objective (``bisect``), so a promotion
+    query is O(k) instead of re-sorting the rung (population sweeps put thousands of points in the
+    bottom rung)."""
 
     def __init__(self, asha, reduction_factor, budgets):
         self.asha = asha
         self.reduction_factor = reduction_factor
         self.rungs = [(int(b), dict()) for b in budgets]
+        self._sorted = [[] for _ in budgets]
 
     def register(self, point, objective, overwrite=True):
         fid = point[self.asha.fidelity_index]
-        rungs = [r for b, r in self.rungs if b == fid]
-        if not rungs:
+        idx = [i for i, (b, _) in enumerate(self.rungs) if b == fid]
+        if not idx:
             raise IndexError(f"Bad fidelity level {fid}. Should be in "
                              f"{[b for b, _ in self.rungs]}. Params: {point}")
+        i = idx[0]
+        rung = self.rungs[i][1]
         _id = self.asha.get_id(point)
-        if overwrite or _id not in rungs[0]:
-            rungs[0][_id] = (objective, tuple(point))
+        if not overwrite and _id in rung:
+            return
+        old = rung.get(_id)
+        if old is not None and old[0] is not None:
+            srt = self._sorted[i]
+            j = bisect.bisect_left(srt, (old[0], _id))
+            if j < len(srt) and srt[j] == (old[0], _id):
+                del srt[j]
+        rung[_id] = (objective, tuple(point))
+        if objective is not None:
+            bisect.insort(self._sorted[i], (objective, _id))
 
     def get_candidate(self, rung_id):
         _, rung = self.rungs[rung_id]
         nxt = self.rungs[rung_id + 1][1]
-        done = sorted(((o, p) for o, p in rung.values() if o is not None), key=lambda x: x[0])
-        k = min(len(rung) // self.reduction_factor, len(done))
+        srt = self._sorted[rung_id]
+        k = min(len(rung) // self.reduction_factor, len(srt))
         for i in range(k):
-            point = done[i][1]
-            if self.asha.get_id(point) not in nxt:
-                return point
+            _id = srt[i][1]
+            if _id not in nxt:
+                return rung[_id][1]
         return None
 
     @property

@@ -76,8 +76,8 @@ class ExperimentBuilder:
     def setup_storage(self, config):
         if self._storage is not None:
             return self._storage
-        if storage_is_set() and not config.get("debug") and not config.get("force_storage"):
-            return get_storage()
+        if storage_is_set() and not config.get("force_storage"):
+            return get_storage()  # process-wide storage: the first configuration wins
         db = dict(config.get("database") or {})
         return setup_storage({"database": db}, debug=bool(config.get("debug")))
 

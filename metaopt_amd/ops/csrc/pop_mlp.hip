@@ -38,6 +38,17 @@ struct MlpTL {
   int64_t pad;
 };
 
+// One (member, layer) to initialise; 48 bytes, mirrored by metaopt_amd/ops/population.py.
+struct InitDesc {
+  int64_t w_off, b_off;   // W [N][K] and bias [N] offsets (elements)
+  int32_t K, N;           // padded dims
+  int32_t k_real, n_real; // real dims (outside them: zeros)
+  uint32_t seed;          // member seed
+  int32_t layer;
+  float bound;            // U(-bound, bound), bound = 1/sqrt(k_real) computed on the host
+  int32_t pad;
+};
+
 // Per-trial hyper-parameters; 32 bytes.  SGD: b1 = momentum.  AdamW: b1, b2, eps, t = step count.
 struct TrialHP {
   float lr, b1, wd, drop, b2, eps;
@@ -482,6 +493,40 @@ __global__ __launch_bounds__(256) void mlp_bwd_opt_kernel(const MlpTL* __restric
   }
 }
 
+// Member initialisation (torch.nn.Linear-style U(-1/sqrt(fan_in), +)) for every new member of a
+// sync in ONE launch: weights and bias from the counter-based RNG (so the PyTorch reference draws
+// the same values), zero padding, the bf16 copy, and zeroed optimizer state.  Replaces ~10 small
+// framework launches per member.
+__global__ __launch_bounds__(256) void mlp_init_kernel(const InitDesc* __restrict__ descs,
+                                                       float* __restrict__ p32,
+                                                       bf16_t* __restrict__ p16,
+                                                       float* __restrict__ m32,
+                                                       float* __restrict__ v32, int zero_v) {
+  const InitDesc d = descs[blockIdx.y];
+  const uint32_t wkey = rng_key(d.seed, 0x1000u + (uint32_t)d.layer, 0u);
+  const uint32_t bkey = rng_key(d.seed, 0x2000u + (uint32_t)d.layer, 0u);
+  const int64_t nw = (int64_t)d.N * d.K;
+  const int64_t total = nw + d.N;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    float v = 0.f;
+    int64_t o;
+    if (e < nw) {
+      const int n = (int)(e / d.K), k = (int)(e - (int64_t)n * d.K);
+      if (n < d.n_real && k < d.k_real) v = (2.f * rng_uniform(wkey, (uint32_t)e) - 1.f) * d.bound;
+      o = d.w_off + e;
+    } else {
+      const int n = (int)(e - nw);
+      if (n < d.n_real) v = (2.f * rng_uniform(bkey, (uint32_t)n) - 1.f) * d.bound;
+      o = d.b_off + n;
+    }
+    p32[o] = v;
+    p16[o] = f2bf(v);
+    m32[o] = 0.f;
+    if (zero_v) v32[o] = 0.f;
+  }
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------------------------
@@ -489,7 +534,16 @@ __global__ __launch_bounds__(256) void mlp_bwd_opt_kernel(const MlpTL* __restric
 // ------------------------------------------------------------------------------------------------
 extern "C" {
 
-int mopt_abi_version() { return 3; }
+int mopt_abi_version() { return 4; }
+
+int mopt_mlp_init(const void* descs, int n_desc, void* p32, void* p16, void* m32, void* v32,
+                  int zero_v, void* stream) {
+  if (n_desc <= 0) return 0;
+  hipLaunchKernelGGL(mlp_init_kernel, dim3(64, n_desc), dim3(256), 0, (hipStream_t)stream,
+                     (const InitDesc*)descs, (float*)p32, (bf16_t*)p16, (float*)m32, (float*)v32,
+                     zero_v);
+  return (int)hipGetLastError();
+}
 
 int mopt_mlp_fwd(const void* tls, const void* work, int n_work, int n_rowblocks, const void* xb,
                  const void* p32, const void* p16, void* act, const void* hp, unsigned step,

@@ -35,7 +35,10 @@ TL_DTYPE = np.dtype([("K", "<i4"), ("N", "<i4"), ("trial", "<i4"), ("n_real", "<
                      ("gx_off", "<i8"), ("pad", "<i8")])
 HP_DTYPE = np.dtype([("lr", "<f4"), ("b1", "<f4"), ("wd", "<f4"), ("drop", "<f4"),
                      ("b2", "<f4"), ("eps", "<f4"), ("seed", "<u4"), ("t", "<u4")])
-assert TL_DTYPE.itemsize == 64 and HP_DTYPE.itemsize == 32
+INIT_DTYPE = np.dtype([("w_off", "<i8"), ("b_off", "<i8"), ("K", "<i4"), ("N", "<i4"),
+                       ("k_real", "<i4"), ("n_real", "<i4"), ("seed", "<u4"), ("layer", "<i4"),
+                       ("bound", "<f4"), ("pad", "<i4")])
+assert TL_DTYPE.itemsize == 64 and HP_DTYPE.itemsize == 32 and INIT_DTYPE.itemsize == 48
 
 TILE = 64
 FWD_RELU, FWD_DROPOUT, FWD_WRITE_GRAD = 1, 2, 4
@@ -132,6 +135,7 @@ class PopulationMLP:
         self.hp = np.zeros(self.capacity, dtype=HP_DTYPE)
         self.hp_dev = torch.zeros(self.capacity * HP_DTYPE.itemsize, dtype=torch.uint8, device=dev)
         self.members: List[Optional[MemberConfig]] = [None] * self.capacity
+        self._pending_init = set()
         self._dirty = True
         self._tables: Dict[str, dict] = {}
 
@@ -203,7 +207,11 @@ class PopulationMLP:
         self.hp_dev.copy_(host, non_blocking=False)
 
     def set_member(self, slot: int, cfg: MemberConfig, init: bool = True) -> None:
-        """Place ``cfg`` in ``slot``; with ``init`` draw fresh weights (torch.nn.Linear init)."""
+        """Place ``cfg`` in ``slot``; with ``init`` draw fresh weights (torch.nn.Linear-style
+        U(-1/sqrt(fan_in), 1/sqrt(fan_in)) from the member's counter-based RNG stream).
+
+        Initialisation is deferred and batched: every member set before the next train/eval call
+        is initialised by one kernel launch."""
         if cfg.width > self.max_width or cfg.width < 1:
             raise ValueError(f"width {cfg.width} outside [1, {self.max_width}]")
         if not (0.0 <= cfg.dropout < 1.0):
@@ -211,7 +219,7 @@ class PopulationMLP:
         self.members[slot] = cfg
         self._write_hp(slot, cfg, 0)
         if init:
-            self._init_slot(slot)
+            self._pending_init.add(slot)
         self._dirty = True
 
     def update_hparams(self, slot: int, **changes) -> None:
@@ -225,6 +233,7 @@ class PopulationMLP:
         self._dirty = True
 
     def remove_member(self, slot: int) -> None:
+        self._pending_init.discard(slot)
         self.members[slot] = None
         self.hp[slot] = np.zeros((), dtype=HP_DTYPE)
         self._dirty = True
@@ -236,27 +245,48 @@ class PopulationMLP:
         b = self.slot_base(slot)
         return slice(b, b + self.slot_params)
 
-    def _init_slot(self, slot: int) -> None:
-        cfg = self.members[slot]
-        reg = self._region(slot)
-        self.p32[reg].zero_()
-        self.m32[reg].zero_()
-        if self.optimizer == "adamw":
-            self.v32[reg].zero_()
-        gen = torch.Generator(device=self.device)
-        gen.manual_seed(int(cfg.seed) & 0x7FFFFFFFFFFFFFFF)
-        base = self.slot_base(slot)
-        for (k, n), (kr, nr), (wo, bo) in zip(self.layer_dims(cfg.width), self.real_dims(cfg.width),
-                                              self.param_offsets(cfg.width)):
-            bound = 1.0 / math.sqrt(kr)
-            w = self.p32[base + wo: base + wo + n * k].view(n, k)
-            w[:nr, :kr] = (torch.rand(nr, kr, generator=gen, device=self.device) * 2 - 1) * bound
-            b = self.p32[base + bo: base + bo + n]
-            b[:nr] = (torch.rand(nr, generator=gen, device=self.device) * 2 - 1) * bound
-        self.p16[reg] = self.p32[reg].to(torch.bfloat16)
+    def _init_descs(self, slots) -> np.ndarray:
+        rows = []
+        for slot in slots:
+            cfg = self.members[slot]
+            base = self.slot_base(slot)
+            for l, ((k, n), (kr, nr), (wo, bo)) in enumerate(zip(
+                    self.layer_dims(cfg.width), self.real_dims(cfg.width),
+                    self.param_offsets(cfg.width))):
+                bound = float(np.float32(1.0) / np.sqrt(np.float32(kr)))
+                rows.append((base + wo, base + bo, k, n, kr, nr, cfg.seed & 0xFFFFFFFF, l, bound, 0))
+        return np.array(rows, dtype=INIT_DTYPE)
+
+    def _run_pending_init(self) -> None:
+        if not self._pending_init:
+            return
+        slots = sorted(s for s in self._pending_init if self.members[s] is not None)
+        self._pending_init.clear()
+        if not slots:
+            return
+        descs = self._init_descs(slots)
+        if self.backend == "hip":
+            from ._lib import check, stream_ptr
+            d = torch.from_numpy(descs.view(np.uint8).copy()).to(self.device)
+            check(self._lib.mopt_mlp_init(d.data_ptr(), len(descs), self.p32.data_ptr(),
+                                          self.p16.data_ptr(), self.m32.data_ptr(),
+                                          self.v32.data_ptr(), int(self.optimizer == "adamw"),
+                                          stream_ptr(self.device)), "mlp_init")
+            self._init_keep = d  # keep the descriptor alive until the launch has run
+        else:
+            for row in descs:
+                ref.init_layer(self.p32, self.m32, self.v32 if self.optimizer == "adamw" else None,
+                               int(row["w_off"]), int(row["b_off"]), int(row["K"]), int(row["N"]),
+                               int(row["k_real"]), int(row["n_real"]), int(row["seed"]),
+                               int(row["layer"]), float(row["bound"]))
+            for s in slots:
+                b = self.slot_base(s)
+                n = self.used_params(s)
+                self.p16[b:b + n] = self.p32[b:b + n].to(torch.bfloat16)
 
     def layer_views(self, slot: int, buf: torch.Tensor = None):
         """[(W [N,K], b [N])] views of ``buf`` (default: f32 master) for the member in ``slot``."""
+        self._run_pending_init()
         buf = self.p32 if buf is None else buf
         cfg = self.members[slot]
         base = self.slot_base(slot)
@@ -274,6 +304,7 @@ class PopulationMLP:
     def slot_state(self, slot: int, to_cpu: bool = False) -> dict:
         """Device checkpoint of a member: config, step count, weights and optimizer state
         (only the used prefix of the slot region is copied)."""
+        self._run_pending_init()
         b = self.slot_base(slot)
         reg = slice(b, b + self.used_params(slot))
         mv = (lambda t: t.detach().cpu().clone()) if to_cpu else (lambda t: t.detach().clone())
@@ -284,6 +315,7 @@ class PopulationMLP:
         return st
 
     def load_slot_state(self, slot: int, state: dict) -> None:
+        self._pending_init.discard(slot)
         cfg = MemberConfig(**state["config"])
         self.members[slot] = cfg
         self._write_hp(slot, cfg, int(state["t"]))
@@ -298,6 +330,8 @@ class PopulationMLP:
 
     def copy_member(self, src: int, dst: int, **hp_changes) -> None:
         """PBT exploit inside one device: dst <- src (weights, optimizer state, step count)."""
+        self._run_pending_init()
+        self._pending_init.discard(dst)
         rs, rd = self._region(src), self._region(dst)
         self.p32[rd].copy_(self.p32[rs])
         self.p16[rd].copy_(self.p16[rs])
@@ -363,6 +397,7 @@ class PopulationMLP:
         return out
 
     def _refresh(self) -> None:
+        self._run_pending_init()
         if not self._dirty:
             return
         self._tables = {"train": self._build_tables(self.batch_size),

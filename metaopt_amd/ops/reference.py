@@ -115,3 +115,26 @@ def adamw_update(w, m, v, g, lr, b1, b2, eps, wd, t):
     bc2 = 1.0 - b2 ** t
     denom = v.sqrt() / math.sqrt(bc2) + eps
     w.sub_((lr / bc1) * m / denom)
+
+
+def init_layer(p32, m32, v32, w_off, b_off, K, N, k_real, n_real, seed, layer, bound):
+    """Reference of ``mlp_init_kernel`` for one (member, layer): same RNG stream, same values."""
+    dev = p32.device
+    wkey = rng_key(seed, 0x1000 + layer, 0)
+    bkey = rng_key(seed, 0x2000 + layer, 0)
+    idx = torch.arange(N * K, device=dev, dtype=torch.int64)
+    u = rng_uniform(wkey, idx)
+    b32 = torch.tensor(bound, dtype=torch.float32, device=dev)
+    w = (u * 2.0 - 1.0) * b32
+    n = idx // K
+    k = idx - n * K
+    w = torch.where((n < n_real) & (k < k_real), w, torch.zeros_like(w))
+    p32[w_off:w_off + N * K] = w
+    bi = torch.arange(N, device=dev, dtype=torch.int64)
+    bv = (rng_uniform(bkey, bi) * 2.0 - 1.0) * b32
+    p32[b_off:b_off + N] = torch.where(bi < n_real, bv, torch.zeros_like(bv))
+    m32[w_off:w_off + N * K] = 0
+    m32[b_off:b_off + N] = 0
+    if v32 is not None:
+        v32[w_off:w_off + N * K] = 0
+        v32[b_off:b_off + N] = 0

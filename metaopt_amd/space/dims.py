@@ -128,8 +128,12 @@ class Dimension:
         raise NotImplementedError
 
     def interval(self, alpha=1.0):
-        """(low inclusive, high exclusive) covering ``alpha`` of the prior's mass."""
-        return self.prior.interval(alpha, *self._args, **self._kwargs)
+        """(low inclusive, high exclusive) covering ``alpha`` of the prior's mass (cached: priors
+        are immutable and scipy's ``interval`` costs tens of microseconds)."""
+        cache = self.__dict__.setdefault("_interval_cache", {})
+        if alpha not in cache:
+            cache[alpha] = self.prior.interval(alpha, *self._args, **self._kwargs)
+        return cache[alpha]
 
     def __contains__(self, point):
         raise NotImplementedError
@@ -199,6 +203,10 @@ class Real(Dimension):
         super().__init__(name, prior, *args, **kwargs)
 
     def __contains__(self, point):
+        if not self.shape and isinstance(point, (int, float, numpy.number)) and \
+                not isinstance(point, (bool, numpy.bool_)):
+            low, high = self.interval()  # scalar fast path (the common case, no numpy)
+            return bool(low <= point < high)
         if not _is_numeric_array(point):
             return False
         low, high = self.interval()
@@ -269,6 +277,9 @@ class Integer(Real, _Discrete):
     """Integer dimension: prior draws are floored (``numpy.floor``), like the reference."""
 
     def __contains__(self, point):
+        if not self.shape and isinstance(point, (int, float, numpy.number)) and \
+                not isinstance(point, (bool, numpy.bool_)):
+            return float(point) % 1 == 0 and super().__contains__(point)
         if not _is_numeric_array(point):
             return False
         p = numpy.asarray(point)
@@ -508,16 +519,23 @@ class Space(dict):
         return "Space([{}])".format(",\n       ".join(map(str, self.values())))
 
     def items(self):
-        return [(k, self[k]) for k in self.keys()]
+        return [(k, dict.__getitem__(self, k)) for k in self._sorted_keys()]
 
     def values(self):
-        return [self[k] for k in self.keys()]
+        return [dict.__getitem__(self, k) for k in self._sorted_keys()]
 
     def keys(self):
-        return list(iter(self))
+        return list(self._sorted_keys())
+
+    def _sorted_keys(self):
+        cache = getattr(self, "_keys_cache", None)
+        if cache is None or cache[0] != len(self):
+            cache = (len(self), tuple(sorted(dict.keys(self))))
+            self._keys_cache = cache
+        return cache[1]
 
     def __iter__(self):
-        return iter(sorted(super().keys()))
+        return iter(self._sorted_keys())
 
     def point_to_dict(self, point: Sequence) -> dict:
         return dict(zip(self.keys(), point))
