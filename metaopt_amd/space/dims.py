@@ -193,7 +193,8 @@ class Dimension:
 class Real(Dimension):
     """Real-valued dimension; optional ``low``/``high`` kwargs truncate the prior's support."""
 
-    MAX_TRIES = 4  # same redraw budget as the reference (space.py:371-391), applied per entry
+    MAX_TRIES = 4  # reference space.py:371-391 gives each draw 4 tries; here 4 rounds that
+    #               accept nothing abort (per-entry tries make large batches fail spuriously)
 
     def __init__(self, name, prior, *args, **kwargs):
         self._low = kwargs.pop("low", -numpy.inf)
@@ -228,18 +229,24 @@ class Real(Dimension):
     def sample(self, n_samples=1, seed=None):
         rng = check_random_state(seed)
         draws = self._rvs(n_samples, rng).astype(float, copy=False)
+        draws = self._redraw(draws, rng, lambda k: self._rvs(k, rng).astype(float, copy=False))
+        return [self._post(d) for d in draws]
+
+    def _redraw(self, draws, rng, draw_fn):
+        """Redraw out-of-bound entries; give up after MAX_TRIES rounds that accept nothing."""
         ok = self._in_bounds(draws)
-        tries = 1
+        stalled = 1 if not ok.any() else 0
         while not ok.all():
-            if tries >= self.MAX_TRIES:
+            if stalled >= self.MAX_TRIES:
                 raise ValueError(f"Improbable bounds: (low={self._low}, high={self._high}). "
                                  "Please make interval larger.")
             bad = numpy.nonzero(~ok)[0]
-            redraw = self._rvs(len(bad), rng).astype(float, copy=False)
+            redraw = draw_fn(len(bad))
             draws[bad] = redraw
-            ok[bad] = self._in_bounds(redraw)
-            tries += 1
-        return [self._post(d) for d in draws]
+            acc = self._in_bounds(redraw)
+            ok[bad] = acc
+            stalled = 0 if acc.any() else stalled + 1
+        return draws
 
     def cast(self, point):
         out = numpy.asarray(point).astype(float)
@@ -290,17 +297,8 @@ class Integer(Real, _Discrete):
     def sample(self, n_samples=1, seed=None):
         rng = check_random_state(seed)
         draws = numpy.floor(self._rvs(n_samples, rng).astype(float))
-        ok = self._in_bounds(draws)
-        tries = 1
-        while not ok.all():
-            if tries >= self.MAX_TRIES:
-                raise ValueError(f"Improbable bounds: (low={self._low}, high={self._high}). "
-                                 "Please make interval larger.")
-            bad = numpy.nonzero(~ok)[0]
-            redraw = numpy.floor(self._rvs(len(bad), rng).astype(float))
-            draws[bad] = redraw
-            ok[bad] = self._in_bounds(redraw)
-            tries += 1
+        draws = self._redraw(draws, rng,
+                             lambda k: numpy.floor(self._rvs(k, rng).astype(float)))
         draws = draws.astype(int)
         return [d if self.shape else int(d) for d in draws]
 

@@ -125,25 +125,29 @@ def match(doc: dict, query: Optional[dict]) -> bool:
     return True
 
 
-def _set_path(doc, key: str, value):
+def _set_path(doc, key: str, value, cow: bool = False):
+    """Set a dotted key; with ``cow`` every dict on the path is shallow-copied first, so a
+    shallow copy of a document can be updated without touching the original's nested dicts."""
     parts = key.split(".")
     cur = doc
     for p in parts[:-1]:
         nxt = cur.get(p)
         if not isinstance(nxt, dict):
             nxt = {}
-            cur[p] = nxt
+        elif cow:
+            nxt = dict(nxt)
+        cur[p] = nxt
         cur = nxt
     cur[parts[-1]] = value
 
 
-def apply_update(doc: dict, data: dict) -> None:
+def apply_update(doc: dict, data: dict, cow: bool = False) -> None:
     """``$set`` (default when no operator is given), ``$inc``, ``$unset``, ``$push``."""
     if any(k.startswith("$") for k in data):
         for op, fields in data.items():
             for key, value in _flatten_set(fields).items():
                 if op == "$set":
-                    _set_path(doc, key, copy.deepcopy(value))
+                    _set_path(doc, key, copy.deepcopy(value), cow)
                 elif op == "$inc":
                     cur = _get_path(doc, key)
                     _set_path(doc, key, (0 if cur is _MISSING or cur is None else cur) + value)
@@ -160,7 +164,7 @@ def apply_update(doc: dict, data: dict) -> None:
                     raise ValueError(f"Update operator '{op}' is not supported")
     else:
         for key, value in _flatten_set(data).items():
-            _set_path(doc, key, copy.deepcopy(value))
+            _set_path(doc, key, copy.deepcopy(value), cow)
 
 
 def _flatten_set(fields: dict) -> dict:
@@ -437,8 +441,8 @@ class _Collection:
         return self._pos.get(_hashable(doc["_id"]), 0)
 
     def update(self, doc: dict, data: dict):
-        new = copy.deepcopy(doc)
-        apply_update(new, data)
+        new = dict(doc)                  # copy-on-write: untouched sub-documents are shared
+        apply_update(new, data, cow=True)
         if new.get("_id") != doc.get("_id"):
             raise DatabaseError("cannot change _id")
         self._unregister(doc)

@@ -28,6 +28,8 @@ import collections
 import datetime
 import logging
 import math
+import queue
+import threading
 import time
 from typing import Dict, List, Optional
 
@@ -74,6 +76,7 @@ class PopulationSweep:
         self.ckpt_index: Dict[str, tuple] = {}        # param key -> (rank, trial key, steps)
         self.ckpt_fifo = [collections.deque() for _ in range(self.comm.world_size)]
         self.next_key = 1
+        self._registered = set()
         self.completed = 0
         self.broken = 0
         self.best = (math.inf, None)
@@ -81,9 +84,11 @@ class PopulationSweep:
         self._last_hb = time.time()
         self.max_trials = (max_trials if max_trials is not None else
                            (experiment.max_trials if experiment is not None else math.inf))
+        self._writer = None
         if self.comm.is_root:
             self.algorithm = experiment.algorithms
             self.space = experiment.space
+            self._writer = _WriteBehind(experiment.storage)
 
     # ------------------------------------------------------------------ main loop
     def start(self) -> None:
@@ -180,7 +185,7 @@ class PopulationSweep:
                              Trial.Result(name="train_loss", type="statistic", value=tl)]
             trial.status = "completed"
             trial.end_time = now
-            self.experiment.storage.push_trial_results(trial)
+            self._writer.put("push_trial_results", trial)
             self.completed += 1
             self.history.append((time.time(), key, vl, budget))
             if vl < self.best[0]:
@@ -249,12 +254,12 @@ class PopulationSweep:
             trial.experiment = self.experiment.id
             trial.status = "reserved"
             trial.submit_time = trial.start_time = trial.heartbeat = stamp
-            try:
-                self.experiment.storage.register_trial(trial)
-            except DuplicateKeyError:
+            if trial.id in self._registered:
                 log.debug("duplicate point %s skipped", point)
                 free_by_rank[row // P].insert(0, row)
                 continue
+            self._registered.add(trial.id)
+            self._writer.put("register_trial", trial)
             key = self.next_key
             self.next_key += 1
             self.trials[key] = trial
@@ -264,17 +269,24 @@ class PopulationSweep:
                            cfg.dropout, cfg.seed, self.task.budget(params), resume)
 
     def _set_status(self, trial, status):
-        try:
-            self.experiment.storage.set_trial_status(trial, status, was="reserved")
-        except Exception as exc:  # pragma: no cover - storage hiccup must not kill the sweep
-            log.warning("could not mark trial %s %s: %s", trial.id, status, exc)
+        self._writer.put("set_trial_status", trial, status, was="reserved")
 
     def _heartbeat(self):
         if time.time() - self._last_hb < self.heartbeat_every:
             return
         self._last_hb = time.time()
-        for t in self.trials.values():
-            self.experiment.storage.update_heartbeat(t)
+        for t in list(self.trials.values()):
+            self._writer.put("update_heartbeat", t)
+
+    def flush(self) -> None:
+        """Wait until every queued storage write has been applied."""
+        if self._writer is not None:
+            self._writer.flush()
+
+    def close(self) -> None:
+        if self._writer is not None:
+            self._writer.close()
+            self._writer = None
 
     # ------------------------------------------------------------------ every rank
     def _apply(self, gathered: np.ndarray, assign: np.ndarray) -> None:
@@ -326,7 +338,54 @@ class PopulationSweep:
 
     # ------------------------------------------------------------------ reporting
     def summary(self) -> dict:
+        self.flush()
         return {"global_step": self.global_step, "samples": self.samples,
                 "completed": self.completed, "broken": self.broken,
                 "best_val_loss": self.best[0], "best_params": self.best[1],
                 "active": int((self.slot_key >= 0).sum())}
+
+
+class _WriteBehind:
+    """Storage writes applied in order by a background thread (write-behind).
+
+    The sweep's decisions never read back what it writes (rank 0 keeps its own bookkeeping), so
+    persisting trials -- registration, results, status changes, heartbeats -- can overlap the
+    GPU work instead of stalling every sync.  ``flush`` waits for the queue to drain; a failing
+    write is logged and the queue continues.
+    """
+
+    def __init__(self, storage):
+        self.storage = storage
+        self.q: "queue.Queue" = queue.Queue()
+        self.errors = 0
+        self._t = threading.Thread(target=self._run, daemon=True)
+        self._t.start()
+
+    def put(self, method, *args, **kwargs):
+        # snapshot trials: the sweep keeps mutating its objects after queueing them
+        args = tuple(Trial(**a.to_dict()) if isinstance(a, Trial) else a for a in args)
+        self.q.put((method, args, kwargs))
+
+    def _run(self):
+        while True:
+            item = self.q.get()
+            try:
+                if item is None:
+                    return
+                method, args, kwargs = item
+                try:
+                    getattr(self.storage, method)(*args, **kwargs)
+                except DuplicateKeyError:
+                    log.debug("duplicate write skipped (%s)", method)
+                except Exception as exc:  # pragma: no cover - storage hiccup
+                    self.errors += 1
+                    log.warning("storage write %s failed: %s", method, exc)
+            finally:
+                self.q.task_done()
+
+    def flush(self):
+        self.q.join()
+
+    def close(self):
+        self.q.put(None)
+        self._t.join()

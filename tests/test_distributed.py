@@ -1,0 +1,103 @@
+"""Multi-process (gloo, CPU) tests of the device data plane: collectives and the sharded
+population sweep (rank 0 owns the experiment; C1 all-gather + C5 broadcast every sync)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _init(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from metaopt_amd.parallel.comm import init_from_env
+    return init_from_env(backend="gloo")
+
+
+def _collectives_worker(rank, world, port, q):
+    comm = _init(rank, world, port)
+    rows = torch.full((3, 2), float(rank))
+    g = comm.all_gather_rows(rows)
+    t = torch.tensor([7.0 if rank == 0 else 0.0])
+    comm.broadcast_(t)
+    s = torch.tensor([float(rank + 1)])
+    comm.all_reduce_(s)
+    mx = comm.max_float(rank * 2.5)
+    if rank == 0:
+        comm.send_tensor(torch.arange(4.0), dst=1)
+        got = None
+    else:
+        got = comm.recv_tensor(torch.empty(4), src=0).tolist()
+    q.put((rank, g[:, 0].tolist(), float(t), float(s), mx, got))
+    dist.destroy_process_group()
+
+
+def test_collectives_gloo():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_collectives_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    for rank, gathered, b, s, mx, got in res:
+        assert gathered == [0, 0, 0, 1, 1, 1]
+        assert b == 7.0 and s == 3.0 and mx == 2.5
+    assert res[1][5] == [0.0, 1.0, 2.0, 3.0]
+
+
+def _sweep_worker(rank, world, port, q):
+    comm = _init(rank, world, port)
+    from metaopt_amd.io.experiment_builder import build_experiment
+    from metaopt_amd.models.data import TeacherClassification
+    from metaopt_amd.models.mlp import MLPSweepTask
+    from metaopt_amd.ops.population import PopulationMLP
+    from metaopt_amd.storage.database import EphemeralDB
+    from metaopt_amd.storage.protocol import DocumentStorage
+    from metaopt_amd.worker.population_sweep import PopulationSweep
+    priors = {"/lr": "loguniform(1e-3, 1.0)", "/width": "loguniform(64, 128, discrete=True)",
+              "/steps": "fidelity(16, 64, 2)"}
+    exp = None
+    if rank == 0:
+        exp = build_experiment("dist-sweep", priors=priors,
+                               algorithms={"asha": {"seed": 3, "repetitions": float("inf")}},
+                               max_trials=20, storage=DocumentStorage(EphemeralDB()))
+    data = TeacherClassification(n_train=512, n_val=128, batch_size=128, seed=1)
+    pop = PopulationMLP(3, max_width=128, eval_batch=128, device="cpu")
+    sweep = PopulationSweep(pop, MLPSweepTask(priors=priors, max_width=128), data, comm=comm,
+                            experiment=exp, sync_every=16)
+    summary = sweep.run(2000)
+    sweep.close()
+    statuses = None
+    if rank == 0:
+        statuses = [t.status for t in exp.fetch_trials()]
+    q.put((rank, sweep.samples, summary["completed"], statuses, sweep.done))
+    dist.destroy_process_group()
+
+
+def test_sharded_sweep_gloo_world2():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_sweep_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=600) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    (r0, samples0, done0, statuses, fin0), (r1, samples1, _, _, fin1) = res
+    assert samples0 > 0 and samples1 > 0          # both ranks trained trials
+    assert done0 == 20 and statuses.count("completed") == 20
+    assert fin0 and fin1                          # both ranks saw the "done" flag

@@ -1,0 +1,125 @@
+"""PopulationMLP on the PyTorch reference backend (CPU) and the population sweep engine."""
+import numpy as np
+import pytest
+import torch
+
+from metaopt_amd.io.experiment_builder import build_experiment
+from metaopt_amd.models.data import TeacherClassification
+from metaopt_amd.models.mlp import MLPSweepTask
+from metaopt_amd.ops import reference as ref
+from metaopt_amd.ops.population import MemberConfig, PopulationMLP, _ranges
+from metaopt_amd.storage.database import EphemeralDB
+from metaopt_amd.storage.protocol import DocumentStorage
+from metaopt_amd.worker.population_sweep import PopulationSweep
+
+
+@pytest.fixture(scope="module")
+def data():
+    return TeacherClassification(n_train=1024, n_val=256, batch_size=128, seed=7)
+
+
+def test_rng_matches_python_int_hash():
+    key = ref.rng_key(1234, 2, 17)
+    idx = torch.arange(0, 1000, dtype=torch.int64)
+    u = ref.rng_uniform(key, idx)
+    for i in (0, 1, 500, 999):
+        h = ref.fmix32(key ^ ((i * 0x9E3779B9) & ref.M32))
+        assert float(u[i]) == (h >> 8) / 16777216.0
+    assert 0.0 <= float(u.min()) and float(u.max()) < 1.0
+
+
+def test_ranges():
+    assert _ranges(np.array([2, 0, 3])).tolist() == [0, 1, 0, 1, 2]
+
+
+def test_learns_and_isolates_members(data):
+    pop = PopulationMLP(3, max_width=128, eval_batch=256, device="cpu")
+    pop.set_member(0, MemberConfig(width=64, lr=0.1, seed=1))
+    pop.set_member(2, MemberConfig(width=100, lr=0.0, seed=2))   # lr 0: must not move
+    w_before = pop.layer_views(2)[0][0].clone()
+    losses = []
+    for step in range(30):
+        pop.train_step(*data.batch(step))
+        losses.append(pop.train_loss())
+    losses = np.array(losses)
+    assert losses[-5:, 0].mean() < losses[:5, 0].mean()
+    assert torch.equal(pop.layer_views(2)[0][0], w_before)
+    assert np.isnan(losses[:, 1]).all()
+
+
+def test_padding_zero_and_init_deterministic():
+    a = PopulationMLP(2, max_width=128, device="cpu")
+    b = PopulationMLP(2, max_width=128, device="cpu")
+    a.set_member(0, MemberConfig(width=70, lr=0.1, seed=9))
+    b.set_member(1, MemberConfig(width=70, lr=0.1, seed=9))
+    for (wa, ba), (wb, bb) in zip(a.layer_views(0), b.layer_views(1)):
+        assert torch.equal(wa, wb) and torch.equal(ba, bb)
+    w0, _ = a.layer_views(0)[0]
+    assert float(w0[70:].abs().max()) == 0.0 and float(w0[:70, :784].abs().max()) > 0
+    bound = 1 / np.sqrt(784)
+    assert float(w0.abs().max()) <= bound + 1e-6
+
+
+def test_checkpoint_roundtrip_and_copy(data):
+    pop = PopulationMLP(3, max_width=128, eval_batch=256, device="cpu")
+    pop.set_member(0, MemberConfig(width=64, lr=0.05, seed=3))
+    for step in range(3):
+        pop.train_step(*data.batch(step))
+    st = pop.slot_state(0)
+    assert st["t"] == 3 and st["p32"].numel() == pop.used_params(0)
+    pop.load_slot_state(1, st)
+    l1, _ = pop.evaluate(*data.validation())
+    assert l1[0] == pytest.approx(l1[1], rel=1e-6)
+    pop.copy_member(0, 2, lr=0.5)
+    assert pop.members[2].lr == 0.5 and pop.steps_done(2) == 3
+    sub, _ = pop.evaluate(*data.validation(), slots=[2])
+    assert np.isnan(sub[0]) and not np.isnan(sub[2])
+
+
+def test_adamw_reference_matches_torch_optim():
+    torch.manual_seed(0)
+    w = torch.randn(5, 3)
+    g = torch.randn(5, 3)
+    p = torch.nn.Parameter(w.clone())
+    opt = torch.optim.AdamW([p], lr=0.01, betas=(0.9, 0.99), eps=1e-8, weight_decay=0.1)
+    m, v, w2 = torch.zeros_like(w), torch.zeros_like(w), w.clone()
+    for t in range(1, 4):
+        p.grad = g.clone()
+        opt.step()
+        ref.adamw_update(w2, m, v, g, 0.01, 0.9, 0.99, 1e-8, 0.1, t)
+    assert torch.allclose(p.detach(), w2, atol=1e-6)
+
+
+def test_sweep_asha_end_to_end(data):
+    priors = {"/lr": "loguniform(1e-3, 1.0)", "/width": "loguniform(64, 128, discrete=True)",
+              "/dropout": "uniform(0, 0.5)", "/steps": "fidelity(16, 64, 2)"}
+    storage = DocumentStorage(EphemeralDB())
+    exp = build_experiment("sweep-test", priors=priors,
+                           algorithms={"asha": {"seed": 1, "repetitions": float("inf")}},
+                           max_trials=24, storage=storage)
+    pop = PopulationMLP(6, max_width=128, eval_batch=256, device="cpu")
+    sweep = PopulationSweep(pop, MLPSweepTask(priors=priors, max_width=128), data,
+                            experiment=exp, sync_every=16)
+    summary = sweep.run(1000)
+    sweep.close()
+    assert summary["completed"] == 24
+    trials = exp.fetch_trials()
+    assert len(trials) == 24 and all(t.status == "completed" for t in trials)
+    budgets = sorted(t.params_dict["/steps"] for t in trials)
+    assert budgets[0] == 16 and budgets[-1] >= 32  # promotions happened
+    assert exp.stats["best_evaluation"] == pytest.approx(summary["best_val_loss"])
+
+
+def test_sweep_marks_diverged_members_broken(data):
+    priors = {"/lr": "loguniform(1e4, 1e5)", "/steps": "fidelity(16, 16, 2)"}
+    storage = DocumentStorage(EphemeralDB())
+    exp = build_experiment("sweep-nan", priors=priors, algorithms={"random": {"seed": 0}},
+                           max_trials=4, storage=storage)
+    pop = PopulationMLP(2, max_width=64, eval_batch=256, device="cpu")
+    task = MLPSweepTask(priors=priors, width=64, max_width=64)
+    sweep = PopulationSweep(pop, task, data, experiment=exp, sync_every=16)
+    summary = sweep.run(200)
+    sweep.close()
+    statuses = [t.status for t in exp.fetch_trials()]
+    assert summary["broken"] + summary["completed"] == 4
+    assert statuses.count("broken") == summary["broken"]

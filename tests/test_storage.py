@@ -1,0 +1,193 @@
+"""Database backends and the storage protocol (reference tests: tests/unittests/core/
+test_ephemeraldb.py, test_pickleddb.py, tests/unittests/storage/test_storage.py)."""
+import datetime
+import multiprocessing
+import os
+
+import pytest
+
+from metaopt_amd.core.trial import Trial
+from metaopt_amd.storage.database import (DuplicateKeyError, EphemeralDB, PickledDB,
+                                          create_database)
+from metaopt_amd.storage.protocol import DocumentStorage, FailedUpdate
+
+
+@pytest.fixture(params=["ephemeral", "pickled"])
+def db(request, tmp_path):
+    if request.param == "ephemeral":
+        return EphemeralDB()
+    return PickledDB(host=str(tmp_path / "db.pkl"))
+
+
+def _fill(db):
+    db.write("exps", [{"name": "a", "version": 1, "meta": {"user": "u1", "n": 3}},
+                      {"name": "b", "version": 1, "meta": {"user": "u2", "n": 5}},
+                      {"name": "a", "version": 2, "meta": {"user": "u1", "n": 7}}])
+
+
+class TestDatabase:
+    def test_insert_assigns_ids_and_reads(self, db):
+        doc = {"name": "x"}
+        assert db.write("c", doc) == 1
+        assert "_id" in doc
+        assert db.read("c", {"_id": doc["_id"]})[0]["name"] == "x"
+
+    def test_queries(self, db):
+        _fill(db)
+        assert len(db.read("exps", {"name": "a"})) == 2
+        assert len(db.read("exps", {"meta.user": "u1"})) == 2
+        assert len(db.read("exps", {"meta.n": {"$gte": 5}})) == 2
+        assert len(db.read("exps", {"meta.n": {"$gt": 5}})) == 1
+        assert len(db.read("exps", {"meta.n": {"$lte": 5}})) == 2
+        assert len(db.read("exps", {"name": {"$in": ["a", "z"]}})) == 2
+        assert len(db.read("exps", {"name": {"$ne": "a"}})) == 1
+        assert len(db.read("exps", {"name": {"$nin": ["a"]}})) == 1
+        assert len(db.read("exps", {"meta": {"user": "u2"}})) == 1
+        assert db.count("exps", {"name": "a"}) == 2
+        assert db.count("exps") == 3
+
+    def test_projection(self, db):
+        _fill(db)
+        docs = db.read("exps", {"name": "b"}, {"meta.user": 1})
+        assert docs[0] == {"_id": docs[0]["_id"], "meta": {"user": "u2"}}
+        docs = db.read("exps", {"name": "b"}, {"meta": 0, "_id": 0})
+        assert docs[0] == {"name": "b", "version": 1}
+        with pytest.raises(ValueError):
+            db.read("exps", {}, {"name": 1, "version": 0})
+
+    def test_update_and_read_and_write(self, db):
+        _fill(db)
+        assert db.write("exps", {"meta.n": 0}, {"name": "a"}) == 2
+        assert all(d["meta"]["n"] == 0 and d["meta"]["user"] == "u1"
+                   for d in db.read("exps", {"name": "a"}))
+        doc = db.read_and_write("exps", {"name": "b"}, {"status": "taken"})
+        assert doc["status"] == "taken"
+        assert db.read_and_write("exps", {"name": "zzz"}, {"x": 1}) is None
+
+    def test_unique_index(self, db):
+        db.ensure_index("exps", [("name", EphemeralDB.ASCENDING),
+                                 ("version", EphemeralDB.ASCENDING)], unique=True)
+        _fill(db)
+        assert db.index_information("exps")["name_1_version_1"] is True
+        with pytest.raises(DuplicateKeyError):
+            db.write("exps", {"name": "a", "version": 2})
+        with pytest.raises(DuplicateKeyError):
+            db.write("exps", {"version": 2}, {"name": "a", "version": 1})
+        db.drop_index("exps", "name_1_version_1")
+        db.write("exps", {"name": "a", "version": 2})
+
+    def test_remove(self, db):
+        _fill(db)
+        assert db.remove("exps", {"name": "a"}) == 2
+        assert db.count("exps") == 1
+
+    def test_duplicate_id(self, db):
+        db.write("c", {"_id": "k", "v": 1})
+        with pytest.raises(DuplicateKeyError):
+            db.write("c", {"_id": "k", "v": 2})
+
+
+def _concurrent_writer(args):
+    path, i = args
+    db = PickledDB(host=path)
+    try:
+        db.write("concurrent", {"_id": i % 5, "writer": i})
+        return 1
+    except DuplicateKeyError:
+        return 0
+
+
+def test_pickleddb_concurrent_unique_writes(tmp_path):
+    """10 processes race to insert 5 unique ids: exactly 5 succeed (reference
+    test_pickleddb.py:335-356)."""
+    path = str(tmp_path / "race.pkl")
+    PickledDB(host=path).ensure_index("concurrent", "_id", unique=True)
+    ctx = multiprocessing.get_context("spawn")
+    with ctx.Pool(4) as pool:
+        res = pool.map(_concurrent_writer, [(path, i) for i in range(10)])
+    assert sum(res) == 5
+    assert PickledDB(host=path).count("concurrent") == 5
+
+
+def test_create_database_by_name(tmp_path):
+    assert isinstance(create_database("EphemeralDB"), EphemeralDB)
+    assert isinstance(create_database("pickleddb", host=str(tmp_path / "x.pkl")), PickledDB)
+
+
+class _Exp:
+    def __init__(self, _id):
+        self._id = _id
+
+
+@pytest.fixture
+def storage():
+    return DocumentStorage(EphemeralDB(), heartbeat=120)
+
+
+def _trial(exp, x, status="new"):
+    t = Trial(experiment=exp._id, status=status, params=[dict(name="/x", type="real", value=x)])
+    t.submit_time = datetime.datetime.utcnow()
+    return t
+
+
+class TestStorageProtocol:
+    def test_experiment_unique_name_version(self, storage):
+        storage.create_experiment({"name": "e", "version": 1, "metadata": {}})
+        with pytest.raises(DuplicateKeyError):
+            storage.create_experiment({"name": "e", "version": 1, "metadata": {}})
+
+    def test_register_dedup(self, storage):
+        exp = _Exp("E")
+        storage.register_trial(_trial(exp, 1.0))
+        with pytest.raises(DuplicateKeyError):
+            storage.register_trial(_trial(exp, 1.0))
+
+    def test_reserve_is_exclusive(self, storage):
+        exp = _Exp("E")
+        for x in range(3):
+            storage.register_trial(_trial(exp, float(x)))
+        got = [storage.reserve_trial(exp) for _ in range(4)]
+        assert sum(t is not None for t in got) == 3
+        assert len({t.id for t in got if t}) == 3
+        assert all(t.status == "reserved" and t.heartbeat is not None for t in got if t)
+
+    def test_cas_status(self, storage):
+        exp = _Exp("E")
+        storage.register_trial(_trial(exp, 1.0))
+        t = storage.reserve_trial(exp)
+        stale = Trial(**t.to_dict())
+        storage.set_trial_status(t, "interrupted")
+        with pytest.raises(FailedUpdate):
+            storage.set_trial_status(stale, "completed")
+        assert storage.get_trial(t).status == "interrupted"
+
+    def test_lost_trials(self, storage):
+        exp = _Exp("E")
+        storage.register_trial(_trial(exp, 1.0))
+        t = storage.reserve_trial(exp)
+        assert storage.fetch_lost_trials(exp) == []
+        old = datetime.datetime.utcnow() - datetime.timedelta(seconds=1000)
+        storage._db.write("trials", {"heartbeat": old}, {"_id": t.id})
+        assert [x.id for x in storage.fetch_lost_trials(exp)] == [t.id]
+
+    def test_results_file(self, storage, tmp_path):
+        exp = _Exp("E")
+        storage.register_trial(_trial(exp, 1.0))
+        t = storage.reserve_trial(exp)
+        f = tmp_path / "results.json"
+        f.write_text('[{"name": "loss", "type": "objective", "value": 0.5}]')
+        storage.retrieve_result(t, str(f))
+        t.status = "completed"
+        storage.push_trial_results(t)
+        assert storage.count_completed_trials(exp) == 1
+        assert storage.get_trial(t).objective.value == 0.5
+
+    def test_counts_and_status_queries(self, storage):
+        exp = _Exp("E")
+        for i, st in enumerate(["new", "completed", "broken", "broken", "suspended"]):
+            storage.register_trial(_trial(exp, float(i), status=st))
+        assert storage.count_broken_trials(exp) == 2
+        assert storage.count_completed_trials(exp) == 1
+        assert len(storage.fetch_pending_trials(exp)) == 2
+        assert len(storage.fetch_noncompleted_trials(exp)) == 4
+        assert len(storage.fetch_trials_by_status(exp, "broken")) == 2
