@@ -40,7 +40,8 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=64)
     ap.add_argument("--population", type=int, default=256)
     ap.add_argument("--max-width", type=int, default=1024)
-    ap.add_argument("--sync-every", type=int, default=16)
+    ap.add_argument("--sync-every", type=int, default=32,
+                    help="population sync interval (steps); budgets are multiples of it")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--algo", default="asha", choices=["asha", "random", "tpe"])
     args = ap.parse_args(argv)

@@ -29,7 +29,7 @@ def add_subparser(parser):
     g.add_argument("--population", type=int, default=256, help="trials per GPU")
     g.add_argument("--max-trials", type=int, default=None)
     g.add_argument("--steps", type=int, default=100000, help="max population steps")
-    g.add_argument("--sync-every", type=int, default=16)
+    g.add_argument("--sync-every", type=int, default=32)
     g.add_argument("--seed", type=int, default=0)
     p.set_defaults(func=main)
     return p

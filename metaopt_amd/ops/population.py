@@ -400,8 +400,7 @@ class PopulationMLP:
         self._run_pending_init()
         if not self._dirty:
             return
-        self._tables = {"train": self._build_tables(self.batch_size),
-                        "eval": self._build_tables(self.eval_batch)}
+        self._tables = {"train": self._build_tables(self.batch_size)}  # eval: built lazily
         if self.device.type == "cuda":
             self._upload_hp()
         self._active_t = torch.tensor(
@@ -516,6 +515,8 @@ class PopulationMLP:
             raise ValueError(f"eval rows must be a multiple of 128 and <= {self.eval_batch}")
         if self.backend == "hip":
             from ._lib import check, stream_ptr
+            if "eval" not in self._tables:
+                self._tables["eval"] = self._build_tables(self.eval_batch)
             lib, tb, L = self._lib, self._tables["eval"], self.L
             if subset is not None:
                 tb = self._subset_table(tb, subset)
