@@ -89,6 +89,8 @@ def main(argv=None):
     comm.barrier()
     sync()
     s0, c0 = sweep.samples, sweep.completed
+    sweep.timers.clear()
+    sweep.n_syncs = 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         sweep.step()
@@ -136,6 +138,7 @@ def main(argv=None):
             else round(summ["best_val_loss"], 5),
             "best_params": summ["best_params"],
             "samples_per_sec": round(samples / elapsed, 1),
+            "host_ms_per_sync": summ["host_ms_per_sync"],
         }
         print(json.dumps(out), flush=True)
     shutdown()

@@ -511,7 +511,10 @@ class Space(dict):
                             "for tuples with parameter values.") from exc
         if not self or len(value) != len(self):
             return False
-        return all(component in dim for component, dim in zip(value, self.values()))
+        for component, dim in zip(value, self._sorted_values()):
+            if component not in dim:
+                return False
+        return True
 
     def __repr__(self):
         return "Space([{}])".format(",\n       ".join(map(str, self.values())))
@@ -520,7 +523,15 @@ class Space(dict):
         return [(k, dict.__getitem__(self, k)) for k in self._sorted_keys()]
 
     def values(self):
-        return [dict.__getitem__(self, k) for k in self._sorted_keys()]
+        return list(self._sorted_values())
+
+    def _sorted_values(self):
+        keys = self._sorted_keys()
+        cache = getattr(self, "_values_cache", None)
+        if cache is None or cache[0] is not keys:
+            cache = (keys, tuple(dict.__getitem__(self, k) for k in keys))
+            self._values_cache = cache
+        return cache[1]
 
     def keys(self):
         return list(self._sorted_keys())

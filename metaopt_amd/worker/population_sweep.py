@@ -74,6 +74,7 @@ class PopulationSweep:
         self.trials: Dict[int, Trial] = {}            # key -> reserved trial
         self.key_params: Dict[int, dict] = {}
         self.ckpt_index: Dict[str, tuple] = {}        # param key -> (rank, trial key, steps)
+        self._ckpt_pkey: Dict[tuple, str] = {}        # (rank, trial key) -> param key
         self.ckpt_fifo = [collections.deque() for _ in range(self.comm.world_size)]
         self.next_key = 1
         self._registered = set()
@@ -85,6 +86,8 @@ class PopulationSweep:
         self.max_trials = (max_trials if max_trials is not None else
                            (experiment.max_trials if experiment is not None else math.inf))
         self._writer = None
+        self.timers: Dict[str, float] = collections.defaultdict(float)  # host seconds per phase
+        self.n_syncs = 0
         if self.comm.is_root:
             self.algorithm = experiment.algorithms
             self.space = experiment.space
@@ -113,7 +116,7 @@ class PopulationSweep:
         return self.summary()
 
     # ------------------------------------------------------------------ sync
-    def _local_status(self, evaluate=True) -> torch.Tensor:
+    def _local_status(self, evaluate=True) -> np.ndarray:
         pop = self.pop
         P = pop.capacity
         st = np.zeros((P, ST_COLS), dtype=np.float64)
@@ -122,6 +125,10 @@ class PopulationSweep:
         st[:, 1] = steps
         st[:, 2] = self.slot_budget
         active = self.slot_key >= 0
+        if self._writer is not None:
+            # hand the storage writes of the previous decision to the writer thread now: the
+            # GPU is busy with the interval just queued and the main thread is about to block
+            self._writer.release()
         if active.any() and self.global_step > 0:
             tl = pop.train_loss()
             st[:, 3] = np.where(active, tl, np.nan)
@@ -137,20 +144,40 @@ class PopulationSweep:
             for s in finished:
                 if not math.isfinite(vl[s]):
                     st[s, 6] = 1
-        return torch.from_numpy(st).to(self.comm._coll_device())
+        return st
 
     def _sync(self, evaluate=True) -> None:
         P = self.pop.capacity
+        tm = self.timers
+        t0 = time.perf_counter()
         status = self._local_status(evaluate)
-        gathered = self.comm.all_gather_rows(status).cpu().numpy()          # C1
+        t1 = time.perf_counter()
+        dist = self.comm.distributed
+        if dist:
+            status_t = torch.from_numpy(status).to(self.comm._coll_device())
+            gathered = self.comm.all_gather_rows(status_t).cpu().numpy()    # C1
+        else:
+            gathered = status
+        t2 = time.perf_counter()
         # one extra row carries the sweep-level "done" flag
         assign = np.zeros((self.comm.world_size * P + 1, AS_COLS), dtype=np.float64)
         if self.comm.is_root:
             assign = self._decide(gathered)
             assign[-1, 0] = float(self.done)
-        assign_t = torch.from_numpy(assign).to(self.comm._coll_device())
-        self.comm.broadcast_(assign_t, src=0)                               # C5
-        self._apply(gathered, assign_t.cpu().numpy())
+        t3 = time.perf_counter()
+        if dist:
+            assign_t = torch.from_numpy(assign).to(self.comm._coll_device())
+            self.comm.broadcast_(assign_t, src=0)                           # C5
+            assign = assign_t.cpu().numpy()
+        t4 = time.perf_counter()
+        self._apply(gathered, assign)
+        t5 = time.perf_counter()
+        tm["status"] += t1 - t0
+        tm["c1_allgather"] += t2 - t1
+        tm["decide"] += t3 - t2
+        tm["c5_broadcast"] += t4 - t3
+        tm["apply"] += t5 - t4
+        self.n_syncs += 1
 
     # ------------------------------------------------------------------ rank 0
     def _decide(self, gathered: np.ndarray) -> np.ndarray:
@@ -207,12 +234,16 @@ class PopulationSweep:
     def _record_ckpt(self, pkey, rank, key, steps):
         fifo = self.ckpt_fifo[rank]
         fifo.append(key)
+        prev = self.ckpt_index.get(pkey)
+        if prev is not None:
+            self._ckpt_pkey.pop((prev[0], prev[1]), None)
         self.ckpt_index[pkey] = (rank, key, steps)
+        self._ckpt_pkey[(rank, key)] = pkey
         while len(fifo) > self.ckpt_capacity:   # mirrors the owner's FIFO eviction exactly
             old = fifo.popleft()
-            for pk, (r, k, _) in list(self.ckpt_index.items()):
-                if r == rank and k == old:
-                    del self.ckpt_index[pk]
+            pk = self._ckpt_pkey.pop((rank, old), None)
+            if pk is not None and self.ckpt_index.get(pk, (None, None))[:2] == (rank, old):
+                del self.ckpt_index[pk]
 
     def _fill(self, free_rows: List[int], assign: np.ndarray) -> None:
         W, P = self.comm.world_size, self.pop.capacity
@@ -240,6 +271,7 @@ class PopulationSweep:
                 row = free_by_rank[owner[0]].pop(0)
                 action, resume = RESUME, owner[1]
                 del self.ckpt_index[pkey]
+                self._ckpt_pkey.pop((owner[0], owner[1]), None)
                 try:  # the owner drops the checkpoint when it resumes it: mirror that
                     self.ckpt_fifo[owner[0]].remove(owner[1])
                 except ValueError:
@@ -342,7 +374,16 @@ class PopulationSweep:
         return {"global_step": self.global_step, "samples": self.samples,
                 "completed": self.completed, "broken": self.broken,
                 "best_val_loss": self.best[0], "best_params": self.best[1],
-                "active": int((self.slot_key >= 0).sum())}
+                "active": int((self.slot_key >= 0).sum()),
+                "host_ms_per_sync": {k: round(1e3 * v / max(self.n_syncs, 1), 3)
+                                     for k, v in self.timers.items()}}
+
+
+class _Snapshot:
+    __slots__ = ("doc",)
+
+    def __init__(self, doc):
+        self.doc = doc
 
 
 class _WriteBehind:
@@ -350,42 +391,54 @@ class _WriteBehind:
 
     The sweep's decisions never read back what it writes (rank 0 keeps its own bookkeeping), so
     persisting trials -- registration, results, status changes, heartbeats -- can overlap the
-    GPU work instead of stalling every sync.  ``flush`` waits for the queue to drain; a failing
-    write is logged and the queue continues.
+    GPU work instead of stalling every sync.  Writes queued by ``put`` are held back until
+    ``release`` (called when the main thread is about to block on the GPU), so the writer does
+    not compete with the decision code for the GIL.  ``flush`` releases and waits for the queue
+    to drain; a failing write is logged and the queue continues.
     """
 
     def __init__(self, storage):
         self.storage = storage
         self.q: "queue.Queue" = queue.Queue()
         self.errors = 0
+        self._held: list = []
         self._t = threading.Thread(target=self._run, daemon=True)
         self._t.start()
 
     def put(self, method, *args, **kwargs):
-        # snapshot trials: the sweep keeps mutating its objects after queueing them
-        args = tuple(Trial(**a.to_dict()) if isinstance(a, Trial) else a for a in args)
-        self.q.put((method, args, kwargs))
+        # snapshot trials (the sweep keeps mutating its objects after queueing them); the Trial
+        # objects are rebuilt from the snapshots on the writer thread
+        args = tuple(_Snapshot(a.to_dict()) if isinstance(a, Trial) else a for a in args)
+        self._held.append((method, args, kwargs))
+
+    def release(self):
+        if self._held:
+            self.q.put(self._held)
+            self._held = []
 
     def _run(self):
         while True:
-            item = self.q.get()
+            batch = self.q.get()
             try:
-                if item is None:
+                if batch is None:
                     return
-                method, args, kwargs = item
-                try:
-                    getattr(self.storage, method)(*args, **kwargs)
-                except DuplicateKeyError:
-                    log.debug("duplicate write skipped (%s)", method)
-                except Exception as exc:  # pragma: no cover - storage hiccup
-                    self.errors += 1
-                    log.warning("storage write %s failed: %s", method, exc)
+                for method, args, kwargs in batch:
+                    args = tuple(Trial(**a.doc) if isinstance(a, _Snapshot) else a for a in args)
+                    try:
+                        getattr(self.storage, method)(*args, **kwargs)
+                    except DuplicateKeyError:
+                        log.debug("duplicate write skipped (%s)", method)
+                    except Exception as exc:  # pragma: no cover - storage hiccup
+                        self.errors += 1
+                        log.warning("storage write %s failed: %s", method, exc)
             finally:
                 self.q.task_done()
 
     def flush(self):
+        self.release()
         self.q.join()
 
     def close(self):
+        self.release()
         self.q.put(None)
         self._t.join()

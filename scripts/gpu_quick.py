@@ -1,11 +1,12 @@
 """Quick GPU diagnostics: build, one-step numerics vs reference, and population step timing."""
+import os
 import sys
 import time
 
 import numpy as np
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from metaopt_amd.ops import build  # noqa: E402
 from metaopt_amd.ops.population import MemberConfig, PopulationMLP  # noqa: E402
 from metaopt_amd.models.data import TeacherClassification  # noqa: E402

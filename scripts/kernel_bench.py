@@ -3,6 +3,7 @@
 Reports time per launch (HIP events) and effective bandwidth against the per-parameter byte
 model of each kernel (fwd: 2 B/param bf16 weight read; bwd+SGD: 18 B/param).
 """
+import os
 import argparse
 import json
 import sys
@@ -10,7 +11,7 @@ import sys
 import numpy as np
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from metaopt_amd.models.data import TeacherClassification  # noqa: E402
 from metaopt_amd.ops import _lib  # noqa: E402
 from metaopt_amd.ops.population import (BWD_HAS_DX, BWD_IN_DROPOUT, BWD_UPDATE_BIAS,  # noqa: E402

@@ -1,0 +1,73 @@
+"""Host cost of the sweep's rank-0 decision step (ASHA observe/suggest, trial bookkeeping) on CPU.
+
+Simulates a 256-slot population where every member reaches its budget on schedule, so the
+decision path sees the same completion/placement volume as the GPU bench, without a GPU.
+"""
+import cProfile
+import os
+import pstats
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from metaopt_amd.io.experiment_builder import build_experiment  # noqa: E402
+from metaopt_amd.models.mlp import MLP_PRIORS, MLPSweepTask  # noqa: E402
+from metaopt_amd.storage.database import EphemeralDB  # noqa: E402
+from metaopt_amd.storage.protocol import DocumentStorage  # noqa: E402
+from metaopt_amd.worker.population_sweep import PopulationSweep  # noqa: E402
+
+
+class _FakePop:
+    """Just enough of PopulationMLP for the decision path."""
+
+    def __init__(self, capacity):
+        self.capacity = capacity
+        self.device = __import__("torch").device("cpu")
+
+
+def main(n_syncs=40, P=256, profile=False):
+    task = MLPSweepTask(priors=dict(MLP_PRIORS), max_width=1024)
+    exp = build_experiment("decide-prof", priors=dict(MLP_PRIORS),
+                           algorithms={"asha": {"seed": 0, "repetitions": float("inf")}},
+                           storage=DocumentStorage(EphemeralDB()), pool_size=P)
+    sw = PopulationSweep(_FakePop(P), task, data=None, experiment=exp, sync_every=32)
+    rng = np.random.default_rng(0)
+    steps = np.zeros(P)
+    gathered = np.zeros((P, 7))
+    gathered[:, 0] = -1
+    assign = sw._decide(gathered)
+    prof = cProfile.Profile() if profile else None
+    t_total = 0.0
+    n_done = 0
+    for _ in range(n_syncs):
+        # apply: new/resumed members start from 0 (resume: from their checkpoint steps)
+        for s in range(P):
+            if assign[s, 0] in (1, 2):
+                gathered[s, 0] = assign[s, 1]
+                gathered[s, 2] = assign[s, 8]
+                steps[s] = 0 if assign[s, 0] == 1 else gathered[s, 2] // 4
+            elif assign[s, 0] == 3:
+                gathered[s, 0] = -1
+        steps += 32
+        gathered[:, 1] = steps
+        fin = (gathered[:, 0] >= 0) & (steps >= gathered[:, 2])
+        n_done += int(fin.sum())
+        gathered[:, 3] = rng.random(P)
+        gathered[:, 4] = np.where(fin, rng.random(P), 0)
+        t0 = time.perf_counter()
+        if prof:
+            prof.enable()
+        assign = sw._decide(gathered)
+        if prof:
+            prof.disable()
+        t_total += time.perf_counter() - t0
+    sw.close()
+    print(f"decide: {1e3 * t_total / n_syncs:.2f} ms/sync, {n_done / n_syncs:.1f} completions/sync")
+    if prof:
+        pstats.Stats(prof).sort_stats("cumulative").print_stats(30)
+
+
+if __name__ == "__main__":
+    main(profile="--profile" in sys.argv)

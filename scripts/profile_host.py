@@ -1,9 +1,10 @@
 """cProfile the headline sweep loop (host overhead between kernel launches)."""
+import os
 import cProfile
 import pstats
 import sys
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 
 out = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/host_profile.txt"
