@@ -82,33 +82,37 @@ __device__ __forceinline__ void fwd_gemm(const bf16_t* __restrict__ X, const bf1
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  uint4 ra[4], rb[2];
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
-      ra[i] = *(const uint4*)(X + (size_t)r * K + k0 + ch * 8);
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
-      rb[i] = *(const uint4*)(W + (size_t)r * K + k0 + ch * 8);
-    }
-  };
-  gload(0);
+  // Staging registers are plain scalars (no arrays captured by a lambda): an array captured by
+  // reference is demoted to scratch, which costs ~10x the forward's useful HBM writes.
+  const int c0 = tid, c1 = tid + 256, c2 = tid + 512, c3 = tid + 768;
+  const int g0 = (c0 >> 3) * K + (c0 & 7) * 8, g1 = (c1 >> 3) * K + (c1 & 7) * 8;
+  const int g2 = (c2 >> 3) * K + (c2 & 7) * 8, g3 = (c3 >> 3) * K + (c3 & 7) * 8;
+  bf16_t* as0 = As + (c0 >> 3) * LS + (c0 & 7) * 8;
+  bf16_t* as1 = As + (c1 >> 3) * LS + (c1 & 7) * 8;
+  bf16_t* as2 = As + (c2 >> 3) * LS + (c2 & 7) * 8;
+  bf16_t* as3 = As + (c3 >> 3) * LS + (c3 & 7) * 8;
+  bf16_t* bs0 = Bs + (c0 >> 3) * LS + (c0 & 7) * 8;
+  bf16_t* bs1 = Bs + (c1 >> 3) * LS + (c1 & 7) * 8;
+  uint4 ra0 = *(const uint4*)(X + g0), ra1 = *(const uint4*)(X + g1),
+        ra2 = *(const uint4*)(X + g2), ra3 = *(const uint4*)(X + g3),
+        rb0 = *(const uint4*)(W + g0), rb1 = *(const uint4*)(W + g1);
   for (int k0 = 0; k0 < K; k0 += BK) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
-      *(uint4*)(As + r * LS + ch * 8) = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
-      *(uint4*)(Bs + r * LS + ch * 8) = rb[i];
-    }
+    *(uint4*)as0 = ra0;
+    *(uint4*)as1 = ra1;
+    *(uint4*)as2 = ra2;
+    *(uint4*)as3 = ra3;
+    *(uint4*)bs0 = rb0;
+    *(uint4*)bs1 = rb1;
     __syncthreads();
-    if (k0 + BK < K) gload(k0 + BK);
+    if (k0 + BK < K) {
+      const int k1 = k0 + BK;
+      ra0 = *(const uint4*)(X + g0 + k1);
+      ra1 = *(const uint4*)(X + g1 + k1);
+      ra2 = *(const uint4*)(X + g2 + k1);
+      ra3 = *(const uint4*)(X + g3 + k1);
+      rb0 = *(const uint4*)(W + g0 + k1);
+      rb1 = *(const uint4*)(W + g1 + k1);
+    }
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
       bf16x8 a[2], b[4];

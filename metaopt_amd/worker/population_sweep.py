@@ -28,8 +28,6 @@ import collections
 import datetime
 import logging
 import math
-import queue
-import threading
 import time
 from typing import Dict, List, Optional
 
@@ -387,58 +385,40 @@ class _Snapshot:
 
 
 class _WriteBehind:
-    """Storage writes applied in order by a background thread (write-behind).
+    """Storage writes deferred to the GPU-wait window (write-behind).
 
     The sweep's decisions never read back what it writes (rank 0 keeps its own bookkeeping), so
-    persisting trials -- registration, results, status changes, heartbeats -- can overlap the
-    GPU work instead of stalling every sync.  Writes queued by ``put`` are held back until
-    ``release`` (called when the main thread is about to block on the GPU), so the writer does
-    not compete with the decision code for the GIL.  ``flush`` releases and waits for the queue
-    to drain; a failing write is logged and the queue continues.
+    persisting trials -- registration, results, status changes, heartbeats -- is taken off the
+    decision path: ``put`` snapshots the arguments, ``release`` applies the held writes in order.
+    The sweep calls ``release`` right after queueing a sync interval's kernels, so the writes run
+    on the host while the GPU trains (in the calling thread: a helper thread would contend with
+    the decision code for the GIL).  A failing write is logged and the rest continue.
     """
 
     def __init__(self, storage):
         self.storage = storage
-        self.q: "queue.Queue" = queue.Queue()
         self.errors = 0
         self._held: list = []
-        self._t = threading.Thread(target=self._run, daemon=True)
-        self._t.start()
 
     def put(self, method, *args, **kwargs):
-        # snapshot trials (the sweep keeps mutating its objects after queueing them); the Trial
-        # objects are rebuilt from the snapshots on the writer thread
+        # snapshot trials: the sweep keeps mutating its objects after queueing them
         args = tuple(_Snapshot(a.to_dict()) if isinstance(a, Trial) else a for a in args)
         self._held.append((method, args, kwargs))
 
     def release(self):
-        if self._held:
-            self.q.put(self._held)
-            self._held = []
-
-    def _run(self):
-        while True:
-            batch = self.q.get()
+        held, self._held = self._held, []
+        for method, args, kwargs in held:
+            args = tuple(Trial(**a.doc) if isinstance(a, _Snapshot) else a for a in args)
             try:
-                if batch is None:
-                    return
-                for method, args, kwargs in batch:
-                    args = tuple(Trial(**a.doc) if isinstance(a, _Snapshot) else a for a in args)
-                    try:
-                        getattr(self.storage, method)(*args, **kwargs)
-                    except DuplicateKeyError:
-                        log.debug("duplicate write skipped (%s)", method)
-                    except Exception as exc:  # pragma: no cover - storage hiccup
-                        self.errors += 1
-                        log.warning("storage write %s failed: %s", method, exc)
-            finally:
-                self.q.task_done()
+                getattr(self.storage, method)(*args, **kwargs)
+            except DuplicateKeyError:
+                log.debug("duplicate write skipped (%s)", method)
+            except Exception as exc:  # pragma: no cover - storage hiccup
+                self.errors += 1
+                log.warning("storage write %s failed: %s", method, exc)
 
     def flush(self):
         self.release()
-        self.q.join()
 
     def close(self):
         self.release()
-        self.q.put(None)
-        self._t.join()
