@@ -275,7 +275,7 @@ __global__ __launch_bounds__(256) void mlp_fwd_ce_kernel(const MlpTL* __restrict
 // One LDS image per operand serves both row reads and ds_read_b64_tr_b16 transposed reads.
 // ----------------------------------------------------------------------------------------------
 template <int OPT>
-__global__ __launch_bounds__(256) void mlp_bwd_opt_kernel(const MlpTL* __restrict__ tls,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void mlp_bwd_opt_kernel(const MlpTL* __restrict__ tls,
                                                           const int2* __restrict__ work, int n_work,
                                                           const bf16_t* __restrict__ xb,
                                                           bf16_t* __restrict__ grad,
@@ -284,11 +284,13 @@ __global__ __launch_bounds__(256) void mlp_bwd_opt_kernel(const MlpTL* __restric
                                                           float* __restrict__ m32,
                                                           float* __restrict__ v32,
                                                           const TrialHP* __restrict__ hp, int flags) {
-  __shared__ __attribute__((aligned(16))) bf16_t smem[(2 * BM + BN) * LS + 2 * 4 * BN];
+  constexpr int DS = BN + 4;  // f32 row stride of the dW staging tile
+  __shared__ __attribute__((aligned(16))) bf16_t smem[(2 * BM + BN) * LS + 2 * 4 * BN + 2 * BN * DS];
   bf16_t* Xs = smem;
   bf16_t* Zs = smem + BM * LS;
   bf16_t* Ws = smem + 2 * BM * LS;
   float* red = (float*)(smem + (2 * BM + BN) * LS);  // [4][64] bias partial sums
+  float* Dw = red + 4 * BN;                           // [64 n][DS] dW of the current chunk
 
   const int2 wi = work[xcd_remap(blockIdx.x, n_work)];
   const MlpTL tl = tls[wi.x];
@@ -297,6 +299,7 @@ __global__ __launch_bounds__(256) void mlp_bwd_opt_kernel(const MlpTL* __restric
   const bf16_t* dZ = grad + tl.y_off;
   float* W32 = p32 + tl.w_off;
   float* M32 = m32 + tl.w_off;
+  float* V32 = v32 + tl.w_off;  // AdamW only
   bf16_t* W16 = p16 + tl.w_off;
   const TrialHP h = hp[tl.trial];
   const bool has_dx = flags & kHasDx;
@@ -322,56 +325,64 @@ __global__ __launch_bounds__(256) void mlp_bwd_opt_kernel(const MlpTL* __restric
   }
   __syncthreads();
 
-  // A fragments of dW^T = X^T dZ for this wave's 32 k-rows, all 128 batch rows (kept in VGPRs).
-  bf16x8 xa[2][4];
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int c0 = 32 * wk + 16 * t + 4 * pp;
-      const s16x4 lo = lds_tr4(Xs + (32 * s + 8 * g + q) * LS + c0);
-      const s16x4 hi = lds_tr4(Xs + (32 * s + 8 * g + 4 + q) * LS + c0);
-      xa[t][s] = cat_frag(lo, hi);
-    }
-
   f32x4 dx[2][4];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) dx[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // Chunk operands are loaded at the top of each chunk (a one-chunk-ahead register prefetch
+  // measured no faster and pushes the kernel to one wave per SIMD); latency is hidden by the
+  // second workgroup per CU.  Staging lives in named registers, never in arrays captured by a
+  // lambda (see fwd_gemm).
+  const int zo0 = (tid >> 3) * N + (tid & 7) * 8, zo1 = ((tid + 256) >> 3) * N + (tid & 7) * 8;
+  const int zo2 = ((tid + 512) >> 3) * N + (tid & 7) * 8, zo3 = ((tid + 768) >> 3) * N + (tid & 7) * 8;
+  bf16_t* zs0 = Zs + (tid >> 3) * LS + (tid & 7) * 8;
+  // Optimizer-state layout: thread -> rows 16i + tid/16 (i < 4), 4 consecutive k at 4 * (tid % 16):
+  // every wave-instruction moves 4 rows x 256 contiguous bytes of W/M (/V), full 128-B lines.
+  const int wo = (tid >> 4) * K + k0 + 4 * (tid & 15);
+  uint4 z0, z1, z2, z3;
+  f32x4 w0, w1, w2, w3, m0, m1, m2, m3, v0, v1, v2, v3;
+#define MOPT_BWD_LOAD(NC)                                                                        \
+  {                                                                                              \
+    const bf16_t* zc = dZ + (NC);                                                                \
+    z0 = *(const uint4*)(zc + zo0);                                                              \
+    z1 = *(const uint4*)(zc + zo1);                                                              \
+    z2 = *(const uint4*)(zc + zo2);                                                              \
+    z3 = *(const uint4*)(zc + zo3);                                                              \
+    const size_t ob = (size_t)(NC) * K + wo;                                                     \
+    w0 = *(const f32x4*)(W32 + ob);                                                              \
+    w1 = *(const f32x4*)(W32 + ob + 16 * K);                                                     \
+    w2 = *(const f32x4*)(W32 + ob + 32 * K);                                                     \
+    w3 = *(const f32x4*)(W32 + ob + 48 * K);                                                     \
+    m0 = *(const f32x4*)(M32 + ob);                                                              \
+    m1 = *(const f32x4*)(M32 + ob + 16 * K);                                                     \
+    m2 = *(const f32x4*)(M32 + ob + 32 * K);                                                     \
+    m3 = *(const f32x4*)(M32 + ob + 48 * K);                                                     \
+    if (OPT == kAdamW) {                                                                         \
+      v0 = *(const f32x4*)(V32 + ob);                                                            \
+      v1 = *(const f32x4*)(V32 + ob + 16 * K);                                                   \
+      v2 = *(const f32x4*)(V32 + ob + 32 * K);                                                   \
+      v3 = *(const f32x4*)(V32 + ob + 48 * K);                                                   \
+    }                                                                                            \
+  }
   for (int nc = 0; nc < N; nc += BN) {
-    // ---- global loads: dZ chunk (row-major), master W and optimizer state in dW^T C-layout ----
-    uint4 zr[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
-      zr[i] = *(const uint4*)(dZ + (size_t)r * N + nc + ch * 8);
-    }
-    f32x4 w[2][2], m[2][2], v[2][2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const size_t o = (size_t)(nc + 32 * wn + 16 * u + li) * K + k0 + 32 * wk + 16 * t + 4 * g;
-        w[t][u] = *(const f32x4*)(W32 + o);
-        m[t][u] = *(const f32x4*)(M32 + o);
-        if (OPT == kAdamW) v[t][u] = *(const f32x4*)(v32 + tl.w_off + o);
-      }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
-      *(uint4*)(Zs + r * LS + ch * 8) = zr[i];
+    MOPT_BWD_LOAD(nc)
+    // ---- this chunk's operands -> LDS (dZ row-major; W^T image as bf16 for the dX MFMAs) ----
+    *(uint4*)(zs0) = z0;
+    *(uint4*)(zs0 + 32 * LS) = z1;
+    *(uint4*)(zs0 + 64 * LS) = z2;
+    *(uint4*)(zs0 + 96 * LS) = z3;
+    const f32x4 w[4] = {w0, w1, w2, w3}, m[4] = {m0, m1, m2, m3};
+    f32x4 v[4];
+    if (OPT == kAdamW) {
+      v[0] = v0; v[1] = v1; v[2] = v2; v[3] = v3;
     }
     if (has_dx) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const f32x4 o = w[t][u];
-          *(uint2*)(Ws + (32 * wn + 16 * u + li) * LS + 32 * wk + 16 * t + 4 * g) =
-              make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
-        }
+      for (int i = 0; i < 4; ++i)
+        *(uint2*)(Ws + (16 * i + (tid >> 4)) * LS + 4 * (tid & 15)) =
+            make_uint2(pack2bf(w[i][0], w[i][1]), pack2bf(w[i][2], w[i][3]));
     }
     __syncthreads();
 
@@ -403,7 +414,14 @@ __global__ __launch_bounds__(256) void mlp_bwd_opt_kernel(const MlpTL* __restric
       for (int u = 0; u < 2; ++u) dw[t][u] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      bf16x8 bz[2];
+      bf16x8 xa[2], bz[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int c0 = 32 * wk + 16 * t + 4 * pp;
+        const s16x4 lo = lds_tr4(Xs + (32 * s + 8 * g + q) * LS + c0);
+        const s16x4 hi = lds_tr4(Xs + (32 * s + 8 * g + 4 + q) * LS + c0);
+        xa[t] = cat_frag(lo, hi);
+      }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int c0 = 32 * wn + 16 * u + 4 * pp;
@@ -414,36 +432,42 @@ __global__ __launch_bounds__(256) void mlp_bwd_opt_kernel(const MlpTL* __restric
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int u = 0; u < 2; ++u) dw[t][u] = mfma16(xa[t][s], bz[u], dw[t][u]);
+        for (int u = 0; u < 2; ++u) dw[t][u] = mfma16(xa[t], bz[u], dw[t][u]);
     }
 
-    // ---- optimizer epilogue: register r of dw[t][u] is dW[n][k + r] ----
+    // ---- optimizer epilogue: dW^T C-fragments (register r of dw[t][u] = dW[n][k + r]) are
+    //      restaged through LDS into the row-contiguous layout of W/M (/V) ----
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const size_t o = (size_t)(nc + 32 * wn + 16 * u + li) * K + k0 + 32 * wk + 16 * t + 4 * g;
-        f32x4 wv = w[t][u], mv = m[t][u], vv;
-        if (OPT == kAdamW) vv = v[t][u];
+      for (int u = 0; u < 2; ++u)
+        *(f32x4*)(Dw + (32 * wn + 16 * u + li) * DS + 32 * wk + 16 * t + 4 * g) = dw[t][u];
+    __syncthreads();
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float gr = dw[t][u][r];
-          if (OPT == kSGD) {
-            const float gg = gr + h.wd * wv[r];
-            mv[r] = h.b1 * mv[r] + gg;
-            wv[r] = wv[r] - h.lr * mv[r];
-          } else {
-            wv[r] = wv[r] * (1.f - h.lr * h.wd);
-            mv[r] = h.b1 * mv[r] + (1.f - h.b1) * gr;
-            vv[r] = h.b2 * vv[r] + (1.f - h.b2) * gr * gr;
-            wv[r] = wv[r] - c1 * mv[r] / (sqrtf(vv[r]) * c2 + h.eps);
-          }
+    for (int i = 0; i < 4; ++i) {
+      const f32x4 gv = *(const f32x4*)(Dw + (16 * i + (tid >> 4)) * DS + 4 * (tid & 15));
+      const size_t o = (size_t)nc * K + wo + (size_t)(16 * i) * K;
+      f32x4 wv = w[i], mv = m[i], vv;
+      if (OPT == kAdamW) vv = v[i];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float gr = gv[r];
+        if (OPT == kSGD) {
+          const float gg = gr + h.wd * wv[r];
+          mv[r] = h.b1 * mv[r] + gg;
+          wv[r] = wv[r] - h.lr * mv[r];
+        } else {
+          wv[r] = wv[r] * (1.f - h.lr * h.wd);
+          mv[r] = h.b1 * mv[r] + (1.f - h.b1) * gr;
+          vv[r] = h.b2 * vv[r] + (1.f - h.b2) * gr * gr;
+          wv[r] = wv[r] - c1 * mv[r] / (sqrtf(vv[r]) * c2 + h.eps);
         }
-        *(f32x4*)(W32 + o) = wv;
-        *(f32x4*)(M32 + o) = mv;
-        if (OPT == kAdamW) *(f32x4*)(v32 + tl.w_off + o) = vv;
-        *(uint2*)(W16 + o) = make_uint2(pack2bf(wv[0], wv[1]), pack2bf(wv[2], wv[3]));
       }
+      *(f32x4*)(W32 + o) = wv;
+      *(f32x4*)(M32 + o) = mv;
+      if (OPT == kAdamW) *(f32x4*)(V32 + o) = vv;
+      *(uint2*)(W16 + o) = make_uint2(pack2bf(wv[0], wv[1]), pack2bf(wv[2], wv[3]));
+    }
 
     // ---- bias: db[n] = sum_b dZ[b][n]; only the k-strip-0 workgroup owns the bias ----
     if (do_bias) {
@@ -474,6 +498,7 @@ __global__ __launch_bounds__(256) void mlp_bwd_opt_kernel(const MlpTL* __restric
     }
     __syncthreads();
   }
+#undef MOPT_BWD_LOAD
 
   if (!has_dx) return;
   // ---- dZ of the layer below: dX * relu'(.) * dropout mask, both read off X (X > 0) ----
