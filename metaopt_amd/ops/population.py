@@ -130,8 +130,12 @@ class PopulationMLP:
         self.grad = torch.zeros_like(self.act)
         self.act_eval = torch.zeros(self.capacity * self.eval_batch * self.act_row,
                                     dtype=torch.bfloat16, device=dev)
-        self.loss = torch.zeros(self.capacity, dtype=torch.float32, device=dev)
-        self.correct = torch.zeros(self.capacity, dtype=torch.float32, device=dev)
+        # per-slot loss sum and #correct of the last train step and of the last evaluation, in
+        # one buffer: one zeroing launch per step, one device->host copy per sync
+        P = self.capacity
+        self.stats = torch.zeros(4 * P, dtype=torch.float32, device=dev)
+        self.loss, self.correct = self.stats[:P], self.stats[P:2 * P]
+        self.eval_loss, self.eval_correct = self.stats[2 * P:3 * P], self.stats[3 * P:]
         self.hp = np.zeros(self.capacity, dtype=HP_DTYPE)
         self.hp_dev = torch.zeros(self.capacity * HP_DTYPE.itemsize, dtype=torch.uint8, device=dev)
         self.members: List[Optional[MemberConfig]] = [None] * self.capacity
@@ -403,8 +407,18 @@ class PopulationMLP:
         self._tables = {"train": self._build_tables(self.batch_size)}  # eval: built lazily
         if self.device.type == "cuda":
             self._upload_hp()
-        self._active_t = torch.tensor(
-            [1 if m is not None else 0 for m in self.members], dtype=torch.int32, device=self.device)
+        self._active_np = np.array([m is not None for m in self.members])
+        self._active_t = torch.from_numpy(self._active_np.astype(np.int32)).to(self.device)
+        self._any_dropout = any(m is not None and m.dropout > 0 for m in self.members)
+        if self.backend == "hip":
+            tb = self._tables["train"]
+            self._ptr = {"p32": self.p32.data_ptr(), "p16": self.p16.data_ptr(),
+                         "m32": self.m32.data_ptr(), "v32": self.v32.data_ptr(),
+                         "act": self.act.data_ptr(), "grad": self.grad.data_ptr(),
+                         "hp": self.hp_dev.data_ptr(), "loss": self.loss.data_ptr(),
+                         "correct": self.correct.data_ptr(), "tl": tb["tl"].data_ptr(),
+                         "fwd": [w.data_ptr() for w in tb["fwd"]],
+                         "bwd": [w.data_ptr() for w in tb["bwd"]]}
         self._dirty = False
 
     # ------------------------------------------------------------------ training
@@ -413,8 +427,7 @@ class PopulationMLP:
         self._refresh()
         if x.shape != (self.batch_size, self.K0):
             raise ValueError(f"x must be [{self.batch_size}, {self.K0}] (padded), got {tuple(x.shape)}")
-        act_mask = np.array([m is not None for m in self.members])
-        self.hp["t"][act_mask] += 1
+        self.hp["t"][self._active_np] += 1
         if self.backend == "hip":
             self._hp_increment()
             self._train_step_hip(x, y)
@@ -427,38 +440,31 @@ class PopulationMLP:
 
     def _train_step_hip(self, x, y) -> None:
         from ._lib import check, stream_ptr
-        lib, tb, L = self._lib, self._tables["train"], self.L
+        lib, tb, L, P = self._lib, self._tables["train"], self.L, self._ptr
         stream = stream_ptr(self.device)
-        self.loss.zero_()
-        self.correct.zero_()
-        drop = any(m is not None and m.dropout > 0 for m in self.members)
-        xb = x.contiguous()
+        self.stats[:2 * self.capacity].zero_()
+        drop = self._any_dropout
+        xp = x.data_ptr() if x.is_contiguous() else x.contiguous().data_ptr()
+        act, tl = P["act"], P["tl"]
         for l in range(L - 1):
-            src = xb if l == 0 else self.act
-            check(lib.mopt_mlp_fwd(tb["tl"].data_ptr(), tb["fwd"][l].data_ptr(), tb["n_fwd"][l], 1,
-                                   src.data_ptr(), self.p32.data_ptr(), self.p16.data_ptr(),
-                                   self.act.data_ptr(), self.hp_dev.data_ptr(), 0, l,
+            check(lib.mopt_mlp_fwd(tl, P["fwd"][l], tb["n_fwd"][l], 1, xp if l == 0 else act,
+                                   P["p32"], P["p16"], act, P["hp"], 0, l,
                                    FWD_RELU | (FWD_DROPOUT if drop else 0), stream), "mlp_fwd")
-        src = xb if L == 1 else self.act
-        check(lib.mopt_mlp_fwd_ce(tb["tl"].data_ptr(), tb["fwd"][L - 1].data_ptr(),
-                                  tb["n_fwd"][L - 1], 1, src.data_ptr(), self.p32.data_ptr(),
-                                  self.p16.data_ptr(), y.data_ptr(), self.grad.data_ptr(),
-                                  self.loss.data_ptr(), self.correct.data_ptr(),
-                                  1.0 / self.batch_size, FWD_WRITE_GRAD, stream), "mlp_fwd_ce")
+        check(lib.mopt_mlp_fwd_ce(tl, P["fwd"][L - 1], tb["n_fwd"][L - 1], 1,
+                                  xp if L == 1 else act, P["p32"], P["p16"], y.data_ptr(),
+                                  P["grad"], P["loss"], P["correct"], 1.0 / self.batch_size,
+                                  FWD_WRITE_GRAD, stream), "mlp_fwd_ce")
         opt = OPTIMIZERS[self.optimizer]
         for l in range(L - 1, -1, -1):
-            src = xb if l == 0 else self.act
             flags = BWD_UPDATE_BIAS
             if l > 0:
                 flags |= BWD_HAS_DX | (BWD_IN_DROPOUT if drop else 0)
-            check(lib.mopt_mlp_bwd(tb["tl"].data_ptr(), tb["bwd"][l].data_ptr(), tb["n_bwd"][l],
-                                   src.data_ptr(), self.grad.data_ptr(), self.p32.data_ptr(),
-                                   self.p16.data_ptr(), self.m32.data_ptr(), self.v32.data_ptr(),
-                                   self.hp_dev.data_ptr(), opt, flags, stream), "mlp_bwd")
+            check(lib.mopt_mlp_bwd(tl, P["bwd"][l], tb["n_bwd"][l], xp if l == 0 else act,
+                                   P["grad"], P["p32"], P["p16"], P["m32"], P["v32"], P["hp"],
+                                   opt, flags, stream), "mlp_bwd")
 
     def _train_step_torch(self, x, y) -> None:
-        self.loss.zero_()
-        self.correct.zero_()
+        self.stats.zero_()
         em = self.emulate_bf16
         xf = x.float()
         for s in self.active_slots():
@@ -508,11 +514,18 @@ class PopulationMLP:
     def evaluate(self, x: torch.Tensor, y: torch.Tensor, slots=None):
         """Mean loss and accuracy per slot (numpy [capacity]; NaN for empty slots and for slots
         outside ``slots`` when a subset is given)."""
+        handle = self.evaluate_async(x, y, slots)
+        return self.eval_result(self.stats_snapshot(), handle)
+
+    @torch.no_grad()
+    def evaluate_async(self, x: torch.Tensor, y: torch.Tensor, slots=None):
+        """Queue the evaluation kernels (no host sync); read back with :meth:`eval_result`."""
         self._refresh()
         rows = x.shape[0]
         subset = None if slots is None else set(int(s) for s in slots)
         if rows % 128 or rows > self.eval_batch:
             raise ValueError(f"eval rows must be a multiple of 128 and <= {self.eval_batch}")
+        handle = {"rows": rows, "subset": subset}
         if self.backend == "hip":
             from ._lib import check, stream_ptr
             if "eval" not in self._tables:
@@ -520,9 +533,9 @@ class PopulationMLP:
             lib, tb, L = self._lib, self._tables["eval"], self.L
             if subset is not None:
                 tb = self._subset_table(tb, subset)
+            handle["table"] = tb  # keeps the subset work lists alive until the kernels ran
             stream = stream_ptr(self.device)
-            self.loss.zero_()
-            self.correct.zero_()
+            self.stats[2 * self.capacity:].zero_()
             xb = x.contiguous()
             rb = rows // 128
             for l in range(L - 1):
@@ -535,13 +548,10 @@ class PopulationMLP:
             check(lib.mopt_mlp_fwd_ce(tb["tl"].data_ptr(), tb["fwd"][L - 1].data_ptr(),
                                       tb["n_fwd"][L - 1], rb, src.data_ptr(), self.p32.data_ptr(),
                                       self.p16.data_ptr(), y.data_ptr(), self.grad.data_ptr(),
-                                      self.loss.data_ptr(), self.correct.data_ptr(), 1.0, 0, stream),
-                  "mlp_fwd_ce(eval)")
-            loss = self.loss.float().cpu().numpy() / rows
-            acc = self.correct.float().cpu().numpy() / rows
+                                      self.eval_loss.data_ptr(), self.eval_correct.data_ptr(), 1.0,
+                                      0, stream), "mlp_fwd_ce(eval)")
         else:
-            loss = np.zeros(self.capacity, dtype=np.float32)
-            acc = np.zeros(self.capacity, dtype=np.float32)
+            self.stats[2 * self.capacity:].zero_()
             xf = x.float()
             em = self.emulate_bf16
             for s in self.active_slots():
@@ -557,13 +567,30 @@ class PopulationMLP:
                 w, b = layers[-1]
                 wq = ref.bf16_round(w) if em else w
                 ls, cs, _ = ref.softmax_ce(a @ wq.t() + b, y, self.num_classes, 1.0, em)
-                loss[s] = float(ls) / rows
-                acc[s] = float(cs) / rows
+                self.eval_loss[s] = ls
+                self.eval_correct[s] = cs
+        return handle
+
+    def stats_snapshot(self) -> np.ndarray:
+        """One device->host copy of the train and eval statistics (waits for queued work)."""
+        return self.stats.cpu().numpy().reshape(4, self.capacity)
+
+    def eval_result(self, snap: np.ndarray, handle):
+        rows, subset = handle["rows"], handle["subset"]
+        loss = snap[2].astype(np.float64) / rows
+        acc = snap[3].astype(np.float64) / rows
         for s in range(self.capacity):
             if self.members[s] is None or (subset is not None and s not in subset):
                 loss[s] = np.nan
                 acc[s] = np.nan
         return loss, acc
+
+    def train_loss(self, snap: Optional[np.ndarray] = None) -> np.ndarray:
+        """Mean training loss of the last step per slot."""
+        snap = self.stats_snapshot() if snap is None else snap
+        out = snap[0].astype(np.float64) / self.batch_size
+        out[~np.array([m is not None for m in self.members])] = np.nan
+        return out
 
     def _subset_table(self, tb: dict, subset) -> dict:
         L = self.L
@@ -575,10 +602,3 @@ class PopulationMLP:
         out["n_fwd"] = [len(w) for w in fwd]
         return out
 
-    def train_loss(self) -> np.ndarray:
-        """Mean training loss of the last step per slot."""
-        out = self.loss.float().cpu().numpy() / self.batch_size
-        for s in range(self.capacity):
-            if self.members[s] is None:
-                out[s] = np.nan
-        return out

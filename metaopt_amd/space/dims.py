@@ -132,8 +132,11 @@ class Dimension:
         are immutable and scipy's ``interval`` costs tens of microseconds)."""
         cache = self.__dict__.setdefault("_interval_cache", {})
         if alpha not in cache:
-            cache[alpha] = self.prior.interval(alpha, *self._args, **self._kwargs)
+            cache[alpha] = self._compute_interval(alpha)
         return cache[alpha]
+
+    def _compute_interval(self, alpha=1.0):
+        return self.prior.interval(alpha, *self._args, **self._kwargs)
 
     def __contains__(self, point):
         raise NotImplementedError
@@ -216,8 +219,8 @@ class Real(Dimension):
             return False
         return bool(numpy.all(p < high) and numpy.all(p >= low))
 
-    def interval(self, alpha=1.0):
-        lo, hi = super().interval(alpha)
+    def _compute_interval(self, alpha=1.0):
+        lo, hi = super()._compute_interval(alpha)
         return (max(lo, self._low), min(hi, self._high))
 
     def _in_bounds(self, draws: numpy.ndarray) -> numpy.ndarray:
@@ -265,8 +268,8 @@ class Real(Dimension):
 
 
 class _Discrete(Dimension):
-    def interval(self, alpha=1.0):
-        low, high = super().interval(alpha)
+    def _compute_interval(self, alpha=1.0):
+        low, high = super()._compute_interval(alpha)
         try:
             int_low = int(numpy.floor(low))
         except OverflowError:

@@ -63,6 +63,7 @@ class PopulationSweep:
         self.heartbeat_every = heartbeat_every
         P = pop.capacity
         self.slot_key = np.full(P, -1, dtype=np.int64)
+        self._n_active = 0
         self.slot_budget = np.zeros(P, dtype=np.int64)
         self.ckpts: "collections.OrderedDict[int, dict]" = collections.OrderedDict()
         self.global_step = 0
@@ -97,10 +98,12 @@ class PopulationSweep:
         self._sync(evaluate=False)
 
     def step(self) -> None:
+        t0 = time.perf_counter()
         x, y = self.data.batch(self.global_step)
         self.pop.train_step(x, y)
         self.global_step += 1
-        self.samples += self.pop.batch_size * int((self.slot_key >= 0).sum())
+        self.samples += self.pop.batch_size * self._n_active
+        self.timers["launch"] += time.perf_counter() - t0
         if self.global_step % self.sync_every == 0:
             self._sync()
 
@@ -119,29 +122,35 @@ class PopulationSweep:
         P = pop.capacity
         st = np.zeros((P, ST_COLS), dtype=np.float64)
         st[:, 0] = self.slot_key
-        steps = np.array([pop.steps_done(s) for s in range(P)], dtype=np.float64)
+        steps = pop.hp["t"].astype(np.float64)  # host mirror of the per-slot step counters
         st[:, 1] = steps
         st[:, 2] = self.slot_budget
         active = self.slot_key >= 0
-        if self._writer is not None:
-            # hand the storage writes of the previous decision to the writer thread now: the
-            # GPU is busy with the interval just queued and the main thread is about to block
-            self._writer.release()
-        if active.any() and self.global_step > 0:
-            tl = pop.train_loss()
-            st[:, 3] = np.where(active, tl, np.nan)
-            bad = active & ~np.isfinite(tl)
-            st[:, 6] = bad
-        finished = [s for s in range(P) if active[s] and steps[s] >= self.slot_budget[s]
-                    and not st[s, 6]]
+        finished = np.flatnonzero(active & (steps >= self.slot_budget)).tolist()
+        # 1) queue the validation of every member that reached its budget behind the interval's
+        #    training kernels (no host sync yet)
+        handle = None
         if evaluate and finished:
             vx, vy = self.data.validation()
-            vl, va = pop.evaluate(vx, vy, slots=finished)
-            st[finished, 4] = vl[finished]
-            st[finished, 5] = va[finished]
-            for s in finished:
-                if not math.isfinite(vl[s]):
-                    st[s, 6] = 1
+            handle = pop.evaluate_async(vx, vy, slots=finished)
+        # 2) storage writes of the previous decision run on the host while the GPU works
+        if self._writer is not None:
+            self._writer.release()
+        # 3) one device->host copy of train + eval statistics
+        if active.any() and self.global_step > 0:
+            snap = pop.stats_snapshot()
+            tl = pop.train_loss(snap)
+            st[:, 3] = np.where(active, tl, np.nan)
+            st[:, 6] = active & ~np.isfinite(tl)
+            if handle is not None:
+                vl, va = pop.eval_result(snap, handle)
+                for s in finished:
+                    if st[s, 6]:
+                        continue
+                    st[s, 4] = vl[s]
+                    st[s, 5] = va[s]
+                    if not math.isfinite(vl[s]):
+                        st[s, 6] = 1
         return st
 
     def _sync(self, evaluate=True) -> None:
@@ -356,6 +365,7 @@ class PopulationSweep:
             self.slot_key[s] = int(a[1])
             self.slot_budget[s] = int(a[8])
         self.done = bool(assign[-1, 0])
+        self._n_active = int((self.slot_key >= 0).sum())
 
     def _max_budget_local(self) -> int:
         return getattr(self, "_mb", None) or self._compute_mb()

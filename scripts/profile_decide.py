@@ -39,7 +39,7 @@ def main(n_syncs=40, P=256, profile=False):
     gathered[:, 0] = -1
     assign = sw._decide(gathered)
     prof = cProfile.Profile() if profile else None
-    t_total = 0.0
+    t_total = t_rel = 0.0
     n_done = 0
     for _ in range(n_syncs):
         # apply: new/resumed members start from 0 (resume: from their checkpoint steps)
@@ -63,11 +63,18 @@ def main(n_syncs=40, P=256, profile=False):
         if prof:
             prof.disable()
         t_total += time.perf_counter() - t0
+        t1 = time.perf_counter()
+        sw._writer.release()
+        t_rel += time.perf_counter() - t1
     sw.close()
-    print(f"decide: {1e3 * t_total / n_syncs:.2f} ms/sync, {n_done / n_syncs:.1f} completions/sync")
+    print(f"decide: {1e3 * t_total / n_syncs:.2f} ms/sync, writes {1e3 * t_rel / n_syncs:.2f} ms/sync, "
+          f"{n_done / n_syncs:.1f} completions/sync")
     if prof:
         pstats.Stats(prof).sort_stats("cumulative").print_stats(30)
 
 
 if __name__ == "__main__":
-    main(profile="--profile" in sys.argv)
+    if "--nogc" in sys.argv:
+        import gc
+        gc.disable()
+    main(n_syncs=int(os.environ.get("N_SYNCS", 40)), profile="--profile" in sys.argv)
