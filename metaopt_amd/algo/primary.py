@@ -60,6 +60,17 @@ class PrimaryAlgo(BaseAlgorithm):
             tpoints.append(self.transformed_space.transform(p))
         self.algorithm.observe(tpoints, results)
 
+    def parent_of(self, point):
+        """Point whose trained state ``point`` resumes from (PBT exploit, ASHA promotion), if the
+        algorithm tracks lineage; None otherwise."""
+        fn = getattr(self.algorithm, "parent_of", None)
+        if fn is None:
+            return None
+        parent = fn(self.transformed_space.transform(point))
+        if parent is None:
+            return None
+        return tuple(_plain(v) for v in self.transformed_space.reverse(parent))
+
     @property
     def is_done(self):
         return self.algorithm.is_done

@@ -15,6 +15,8 @@ Config 1 (logistic regression, CPU) is the same task with ``n_hidden=0`` and a 2
 from __future__ import annotations
 
 import hashlib
+
+import numpy as np
 from dataclasses import dataclass, field
 from typing import Dict, Optional
 
@@ -36,8 +38,17 @@ LOGREG_PRIORS = {
 
 def param_key(params: Dict, fidelity_name: str) -> str:
     """Identity of a configuration regardless of its budget (the ASHA promotion key)."""
-    items = sorted((k, v) for k, v in params.items() if k != fidelity_name)
+    items = sorted((k, _plain(v)) for k, v in params.items() if k != fidelity_name)
     return hashlib.md5(repr(items).encode("utf-8")).hexdigest()
+
+
+def _plain(v):
+    """numpy scalars/arrays -> Python values, so equal configurations hash equally."""
+    if isinstance(v, np.ndarray):
+        return v.tolist()
+    if isinstance(v, np.generic):
+        return v.item()
+    return v
 
 
 @dataclass

@@ -302,8 +302,36 @@ class PopulationMLP:
     # ------------------------------------------------------------------ checkpoints (device)
     def used_params(self, slot: int) -> int:
         """Length of the prefix of the slot region the member actually uses."""
-        cfg = self.members[slot]
-        return sum(pad64(k * n) + pad64(n) for k, n in self.layer_dims(cfg.width))
+        return self.used_params_for(self.members[slot].width)
+
+    def used_params_for(self, width: int) -> int:
+        return sum(pad64(k * n) + pad64(n) for k, n in self.layer_dims(width))
+
+    # -- flat checkpoint images (C4: point-to-point copies between ranks) ----------------------
+    def _n_state_buffers(self) -> int:
+        return 3 if self.optimizer == "adamw" else 2
+
+    def empty_packed_state(self, width: int) -> torch.Tensor:
+        n = self.used_params_for(width)
+        return torch.empty(2 + self._n_state_buffers() * n, dtype=torch.float32,
+                           device=self.device)
+
+    def pack_state(self, state: dict) -> torch.Tensor:
+        """[t, seed (int32 bit patterns), p32, m32(, v32)] as one f32 tensor."""
+        head = torch.tensor([int(state["t"]), int(state["config"]["seed"])], dtype=torch.int32)
+        parts = [head.view(torch.float32).to(self.device), state["p32"], state["m32"]]
+        if self.optimizer == "adamw":
+            parts.append(state["v32"])
+        return torch.cat([t.reshape(-1).to(self.device, torch.float32) for t in parts])
+
+    def unpack_state(self, buf: torch.Tensor, width: int) -> dict:
+        n = self.used_params_for(width)
+        t, seed = (int(v) for v in buf[:2].view(torch.int32).cpu().tolist())
+        st = {"config": MemberConfig(width=width, lr=0.0, seed=seed).to_dict(), "t": t,
+              "p32": buf[2:2 + n], "m32": buf[2 + n:2 + 2 * n], "optimizer": self.optimizer}
+        if self.optimizer == "adamw":
+            st["v32"] = buf[2 + 2 * n:2 + 3 * n]
+        return st
 
     def slot_state(self, slot: int, to_cpu: bool = False) -> dict:
         """Device checkpoint of a member: config, step count, weights and optimizer state

@@ -73,6 +73,18 @@ class Comm:
         dist.recv(t, src=src, group=self.group)
         return t
 
+    def exchange(self, ops) -> None:
+        """Batched point-to-point transfers: ``ops`` = [("send"|"recv", tensor, peer)].  One
+        ``batch_isend_irecv`` group, so pairs of ranks sending to each other cannot deadlock."""
+        if not ops:
+            return
+        if not self.distributed:
+            raise RuntimeError("point-to-point exchange needs a process group")
+        p2p = [dist.P2POp(dist.isend if kind == "send" else dist.irecv, t, peer, group=self.group)
+               for kind, t, peer in ops]
+        for req in dist.batch_isend_irecv(p2p):
+            req.wait()
+
     def barrier(self) -> None:
         if self.distributed:
             if self.device.type == "cuda":

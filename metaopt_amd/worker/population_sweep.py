@@ -44,7 +44,7 @@ log = logging.getLogger(__name__)
 
 NONE, NEW, RESUME, CLEAR = 0, 1, 2, 3
 ST_COLS = 7     # key, steps, budget, train_loss, val_loss, val_acc, bad
-AS_COLS = 10    # action, key, width, lr, momentum, wd, dropout, seed, budget, resume_key
+AS_COLS = 11    # action, key, width, lr, momentum, wd, dropout, seed, budget, resume_key, src_rank
 
 
 class PopulationSweep:
@@ -86,6 +86,8 @@ class PopulationSweep:
                            (experiment.max_trials if experiment is not None else math.inf))
         self._writer = None
         self.timers: Dict[str, float] = collections.defaultdict(float)  # host seconds per phase
+        self.n_resumed = 0            # members resumed from a device checkpoint (this rank)
+        self.n_resume_missing = 0
         self.n_syncs = 0
         if self.comm.is_root:
             self.algorithm = experiment.algorithms
@@ -270,27 +272,37 @@ class PopulationSweep:
             return
         free_by_rank = {r: [row for row in free_rows if row // P == r] for r in range(W)}
         stamp = datetime.datetime.utcnow()
+        parent_of = getattr(self.algorithm, "parent_of", None)
+        keys = self.space.keys()
         for point in points:
-            params = dict(zip(self.space.keys(), point))
+            params = dict(zip(keys, point))
             pkey = self.task.key(params)
-            owner = self.ckpt_index.get(pkey)
+            # lineage-tracking algorithms (PBT exploit, Hyperband/ASHA promotion) name the point
+            # whose device state the new trial continues; otherwise the same hyper-parameters at
+            # a lower fidelity are looked up (ASHA promotion)
+            parent = parent_of(point) if parent_of is not None else None
+            ckey = self.task.key(dict(zip(keys, parent))) if parent is not None else pkey
+            owner = self.ckpt_index.get(ckey)
+            src = -1
             if owner is not None and free_by_rank[owner[0]]:
+                # resume next to the checkpoint (no copy between GPUs)
                 row = free_by_rank[owner[0]].pop(0)
-                action, resume = RESUME, owner[1]
-                del self.ckpt_index[pkey]
-                self._ckpt_pkey.pop((owner[0], owner[1]), None)
-                try:  # the owner drops the checkpoint when it resumes it: mirror that
-                    self.ckpt_fifo[owner[0]].remove(owner[1])
-                except ValueError:
-                    pass
+                action, resume, src = RESUME, owner[1], owner[0]
             else:
                 rank = max(free_by_rank, key=lambda r: len(free_by_rank[r]))
                 if not free_by_rank[rank]:
                     break
                 row = free_by_rank[rank].pop(0)
-                action, resume = NEW, -1
+                if owner is not None:   # C4: the owner sends the checkpoint to that rank (P2P)
+                    action, resume, src = RESUME, owner[1], owner[0]
+                else:
+                    action, resume = NEW, -1
             trial = format_trials.tuple_to_trial(point, self.space)
             trial.experiment = self.experiment.id
+            if parent is not None:
+                ptrial = format_trials.tuple_to_trial(parent, self.space)
+                ptrial.experiment = self.experiment.id
+                trial.parents = [ptrial.id]
             trial.status = "reserved"
             trial.submit_time = trial.start_time = trial.heartbeat = stamp
             if trial.id in self._registered:
@@ -305,7 +317,7 @@ class PopulationSweep:
             self.key_params[key] = params
             cfg = self.task.member_config(params, self.task.seed_of(pkey))
             assign[row] = (action, key, cfg.width, cfg.lr, cfg.momentum, cfg.weight_decay,
-                           cfg.dropout, cfg.seed, self.task.budget(params), resume)
+                           cfg.dropout, cfg.seed, self.task.budget(params), resume, src)
 
     def _set_status(self, trial, status):
         self._writer.put("set_trial_status", trial, status, was="reserved")
@@ -335,10 +347,14 @@ class PopulationSweep:
         mine = assign[r0:r0 + P]
         g = gathered[r0:r0 + P]
         max_b = None
-        # checkpoint every member that completed below the top budget (rank 0 mirrors the rule)
+        # every member that finished (or broke) at this sync leaves its slot -- whether the slot
+        # is CLEARed or immediately re-assigned; the ones that completed below the top budget are
+        # checkpointed first (rank 0 mirrors the rule in _decide/_record_ckpt)
         for s in range(P):
-            if mine[s, 0] == CLEAR and self.slot_key[s] >= 0:
-                finished_ok = g[s, 6] == 0 and g[s, 1] >= g[s, 2]
+            if self.slot_key[s] < 0:
+                continue
+            if g[s, 6] > 0 or g[s, 1] >= g[s, 2]:
+                finished_ok = g[s, 6] == 0
                 if max_b is None:
                     max_b = self._max_budget_local()
                 if finished_ok and self.slot_budget[s] < max_b:
@@ -348,6 +364,7 @@ class PopulationSweep:
                 pop.remove_member(s)
                 self.slot_key[s] = -1
                 self.slot_budget[s] = 0
+        received = self._exchange_checkpoints(assign)
         for s in range(P):
             a = mine[s]
             act = int(a[0])
@@ -355,17 +372,52 @@ class PopulationSweep:
                 continue
             cfg = MemberConfig(width=int(a[2]), lr=float(a[3]), momentum=float(a[4]),
                                weight_decay=float(a[5]), dropout=float(a[6]), seed=int(a[7]))
-            st = self.ckpts.pop(int(a[9]), None) if act == RESUME else None
+            st = None
+            if act == RESUME:
+                # checkpoints are not consumed: a PBT winner can seed several members
+                st = received.get(s) if s in received else self.ckpts.get(int(a[9]))
             if st is not None:
                 pop.load_slot_state(s, st)
                 pop.update_hparams(s, lr=cfg.lr, momentum=cfg.momentum,
                                    weight_decay=cfg.weight_decay, dropout=cfg.dropout)
+                self.n_resumed += 1
             else:
+                if act == RESUME:  # evicted checkpoint: the trial retrains from scratch
+                    self.n_resume_missing += 1
+                    log.warning("checkpoint of trial %d missing; trial %d starts from scratch",
+                                int(a[9]), int(a[1]))
                 pop.set_member(s, cfg, init=True)
             self.slot_key[s] = int(a[1])
             self.slot_budget[s] = int(a[8])
         self.done = bool(assign[-1, 0])
         self._n_active = int((self.slot_key >= 0).sum())
+
+    def _exchange_checkpoints(self, assign: np.ndarray) -> Dict[int, dict]:
+        """C4: checkpoints resumed on another rank travel point-to-point (one batched group of
+        isend/irecv over RCCL/xGMI).  Returns {local slot: state} of the received ones."""
+        W, P, me = self.comm.world_size, self.pop.capacity, self.comm.rank
+        if W == 1:
+            return {}
+        ops, recv = [], {}
+        for row in range(W * P):
+            a = assign[row]
+            if int(a[0]) != RESUME:
+                continue
+            src, dst = int(a[10]), row // P
+            if src == dst or src < 0:
+                continue
+            if me == src:
+                st = self.ckpts.get(int(a[9]))
+                if st is None:
+                    raise RuntimeError(f"rank {me} lost checkpoint of trial {int(a[9])}")
+                ops.append(("send", self.pop.pack_state(st), dst))
+            elif me == dst:
+                buf = self.pop.empty_packed_state(int(a[2]))
+                recv[row % P] = buf
+                ops.append(("recv", buf, src))
+        self.comm.exchange(ops)
+        return {s: self.pop.unpack_state(buf, int(assign[me * P + s, 2]))
+                for s, buf in recv.items()}
 
     def _max_budget_local(self) -> int:
         return getattr(self, "_mb", None) or self._compute_mb()

@@ -230,3 +230,94 @@ class TestStrategies:
         t.results = [Trial.Result(name="o", type="objective", value=1.0)]
         with pytest.raises(RuntimeError):
             MaxParallelStrategy().lie(t)
+
+
+class TestPBT:
+    def _space(self):
+        return build_space({"/lr": "loguniform(1e-4, 1)", "/width": "choices([64, 128])",
+                            "/steps": "fidelity(10, 40, 2)"})
+
+    def test_timeline_and_initial_population(self):
+        pbt = create_algo(self._space(), {"pbt": {"seed": 1, "population_size": 6,
+                                                   "interval": 10}})
+        assert pbt.timeline == [10, 20, 30, 40]
+        pts = pbt.suggest(10)
+        assert len(pts) == 6 and all(p[1] == 10 for p in pts)
+        assert pbt.suggest(1) is None           # waits for results
+
+    def test_exploit_copies_winner_and_perturbs(self):
+        space = self._space()
+        pbt = create_algo(space, {"pbt": {"seed": 2, "population_size": 10, "interval": 10,
+                                           "min_forking_population": 10, "freeze": ["/width"]}})
+        pts = pbt.suggest(10)
+        objs = {p: float(i) for i, p in enumerate(sorted(pts, key=lambda p: p[0]))}
+        pbt.observe(list(objs), [{"objective": o} for o in objs.values()])
+        succ = pbt.suggest(10)
+        assert len(succ) == 10 and all(s[1] == 20 for s in succ)
+        best = min(objs, key=objs.get)
+        worst = max(objs, key=objs.get)
+        for s in succ:
+            parent = pbt.parent_of(s)
+            assert parent is not None and parent[1] == 10
+            if objs[parent] <= 1.0 and parent != s[:1] + (10,) + s[2:]:
+                # exploited child: copy of a top member, lr perturbed by 1.2**+-1, width frozen
+                assert s[2] == parent[2]
+                assert abs(s[0] / parent[0] - 1.2) < 1e-9 or abs(parent[0] / s[0] - 1.2) < 1e-9
+        # the worst member never continues itself
+        assert all(pbt.parent_of(s) != worst for s in succ)
+        assert any(pbt.parent_of(s) == best for s in succ)
+        assert all(s in space for s in succ)
+
+    def test_done_after_last_generation(self):
+        pbt = create_algo(self._space(), {"pbt": {"seed": 3, "population_size": 4,
+                                                   "interval": 10, "min_forking_population": 2}})
+        pts = pbt.suggest(4)
+        for _ in range(4):
+            pbt.observe(pts, [{"objective": float(i)} for i in range(len(pts))])
+            if pbt.is_done:
+                break
+            pts = pbt.suggest(4)
+        assert pbt.is_done
+
+    def test_primary_forwards_parent(self):
+        space = self._space()
+        primary = PrimaryAlgo(space, {"pbt": {"seed": 4, "population_size": 5, "interval": 10,
+                                              "min_forking_population": 5}})
+        pts = primary.suggest(5)
+        primary.observe(pts, [{"objective": float(i)} for i in range(5)])
+        nxt = primary.suggest(5)
+        assert all(primary.parent_of(p) in pts for p in nxt)
+
+
+class TestGridAndHyperband:
+    def test_grid(self):
+        space = build_space({"/x": "uniform(0, 1)", "/c": "choices(['a', 'b'])",
+                             "/lr": "loguniform(1e-3, 1)"})
+        grid = create_algo(space, {"gridsearch": {"n_values": 3}})
+        pts = []
+        while True:
+            got = grid.suggest(5)
+            if got is None:
+                break
+            pts.extend(got)
+        assert len(pts) == 2 * 3 * 3 and len(set(pts)) == 18
+        lrs = sorted({p[1] for p in pts})
+        assert abs(lrs[1] / lrs[0] - lrs[2] / lrs[1]) < 1e-6   # log-spaced
+        grid.observe(pts, [{"objective": 0.0}] * len(pts))
+        assert grid.is_done
+
+    def test_hyperband_synchronous_halving(self):
+        space = build_space({"/x": "uniform(0, 1)", "/e": "fidelity(1, 9, 3)"})
+        hb = create_algo(space, {"hyperband": {"seed": 1}})
+        assert [len(r) for r in hb.schedule] == [3, 2, 1]
+        assert hb.schedule[0] == [(9, 1), (3, 3), (1, 9)]
+        first = hb.suggest(100)
+        assert len(first) == 9 and all(p[0] == 1 for p in first)
+        hb.observe(first[:8], [{"objective": p[1]} for p in first[:8]])
+        assert hb.suggest(5) is None            # synchronous: waits for the whole rung
+        hb.observe(first[8:], [{"objective": first[8][1]}])
+        promo = hb.suggest(10)
+        best3 = sorted(first, key=lambda p: p[1])[:3]
+        assert sorted(p[1] for p in promo) == sorted(p[1] for p in best3)
+        assert all(p[0] == 3 for p in promo)
+        assert all(hb.parent_of(p) in first for p in promo)

@@ -94,10 +94,73 @@ def test_sharded_sweep_gloo_world2():
     procs = [ctx.Process(target=_sweep_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted(q.get(timeout=600) for _ in range(world))
+    res = sorted(q.get(timeout=300) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
     (r0, samples0, done0, statuses, fin0), (r1, samples1, _, _, fin1) = res
     assert samples0 > 0 and samples1 > 0          # both ranks trained trials
     assert done0 == 20 and statuses.count("completed") == 20
     assert fin0 and fin1                          # both ranks saw the "done" flag
+
+
+def _pbt_worker(rank, world, port, q):
+    comm = _init(rank, world, port)
+    import numpy as np
+    from metaopt_amd.io.experiment_builder import build_experiment
+    from metaopt_amd.models.data import TeacherClassification
+    from metaopt_amd.models.mlp import MLPSweepTask
+    from metaopt_amd.ops.population import PopulationMLP
+    from metaopt_amd.storage.database import EphemeralDB
+    from metaopt_amd.storage.protocol import DocumentStorage
+    from metaopt_amd.worker.population_sweep import NEW, RESUME, AS_COLS, PopulationSweep
+    priors = {"/lr": "loguniform(1e-3, 1.0)", "/width": "choices([64])",
+              "/steps": "fidelity(16, 48, 2)"}
+    exp = None
+    if rank == 0:
+        exp = build_experiment("dist-pbt", priors=priors,
+                               algorithms={"pbt": {"seed": 3, "population_size": 6,
+                                                   "interval": 16, "min_forking_population": 6,
+                                                   "freeze": ["/width"]}},
+                               storage=DocumentStorage(EphemeralDB()))
+    data = TeacherClassification(n_train=512, n_val=128, batch_size=128, seed=1)
+    pop = PopulationMLP(3, max_width=64, eval_batch=128, device="cpu")
+    sweep = PopulationSweep(pop, MLPSweepTask(priors=priors, max_width=64), data, comm=comm,
+                            experiment=exp, sync_every=16)
+    # C4 directly: rank 0 holds a checkpoint that rank 1 resumes in its slot 2
+    sweep.start()
+    st = pop.slot_state(0)
+    sweep.ckpts[999] = st
+    assign = np.zeros((2 * 3 + 1, AS_COLS))
+    assign[3 + 2] = (RESUME, 0, 64, 0.1, 0.9, 0, 0, 7, 16, 999, 0)
+    got = sweep._exchange_checkpoints(assign)
+    c4 = None
+    if rank == 1:
+        c4 = (sorted(got), got[2]["t"], got[2]["p32"].shape[0])
+    ref = (int(st["t"]), st["p32"].shape[0], float(st["p32"].sum())) if rank == 0 else None
+    del sweep.ckpts[999]
+    summary = sweep.run(400)
+    sweep.close()
+    parents = None
+    if rank == 0:
+        trials = exp.fetch_trials()
+        parents = (len(trials), sum(1 for t in trials if t.parents),
+                   sum(1 for t in trials if t.status == "completed"))
+    q.put((rank, c4, ref, parents, summary["completed"], sweep.done))
+    dist.destroy_process_group()
+
+
+def test_pbt_sweep_and_c4_copy_gloo_world2():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_pbt_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    (r0, _, ref, parents, done0, fin0), (r1, c4, _, _, _, fin1) = res
+    assert c4[0] == [2] and c4[1] == ref[0] and c4[2] == ref[1]
+    n_trials, n_children, n_completed = parents
+    assert n_trials == 18 and n_children == 12      # 6 members x 3 generations
+    assert n_completed == 18 and fin0 and fin1

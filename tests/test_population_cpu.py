@@ -107,6 +107,9 @@ def test_sweep_asha_end_to_end(data):
     assert len(trials) == 24 and all(t.status == "completed" for t in trials)
     budgets = sorted(t.params_dict["/steps"] for t in trials)
     assert budgets[0] == 16 and budgets[-1] >= 32  # promotions happened
+    # every promotion continued from the lower-rung device checkpoint (none retrained)
+    assert sweep.n_resumed == sum(1 for b in budgets if b > 16)
+    assert sweep.n_resume_missing == 0
     assert exp.stats["best_evaluation"] == pytest.approx(summary["best_val_loss"])
 
 
@@ -123,3 +126,25 @@ def test_sweep_marks_diverged_members_broken(data):
     statuses = [t.status for t in exp.fetch_trials()]
     assert summary["broken"] + summary["completed"] == 4
     assert statuses.count("broken") == summary["broken"]
+
+
+def test_sweep_pbt_generations_resume_state(data):
+    priors = {"/lr": "loguniform(1e-3, 1.0)", "/width": "choices([64])",
+              "/steps": "fidelity(16, 48, 2)"}
+    exp = build_experiment("sweep-pbt", priors=priors,
+                           algorithms={"pbt": {"seed": 3, "population_size": 6, "interval": 16,
+                                               "min_forking_population": 6,
+                                               "freeze": ["/width"]}},
+                           storage=DocumentStorage(EphemeralDB()))
+    pop = PopulationMLP(6, max_width=64, eval_batch=256, device="cpu")
+    sweep = PopulationSweep(pop, MLPSweepTask(priors=priors, max_width=64), data,
+                            experiment=exp, sync_every=16)
+    summary = sweep.run(200)
+    sweep.close()
+    assert sweep.done and summary["completed"] == 18
+    assert sweep.global_step == 48          # 3 generations x 16 steps, no retraining
+    assert sweep.n_resumed == 12 and sweep.n_resume_missing == 0
+    trials = exp.fetch_trials()
+    ids = {t.id for t in trials}
+    children = [t for t in trials if t.parents]
+    assert len(children) == 12 and all(t.parents[0] in ids for t in children)
