@@ -1,0 +1,60 @@
+"""Batched device copies (``mopt_multi_copy``) used by the sweep's checkpoint pool.
+
+``multi_copy(items)`` moves every ``(src, dst, dst16)`` triple of f32 views in ONE kernel launch
+on the GPU (``dst16``: optional bf16 view that receives the rounded copy), or with plain tensor
+copies on the CPU reference backend.  Replaces the one-framework-copy-per-tensor checkpoint and
+resume path that left the GPU idle for ~0.3 ms per copy at every sync.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Iterable, Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+
+DESC_DTYPE = np.dtype([("src", "<u8"), ("dst", "<u8"), ("dst16", "<u8"), ("n", "<i8")])
+CHUNK_DTYPE = np.dtype([("desc", "<i4"), ("pad", "<i4"), ("start", "<i8")])
+CHUNK = 4096
+
+_lib.register_signatures({
+    "mopt_multi_copy": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p],
+                        ctypes.c_int),
+})
+
+
+def multi_copy(items: Iterable[Tuple[torch.Tensor, torch.Tensor, Optional[torch.Tensor]]]):
+    items = list(items)
+    if not items:
+        return
+    dev = items[0][1].device
+    if dev.type != "cuda":
+        for src, dst, dst16 in items:
+            dst.copy_(src)
+            if dst16 is not None:
+                dst16.copy_(src.to(dst16.dtype))
+        return
+    descs = np.zeros(len(items), dtype=DESC_DTYPE)
+    counts = []
+    for i, (src, dst, dst16) in enumerate(items):
+        n = src.numel()
+        if dst.numel() != n or (dst16 is not None and dst16.numel() != n):
+            raise ValueError("multi_copy: size mismatch")
+        if n % 4 or not (src.is_contiguous() and dst.is_contiguous()):
+            raise ValueError("multi_copy: views must be contiguous with a multiple of 4 elements")
+        if src.dtype != torch.float32 or dst.dtype != torch.float32:
+            raise TypeError("multi_copy moves f32 data")
+        descs[i] = (src.data_ptr(), dst.data_ptr(), 0 if dst16 is None else dst16.data_ptr(), n)
+        counts.append((n + CHUNK - 1) // CHUNK)
+    counts = np.array(counts, dtype=np.int64)
+    chunks = np.zeros(int(counts.sum()), dtype=CHUNK_DTYPE)
+    chunks["desc"] = np.repeat(np.arange(len(items), dtype=np.int32), counts)
+    first = np.concatenate([[0], np.cumsum(counts)[:-1]])
+    chunks["start"] = (np.arange(len(chunks)) - np.repeat(first, counts)) * CHUNK
+    d = torch.from_numpy(descs.view(np.uint8).copy()).to(dev, non_blocking=True)
+    c = torch.from_numpy(chunks.view(np.uint8).copy()).to(dev, non_blocking=True)
+    lib = _lib.get_lib()
+    _lib.check(lib.mopt_multi_copy(d.data_ptr(), c.data_ptr(), len(chunks),
+                                   _lib.stream_ptr(dev)), "multi_copy")

@@ -307,6 +307,57 @@ class PopulationMLP:
     def used_params_for(self, width: int) -> int:
         return sum(pad64(k * n) + pad64(n) for k, n in self.layer_dims(width))
 
+    # -- checkpoint pool: batched save / restore of members (one kernel launch each) ------------
+    def alloc_ckpt_pool(self, n: int) -> None:
+        """``n`` checkpoint slots, each as large as a population slot (f32 master weights and
+        optimizer state; 288 GB of HBM holds thousands)."""
+        self.ck = torch.zeros(n, self._n_state_buffers(), self.slot_params, dtype=torch.float32,
+                              device=self.device)
+
+    def _state_tensors(self):
+        return [self.p32, self.m32] + ([self.v32] if self.optimizer == "adamw" else [])
+
+    def save_states(self, pairs) -> list:
+        """Checkpoint members: ``pairs`` = [(slot, pool index)]; returns per-member metadata."""
+        from .ckpt import multi_copy
+        self._run_pending_init()
+        items, metas = [], []
+        for slot, idx in pairs:
+            n = self.used_params(slot)
+            b = self.slot_base(slot)
+            for j, buf in enumerate(self._state_tensors()):
+                items.append((buf[b:b + n], self.ck[idx, j, :n], None))
+            metas.append({"config": self.members[slot].to_dict(), "t": int(self.hp[slot]["t"]),
+                          "ck": int(idx), "n": n})
+        multi_copy(items)
+        return metas
+
+    def load_states(self, pairs) -> None:
+        """Restore members from the pool: ``pairs`` = [(slot, metadata)] (bf16 copy included)."""
+        from .ckpt import multi_copy
+        items = []
+        for slot, meta in pairs:
+            n, idx = meta["n"], meta["ck"]
+            b = self.slot_base(slot)
+            for j, buf in enumerate(self._state_tensors()):
+                items.append((self.ck[idx, j, :n], buf[b:b + n],
+                              self.p16[b:b + n] if j == 0 else None))
+            self._pending_init.discard(slot)
+            cfg = MemberConfig(**meta["config"])
+            self.members[slot] = cfg
+            self._write_hp(slot, cfg, int(meta["t"]))
+        multi_copy(items)
+        self._dirty = True
+
+    def pool_state(self, meta: dict) -> dict:
+        """A pool checkpoint in the ``slot_state`` format (views, no copy)."""
+        n, idx = meta["n"], meta["ck"]
+        st = {"config": meta["config"], "t": meta["t"], "p32": self.ck[idx, 0, :n],
+              "m32": self.ck[idx, 1, :n], "optimizer": self.optimizer}
+        if self.optimizer == "adamw":
+            st["v32"] = self.ck[idx, 2, :n]
+        return st
+
     # -- flat checkpoint images (C4: point-to-point copies between ranks) ----------------------
     def _n_state_buffers(self) -> int:
         return 3 if self.optimizer == "adamw" else 2

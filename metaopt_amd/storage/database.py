@@ -19,6 +19,7 @@ Query operators: equality on dotted keys, ``$ne $in $nin $gt $gte $lt $lte $exis
 """
 from __future__ import annotations
 
+
 import copy
 import datetime
 import logging
@@ -28,6 +29,25 @@ from contextlib import contextmanager
 from typing import Any, Dict, Iterable, List, Optional
 
 from ..utils.registry import Registry
+
+
+_ATOMIC = (str, int, float, bool, type(None), bytes, datetime.datetime, datetime.date)
+
+
+def _copy_doc(value):
+    """Deep copy of a JSON/BSON-like document (dicts, lists, tuples, scalars, datetimes):
+    several times faster than ``copy.deepcopy`` (no memo, no reduce protocol), which matters
+    because every insert/read/update of the in-memory backends copies documents."""
+    t = type(value)
+    if t is dict:
+        return {k: _copy_doc(v) for k, v in value.items()}
+    if t is list:
+        return [_copy_doc(v) for v in value]
+    if t in _ATOMIC or isinstance(value, _ATOMIC):
+        return value
+    if t is tuple:
+        return tuple(_copy_doc(v) for v in value)
+    return copy.deepcopy(value)
 
 log = logging.getLogger(__name__)
 logging.getLogger("filelock").setLevel("ERROR")
@@ -147,7 +167,7 @@ def apply_update(doc: dict, data: dict, cow: bool = False) -> None:
         for op, fields in data.items():
             for key, value in _flatten_set(fields).items():
                 if op == "$set":
-                    _set_path(doc, key, copy.deepcopy(value), cow)
+                    _set_path(doc, key, _copy_doc(value), cow)
                 elif op == "$inc":
                     cur = _get_path(doc, key)
                     _set_path(doc, key, (0 if cur is _MISSING or cur is None else cur) + value)
@@ -159,12 +179,12 @@ def apply_update(doc: dict, data: dict, cow: bool = False) -> None:
                 elif op == "$push":
                     cur = _get_path(doc, key)
                     _set_path(doc, key, ([] if cur is _MISSING or cur is None else list(cur))
-                              + [copy.deepcopy(value)])
+                              + [_copy_doc(value)])
                 else:
                     raise ValueError(f"Update operator '{op}' is not supported")
     else:
         for key, value in _flatten_set(data).items():
-            _set_path(doc, key, copy.deepcopy(value), cow)
+            _set_path(doc, key, _copy_doc(value), cow)
 
 
 def _flatten_set(fields: dict) -> dict:
@@ -178,7 +198,7 @@ def _flatten_set(fields: dict) -> dict:
 def project(doc: dict, selection: Optional[dict]) -> dict:
     """Mongo-style projection: all-1 (include) or all-0 (exclude); ``_id`` shown unless 0."""
     if not selection:
-        return copy.deepcopy(doc)
+        return _copy_doc(doc)
     sel = dict(selection)
     id_flag = sel.pop("_id", 1)
     if sel:
@@ -189,19 +209,19 @@ def project(doc: dict, selection: Optional[dict]) -> dict:
     else:
         include = bool(id_flag)
         if include:
-            return {"_id": copy.deepcopy(doc.get("_id"))} if "_id" in doc else {}
-        out = copy.deepcopy(doc)
+            return {"_id": _copy_doc(doc.get("_id"))} if "_id" in doc else {}
+        out = _copy_doc(doc)
         out.pop("_id", None)
         return out
     if include:
         out: Dict[str, Any] = {}
         for key in sel:
             val = _get_path(doc, key)
-            _set_path(out, key, None if val is _MISSING else copy.deepcopy(val))
+            _set_path(out, key, None if val is _MISSING else _copy_doc(val))
         if id_flag and "_id" in doc:
-            out["_id"] = copy.deepcopy(doc["_id"])
+            out["_id"] = _copy_doc(doc["_id"])
         return out
-    out = copy.deepcopy(doc)
+    out = _copy_doc(doc)
     for key in sel:
         parts = key.split(".")
         parent = _get_path(out, ".".join(parts[:-1])) if len(parts) > 1 else out
@@ -391,7 +411,7 @@ class _Collection:
                 self._next_id += 1
             doc["_id"] = self._next_id
             self._next_id += 1
-        stored = copy.deepcopy(doc)
+        stored = _copy_doc(doc)
         self._check_unique(stored)
         self.docs[_hashable(stored["_id"])] = stored
         self._register(stored)

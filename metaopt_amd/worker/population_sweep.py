@@ -65,7 +65,11 @@ class PopulationSweep:
         self.slot_key = np.full(P, -1, dtype=np.int64)
         self._n_active = 0
         self.slot_budget = np.zeros(P, dtype=np.int64)
+        # device checkpoints of finished members (ASHA promotion, PBT exploit): trial key ->
+        # metadata of a slot in the population's checkpoint pool, evicted FIFO
         self.ckpts: "collections.OrderedDict[int, dict]" = collections.OrderedDict()
+        pop.alloc_ckpt_pool(self.ckpt_capacity)
+        self._free_ck = list(range(self.ckpt_capacity - 1, -1, -1))
         self.global_step = 0
         self.samples = 0
         self.done = False
@@ -349,22 +353,34 @@ class PopulationSweep:
         max_b = None
         # every member that finished (or broke) at this sync leaves its slot -- whether the slot
         # is CLEARed or immediately re-assigned; the ones that completed below the top budget are
-        # checkpointed first (rank 0 mirrors the rule in _decide/_record_ckpt)
+        # checkpointed first, all in one batched copy (rank 0 mirrors the FIFO in _record_ckpt)
+        to_save, leaving = [], []
         for s in range(P):
             if self.slot_key[s] < 0:
                 continue
             if g[s, 6] > 0 or g[s, 1] >= g[s, 2]:
-                finished_ok = g[s, 6] == 0
+                leaving.append(s)
                 if max_b is None:
                     max_b = self._max_budget_local()
-                if finished_ok and self.slot_budget[s] < max_b:
-                    self.ckpts[int(self.slot_key[s])] = pop.slot_state(s)
-                    while len(self.ckpts) > self.ckpt_capacity:
-                        self.ckpts.popitem(last=False)
-                pop.remove_member(s)
-                self.slot_key[s] = -1
-                self.slot_budget[s] = 0
+                if g[s, 6] == 0 and self.slot_budget[s] < max_b:
+                    if len(self.ckpts) + len(to_save) >= self.ckpt_capacity:
+                        if self.ckpts:
+                            _, old = self.ckpts.popitem(last=False)
+                            self._free_ck.append(old["ck"])
+                        else:  # capacity smaller than one sync's worth: drop the oldest new one
+                            _, idx_old, _ = to_save.pop(0)
+                            self._free_ck.append(idx_old)
+                    to_save.append((s, self._free_ck.pop(), int(self.slot_key[s])))
+        if to_save:
+            metas = pop.save_states([(s, idx) for s, idx, _ in to_save])
+            for (_, _, key), meta in zip(to_save, metas):
+                self.ckpts[key] = meta
+        for s in leaving:
+            pop.remove_member(s)
+            self.slot_key[s] = -1
+            self.slot_budget[s] = 0
         received = self._exchange_checkpoints(assign)
+        loads, hp_updates = [], []
         for s in range(P):
             a = mine[s]
             act = int(a[0])
@@ -372,15 +388,14 @@ class PopulationSweep:
                 continue
             cfg = MemberConfig(width=int(a[2]), lr=float(a[3]), momentum=float(a[4]),
                                weight_decay=float(a[5]), dropout=float(a[6]), seed=int(a[7]))
-            st = None
-            if act == RESUME:
-                # checkpoints are not consumed: a PBT winner can seed several members
-                st = received.get(s) if s in received else self.ckpts.get(int(a[9]))
-            if st is not None:
-                pop.load_slot_state(s, st)
-                pop.update_hparams(s, lr=cfg.lr, momentum=cfg.momentum,
-                                   weight_decay=cfg.weight_decay, dropout=cfg.dropout)
-                self.n_resumed += 1
+            # checkpoints are not consumed: a PBT winner can seed several members
+            meta = self.ckpts.get(int(a[9])) if act == RESUME and s not in received else None
+            if act == RESUME and s in received:
+                pop.load_slot_state(s, received[s])
+                hp_updates.append((s, cfg))
+            elif meta is not None:
+                loads.append((s, meta))
+                hp_updates.append((s, cfg))
             else:
                 if act == RESUME:  # evicted checkpoint: the trial retrains from scratch
                     self.n_resume_missing += 1
@@ -389,6 +404,12 @@ class PopulationSweep:
                 pop.set_member(s, cfg, init=True)
             self.slot_key[s] = int(a[1])
             self.slot_budget[s] = int(a[8])
+        if loads:
+            pop.load_states(loads)
+        for s, cfg in hp_updates:
+            pop.update_hparams(s, lr=cfg.lr, momentum=cfg.momentum,
+                               weight_decay=cfg.weight_decay, dropout=cfg.dropout)
+            self.n_resumed += 1
         self.done = bool(assign[-1, 0])
         self._n_active = int((self.slot_key >= 0).sum())
 
@@ -407,10 +428,10 @@ class PopulationSweep:
             if src == dst or src < 0:
                 continue
             if me == src:
-                st = self.ckpts.get(int(a[9]))
-                if st is None:
+                meta = self.ckpts.get(int(a[9]))
+                if meta is None:
                     raise RuntimeError(f"rank {me} lost checkpoint of trial {int(a[9])}")
-                ops.append(("send", self.pop.pack_state(st), dst))
+                ops.append(("send", self.pop.pack_state(self.pop.pool_state(meta)), dst))
             elif me == dst:
                 buf = self.pop.empty_packed_state(int(a[2]))
                 recv[row % P] = buf

@@ -129,7 +129,7 @@ def _pbt_worker(rank, world, port, q):
     # C4 directly: rank 0 holds a checkpoint that rank 1 resumes in its slot 2
     sweep.start()
     st = pop.slot_state(0)
-    sweep.ckpts[999] = st
+    sweep.ckpts[999] = pop.save_states([(0, sweep._free_ck.pop())])[0]
     assign = np.zeros((2 * 3 + 1, AS_COLS))
     assign[3 + 2] = (RESUME, 0, 64, 0.1, 0.9, 0, 0, 7, 16, 999, 0)
     got = sweep._exchange_checkpoints(assign)
@@ -137,7 +137,7 @@ def _pbt_worker(rank, world, port, q):
     if rank == 1:
         c4 = (sorted(got), got[2]["t"], got[2]["p32"].shape[0])
     ref = (int(st["t"]), st["p32"].shape[0], float(st["p32"].sum())) if rank == 0 else None
-    del sweep.ckpts[999]
+    sweep._free_ck.append(sweep.ckpts.pop(999)["ck"])
     summary = sweep.run(400)
     sweep.close()
     parents = None

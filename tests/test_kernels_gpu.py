@@ -127,3 +127,32 @@ def test_copy_member_and_checkpoint(data):
     b = hip.slot_base(5)
     assert torch.equal(hip.p32[b:b + st["p32"].numel()].cpu(), st["p32"])
     assert hip.steps_done(5) == 3
+
+
+def test_multi_copy_and_checkpoint_pool(data):
+    from metaopt_amd.ops.ckpt import multi_copy
+    src = [torch.randn(n, device="cuda") for n in (4, 4100, 12288, 64)]
+    dst = [torch.empty_like(t) for t in src]
+    d16 = [torch.empty(t.numel(), dtype=torch.bfloat16, device="cuda") for t in src]
+    multi_copy([(s, d, h if i % 2 else None) for i, (s, d, h) in enumerate(zip(src, dst, d16))])
+    torch.cuda.synchronize()
+    for i, (s, d, h) in enumerate(zip(src, dst, d16)):
+        assert torch.equal(s, d)
+        if i % 2:
+            assert torch.equal(h, s.to(torch.bfloat16))
+    # pool save/restore == slot_state/load_slot_state, bitwise
+    hip, _ = _pair()
+    x, y = data.batch(0)
+    hip.train_step(x, y)
+    hip.alloc_ckpt_pool(4)
+    metas = hip.save_states([(1, 2), (3, 0)])
+    ref1 = hip.slot_state(1)
+    hip.train_step(x, y)                                      # move the weights on
+    hip.load_states([(4, metas[0])])                          # restore slot 1's state into 4
+    torch.cuda.synchronize()
+    b = hip.slot_base(4)
+    n = ref1["p32"].numel()
+    assert torch.equal(hip.p32[b:b + n], ref1["p32"])
+    assert torch.equal(hip.m32[b:b + n], ref1["m32"])
+    assert torch.equal(hip.p16[b:b + n], ref1["p32"].to(torch.bfloat16))
+    assert hip.steps_done(4) == ref1["t"] and hip.members[4].width == CONFIGS[0].width
