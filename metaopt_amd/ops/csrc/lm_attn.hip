@@ -1,0 +1,366 @@
+// Causal flash attention (forward + backward) for the population LM (north-star kernel K10).
+//
+// Layouts (head dim 64, bf16):
+//   Q, K, V, dQ, dK, dV   [BH][T][64]            BH = population * batch * heads
+//   O, dO                 [B'][T][H][64]        = the [rows, d_model] activation layout
+//   LSE2, Dsum            [BH][T] f32           log2-domain logsumexp / rowsum(dO * O)
+// T is a multiple of 64.  Softmax runs in the exp2 domain: s = (q.k) * scale * log2(e).
+//
+// Every MFMA is v_mfma_f32_16x16x32_bf16 with the fragment layout of common.h.  The trick that
+// keeps P (and dS) in registers between the two GEMMs of each step: scores are computed
+// TRANSPOSED (S^T = K Q^T, lane = one query) with the K rows fed to the MFMA in a permuted order,
+// so that the 4+4 accumulator registers a lane holds for key tiles 2s and 2s+1 are exactly the 8
+// consecutive keys 32s + 8g .. 32s + 8g + 7 that the B operand of the P.V MFMA wants in that lane.
+// The row-max / row-sum of the online softmax are then a 4-lane reduction (lanes l, l^16, l^32,
+// l^48), and the P.V product reads V through ds_read_b64_tr_b16 (no LDS transpose pass).
+//
+// Kernels: attn_fwd (one 64-query block per workgroup, 16 queries per wave), attn_bwd_dq (same
+// decomposition, loops over key blocks), attn_bwd_dkdv (one 64-key block per workgroup, 16 keys
+// per wave, loops over query blocks) and attn_bwd_prep (Dsum).  No atomics anywhere.
+#include "common.h"
+
+using namespace mopt;
+
+namespace {
+
+constexpr int D = 64;          // head dim
+constexpr int BQ = 64;         // queries per workgroup
+constexpr int BKV = 64;        // keys per block
+constexpr int LS = kLdsStride;
+
+// Load a [64][64] bf16 tile (rows contiguous, row stride 64) into LDS [64][LS].
+__device__ __forceinline__ void tile_to_lds(const bf16_t* __restrict__ g, bf16_t* s, int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
+    *(uint4*)(s + r * LS + ch * 8) = *(const uint4*)(g + r * D + ch * 8);
+  }
+}
+
+// Key row of the permuted K/V fragment: tile j = 2s + h, fragment row m.
+__device__ __forceinline__ int perm_row(int s, int h, int m) {
+  return 32 * s + 8 * (m >> 2) + 4 * h + (m & 3);
+}
+
+// V^T (or K^T) A-fragment for keys 32s + 8g .. +7, head-dim columns 16 dt .. +15, from LDS [key][dh].
+__device__ __forceinline__ bf16x8 tr_frag(const bf16_t* s, int ks, int g, int q, int pp, int dt) {
+  const s16x4 lo = lds_tr4(s + (32 * ks + 8 * g + q) * LS + 16 * dt + 4 * pp);
+  const s16x4 hi = lds_tr4(s + (32 * ks + 8 * g + 4 + q) * LS + 16 * dt + 4 * pp);
+  return cat_frag(lo, hi);
+}
+
+__device__ __forceinline__ bf16x8 pack_frag(const f32x4& a, const f32x4& b) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 w = {pack2bf(a[0], a[1]), pack2bf(a[2], a[3]), pack2bf(b[0], b[1]), pack2bf(b[2], b[3])};
+  return __builtin_bit_cast(bf16x8, w);
+}
+
+__device__ __forceinline__ float max4(float v) {
+  v = fmaxf(v, __shfl_xor(v, 16, 64));
+  return fmaxf(v, __shfl_xor(v, 32, 64));
+}
+__device__ __forceinline__ float sum4(float v) {
+  v += __shfl_xor(v, 16, 64);
+  return v + __shfl_xor(v, 32, 64);
+}
+
+// S^T tiles for one 64-key block: st[j][r] = s(query li, key 32s + 8g + 4h + r), j = 2s + h.
+__device__ __forceinline__ void scores_T(const bf16_t* Ks, const bf16x8 (&qf)[2], int li, int g,
+                                         f32x4 (&st)[4]) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int j = 2 * s + h, row = perm_row(s, h, li);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) acc = mfma16(lds_frag(Ks + row * LS + 32 * ks + 8 * g), qf[ks], acc);
+      st[j] = acc;
+    }
+}
+
+// Forward: O = softmax(QK^T * scale, causal) V.   grid (T/64, BH), 256 threads.
+__global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict__ Q,
+                                                       const bf16_t* __restrict__ K,
+                                                       const bf16_t* __restrict__ V,
+                                                       bf16_t* __restrict__ O,
+                                                       float* __restrict__ LSE2, int T, int H,
+                                                       float c) {
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[BKV * LS];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[BKV * LS];
+  const int nqb = gridDim.x;
+  const int qb = nqb - 1 - (int)blockIdx.x;          // longest (most key blocks) first
+  const int bh = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, g = lane >> 4, q = li >> 2, pp = li & 3;
+  const size_t base = (size_t)bh * T * D;
+  const int qrow = qb * BQ + wave * 16 + li;            // this lane's query
+
+  bf16x8 qf[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) qf[ks] = lds_frag(Q + base + (size_t)qrow * D + 32 * ks + 8 * g);
+
+  f32x4 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+
+  for (int kb = 0; kb <= qb; ++kb) {
+    __syncthreads();
+    tile_to_lds(K + base + (size_t)kb * BKV * D, Ks, tid);
+    tile_to_lds(V + base + (size_t)kb * BKV * D, Vs, tid);
+    __syncthreads();
+    f32x4 st[4];
+    scores_T(Ks, qf, li, g, st);
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = st[j][r] * c;
+        if (kb == qb) {
+          const int key = kb * BKV + 32 * (j >> 1) + 8 * g + 4 * (j & 1) + r;
+          if (key > qrow) v = -INFINITY;
+        }
+        st[j][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    const float m_new = fmaxf(m, max4(mx));
+    const float alpha = exp2f(m - m_new);
+    float ls = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = exp2f(st[j][r] - m_new);
+        st[j][r] = p;
+        ls += p;
+      }
+    l = l * alpha + sum4(ls);
+    m = m_new;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 pb = pack_frag(st[2 * s], st[2 * s + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) o[dt] = mfma16(tr_frag(Vs, s, g, q, pp, dt), pb, o[dt]);
+    }
+  }
+  // o[dt][r] = O^T[dh 16 dt + 4 g + r][query li]
+  const float inv = 1.f / l;
+  const int b = bh / H, hh = bh % H;
+  bf16_t* out = O + (((size_t)b * T + qrow) * H + hh) * D;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+    *(uint2*)(out + 16 * dt + 4 * g) =
+        make_uint2(pack2bf(o[dt][0] * inv, o[dt][1] * inv), pack2bf(o[dt][2] * inv, o[dt][3] * inv));
+  if (g == 0) LSE2[(size_t)bh * T + qrow] = m + log2f(l);
+}
+
+// Dsum[bh][t] = sum_d dO * O  (one thread per query row).
+__global__ __launch_bounds__(256) void attn_bwd_prep_kernel(const bf16_t* __restrict__ O,
+                                                            const bf16_t* __restrict__ dO,
+                                                            float* __restrict__ Dsum, int T, int H,
+                                                            int n_rows) {
+  const int i = blockIdx.x * 256 + threadIdx.x;     // i = bh * T + t
+  if (i >= n_rows) return;
+  const int bh = i / T, t = i % T, b = bh / H, hh = bh % H;
+  const size_t off = (((size_t)b * T + t) * H + hh) * D;
+  float acc = 0.f;
+#pragma unroll
+  for (int c8 = 0; c8 < D / 8; ++c8) {
+    const uint4 a = *(const uint4*)(O + off + 8 * c8);
+    const uint4 d = *(const uint4*)(dO + off + 8 * c8);
+    const uint32_t aw[4] = {a.x, a.y, a.z, a.w}, dw[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      acc += bf2f(aw[e] & 0xFFFF) * bf2f(dw[e] & 0xFFFF) + bf2f(aw[e] >> 16) * bf2f(dw[e] >> 16);
+  }
+  Dsum[i] = acc;
+}
+
+// dQ = scale * sum_k dS K, dS = P * (dP - Dsum), dP = dO V^T.   grid (T/64, BH).
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16_t* __restrict__ Q,
+                                                          const bf16_t* __restrict__ K,
+                                                          const bf16_t* __restrict__ V,
+                                                          const bf16_t* __restrict__ dO,
+                                                          const float* __restrict__ LSE2,
+                                                          const float* __restrict__ Dsum,
+                                                          bf16_t* __restrict__ dQ, int T, int H,
+                                                          float c, float scale) {
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[BKV * LS];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[BKV * LS];
+  const int nqb = gridDim.x;
+  const int qb = nqb - 1 - (int)blockIdx.x;
+  const int bh = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, g = lane >> 4, q = li >> 2, pp = li & 3;
+  const size_t base = (size_t)bh * T * D;
+  const int qrow = qb * BQ + wave * 16 + li;
+  const int b = bh / H, hh = bh % H;
+  const size_t orow = (((size_t)b * T + qrow) * H + hh) * D;
+
+  bf16x8 qf[2], df[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    qf[ks] = lds_frag(Q + base + (size_t)qrow * D + 32 * ks + 8 * g);
+    df[ks] = lds_frag(dO + orow + 32 * ks + 8 * g);
+  }
+  const float lse = LSE2[(size_t)bh * T + qrow], dsum = Dsum[(size_t)bh * T + qrow];
+  f32x4 acc[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) acc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int kb = 0; kb <= qb; ++kb) {
+    __syncthreads();
+    tile_to_lds(K + base + (size_t)kb * BKV * D, Ks, tid);
+    tile_to_lds(V + base + (size_t)kb * BKV * D, Vs, tid);
+    __syncthreads();
+    f32x4 st[4], dpt[4];
+    scores_T(Ks, qf, li, g, st);
+    scores_T(Vs, df, li, g, dpt);     // dP^T = V dO^T, same permuted key order
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float p = exp2f(st[j][r] * c - lse);
+        if (kb == qb) {
+          const int key = kb * BKV + 32 * (j >> 1) + 8 * g + 4 * (j & 1) + r;
+          if (key > qrow) p = 0.f;
+        }
+        st[j][r] = p * (dpt[j][r] - dsum);   // dS (without the scale)
+      }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 sb = pack_frag(st[2 * s], st[2 * s + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma16(tr_frag(Ks, s, g, q, pp, dt), sb, acc[dt]);
+    }
+  }
+  bf16_t* out = dQ + base + (size_t)qrow * D;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+    *(uint2*)(out + 16 * dt + 4 * g) = make_uint2(pack2bf(acc[dt][0] * scale, acc[dt][1] * scale),
+                                                  pack2bf(acc[dt][2] * scale, acc[dt][3] * scale));
+}
+
+// dV = sum_q P^T dO,  dK = scale * sum_q dS^T Q.   grid (T/64, BH); one 64-key block per WG.
+// Scores are computed un-transposed here (S = Q K^T, lane = one key) with the Q / dO rows fed in
+// the permuted order, so P^T and dS^T land in A-fragment order for the two accumulating MFMAs.
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q,
+                                                            const bf16_t* __restrict__ K,
+                                                            const bf16_t* __restrict__ V,
+                                                            const bf16_t* __restrict__ dO,
+                                                            const float* __restrict__ LSE2,
+                                                            const float* __restrict__ Dsum,
+                                                            bf16_t* __restrict__ dK,
+                                                            bf16_t* __restrict__ dV, int T, int H,
+                                                            float c, float scale) {
+  __shared__ __attribute__((aligned(16))) bf16_t Qs[BQ * LS];
+  __shared__ __attribute__((aligned(16))) bf16_t dOs[BQ * LS];
+  __shared__ float lse_s[BQ], dsum_s[BQ];
+  const int kb = (int)blockIdx.x;                 // blocks with more query blocks are early ids
+  const int bh = blockIdx.y;
+  const int nqb = T / BQ;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, g = lane >> 4, q = li >> 2, pp = li & 3;
+  const size_t base = (size_t)bh * T * D;
+  const int krow = kb * BKV + wave * 16 + li;    // this lane's key
+  const int b = bh / H, hh = bh % H;
+
+  bf16x8 kf[2], vf[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    kf[ks] = lds_frag(K + base + (size_t)krow * D + 32 * ks + 8 * g);
+    vf[ks] = lds_frag(V + base + (size_t)krow * D + 32 * ks + 8 * g);
+  }
+  f32x4 dk[4], dv[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) dk[dt] = dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int qb = kb; qb < nqb; ++qb) {
+    __syncthreads();
+    tile_to_lds(Q + base + (size_t)qb * BQ * D, Qs, tid);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {      // dO rows of this query block: [B'][T][H][64] layout
+      const int cc = tid + 256 * i, r = cc >> 3, ch = cc & 7;
+      *(uint4*)(dOs + r * LS + ch * 8) =
+          *(const uint4*)(dO + (((size_t)b * T + qb * BQ + r) * H + hh) * D + ch * 8);
+    }
+    if (tid < BQ) {
+      lse_s[tid] = LSE2[(size_t)bh * T + qb * BQ + tid];
+      dsum_s[tid] = Dsum[(size_t)bh * T + qb * BQ + tid];
+    }
+    __syncthreads();
+    // S and dP tiles j = 2s + h: rows = queries 32s + 8g + 4h + r (C layout), column = key li.
+    f32x4 st[4], dp[4];
+    scores_T(Qs, kf, li, g, st);
+    scores_T(dOs, vf, li, g, dp);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qi = 32 * (j >> 1) + 8 * g + 4 * (j & 1) + r;
+        float p = exp2f(st[j][r] * c - lse_s[qi]);
+        if (qb == kb && qb * BQ + qi < krow) p = 0.f;
+        st[j][r] = p;
+        dp[j][r] = p * (dp[j][r] - dsum_s[qi]);
+      }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 pa = pack_frag(st[2 * s], st[2 * s + 1]);
+      const bf16x8 sa = pack_frag(dp[2 * s], dp[2 * s + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        // dV^T[dh][key] += dO^T P^T : A = dO^T (tr-read), B = P^T fragment (this lane's key)
+        dv[dt] = mfma16(tr_frag(dOs, s, g, q, pp, dt), pa, dv[dt]);
+        dk[dt] = mfma16(tr_frag(Qs, s, g, q, pp, dt), sa, dk[dt]);
+      }
+    }
+  }
+  // dv[dt][r] = dV^T[dh 16 dt + 4 g + r][key li]
+  bf16_t* okp = dK + base + (size_t)krow * D;
+  bf16_t* ovp = dV + base + (size_t)krow * D;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    *(uint2*)(okp + 16 * dt + 4 * g) = make_uint2(pack2bf(dk[dt][0] * scale, dk[dt][1] * scale),
+                                                  pack2bf(dk[dt][2] * scale, dk[dt][3] * scale));
+    *(uint2*)(ovp + 16 * dt + 4 * g) =
+        make_uint2(pack2bf(dv[dt][0], dv[dt][1]), pack2bf(dv[dt][2], dv[dt][3]));
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int mopt_attn_fwd(const void* q, const void* k, const void* v, void* o, void* lse2, int bh, int T,
+                  int H, float scale, void* stream) {
+  if (T % 64 || bh <= 0) return 1;
+  const float c = scale * 1.4426950408889634f;
+  hipLaunchKernelGGL(attn_fwd_kernel, dim3(T / 64, bh), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o,
+                     (float*)lse2, T, H, c);
+  return (int)hipGetLastError();
+}
+
+int mopt_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                  const void* lse2, void* dsum, void* dq, void* dk, void* dv, int bh, int T, int H,
+                  float scale, void* stream) {
+  if (T % 64 || bh <= 0) return 1;
+  const float c = scale * 1.4426950408889634f;
+  const int rows = bh * T;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((rows + 255) / 256), dim3(256), 0, st,
+                     (const bf16_t*)o, (const bf16_t*)dout, (float*)dsum, T, H, rows);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3(T / 64, bh), dim3(256), 0, st, (const bf16_t*)q,
+                     (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, (const float*)lse2,
+                     (const float*)dsum, (bf16_t*)dk, (bf16_t*)dv, T, H, c, scale);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(T / 64, bh), dim3(256), 0, st, (const bf16_t*)q,
+                     (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, (const float*)lse2,
+                     (const float*)dsum, (bf16_t*)dq, T, H, c, scale);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

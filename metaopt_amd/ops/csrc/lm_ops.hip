@@ -1,0 +1,575 @@
+// Elementwise / normalisation / loss / optimizer kernels of the population LM (north-star
+// kernels K4, K6, K9).  Every tensor carries a leading population dimension: rows of trial p are
+// rows [p * rows_per_trial, (p + 1) * rows_per_trial) and per-trial parameters are indexed by p.
+//
+//   rmsnorm_fwd / rmsnorm_bwd_dx / rmsnorm_bwd_dw   y = x * rsqrt(mean(x^2) + eps) * w[p]
+//   rope_fwd / rope_bwd       split qkv [rows][3 H 64] into head-major Q/K/V [B'][H][T][64] with
+//                             rotate-half RoPE on q and k (and the inverse for the gradients)
+//   swiglu_fwd / swiglu_bwd   h = silu(gate) * up on a fused [rows][2F] projection
+//   ce_fwd_bwd                row softmax cross-entropy over the vocabulary, dlogits in place
+//   embed_fwd / embed_bwd     token gather / f32 atomic scatter-add into the per-trial table
+//   grad_sumsq / adamw_multi  per-trial global grad norm (clipping) and the fused AdamW update
+//                             over the flat parameter buffers, per-trial lr / betas / wd / step
+#include "common.h"
+
+using namespace mopt;
+
+extern "C" {
+
+struct LmHP {          // per-trial optimizer hyper-parameters, 32 bytes (mirrored in lm.py)
+  float lr, b1, b2, eps, wd, max_norm;
+  int32_t t, pad;
+};
+
+struct Segment {       // one parameter tensor of the flat buffers: [P][numel] at offset off
+  int64_t off;
+  int64_t numel;       // per trial, multiple of 8
+};
+
+struct SegChunk {      // <= 2048 elements of ONE trial inside a segment
+  int32_t seg, trial;
+  int64_t start;       // element offset inside the segment ([P * numel])
+};
+
+}  // extern "C"
+
+namespace {
+
+constexpr int kAdamChunk = 2048;
+
+__device__ __forceinline__ void unpack8(const uint4& u, float (&f)[8]) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    f[2 * e] = bf2f(w[e] & 0xFFFF);
+    f[2 * e + 1] = bf2f(w[e] >> 16);
+  }
+}
+
+__device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
+  return make_uint4(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]),
+                    pack2bf(f[6], f[7]));
+}
+
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  float s = 0.f;
+  for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += red[w];
+  return s;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---------------------------------------------------------------------------------- RMSNorm
+constexpr int kMaxChunks = 4;  // d <= 64 lanes * 8 * 4 = 2048
+
+// One wave per row, 4 rows per workgroup.
+__global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const bf16_t* __restrict__ x,
+                                                          const bf16_t* __restrict__ w,
+                                                          bf16_t* __restrict__ y,
+                                                          float* __restrict__ rstd, int rows,
+                                                          int d, int rows_per_trial, float eps) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int p = row / rows_per_trial, nc = d >> 3;
+  const bf16_t* xr = x + (size_t)row * d;
+  float v[kMaxChunks][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < kMaxChunks; ++k) {
+    const int c = lane + 64 * k;
+    if (c < nc) {
+      unpack8(*(const uint4*)(xr + 8 * c), v[k]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ss += v[k][e] * v[k][e];
+    }
+  }
+  const float r = rsqrtf(wave_sum(ss) / d + eps);
+  const bf16_t* wr = w + (size_t)p * d;
+#pragma unroll
+  for (int k = 0; k < kMaxChunks; ++k) {
+    const int c = lane + 64 * k;
+    if (c < nc) {
+      float wv[8], o[8];
+      unpack8(*(const uint4*)(wr + 8 * c), wv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = v[k][e] * r * wv[e];
+      *(uint4*)(y + (size_t)row * d + 8 * c) = pack8(o);
+    }
+  }
+  if (lane == 0) rstd[row] = r;
+}
+
+// dx = r * (g - xhat * mean(g * xhat)),  g = dy * w,  xhat = x * r.
+__global__ __launch_bounds__(256) void rmsnorm_bwd_dx_kernel(const bf16_t* __restrict__ x,
+                                                             const bf16_t* __restrict__ w,
+                                                             const bf16_t* __restrict__ dy,
+                                                             const float* __restrict__ rstd,
+                                                             bf16_t* __restrict__ dx, int rows,
+                                                             int d, int rows_per_trial) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int p = row / rows_per_trial, nc = d >> 3;
+  const float r = rstd[row];
+  float xh[kMaxChunks][8], gv[kMaxChunks][8];
+  float dot = 0.f;
+#pragma unroll
+  for (int k = 0; k < kMaxChunks; ++k) {
+    const int c = lane + 64 * k;
+    if (c < nc) {
+      float wv[8], dv[8];
+      unpack8(*(const uint4*)(x + (size_t)row * d + 8 * c), xh[k]);
+      unpack8(*(const uint4*)(w + (size_t)p * d + 8 * c), wv);
+      unpack8(*(const uint4*)(dy + (size_t)row * d + 8 * c), dv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        xh[k][e] *= r;
+        gv[k][e] = dv[e] * wv[e];
+        dot += gv[k][e] * xh[k][e];
+      }
+    }
+  }
+  const float mdot = wave_sum(dot) / d;
+#pragma unroll
+  for (int k = 0; k < kMaxChunks; ++k) {
+    const int c = lane + 64 * k;
+    if (c < nc) {
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = r * (gv[k][e] - xh[k][e] * mdot);
+      *(uint4*)(dx + (size_t)row * d + 8 * c) = pack8(o);
+    }
+  }
+}
+
+// dw[p][col] += sum over a slice of trial p's rows of dy * x * rstd.  grid (d/256, splits, P).
+__global__ __launch_bounds__(256) void rmsnorm_bwd_dw_kernel(const bf16_t* __restrict__ x,
+                                                             const bf16_t* __restrict__ dy,
+                                                             const float* __restrict__ rstd,
+                                                             float* __restrict__ dw32, int d,
+                                                             int rows_per_trial) {
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= d) return;
+  const int p = blockIdx.z, splits = gridDim.y;
+  const int per = (rows_per_trial + splits - 1) / splits;
+  const int r0 = p * rows_per_trial + blockIdx.y * per;
+  const int r1 = min(r0 + per, (p + 1) * rows_per_trial);
+  float acc = 0.f;
+  for (int r = r0; r < r1; ++r)
+    acc += bf2f(dy[(size_t)r * d + col]) * bf2f(x[(size_t)r * d + col]) * rstd[r];
+  atomicAdd(dw32 + (size_t)p * d + col, acc);
+}
+
+// ---------------------------------------------------------------------------------- RoPE
+// qkv [B' * T][3][H][64] -> Q/K/V [B'][H][T][64]; thread = (row, part, head, 8-pair chunk).
+__global__ __launch_bounds__(256) void rope_fwd_kernel(const bf16_t* __restrict__ qkv,
+                                                       const float* __restrict__ cosv,
+                                                       const float* __restrict__ sinv,
+                                                       bf16_t* __restrict__ Q,
+                                                       bf16_t* __restrict__ K,
+                                                       bf16_t* __restrict__ V, int rows, int T,
+                                                       int H) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = (int64_t)rows * 3 * H * 4;
+  if (i >= total) return;
+  const int chunk = i & 3;
+  const int64_t rest = i >> 2;
+  const int hh = rest % H, part = (rest / H) % 3;
+  const int64_t row = rest / (3 * H);
+  const int t = row % T;
+  const int64_t b = row / T;
+  const bf16_t* src = qkv + ((row * 3 + part) * H + hh) * 64 + 8 * chunk;
+  bf16_t* dst = (part == 0 ? Q : part == 1 ? K : V) + ((b * H + hh) * T + t) * 64 + 8 * chunk;
+  const uint4 a = *(const uint4*)src, bb = *(const uint4*)(src + 32);
+  if (part == 2) {
+    *(uint4*)dst = a;
+    *(uint4*)(dst + 32) = bb;
+    return;
+  }
+  float x1[8], x2[8], o1[8], o2[8];
+  unpack8(a, x1);
+  unpack8(bb, x2);
+  const float* cs = cosv + (size_t)t * 32 + 8 * chunk;
+  const float* sn = sinv + (size_t)t * 32 + 8 * chunk;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    o1[e] = x1[e] * cs[e] - x2[e] * sn[e];
+    o2[e] = x2[e] * cs[e] + x1[e] * sn[e];
+  }
+  *(uint4*)dst = pack8(o1);
+  *(uint4*)(dst + 32) = pack8(o2);
+}
+
+__global__ __launch_bounds__(256) void rope_bwd_kernel(const bf16_t* __restrict__ dQ,
+                                                       const bf16_t* __restrict__ dK,
+                                                       const bf16_t* __restrict__ dV,
+                                                       const float* __restrict__ cosv,
+                                                       const float* __restrict__ sinv,
+                                                       bf16_t* __restrict__ dqkv, int rows, int T,
+                                                       int H) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = (int64_t)rows * 3 * H * 4;
+  if (i >= total) return;
+  const int chunk = i & 3;
+  const int64_t rest = i >> 2;
+  const int hh = rest % H, part = (rest / H) % 3;
+  const int64_t row = rest / (3 * H);
+  const int t = row % T;
+  const int64_t b = row / T;
+  const bf16_t* src = (part == 0 ? dQ : part == 1 ? dK : dV) + ((b * H + hh) * T + t) * 64 + 8 * chunk;
+  bf16_t* dst = dqkv + ((row * 3 + part) * H + hh) * 64 + 8 * chunk;
+  const uint4 a = *(const uint4*)src, bb = *(const uint4*)(src + 32);
+  if (part == 2) {
+    *(uint4*)dst = a;
+    *(uint4*)(dst + 32) = bb;
+    return;
+  }
+  float y1[8], y2[8], o1[8], o2[8];
+  unpack8(a, y1);
+  unpack8(bb, y2);
+  const float* cs = cosv + (size_t)t * 32 + 8 * chunk;
+  const float* sn = sinv + (size_t)t * 32 + 8 * chunk;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    o1[e] = y1[e] * cs[e] + y2[e] * sn[e];
+    o2[e] = y2[e] * cs[e] - y1[e] * sn[e];
+  }
+  *(uint4*)dst = pack8(o1);
+  *(uint4*)(dst + 32) = pack8(o2);
+}
+
+// ---------------------------------------------------------------------------------- SwiGLU
+__global__ __launch_bounds__(256) void swiglu_fwd_kernel(const bf16_t* __restrict__ gu,
+                                                         bf16_t* __restrict__ h, int64_t rows,
+                                                         int F) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;   // 8-element chunk of h
+  const int64_t nch = rows * (F >> 3);
+  if (i >= nch) return;
+  const int64_t r = i / (F >> 3);
+  const int c = (int)(i % (F >> 3)) * 8;
+  float gv[8], uv[8], o[8];
+  unpack8(*(const uint4*)(gu + r * 2 * F + c), gv);
+  unpack8(*(const uint4*)(gu + r * 2 * F + F + c), uv);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = gv[e] / (1.f + __expf(-gv[e])) * uv[e];
+  *(uint4*)(h + r * F + c) = pack8(o);
+}
+
+__global__ __launch_bounds__(256) void swiglu_bwd_kernel(const bf16_t* __restrict__ gu,
+                                                         const bf16_t* __restrict__ dh,
+                                                         bf16_t* __restrict__ dgu, int64_t rows,
+                                                         int F) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t nch = rows * (F >> 3);
+  if (i >= nch) return;
+  const int64_t r = i / (F >> 3);
+  const int c = (int)(i % (F >> 3)) * 8;
+  float gv[8], uv[8], dv[8], dg[8], du[8];
+  unpack8(*(const uint4*)(gu + r * 2 * F + c), gv);
+  unpack8(*(const uint4*)(gu + r * 2 * F + F + c), uv);
+  unpack8(*(const uint4*)(dh + r * F + c), dv);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float sg = 1.f / (1.f + __expf(-gv[e]));
+    const float silu = gv[e] * sg;
+    du[e] = dv[e] * silu;
+    dg[e] = dv[e] * uv[e] * sg * (1.f + gv[e] * (1.f - sg));
+  }
+  *(uint4*)(dgu + r * 2 * F + c) = pack8(dg);
+  *(uint4*)(dgu + r * 2 * F + F + c) = pack8(du);
+}
+
+// ---------------------------------------------------------------------------------- loss
+// One workgroup per row: loss_sum[p] += logsumexp(z) - z[y];  z <- (softmax(z) - onehot) * scale.
+__global__ __launch_bounds__(256) void ce_fwd_bwd_kernel(bf16_t* __restrict__ logits,
+                                                         const int32_t* __restrict__ labels,
+                                                         float* __restrict__ loss_sum, int V,
+                                                         int rows_per_trial, float scale,
+                                                         int write_grad) {
+  __shared__ float red[8];
+  const int64_t row = blockIdx.x;
+  bf16_t* z = logits + row * V;
+  const int nc = V >> 3;
+  float m = -INFINITY, s = 0.f;
+  for (int c = threadIdx.x; c < nc; c += 256) {
+    float v[8];
+    unpack8(*(const uint4*)(z + 8 * c), v);
+    float mx = v[0];
+#pragma unroll
+    for (int e = 1; e < 8; ++e) mx = fmaxf(mx, v[e]);
+    const float mn = fmaxf(m, mx);
+    float acc = s * __expf(m - mn);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc += __expf(v[e] - mn);
+    m = mn;
+    s = acc;
+  }
+  // combine (m, s) over the block
+  const float wm = wave_max(m);
+  float ws = s * __expf(m - wm);
+  ws = wave_sum(ws);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) {
+    red[wave] = wm;
+    red[4 + wave] = ws;
+  }
+  __syncthreads();
+  float M = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  float S = 0.f;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) S += red[4 + w] * __expf(red[w] - M);
+  const int y = labels[row];
+  if (threadIdx.x == 0) {
+    const float zy = bf2f(z[y]);
+    atomicAdd(loss_sum + row / rows_per_trial, M + __logf(S) - zy);
+  }
+  if (!write_grad) return;
+  __syncthreads();   // z[y] read above before it is overwritten
+  const float inv = 1.f / S;
+  for (int c = threadIdx.x; c < nc; c += 256) {
+    float v[8];
+    unpack8(*(const uint4*)(z + 8 * c), v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float p = __expf(v[e] - M) * inv - ((8 * c + e) == y ? 1.f : 0.f);
+      v[e] = p * scale;
+    }
+    *(uint4*)(z + 8 * c) = pack8(v);
+  }
+}
+
+// ---------------------------------------------------------------------------------- embedding
+__global__ __launch_bounds__(256) void embed_fwd_kernel(const int32_t* __restrict__ tok,
+                                                        const bf16_t* __restrict__ table,
+                                                        bf16_t* __restrict__ out, int64_t rows,
+                                                        int d, int V, int rows_per_trial) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int per = d >> 3;
+  if (i >= rows * per) return;
+  const int64_t r = i / per;
+  const int c = (int)(i % per) * 8;
+  const int64_t p = r / rows_per_trial;
+  *(uint4*)(out + r * d + c) = *(const uint4*)(table + (p * V + tok[r]) * (int64_t)d + c);
+}
+
+__global__ __launch_bounds__(256) void embed_bwd_kernel(const int32_t* __restrict__ tok,
+                                                        const bf16_t* __restrict__ dout,
+                                                        float* __restrict__ dtable32,
+                                                        int64_t rows, int d, int V,
+                                                        int rows_per_trial) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int per = d >> 3;
+  if (i >= rows * per) return;
+  const int64_t r = i / per;
+  const int c = (int)(i % per) * 8;
+  const int64_t p = r / rows_per_trial;
+  float v[8];
+  unpack8(*(const uint4*)(dout + r * d + c), v);
+  float* dst = dtable32 + (p * V + tok[r]) * (int64_t)d + c;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) atomicAdd(dst + e, v[e]);
+}
+
+// f32 -> bf16 (n multiple of 8).
+__global__ __launch_bounds__(256) void cast_bf16_kernel(const float* __restrict__ src,
+                                                        bf16_t* __restrict__ dst, int64_t n) {
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (i >= n) return;
+  const f32x4 a = *(const f32x4*)(src + i), b = *(const f32x4*)(src + i + 4);
+  const float f[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  *(uint4*)(dst + i) = pack8(f);
+}
+
+// ---------------------------------------------------------------------------------- AdamW
+__global__ __launch_bounds__(256) void grad_sumsq_kernel(const Segment* __restrict__ segs,
+                                                         const SegChunk* __restrict__ chunks,
+                                                         const bf16_t* __restrict__ g16,
+                                                         float* __restrict__ sumsq) {
+  __shared__ float red[4];
+  const SegChunk ch = chunks[blockIdx.x];
+  const Segment sg = segs[ch.seg];
+  const int64_t i = ch.start + 8 * threadIdx.x;
+  const int64_t end = min(ch.start + (int64_t)kAdamChunk, (int64_t)(ch.trial + 1) * sg.numel);
+  float acc = 0.f;
+  if (i < end) {
+    float v[8];
+    unpack8(*(const uint4*)(g16 + sg.off + i), v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc += v[e] * v[e];
+  }
+  const float tot = block_sum(acc, red);
+  if (threadIdx.x == 0) atomicAdd(sumsq + ch.trial, tot);
+}
+
+__global__ __launch_bounds__(256) void adamw_multi_kernel(const Segment* __restrict__ segs,
+                                                          const SegChunk* __restrict__ chunks,
+                                                          const LmHP* __restrict__ hp,
+                                                          const float* __restrict__ sumsq,
+                                                          float* __restrict__ p32,
+                                                          bf16_t* __restrict__ p16,
+                                                          const bf16_t* __restrict__ g16,
+                                                          float* __restrict__ m32,
+                                                          float* __restrict__ v32) {
+  const SegChunk ch = chunks[blockIdx.x];
+  const Segment sg = segs[ch.seg];
+  const int64_t i = ch.start + 8 * threadIdx.x;
+  const int64_t end = min(ch.start + (int64_t)kAdamChunk, (int64_t)(ch.trial + 1) * sg.numel);
+  if (i >= end) return;
+  const int p = ch.trial;
+  const LmHP h = hp[p];
+  float clip = 1.f;
+  if (h.max_norm > 0.f) {
+    const float nrm = sqrtf(sumsq[p]);
+    if (nrm > h.max_norm) clip = h.max_norm / (nrm + 1e-6f);
+  }
+  const float tf = (float)h.t;
+  const float bc1 = 1.f - __powf(h.b1, tf), bc2 = 1.f - __powf(h.b2, tf);
+  const float step = h.lr / bc1, rbc2 = rsqrtf(bc2);
+  const int64_t o = sg.off + i;
+  float gv[8];
+  unpack8(*(const uint4*)(g16 + o), gv);
+  const f32x4 w0 = *(const f32x4*)(p32 + o), w1 = *(const f32x4*)(p32 + o + 4);
+  const f32x4 m0 = *(const f32x4*)(m32 + o), m1 = *(const f32x4*)(m32 + o + 4);
+  const f32x4 v0 = *(const f32x4*)(v32 + o), v1 = *(const f32x4*)(v32 + o + 4);
+  float we[8] = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
+  float me[8] = {m0[0], m0[1], m0[2], m0[3], m1[0], m1[1], m1[2], m1[3]};
+  float ve[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float gr = gv[e] * clip;
+    we[e] *= 1.f - h.lr * h.wd;
+    me[e] = h.b1 * me[e] + (1.f - h.b1) * gr;
+    ve[e] = h.b2 * ve[e] + (1.f - h.b2) * gr * gr;
+    we[e] -= step * me[e] / (sqrtf(ve[e]) * rbc2 + h.eps);
+  }
+  *(f32x4*)(p32 + o) = f32x4{we[0], we[1], we[2], we[3]};
+  *(f32x4*)(p32 + o + 4) = f32x4{we[4], we[5], we[6], we[7]};
+  *(f32x4*)(m32 + o) = f32x4{me[0], me[1], me[2], me[3]};
+  *(f32x4*)(m32 + o + 4) = f32x4{me[4], me[5], me[6], me[7]};
+  *(f32x4*)(v32 + o) = f32x4{ve[0], ve[1], ve[2], ve[3]};
+  *(f32x4*)(v32 + o + 4) = f32x4{ve[4], ve[5], ve[6], ve[7]};
+  *(uint4*)(p16 + o) = pack8(we);
+}
+
+inline dim3 grid1(int64_t n) { return dim3((unsigned)((n + 255) / 256)); }
+
+}  // namespace
+
+extern "C" {
+
+int mopt_rmsnorm_fwd(const void* x, const void* w, void* y, void* rstd, int rows, int d,
+                     int rows_per_trial, float eps, void* stream) {
+  if (d % 8 || d > 64 * 8 * kMaxChunks) return 1;
+  hipLaunchKernelGGL(rmsnorm_fwd_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)rstd, rows, d,
+                     rows_per_trial, eps);
+  return (int)hipGetLastError();
+}
+
+int mopt_rmsnorm_bwd(const void* x, const void* w, const void* dy, const void* rstd, void* dx,
+                     void* dw32, int rows, int d, int rows_per_trial, void* stream) {
+  if (d % 8 || d > 64 * 8 * kMaxChunks) return 1;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(rmsnorm_bwd_dx_kernel, dim3((rows + 3) / 4), dim3(256), 0, st,
+                     (const bf16_t*)x, (const bf16_t*)w, (const bf16_t*)dy, (const float*)rstd,
+                     (bf16_t*)dx, rows, d, rows_per_trial);
+  const int P = rows / rows_per_trial;
+  const int splits = max(1, min(64, rows_per_trial / 64));
+  hipLaunchKernelGGL(rmsnorm_bwd_dw_kernel, dim3((d + 255) / 256, splits, P), dim3(256), 0, st,
+                     (const bf16_t*)x, (const bf16_t*)dy, (const float*)rstd, (float*)dw32, d,
+                     rows_per_trial);
+  return (int)hipGetLastError();
+}
+
+int mopt_rope_fwd(const void* qkv, const void* cosv, const void* sinv, void* q, void* k, void* v,
+                  int rows, int T, int H, void* stream) {
+  const int64_t total = (int64_t)rows * 3 * H * 4;
+  hipLaunchKernelGGL(rope_fwd_kernel, grid1(total), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)qkv, (const float*)cosv, (const float*)sinv, (bf16_t*)q,
+                     (bf16_t*)k, (bf16_t*)v, rows, T, H);
+  return (int)hipGetLastError();
+}
+
+int mopt_rope_bwd(const void* dq, const void* dk, const void* dv, const void* cosv,
+                  const void* sinv, void* dqkv, int rows, int T, int H, void* stream) {
+  const int64_t total = (int64_t)rows * 3 * H * 4;
+  hipLaunchKernelGGL(rope_bwd_kernel, grid1(total), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)dq, (const bf16_t*)dk, (const bf16_t*)dv, (const float*)cosv,
+                     (const float*)sinv, (bf16_t*)dqkv, rows, T, H);
+  return (int)hipGetLastError();
+}
+
+int mopt_swiglu_fwd(const void* gu, void* h, int64_t rows, int F, void* stream) {
+  if (F % 8) return 1;
+  hipLaunchKernelGGL(swiglu_fwd_kernel, grid1(rows * (F / 8)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)gu, (bf16_t*)h, rows, F);
+  return (int)hipGetLastError();
+}
+
+int mopt_swiglu_bwd(const void* gu, const void* dh, void* dgu, int64_t rows, int F, void* stream) {
+  if (F % 8) return 1;
+  hipLaunchKernelGGL(swiglu_bwd_kernel, grid1(rows * (F / 8)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)gu, (const bf16_t*)dh, (bf16_t*)dgu, rows, F);
+  return (int)hipGetLastError();
+}
+
+int mopt_ce_fwd_bwd(void* logits, const void* labels, void* loss_sum, int rows, int V,
+                    int rows_per_trial, float scale, int write_grad, void* stream) {
+  if (V % 8) return 1;
+  hipLaunchKernelGGL(ce_fwd_bwd_kernel, dim3(rows), dim3(256), 0, (hipStream_t)stream,
+                     (bf16_t*)logits, (const int32_t*)labels, (float*)loss_sum, V, rows_per_trial,
+                     scale, write_grad);
+  return (int)hipGetLastError();
+}
+
+int mopt_embed_fwd(const void* tok, const void* table, void* out, int64_t rows, int d, int V,
+                   int rows_per_trial, void* stream) {
+  if (d % 8) return 1;
+  hipLaunchKernelGGL(embed_fwd_kernel, grid1(rows * (d / 8)), dim3(256), 0, (hipStream_t)stream,
+                     (const int32_t*)tok, (const bf16_t*)table, (bf16_t*)out, rows, d, V,
+                     rows_per_trial);
+  return (int)hipGetLastError();
+}
+
+int mopt_embed_bwd(const void* tok, const void* dout, void* dtable32, int64_t rows, int d, int V,
+                   int rows_per_trial, void* stream) {
+  if (d % 8) return 1;
+  hipLaunchKernelGGL(embed_bwd_kernel, grid1(rows * (d / 8)), dim3(256), 0, (hipStream_t)stream,
+                     (const int32_t*)tok, (const bf16_t*)dout, (float*)dtable32, rows, d, V,
+                     rows_per_trial);
+  return (int)hipGetLastError();
+}
+
+int mopt_cast_bf16(const void* src, void* dst, int64_t n, void* stream) {
+  if (n % 8) return 1;
+  hipLaunchKernelGGL(cast_bf16_kernel, grid1(n / 8), dim3(256), 0, (hipStream_t)stream,
+                     (const float*)src, (bf16_t*)dst, n);
+  return (int)hipGetLastError();
+}
+
+int mopt_adamw_multi(const void* segs, const void* chunks, int n_chunks, const void* hp,
+                     void* sumsq, void* p32, void* p16, const void* g16, void* m32, void* v32,
+                     int P, int clip, void* stream) {
+  if (n_chunks <= 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (clip) {
+    (void)hipMemsetAsync(sumsq, 0, sizeof(float) * P, st);
+    hipLaunchKernelGGL(grad_sumsq_kernel, dim3(n_chunks), dim3(256), 0, st,
+                       (const Segment*)segs, (const SegChunk*)chunks, (const bf16_t*)g16,
+                       (float*)sumsq);
+  }
+  hipLaunchKernelGGL(adamw_multi_kernel, dim3(n_chunks), dim3(256), 0, st, (const Segment*)segs,
+                     (const SegChunk*)chunks, (const LmHP*)hp, (const float*)sumsq, (float*)p32,
+                     (bf16_t*)p16, (const bf16_t*)g16, (float*)m32, (float*)v32);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -1,0 +1,396 @@
+"""Population-LM operators: HIP kernels (gfx950) behind autograd Functions, plus fp32 PyTorch
+references of the same math (the CPU backend and the numerics oracle of tests/test_lm_gpu.py).
+
+Every op carries a leading population dimension.  Row layout: activations are ``[R, d]`` with
+``R = P * B * T`` rows ordered (trial, sequence, position); per-trial parameters are ``[P, ...]``.
+Attention uses head-major ``[P * B, H, T, 64]`` for Q/K/V and the row layout for its output.
+
+On a GPU the HIP path is the only path: a missing kernel library raises
+(:class:`~metaopt_amd.ops._lib.KernelLibraryError`) instead of falling back to PyTorch.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from typing import List, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+
+c_void_p, c_int, c_float, c_int64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_int64
+
+_lib.register_signatures({
+    "mopt_attn_fwd": ([c_void_p] * 5 + [c_int, c_int, c_int, c_float, c_void_p], c_int),
+    "mopt_attn_bwd": ([c_void_p] * 10 + [c_int, c_int, c_int, c_float, c_void_p], c_int),
+    "mopt_rmsnorm_fwd": ([c_void_p] * 4 + [c_int, c_int, c_int, c_float, c_void_p], c_int),
+    "mopt_rmsnorm_bwd": ([c_void_p] * 6 + [c_int, c_int, c_int, c_void_p], c_int),
+    "mopt_rope_fwd": ([c_void_p] * 6 + [c_int, c_int, c_int, c_void_p], c_int),
+    "mopt_rope_bwd": ([c_void_p] * 6 + [c_int, c_int, c_int, c_void_p], c_int),
+    "mopt_swiglu_fwd": ([c_void_p, c_void_p, c_int64, c_int, c_void_p], c_int),
+    "mopt_swiglu_bwd": ([c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p], c_int),
+    "mopt_ce_fwd_bwd": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_int,
+                         c_void_p], c_int),
+    "mopt_embed_fwd": ([c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_void_p],
+                       c_int),
+    "mopt_embed_bwd": ([c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_void_p],
+                       c_int),
+    "mopt_cast_bf16": ([c_void_p, c_void_p, c_int64, c_void_p], c_int),
+    "mopt_adamw_multi": ([c_void_p, c_void_p, c_int] + [c_void_p] * 7 + [c_int, c_int, c_void_p],
+                         c_int),
+})
+
+LM_HP_DTYPE = np.dtype([("lr", "<f4"), ("b1", "<f4"), ("b2", "<f4"), ("eps", "<f4"),
+                        ("wd", "<f4"), ("max_norm", "<f4"), ("t", "<i4"), ("pad", "<i4")])
+SEG_DTYPE = np.dtype([("off", "<i8"), ("numel", "<i8")])
+SEGCHUNK_DTYPE = np.dtype([("seg", "<i4"), ("trial", "<i4"), ("start", "<i8")])
+ADAM_CHUNK = 2048
+
+
+def _hip(t: torch.Tensor) -> bool:
+    return t.device.type == "cuda"
+
+
+def _call(name, *args):
+    lib = _lib.get_lib()
+    _lib.check(getattr(lib, name)(*args), name)
+
+
+def _stream(t):
+    return _lib.stream_ptr(t.device)
+
+
+def _p(t):
+    return t.data_ptr()
+
+
+# ============================================================================ references (fp32)
+def rmsnorm_ref(x, w, rows_per_trial, eps=1e-5):
+    xf = x.float()
+    r = torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
+    wf = w.float().repeat_interleave(rows_per_trial, 0)
+    return (xf * r * wf).to(x.dtype)
+
+
+def rope_tables(T: int, base: float = 10000.0, device=None):
+    inv = base ** (-torch.arange(0, 32, dtype=torch.float64) / 32.0)
+    ang = torch.arange(T, dtype=torch.float64)[:, None] * inv[None, :]
+    return (torch.cos(ang).float().contiguous().to(device),
+            torch.sin(ang).float().contiguous().to(device))
+
+
+def rope_split_ref(qkv, cos, sin, T, H):
+    R = qkv.shape[0]
+    Bp = R // T
+    x = qkv.float().view(Bp, T, 3, H, 64).permute(2, 0, 3, 1, 4)  # [3, B', H, T, 64]
+    q, k, v = x[0], x[1], x[2]
+
+    def rot(t):
+        t1, t2 = t[..., :32], t[..., 32:]
+        c, s = cos[None, None], sin[None, None]
+        return torch.cat([t1 * c - t2 * s, t2 * c + t1 * s], -1)
+    return (rot(q).to(qkv.dtype).contiguous(), rot(k).to(qkv.dtype).contiguous(),
+            v.to(qkv.dtype).contiguous())
+
+
+def attention_ref(q, k, v, scale):
+    """Causal softmax attention in fp32; returns [B', T, H, 64] flattened to rows."""
+    Bp, H, T, Dh = q.shape
+    s = torch.einsum("bhqd,bhkd->bhqk", q.float(), k.float()) * scale
+    mask = torch.ones(T, T, dtype=torch.bool, device=q.device).triu(1)
+    s = s.masked_fill(mask, float("-inf"))
+    o = torch.einsum("bhqk,bhkd->bhqd", s.softmax(-1), v.float())
+    return o.permute(0, 2, 1, 3).reshape(Bp * T, H * Dh).to(q.dtype)
+
+
+def swiglu_ref(gu):
+    F = gu.shape[-1] // 2
+    g, u = gu.float()[..., :F], gu.float()[..., F:]
+    return (torch.nn.functional.silu(g) * u).to(gu.dtype)
+
+
+def ce_ref(logits, labels, rows_per_trial):
+    """Per-trial SUM of token losses, fp32."""
+    lz = torch.nn.functional.cross_entropy(logits.float(), labels.long(), reduction="none")
+    return lz.view(-1, rows_per_trial).sum(1)
+
+
+def embed_ref(tok, table, rows_per_trial):
+    P, V, d = table.shape
+    p = torch.arange(tok.numel(), device=tok.device) // rows_per_trial
+    return table[p, tok.long()]
+
+
+# ============================================================================ autograd Functions
+class _RMSNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, rows_per_trial, eps):
+        R, d = x.shape
+        y = torch.empty_like(x)
+        rstd = torch.empty(R, dtype=torch.float32, device=x.device)
+        _call("mopt_rmsnorm_fwd", _p(x), _p(w), _p(y), _p(rstd), R, d, rows_per_trial, eps,
+              _stream(x))
+        ctx.save_for_backward(x, w, rstd)
+        ctx.rpt = rows_per_trial
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, rstd = ctx.saved_tensors
+        dy = dy.contiguous()
+        R, d = x.shape
+        dx = torch.empty_like(x)
+        dw32 = torch.zeros(w.shape, dtype=torch.float32, device=x.device)
+        _call("mopt_rmsnorm_bwd", _p(x), _p(w), _p(dy), _p(rstd), _p(dx), _p(dw32), R, d,
+              ctx.rpt, _stream(x))
+        return dx, dw32.to(w.dtype), None, None
+
+
+def rmsnorm(x, w, rows_per_trial, eps=1e-5):
+    if _hip(x):
+        return _RMSNorm.apply(x.contiguous(), w.contiguous(), rows_per_trial, eps)
+    return rmsnorm_ref(x, w, rows_per_trial, eps)
+
+
+class _RopeSplit(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, T, H):
+        R = qkv.shape[0]
+        Bp = R // T
+        shape = (Bp, H, T, 64)
+        q = torch.empty(shape, dtype=qkv.dtype, device=qkv.device)
+        k, v = torch.empty_like(q), torch.empty_like(q)
+        _call("mopt_rope_fwd", _p(qkv), _p(cos), _p(sin), _p(q), _p(k), _p(v), R, T, H,
+              _stream(qkv))
+        ctx.save_for_backward(cos, sin)
+        ctx.dims = (R, T, H, qkv.shape)
+        return q, k, v
+
+    @staticmethod
+    def backward(ctx, dq, dk, dv):
+        cos, sin = ctx.saved_tensors
+        R, T, H, shape = ctx.dims
+        dqkv = torch.empty(shape, dtype=dq.dtype, device=dq.device)
+        _call("mopt_rope_bwd", _p(dq.contiguous()), _p(dk.contiguous()), _p(dv.contiguous()),
+              _p(cos), _p(sin), _p(dqkv), R, T, H, _stream(dq))
+        return dqkv, None, None, None, None
+
+
+def rope_split(qkv, cos, sin, T, H):
+    if _hip(qkv):
+        return _RopeSplit.apply(qkv.contiguous(), cos, sin, T, H)
+    return rope_split_ref(qkv, cos, sin, T, H)
+
+
+class _Attention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, scale):
+        Bp, H, T, Dh = q.shape
+        if Dh != 64 or T % 64:
+            raise ValueError("attention kernel: head dim 64, T multiple of 64")
+        o = torch.empty(Bp * T, H * Dh, dtype=q.dtype, device=q.device)
+        lse = torch.empty(Bp * H, T, dtype=torch.float32, device=q.device)
+        _call("mopt_attn_fwd", _p(q), _p(k), _p(v), _p(o), _p(lse), Bp * H, T, H, scale,
+              _stream(q))
+        ctx.save_for_backward(q, k, v, o, lse)
+        ctx.scale = scale
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse = ctx.saved_tensors
+        Bp, H, T, _ = q.shape
+        do = do.contiguous()
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        dsum = torch.empty_like(lse)
+        _call("mopt_attn_bwd", _p(q), _p(k), _p(v), _p(o), _p(do), _p(lse), _p(dsum), _p(dq),
+              _p(dk), _p(dv), Bp * H, T, H, ctx.scale, _stream(q))
+        return dq, dk, dv, None
+
+
+def attention(q, k, v, scale=None):
+    scale = 1.0 / math.sqrt(q.shape[-1]) if scale is None else scale
+    if _hip(q):
+        return _Attention.apply(q, k, v, scale)
+    return attention_ref(q, k, v, scale)
+
+
+class _SwiGLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gu):
+        rows, F2 = gu.shape[0] * (gu.shape[1] if gu.dim() == 3 else 1), gu.shape[-1]
+        h = torch.empty(*gu.shape[:-1], F2 // 2, dtype=gu.dtype, device=gu.device)
+        _call("mopt_swiglu_fwd", _p(gu), _p(h), rows, F2 // 2, _stream(gu))
+        ctx.save_for_backward(gu)
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        (gu,) = ctx.saved_tensors
+        rows, F2 = gu.numel() // gu.shape[-1], gu.shape[-1]
+        dgu = torch.empty_like(gu)
+        _call("mopt_swiglu_bwd", _p(gu), _p(dh.contiguous()), _p(dgu), rows, F2 // 2,
+              _stream(gu))
+        return dgu
+
+
+def swiglu(gu):
+    if _hip(gu):
+        return _SwiGLU.apply(gu.contiguous())
+    return swiglu_ref(gu)
+
+
+class _CrossEntropy(torch.autograd.Function):
+    """Per-trial sum of token losses; the gradient (softmax - onehot) is written over the
+    logits buffer in the forward pass (the logits are not needed afterwards)."""
+
+    @staticmethod
+    def forward(ctx, logits, labels, rows_per_trial, grad_scale):
+        R, V = logits.shape[-2] * (logits.shape[0] if logits.dim() == 3 else 1), logits.shape[-1]
+        P = R // rows_per_trial
+        loss = torch.zeros(P, dtype=torch.float32, device=logits.device)
+        _call("mopt_ce_fwd_bwd", _p(logits), _p(labels), _p(loss), R, V, rows_per_trial,
+              grad_scale, 1, _stream(logits))
+        ctx.save_for_backward(logits)
+        return loss
+
+    @staticmethod
+    def backward(ctx, dloss):
+        (dlogits,) = ctx.saved_tensors
+        # d(sum_p w_p * loss_p): each trial's rows scale by its own weight
+        P = dloss.numel()
+        g = dlogits.view(P, -1, dlogits.shape[-1])
+        if not torch.all(dloss == 1):
+            g = g * dloss.view(P, 1, 1).to(g.dtype)
+        return g.view_as(dlogits), None, None, None
+
+
+def cross_entropy(logits, labels, rows_per_trial, grad_scale=1.0):
+    """Returns the per-trial SUM of token losses [P] (fp32).  ``grad_scale`` multiplies the
+    gradient written for the backward (``1 / rows_per_trial`` gives mean-loss gradients)."""
+    if _hip(logits):
+        return _CrossEntropy.apply(logits.contiguous(), labels.contiguous(), rows_per_trial,
+                                   grad_scale)
+    loss = ce_ref(logits.reshape(-1, logits.shape[-1]), labels, rows_per_trial)
+    return loss if grad_scale == 1.0 else _ScaledGrad.apply(loss, grad_scale)
+
+
+class _ScaledGrad(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, s):
+        ctx.s = s
+        return x.clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g * ctx.s, None
+
+
+def ce_eval(logits, labels, rows_per_trial):
+    """Loss sums without writing gradients (validation)."""
+    if _hip(logits):
+        R, V = logits.numel() // logits.shape[-1], logits.shape[-1]
+        loss = torch.zeros(R // rows_per_trial, dtype=torch.float32, device=logits.device)
+        _call("mopt_ce_fwd_bwd", _p(logits.contiguous()), _p(labels.contiguous()), _p(loss), R, V,
+              rows_per_trial, 1.0, 0, _stream(logits))
+        return loss
+    return ce_ref(logits.reshape(-1, logits.shape[-1]), labels, rows_per_trial)
+
+
+class _Embedding(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, tok, table, rows_per_trial):
+        P, V, d = table.shape
+        R = tok.numel()
+        out = torch.empty(R, d, dtype=table.dtype, device=table.device)
+        _call("mopt_embed_fwd", _p(tok), _p(table), _p(out), R, d, V, rows_per_trial,
+              _stream(table))
+        ctx.save_for_backward(tok)
+        ctx.dims = (P, V, d, rows_per_trial, table.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (tok,) = ctx.saved_tensors
+        P, V, d, rpt, dtype = ctx.dims
+        d32 = torch.zeros(P, V, d, dtype=torch.float32, device=dout.device)
+        _call("mopt_embed_bwd", _p(tok), _p(dout.contiguous()), _p(d32), tok.numel(), d, V, rpt,
+              _stream(dout))
+        d16 = torch.empty(P, V, d, dtype=dtype, device=dout.device)
+        _call("mopt_cast_bf16", _p(d32), _p(d16), d32.numel(), _stream(dout))
+        return None, d16, None
+
+
+def embedding(tok, table, rows_per_trial):
+    if _hip(table):
+        return _Embedding.apply(tok.contiguous(), table, rows_per_trial)
+    return embed_ref(tok, table, rows_per_trial)
+
+
+# ============================================================================ fused AdamW
+class FlatAdamW:
+    """Fused per-trial AdamW over flat parameter buffers (north-star kernel K6).
+
+    ``segments``: [(offset, numel_per_trial)] of every parameter tensor inside the flat buffers,
+    each tensor laid out ``[P, numel]``.  State: f32 master weights ``p32``, ``m``, ``v``; the
+    bf16 working copy ``p16`` is rewritten by the same kernel; ``g16`` is the flat bf16 gradient.
+    Hyper-parameters are per trial (``hp`` structured array, :data:`LM_HP_DTYPE`).
+    """
+
+    def __init__(self, segments: List[Tuple[int, int]], P: int, device):
+        self.P = P
+        self.device = torch.device(device)
+        segs = np.array(segments, dtype=SEG_DTYPE)
+        chunks = []
+        for j, (off, numel) in enumerate(segments):
+            for p in range(P):
+                starts = np.arange(p * numel, (p + 1) * numel, ADAM_CHUNK, dtype=np.int64)
+                c = np.zeros(len(starts), dtype=SEGCHUNK_DTYPE)
+                c["seg"], c["trial"], c["start"] = j, p, starts
+                chunks.append(c)
+        chunks = np.concatenate(chunks) if chunks else np.zeros(0, SEGCHUNK_DTYPE)
+        self.segments = segments
+        self.n_chunks = len(chunks)
+        if self.device.type == "cuda":
+            self._segs = torch.from_numpy(segs.view(np.uint8).copy()).to(self.device)
+            self._chunks = torch.from_numpy(chunks.view(np.uint8).copy()).to(self.device)
+            self._sumsq = torch.zeros(P, dtype=torch.float32, device=self.device)
+
+    def step(self, p32, p16, g16, m, v, hp: np.ndarray):
+        clip = int(bool((hp["max_norm"] > 0).any()))
+        if self.device.type == "cuda":
+            hp_dev = torch.from_numpy(hp.view(np.uint8).copy()).to(self.device, non_blocking=True)
+            _call("mopt_adamw_multi", _p(self._segs), _p(self._chunks), self.n_chunks, _p(hp_dev),
+                  _p(self._sumsq), _p(p32), _p(p16), _p(g16), _p(m), _p(v), self.P, clip,
+                  _lib.stream_ptr(self.device))
+            return
+        adamw_flat_ref(self.segments, self.P, p32, p16, g16, m, v, hp)
+
+
+def adamw_flat_ref(segments, P, p32, p16, g16, m, v, hp):
+    """fp32 reference of :class:`FlatAdamW` (same clipping and bias correction)."""
+    g = g16.float()
+    sumsq = torch.zeros(P, dtype=torch.float64)
+    for off, numel in segments:
+        gs = g[off:off + P * numel].view(P, numel)
+        sumsq += gs.double().pow(2).sum(1).cpu()
+    for off, numel in segments:
+        sl = slice(off, off + P * numel)
+        for p in range(P):
+            h = hp[p]
+            lo, hi = off + p * numel, off + (p + 1) * numel
+            gr = g[lo:hi]
+            if h["max_norm"] > 0:
+                nrm = math.sqrt(float(sumsq[p]))
+                if nrm > h["max_norm"]:
+                    gr = gr * (float(h["max_norm"]) / (nrm + 1e-6))
+            t = float(h["t"])
+            bc1, bc2 = 1 - float(h["b1"]) ** t, 1 - float(h["b2"]) ** t
+            w = p32[lo:hi]
+            w.mul_(1 - float(h["lr"]) * float(h["wd"]))
+            m[lo:hi].mul_(float(h["b1"])).add_(gr, alpha=1 - float(h["b1"]))
+            v[lo:hi].mul_(float(h["b2"])).addcmul_(gr, gr, value=1 - float(h["b2"]))
+            denom = v[lo:hi].sqrt() / math.sqrt(bc2) + float(h["eps"])
+            w.addcdiv_(m[lo:hi], denom, value=-float(h["lr"]) / bc1)
+        p16[sl] = p32[sl].to(p16.dtype)

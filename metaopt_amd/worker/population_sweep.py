@@ -221,7 +221,8 @@ class PopulationSweep:
                 continue
             vl, va, tl = float(gathered[row, 4]), float(gathered[row, 5]), float(gathered[row, 3])
             trial.results = [Trial.Result(name="val_loss", type="objective", value=vl),
-                             Trial.Result(name="val_acc", type="statistic", value=va),
+                             Trial.Result(name=getattr(self.task, "secondary_stat", "val_acc"),
+                                          type="statistic", value=va),
                              Trial.Result(name="train_loss", type="statistic", value=tl)]
             trial.status = "completed"
             trial.end_time = now
@@ -387,7 +388,8 @@ class PopulationSweep:
             if act not in (NEW, RESUME):
                 continue
             cfg = MemberConfig(width=int(a[2]), lr=float(a[3]), momentum=float(a[4]),
-                               weight_decay=float(a[5]), dropout=float(a[6]), seed=int(a[7]))
+                               weight_decay=float(a[5]), dropout=float(a[6]), seed=int(a[7]),
+                               **getattr(self.task, "member_defaults", {}))
             # checkpoints are not consumed: a PBT winner can seed several members
             meta = self.ckpts.get(int(a[9])) if act == RESUME and s not in received else None
             if act == RESUME and s in received:

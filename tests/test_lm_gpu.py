@@ -1,0 +1,166 @@
+"""Numerics of the population-LM HIP kernels (attention, RMSNorm, RoPE, SwiGLU, cross-entropy,
+embedding, fused AdamW) against fp32 PyTorch references of the same ops."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from metaopt_amd.ops import lm as ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _close(a, b, tol):
+    a, b = a.float(), b.float()
+    err = (a - b).abs().max().item()
+    scale = b.abs().max().item() + 1e-6
+    assert err <= tol * scale, f"max err {err} vs scale {scale}"
+
+
+@pytest.mark.parametrize("T,H,Bp", [(64, 1, 1), (256, 2, 3), (512, 4, 2)])
+def test_attention_fwd_bwd(T, H, Bp):
+    torch.manual_seed(0)
+    q, k, v = (torch.randn(Bp, H, T, 64, device=DEV).to(torch.bfloat16).requires_grad_(True)
+               for _ in range(3))
+    do = torch.randn(Bp * T, H * 64, device=DEV).to(torch.bfloat16)
+    o = ops.attention(q, k, v)
+    o.backward(do)
+    grads = [t.grad.clone() for t in (q, k, v)]
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    orf = ops.attention_ref(qr, kr, vr, 1 / 8)
+    orf.backward(do.float())
+    _close(o, orf, 2e-2)
+    for g, r in zip(grads, (qr.grad, kr.grad, vr.grad)):
+        _close(g, r, 3e-2)
+
+
+def test_rmsnorm_fwd_bwd():
+    torch.manual_seed(1)
+    P, rpt, d = 3, 128, 768
+    x = torch.randn(P * rpt, d, device=DEV).to(torch.bfloat16).requires_grad_(True)
+    w = (1 + 0.1 * torch.randn(P, d, device=DEV)).to(torch.bfloat16).requires_grad_(True)
+    dy = torch.randn(P * rpt, d, device=DEV).to(torch.bfloat16)
+    y = ops.rmsnorm(x, w, rpt)
+    y.backward(dy)
+    xr, wr = x.detach().float().requires_grad_(True), w.detach().float().requires_grad_(True)
+    yr = ops.rmsnorm_ref(xr, wr, rpt)
+    yr.backward(dy.float())
+    _close(y, yr, 1e-2)
+    _close(x.grad, xr.grad, 2e-2)
+    _close(w.grad, wr.grad, 2e-2)
+
+
+def test_rope_split_roundtrip():
+    torch.manual_seed(2)
+    Bp, T, H = 2, 128, 3
+    qkv = torch.randn(Bp * T, 3 * H * 64, device=DEV).to(torch.bfloat16).requires_grad_(True)
+    cos, sin = ops.rope_tables(T, device=DEV)
+    q, k, v = ops.rope_split(qkv, cos, sin, T, H)
+    qr, kr, vr = ops.rope_split_ref(qkv.detach(), cos, sin, T, H)
+    for a, b in ((q, qr), (k, kr), (v, vr)):
+        _close(a, b, 1e-2)
+    g = [torch.randn_like(t) for t in (q, k, v)]
+    torch.autograd.backward([q, k, v], g)
+    xr = qkv.detach().float().requires_grad_(True)
+    outs = ops.rope_split_ref(xr, cos, sin, T, H)
+    torch.autograd.backward(list(outs), [t.float() for t in g])
+    _close(qkv.grad, xr.grad, 2e-2)
+
+
+def test_swiglu_fwd_bwd():
+    torch.manual_seed(3)
+    gu = torch.randn(2, 64, 2 * 704, device=DEV).to(torch.bfloat16).requires_grad_(True)
+    dh = torch.randn(2, 64, 704, device=DEV).to(torch.bfloat16)
+    h = ops.swiglu(gu)
+    h.backward(dh)
+    gr = gu.detach().float().requires_grad_(True)
+    hr = ops.swiglu_ref(gr)
+    hr.backward(dh.float())
+    _close(h, hr, 1e-2)
+    _close(gu.grad, gr.grad, 2e-2)
+
+
+def test_cross_entropy_loss_and_grad():
+    torch.manual_seed(4)
+    P, rpt, V = 2, 64, 32000
+    logits = (3 * torch.randn(P * rpt, V, device=DEV)).to(torch.bfloat16)
+    labels = torch.randint(0, V, (P * rpt,), device=DEV, dtype=torch.int32)
+    lr_ = logits.float().requires_grad_(True)
+    ref = ops.ce_ref(lr_, labels, rpt)
+    (ref.sum() / rpt).backward()
+    work = logits.clone().requires_grad_(True)
+    loss = ops.cross_entropy(work, labels, rpt, grad_scale=1.0 / rpt)
+    loss.sum().backward()
+    _close(loss, ref, 1e-3)
+    _close(work.grad, lr_.grad, 2e-2)
+    ev = ops.ce_eval(logits.clone(), labels, rpt)
+    _close(ev, ref, 1e-3)
+
+
+def test_embedding_fwd_bwd():
+    torch.manual_seed(5)
+    P, V, d, rpt = 2, 1000, 256, 300
+    table = torch.randn(P, V, d, device=DEV).to(torch.bfloat16).requires_grad_(True)
+    tok = torch.randint(0, V, (P * rpt,), device=DEV, dtype=torch.int32)
+    out = ops.embedding(tok, table, rpt)
+    g = torch.randn_like(out)
+    out.backward(g)
+    tr = table.detach().float().requires_grad_(True)
+    ref = ops.embed_ref(tok, tr, rpt)
+    ref.backward(g.float())
+    assert torch.equal(out, ref.to(torch.bfloat16))
+    _close(table.grad, tr.grad, 1e-2)
+
+
+def test_fused_adamw_matches_reference():
+    torch.manual_seed(6)
+    P = 3
+    segments, off = [], 0
+    for n in (768, 4096, 3000 * 8):
+        segments.append((off, n))
+        off += P * n
+    bufs = {k: torch.randn(off, device=DEV) * (0.1 if k != "v" else 0.01) for k in ("p", "m", "v")}
+    bufs["v"] = bufs["v"].abs()
+    g16 = torch.randn(off, device=DEV).to(torch.bfloat16)
+    hp = np.zeros(P, dtype=ops.LM_HP_DTYPE)
+    for p in range(P):
+        hp[p] = (1e-3 * (p + 1), 0.9, 0.95, 1e-8, 0.1 * p, 1.0 if p != 1 else 0.0, 5 + p, 0)
+    opt = ops.FlatAdamW(segments, P, DEV)
+    hip = {k: v.clone() for k, v in bufs.items()}
+    p16 = torch.empty(off, dtype=torch.bfloat16, device=DEV)
+    opt.step(hip["p"], p16, g16, hip["m"], hip["v"], hp)
+    ref = {k: v.clone().cpu() for k, v in bufs.items()}
+    r16 = torch.empty(off, dtype=torch.bfloat16)
+    ops.adamw_flat_ref(segments, P, ref["p"], r16, g16.cpu(), ref["m"], ref["v"], hp)
+    torch.cuda.synchronize()
+    for k in ("p", "m", "v"):
+        torch.testing.assert_close(hip[k].cpu(), ref[k], rtol=1e-5, atol=1e-6)
+    assert torch.equal(p16.cpu(), r16)
+
+
+def test_population_lm_step_matches_reference():
+    from metaopt_amd.models.llama import PopulationLM, SyntheticLM
+    from metaopt_amd.ops.population import MemberConfig
+    data = SyntheticLM(512, 64, 4, n_tokens=1 << 14, seed=0, device=DEV)
+    pops = []
+    for dev in (DEV, "cpu"):
+        pop = PopulationLM(2, "micro", batch_size=4, device=dev)
+        for s in range(2):
+            pop.set_member(s, MemberConfig(width=128, lr=2e-3 * (s + 1), momentum=0.9,
+                                           seed=7 + s, beta2=0.95))
+        pops.append(pop)
+    # identical starting weights (the generators differ between devices)
+    with torch.no_grad():
+        pops[1].p32.copy_(pops[0].p32.cpu())
+        pops[1].p16.copy_(pops[0].p16.cpu())
+    losses = [[], []]
+    for step in range(5):
+        x, y = data.batch(step)
+        for i, pop in enumerate(pops):
+            pop.train_step(x.to(pop.device), y.to(pop.device))
+            losses[i].append(pop.train_loss())
+    a, b = np.array(losses[0]), np.array(losses[1])
+    assert np.allclose(a, b, rtol=2e-2, atol=2e-2), (a, b)
+    assert (a[-1] < a[0]).all()
