@@ -1,0 +1,253 @@
+"""Unrolled-hypergradient meta-optimisation of (learning rate, momentum) on a small transformer LM
+(BASELINE.json config 4).
+
+``HypergradLM`` trains ``P`` independent inner runs of a Llama-style LM (the ``tiny-2layer``
+preset by default) with SGD-momentum, and propagates forward-mode tangents of the weights with
+respect to the two hyper-parameters through every inner step (Franceschi et al., "Forward and
+Reverse Gradient-Based Hyperparameter Optimization", ICML 2017):
+
+* the inner loss is written with differentiable fp32 PyTorch ops (GEMMs on hipBLASLt), so one
+  forward-over-reverse pass (``torch.func.jvp`` of ``torch.func.grad``) yields the gradient and a
+  Hessian-vector product along each tangent, exactly (no finite differences);
+* the fused update of weights, momentum and the four tangent buffers is the hand-written K11
+  kernel (``mopt_hyper_sgdm``), and the final ``<grad L_val, Z>`` reductions are ``mopt_hyper_dot``;
+* ``HypergradientSweep`` runs the outer loop over ranks: every rank trains its own ``P`` inner runs
+  (different seeds and data shards), the per-rank mean hypergradient is averaged with ONE
+  all-reduce (C2) per outer step, and the shared (log lr, logit momentum) take an Adam step.
+  Each outer step is recorded as a trial (objective = validation loss, ``gradient`` result =
+  d L_val / d(lr, momentum)) in the experiment storage, the reference's gradient-result contract.
+"""
+from __future__ import annotations
+
+import ctypes
+import datetime
+import math
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from ..ops import _lib
+from ..ops import lm as ops
+from .llama import PRESETS, LMConfig, SyntheticLM, param_specs
+
+_lib.register_signatures({
+    "mopt_hyper_sgdm": ([ctypes.c_void_p] * 11 + [ctypes.c_int64, ctypes.c_int, ctypes.c_void_p],
+                        ctypes.c_int),
+    "mopt_hyper_dot": ([ctypes.c_void_p] * 4 + [ctypes.c_int64, ctypes.c_int, ctypes.c_void_p],
+                       ctypes.c_int),
+})
+
+
+def lm_losses(params: Dict[str, torch.Tensor], tok, tgt, cfg: LMConfig, cos, sin):
+    """Per-trial mean token loss [P] of a population LM, differentiable to second order."""
+    P = tok.shape[0]
+    T, d, H = cfg.seq_len, cfg.d_model, cfg.n_heads
+    rpt = tok[0].numel()
+    R = P * rpt
+    x = ops.embed_ref(tok.reshape(-1), params["embed"], rpt)
+    for l in range(cfg.n_layers):
+        h = ops.rmsnorm_ref(x, params[f"l{l}.attn_norm"], rpt, cfg.norm_eps)
+        qkv = torch.bmm(h.view(P, rpt, d), params[f"l{l}.wqkv"]).reshape(R, 3 * d)
+        q, k, v = ops.rope_split_ref(qkv, cos, sin, T, H)
+        o = ops.attention_ref(q, k, v, 1.0 / math.sqrt(cfg.head_dim))
+        x = x + torch.bmm(o.view(P, rpt, d), params[f"l{l}.wo"]).reshape(R, d)
+        h = ops.rmsnorm_ref(x, params[f"l{l}.mlp_norm"], rpt, cfg.norm_eps)
+        a = ops.swiglu_ref(torch.bmm(h.view(P, rpt, d), params[f"l{l}.wgu"]))
+        x = x + torch.bmm(a, params[f"l{l}.wdown"]).reshape(R, d)
+    h = ops.rmsnorm_ref(x, params["final_norm"], rpt, cfg.norm_eps)
+    logits = torch.bmm(h.view(P, rpt, d), params["head"]).reshape(R, cfg.vocab)
+    lz = torch.nn.functional.cross_entropy(logits, tgt.reshape(-1).long(), reduction="none")
+    return lz.view(P, rpt).mean(1)
+
+
+def hyper_sgdm_ref(w, v, ze, zm, ye, ym, g, he, hm, eta, mu):
+    """fp32 reference of the K11 update (in place)."""
+    e, m = eta[:, None], mu[:, None]
+    vn = m * v + g
+    yen = m * ye + he
+    ymn = m * ym + hm + v
+    ze.sub_(e * yen + vn)
+    zm.sub_(e * ymn)
+    w.sub_(e * vn)
+    v.copy_(vn)
+    ye.copy_(yen)
+    ym.copy_(ymn)
+
+
+class HypergradLM:
+    def __init__(self, capacity: int, config="tiny-2layer", batch_size: int = 4,
+                 seq_len: Optional[int] = None, device="cuda"):
+        cfg = PRESETS[config] if isinstance(config, str) else config
+        if seq_len is not None:
+            import dataclasses
+            cfg = dataclasses.replace(cfg, seq_len=seq_len)
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.P = P = int(capacity)
+        self.batch_size = batch_size
+        self.specs = param_specs(cfg)
+        self.offsets = []
+        n = 0
+        for _, shape, _ in self.specs:
+            k = int(np.prod(shape))
+            self.offsets.append((n, k))
+            n += k
+        self.n = n = (n + 3) // 4 * 4
+        z = lambda: torch.zeros(P, n, dtype=torch.float32, device=self.device)  # noqa: E731
+        self.w, self.v, self.ze, self.zm, self.ye, self.ym = z(), z(), z(), z(), z(), z()
+        self.eta = torch.zeros(P, dtype=torch.float32, device=self.device)
+        self.mu = torch.zeros(P, dtype=torch.float32, device=self.device)
+        self.cos, self.sin = ops.rope_tables(cfg.seq_len, cfg.rope_base, device=self.device)
+        self.steps = 0
+
+    def params(self, W: torch.Tensor) -> Dict[str, torch.Tensor]:
+        return {name: W[:, o:o + k].view(self.P, *shape)
+                for (name, shape, _), (o, k) in zip(self.specs, self.offsets)}
+
+    def reset(self, seeds: List[int], eta, mu) -> None:
+        """Fresh inner runs: weights from per-run seeds, zero momentum and tangents."""
+        for buf in (self.v, self.ze, self.zm, self.ye, self.ym):
+            buf.zero_()
+        self.w.zero_()
+        for p, seed in enumerate(seeds):
+            gen = torch.Generator(device=self.device)
+            gen.manual_seed(int(seed) & 0x7FFFFFFF)
+            for (name, shape, init), (o, k) in zip(self.specs, self.offsets):
+                dst = self.w[p, o:o + k]
+                if init[0] == "ones":
+                    dst.fill_(1.0)
+                else:
+                    dst.normal_(0.0, init[1], generator=gen)
+        self.eta.copy_(torch.as_tensor(eta, dtype=torch.float32).expand(self.P))
+        self.mu.copy_(torch.as_tensor(mu, dtype=torch.float32).expand(self.P))
+        self.steps = 0
+
+    def _loss_sum(self, W, tok, tgt):
+        return lm_losses(self.params(W), tok, tgt, self.cfg, self.cos, self.sin).sum()
+
+    def _expand(self, t):
+        t = t.to(self.device)
+        return t.unsqueeze(0).expand(self.P, *t.shape) if t.dim() == 2 else t
+
+    def inner_step(self, tok, tgt) -> torch.Tensor:
+        """One SGD-momentum step of every run with tangent propagation; returns losses [P]."""
+        tok, tgt = self._expand(tok), self._expand(tgt)
+        grad_fn = torch.func.grad_and_value(lambda W: self._loss_sum(W, tok, tgt))
+        (g, loss), (he, _) = torch.func.jvp(grad_fn, (self.w,), (self.ze,))
+        (_, _), (hm, _) = torch.func.jvp(grad_fn, (self.w,), (self.zm,))
+        with torch.no_grad():
+            losses = lm_losses(self.params(self.w), tok, tgt, self.cfg, self.cos, self.sin)
+        self._update(g.contiguous(), he.contiguous(), hm.contiguous())
+        self.steps += 1
+        return losses
+
+    def _update(self, g, he, hm):
+        if self.device.type == "cuda":
+            lib = _lib.get_lib()
+            _lib.check(lib.mopt_hyper_sgdm(*(t.data_ptr() for t in (
+                self.w, self.v, self.ze, self.zm, self.ye, self.ym, g, he, hm, self.eta,
+                self.mu)), self.n, self.P, _lib.stream_ptr(self.device)), "hyper_sgdm")
+        else:
+            hyper_sgdm_ref(self.w, self.v, self.ze, self.zm, self.ye, self.ym, g, he, hm,
+                           self.eta, self.mu)
+
+    def hypergradient(self, tok, tgt):
+        """(d L_val / d eta, d L_val / d mu) per run [P, 2] and the validation losses [P]."""
+        tok, tgt = self._expand(tok), self._expand(tgt)
+        gval, lval = torch.func.grad_and_value(lambda W: self._loss_sum(W, tok, tgt))(self.w)
+        with torch.no_grad():
+            losses = lm_losses(self.params(self.w), tok, tgt, self.cfg, self.cos, self.sin)
+        gval = gval.contiguous()
+        if self.device.type == "cuda":
+            out = torch.empty(self.P, 2, dtype=torch.float32, device=self.device)
+            lib = _lib.get_lib()
+            _lib.check(lib.mopt_hyper_dot(gval.data_ptr(), self.ze.data_ptr(), self.zm.data_ptr(),
+                                          out.data_ptr(), self.n, self.P,
+                                          _lib.stream_ptr(self.device)), "hyper_dot")
+        else:
+            out = torch.stack([(gval * self.ze).sum(1), (gval * self.zm).sum(1)], 1)
+        return out, losses
+
+
+class HypergradientSweep:
+    """Outer loop: shared (lr, momentum) meta-learned from ``world * P`` unrolled inner runs.
+
+    Every outer step: rank 0 broadcasts the current hyper-parameters (C5), each rank resets its
+    runs (seeds differ per rank, run and step), trains ``inner_steps`` with tangents, computes
+    the hypergradient on its validation shard, and ONE all-reduce averages [d/d lr, d/d mu,
+    val loss] across ranks (C2).  The meta-parameters (log lr, logit mu) then take an Adam step.
+    """
+
+    def __init__(self, model: HypergradLM, data: SyntheticLM, comm=None, experiment=None,
+                 lr0: float = 0.05, mu0: float = 0.5, meta_lr: float = 0.1,
+                 inner_steps: int = 20):
+        from ..parallel.comm import Comm
+        self.model, self.data = model, data
+        self.comm = comm or Comm(device=model.device)
+        self.experiment = experiment
+        self.theta = np.array([math.log(lr0), math.log(mu0 / (1 - mu0))], dtype=np.float64)
+        self.meta_lr = meta_lr
+        self.inner_steps = inner_steps
+        self._m = np.zeros(2)
+        self._v = np.zeros(2)
+        self.history: List[dict] = []
+        self.outer = 0
+
+    @property
+    def hparams(self):
+        return float(math.exp(self.theta[0])), float(1 / (1 + math.exp(-self.theta[1])))
+
+    def step(self) -> dict:
+        comm, model = self.comm, self.model
+        theta = torch.tensor(self.theta, dtype=torch.float64, device=comm._coll_device())
+        comm.broadcast_(theta, src=0)                                           # C5
+        self.theta = theta.cpu().numpy()
+        lr, mu = self.hparams
+        base = (self.outer * comm.world_size + comm.rank) * model.P
+        model.reset([1000003 * (base + p) + 17 for p in range(model.P)], lr, mu)
+        shard = self.outer * comm.world_size + comm.rank
+        for k in range(self.inner_steps):
+            tok, tgt = self.data.batch(shard * self.inner_steps + k)
+            model.inner_step(tok, tgt)
+        hg, vl = model.hypergradient(*self.data.validation())
+        red = torch.cat([hg.mean(0).double(), vl.mean().double().view(1)])
+        red = red.to(comm._coll_device())
+        comm.all_reduce_mean_(red)                                              # C2
+        g_lr, g_mu, val = (float(x) for x in red.cpu())
+        # chain rule into the unconstrained meta-parameters, then Adam
+        grad = np.array([g_lr * lr, g_mu * mu * (1 - mu)])
+        self.outer += 1
+        b1, b2 = 0.9, 0.999
+        self._m = b1 * self._m + (1 - b1) * grad
+        self._v = b2 * self._v + (1 - b2) * grad ** 2
+        mh = self._m / (1 - b1 ** self.outer)
+        vh = self._v / (1 - b2 ** self.outer)
+        self.theta = self.theta - self.meta_lr * mh / (np.sqrt(vh) + 1e-8)
+        rec = {"outer": self.outer, "lr": lr, "momentum": mu, "val_loss": val,
+               "d_lr": g_lr, "d_momentum": g_mu}
+        self.history.append(rec)
+        if comm.is_root and self.experiment is not None:
+            self._record(rec)
+        return rec
+
+    def _record(self, rec):
+        from ..core.trial import Trial
+        exp = self.experiment
+        now = datetime.datetime.utcnow()
+        t = Trial(experiment=exp.id, status="completed",
+                  params=[dict(name="/lr", type="real", value=rec["lr"]),
+                          dict(name="/momentum", type="real", value=rec["momentum"])],
+                  results=[dict(name="val_loss", type="objective", value=rec["val_loss"]),
+                           dict(name="hypergradient", type="gradient",
+                                value=[rec["d_lr"], rec["d_momentum"]])])
+        t.submit_time = t.start_time = t.end_time = now
+        try:
+            exp.storage.register_trial(t)
+        except Exception:  # duplicate point (same lr/mu twice): keep the first record
+            pass
+
+    def run(self, outer_steps: int) -> List[dict]:
+        for _ in range(outer_steps):
+            self.step()
+        return self.history

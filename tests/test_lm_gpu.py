@@ -164,3 +164,41 @@ def test_population_lm_step_matches_reference():
     a, b = np.array(losses[0]), np.array(losses[1])
     assert np.allclose(a, b, rtol=2e-2, atol=2e-2), (a, b)
     assert (a[-1] < a[0]).all()
+
+
+def test_k11_hyper_kernels_match_reference():
+    from metaopt_amd.models.hyper import HypergradLM, hyper_sgdm_ref
+    torch.manual_seed(8)
+    P, n = 3, 4096 + 64
+    bufs = [torch.randn(P, n, device=DEV) for _ in range(9)]
+    eta = torch.tensor([0.1, 0.05, 0.3], device=DEV)
+    mu = torch.tensor([0.9, 0.5, 0.0], device=DEV)
+    ref = [b.clone() for b in bufs]
+    hyper_sgdm_ref(*ref, eta, mu)
+    m = HypergradLM.__new__(HypergradLM)
+    m.device, m.P, m.n = torch.device(DEV), P, n
+    m.w, m.v, m.ze, m.zm, m.ye, m.ym = bufs[:6]
+    m.eta, m.mu = eta, mu
+    m._update(*bufs[6:])
+    torch.cuda.synchronize()
+    for a, b in zip(bufs[:6], ref[:6]):
+        torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-6)
+
+
+def test_hypergradient_on_gpu_matches_cpu():
+    from metaopt_amd.models.hyper import HypergradLM
+    from metaopt_amd.models.llama import SyntheticLM
+    out = []
+    for dev in (DEV, "cpu"):
+        data = SyntheticLM(512, 64, 2, n_tokens=1 << 13, seed=0, device=dev)
+        m = HypergradLM(2, "micro", batch_size=2, device=dev)
+        m.reset([1, 2], 0.3, 0.5)
+        if dev == "cpu":
+            m.w.copy_(out[0][2])
+        w0 = m.w.detach().clone().cpu()
+        for k in range(3):
+            m.inner_step(*data.batch(k))
+        hg, vl = m.hypergradient(*data.validation())
+        out.append((hg.cpu(), vl.cpu(), w0))
+    torch.testing.assert_close(out[0][0], out[1][0], rtol=5e-2, atol=5e-3)
+    torch.testing.assert_close(out[0][1], out[1][1], rtol=1e-3, atol=1e-3)
