@@ -313,8 +313,9 @@ __global__ __launch_bounds__(256) void ce_fwd_bwd_kernel(bf16_t* __restrict__ lo
     s = acc;
   }
   // combine (m, s) over the block
+  // lanes (or whole waves) without any chunk hold m = -inf: they contribute 0, never NaN
   const float wm = wave_max(m);
-  float ws = s * __expf(m - wm);
+  float ws = (m == -INFINITY) ? 0.f : s * __expf(m - wm);
   ws = wave_sum(ws);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (lane == 0) {
@@ -325,7 +326,8 @@ __global__ __launch_bounds__(256) void ce_fwd_bwd_kernel(bf16_t* __restrict__ lo
   float M = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
   float S = 0.f;
 #pragma unroll
-  for (int w = 0; w < 4; ++w) S += red[4 + w] * __expf(red[w] - M);
+  for (int w = 0; w < 4; ++w)
+    if (red[w] != -INFINITY) S += red[4 + w] * __expf(red[w] - M);
   const int y = labels[row];
   if (threadIdx.x == 0) {
     const float zy = bf2f(z[y]);
