@@ -94,6 +94,7 @@ def main(argv=None):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         sweep.step()
+    sweep.flush()            # deferred storage writes belong to the timed work
     sync()
     comm.barrier()
     sync()

@@ -244,6 +244,21 @@ def index_name(keys) -> str:
     return "_".join(f"{n}_{o}" for n, o in zip(names, orders))
 
 
+def _touched_keys(data) -> set:
+    """Top-level document keys an update writes (``$set``-style dotted keys included)."""
+    keys = set()
+    for k, v in data.items():
+        if k.startswith("$") and isinstance(v, dict):
+            keys |= {kk.split(".", 1)[0] for kk in v}
+        else:
+            keys.add(k.split(".", 1)[0])
+    return keys
+
+
+def _affected(fields, touched) -> bool:
+    return touched is None or any(f.split(".", 1)[0] in touched for f in fields)
+
+
 def _hashable(v):
     if isinstance(v, dict):
         return tuple(sorted((k, _hashable(x)) for k, x in v.items()))
@@ -381,29 +396,33 @@ class _Collection:
         return tuple(_hashable(None if (v := _get_path(doc, f)) is _MISSING else v)
                      for f in fields)
 
-    def _check_unique(self, doc):
+    def _check_unique(self, doc, touched=None):
         for name, (fields, unique, values) in self.indexes.items():
-            if unique and self._key(doc, fields) in values:
+            if unique and _affected(fields, touched) and self._key(doc, fields) in values:
                 raise DuplicateKeyError(f"Duplicate key error: index={name} "
                                         f"value={self._key(doc, fields)}")
 
-    def _register(self, doc):
+    def _register(self, doc, touched=None):
+        """Add ``doc`` to the indexes (only those over a top-level key in ``touched``, if given:
+        an update re-indexes just what it changed)."""
         hid = _hashable(doc["_id"])
         for fields, unique, values in self.indexes.values():
-            if unique:
+            if unique and _affected(fields, touched):
                 values.add(self._key(doc, fields))
         for field, hidx in self.hash_index.items():
-            hidx.setdefault(self._hval(doc, field), set()).add(hid)
+            if _affected((field,), touched):
+                hidx.setdefault(self._hval(doc, field), set()).add(hid)
 
-    def _unregister(self, doc):
+    def _unregister(self, doc, touched=None):
         hid = _hashable(doc["_id"])
         for fields, unique, values in self.indexes.values():
-            if unique:
+            if unique and _affected(fields, touched):
                 values.discard(self._key(doc, fields))
         for field, hidx in self.hash_index.items():
-            s = hidx.get(self._hval(doc, field))
-            if s is not None:
-                s.discard(hid)
+            if _affected((field,), touched):
+                s = hidx.get(self._hval(doc, field))
+                if s is not None:
+                    s.discard(hid)
 
     def insert(self, doc: dict):
         if "_id" not in doc:
@@ -465,15 +484,16 @@ class _Collection:
         apply_update(new, data, cow=True)
         if new.get("_id") != doc.get("_id"):
             raise DatabaseError("cannot change _id")
-        self._unregister(doc)
+        touched = _touched_keys(data)
+        self._unregister(doc, touched)
         try:
-            self._check_unique(new)
+            self._check_unique(new, touched)
         except DuplicateKeyError:
-            self._register(doc)
+            self._register(doc, touched)
             raise
         doc.clear()
         doc.update(new)
-        self._register(doc)
+        self._register(doc, touched)
 
     def delete(self, doc):
         self._unregister(doc)

@@ -221,6 +221,14 @@ class DocumentStorage(BaseStorageProtocol):
         d.pop("_id")
         return self._update_trial(trial, **d)
 
+    def complete_trial(self, trial: Trial) -> int:
+        """Write the outcome of a finished trial: results, status, end time and heartbeat only
+        (the other fields are unchanged since registration, so the document ends up identical
+        to :meth:`push_trial_results` at a fraction of the cost)."""
+        return self._update_trial(trial, results=[r.to_dict() for r in trial.results],
+                                  status=trial.status, end_time=trial.end_time,
+                                  heartbeat=trial.heartbeat)
+
     def set_trial_status(self, trial: Trial, status: str, heartbeat=None, was=None):
         """CAS: move ``trial`` from its current status (or ``was``) to ``status``."""
         heartbeat = heartbeat or utcnow()

@@ -28,6 +28,8 @@ import collections
 import datetime
 import logging
 import math
+import sys
+import threading
 import time
 from typing import Dict, List, Optional
 
@@ -97,6 +99,8 @@ class PopulationSweep:
             self.algorithm = experiment.algorithms
             self.space = experiment.space
             self._writer = _WriteBehind(experiment.storage)
+            # the writer thread hands the GIL back within 0.2 ms when this thread wakes up
+            sys.setswitchinterval(min(sys.getswitchinterval(), 2e-4))
 
     # ------------------------------------------------------------------ main loop
     def start(self) -> None:
@@ -139,9 +143,11 @@ class PopulationSweep:
         if evaluate and finished:
             vx, vy = self.data.validation()
             handle = pop.evaluate_async(vx, vy, slots=finished)
-        # 2) storage writes of the previous decision run on the host while the GPU works
+        # 2) storage writes of the previous decision run on the writer thread while this thread
+        #    waits for the GPU
         if self._writer is not None:
             self._writer.release()
+            self._writer.open_window()
         # 3) one device->host copy of train + eval statistics
         if active.any() and self.global_step > 0:
             snap = pop.stats_snapshot()
@@ -157,6 +163,8 @@ class PopulationSweep:
                     st[s, 5] = va[s]
                     if not math.isfinite(vl[s]):
                         st[s, 6] = 1
+        if self._writer is not None:
+            self._writer.close_window()
         return st
 
     def _sync(self, evaluate=True) -> None:
@@ -226,7 +234,7 @@ class PopulationSweep:
                              Trial.Result(name="train_loss", type="statistic", value=tl)]
             trial.status = "completed"
             trial.end_time = now
-            self._writer.put("push_trial_results", trial)
+            self._writer.put("complete_trial", trial)
             self.completed += 1
             self.history.append((time.time(), key, vl, budget))
             if vl < self.best[0]:
@@ -470,40 +478,123 @@ class _Snapshot:
 
 
 class _WriteBehind:
-    """Storage writes deferred to the GPU-wait window (write-behind).
+    """Storage writes taken off the decision path (write-behind).
 
     The sweep's decisions never read back what it writes (rank 0 keeps its own bookkeeping), so
-    persisting trials -- registration, results, status changes, heartbeats -- is taken off the
-    decision path: ``put`` snapshots the arguments, ``release`` applies the held writes in order.
-    The sweep calls ``release`` right after queueing a sync interval's kernels, so the writes run
-    on the host while the GPU trains (in the calling thread: a helper thread would contend with
-    the decision code for the GIL).  A failing write is logged and the rest continue.
+    persisting trials -- registration, results, status changes, heartbeats -- runs on a helper
+    thread while the main thread is blocked on the GPU: ``put`` snapshots the arguments,
+    ``release`` hands the held writes to the thread, and the thread only works while the *window*
+    is open (``open_window`` right before the main thread blocks on the device, ``close_window``
+    when it resumes), so it never competes with the decision code for the GIL.  Writes keep their
+    order; consecutive registrations become one bulk insert; ``flush`` drains everything.
     """
 
-    def __init__(self, storage):
+    def __init__(self, storage, background: bool = True):
         self.storage = storage
         self.errors = 0
         self._held: list = []
+        self._queue: "collections.deque" = collections.deque()
+        self._cv = threading.Condition()
+        self._window = False
+        self._busy = False
+        self._stop = False
+        self._thread = None
+        if background:
+            self._thread = threading.Thread(target=self._run, name="mopt-write-behind",
+                                            daemon=True)
+            self._thread.start()
 
     def put(self, method, *args, **kwargs):
-        # snapshot trials: the sweep keeps mutating its objects after queueing them
+        # snapshot trials (the sweep keeps mutating its objects after queueing them); the Trial
+        # objects are rebuilt from the snapshots when the write is applied
         args = tuple(_Snapshot(a.to_dict()) if isinstance(a, Trial) else a for a in args)
         self._held.append((method, args, kwargs))
 
     def release(self):
-        held, self._held = self._held, []
-        for method, args, kwargs in held:
-            args = tuple(Trial(**a.doc) if isinstance(a, _Snapshot) else a for a in args)
+        if not self._held:
+            return
+        with self._cv:
+            self._queue.append(self._held)
+            self._held = []
+            self._cv.notify_all()
+        if self._thread is None:
+            self._drain()
+
+    def open_window(self):
+        with self._cv:
+            self._window = True
+            self._cv.notify_all()
+
+    def close_window(self):
+        with self._cv:
+            self._window = False
+
+    def _run(self):
+        while True:
+            with self._cv:
+                while not self._stop and not (self._window and self._queue):
+                    self._cv.wait()
+                if self._stop and not self._queue:
+                    return
+                batch = self._queue.popleft()
+                self._busy = True
             try:
-                getattr(self.storage, method)(*args, **kwargs)
-            except DuplicateKeyError:
+                self._apply_batch(batch)
+            finally:
+                with self._cv:
+                    self._busy = False
+                    self._cv.notify_all()
+
+    def _drain(self):
+        while self._queue:
+            self._apply_batch(self._queue.popleft())
+
+    def _apply_batch(self, held):
+        i = 0
+        while i < len(held):
+            method, args, kwargs = held[i]
+            if method == "register_trial":   # consecutive registrations: one bulk insert
+                j = i
+                while j < len(held) and held[j][0] == "register_trial":
+                    j += 1
+                trials = [Trial(**h[1][0].doc) for h in held[i:j]]
+                self._apply("register_trials", (trials,), {}, fallback=trials)
+                i = j
+                continue
+            args = tuple(Trial(**a.doc) if isinstance(a, _Snapshot) else a for a in args)
+            self._apply(method, args, kwargs)
+            i += 1
+
+    def _apply(self, method, args, kwargs, fallback=None):
+        try:
+            getattr(self.storage, method)(*args, **kwargs)
+        except DuplicateKeyError:
+            if fallback is None:
                 log.debug("duplicate write skipped (%s)", method)
-            except Exception as exc:  # pragma: no cover - storage hiccup
-                self.errors += 1
-                log.warning("storage write %s failed: %s", method, exc)
+                return
+            for t in fallback:           # a bulk insert hit a duplicate: insert one by one
+                self._apply("register_trial", (t,), {})
+        except Exception as exc:  # pragma: no cover - storage hiccup
+            self.errors += 1
+            log.warning("storage write %s failed: %s", method, exc)
 
     def flush(self):
+        """Apply every held and queued write (blocks until done)."""
         self.release()
+        if self._thread is None:
+            return
+        with self._cv:
+            self._window = True
+            self._cv.notify_all()
+            while self._queue or self._busy:
+                self._cv.wait()
+            self._window = False
 
     def close(self):
-        self.release()
+        self.flush()
+        if self._thread is not None:
+            with self._cv:
+                self._stop = True
+                self._cv.notify_all()
+            self._thread.join()
+            self._thread = None

@@ -26,6 +26,9 @@ class _FakePop:
         self.capacity = capacity
         self.device = __import__("torch").device("cpu")
 
+    def alloc_ckpt_pool(self, n):
+        pass
+
 
 def main(n_syncs=40, P=256, profile=False):
     task = MLPSweepTask(priors=dict(MLP_PRIORS), max_width=1024)
