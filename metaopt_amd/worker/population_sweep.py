@@ -530,20 +530,37 @@ class _WriteBehind:
             self._window = False
 
     def _run(self):
+        # one write at a time, re-checking the window in between: when the main thread wakes
+        # up, the writer stops within one write (~0.1 ms) instead of finishing a whole batch
         while True:
             with self._cv:
                 while not self._stop and not (self._window and self._queue):
                     self._cv.wait()
                 if self._stop and not self._queue:
                     return
-                batch = self._queue.popleft()
+                batch = self._queue[0]
+                item = self._take(batch)
+                if not batch:
+                    self._queue.popleft()
                 self._busy = True
             try:
-                self._apply_batch(batch)
+                self._apply_batch(item)
             finally:
                 with self._cv:
                     self._busy = False
                     self._cv.notify_all()
+
+    @staticmethod
+    def _take(batch):
+        """Pop the next unit of work off a batch: a run of registrations (one bulk insert, up
+        to 64 documents) or a single write."""
+        n = 1
+        if batch[0][0] == "register_trial":
+            while n < min(len(batch), 64) and batch[n][0] == "register_trial":
+                n += 1
+        item = batch[:n]
+        del batch[:n]
+        return item
 
     def _drain(self):
         while self._queue:
