@@ -222,6 +222,10 @@ class PopulationLM:
         return {"rows": inp.shape[-1] * inp.shape[-2], "subset": None if slots is None
                 else set(int(s) for s in slots)}
 
+    def device_busy(self):
+        from ..ops.population import device_busy
+        return device_busy(self.device)
+
     def stats_snapshot(self) -> np.ndarray:
         return self.stats.cpu().numpy().reshape(4, self.capacity)
 

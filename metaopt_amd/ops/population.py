@@ -77,6 +77,14 @@ class MemberConfig:
         return dataclasses.asdict(self)
 
 
+def device_busy(device):
+    if torch.device(device).type != "cuda":
+        return lambda: True
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(device))
+    return lambda: not ev.query()
+
+
 class PopulationMLP:
     """``capacity`` MLP trials (``n_hidden`` ReLU layers of per-trial width) on one device."""
 
@@ -649,6 +657,11 @@ class PopulationMLP:
                 self.eval_loss[s] = ls
                 self.eval_correct[s] = cs
         return handle
+
+    def device_busy(self):
+        """A callable that stays True while the work queued so far is still running on the GPU
+        (always True on the CPU backend, where nothing runs asynchronously)."""
+        return device_busy(self.device)
 
     def stats_snapshot(self) -> np.ndarray:
         """One device->host copy of the train and eval statistics (waits for queued work)."""

@@ -25,11 +25,10 @@ dies they become *lost* and other workers re-run them.
 from __future__ import annotations
 
 import collections
+import gc
 import datetime
 import logging
 import math
-import sys
-import threading
 import time
 from typing import Dict, List, Optional
 
@@ -92,6 +91,9 @@ class PopulationSweep:
                            (experiment.max_trials if experiment is not None else math.inf))
         self._writer = None
         self.timers: Dict[str, float] = collections.defaultdict(float)  # host seconds per phase
+        self._gc_t0 = 0.0
+        self.max_write_backlog = 4 * pop.capacity * self.comm.world_size
+        gc.callbacks.append(self._gc_callback)   # host GC pauses show up in the phase timers
         self.n_resumed = 0            # members resumed from a device checkpoint (this rank)
         self.n_resume_missing = 0
         self.n_syncs = 0
@@ -99,8 +101,12 @@ class PopulationSweep:
             self.algorithm = experiment.algorithms
             self.space = experiment.space
             self._writer = _WriteBehind(experiment.storage)
-            # the writer thread hands the GIL back within 0.2 ms when this thread wakes up
-            sys.setswitchinterval(min(sys.getswitchinterval(), 2e-4))
+
+    def _gc_callback(self, phase, info):
+        if phase == "start":
+            self._gc_t0 = time.perf_counter()
+        else:
+            self.timers[f"gc_gen{info.get('generation', 0)}"] += time.perf_counter() - self._gc_t0
 
     # ------------------------------------------------------------------ main loop
     def start(self) -> None:
@@ -143,11 +149,10 @@ class PopulationSweep:
         if evaluate and finished:
             vx, vy = self.data.validation()
             handle = pop.evaluate_async(vx, vy, slots=finished)
-        # 2) storage writes of the previous decision run on the writer thread while this thread
-        #    waits for the GPU
-        if self._writer is not None:
-            self._writer.release()
-            self._writer.open_window()
+        # 2) storage writes of the previous decision run on the host while the GPU is still busy
+        #    with the interval (and the evaluation) just queued
+        if self._writer is not None and len(self._writer):
+            self._writer.drain_while(pop.device_busy())
         # 3) one device->host copy of train + eval statistics
         if active.any() and self.global_step > 0:
             snap = pop.stats_snapshot()
@@ -164,7 +169,11 @@ class PopulationSweep:
                     if not math.isfinite(vl[s]):
                         st[s, 6] = 1
         if self._writer is not None:
-            self._writer.close_window()
+            self.timers["writes_backlog"] += len(self._writer)
+            self.timers["writes_busy"] += self._writer.busy_s
+            self._writer.busy_s = 0.0
+            if len(self._writer) > self.max_write_backlog:
+                self._writer.flush()  # the host cannot keep up: do not let the queue grow
         return st
 
     def _sync(self, evaluate=True) -> None:
@@ -192,6 +201,9 @@ class PopulationSweep:
             assign = assign_t.cpu().numpy()
         t4 = time.perf_counter()
         self._apply(gathered, assign)
+        # long-lived bookkeeping (trial documents, algorithm state) moves to the permanent GC
+        # generation: full collections would otherwise rescan it every few syncs
+        gc.freeze()
         t5 = time.perf_counter()
         tm["status"] += t1 - t0
         tm["c1_allgather"] += t2 - t1
@@ -243,10 +255,14 @@ class PopulationSweep:
             done_res.append({"objective": vl, "constraint": [], "gradient": None})
             if budget < self._max_budget():
                 self._record_ckpt(self.task.key(params), rank, key, steps)
+        t0 = time.perf_counter()
         if done_pts:
             self.algorithm.observe(done_pts, done_res)
+        t1 = time.perf_counter()
         self._heartbeat()
         self._fill(free, assign)
+        self.timers["decide_observe"] += t1 - t0
+        self.timers["decide_fill"] += time.perf_counter() - t1
         return assign
 
     def _max_budget(self) -> int:
@@ -348,6 +364,8 @@ class PopulationSweep:
             self._writer.flush()
 
     def close(self) -> None:
+        if self._gc_callback in gc.callbacks:
+            gc.callbacks.remove(self._gc_callback)
         if self._writer is not None:
             self._writer.close()
             self._writer = None
@@ -481,28 +499,19 @@ class _WriteBehind:
     """Storage writes taken off the decision path (write-behind).
 
     The sweep's decisions never read back what it writes (rank 0 keeps its own bookkeeping), so
-    persisting trials -- registration, results, status changes, heartbeats -- runs on a helper
-    thread while the main thread is blocked on the GPU: ``put`` snapshots the arguments,
-    ``release`` hands the held writes to the thread, and the thread only works while the *window*
-    is open (``open_window`` right before the main thread blocks on the device, ``close_window``
-    when it resumes), so it never competes with the decision code for the GIL.  Writes keep their
-    order; consecutive registrations become one bulk insert; ``flush`` drains everything.
+    persisting trials -- registration, results, status changes, heartbeats -- is deferred: ``put``
+    snapshots the arguments; ``drain_while(busy)`` applies held writes in order, one unit at a
+    time, for as long as ``busy()`` says the GPU is still working on the interval just queued, so
+    the host does its bookkeeping inside the device time instead of after it (no helper thread:
+    a thread would need the GIL that the waiting thread holds).  Consecutive registrations become
+    one bulk insert.  ``flush`` applies everything.
     """
 
-    def __init__(self, storage, background: bool = True):
+    def __init__(self, storage):
         self.storage = storage
         self.errors = 0
-        self._held: list = []
-        self._queue: "collections.deque" = collections.deque()
-        self._cv = threading.Condition()
-        self._window = False
-        self._busy = False
-        self._stop = False
-        self._thread = None
-        if background:
-            self._thread = threading.Thread(target=self._run, name="mopt-write-behind",
-                                            daemon=True)
-            self._thread.start()
+        self._held: "collections.deque" = collections.deque()
+        self.busy_s = 0.0             # seconds spent applying writes
 
     def put(self, method, *args, **kwargs):
         # snapshot trials (the sweep keeps mutating its objects after queueing them); the Trial
@@ -510,61 +519,24 @@ class _WriteBehind:
         args = tuple(_Snapshot(a.to_dict()) if isinstance(a, Trial) else a for a in args)
         self._held.append((method, args, kwargs))
 
-    def release(self):
-        if not self._held:
-            return
-        with self._cv:
-            self._queue.append(self._held)
-            self._held = []
-            self._cv.notify_all()
-        if self._thread is None:
-            self._drain()
+    def __len__(self):
+        return len(self._held)
 
-    def open_window(self):
-        with self._cv:
-            self._window = True
-            self._cv.notify_all()
+    def drain_while(self, busy) -> None:
+        t0 = time.perf_counter()
+        while self._held and busy():
+            self._apply_batch(self._take())
+        self.busy_s += time.perf_counter() - t0
 
-    def close_window(self):
-        with self._cv:
-            self._window = False
-
-    def _run(self):
-        # one write at a time, re-checking the window in between: when the main thread wakes
-        # up, the writer stops within one write (~0.1 ms) instead of finishing a whole batch
-        while True:
-            with self._cv:
-                while not self._stop and not (self._window and self._queue):
-                    self._cv.wait()
-                if self._stop and not self._queue:
-                    return
-                batch = self._queue[0]
-                item = self._take(batch)
-                if not batch:
-                    self._queue.popleft()
-                self._busy = True
-            try:
-                self._apply_batch(item)
-            finally:
-                with self._cv:
-                    self._busy = False
-                    self._cv.notify_all()
-
-    @staticmethod
-    def _take(batch):
-        """Pop the next unit of work off a batch: a run of registrations (one bulk insert, up
-        to 64 documents) or a single write."""
-        n = 1
-        if batch[0][0] == "register_trial":
-            while n < min(len(batch), 64) and batch[n][0] == "register_trial":
-                n += 1
-        item = batch[:n]
-        del batch[:n]
+    def _take(self):
+        """Next unit of work: a run of registrations (one bulk insert of <= 64 documents) or a
+        single write."""
+        first = self._held.popleft()
+        item = [first]
+        if first[0] == "register_trial":
+            while self._held and len(item) < 64 and self._held[0][0] == "register_trial":
+                item.append(self._held.popleft())
         return item
-
-    def _drain(self):
-        while self._queue:
-            self._apply_batch(self._queue.popleft())
 
     def _apply_batch(self, held):
         i = 0
@@ -596,22 +568,8 @@ class _WriteBehind:
             log.warning("storage write %s failed: %s", method, exc)
 
     def flush(self):
-        """Apply every held and queued write (blocks until done)."""
-        self.release()
-        if self._thread is None:
-            return
-        with self._cv:
-            self._window = True
-            self._cv.notify_all()
-            while self._queue or self._busy:
-                self._cv.wait()
-            self._window = False
+        """Apply every held write."""
+        self.drain_while(lambda: True)
 
     def close(self):
         self.flush()
-        if self._thread is not None:
-            with self._cv:
-                self._stop = True
-                self._cv.notify_all()
-            self._thread.join()
-            self._thread = None

@@ -67,7 +67,7 @@ def main(n_syncs=40, P=256, profile=False):
             prof.disable()
         t_total += time.perf_counter() - t0
         t1 = time.perf_counter()
-        sw._writer.release()
+        sw._writer.flush()
         t_rel += time.perf_counter() - t1
     sw.close()
     print(f"decide: {1e3 * t_total / n_syncs:.2f} ms/sync, writes {1e3 * t_rel / n_syncs:.2f} ms/sync, "
