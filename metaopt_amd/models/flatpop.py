@@ -1,0 +1,361 @@
+"""Populations of same-architecture trials on flat parameter buffers (the LM and CNN paths).
+
+A :class:`FlatPopulation` keeps ``capacity`` trials of ONE architecture on a device.  Every
+parameter tensor is stacked over the population (``[P, ...]``) and lives in flat buffers:
+
+* ``p16`` -- bf16 working weights; the autograd leaves are views of it, and their ``.grad`` is
+  pre-bound to views of the flat bf16 gradient ``g16`` (autograd accumulates in place, so the
+  whole population's gradient is one contiguous buffer);
+* ``p32`` -- f32 master weights, ``m``/``v`` -- optimizer state; one fused kernel updates every
+  tensor of every trial with per-trial hyper-parameters (AdamW: K6, SGD-momentum: K5);
+* ``aux`` -- per-trial non-parameter state (e.g. BatchNorm running statistics), checkpointed
+  with the weights.
+
+Subclasses define ``param_specs()`` / ``aux_size()`` and ``_loss(x, y, train)`` (per-trial loss
+sums, optionally per-trial #correct).  The member interface -- ``set_member``,
+``update_hparams``, ``remove_member``, ``train_step``, ``evaluate_async`` / ``eval_result``,
+``save_states`` / ``load_states`` (one batched copy kernel), ``pack_state`` / ``unpack_state``
+(C4 transfers) -- is what :class:`~metaopt_amd.worker.population_sweep.PopulationSweep` drives.
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from ..ops import lm as ops
+from ..ops.population import MemberConfig, device_busy
+
+
+class FlatPopulation:
+    optimizer = "adamw"            # or "sgd"
+    secondary = "acc"              # eval_result's second array: "acc" or "ppl"
+
+    def __init__(self, capacity: int, device="cuda", max_grad_norm: float = 0.0):
+        self.device = torch.device(device)
+        self.backend = "hip" if self.device.type == "cuda" else "torch"
+        self.capacity = P = int(capacity)
+        self.max_grad_norm = float(max_grad_norm)
+        self.specs = self.param_specs()
+        self.segments = []
+        off = 0
+        for name, shape, _ in self.specs:
+            n = int(np.prod(shape))
+            if n % 8:
+                raise ValueError(f"parameter {name}: per-trial size {n} must be a multiple of 8 "
+                                 "(the fused optimizer moves 8 elements per lane)")
+            self.segments.append((off, n))
+            off += P * n
+        self.n_flat = off
+        dev = self.device
+        self.p32 = torch.zeros(off, dtype=torch.float32, device=dev)
+        self.p16 = torch.zeros(off, dtype=torch.bfloat16, device=dev)
+        self.g16 = torch.zeros(off, dtype=torch.bfloat16, device=dev)
+        self.m = torch.zeros(off, dtype=torch.float32, device=dev)
+        self.v = (torch.zeros(off, dtype=torch.float32, device=dev) if self.optimizer == "adamw"
+                  else torch.zeros(0, dtype=torch.float32, device=dev))
+        # per-trial non-parameter state, segment-major like the parameters: A[name] is [P, n]
+        self.aux_segments, aoff = [], 0
+        for name, n in self.aux_specs():
+            self.aux_segments.append((name, aoff, int(n)))
+            aoff += P * int(n)
+        self.n_aux = sum(n for _, _, n in self.aux_segments)
+        self.aux = torch.zeros(max(aoff, 4), dtype=torch.float32, device=dev)
+        self.A = {name: self.aux[o:o + P * n].view(P, n) for name, o, n in self.aux_segments}
+        self.W: Dict[str, torch.Tensor] = {}
+        for (name, shape, _), (o, n) in zip(self.specs, self.segments):
+            leaf = self.p16[o:o + P * n].view(P, *shape)
+            leaf.requires_grad_(True)
+            leaf.grad = self.g16[o:o + P * n].view(P, *shape)
+            self.W[name] = leaf
+        self.opt = ops.FlatOptimizer(self.segments, P, dev, kind=self.optimizer)
+        self.hp = np.zeros(P, dtype=[("t", "<i4")])
+        self.opt_hp = np.zeros(P, dtype=ops.LM_HP_DTYPE)
+        self.members: List[Optional[MemberConfig]] = [None] * P
+        self.stats = torch.zeros(4 * P, dtype=torch.float32, device=dev)
+        self._ck = None
+        self._ck_aux = None
+
+    # ------------------------------------------------------------------ subclass hooks
+    def param_specs(self):
+        """[(name, per-trial shape, init)]; init = ('normal', std) | ('ones',) | ('zeros',) |
+        ('kaiming', fan_in)."""
+        raise NotImplementedError
+
+    def aux_specs(self):
+        """[(name, per-trial numel)] of the non-parameter state (checkpointed with the weights)."""
+        return []
+
+    def init_aux(self, slot: int) -> None:
+        pass
+
+    def _loss(self, x, y, train: bool):
+        """Per-trial loss sums [P] (and optionally #correct [P]) of batch (x, y)."""
+        raise NotImplementedError
+
+    def rows_per_batch(self, x) -> int:
+        return int(x.shape[0])
+
+    # ------------------------------------------------------------------ members
+    @property
+    def n_params(self) -> int:
+        return sum(n for _, n in self.segments)
+
+    def active_slots(self):
+        return [s for s, m in enumerate(self.members) if m is not None]
+
+    def _write_hp(self, slot, cfg: MemberConfig, t: int):
+        self.hp[slot]["t"] = t
+        self.opt_hp[slot] = (cfg.lr, cfg.momentum, cfg.beta2, cfg.eps, cfg.weight_decay,
+                             self.max_grad_norm, t, 0)
+
+    def _slices(self, slot):
+        return [slice(o + slot * n, o + (slot + 1) * n) for o, n in self.segments]
+
+    def _aux_slices(self, slot):
+        return [slice(o + slot * n, o + (slot + 1) * n) for _, o, n in self.aux_segments]
+
+    def _aux_of(self, slot) -> torch.Tensor:
+        sl = self._aux_slices(slot)
+        return torch.cat([self.aux[x] for x in sl]) if sl else torch.zeros(0, device=self.device)
+
+    def _set_aux(self, slot, flat) -> None:
+        o = 0
+        for x in self._aux_slices(slot):
+            n = x.stop - x.start
+            self.aux[x] = flat[o:o + n]
+            o += n
+
+    @torch.no_grad()
+    def set_member(self, slot: int, cfg: MemberConfig, init: bool = True) -> None:
+        self.members[slot] = cfg
+        self._write_hp(slot, cfg, 0)
+        if not init:
+            return
+        gen = torch.Generator(device=self.device)
+        gen.manual_seed(int(cfg.seed) & 0x7FFFFFFF)
+        for (name, shape, init_), sl in zip(self.specs, self._slices(slot)):
+            dst = self.p32[sl]
+            kind = init_[0]
+            if kind == "ones":
+                dst.fill_(1.0)
+            elif kind == "zeros":
+                dst.zero_()
+            elif kind == "normal":
+                dst.normal_(0.0, init_[1], generator=gen)
+            elif kind == "kaiming":
+                dst.normal_(0.0, (2.0 / init_[1]) ** 0.5, generator=gen)
+            else:
+                raise ValueError(f"unknown init {init_}")
+            self.p16[sl] = dst.to(torch.bfloat16)
+            self.m[sl].zero_()
+            if self.v.numel():
+                self.v[sl].zero_()
+        self.init_aux(slot)
+
+    def update_hparams(self, slot: int, **changes) -> None:
+        cfg = dataclasses.replace(self.members[slot], **changes)
+        self.members[slot] = cfg
+        self._write_hp(slot, cfg, int(self.hp[slot]["t"]))
+
+    def remove_member(self, slot: int) -> None:
+        self.members[slot] = None
+        self.hp[slot]["t"] = 0
+        self.opt_hp[slot] = 0
+
+    def steps_done(self, slot: int) -> int:
+        return int(self.hp[slot]["t"])
+
+    # ------------------------------------------------------------------ training
+    def _expand(self, t: torch.Tensor, dtype=None) -> torch.Tensor:
+        """The shared batch of every trial, with a leading population dimension."""
+        t = t.to(self.device) if dtype is None else t.to(self.device, dtype)
+        return t.unsqueeze(0).expand(self.capacity, *t.shape).contiguous()
+
+    def train_step(self, x: torch.Tensor, y: torch.Tensor) -> None:
+        active = np.array([m is not None for m in self.members])
+        self.hp["t"][active] += 1
+        self.opt_hp["t"] = self.hp["t"]
+        self.g16.zero_()
+        out = self._loss(x, y, train=True)
+        loss = out[0] if isinstance(out, tuple) else out
+        loss.sum().backward()
+        P = self.capacity
+        self.stats[:P].copy_(loss.detach())
+        if isinstance(out, tuple):
+            self.stats[P:2 * P].copy_(out[1].detach())
+        with torch.no_grad():
+            self.opt.step(self.p32, self.p16, self.g16, self.m, self.v, self.opt_hp)
+
+    # ------------------------------------------------------------------ evaluation / stats
+    @torch.no_grad()
+    def evaluate_async(self, x, y, slots=None):
+        out = self._loss(x, y, train=False)
+        P = self.capacity
+        loss = out[0] if isinstance(out, tuple) else out
+        self.stats[2 * P:3 * P].copy_(loss)
+        if isinstance(out, tuple):
+            self.stats[3 * P:].copy_(out[1])
+        return {"rows": self.rows_per_batch(x), "subset": None if slots is None
+                else set(int(s) for s in slots)}
+
+    def device_busy(self):
+        return device_busy(self.device)
+
+    def stats_snapshot(self) -> np.ndarray:
+        return self.stats.cpu().numpy().reshape(4, self.capacity)
+
+    def train_rows(self) -> int:
+        return self.batch_size
+
+    def train_loss(self, snap=None) -> np.ndarray:
+        snap = self.stats_snapshot() if snap is None else snap
+        out = snap[0].astype(np.float64) / self.train_rows()
+        out[[m is None for m in self.members]] = np.nan
+        return out
+
+    def eval_result(self, snap, handle):
+        rows = handle["rows"]
+        loss = snap[2].astype(np.float64) / rows
+        second = (np.exp(np.minimum(loss, 50.0)) if self.secondary == "ppl"
+                  else snap[3].astype(np.float64) / rows)
+        for s in range(self.capacity):
+            if self.members[s] is None or (handle["subset"] is not None
+                                           and s not in handle["subset"]):
+                loss[s] = second[s] = np.nan
+        return loss, second
+
+    def evaluate(self, x, y, slots=None):
+        return self.eval_result(self.stats_snapshot(), self.evaluate_async(x, y, slots))
+
+    # ------------------------------------------------------------------ checkpoints
+    def _state_bufs(self):
+        return [self.p32, self.m] + ([self.v] if self.v.numel() else [])
+
+    def used_params_for(self, width=None) -> int:
+        return self.n_params
+
+    def alloc_ckpt_pool(self, n: int) -> None:
+        k = len(self._state_bufs())
+        self._ck = torch.zeros(n, k, self.n_params, dtype=torch.float32, device=self.device)
+        self._ck_aux = torch.zeros(n, max(self.n_aux, 4), dtype=torch.float32, device=self.device)
+
+    def _copy_items(self, slot, idx, to_pool: bool):
+        items = []
+        for j, buf in enumerate(self._state_bufs()):
+            o = 0
+            for sl in self._slices(slot):
+                n = sl.stop - sl.start
+                pool = self._ck[idx, j, o:o + n]
+                if to_pool:
+                    items.append((buf[sl], pool, None))
+                else:
+                    items.append((pool, buf[sl], self.p16[sl] if j == 0 else None))
+                o += n
+        o = 0
+        for x in self._aux_slices(slot):
+            n = x.stop - x.start
+            pool = self._ck_aux[idx, o:o + n]
+            items.append((self.aux[x], pool, None) if to_pool else (pool, self.aux[x], None))
+            o += n
+        return items
+
+    @torch.no_grad()
+    def save_states(self, pairs) -> list:
+        from ..ops.ckpt import multi_copy
+        items, metas = [], []
+        for slot, idx in pairs:
+            items += self._copy_items(slot, idx, True)
+            metas.append({"config": self.members[slot].to_dict(), "t": int(self.hp[slot]["t"]),
+                          "ck": int(idx), "n": self.n_params})
+        multi_copy(items)
+        return metas
+
+    @torch.no_grad()
+    def load_states(self, pairs) -> None:
+        from ..ops.ckpt import multi_copy
+        items = []
+        for slot, meta in pairs:
+            items += self._copy_items(slot, meta["ck"], False)
+            cfg = MemberConfig(**meta["config"])
+            self.members[slot] = cfg
+            self._write_hp(slot, cfg, int(meta["t"]))
+        multi_copy(items)
+
+    def pool_state(self, meta: dict) -> dict:
+        idx = meta["ck"]
+        st = {"config": meta["config"], "t": meta["t"], "p32": self._ck[idx, 0],
+              "m32": self._ck[idx, 1], "aux": self._ck_aux[idx, :self.n_aux],
+              "optimizer": self.optimizer}
+        if self.v.numel():
+            st["v32"] = self._ck[idx, 2]
+        return st
+
+    def slot_state(self, slot: int) -> dict:
+        cat = lambda buf: torch.cat([buf[sl] for sl in self._slices(slot)])  # noqa: E731
+        st = {"config": self.members[slot].to_dict(), "t": int(self.hp[slot]["t"]),
+              "p32": cat(self.p32), "m32": cat(self.m), "aux": self._aux_of(slot),
+              "optimizer": self.optimizer}
+        if self.v.numel():
+            st["v32"] = cat(self.v)
+        return st
+
+    @torch.no_grad()
+    def load_slot_state(self, slot: int, state: dict) -> None:
+        o = 0
+        for sl in self._slices(slot):
+            n = sl.stop - sl.start
+            self.p32[sl] = state["p32"][o:o + n]
+            self.m[sl] = state["m32"][o:o + n]
+            if self.v.numel():
+                self.v[sl] = state["v32"][o:o + n]
+            self.p16[sl] = self.p32[sl].to(torch.bfloat16)
+            o += n
+        if "aux" in state and self.n_aux:
+            self._set_aux(slot, state["aux"])
+        cfg = MemberConfig(**state["config"])
+        self.members[slot] = cfg
+        self._write_hp(slot, cfg, int(state["t"]))
+
+    @torch.no_grad()
+    def copy_member(self, src: int, dst: int, **hp_changes) -> None:
+        """PBT exploit inside one device: dst <- src (weights, optimizer state, step count)."""
+        for a, b in zip(self._slices(src), self._slices(dst)):
+            for buf in [self.p16] + self._state_bufs():
+                buf[b] = buf[a]
+        for a, b in zip(self._aux_slices(src), self._aux_slices(dst)):
+            self.aux[b] = self.aux[a]
+        cfg = dataclasses.replace(self.members[src], **hp_changes)
+        self.members[dst] = cfg
+        self._write_hp(dst, cfg, int(self.hp[src]["t"]))
+
+    def _n_packed(self) -> int:
+        return 2 + len(self._state_bufs()) * self.n_params + self.n_aux
+
+    def empty_packed_state(self, width=None) -> torch.Tensor:
+        return torch.empty(self._n_packed(), dtype=torch.float32, device=self.device)
+
+    def pack_state(self, state: dict) -> torch.Tensor:
+        head = torch.tensor([int(state["t"]), int(state["config"]["seed"])], dtype=torch.int32)
+        parts = [head.view(torch.float32).to(self.device), state["p32"].reshape(-1),
+                 state["m32"].reshape(-1)]
+        if self.v.numel():
+            parts.append(state["v32"].reshape(-1))
+        aux = state.get("aux")
+        parts.append(aux.reshape(-1) if aux is not None
+                     else torch.zeros(self.n_aux, device=self.device))
+        return torch.cat([p.to(self.device, torch.float32) for p in parts])
+
+    def unpack_state(self, buf: torch.Tensor, width=None) -> dict:
+        n = self.n_params
+        t, seed = (int(v) for v in buf[:2].view(torch.int32).cpu().tolist())
+        st = {"config": MemberConfig(width=0, lr=0.0, seed=seed).to_dict(), "t": t,
+              "p32": buf[2:2 + n], "m32": buf[2 + n:2 + 2 * n], "optimizer": self.optimizer}
+        o = 2 + 2 * n
+        if self.v.numel():
+            st["v32"] = buf[o:o + n]
+            o += n
+        st["aux"] = buf[o:]
+        return st

@@ -1,0 +1,200 @@
+"""ResNet-20 populations on CIFAR-shaped data (BASELINE.json config 3: TPE over ResNet-20,
+trial-parallel over 8 GPUs with the RCCL metric all-gather).
+
+Architecture (He et al. 2016, CIFAR variant): 3x3 conv 16 -> 3 stages x 3 basic blocks (16, 32,
+64 channels; stride 2 at stages 2 and 3 with the parameter-free "option A" shortcut: subsample +
+zero-pad channels) -> global average pool -> linear 64 -> 10; ~0.27M parameters per trial.
+Activations are NHWC bf16 with the population folded into the batch; images carry 8 channels
+(3 real + 5 zero) so every kernel moves 16-byte vectors.  Convolutions: HIP im2col/col2im +
+population-batched GEMMs; BatchNorm (+ residual + ReLU) fused HIP kernels with per-trial batch
+and running statistics; SGD-momentum with per-trial lr / momentum / weight decay (fused K5).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from ..ops import conv as cops
+from ..ops.population import MemberConfig
+from .flatpop import FlatPopulation
+
+IN_CH = 8          # 3 image channels + 5 zero channels
+STAGES = (16, 32, 64)
+NCLS = 10
+NCLS_PAD = 16      # head width padded to a multiple of 8 (only the first 10 logits are used)
+
+
+def resnet20_layout(blocks_per_stage: int = 3):
+    """[(conv name, cin, cout, stride)] in forward order (BN after each conv)."""
+    convs = [("conv0", IN_CH, STAGES[0], 1)]
+    cin = STAGES[0]
+    for si, cout in enumerate(STAGES):
+        for b in range(blocks_per_stage):
+            stride = 2 if (si > 0 and b == 0) else 1
+            convs.append((f"s{si}b{b}c1", cin, cout, stride))
+            convs.append((f"s{si}b{b}c2", cout, cout, 1))
+            cin = cout
+    return convs
+
+
+class PopulationResNet(FlatPopulation):
+    optimizer = "sgd"
+    secondary = "acc"
+
+    def __init__(self, capacity: int, batch_size: int = 128, device="cuda",
+                 blocks_per_stage: int = 3, image_size: int = 32):
+        self.batch_size = int(batch_size)
+        self.blocks = int(blocks_per_stage)
+        self.image_size = int(image_size)
+        self.layout = resnet20_layout(self.blocks)
+        super().__init__(capacity, device=device)
+
+    # ------------------------------------------------------------------ structure
+    def param_specs(self):
+        specs = []
+        for name, cin, cout, _ in self.layout:
+            specs.append((f"{name}.w", (9 * cin, cout), ("kaiming", 9 * cin)))
+            specs.append((f"{name}.g", (cout,), ("ones",)))
+            specs.append((f"{name}.b", (cout,), ("zeros",)))
+        specs.append(("fc.w", (STAGES[-1], NCLS_PAD), ("normal", 1.0 / math.sqrt(STAGES[-1]))))
+        specs.append(("fc.b", (NCLS_PAD,), ("zeros",)))
+        return specs
+
+    def aux_specs(self):
+        return [(f"{name}.running", 2 * cout) for name, _, cout, _ in self.layout]
+
+    def init_aux(self, slot: int) -> None:
+        for name, _, cout, _ in self.layout:
+            r = self.A[f"{name}.running"][slot].view(2, cout)
+            r[0].zero_()
+            r[1].fill_(1.0)
+
+    def rows_per_batch(self, x) -> int:
+        return int(x.shape[0])
+
+    # ------------------------------------------------------------------ forward
+    def _bn(self, name, x, train, res=None, relu=True):
+        P = self.capacity
+        C = x.shape[-1]
+        running = self.A[f"{name}.running"].view(P, 2, C)
+        return cops.bn_act(x, self.W[f"{name}.g"], self.W[f"{name}.b"], running, P, train,
+                           res=res, relu=relu)
+
+    @staticmethod
+    def _shortcut(x, cout, stride):
+        if stride == 1 and x.shape[-1] == cout:
+            return x
+        y = x[:, ::stride, ::stride, :]
+        return torch.nn.functional.pad(y, (0, cout - x.shape[-1])).contiguous()
+
+    def _loss(self, x, y, train: bool):
+        P, W = self.capacity, self.W
+        h = self._expand(x, torch.bfloat16).view(-1, *x.shape[1:])     # [P*B, H, W, 8]
+        B = x.shape[0]
+        it = iter(self.layout)
+        name, _, cout, stride = next(it)
+        h = self._bn(name, cops.conv3x3(h, W[f"{name}.w"], P, stride), train)
+        for si in range(len(STAGES)):
+            for b in range(self.blocks):
+                n1, _, c1, s1 = next(it)
+                n2, _, c2, _ = next(it)
+                r = self._shortcut(h, c2, s1)
+                t = self._bn(n1, cops.conv3x3(h, W[f"{n1}.w"], P, s1), train)
+                h = self._bn(n2, cops.conv3x3(t, W[f"{n2}.w"], P, 1), train, res=r)
+        feat = h.view(P, B, -1, h.shape[-1]).float().mean(2)            # [P, B, 64]
+        logits = torch.baddbmm(W["fc.b"].float()[:, None, :], feat,
+                               W["fc.w"].float())[..., :NCLS]           # [P, B, 10]
+        labels = self._expand(y, torch.long)
+        loss = torch.nn.functional.cross_entropy(logits.reshape(-1, NCLS), labels.reshape(-1),
+                                                 reduction="none").view(P, B).sum(1)
+        correct = (logits.argmax(-1) == labels).float().sum(1)
+        if train:
+            loss = _GradScale.apply(loss, 1.0 / B)
+        return loss, correct
+
+
+class _GradScale(torch.autograd.Function):
+    """Identity forward, scales the gradient (loss SUMS are reported, mean-loss gradients used)."""
+
+    @staticmethod
+    def forward(ctx, x, s):
+        ctx.s = s
+        return x.clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g * ctx.s, None
+
+
+class SyntheticCIFAR:
+    """CIFAR-shaped synthetic classification: N(0, 1) 32x32x3 images (NHWC, padded to 8
+    channels, bf16) labelled by a fixed random two-layer teacher on 4x4-pooled pixels."""
+
+    def __init__(self, n_train: int = 50048, n_val: int = 1024, batch_size: int = 128,
+                 seed: int = 0, device=None, image_size: int = 32):
+        g = torch.Generator().manual_seed(seed)
+        S = image_size
+        w1 = torch.randn(3 * (S // 4) ** 2, 256, generator=g) / math.sqrt(3 * (S // 4) ** 2)
+        w2 = torch.randn(256, NCLS, generator=g) / 16.0
+        dev = torch.device(device) if device is not None else torch.device("cpu")
+
+        def draw(n):
+            x = torch.randn(n, S, S, 3, generator=g)
+            pooled = x.view(n, S // 4, 4, S // 4, 4, 3).mean((2, 4)).reshape(n, -1)
+            y = (torch.tanh(pooled @ w1 * 4) @ w2).argmax(1)
+            xp = torch.zeros(n, S, S, IN_CH)
+            xp[..., :3] = x
+            return xp.to(torch.bfloat16).to(dev), y.to(dev)
+
+        self.batch_size = batch_size
+        n_train = n_train // batch_size * batch_size
+        self.train_x, self.train_y = draw(n_train)
+        self.val_x, self.val_y = draw(n_val)
+        self.n_batches = n_train // batch_size
+
+    def batch(self, step: int):
+        i = step % self.n_batches
+        sl = slice(i * self.batch_size, (i + 1) * self.batch_size)
+        return self.train_x[sl], self.train_y[sl]
+
+    def validation(self):
+        return self.val_x, self.val_y
+
+
+RESNET_TPE_PRIORS = {
+    "/lr": "loguniform(0.01, 0.5)",
+    "/momentum": "uniform(0.5, 0.99)",
+    "/weight_decay": "loguniform(1e-5, 1e-2)",
+}
+
+
+@dataclass
+class ResNetSweepTask:
+    """Trial parameters -> ResNet population members (SGD lr / momentum / weight decay); trials
+    train a fixed budget of ``steps`` unless the space has a fidelity dimension."""
+
+    priors: Dict[str, str] = field(default_factory=lambda: dict(RESNET_TPE_PRIORS))
+    fidelity: str = "/steps"
+    steps: int = 390
+    secondary_stat: str = "val_acc"
+
+    def member_config(self, params: Dict, seed: int) -> MemberConfig:
+        return MemberConfig(width=0, lr=float(params["/lr"]),
+                            momentum=float(params.get("/momentum", 0.9)),
+                            weight_decay=float(params.get("/weight_decay", 5e-4)),
+                            seed=int(seed) & 0x7FFFFFFF)
+
+    def budget(self, params: Dict) -> int:
+        return int(params.get(self.fidelity, self.steps))
+
+    def key(self, params: Dict) -> str:
+        from .mlp import param_key
+        return param_key(params, self.fidelity)
+
+    @staticmethod
+    def seed_of(key: str) -> int:
+        return int(key[:8], 16)

@@ -1,0 +1,302 @@
+// Convolution data movement and fused BatchNorm(+residual)(+ReLU) for the population ResNet
+// (north-star kernels K3 / K8).  Activations are NHWC bf16 with a leading population dimension
+// folded into N: x[(p * B + n)][h][w][c]; C is a multiple of 8 so every lane moves 16 bytes.
+//
+//   im2col      x -> col[(n, oh, ow)][(kh, kw, c)]  (3x3, pad 1, stride 1 or 2, zero padding)
+//               so the convolution is a population-batched GEMM col[P, M, 9C] . W[P, 9C, Cout]
+//   col2im      dcol -> dx, in GATHER form (each input pixel sums its <= 9 taps): no atomics
+//   bn_stats    per (trial, channel) sum / sum of squares over the trial's N*H*W rows
+//   bn_finalize mean / rstd per (trial, channel), running-statistics update (momentum, unbiased)
+//   bn_apply    y = relu?(gamma (x - mean) rstd + beta + residual?)
+//   bn_bwd_*    dz = dy * relu'(y); sums of dz and dz * xhat; dx, dgamma, dbeta, dresidual
+#include "common.h"
+
+using namespace mopt;
+
+namespace {
+
+__device__ __forceinline__ void unpack8(const uint4& u, float (&f)[8]) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    f[2 * e] = bf2f(w[e] & 0xFFFF);
+    f[2 * e + 1] = bf2f(w[e] >> 16);
+  }
+}
+
+__device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
+  return make_uint4(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]),
+                    pack2bf(f[6], f[7]));
+}
+
+// thread = (output pixel, tap, 8-channel chunk)
+__global__ __launch_bounds__(256) void im2col_kernel(const bf16_t* __restrict__ x,
+                                                     bf16_t* __restrict__ col, int N, int H,
+                                                     int W, int C, int OH, int OW, int stride) {
+  const int cc = C >> 3;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = (int64_t)N * OH * OW * 9 * cc;
+  if (i >= total) return;
+  const int ch = i % cc;
+  int64_t r = i / cc;
+  const int tap = r % 9;
+  r /= 9;                          // output pixel index (n, oh, ow)
+  const int ow = r % OW, oh = (r / OW) % OH;
+  const int64_t n = r / ((int64_t)OW * OH);
+  const int ih = oh * stride + tap / 3 - 1, iw = ow * stride + tap % 3 - 1;
+  uint4 v = make_uint4(0, 0, 0, 0);
+  if (ih >= 0 && ih < H && iw >= 0 && iw < W)
+    v = *(const uint4*)(x + (((n * H + ih) * W + iw) * C + 8 * ch));
+  *(uint4*)(col + (r * 9 + tap) * C + 8 * ch) = v;
+}
+
+// thread = (input pixel, 8-channel chunk): dx = sum over the taps that read this pixel
+__global__ __launch_bounds__(256) void col2im_kernel(const bf16_t* __restrict__ dcol,
+                                                     bf16_t* __restrict__ dx, int N, int H, int W,
+                                                     int C, int OH, int OW, int stride) {
+  const int cc = C >> 3;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = (int64_t)N * H * W * cc;
+  if (i >= total) return;
+  const int ch = i % cc;
+  int64_t r = i / cc;
+  const int iw = r % W, ih = (r / W) % H;
+  const int64_t n = r / ((int64_t)W * H);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kh = 0; kh < 3; ++kh) {
+    const int t = ih + 1 - kh;
+    if (t < 0 || t % stride) continue;
+    const int oh = t / stride;
+    if (oh >= OH) continue;
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const int u = iw + 1 - kw;
+      if (u < 0 || u % stride) continue;
+      const int ow = u / stride;
+      if (ow >= OW) continue;
+      float v[8];
+      unpack8(*(const uint4*)(dcol + ((((n * OH + oh) * OW + ow) * 9 + kh * 3 + kw) * C + 8 * ch)),
+              v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += v[e];
+    }
+  }
+  *(uint4*)(dx + r * C + 8 * ch) = pack8(acc);
+}
+
+// grid (row chunks, P); thread = (row group, channel); C divides 256.
+__global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict__ x,
+                                                       float* __restrict__ sums, int64_t M,
+                                                       int C, int rows_per_block) {
+  __shared__ float s1[256], s2[256];
+  const int p = blockIdx.y, c = threadIdx.x % C, rg = threadIdx.x / C, ng = 256 / C;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(r0 + rows_per_block, M);
+  const bf16_t* xp = x + (int64_t)p * M * C;
+  float a = 0.f, b = 0.f;
+  for (int64_t r = r0 + rg; r < r1; r += ng) {
+    const float v = bf2f(xp[r * C + c]);
+    a += v;
+    b += v * v;
+  }
+  s1[threadIdx.x] = a;
+  s2[threadIdx.x] = b;
+  __syncthreads();
+  if (rg == 0) {
+    for (int g = 1; g < ng; ++g) {
+      a += s1[g * C + c];
+      b += s2[g * C + c];
+    }
+    atomicAdd(sums + (2 * p) * C + c, a);
+    atomicAdd(sums + (2 * p + 1) * C + c, b);
+  }
+}
+
+// one thread per (trial, channel): mean / rstd (train: batch stats, eval: running stats)
+__global__ void bn_finalize_kernel(const float* __restrict__ sums, float* __restrict__ stat,
+                                   float* __restrict__ running, int P, int C, int64_t M,
+                                   float eps, float momentum, int train) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P * C) return;
+  const int p = i / C, c = i % C;
+  float* rm = running + (int64_t)p * 2 * C;  // [P][2][C]: running mean, running var
+  float mean, var;
+  if (train) {
+    mean = sums[(2 * p) * C + c] / (float)M;
+    var = fmaxf(sums[(2 * p + 1) * C + c] / (float)M - mean * mean, 0.f);
+    rm[c] = (1.f - momentum) * rm[c] + momentum * mean;
+    rm[C + c] = (1.f - momentum) * rm[C + c] + momentum * var * (float)M / (float)max(M - 1, (int64_t)1);
+  } else {
+    mean = rm[c];
+    var = rm[C + c];
+  }
+  stat[(2 * p) * C + c] = mean;
+  stat[(2 * p + 1) * C + c] = rsqrtf(var + eps);
+}
+
+// thread = (row, 8-channel chunk); gamma/beta bf16 [P][C]; stat [P][2][C]
+__global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict__ x,
+                                                       const float* __restrict__ stat,
+                                                       const bf16_t* __restrict__ gamma,
+                                                       const bf16_t* __restrict__ beta,
+                                                       const bf16_t* __restrict__ res,
+                                                       bf16_t* __restrict__ y, int64_t M, int C,
+                                                       int P, int relu) {
+  const int cc = C >> 3;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)P * M * cc) return;
+  const int ch = i % cc;
+  const int64_t row = i / cc;
+  const int p = (int)(row / M);
+  float v[8], g[8], b[8];
+  unpack8(*(const uint4*)(x + row * C + 8 * ch), v);
+  unpack8(*(const uint4*)(gamma + (int64_t)p * C + 8 * ch), g);
+  unpack8(*(const uint4*)(beta + (int64_t)p * C + 8 * ch), b);
+  float rr[8];
+  if (res) unpack8(*(const uint4*)(res + row * C + 8 * ch), rr);
+  const float* mean = stat + (2 * p) * C + 8 * ch;
+  const float* rstd = stat + (2 * p + 1) * C + 8 * ch;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float o = (v[e] - mean[e]) * rstd[e] * g[e] + b[e];
+    if (res) o += rr[e];
+    v[e] = relu ? fmaxf(o, 0.f) : o;
+  }
+  *(uint4*)(y + row * C + 8 * ch) = pack8(v);
+}
+
+// dz = dy * relu'(y); per (p, c): sums[0] += dz, sums[1] += dz * xhat.  grid (row chunks, P).
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __restrict__ x,
+                                                            const bf16_t* __restrict__ y,
+                                                            const bf16_t* __restrict__ dy,
+                                                            const float* __restrict__ stat,
+                                                            float* __restrict__ sums, int64_t M,
+                                                            int C, int rows_per_block, int relu) {
+  __shared__ float s1[256], s2[256];
+  const int p = blockIdx.y, c = threadIdx.x % C, rg = threadIdx.x / C, ng = 256 / C;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(r0 + rows_per_block, M);
+  const int64_t base = (int64_t)p * M * C;
+  const float mean = stat[(2 * p) * C + c], rstd = stat[(2 * p + 1) * C + c];
+  float a = 0.f, b = 0.f;
+  for (int64_t r = r0 + rg; r < r1; r += ng) {
+    const int64_t o = base + r * C + c;
+    float dz = bf2f(dy[o]);
+    if (relu && bf2f(y[o]) <= 0.f) dz = 0.f;
+    a += dz;
+    b += dz * (bf2f(x[o]) - mean) * rstd;
+  }
+  s1[threadIdx.x] = a;
+  s2[threadIdx.x] = b;
+  __syncthreads();
+  if (rg == 0) {
+    for (int g = 1; g < ng; ++g) {
+      a += s1[g * C + c];
+      b += s2[g * C + c];
+    }
+    atomicAdd(sums + (2 * p) * C + c, a);
+    atomicAdd(sums + (2 * p + 1) * C + c, b);
+  }
+}
+
+// dx = gamma rstd (dz - sum(dz)/M - xhat sum(dz xhat)/M);  dres = dz.
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restrict__ x,
+                                                           const bf16_t* __restrict__ y,
+                                                           const bf16_t* __restrict__ dy,
+                                                           const float* __restrict__ stat,
+                                                           const float* __restrict__ sums,
+                                                           const bf16_t* __restrict__ gamma,
+                                                           bf16_t* __restrict__ dx,
+                                                           bf16_t* __restrict__ dres, int64_t M,
+                                                           int C, int P, int relu) {
+  const int cc = C >> 3;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)P * M * cc) return;
+  const int ch = i % cc;
+  const int64_t row = i / cc;
+  const int p = (int)(row / M);
+  float xv[8], yv[8], dv[8], g[8], o[8];
+  unpack8(*(const uint4*)(x + row * C + 8 * ch), xv);
+  unpack8(*(const uint4*)(y + row * C + 8 * ch), yv);
+  unpack8(*(const uint4*)(dy + row * C + 8 * ch), dv);
+  unpack8(*(const uint4*)(gamma + (int64_t)p * C + 8 * ch), g);
+  const float invM = 1.f / (float)M;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int c = 8 * ch + e;
+    const float mean = stat[(2 * p) * C + c], rstd = stat[(2 * p + 1) * C + c];
+    const float sdz = sums[(2 * p) * C + c], sdx = sums[(2 * p + 1) * C + c];
+    const float dz = (relu && yv[e] <= 0.f) ? 0.f : dv[e];
+    const float xh = (xv[e] - mean) * rstd;
+    o[e] = g[e] * rstd * (dz - sdz * invM - xh * sdx * invM);
+    dv[e] = dz;
+  }
+  *(uint4*)(dx + row * C + 8 * ch) = pack8(o);
+  if (dres) *(uint4*)(dres + row * C + 8 * ch) = pack8(dv);
+}
+
+inline dim3 grid1(int64_t n) { return dim3((unsigned)((n + 255) / 256)); }
+
+}  // namespace
+
+extern "C" {
+
+int mopt_im2col(const void* x, void* col, int N, int H, int W, int C, int OH, int OW, int stride,
+                void* stream) {
+  if (C % 8) return 1;
+  const int64_t total = (int64_t)N * OH * OW * 9 * (C / 8);
+  hipLaunchKernelGGL(im2col_kernel, grid1(total), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)x, (bf16_t*)col, N, H, W, C, OH, OW, stride);
+  return (int)hipGetLastError();
+}
+
+int mopt_col2im(const void* dcol, void* dx, int N, int H, int W, int C, int OH, int OW,
+                int stride, void* stream) {
+  if (C % 8) return 1;
+  const int64_t total = (int64_t)N * H * W * (C / 8);
+  hipLaunchKernelGGL(col2im_kernel, grid1(total), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)dcol, (bf16_t*)dx, N, H, W, C, OH, OW, stride);
+  return (int)hipGetLastError();
+}
+
+// x [P][M][C] -> y; stat [P][2][C] (mean, rstd) out; running [P][2][C] in/out; sums scratch.
+int mopt_bn_fwd(const void* x, const void* gamma, const void* beta, const void* res, void* y,
+                void* stat, void* running, void* sums, int P, int64_t M, int C, float eps,
+                float momentum, int train, int relu, void* stream) {
+  if (C % 8 || 256 % C) return 1;
+  hipStream_t st = (hipStream_t)stream;
+  if (train) {
+    (void)hipMemsetAsync(sums, 0, sizeof(float) * 2 * P * C, st);
+    const int rpb = 2048;
+    hipLaunchKernelGGL(bn_stats_kernel, dim3((unsigned)((M + rpb - 1) / rpb), P), dim3(256), 0,
+                       st, (const bf16_t*)x, (float*)sums, M, C, rpb);
+  }
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((P * C + 255) / 256), dim3(256), 0, st,
+                     (const float*)sums, (float*)stat, (float*)running, P, C, M, eps, momentum,
+                     train);
+  hipLaunchKernelGGL(bn_apply_kernel, grid1((int64_t)P * M * (C / 8)), dim3(256), 0, st,
+                     (const bf16_t*)x, (const float*)stat, (const bf16_t*)gamma,
+                     (const bf16_t*)beta, (const bf16_t*)res, (bf16_t*)y, M, C, P, relu);
+  return (int)hipGetLastError();
+}
+
+// sums [P][2][C] out: (sum dz, sum dz * xhat) = (dbeta, dgamma) in f32.
+int mopt_bn_bwd(const void* x, const void* y, const void* dy, const void* stat, const void* gamma,
+                void* dx, void* dres, void* sums, int P, int64_t M, int C, int relu,
+                void* stream) {
+  if (C % 8 || 256 % C) return 1;
+  hipStream_t st = (hipStream_t)stream;
+  (void)hipMemsetAsync(sums, 0, sizeof(float) * 2 * P * C, st);
+  const int rpb = 2048;
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3((unsigned)((M + rpb - 1) / rpb), P), dim3(256),
+                     0, st, (const bf16_t*)x, (const bf16_t*)y, (const bf16_t*)dy,
+                     (const float*)stat, (float*)sums, M, C, rpb, relu);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, grid1((int64_t)P * M * (C / 8)), dim3(256), 0, st,
+                     (const bf16_t*)x, (const bf16_t*)y, (const bf16_t*)dy, (const float*)stat,
+                     (const float*)sums, (const bf16_t*)gamma, (bf16_t*)dx, (bf16_t*)dres, M, C,
+                     P, relu);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -461,6 +461,46 @@ __global__ __launch_bounds__(256) void adamw_multi_kernel(const Segment* __restr
   *(uint4*)(p16 + o) = pack8(we);
 }
 
+// SGD with momentum (PyTorch convention: m = mu m + (g + wd w); w -= lr m), per-trial lr /
+// momentum (LmHP.b1) / wd, optional per-trial grad-norm clipping (north-star kernel K5).
+__global__ __launch_bounds__(256) void sgd_multi_kernel(const Segment* __restrict__ segs,
+                                                        const SegChunk* __restrict__ chunks,
+                                                        const LmHP* __restrict__ hp,
+                                                        const float* __restrict__ sumsq,
+                                                        float* __restrict__ p32,
+                                                        bf16_t* __restrict__ p16,
+                                                        const bf16_t* __restrict__ g16,
+                                                        float* __restrict__ m32) {
+  const SegChunk ch = chunks[blockIdx.x];
+  const Segment sg = segs[ch.seg];
+  const int64_t i = ch.start + 8 * threadIdx.x;
+  const int64_t end = min(ch.start + (int64_t)kAdamChunk, (int64_t)(ch.trial + 1) * sg.numel);
+  if (i >= end) return;
+  const LmHP h = hp[ch.trial];
+  float clip = 1.f;
+  if (h.max_norm > 0.f) {
+    const float nrm = sqrtf(sumsq[ch.trial]);
+    if (nrm > h.max_norm) clip = h.max_norm / (nrm + 1e-6f);
+  }
+  const int64_t o = sg.off + i;
+  float gv[8];
+  unpack8(*(const uint4*)(g16 + o), gv);
+  const f32x4 w0 = *(const f32x4*)(p32 + o), w1 = *(const f32x4*)(p32 + o + 4);
+  const f32x4 m0 = *(const f32x4*)(m32 + o), m1 = *(const f32x4*)(m32 + o + 4);
+  float we[8] = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
+  float me[8] = {m0[0], m0[1], m0[2], m0[3], m1[0], m1[1], m1[2], m1[3]};
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    me[e] = h.b1 * me[e] + gv[e] * clip + h.wd * we[e];
+    we[e] -= h.lr * me[e];
+  }
+  *(f32x4*)(p32 + o) = f32x4{we[0], we[1], we[2], we[3]};
+  *(f32x4*)(p32 + o + 4) = f32x4{we[4], we[5], we[6], we[7]};
+  *(f32x4*)(m32 + o) = f32x4{me[0], me[1], me[2], me[3]};
+  *(f32x4*)(m32 + o + 4) = f32x4{me[4], me[5], me[6], me[7]};
+  *(uint4*)(p16 + o) = pack8(we);
+}
+
 inline dim3 grid1(int64_t n) { return dim3((unsigned)((n + 255) / 256)); }
 
 }  // namespace
@@ -571,6 +611,23 @@ int mopt_adamw_multi(const void* segs, const void* chunks, int n_chunks, const v
   hipLaunchKernelGGL(adamw_multi_kernel, dim3(n_chunks), dim3(256), 0, st, (const Segment*)segs,
                      (const SegChunk*)chunks, (const LmHP*)hp, (const float*)sumsq, (float*)p32,
                      (bf16_t*)p16, (const bf16_t*)g16, (float*)m32, (float*)v32);
+  return (int)hipGetLastError();
+}
+
+int mopt_sgd_multi(const void* segs, const void* chunks, int n_chunks, const void* hp,
+                   void* sumsq, void* p32, void* p16, const void* g16, void* m32, int P, int clip,
+                   void* stream) {
+  if (n_chunks <= 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (clip) {
+    (void)hipMemsetAsync(sumsq, 0, sizeof(float) * P, st);
+    hipLaunchKernelGGL(grad_sumsq_kernel, dim3(n_chunks), dim3(256), 0, st,
+                       (const Segment*)segs, (const SegChunk*)chunks, (const bf16_t*)g16,
+                       (float*)sumsq);
+  }
+  hipLaunchKernelGGL(sgd_multi_kernel, dim3(n_chunks), dim3(256), 0, st, (const Segment*)segs,
+                     (const SegChunk*)chunks, (const LmHP*)hp, (const float*)sumsq, (float*)p32,
+                     (bf16_t*)p16, (const bf16_t*)g16, (float*)m32);
   return (int)hipGetLastError();
 }
 

@@ -39,6 +39,8 @@ _lib.register_signatures({
     "mopt_cast_bf16": ([c_void_p, c_void_p, c_int64, c_void_p], c_int),
     "mopt_adamw_multi": ([c_void_p, c_void_p, c_int] + [c_void_p] * 7 + [c_int, c_int, c_void_p],
                          c_int),
+    "mopt_sgd_multi": ([c_void_p, c_void_p, c_int] + [c_void_p] * 6 + [c_int, c_int, c_void_p],
+                       c_int),
 })
 
 LM_HP_DTYPE = np.dtype([("lr", "<f4"), ("b1", "<f4"), ("b2", "<f4"), ("eps", "<f4"),
@@ -329,16 +331,22 @@ def embedding(tok, table, rows_per_trial):
 
 
 # ============================================================================ fused AdamW
-class FlatAdamW:
-    """Fused per-trial AdamW over flat parameter buffers (north-star kernel K6).
+class FlatOptimizer:
+    """Fused per-trial optimizer over flat parameter buffers: AdamW (north-star kernel K6) or
+    SGD-momentum (K5), with optional per-trial global-norm gradient clipping.
 
     ``segments``: [(offset, numel_per_trial)] of every parameter tensor inside the flat buffers,
-    each tensor laid out ``[P, numel]``.  State: f32 master weights ``p32``, ``m``, ``v``; the
-    bf16 working copy ``p16`` is rewritten by the same kernel; ``g16`` is the flat bf16 gradient.
-    Hyper-parameters are per trial (``hp`` structured array, :data:`LM_HP_DTYPE`).
+    each tensor laid out ``[P, numel]``.  State: f32 master weights ``p32``, ``m`` (and ``v`` for
+    AdamW); the bf16 working copy ``p16`` is rewritten by the same kernel; ``g16`` is the flat bf16
+    gradient.  Hyper-parameters are per trial (``hp`` structured array, :data:`LM_HP_DTYPE`;
+    SGD reads ``lr``, ``b1`` = momentum, ``wd``, ``max_norm``).  Work is listed as chunks of at
+    most 2048 elements of ONE trial, so every lane knows its trial without a division.
     """
 
-    def __init__(self, segments: List[Tuple[int, int]], P: int, device):
+    def __init__(self, segments: List[Tuple[int, int]], P: int, device, kind: str = "adamw"):
+        if kind not in ("adamw", "sgd"):
+            raise ValueError(f"unknown optimizer {kind}")
+        self.kind = kind
         self.P = P
         self.device = torch.device(device)
         segs = np.array(segments, dtype=SEG_DTYPE)
@@ -361,30 +369,64 @@ class FlatAdamW:
         clip = int(bool((hp["max_norm"] > 0).any()))
         if self.device.type == "cuda":
             hp_dev = torch.from_numpy(hp.view(np.uint8).copy()).to(self.device, non_blocking=True)
-            _call("mopt_adamw_multi", _p(self._segs), _p(self._chunks), self.n_chunks, _p(hp_dev),
-                  _p(self._sumsq), _p(p32), _p(p16), _p(g16), _p(m), _p(v), self.P, clip,
-                  _lib.stream_ptr(self.device))
+            if self.kind == "adamw":
+                _call("mopt_adamw_multi", _p(self._segs), _p(self._chunks), self.n_chunks,
+                      _p(hp_dev), _p(self._sumsq), _p(p32), _p(p16), _p(g16), _p(m), _p(v),
+                      self.P, clip, _lib.stream_ptr(self.device))
+            else:
+                _call("mopt_sgd_multi", _p(self._segs), _p(self._chunks), self.n_chunks,
+                      _p(hp_dev), _p(self._sumsq), _p(p32), _p(p16), _p(g16), _p(m), self.P,
+                      clip, _lib.stream_ptr(self.device))
             return
-        adamw_flat_ref(self.segments, self.P, p32, p16, g16, m, v, hp)
+        if self.kind == "adamw":
+            adamw_flat_ref(self.segments, self.P, p32, p16, g16, m, v, hp)
+        else:
+            sgd_flat_ref(self.segments, self.P, p32, p16, g16, m, hp)
+
+
+FlatAdamW = FlatOptimizer
+
+
+def _clip_scales(segments, P, g, hp):
+    sumsq = torch.zeros(P, dtype=torch.float64)
+    for off, numel in segments:
+        sumsq += g[off:off + P * numel].view(P, numel).double().pow(2).sum(1).cpu()
+    scales = []
+    for p in range(P):
+        s = 1.0
+        if hp[p]["max_norm"] > 0:
+            nrm = math.sqrt(float(sumsq[p]))
+            if nrm > hp[p]["max_norm"]:
+                s = float(hp[p]["max_norm"]) / (nrm + 1e-6)
+        scales.append(s)
+    return scales
+
+
+def sgd_flat_ref(segments, P, p32, p16, g16, m, hp):
+    """fp32 reference of the flat SGD-momentum update."""
+    g = g16.float()
+    scales = _clip_scales(segments, P, g, hp)
+    for off, numel in segments:
+        for p in range(P):
+            h = hp[p]
+            lo, hi = off + p * numel, off + (p + 1) * numel
+            d = g[lo:hi] * scales[p] + float(h["wd"]) * p32[lo:hi]
+            m[lo:hi].mul_(float(h["b1"])).add_(d)
+            p32[lo:hi].sub_(float(h["lr"]) * m[lo:hi])
+        sl = slice(off, off + P * numel)
+        p16[sl] = p32[sl].to(p16.dtype)
 
 
 def adamw_flat_ref(segments, P, p32, p16, g16, m, v, hp):
-    """fp32 reference of :class:`FlatAdamW` (same clipping and bias correction)."""
+    """fp32 reference of the flat AdamW update (same clipping and bias correction)."""
     g = g16.float()
-    sumsq = torch.zeros(P, dtype=torch.float64)
-    for off, numel in segments:
-        gs = g[off:off + P * numel].view(P, numel)
-        sumsq += gs.double().pow(2).sum(1).cpu()
+    scales = _clip_scales(segments, P, g, hp)
     for off, numel in segments:
         sl = slice(off, off + P * numel)
         for p in range(P):
             h = hp[p]
             lo, hi = off + p * numel, off + (p + 1) * numel
-            gr = g[lo:hi]
-            if h["max_norm"] > 0:
-                nrm = math.sqrt(float(sumsq[p]))
-                if nrm > h["max_norm"]:
-                    gr = gr * (float(h["max_norm"]) / (nrm + 1e-6))
+            gr = g[lo:hi] * scales[p]
             t = float(h["t"])
             bc1, bc2 = 1 - float(h["b1"]) ** t, 1 - float(h["b2"]) ** t
             w = p32[lo:hi]

@@ -473,8 +473,8 @@ class PopulationSweep:
 
     def _compute_mb(self):
         from ..space.builder import build_space
-        dim = build_space(self.task.priors)[self.task.fidelity]
-        self._mb = int(dim.high)
+        space = build_space(self.task.priors)
+        self._mb = int(space[self.task.fidelity].high) if self.task.fidelity in space else 0
         return self._mb
 
     # ------------------------------------------------------------------ reporting

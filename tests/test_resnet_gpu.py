@@ -1,0 +1,87 @@
+"""Numerics of the conv / BatchNorm HIP kernels (K3, K8) and the population ResNet on gfx950."""
+import numpy as np
+import pytest
+import torch
+
+from metaopt_amd.ops import conv as cops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _close(a, b, tol):
+    a, b = a.float(), b.float()
+    err = (a - b).abs().max().item()
+    assert err <= tol * (b.abs().max().item() + 1e-6), err
+
+
+@pytest.mark.parametrize("stride,C,Cout", [(1, 16, 16), (2, 16, 32), (1, 8, 16), (2, 32, 64)])
+def test_conv3x3_fwd_bwd(stride, C, Cout):
+    torch.manual_seed(0)
+    P, B, H = 3, 4, 16
+    x = torch.randn(P * B, H, H, C, device=DEV).to(torch.bfloat16).requires_grad_(True)
+    w = (0.1 * torch.randn(P, 9 * C, Cout, device=DEV)).to(torch.bfloat16).requires_grad_(True)
+    out = cops.conv3x3(x, w, P, stride)
+    g = torch.randn_like(out)
+    out.backward(g)
+    xr, wr = x.detach().float().requires_grad_(True), w.detach().float().requires_grad_(True)
+    ref = cops.conv3x3_ref(xr, wr, P, stride)
+    ref.backward(g.float())
+    _close(out, ref, 2e-2)
+    _close(x.grad, xr.grad, 2e-2)
+    _close(w.grad, wr.grad, 2e-2)
+
+
+@pytest.mark.parametrize("relu,res", [(True, False), (True, True), (False, False)])
+def test_bn_act_train_and_eval(relu, res):
+    torch.manual_seed(1)
+    P, B, H, C = 2, 8, 8, 32
+    x = (2 * torch.randn(P * B, H, H, C, device=DEV) + 0.5).to(torch.bfloat16).requires_grad_(True)
+    gamma = (1 + 0.1 * torch.randn(P, C, device=DEV)).to(torch.bfloat16).requires_grad_(True)
+    beta = (0.1 * torch.randn(P, C, device=DEV)).to(torch.bfloat16).requires_grad_(True)
+    r = torch.randn(P * B, H, H, C, device=DEV).to(torch.bfloat16).requires_grad_(True) if res else None
+    run_h = torch.stack([torch.zeros(P, C), torch.ones(P, C)], 1).to(DEV).contiguous()
+    run_r = run_h.clone().cpu()
+    y = cops.bn_act(x, gamma, beta, run_h, P, True, res=r, relu=relu)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    leaves = [x.detach().float().cpu().requires_grad_(True),
+              gamma.detach().float().cpu().requires_grad_(True),
+              beta.detach().float().cpu().requires_grad_(True)]
+    rr = r.detach().float().cpu().requires_grad_(True) if res else None
+    yr = cops.bn_act_ref(*leaves, run_r, P, True, res=rr, relu=relu)
+    yr.backward(dy.float().cpu())
+    _close(y.cpu(), yr, 3e-2)
+    for a, b in zip((x.grad, gamma.grad, beta.grad), [t.grad for t in leaves]):
+        _close(a.cpu(), b, 3e-2)
+    if res:
+        _close(r.grad.cpu(), rr.grad, 3e-2)
+    torch.testing.assert_close(run_h.cpu(), run_r, rtol=1e-3, atol=1e-3)
+    with torch.no_grad():
+        ye = cops.bn_act(x, gamma, beta, run_h, P, False, res=r, relu=relu)
+        yre = cops.bn_act_ref(*[t.detach() for t in leaves], run_r, P, False,
+                              res=None if rr is None else rr.detach(), relu=relu)
+    _close(ye.cpu(), yre, 3e-2)
+
+
+def test_population_resnet_step_matches_cpu():
+    from metaopt_amd.models.resnet import PopulationResNet, SyntheticCIFAR
+    from metaopt_amd.ops.population import MemberConfig
+    pops = []
+    for dev in (DEV, "cpu"):
+        pop = PopulationResNet(2, batch_size=16, device=dev, blocks_per_stage=1, image_size=16)
+        for s in range(2):
+            pop.set_member(s, MemberConfig(width=0, lr=0.05 * (s + 1), momentum=0.9, seed=s))
+        pops.append(pop)
+    with torch.no_grad():
+        pops[1].p32.copy_(pops[0].p32.cpu())
+        pops[1].p16.copy_(pops[0].p16.cpu())
+    data = SyntheticCIFAR(n_train=16 * 8, n_val=32, batch_size=16, image_size=16)
+    losses = [[], []]
+    for step in range(4):
+        x, y = data.batch(step)
+        for i, pop in enumerate(pops):
+            pop.train_step(x.to(pop.device), y.to(pop.device))
+            losses[i].append(pop.train_loss())
+    a, b = np.array(losses[0]), np.array(losses[1])
+    assert np.allclose(a, b, rtol=3e-2, atol=3e-2), (a, b)
