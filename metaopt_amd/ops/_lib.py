@@ -13,6 +13,7 @@ import ctypes
 import os
 import threading
 
+import numpy as np
 import torch  # noqa: F401  (must be imported before the HIP library is dlopen'ed)
 
 from . import build as _build
@@ -96,6 +97,31 @@ def check(err: int, what: str) -> None:
 
 def stream_ptr(device=None) -> int:
     return torch.cuda.current_stream(device).cuda_stream
+
+
+def upload(data, device, dtype=None) -> torch.Tensor:
+    """Host -> device copy that does NOT stall the host on the queued GPU work.
+
+    A copy from pageable host memory makes the runtime wait for the stream to drain first, which
+    during a sweep means waiting for every kernel already queued (tens of ms).  The bytes are
+    staged in pinned memory from torch's caching host allocator (which keeps the block alive
+    until the asynchronous copy has run) and copied with ``non_blocking=True``.
+    """
+    t = data if isinstance(data, torch.Tensor) else torch.from_numpy(
+        np.ascontiguousarray(data))
+    if dtype is not None:
+        t = t.to(dtype)
+    device = torch.device(device)
+    if device.type != "cuda":
+        return t.to(device)
+    staged = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    staged.copy_(t)
+    return staged.to(device, non_blocking=True)
+
+
+def upload_bytes(arr, device) -> torch.Tensor:
+    """``upload`` of a numpy structured array as raw bytes."""
+    return upload(np.ascontiguousarray(arr).view(np.uint8), device)
 
 
 def available() -> bool:

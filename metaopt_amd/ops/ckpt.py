@@ -53,8 +53,8 @@ def multi_copy(items: Iterable[Tuple[torch.Tensor, torch.Tensor, Optional[torch.
     chunks["desc"] = np.repeat(np.arange(len(items), dtype=np.int32), counts)
     first = np.concatenate([[0], np.cumsum(counts)[:-1]])
     chunks["start"] = (np.arange(len(chunks)) - np.repeat(first, counts)) * CHUNK
-    d = torch.from_numpy(descs.view(np.uint8).copy()).to(dev, non_blocking=True)
-    c = torch.from_numpy(chunks.view(np.uint8).copy()).to(dev, non_blocking=True)
+    d = _lib.upload_bytes(descs, dev)
+    c = _lib.upload_bytes(chunks, dev)
     lib = _lib.get_lib()
     _lib.check(lib.mopt_multi_copy(d.data_ptr(), c.data_ptr(), len(chunks),
                                    _lib.stream_ptr(dev)), "multi_copy")

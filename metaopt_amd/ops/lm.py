@@ -361,14 +361,14 @@ class FlatOptimizer:
         self.segments = segments
         self.n_chunks = len(chunks)
         if self.device.type == "cuda":
-            self._segs = torch.from_numpy(segs.view(np.uint8).copy()).to(self.device)
-            self._chunks = torch.from_numpy(chunks.view(np.uint8).copy()).to(self.device)
+            self._segs = _lib.upload_bytes(segs, self.device)
+            self._chunks = _lib.upload_bytes(chunks, self.device)
             self._sumsq = torch.zeros(P, dtype=torch.float32, device=self.device)
 
     def step(self, p32, p16, g16, m, v, hp: np.ndarray):
         clip = int(bool((hp["max_norm"] > 0).any()))
         if self.device.type == "cuda":
-            hp_dev = torch.from_numpy(hp.view(np.uint8).copy()).to(self.device, non_blocking=True)
+            hp_dev = _lib.upload_bytes(hp, self.device)
             if self.kind == "adamw":
                 _call("mopt_adamw_multi", _p(self._segs), _p(self._chunks), self.n_chunks,
                       _p(hp_dev), _p(self._sumsq), _p(p32), _p(p16), _p(g16), _p(m), _p(v),

@@ -215,8 +215,8 @@ class PopulationMLP:
                          cfg.seed & 0xFFFFFFFF, t)
 
     def _upload_hp(self) -> None:
-        host = torch.from_numpy(self.hp.view(np.uint8).copy())
-        self.hp_dev.copy_(host, non_blocking=False)
+        from ._lib import upload_bytes
+        self.hp_dev.copy_(upload_bytes(self.hp, self.device))
 
     def set_member(self, slot: int, cfg: MemberConfig, init: bool = True) -> None:
         """Place ``cfg`` in ``slot``; with ``init`` draw fresh weights (torch.nn.Linear-style
@@ -279,7 +279,8 @@ class PopulationMLP:
         descs = self._init_descs(slots)
         if self.backend == "hip":
             from ._lib import check, stream_ptr
-            d = torch.from_numpy(descs.view(np.uint8).copy()).to(self.device)
+            from ._lib import upload_bytes
+            d = upload_bytes(descs, self.device)
             check(self._lib.mopt_mlp_init(d.data_ptr(), len(descs), self.p32.data_ptr(),
                                           self.p16.data_ptr(), self.m32.data_ptr(),
                                           self.v32.data_ptr(), int(self.optimizer == "adamw"),
@@ -480,9 +481,10 @@ class PopulationMLP:
             bwd = [np.zeros((0, 2), np.int32) for _ in range(L)]
         out = {"tl_np": tl, "rows": rows, "fwd_np": fwd, "bwd_np": bwd}
         if self.device.type == "cuda":
-            out["tl"] = torch.from_numpy(tl.view(np.uint8).copy()).to(self.device)
-            out["fwd"] = [torch.from_numpy(np.ascontiguousarray(w)).to(self.device) for w in fwd]
-            out["bwd"] = [torch.from_numpy(np.ascontiguousarray(w)).to(self.device) for w in bwd]
+            from ._lib import upload, upload_bytes
+            out["tl"] = upload_bytes(tl, self.device)
+            out["fwd"] = [upload(w, self.device) for w in fwd]
+            out["bwd"] = [upload(w, self.device) for w in bwd]
         out["n_fwd"] = [len(w) for w in fwd]
         out["n_bwd"] = [len(w) for w in bwd]
         return out
@@ -495,7 +497,8 @@ class PopulationMLP:
         if self.device.type == "cuda":
             self._upload_hp()
         self._active_np = np.array([m is not None for m in self.members])
-        self._active_t = torch.from_numpy(self._active_np.astype(np.int32)).to(self.device)
+        from ._lib import upload
+        self._active_t = upload(self._active_np.astype(np.int32), self.device)
         self._any_dropout = any(m is not None and m.dropout > 0 for m in self.members)
         if self.backend == "hip":
             tb = self._tables["train"]
@@ -690,7 +693,8 @@ class PopulationMLP:
         keep[list(subset)] = True
         out = dict(tb)
         fwd = [w[keep[w[:, 0] // L]] for w in tb["fwd_np"]]
-        out["fwd"] = [torch.from_numpy(np.ascontiguousarray(w)).to(self.device) for w in fwd]
+        from ._lib import upload
+        out["fwd"] = [upload(w, self.device) for w in fwd]
         out["n_fwd"] = [len(w) for w in fwd]
         return out
 
