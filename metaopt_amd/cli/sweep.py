@@ -16,17 +16,22 @@ from .base import get_basic_args_group
 
 log = logging.getLogger(__name__)
 
-ALGOS = {"asha": lambda seed: {"asha": {"seed": seed, "repetitions": float("inf")}},
-         "random": lambda seed: {"random": {"seed": seed}},
-         "tpe": lambda seed: {"tpe": {"seed": seed}}}
+ALGOS = {"asha": lambda seed, n: {"asha": {"seed": seed, "repetitions": float("inf")}},
+         "random": lambda seed, n: {"random": {"seed": seed}},
+         "tpe": lambda seed, n: {"tpe": {"seed": seed, "n_initial_points": n}},
+         "pbt": lambda seed, n: {"pbt": {"seed": seed, "population_size": n}},
+         "hyperband": lambda seed, n: {"hyperband": {"seed": seed}},
+         "gridsearch": lambda seed, n: {"gridsearch": {"n_values": 4}}}
 
 
 def add_subparser(parser):
+    from ..worker.tasks import TASKS
     p = parser.add_parser("sweep", help="Device population sweep (trials trained on GPU).")
     g = get_basic_args_group(p)
-    g.add_argument("--task", default="mlp", choices=["mlp", "logreg"])
-    g.add_argument("--algo", default="asha", choices=sorted(ALGOS))
-    g.add_argument("--population", type=int, default=256, help="trials per GPU")
+    g.add_argument("--task", default="mlp", choices=sorted(TASKS))
+    g.add_argument("--algo", default=None, choices=sorted(ALGOS),
+                   help="search algorithm (default: the task's)")
+    g.add_argument("--population", type=int, default=None, help="trials per GPU")
     g.add_argument("--max-trials", type=int, default=None)
     g.add_argument("--steps", type=int, default=100000, help="max population steps")
     g.add_argument("--sync-every", type=int, default=32)
@@ -35,39 +40,34 @@ def add_subparser(parser):
     return p
 
 
+DEFAULT_POPULATION = {"logreg": 64, "mlp": 256, "resnet20": 32, "lm-125m": 8, "lm-tiny": 16}
+
+
 def main(args):
-    import torch
-    from ..io.experiment_builder import build_experiment, ExperimentBuilder
-    from ..models.data import TeacherClassification
-    from ..models.mlp import LOGREG_PRIORS, MLP_PRIORS, MLPSweepTask
-    from ..ops.population import PopulationMLP
+    from ..io.experiment_builder import ExperimentBuilder, build_experiment
     from ..parallel.comm import init_from_env, shutdown
     from ..worker.population_sweep import PopulationSweep
+    from ..worker.tasks import get
 
     comm = init_from_env()
-    logreg = args["task"] == "logreg"
-    priors = dict(LOGREG_PRIORS if logreg else MLP_PRIORS)
-    task = MLPSweepTask(priors=priors, n_hidden=0 if logreg else 3,
-                        in_features=2 if logreg else 784, num_classes=2 if logreg else 10)
+    spec = get(args["task"])
+    P = args["population"] or DEFAULT_POPULATION.get(args["task"], 64)
+    algo = (ALGOS[args["algo"]](args["seed"], P * comm.world_size) if args["algo"]
+            else spec.algorithm(args["seed"], P * comm.world_size))
+    task, pop, data = spec.build(P, comm.device, args["seed"])
     experiment = None
     if comm.is_root:
         builder = ExperimentBuilder()
         builder.setup_storage({"debug": args.get("debug"), "database": {}})
-        experiment = build_experiment(args["name"] or f"sweep-{args['task']}", priors=priors,
-                                      algorithms=ALGOS[args["algo"]](args["seed"]),
+        experiment = build_experiment(args["name"] or f"sweep-{args['task']}",
+                                      priors=dict(task.priors), algorithms=algo,
                                       max_trials=args["max_trials"] or float("inf"),
-                                      pool_size=args["population"] * comm.world_size)
-    data = TeacherClassification(n_train=60032 if not logreg else 8192, n_val=1024,
-                                 in_features=task.in_features, num_classes=task.num_classes,
-                                 teacher_hidden=128 if not logreg else 4, seed=args["seed"],
-                                 device=comm.device)
-    pop = PopulationMLP(args["population"], in_features=task.in_features,
-                        num_classes=task.num_classes, n_hidden=task.n_hidden,
-                        max_width=task.max_width if not logreg else 64, eval_batch=1024,
-                        device=comm.device)
+                                      pool_size=P * comm.world_size)
     sweep = PopulationSweep(pop, task, data, comm=comm, experiment=experiment,
-                            sync_every=args["sync_every"])
+                            sync_every=args["sync_every"],
+                            ckpt_capacity=max(4, int(spec.ckpt_factor * P)))
     summary = sweep.run(args["steps"])
+    sweep.close()
     if comm.is_root:
         print(json.dumps({k: v for k, v in summary.items()}, default=str))
     shutdown()

@@ -1,0 +1,109 @@
+"""Named device-population tasks: what ``mopt sweep`` and ``scripts/bench_configs.py`` train.
+
+Each entry builds, for one rank, the trial->member mapping (task), the device population and
+the synthetic dataset of a BASELINE.json configuration:
+
+=========  ===============================================================  =======================
+name       model / data                                                      default algorithm
+=========  ===============================================================  =======================
+logreg     logistic regression, 2-D synthetic 2-class data (config 1)        random
+mlp        4-layer MLP 784-w-w-w-10, MNIST-shaped teacher data (config 2)    asha
+resnet20   ResNet-20, CIFAR-shaped teacher data (config 3)                   tpe
+lm-125m    Llama-style 125M LM, synthetic bigram tokens (config 5)          pbt
+lm-tiny    2-layer LM (d 256), same data (config 4's model)                  pbt
+=========  ===============================================================  =======================
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, Dict
+
+
+@dataclass
+class TaskSpec:
+    priors: Dict[str, str]
+    algorithm: Callable[[int, int], dict]     # (seed, population) -> algorithm config
+    build: Callable                            # (population, device, seed, **kw) -> (task, pop, data)
+    samples_per_trial: int                     # throughput unit (samples of one "trial")
+    unit: str
+    ckpt_factor: float = 4.0                   # checkpoint pool = factor x population
+
+
+def _mlp(population, device, seed, logreg=False, **kw):
+    from ..models.data import TeacherClassification
+    from ..models.mlp import LOGREG_PRIORS, MLP_PRIORS, MLPSweepTask
+    from ..ops.population import PopulationMLP
+    priors = dict(LOGREG_PRIORS if logreg else MLP_PRIORS)
+    task = MLPSweepTask(priors=priors, n_hidden=0 if logreg else 3,
+                        in_features=2 if logreg else 784, num_classes=2 if logreg else 10,
+                        width=64 if logreg else 256)
+    data = TeacherClassification(n_train=8192 if logreg else 60032, n_val=1024,
+                                 in_features=task.in_features, num_classes=task.num_classes,
+                                 teacher_hidden=4 if logreg else 128, seed=1234 + seed,
+                                 device=device)
+    pop = PopulationMLP(population, in_features=task.in_features, num_classes=task.num_classes,
+                        n_hidden=task.n_hidden, max_width=64 if logreg else task.max_width,
+                        eval_batch=1024, device=device)
+    return task, pop, data
+
+
+def _resnet(population, device, seed, batch_size=128, blocks=3, image_size=32, **kw):
+    from ..models.resnet import PopulationResNet, ResNetSweepTask, SyntheticCIFAR
+    task = ResNetSweepTask(steps=kw.get("steps_per_trial", 390))
+    pop = PopulationResNet(population, batch_size=batch_size, device=device,
+                           blocks_per_stage=blocks, image_size=image_size)
+    data = SyntheticCIFAR(n_train=kw.get("n_train", 50048), n_val=1024, batch_size=batch_size,
+                          seed=seed, device=device, image_size=image_size)
+    return task, pop, data
+
+
+def _lm(population, device, seed, preset="llama-125m", batch_size=8, seq_len=512, **kw):
+    from ..models.llama import PRESETS, LM_PBT_PRIORS, LMSweepTask, PopulationLM, SyntheticLM
+    cfg = PRESETS[preset]
+    task = LMSweepTask(priors=dict(kw.get("priors", LM_PBT_PRIORS)), d_model=cfg.d_model)
+    pop = PopulationLM(population, preset, batch_size=batch_size, seq_len=seq_len,
+                       device=device)
+    data = SyntheticLM(cfg.vocab, seq_len, batch_size, n_tokens=kw.get("n_tokens", 1 << 22),
+                       seed=seed, device=device)
+    return task, pop, data
+
+
+def _pbt(interval):
+    return lambda seed, population: {"pbt": {"seed": seed, "population_size": population,
+                                             "interval": interval,
+                                             "min_forking_population": min(5, population)}}
+
+
+TASKS: Dict[str, TaskSpec] = {
+    "logreg": TaskSpec({"/lr": "loguniform(1e-3, 1.0)", "/weight_decay": "loguniform(1e-6, 1e-1)",
+                        "/steps": "fidelity(64, 256, 2)"},
+                       lambda seed, n: {"random": {"seed": seed}},
+                       lambda p, d, s, **kw: _mlp(p, d, s, logreg=True, **kw), 8192,
+                       "trials/s (1 trial = one pass over 8,192 samples)"),
+    "mlp": TaskSpec({"/lr": "loguniform(1e-3, 1.0)",
+                     "/width": "loguniform(64, 1024, discrete=True)",
+                     "/dropout": "uniform(0, 0.5)", "/steps": "fidelity(32, 2048, 4)"},
+                    lambda seed, n: {"asha": {"seed": seed, "repetitions": float("inf")}},
+                    _mlp, 60032, "trials/s (1 trial = 60,032 samples)"),
+    "resnet20": TaskSpec({"/lr": "loguniform(0.01, 0.5)", "/momentum": "uniform(0.5, 0.99)",
+                          "/weight_decay": "loguniform(1e-5, 1e-2)"},
+                         lambda seed, n: {"tpe": {"seed": seed, "n_initial_points": n}},
+                         _resnet, 50048, "trials/s (1 trial = one CIFAR-sized epoch, 50,048 "
+                                         "images)"),
+    "lm-125m": TaskSpec({"/lr": "loguniform(1e-4, 3e-3)",
+                         "/weight_decay": "loguniform(1e-3, 0.3)", "/beta1": "uniform(0.8, 0.95)",
+                         "/steps": "fidelity(200, 2000, 2)"},
+                        _pbt(200), _lm, 8 * 512, "tokens/s", ckpt_factor=2.0),
+    "lm-tiny": TaskSpec({"/lr": "loguniform(1e-4, 3e-3)",
+                         "/weight_decay": "loguniform(1e-3, 0.3)", "/beta1": "uniform(0.8, 0.95)",
+                         "/steps": "fidelity(200, 2000, 2)"},
+                        _pbt(200), lambda p, d, s, **kw: _lm(p, d, s, preset="tiny-2layer",
+                                                             seq_len=256, **kw),
+                        8 * 256, "tokens/s", ckpt_factor=2.0),
+}
+
+
+def get(name: str) -> TaskSpec:
+    if name not in TASKS:
+        raise KeyError(f"unknown task {name!r}; choose from {sorted(TASKS)}")
+    return TASKS[name]

@@ -1,0 +1,145 @@
+#!/usr/bin/env python
+"""Throughput of the other BASELINE.json configurations (bench.py is the headline config 2).
+
+    python scripts/bench_configs.py --config resnet20 --steps 40 --warmup 10
+    python scripts/bench_configs.py --config lm-125m --population 8 --steps 20
+    python scripts/bench_configs.py --config hyper --steps 3
+    torchrun --nproc-per-node N scripts/bench_configs.py --config resnet20 ...
+
+Each run is a real sweep: the task's search algorithm (TPE / PBT / random) on rank 0, device
+populations on every rank, C1/C5 collectives every ``--sync-every`` steps (config 4: the C2
+hypergradient all-reduce per outer step).  Data is synthetic, weights random-init.  Rank 0 prints
+one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+DEFAULT_POP = {"logreg": 64, "mlp": 256, "resnet20": 32, "lm-125m": 8, "lm-tiny": 16}
+DEFAULT_SYNC = {"logreg": 32, "mlp": 32, "resnet20": 30, "lm-125m": 50, "lm-tiny": 50}
+
+
+def run_sweep(args, comm):
+    from metaopt_amd.io.experiment_builder import build_experiment
+    from metaopt_amd.storage.database import EphemeralDB
+    from metaopt_amd.storage.protocol import DocumentStorage
+    from metaopt_amd.worker.population_sweep import PopulationSweep
+    from metaopt_amd.worker.tasks import get
+
+    spec = get(args.config)
+    P = args.population or DEFAULT_POP[args.config]
+    sync_every = args.sync_every or DEFAULT_SYNC[args.config]
+    kw = {}
+    if args.config == "resnet20":
+        kw["steps_per_trial"] = 390 // sync_every * sync_every
+    task, pop, data = spec.build(P, comm.device, args.seed, **kw)
+    exp = None
+    if comm.is_root:
+        exp = build_experiment(f"bench-{args.config}", priors=dict(task.priors),
+                               algorithms=spec.algorithm(args.seed, P * comm.world_size),
+                               storage=DocumentStorage(EphemeralDB()),
+                               pool_size=P * comm.world_size)
+    sweep = PopulationSweep(pop, task, data, comm=comm, experiment=exp, sync_every=sync_every,
+                            ckpt_capacity=max(4, int(spec.ckpt_factor * P)))
+    sweep.start()
+    for _ in range(args.warmup):
+        sweep.step()
+    sync(comm)
+    s0, c0 = sweep.samples, sweep.completed
+    sweep.timers.clear()
+    sweep.n_syncs = 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        sweep.step()
+    sweep.flush()
+    sync(comm)
+    elapsed = comm.max_float(time.perf_counter() - t0)
+    samples = torch.tensor([float(sweep.samples - s0)], dtype=torch.float64,
+                           device=comm._coll_device())
+    comm.all_reduce_(samples)
+    samples = float(samples.item())
+    # samples count sequences for the LMs: report tokens too
+    per_sample = getattr(pop, "cfg", None)
+    tokens = samples * per_sample.seq_len if per_sample is not None else None
+    out = {"config": args.config, "n_gpus": comm.world_size, "population_per_gpu": P,
+           "steps": args.steps, "warmup": args.warmup, "sync_every": sync_every,
+           "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+           "samples_per_sec": round(samples / elapsed, 1),
+           "trials_per_sec": round(samples / spec.samples_per_trial / elapsed, 4)
+           if tokens is None else None,
+           "tokens_per_sec": round(tokens / elapsed, 1) if tokens is not None else None,
+           "completed_trials": sweep.completed - c0, "dtype": "bf16",
+           "data": "synthetic",
+           "params_per_trial": pop.n_params if isinstance(getattr(pop, "n_params", None), int)
+           else None,
+           "host_ms_per_sync": {k: round(1e3 * v / max(sweep.n_syncs, 1), 3)
+                                for k, v in sweep.timers.items()}}
+    if comm.is_root:
+        summ = sweep.summary()
+        out["best_val_loss"] = summ["best_val_loss"]
+    sweep.close()
+    return out
+
+
+def run_hyper(args, comm):
+    from metaopt_amd.models.hyper import HypergradientSweep, HypergradLM
+    from metaopt_amd.models.llama import SyntheticLM
+    P = args.population or 8
+    model = HypergradLM(P, "tiny-2layer", batch_size=4, seq_len=128, device=comm.device)
+    data = SyntheticLM(4096, 128, 4, n_tokens=1 << 20, seed=args.seed, device=comm.device)
+    sweep = HypergradientSweep(model, data, comm=comm, inner_steps=args.inner_steps)
+    for _ in range(args.warmup):
+        sweep.step()
+    sync(comm)
+    t0 = time.perf_counter()
+    hist = sweep.run(args.steps)
+    sync(comm)
+    elapsed = comm.max_float(time.perf_counter() - t0)
+    inner = args.steps * args.inner_steps * P * comm.world_size
+    return {"config": "hyper", "n_gpus": comm.world_size, "inner_runs_per_gpu": P,
+            "outer_steps": args.steps, "inner_steps": args.inner_steps,
+            "outer_steps_per_sec": round(args.steps / elapsed, 4),
+            "inner_steps_per_sec": round(inner / elapsed, 2),
+            "tokens_per_sec": round(inner * 4 * 128 / elapsed, 1),
+            "final": hist[-1] if hist else None, "dtype": "fp32 (second-order)",
+            "data": "synthetic"}
+
+
+def sync(comm):
+    if comm.device.type == "cuda":
+        torch.cuda.synchronize()
+    comm.barrier()
+    if comm.device.type == "cuda":
+        torch.cuda.synchronize()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="resnet20",
+                    choices=["logreg", "mlp", "resnet20", "lm-125m", "lm-tiny", "hyper"])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--population", type=int, default=None)
+    ap.add_argument("--steps", type=int, default=60)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--sync-every", type=int, default=None)
+    ap.add_argument("--inner-steps", type=int, default=10)
+    ap.add_argument("--seed", type=int, default=0)
+    args = ap.parse_args()
+    from metaopt_amd.parallel.comm import init_from_env, shutdown
+    comm = init_from_env()
+    out = run_hyper(args, comm) if args.config == "hyper" else run_sweep(args, comm)
+    if comm.is_root:
+        print(json.dumps(out, default=str), flush=True)
+    shutdown()
+
+
+if __name__ == "__main__":
+    main()
