@@ -33,8 +33,11 @@ class FlatPopulation:
     optimizer = "adamw"            # or "sgd"
     secondary = "acc"              # eval_result's second array: "acc" or "ppl"
 
-    def __init__(self, capacity: int, device="cuda", max_grad_norm: float = 0.0):
+    def __init__(self, capacity: int, device="cuda", max_grad_norm: float = 0.0,
+                 use_graph: bool = True):
         self.device = torch.device(device)
+        self.use_graph = bool(use_graph)
+        self._graph = None
         self.backend = "hip" if self.device.type == "cuda" else "torch"
         self.capacity = P = int(capacity)
         self.max_grad_norm = float(max_grad_norm)
@@ -175,9 +178,22 @@ class FlatPopulation:
         return t.unsqueeze(0).expand(self.capacity, *t.shape).contiguous()
 
     def train_step(self, x: torch.Tensor, y: torch.Tensor) -> None:
+        """One optimizer step of every member on the shared batch (x, y).
+
+        On a GPU the whole step -- forward, backward, gradient clipping and the fused optimizer
+        -- is captured once into a HIP graph and replayed (the per-step host cost of autograd
+        and ~100 launches is what bounds small models such as ResNet-20); the per-trial
+        hyper-parameters and step counters reach the graph through a static device buffer.
+        """
         active = np.array([m is not None for m in self.members])
         self.hp["t"][active] += 1
         self.opt_hp["t"] = self.hp["t"]
+        if self.use_graph and self.device.type == "cuda":
+            self._graph_step(x, y)
+            return
+        self._body(x, y, None)
+
+    def _body(self, x, y, hp_dev):
         self.g16.zero_()
         out = self._loss(x, y, train=True)
         loss = out[0] if isinstance(out, tuple) else out
@@ -187,7 +203,39 @@ class FlatPopulation:
         if isinstance(out, tuple):
             self.stats[P:2 * P].copy_(out[1].detach())
         with torch.no_grad():
-            self.opt.step(self.p32, self.p16, self.g16, self.m, self.v, self.opt_hp)
+            self.opt.step(self.p32, self.p16, self.g16, self.m, self.v, self.opt_hp,
+                          hp_dev=hp_dev)
+
+    def _graph_step(self, x, y):
+        from ..ops._lib import upload_bytes
+        if self._graph is None or self._gx.shape != x.shape or self._gy.shape != y.shape:
+            self._capture(x, y)
+        self._gx.copy_(x)
+        self._gy.copy_(y)
+        self._hp_dev.copy_(upload_bytes(self.opt_hp, self.device))
+        self._graph.replay()
+
+    def _capture(self, x, y):
+        from ..ops._lib import upload_bytes
+        self._gx = x.detach().clone()
+        self._gy = y.detach().clone()
+        self._hp_dev = upload_bytes(self.opt_hp, self.device)
+        state = [self.p32, self.p16, self.m, self.v, self.aux, self.stats]
+        backup = [t.clone() for t in state]
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            for _ in range(2):          # warm-up: library handles, allocator pools, autograd
+                self._body(self._gx, self._gy, self._hp_dev)
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        with torch.no_grad():
+            for t, b in zip(state, backup):
+                t.copy_(b)
+        del backup
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            self._body(self._gx, self._gy, self._hp_dev)
+        self._graph = graph
 
     # ------------------------------------------------------------------ evaluation / stats
     @torch.no_grad()

@@ -85,7 +85,7 @@ class PopulationLM(FlatPopulation):
 
     def __init__(self, capacity: int, config="tiny-2layer", batch_size: int = 8,
                  seq_len: Optional[int] = None, device="cuda", max_grad_norm: float = 1.0,
-                 eval_batch: Optional[int] = None):
+                 eval_batch: Optional[int] = None, use_graph: bool = True):
         self.cfg = PRESETS[config] if isinstance(config, str) else config
         if seq_len is not None:
             self.cfg = dataclasses.replace(self.cfg, seq_len=seq_len)
@@ -95,7 +95,8 @@ class PopulationLM(FlatPopulation):
         self.batch_size = int(batch_size)          # sequences per trial per step
         self.eval_batch = int(eval_batch or batch_size)
         self.tokens_per_step = self.batch_size * c.seq_len
-        super().__init__(capacity, device=device, max_grad_norm=max_grad_norm)
+        super().__init__(capacity, device=device, max_grad_norm=max_grad_norm,
+                         use_graph=use_graph)
         self.cos, self.sin = ops.rope_tables(c.seq_len, c.rope_base, device=self.device)
 
     def param_specs(self):
@@ -128,7 +129,8 @@ class PopulationLM(FlatPopulation):
         h = ops.rmsnorm(x, W["final_norm"], rpt, c.norm_eps)
         logits = torch.bmm(h.view(P, rpt, d), W["head"]).view(R, c.vocab)
         if train:
-            return ops.cross_entropy(logits, labels.reshape(-1), rpt, grad_scale=1.0 / rpt)
+            return ops.cross_entropy(logits, labels.reshape(-1), rpt, grad_scale=1.0 / rpt,
+                                     unit_weights=True)
         return ops.ce_eval(logits, labels.reshape(-1), rpt)
 
 

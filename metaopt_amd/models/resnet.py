@@ -46,12 +46,12 @@ class PopulationResNet(FlatPopulation):
     secondary = "acc"
 
     def __init__(self, capacity: int, batch_size: int = 128, device="cuda",
-                 blocks_per_stage: int = 3, image_size: int = 32):
+                 blocks_per_stage: int = 3, image_size: int = 32, use_graph: bool = True):
         self.batch_size = int(batch_size)
         self.blocks = int(blocks_per_stage)
         self.image_size = int(image_size)
         self.layout = resnet20_layout(self.blocks)
-        super().__init__(capacity, device=device)
+        super().__init__(capacity, device=device, use_graph=use_graph)
 
     # ------------------------------------------------------------------ structure
     def param_specs(self):

@@ -248,7 +248,8 @@ class _CrossEntropy(torch.autograd.Function):
     logits buffer in the forward pass (the logits are not needed afterwards)."""
 
     @staticmethod
-    def forward(ctx, logits, labels, rows_per_trial, grad_scale):
+    def forward(ctx, logits, labels, rows_per_trial, grad_scale, unit_weights):
+        ctx.unit_weights = unit_weights
         R, V = logits.shape[-2] * (logits.shape[0] if logits.dim() == 3 else 1), logits.shape[-1]
         P = R // rows_per_trial
         loss = torch.zeros(P, dtype=torch.float32, device=logits.device)
@@ -260,20 +261,22 @@ class _CrossEntropy(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dloss):
         (dlogits,) = ctx.saved_tensors
-        # d(sum_p w_p * loss_p): each trial's rows scale by its own weight
+        if ctx.unit_weights:
+            # the caller differentiates sum_p loss_p: d/dloss_p = 1, no pass over the logits
+            # (and no host-side check, so the step can be captured in a HIP graph)
+            return dlogits, None, None, None, None
         P = dloss.numel()
-        g = dlogits.view(P, -1, dlogits.shape[-1])
-        if not torch.all(dloss == 1):
-            g = g * dloss.view(P, 1, 1).to(g.dtype)
-        return g.view_as(dlogits), None, None, None
+        g = dlogits.view(P, -1, dlogits.shape[-1]) * dloss.view(P, 1, 1).to(dlogits.dtype)
+        return g.view_as(dlogits), None, None, None, None
 
 
-def cross_entropy(logits, labels, rows_per_trial, grad_scale=1.0):
+def cross_entropy(logits, labels, rows_per_trial, grad_scale=1.0, unit_weights=False):
     """Returns the per-trial SUM of token losses [P] (fp32).  ``grad_scale`` multiplies the
-    gradient written for the backward (``1 / rows_per_trial`` gives mean-loss gradients)."""
+    gradient written for the backward (``1 / rows_per_trial`` gives mean-loss gradients).
+    ``unit_weights=True`` promises the result is only differentiated through ``loss.sum()``."""
     if _hip(logits):
         return _CrossEntropy.apply(logits.contiguous(), labels.contiguous(), rows_per_trial,
-                                   grad_scale)
+                                   grad_scale, unit_weights)
     loss = ce_ref(logits.reshape(-1, logits.shape[-1]), labels, rows_per_trial)
     return loss if grad_scale == 1.0 else _ScaledGrad.apply(loss, grad_scale)
 
@@ -365,10 +368,13 @@ class FlatOptimizer:
             self._chunks = _lib.upload_bytes(chunks, self.device)
             self._sumsq = torch.zeros(P, dtype=torch.float32, device=self.device)
 
-    def step(self, p32, p16, g16, m, v, hp: np.ndarray):
+    def step(self, p32, p16, g16, m, v, hp: np.ndarray, hp_dev=None):
+        """``hp_dev``: the hyper-parameters already on the device (graph replay); else ``hp`` is
+        uploaded."""
         clip = int(bool((hp["max_norm"] > 0).any()))
         if self.device.type == "cuda":
-            hp_dev = _lib.upload_bytes(hp, self.device)
+            if hp_dev is None:
+                hp_dev = _lib.upload_bytes(hp, self.device)
             if self.kind == "adamw":
                 _call("mopt_adamw_multi", _p(self._segs), _p(self._chunks), self.n_chunks,
                       _p(hp_dev), _p(self._sumsq), _p(p32), _p(p16), _p(g16), _p(m), _p(v),
