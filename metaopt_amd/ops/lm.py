@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 from typing import List, Tuple
 
 import numpy as np
@@ -50,8 +51,15 @@ SEGCHUNK_DTYPE = np.dtype([("seg", "<i4"), ("trial", "<i4"), ("start", "<i8")])
 ADAM_CHUNK = 2048
 
 
-def _hip(t: torch.Tensor) -> bool:
-    return t.device.type == "cuda"
+_FORCE_REF = {x.strip() for x in os.environ.get("MOPT_LM_REFERENCE", "").split(",") if x.strip()}
+
+
+def _hip(t: torch.Tensor, op: str = "") -> bool:
+    """HIP kernel on a GPU.  ``MOPT_LM_REFERENCE=all`` or ``=attn,ce,...`` explicitly selects the
+    PyTorch reference for those ops (a debugging / bisection aid; never a silent fallback)."""
+    if t.device.type != "cuda":
+        return False
+    return not (_FORCE_REF and ("all" in _FORCE_REF or op in _FORCE_REF))
 
 
 def _call(name, *args):
@@ -150,7 +158,7 @@ class _RMSNorm(torch.autograd.Function):
 
 
 def rmsnorm(x, w, rows_per_trial, eps=1e-5):
-    if _hip(x):
+    if _hip(x, "rmsnorm"):
         return _RMSNorm.apply(x.contiguous(), w.contiguous(), rows_per_trial, eps)
     return rmsnorm_ref(x, w, rows_per_trial, eps)
 
@@ -180,7 +188,7 @@ class _RopeSplit(torch.autograd.Function):
 
 
 def rope_split(qkv, cos, sin, T, H):
-    if _hip(qkv):
+    if _hip(qkv, "rope"):
         return _RopeSplit.apply(qkv.contiguous(), cos, sin, T, H)
     return rope_split_ref(qkv, cos, sin, T, H)
 
@@ -213,7 +221,7 @@ class _Attention(torch.autograd.Function):
 
 def attention(q, k, v, scale=None):
     scale = 1.0 / math.sqrt(q.shape[-1]) if scale is None else scale
-    if _hip(q):
+    if _hip(q, "attn"):
         return _Attention.apply(q, k, v, scale)
     return attention_ref(q, k, v, scale)
 
@@ -238,7 +246,7 @@ class _SwiGLU(torch.autograd.Function):
 
 
 def swiglu(gu):
-    if _hip(gu):
+    if _hip(gu, "swiglu"):
         return _SwiGLU.apply(gu.contiguous())
     return swiglu_ref(gu)
 
@@ -274,7 +282,7 @@ def cross_entropy(logits, labels, rows_per_trial, grad_scale=1.0, unit_weights=F
     """Returns the per-trial SUM of token losses [P] (fp32).  ``grad_scale`` multiplies the
     gradient written for the backward (``1 / rows_per_trial`` gives mean-loss gradients).
     ``unit_weights=True`` promises the result is only differentiated through ``loss.sum()``."""
-    if _hip(logits):
+    if _hip(logits, "ce"):
         return _CrossEntropy.apply(logits.contiguous(), labels.contiguous(), rows_per_trial,
                                    grad_scale, unit_weights)
     loss = ce_ref(logits.reshape(-1, logits.shape[-1]), labels, rows_per_trial)
@@ -294,7 +302,7 @@ class _ScaledGrad(torch.autograd.Function):
 
 def ce_eval(logits, labels, rows_per_trial):
     """Loss sums without writing gradients (validation)."""
-    if _hip(logits):
+    if _hip(logits, "ce"):
         R, V = logits.numel() // logits.shape[-1], logits.shape[-1]
         loss = torch.zeros(R // rows_per_trial, dtype=torch.float32, device=logits.device)
         _call("mopt_ce_fwd_bwd", _p(logits.contiguous()), _p(labels.contiguous()), _p(loss), R, V,
@@ -328,7 +336,7 @@ class _Embedding(torch.autograd.Function):
 
 
 def embedding(tok, table, rows_per_trial):
-    if _hip(table):
+    if _hip(table, "embed"):
         return _Embedding.apply(tok.contiguous(), table, rows_per_trial)
     return embed_ref(tok, table, rows_per_trial)
 
