@@ -225,6 +225,11 @@ class Experiment:
     # -- configuration ------------------------------------------------------------------------
     def configure(self, config, enable_branching=True, enable_update=True):
         """Validate ``config``, branch if it conflicts with the stored version, persist."""
+        from ..evc.conflicts import using_storage
+        with using_storage(self._storage):
+            return self._configure(config, enable_branching, enable_update)
+
+    def _configure(self, config, enable_branching=True, enable_update=True):
         from ..evc.conflicts import ExperimentNameConflict, detect_conflicts
         log.debug("configuring (name: %s)", config["name"])
         if self._init_done:

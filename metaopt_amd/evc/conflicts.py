@@ -38,9 +38,30 @@ log = logging.getLogger(__name__)
 NO_DEFAULT = Dimension.NO_DEFAULT_VALUE
 
 
+_STORAGE_OVERRIDE = []
+
+
 def _storage():
+    """The storage of the experiment being configured (``using_storage``), else the
+    process-wide one."""
+    if _STORAGE_OVERRIDE:
+        return _STORAGE_OVERRIDE[-1]
     from ..storage.protocol import get_storage
     return get_storage()
+
+
+class using_storage:
+    """Context: conflict detection/resolution queries go to ``storage``."""
+
+    def __init__(self, storage):
+        self.storage = storage
+
+    def __enter__(self):
+        _STORAGE_OVERRIDE.append(self.storage)
+        return self.storage
+
+    def __exit__(self, *exc):
+        _STORAGE_OVERRIDE.pop()
 
 
 def _create_param(dimension, default_value):
