@@ -32,6 +32,7 @@ import numpy as np
 import torch
 
 from ..ops import lm as ops
+from ..ops.gemm import pbmm
 from ..ops.population import MemberConfig
 from .flatpop import FlatPopulation
 
@@ -118,16 +119,16 @@ class PopulationLM(FlatPopulation):
         x = ops.embedding(tok.reshape(-1), W["embed"], rpt)
         for l in range(c.n_layers):
             h = ops.rmsnorm(x, W[f"l{l}.attn_norm"], rpt, c.norm_eps)
-            qkv = torch.bmm(h.view(P, rpt, d), W[f"l{l}.wqkv"]).view(R, 3 * d)
+            qkv = pbmm(h.view(P, rpt, d), W[f"l{l}.wqkv"]).view(R, 3 * d)
             q, k, v = ops.rope_split(qkv, self.cos, self.sin, T, H)
             o = ops.attention(q, k, v)
-            x = x + torch.bmm(o.view(P, rpt, d), W[f"l{l}.wo"]).view(R, d)
+            x = x + pbmm(o.view(P, rpt, d), W[f"l{l}.wo"]).view(R, d)
             h = ops.rmsnorm(x, W[f"l{l}.mlp_norm"], rpt, c.norm_eps)
-            gu = torch.bmm(h.view(P, rpt, d), W[f"l{l}.wgu"])
+            gu = pbmm(h.view(P, rpt, d), W[f"l{l}.wgu"])
             a = ops.swiglu(gu)
-            x = x + torch.bmm(a, W[f"l{l}.wdown"]).view(R, d)
+            x = x + pbmm(a, W[f"l{l}.wdown"]).view(R, d)
         h = ops.rmsnorm(x, W["final_norm"], rpt, c.norm_eps)
-        logits = torch.bmm(h.view(P, rpt, d), W["head"]).view(R, c.vocab)
+        logits = pbmm(h.view(P, rpt, d), W["head"]).view(R, c.vocab)
         if train:
             return ops.cross_entropy(logits, labels.reshape(-1), rpt, grad_scale=1.0 / rpt,
                                      unit_weights=True)

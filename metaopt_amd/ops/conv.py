@@ -16,6 +16,7 @@ import ctypes
 import torch
 
 from . import _lib
+from .gemm import pbmm
 
 c_void_p, c_int, c_float, c_int64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_int64
 
@@ -111,7 +112,7 @@ def conv3x3(x, w, P, stride):
         return conv3x3_ref(x, w, P, stride)
     N, H, W, C = x.shape
     col = _Im2Col.apply(x.contiguous(), stride)
-    out = torch.bmm(col.view(P, -1, 9 * C), w)
+    out = pbmm(col.view(P, -1, 9 * C), w)
     return out.view(N, out_hw(H, stride), out_hw(W, stride), w.shape[-1])
 
 

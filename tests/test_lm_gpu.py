@@ -203,3 +203,43 @@ def test_hypergradient_on_gpu_matches_cpu():
         out.append((hg.cpu(), vl.cpu(), w0))
     torch.testing.assert_close(out[0][0], out[1][0], rtol=5e-2, atol=5e-3)
     torch.testing.assert_close(out[0][1], out[1][1], rtol=1e-3, atol=1e-3)
+
+
+def test_fused_adamw_at_125m_layout_is_finite_and_exact_on_samples():
+    """The 125M-LM segment layout (8 trials, ~1.07B elements): no NaN, and every segment's first
+    trial and last trial match the reference."""
+    from metaopt_amd.models.llama import PRESETS, param_specs
+    P = 8
+    segments, off = [], 0
+    for _, shape, _ in param_specs(PRESETS["llama-125m"]):
+        n = int(np.prod(shape))
+        segments.append((off, n))
+        off += P * n
+    g = torch.Generator(device=DEV).manual_seed(0)
+    p32 = torch.randn(off, device=DEV, generator=g) * 0.02
+    g16 = (torch.randn(off, device=DEV, generator=g) * 1e-3).to(torch.bfloat16)
+    m = torch.zeros(off, device=DEV)
+    v = torch.zeros(off, device=DEV)
+    p16 = torch.empty(off, dtype=torch.bfloat16, device=DEV)
+    hp = np.zeros(P, dtype=ops.LM_HP_DTYPE)
+    for p in range(P):
+        hp[p] = (3e-4 * (p + 1), 0.9, 0.95, 1e-8, 0.1, 1.0, 1, 0)
+    before = p32.clone()
+    ops.FlatOptimizer(segments, P, DEV).step(p32, p16, g16, m, v, hp)
+    torch.cuda.synchronize()
+    assert torch.isfinite(p32).all() and torch.isfinite(m).all() and torch.isfinite(v).all()
+    # reference on a subset: all segments, trials 0 and P-1 (clipping uses the full trial norm)
+    sumsq = torch.zeros(P, dtype=torch.float64, device=DEV)
+    for o, n in segments:
+        sumsq += g16[o:o + P * n].view(P, n).double().pow(2).sum(1)
+    for o, n in segments:
+        for p in (0, P - 1):
+            sl = slice(o + p * n, o + (p + 1) * n)
+            nrm = float(sumsq[p].sqrt())
+            scale = 1.0 / (nrm + 1e-6) if nrm > 1.0 else 1.0
+            gr = g16[sl].float() * scale
+            lr, b1, b2, eps, wd = (float(hp[p][k]) for k in ("lr", "b1", "b2", "eps", "wd"))
+            mm = (1 - b1) * gr
+            vv = (1 - b2) * gr * gr
+            w = before[sl] * (1 - lr * wd) - lr / (1 - b1) * mm / (vv.sqrt() / (1 - b2) ** 0.5 + eps)
+            torch.testing.assert_close(p32[sl], w, rtol=1e-4, atol=1e-6)
