@@ -39,6 +39,10 @@ class BaseAlgorithm:
     """
 
     requires: Optional[str] = None
+    #: True when suggestions at a sync depend on the results of trials finishing at that same
+    #: sync (PBT generations); device sweeps then decide synchronously instead of one interval
+    #: behind the GPU (see ``PopulationSweep``)
+    synchronous: bool = False
 
     def __init__(self, space, **kwargs):
         log.debug("Creating %s with parameters %s", type(self).__name__, kwargs)

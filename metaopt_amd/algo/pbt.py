@@ -39,6 +39,8 @@ def _key(point) -> tuple:
 
 @ALGORITHMS.register()
 class PBT(BaseAlgorithm):
+    synchronous = True   # a generation's exploit needs that generation's results
+
     def __init__(self, space, seed=None, population_size=16, interval=None,
                  min_forking_population=5, truncation_quantile=0.8, candidate_pool_ratio=0.2,
                  factor=1.2, resample_probability=0.2, freeze=()):

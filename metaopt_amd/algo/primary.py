@@ -75,6 +75,10 @@ class PrimaryAlgo(BaseAlgorithm):
     def is_done(self):
         return self.algorithm.is_done
 
+    @property
+    def synchronous(self):
+        return bool(getattr(self.algorithm, "synchronous", False))
+
     def score(self, point):
         return self.algorithm.score(self.transformed_space.transform(point))
 

@@ -258,6 +258,22 @@ class FlatPopulation:
     def train_rows(self) -> int:
         return self.batch_size
 
+    def stats_snapshot_async(self):
+        from ..ops.population import StatsSnapshot
+        return StatsSnapshot(self.stats, self.capacity)
+
+    def raw_results(self, snap, handle):
+        """(train loss, eval loss, eval secondary) per slot from a snapshot, unmasked."""
+        tl = snap[0].astype(np.float64) / self.train_rows()
+        if handle is None:
+            nan = np.full(self.capacity, np.nan)
+            return tl, nan, nan
+        rows = handle["rows"]
+        loss = snap[2].astype(np.float64) / rows
+        second = (np.exp(np.minimum(loss, 50.0)) if self.secondary == "ppl"
+                  else snap[3].astype(np.float64) / rows)
+        return tl, loss, second
+
     def train_loss(self, snap=None) -> np.ndarray:
         snap = self.stats_snapshot() if snap is None else snap
         out = snap[0].astype(np.float64) / self.train_rows()

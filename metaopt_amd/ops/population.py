@@ -77,6 +77,34 @@ class MemberConfig:
         return dataclasses.asdict(self)
 
 
+class StatsSnapshot:
+    """Device->host copy of a population's ``[4, capacity]`` statistics queued on the current
+    stream (pinned, non-blocking): :meth:`get` waits for that copy only, so the host can read
+    the statistics of an earlier sync while the GPU already trains the next interval."""
+
+    __slots__ = ("capacity", "_host", "_ev")
+
+    def __init__(self, stats: torch.Tensor, capacity: int):
+        self.capacity = capacity
+        if stats.device.type == "cuda":
+            self._host = torch.empty(stats.shape, dtype=stats.dtype, pin_memory=True)
+            self._host.copy_(stats, non_blocking=True)
+            self._ev = torch.cuda.Event()
+            self._ev.record(torch.cuda.current_stream(stats.device))
+        else:
+            self._host = stats.detach().clone()
+            self._ev = None
+
+    def ready(self) -> bool:
+        return self._ev is None or self._ev.query()
+
+    def get(self) -> np.ndarray:
+        if self._ev is not None:
+            self._ev.synchronize()
+            self._ev = None
+        return self._host.numpy().reshape(4, self.capacity)
+
+
 def device_busy(device):
     if torch.device(device).type != "cuda":
         return lambda: True
@@ -669,6 +697,19 @@ class PopulationMLP:
     def stats_snapshot(self) -> np.ndarray:
         """One device->host copy of the train and eval statistics (waits for queued work)."""
         return self.stats.cpu().numpy().reshape(4, self.capacity)
+
+    def stats_snapshot_async(self) -> StatsSnapshot:
+        return StatsSnapshot(self.stats, self.capacity)
+
+    def raw_results(self, snap: np.ndarray, handle):
+        """(train loss, eval loss, eval accuracy) per slot from a snapshot, unmasked: the slots
+        may have been re-assigned since the snapshot was queued."""
+        tl = snap[0].astype(np.float64) / self.batch_size
+        if handle is None:
+            nan = np.full(self.capacity, np.nan)
+            return tl, nan, nan
+        rows = handle["rows"]
+        return tl, snap[2].astype(np.float64) / rows, snap[3].astype(np.float64) / rows
 
     def eval_result(self, snap: np.ndarray, handle):
         rows, subset = handle["rows"], handle["subset"]

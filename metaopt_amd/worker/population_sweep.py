@@ -44,14 +44,16 @@ from ..utils import format_trials
 log = logging.getLogger(__name__)
 
 NONE, NEW, RESUME, CLEAR = 0, 1, 2, 3
-ST_COLS = 7     # key, steps, budget, train_loss, val_loss, val_acc, bad
+# status row: key, steps, budget, nan flag | result key, train loss, val loss, val acc, broken
+ST_COLS = 9
 AS_COLS = 11    # action, key, width, lr, momentum, wd, dropout, seed, budget, resume_key, src_rank
 
 
 class PopulationSweep:
     def __init__(self, pop: PopulationMLP, task, data, comm: Optional[Comm] = None,
                  experiment=None, sync_every: int = 16, ckpt_capacity: int = 512,
-                 heartbeat_every: float = 30.0, max_trials: Optional[float] = None):
+                 heartbeat_every: float = 30.0, max_trials: Optional[float] = None,
+                 pipelined: Optional[bool] = None):
         self.pop = pop
         self.task = task
         self.data = data
@@ -97,6 +99,16 @@ class PopulationSweep:
         self.n_resumed = 0            # members resumed from a device checkpoint (this rank)
         self.n_resume_missing = 0
         self.n_syncs = 0
+        self._ckpt_alive = set()      # rank 0: (rank, trial key) held in the owners' pools
+        self._pending = None          # pipelined: (snapshot, eval handle, slot keys, finished)
+        self._bad_now = np.zeros(P, dtype=bool)
+        self._busy_marker = None
+        self._ctl_stream = None
+        if pipelined is None:   # every rank must agree: rank 0 knows the algorithm
+            sync_algo = bool(getattr(experiment.algorithms, "synchronous", False)) \
+                if self.comm.is_root else False
+            pipelined = not self.comm.broadcast_object(sync_algo)
+        self.pipelined = bool(pipelined)
         if self.comm.is_root:
             self.algorithm = experiment.algorithms
             self.space = experiment.space
@@ -119,6 +131,10 @@ class PopulationSweep:
         self.pop.train_step(x, y)
         self.global_step += 1
         self.samples += self.pop.batch_size * self._n_active
+        left = self.sync_every - self.global_step % self.sync_every
+        if self.pipelined and left == min(2, self.sync_every - 1):
+            # the writes drained at the sync stop once the GPU gets this close to the boundary
+            self._busy_marker = self.pop.device_busy()
         self.timers["launch"] += time.perf_counter() - t0
         if self.global_step % self.sync_every == 0:
             self._sync()
@@ -134,40 +150,54 @@ class PopulationSweep:
 
     # ------------------------------------------------------------------ sync
     def _local_status(self, evaluate=True) -> np.ndarray:
+        """This rank's status block (one row per slot, ST_COLS columns).
+
+        Columns 0-3 describe the member in the slot *now* (key, steps, budget, NaN flag); columns
+        4-8 carry the result of the member that finished in this slot (key, train loss, val
+        loss, val accuracy, broken flag).  Synchronous mode: the members finishing at this sync
+        are evaluated and read back here (the host waits for the interval).  Pipelined mode:
+        the evaluation and statistics of this sync are only *queued* (pinned async copy) and
+        the block reports the previous sync's, which the GPU produced one interval ago -- so
+        the host decides while the GPU trains the interval just queued.
+        """
         pop = self.pop
         P = pop.capacity
-        st = np.zeros((P, ST_COLS), dtype=np.float64)
+        st = np.full((P, ST_COLS), np.nan, dtype=np.float64)
         st[:, 0] = self.slot_key
         steps = pop.hp["t"].astype(np.float64)  # host mirror of the per-slot step counters
         st[:, 1] = steps
         st[:, 2] = self.slot_budget
+        st[:, 3] = 0.0
+        st[:, 4] = -1.0
         active = self.slot_key >= 0
         finished = np.flatnonzero(active & (steps >= self.slot_budget)).tolist()
         # 1) queue the validation of every member that reached its budget behind the interval's
-        #    training kernels (no host sync yet)
+        #    training kernels, and the copy of the statistics behind it (no host sync)
         handle = None
         if evaluate and finished:
             vx, vy = self.data.validation()
             handle = pop.evaluate_async(vx, vy, slots=finished)
-        # 2) storage writes of the previous decision run on the host while the GPU is still busy
-        #    with the interval (and the evaluation) just queued
-        if self._writer is not None and len(self._writer):
-            self._writer.drain_while(pop.device_busy())
-        # 3) one device->host copy of train + eval statistics
-        if active.any() and self.global_step > 0:
-            snap = pop.stats_snapshot()
-            tl = pop.train_loss(snap)
-            st[:, 3] = np.where(active, tl, np.nan)
-            st[:, 6] = active & ~np.isfinite(tl)
-            if handle is not None:
-                vl, va = pop.eval_result(snap, handle)
-                for s in finished:
-                    if st[s, 6]:
-                        continue
-                    st[s, 4] = vl[s]
-                    st[s, 5] = va[s]
-                    if not math.isfinite(vl[s]):
-                        st[s, 6] = 1
+        snap = pop.stats_snapshot_async() if active.any() and self.global_step > 0 else None
+        if self.pipelined:
+            prev, self._pending = self._pending, (snap, handle, self.slot_key.copy(), finished)
+            self._bad_now = np.zeros(P, dtype=bool)
+            if prev is not None and prev[0] is not None:
+                psnap, phandle, pkeys, pfinished = prev
+                tl, vl, va = pop.raw_results(psnap.get(), phandle)
+                # members still training that already diverged one interval ago
+                live = active & (pkeys == self.slot_key)
+                bad = live & ~np.isfinite(tl)
+                st[:, 3] = bad
+                self._bad_now = bad
+                self._fill_results(st, pfinished, pkeys, tl, vl, va, phandle)
+            self._drain_writes()
+        else:
+            self._drain_writes()
+            if snap is not None:
+                tl, vl, va = pop.raw_results(snap.get(), handle)
+                st[:, 3] = active & ~np.isfinite(tl)
+                self._fill_results(st, finished, self.slot_key, tl, vl, va, handle)
+            self._bad_now = st[:, 3] > 0
         if self._writer is not None:
             self.timers["writes_backlog"] += len(self._writer)
             self.timers["writes_busy"] += self._writer.busy_s
@@ -175,6 +205,23 @@ class PopulationSweep:
             if len(self._writer) > self.max_write_backlog:
                 self._writer.flush()  # the host cannot keep up: do not let the queue grow
         return st
+
+    @staticmethod
+    def _fill_results(st, finished, keys, tl, vl, va, handle):
+        for s in finished:
+            st[s, 4] = keys[s]
+            st[s, 5] = tl[s]
+            if handle is None:      # finished without an evaluation (start-up sync)
+                st[s, 8] = 1
+                continue
+            st[s, 6] = vl[s]
+            st[s, 7] = va[s]
+            st[s, 8] = not (math.isfinite(tl[s]) and math.isfinite(vl[s]))
+
+    def _drain_writes(self):
+        """Apply held storage writes while the GPU still has queued work ahead of the host."""
+        if self._writer is not None and len(self._writer):
+            self._writer.drain_while(self._busy_marker or self.pop.device_busy())
 
     def _sync(self, evaluate=True) -> None:
         P = self.pop.capacity
@@ -184,8 +231,9 @@ class PopulationSweep:
         t1 = time.perf_counter()
         dist = self.comm.distributed
         if dist:
-            status_t = torch.from_numpy(status).to(self.comm._coll_device())
-            gathered = self.comm.all_gather_rows(status_t).cpu().numpy()    # C1
+            with self._ctl_stream_ctx():
+                status_t = torch.from_numpy(status).to(self.comm._coll_device())
+                gathered = self.comm.all_gather_rows(status_t).cpu().numpy()    # C1
         else:
             gathered = status
         t2 = time.perf_counter()
@@ -196,14 +244,17 @@ class PopulationSweep:
             assign[-1, 0] = float(self.done)
         t3 = time.perf_counter()
         if dist:
-            assign_t = torch.from_numpy(assign).to(self.comm._coll_device())
-            self.comm.broadcast_(assign_t, src=0)                           # C5
-            assign = assign_t.cpu().numpy()
+            with self._ctl_stream_ctx():
+                assign_t = torch.from_numpy(assign).to(self.comm._coll_device())
+                self.comm.broadcast_(assign_t, src=0)                           # C5
+                assign = assign_t.cpu().numpy()
         t4 = time.perf_counter()
         self._apply(gathered, assign)
         # long-lived bookkeeping (trial documents, algorithm state) moves to the permanent GC
         # generation: full collections would otherwise rescan it every few syncs
         gc.freeze()
+        if self.pipelined:
+            self._drain_writes()
         t5 = time.perf_counter()
         tm["status"] += t1 - t0
         tm["c1_allgather"] += t2 - t1
@@ -212,6 +263,22 @@ class PopulationSweep:
         tm["apply"] += t5 - t4
         self.n_syncs += 1
 
+    def _ctl_stream_ctx(self):
+        """Control-plane collectives (C1/C5, KB payloads) run on their own stream so they do not
+        queue behind the training kernels already submitted to the compute stream."""
+        import contextlib
+        if self.comm.device.type != "cuda":
+            return contextlib.nullcontext()
+        if self._ctl_stream is None:
+            self._ctl_stream = torch.cuda.Stream(device=self.comm.device)
+        return torch.cuda.stream(self._ctl_stream)
+
+    def drain(self) -> None:
+        """Pipelined mode: run one more sync round without training so the results of the
+        members that finished at the last sync reach the algorithm and the storage."""
+        if self.pipelined and self._pending is not None and self._pending[3]:
+            self._sync()
+
     # ------------------------------------------------------------------ rank 0
     def _decide(self, gathered: np.ndarray) -> np.ndarray:
         W, P = self.comm.world_size, self.pop.capacity
@@ -219,27 +286,40 @@ class PopulationSweep:
         free = []
         done_pts, done_res = [], []
         now = datetime.datetime.utcnow()
+        max_b = self._max_budget()
         for row in range(W * P):
-            key = int(gathered[row, 0])
             rank, slot = divmod(row, P)
+            key = int(gathered[row, 0])
+            # 1) the slot's current member: leaves when it reached its budget or diverged; the
+            #    owner checkpoints it (below the top budget) -- mirrored here in FIFO order
             if key < 0:
                 free.append(row)
+            else:
+                steps, budget = int(gathered[row, 1]), int(gathered[row, 2])
+                bad = gathered[row, 3] > 0
+                if bad or steps >= budget:
+                    free.append(row)
+                    assign[row, 0] = CLEAR
+                    if not bad and budget < max_b:
+                        self._mirror_save(rank, key)
+                    if bad and key in self.trials:
+                        self.key_params.pop(key, None)
+                        self.broken += 1
+                        self._set_status(self.trials.pop(key), "broken")
+            # 2) the result of the member that finished in this slot (this sync or, pipelined,
+            #    the previous one)
+            rkey = int(gathered[row, 4])
+            if rkey < 0:
                 continue
-            steps, budget = int(gathered[row, 1]), int(gathered[row, 2])
-            bad = gathered[row, 6] > 0
-            if not bad and steps < budget:
-                continue
-            trial = self.trials.pop(key, None)
-            params = self.key_params.pop(key, None)
-            free.append(row)
-            assign[row, 0] = CLEAR
+            trial = self.trials.pop(rkey, None)
+            params = self.key_params.pop(rkey, None)
             if trial is None:
                 continue
-            if bad:
+            if gathered[row, 8] > 0:
                 self.broken += 1
                 self._set_status(trial, "broken")
                 continue
-            vl, va, tl = float(gathered[row, 4]), float(gathered[row, 5]), float(gathered[row, 3])
+            vl, va, tl = float(gathered[row, 6]), float(gathered[row, 7]), float(gathered[row, 5])
             trial.results = [Trial.Result(name="val_loss", type="objective", value=vl),
                              Trial.Result(name=getattr(self.task, "secondary_stat", "val_acc"),
                                           type="statistic", value=va),
@@ -248,13 +328,14 @@ class PopulationSweep:
             trial.end_time = now
             self._writer.put("complete_trial", trial)
             self.completed += 1
-            self.history.append((time.time(), key, vl, budget))
+            budget = int(self.task.budget(params))
+            self.history.append((time.time(), rkey, vl, budget))
             if vl < self.best[0]:
                 self.best = (vl, dict(params))
             done_pts.append(format_trials.trial_to_tuple(trial, self.space))
             done_res.append({"objective": vl, "constraint": [], "gradient": None})
-            if budget < self._max_budget():
-                self._record_ckpt(self.task.key(params), rank, key, steps)
+            if budget < max_b:
+                self._index_ckpt(self.task.key(params), rank, rkey, budget)
         t0 = time.perf_counter()
         if done_pts:
             self.algorithm.observe(done_pts, done_res)
@@ -269,19 +350,28 @@ class PopulationSweep:
         dim = self.space[self.task.fidelity] if self.task.fidelity in self.space else None
         return int(dim.high) if dim is not None else 0
 
-    def _record_ckpt(self, pkey, rank, key, steps):
+    def _mirror_save(self, rank, key):
+        """Rank 0's copy of ``rank``'s checkpoint FIFO: the owner saves exactly the members that
+        leave below the top budget without a NaN flag, in slot order, and evicts the oldest."""
         fifo = self.ckpt_fifo[rank]
         fifo.append(key)
+        self._ckpt_alive.add((rank, key))
+        while len(fifo) > self.ckpt_capacity:
+            old = fifo.popleft()
+            self._ckpt_alive.discard((rank, old))
+            pk = self._ckpt_pkey.pop((rank, old), None)
+            if pk is not None and self.ckpt_index.get(pk, (None, None))[:2] == (rank, old):
+                del self.ckpt_index[pk]
+
+    def _index_ckpt(self, pkey, rank, key, steps):
+        """Make a saved checkpoint findable by its parameters once its result is known."""
+        if (rank, key) not in self._ckpt_alive:
+            return                   # evicted before its result arrived
         prev = self.ckpt_index.get(pkey)
         if prev is not None:
             self._ckpt_pkey.pop((prev[0], prev[1]), None)
         self.ckpt_index[pkey] = (rank, key, steps)
         self._ckpt_pkey[(rank, key)] = pkey
-        while len(fifo) > self.ckpt_capacity:   # mirrors the owner's FIFO eviction exactly
-            old = fifo.popleft()
-            pk = self._ckpt_pkey.pop((rank, old), None)
-            if pk is not None and self.ckpt_index.get(pk, (None, None))[:2] == (rank, old):
-                del self.ckpt_index[pk]
 
     def _fill(self, free_rows: List[int], assign: np.ndarray) -> None:
         W, P = self.comm.world_size, self.pop.capacity
@@ -380,16 +470,16 @@ class PopulationSweep:
         max_b = None
         # every member that finished (or broke) at this sync leaves its slot -- whether the slot
         # is CLEARed or immediately re-assigned; the ones that completed below the top budget are
-        # checkpointed first, all in one batched copy (rank 0 mirrors the FIFO in _record_ckpt)
+        # checkpointed first, all in one batched copy (rank 0 mirrors the FIFO in _mirror_save)
         to_save, leaving = [], []
         for s in range(P):
             if self.slot_key[s] < 0:
                 continue
-            if g[s, 6] > 0 or g[s, 1] >= g[s, 2]:
+            if g[s, 3] > 0 or g[s, 1] >= g[s, 2]:
                 leaving.append(s)
                 if max_b is None:
                     max_b = self._max_budget_local()
-                if g[s, 6] == 0 and self.slot_budget[s] < max_b:
+                if g[s, 3] == 0 and self.slot_budget[s] < max_b:
                     if len(self.ckpts) + len(to_save) >= self.ckpt_capacity:
                         if self.ckpts:
                             _, old = self.ckpts.popitem(last=False)

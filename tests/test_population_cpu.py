@@ -90,7 +90,10 @@ def test_adamw_reference_matches_torch_optim():
     assert torch.allclose(p.detach(), w2, atol=1e-6)
 
 
-def test_sweep_asha_end_to_end(data):
+@pytest.mark.parametrize("pipelined", [None, False])
+def test_sweep_asha_end_to_end(data, pipelined):
+    """ASHA decides one interval behind the GPU by default (pipelined) and synchronously on
+    request; both complete every trial and resume every promotion from its checkpoint."""
     priors = {"/lr": "loguniform(1e-3, 1.0)", "/width": "loguniform(64, 128, discrete=True)",
               "/dropout": "uniform(0, 0.5)", "/steps": "fidelity(16, 64, 2)"}
     storage = DocumentStorage(EphemeralDB())
@@ -99,7 +102,8 @@ def test_sweep_asha_end_to_end(data):
                            max_trials=24, storage=storage)
     pop = PopulationMLP(6, max_width=128, eval_batch=256, device="cpu")
     sweep = PopulationSweep(pop, MLPSweepTask(priors=priors, max_width=128), data,
-                            experiment=exp, sync_every=16)
+                            experiment=exp, sync_every=16, pipelined=pipelined)
+    assert sweep.pipelined == (pipelined is None)
     summary = sweep.run(1000)
     sweep.close()
     assert summary["completed"] == 24
@@ -139,6 +143,7 @@ def test_sweep_pbt_generations_resume_state(data):
     pop = PopulationMLP(6, max_width=64, eval_batch=256, device="cpu")
     sweep = PopulationSweep(pop, MLPSweepTask(priors=priors, max_width=64), data,
                             experiment=exp, sync_every=16)
+    assert not sweep.pipelined              # PBT generations decide synchronously
     summary = sweep.run(200)
     sweep.close()
     assert sweep.done and summary["completed"] == 18
