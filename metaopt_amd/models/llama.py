@@ -77,6 +77,12 @@ def param_specs(cfg: LMConfig):
     return specs
 
 
+def _lin(x, w):
+    """Population linear layer; the weight gradient goes straight into the leaf's preset
+    ``.grad`` (a view of the flat gradient buffer the fused AdamW reads)."""
+    return pbmm(x, w, w.grad if w.requires_grad else None)
+
+
 class PopulationLM(FlatPopulation):
     """``capacity`` Llama-style LM trials of one architecture (AdamW, per-trial lr / betas /
     weight decay, per-trial gradient clipping)."""
@@ -119,16 +125,16 @@ class PopulationLM(FlatPopulation):
         x = ops.embedding(tok.reshape(-1), W["embed"], rpt)
         for l in range(c.n_layers):
             h = ops.rmsnorm(x, W[f"l{l}.attn_norm"], rpt, c.norm_eps)
-            qkv = pbmm(h.view(P, rpt, d), W[f"l{l}.wqkv"]).view(R, 3 * d)
+            qkv = _lin(h.view(P, rpt, d), W[f"l{l}.wqkv"]).view(R, 3 * d)
             q, k, v = ops.rope_split(qkv, self.cos, self.sin, T, H)
             o = ops.attention(q, k, v)
-            x = x + pbmm(o.view(P, rpt, d), W[f"l{l}.wo"]).view(R, d)
+            x = x + _lin(o.view(P, rpt, d), W[f"l{l}.wo"]).view(R, d)
             h = ops.rmsnorm(x, W[f"l{l}.mlp_norm"], rpt, c.norm_eps)
-            gu = pbmm(h.view(P, rpt, d), W[f"l{l}.wgu"])
+            gu = _lin(h.view(P, rpt, d), W[f"l{l}.wgu"])
             a = ops.swiglu(gu)
-            x = x + pbmm(a, W[f"l{l}.wdown"]).view(R, d)
+            x = x + _lin(a, W[f"l{l}.wdown"]).view(R, d)
         h = ops.rmsnorm(x, W["final_norm"], rpt, c.norm_eps)
-        logits = pbmm(h.view(P, rpt, d), W["head"]).view(R, c.vocab)
+        logits = _lin(h.view(P, rpt, d), W["head"]).view(R, c.vocab)
         if train:
             return ops.cross_entropy(logits, labels.reshape(-1), rpt, grad_scale=1.0 / rpt,
                                      unit_weights=True)

@@ -112,7 +112,7 @@ def conv3x3(x, w, P, stride):
         return conv3x3_ref(x, w, P, stride)
     N, H, W, C = x.shape
     col = _Im2Col.apply(x.contiguous(), stride)
-    out = pbmm(col.view(P, -1, 9 * C), w)
+    out = pbmm(col.view(P, -1, 9 * C), w, w.grad if w.requires_grad and w.is_leaf else None)
     return out.view(N, out_hw(H, stride), out_hw(W, stride), w.shape[-1])
 
 

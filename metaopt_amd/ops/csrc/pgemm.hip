@@ -1,0 +1,282 @@
+// Population-batched bf16 GEMM on MFMA (gfx950): C[p] = op(A[p]) . op(B[p]) for p < P.
+//
+// The trial population is the batch dimension.  Each operand is read in the layout it is stored
+// in, so the three GEMMs of a linear layer never materialise a transpose:
+//     forward   Y  = X . W        A = X [M][K]   B = W [K][N]          (NN)
+//     input     dX = dY . W^T     A = dY [M][N]  B = W stored [K][N]   (NT: B is [n][k])
+//     weight    dW = X^T . dY     A = X stored [M][K]  B = dY [M][N]   (TN: A is [k][m])
+// (this also sidesteps the transposed-operand batched GEMM of the installed library stack that
+// returns wrong results for some shapes -- scripts/check_bmm.py).
+//
+// Structure: 256 threads = 4 waves arranged WM x (4/WM); each wave owns FM x FN fragments of
+// v_mfma_f32_16x16x32_bf16 (a 16*FM x 16*FN sub-tile), so the block tile is BM x BN with
+// BM = WM*16*FM, BN = (4/WM)*16*FN; BK = 64.  Operand tiles are staged global -> registers ->
+// LDS (double-buffered LDS, one barrier per K tile, the next tile's global loads in flight
+// while the current one is multiplied).  The LDS image keeps the stored orientation:
+//   * k-contiguous operands ([m][k] / [n][k]) as [row][64 + 8 pad] -> fragments by ds_read_b128;
+//   * row-contiguous operands ([k][m] / [k][n]) as [k][rows + 8 pad] -> fragments by the
+//     transposing ds_read_b64_tr_b16 (two per fragment).
+// Split-K (for the weight gradient's long reduction over tokens / pixels) writes f32 partial
+// tiles that a second pass sums and rounds to bf16.  Blocks are remapped XCD-aware so the tiles
+// sharing an A row panel run on one XCD (one L2).
+#include "common.h"
+
+using namespace mopt;
+
+namespace {
+
+constexpr int BK = 64;
+constexpr int LSK = BK + 8;  // row stride of k-contiguous LDS images (144 B)
+
+template <int ROWS, bool KCONTIG>
+struct Img {
+  static constexpr int LS = KCONTIG ? LSK : ROWS + 8;
+  static constexpr int ELEMS = KCONTIG ? ROWS * LSK : BK * (ROWS + 8);
+  static constexpr int CHUNKS = ROWS * BK / 8;  // 16-byte chunks per tile
+  static constexpr int NC = (CHUNKS + 255) / 256;
+  static constexpr int RCH = ROWS / 8;          // chunks per k-row of a row-contiguous tile
+
+  // global -> registers: chunk c of the tile starting at (row0, k0); zero outside [R) x [k_end)
+  __device__ __forceinline__ static void load(uint4 (&r)[NC], const bf16_t* __restrict__ base,
+                                              int ld, int row0, int k0, int R, int k_end) {
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (c < CHUNKS) {
+        int gr, gk;
+        if (KCONTIG) {
+          gr = row0 + (c >> 3);
+          gk = k0 + 8 * (c & 7);
+        } else {
+          gk = k0 + c / RCH;
+          gr = row0 + 8 * (c % RCH);
+        }
+        if (gr < R && gk < k_end) {
+          const bf16_t* src = KCONTIG ? base + (int64_t)gr * ld + gk : base + (int64_t)gk * ld + gr;
+          v = *(const uint4*)src;
+        }
+      }
+      r[i] = v;
+    }
+  }
+
+  __device__ __forceinline__ static void store(const uint4 (&r)[NC], bf16_t* img) {
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      if (c < CHUNKS) {
+        const int off = KCONTIG ? (c >> 3) * LSK + 8 * (c & 7) : (c / RCH) * LS + 8 * (c % RCH);
+        *(uint4*)(img + off) = r[i];
+      }
+    }
+  }
+
+  // fragment of rows row16 .. row16+15 (lane li -> row row16 + li), k = 32 s + 8 g .. + 7
+  __device__ __forceinline__ static bf16x8 frag(const bf16_t* img, int row16, int s, int li, int g,
+                                                int q, int pp) {
+    if (KCONTIG) return lds_frag(img + (row16 + li) * LSK + 32 * s + 8 * g);
+    const s16x4 lo = lds_tr4(img + (32 * s + 8 * g + q) * LS + row16 + 4 * pp);
+    const s16x4 hi = lds_tr4(img + (32 * s + 8 * g + 4 + q) * LS + row16 + 4 * pp);
+    return cat_frag(lo, hi);
+  }
+};
+
+struct GemmArgs {
+  const bf16_t* A;
+  const bf16_t* B;
+  bf16_t* C;
+  float* part;     // split-K partials [splits][P][M][N] (nullptr when splits == 1)
+  int64_t sA, sB, sC;
+  int P, M, N, K, lda, ldb, ldc;
+  int tiles_m, tiles_n, splits, k_per_split, nwg;
+};
+
+template <bool TA, bool TB, int WM, int FM, int FN>
+__global__ __launch_bounds__(256) void pgemm_kernel(const GemmArgs g) {
+  constexpr int WN = 4 / WM;
+  constexpr int BM = WM * 16 * FM, BN = WN * 16 * FN;
+  using IA = Img<BM, !TA>;
+  using IB = Img<BN, TB>;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * (IA::ELEMS + IB::ELEMS)];
+  constexpr int BUF = IA::ELEMS + IB::ELEMS;  // buffer b: A image at b*BUF, B image after it
+
+  int t = xcd_remap(blockIdx.x, g.nwg);
+  const int tn = t % g.tiles_n;
+  t /= g.tiles_n;
+  const int tm = t % g.tiles_m;
+  t /= g.tiles_m;
+  const int sp = t % g.splits;
+  const int p = t / g.splits;
+
+  const bf16_t* A = g.A + p * g.sA;
+  const bf16_t* B = g.B + p * g.sB;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kb = sp * g.k_per_split;
+  const int ke = min(g.K, kb + g.k_per_split);
+  const int nk = (ke - kb + BK - 1) / BK;
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 15, gq = lane >> 4, q = li >> 2, pp = li & 3;
+  const int wm = wave / WN, wn = wave % WN;
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  uint4 ra[IA::NC], rb[IB::NC];
+  IA::load(ra, A, g.lda, m0, kb, g.M, ke);
+  IB::load(rb, B, g.ldb, n0, kb, g.N, ke);
+  IA::store(ra, smem);
+  IB::store(rb, smem + IA::ELEMS);
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      IA::load(ra, A, g.lda, m0, kb + (kt + 1) * BK, g.M, ke);
+      IB::load(rb, B, g.ldb, n0, kb + (kt + 1) * BK, g.N, ke);
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 a[FM], b[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        a[i] = IA::frag(smem + cur * BUF, wm * 16 * FM + 16 * i, s, li, gq, q, pp);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        b[j] = IB::frag(smem + cur * BUF + IA::ELEMS, wn * 16 * FN + 16 * j, s, li, gq, q, pp);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
+    }
+    if (more) {
+      IA::store(ra, smem + (cur ^ 1) * BUF);
+      IB::store(rb, smem + (cur ^ 1) * BUF + IA::ELEMS);
+    }
+    __syncthreads();
+  }
+
+  // epilogue: lane holds C[row 4 gq + r][col li] of every fragment.  bf16 output is restaged
+  // through LDS (the operand buffers are free after the loop's last barrier) so every lane
+  // stores whole 16-byte row segments instead of scattered 2-byte elements.
+  if (g.splits == 1) {
+    constexpr int LSC = BN + 8;
+    static_assert(BM * LSC <= 2 * BUF, "C tile must fit in the operand buffers");
+    bf16_t* Cs = smem;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          Cs[(wm * 16 * FM + 16 * i + 4 * gq + r) * LSC + wn * 16 * FN + 16 * j + li] =
+              f2bf(acc[i][j][r]);
+    __syncthreads();
+    bf16_t* C = g.C + p * g.sC;
+    constexpr int CPR = BN / 8;  // 16-byte chunks per tile row
+#pragma unroll
+    for (int c = threadIdx.x; c < BM * CPR; c += 256) {
+      const int row = c / CPR, cc = c % CPR;
+      const int m = m0 + row, n = n0 + 8 * cc;
+      if (m < g.M && n < g.N)
+        *(uint4*)(C + (int64_t)m * g.ldc + n) = *(const uint4*)(Cs + row * LSC + 8 * cc);
+    }
+  } else {
+    float* C = g.part + ((int64_t)sp * g.P + p) * g.M * g.N;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = n0 + wn * 16 * FN + 16 * j + li;
+        if (n >= g.N) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * 16 * FM + 16 * i + 4 * gq + r;
+          if (m < g.M) C[(int64_t)m * g.N + n] = acc[i][j][r];
+        }
+      }
+  }
+}
+
+// sum of the split-K partials [splits][P][M][N] -> C[p][m][n * ldc] bf16
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part,
+                                                            bf16_t* __restrict__ C, int64_t sC,
+                                                            int ldc, int P, int M, int N,
+                                                            int splits) {
+  const int64_t total = (int64_t)P * M * N;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  float s = 0.f;
+  for (int k = 0; k < splits; ++k) s += part[k * total + i];
+  const int64_t n = i % N, m = (i / N) % M, p = i / ((int64_t)M * N);
+  C[p * sC + m * ldc + n] = f2bf(s);
+}
+
+template <bool TA, bool TB, int WM, int FM, int FN>
+int launch(GemmArgs g, hipStream_t st) {
+  constexpr int BM = WM * 16 * FM, BN = (4 / WM) * 16 * FN;
+  g.tiles_m = (g.M + BM - 1) / BM;
+  g.tiles_n = (g.N + BN - 1) / BN;
+  const int64_t nwg = (int64_t)g.P * g.splits * g.tiles_m * g.tiles_n;
+  if (nwg <= 0 || nwg > 0x7FFFFFFF) return (int)hipErrorInvalidValue;
+  g.nwg = (int)nwg;
+  hipLaunchKernelGGL((pgemm_kernel<TA, TB, WM, FM, FN>), dim3(g.nwg), dim3(256), 0, st, g);
+  return (int)hipGetLastError();
+}
+
+template <bool TA, bool TB>
+int dispatch_tile(const GemmArgs& g, int cfg, hipStream_t st) {
+  switch (cfg) {
+    case 0: return launch<TA, TB, 2, 4, 4>(g, st);  // 128 x 128
+    case 1: return launch<TA, TB, 4, 2, 1>(g, st);  // 128 x 16
+    case 2: return launch<TA, TB, 4, 2, 2>(g, st);  // 128 x 32
+    case 3: return launch<TA, TB, 4, 1, 4>(g, st);  // 64 x 64
+    case 4: return launch<TA, TB, 2, 2, 4>(g, st);  // 64 x 128
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// Tile of configuration ``cfg`` (rows, cols): lets the host size grids and split-K.
+int mopt_pgemm_tile(int cfg, int* bm, int* bn) {
+  static const int t[5][2] = {{128, 128}, {128, 16}, {128, 32}, {64, 64}, {64, 128}};
+  if (cfg < 0 || cfg > 4) return (int)hipErrorInvalidValue;
+  *bm = t[cfg][0];
+  *bn = t[cfg][1];
+  return 0;
+}
+
+// C[p] = op(A[p]) . op(B[p]); ta: A stored [K][M] (else [M][K]); tb: B stored [N][K] (else
+// [K][N]).  Contiguous-dimension extents must be multiples of 8 and every row 16-byte aligned;
+// k_per_split a multiple of 64 (splits > 1 needs ``part`` = f32 [splits][P][M][N]).
+int mopt_pgemm(const void* A, const void* B, void* C, void* part, int P, int M, int N, int K,
+               int lda, int ldb, int ldc, int64_t sA, int64_t sB, int64_t sC, int ta, int tb,
+               int cfg, int splits, int k_per_split, void* stream) {
+  if (P <= 0 || M <= 0 || N <= 0 || K <= 0) return 0;
+  if (splits < 1 || (splits > 1 && (part == nullptr || k_per_split % BK))) {
+    return (int)hipErrorInvalidValue;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  GemmArgs g{(const bf16_t*)A, (const bf16_t*)B, (bf16_t*)C, (float*)part, sA, sB, sC,
+             P, M, N, K, lda, ldb, ldc, 0, 0, splits, splits > 1 ? k_per_split : K, 0};
+  int err;
+  if (!ta && !tb) err = dispatch_tile<false, false>(g, cfg, st);
+  else if (!ta && tb) err = dispatch_tile<false, true>(g, cfg, st);
+  else if (ta && !tb) err = dispatch_tile<true, false>(g, cfg, st);
+  else err = dispatch_tile<true, true>(g, cfg, st);
+  if (err || splits == 1) return err;
+  const int64_t total = (int64_t)P * M * N;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     st, (const float*)part, (bf16_t*)C, sC, ldc, P, M, N, splits);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -1,25 +1,135 @@
-"""Population-batched GEMM with a backward that only issues NN-layout GEMMs.
+"""Population-batched GEMMs on the hand-written MFMA kernel (``csrc/pgemm.hip``).
 
-``pbmm(a, b)`` = ``torch.bmm(a, b)`` (hipBLASLt strided-batched, [P, M, K] x [P, K, N]).  Its
-backward materialises the transposed operand and calls ``bmm`` on contiguous tensors instead of
-handing transposed views to the library: with the installed ROCm stack, the transposed-operand
-bf16 batched GEMM of shape (m 2048, n 4096, k 768) -- the input gradient of the 125M LM's FFN
-down projection -- returns wrong results for batches 1..P-1 (hipBLASLt reports an internal
-error and the fallback path then faults).  ``scripts/check_bmm.py`` reproduces it; the NN-layout
-forms are exact for every shape the LM and CNN paths use.  The extra transposes move a few MB
-per GEMM.
+``pgemm(a, b, ta, tb)`` computes ``C[p] = op(a[p]) @ op(b[p])`` for every trial ``p`` of the
+population, reading each operand in the layout it is stored in (``ta``: ``a`` is stored
+``[K, M]``; ``tb``: ``b`` is stored ``[N, K]``), so the backward GEMMs of a linear layer need no
+transposed copies.  ``pbmm(x, w)`` is the differentiable ``x @ w`` of the LM and CNN paths:
+
+* forward ``y = x w`` (NN), input gradient ``dx = dy w^T`` (NT), weight gradient
+  ``dw = x^T dy`` (TN, split-K over the token / pixel dimension when the output tile grid is too
+  small to fill the 256 CUs);
+* ``grad_out``: the weight gradient is written straight into that buffer (the flat gradient
+  buffer the fused optimizer reads) instead of being returned to autograd and accumulated.
+
+The kernel replaced ``torch.bmm`` (hipBLASLt) in the backward, whose transposed-operand batched
+bf16 GEMM returns wrong results for some shapes on the installed stack (``scripts/check_bmm.py``);
+the copies that worked around it were ~20-40 % of the LM / ResNet step.  CPU tensors use ``torch.bmm`` (the
+reference path of the tests).
 """
 from __future__ import annotations
 
+import ctypes
+import math
+from typing import Optional
+
 import torch
+
+from . import _lib
+
+c_void_p, c_int, c_int64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+
+_lib.register_signatures({
+    "mopt_pgemm": ([c_void_p] * 4 + [c_int] * 7 + [c_int64] * 3 + [c_int] * 5 + [c_void_p],
+                   c_int),
+})
+
+# tile configurations of csrc/pgemm.hip: cfg -> (BM, BN)
+TILES = {0: (128, 128), 1: (128, 16), 2: (128, 32), 3: (64, 64), 4: (64, 128)}
+NUM_CU = 256
+
+
+def pick_tile(M: int, N: int) -> int:
+    if N <= 16:
+        return 1
+    if N <= 32:
+        return 2
+    if N <= 64:
+        return 3
+    if M <= 64:
+        return 4
+    return 0
+
+
+def plan(P: int, M: int, N: int, K: int, cfg: Optional[int] = None):
+    """(tile cfg, splits, k_per_split) for a [P] x (M x K) . (K x N) problem: split the K
+    reduction when the output tiles alone give fewer than ~2 workgroups per CU."""
+    cfg = pick_tile(M, N) if cfg is None else cfg
+    bm, bn = TILES[cfg]
+    blocks = P * math.ceil(M / bm) * math.ceil(N / bn)
+    splits = 1
+    if blocks < 2 * NUM_CU and K >= 512:
+        splits = min(math.ceil(2 * NUM_CU / blocks), K // 256, 32)
+    if splits <= 1:
+        return cfg, 1, K
+    kps = math.ceil(K / splits / 64) * 64
+    return cfg, math.ceil(K / kps), kps
+
+
+def _check_operand(t: torch.Tensor, name: str) -> None:
+    if t.dtype != torch.bfloat16 or t.dim() != 3 or t.stride(2) != 1:
+        raise ValueError(f"pgemm: {name} must be a [P, rows, cols] bf16 tensor with unit column "
+                         f"stride, got {t.dtype} {tuple(t.shape)} strides {t.stride()}")
+    if t.shape[2] % 8 or t.stride(1) % 8 or (t.shape[0] > 1 and t.stride(0) % 8) or \
+            t.data_ptr() % 16:
+        raise ValueError(f"pgemm: {name} rows must be 16-byte aligned multiples of 8 elements "
+                         f"(shape {tuple(t.shape)}, strides {t.stride()})")
+
+
+def pgemm(a: torch.Tensor, b: torch.Tensor, ta: bool = False, tb: bool = False,
+          out: Optional[torch.Tensor] = None, cfg: Optional[int] = None) -> torch.Tensor:
+    """``out[p] = op(a[p]) @ op(b[p])`` in bf16 with f32 accumulation on the MFMA kernel."""
+    if a.device.type != "cuda":
+        aa = a.transpose(1, 2) if ta else a
+        bb = b.transpose(1, 2) if tb else b
+        r = torch.bmm(aa.float(), bb.float()).to(a.dtype)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    _check_operand(a, "a")
+    _check_operand(b, "b")
+    P = a.shape[0]
+    K, M = (a.shape[1], a.shape[2]) if ta else (a.shape[2], a.shape[1])
+    N, Kb = (b.shape[1], b.shape[2]) if tb else (b.shape[2], b.shape[1])
+    if K != Kb or b.shape[0] != P:
+        raise ValueError(f"pgemm: shape mismatch a {tuple(a.shape)} (ta={ta}) b "
+                         f"{tuple(b.shape)} (tb={tb})")
+    if N % 8:
+        raise ValueError(f"pgemm: N = {N} must be a multiple of 8 (16-byte output rows)")
+    if out is None:
+        out = torch.empty(P, M, N, dtype=torch.bfloat16, device=a.device)
+    elif tuple(out.shape) != (P, M, N) or out.stride(2) != 1 or out.dtype != torch.bfloat16:
+        raise ValueError(f"pgemm: out must be [P, M, N] = {(P, M, N)} bf16 row-major")
+    _check_operand(out, "out")
+    cfg, splits, kps = plan(P, M, N, K, cfg)
+    part = (torch.empty(splits, P, M, N, dtype=torch.float32, device=a.device)
+            if splits > 1 else None)
+    _lib.check(_lib.get_lib().mopt_pgemm(
+        a.data_ptr(), b.data_ptr(), out.data_ptr(), 0 if part is None else part.data_ptr(),
+        P, M, N, K, a.stride(1), b.stride(1), out.stride(1), a.stride(0), b.stride(0),
+        out.stride(0), int(ta), int(tb), cfg, splits, kps, _lib.stream_ptr(a.device)),
+        "pgemm")
+    return out
+
+
+#: wide NN products (the LM's projections, N >= 256) go to hipBLASLt, which is correct for the
+#: NN layout and currently ~1.4x faster than pgemm there (scripts/gemm_bench.py); the backward's
+#: NT / TN products and every CNN product stay on pgemm
+LIBRARY_NN_MIN_N = 256
+
+
+def nn_forward(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    if LIBRARY_NN_MIN_N is not None and b.shape[2] >= LIBRARY_NN_MIN_N:
+        return torch.bmm(a, b)
+    return pgemm(a, b)
 
 
 class _PBmm(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, a, b):
-        a, b = a.contiguous(), b.contiguous()
+    def forward(ctx, a, b, grad_out):
         ctx.save_for_backward(a, b)
-        return torch.bmm(a, b)
+        ctx.grad_out = grad_out
+        return nn_forward(a, b)
 
     @staticmethod
     def backward(ctx, g):
@@ -27,13 +137,18 @@ class _PBmm(torch.autograd.Function):
         g = g.contiguous()
         da = db = None
         if ctx.needs_input_grad[0]:
-            da = torch.bmm(g, b.transpose(1, 2).contiguous())
+            da = pgemm(g, b, tb=True)
         if ctx.needs_input_grad[1]:
-            db = torch.bmm(a.transpose(1, 2).contiguous(), g)
-        return da, db
+            if ctx.grad_out is not None:       # written in place: nothing to accumulate
+                pgemm(a, g, ta=True, out=ctx.grad_out)
+            else:
+                db = pgemm(a, g, ta=True)
+        return da, db, None
 
 
-def pbmm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+def pbmm(a: torch.Tensor, b: torch.Tensor, grad_out: Optional[torch.Tensor] = None):
+    """Differentiable population GEMM ``a [P, M, K] @ b [P, K, N]``.  ``grad_out``: buffer that
+    receives ``b``'s gradient directly (then autograd gets none for ``b``)."""
     if a.device.type != "cuda":
         return torch.bmm(a, b)
-    return _PBmm.apply(a, b)
+    return _PBmm.apply(a.contiguous(), b.contiguous(), grad_out)
