@@ -1,0 +1,251 @@
+"""Worker layer on CPU: producer (lies to a naive algorithm copy, duplicates, idle timeout,
+lineage), consumer (black-box subprocess, environment, templates, broken / interrupted
+trials), heartbeat pacemaker, trials history, the worker loop and the study API
+(reference: tests/unittests/core/test_producer.py, core/worker/test_consumer.py,
+core/worker/test_trial_pacemaker.py, test_trials_history.py -- behaviour, not code)."""
+import datetime
+import json
+import os
+import sys
+import textwrap
+import time
+
+import pytest
+
+from metaopt_amd.client.study import Study
+from metaopt_amd.core.trial import Trial
+from metaopt_amd.io.experiment_builder import build_experiment
+from metaopt_amd.storage.database import EphemeralDB
+from metaopt_amd.storage.protocol import DocumentStorage
+from metaopt_amd.utils.exceptions import SampleTimeout
+from metaopt_amd.worker.consumer import Consumer
+from metaopt_amd.worker.pacemaker import TrialPacemaker
+from metaopt_amd.worker.producer import Producer
+from metaopt_amd.worker.strategy import MaxParallelStrategy
+from metaopt_amd.worker.trials_history import TrialsHistory
+from metaopt_amd.worker.workon import workon
+
+
+def _storage():
+    return DocumentStorage(EphemeralDB())
+
+
+def _exp(name="w", priors=None, **kw):
+    return build_experiment(name, priors=priors or {"/x": "uniform(-5, 5)"},
+                            storage=_storage(), **kw)
+
+
+def _complete(exp, trial, value):
+    trial.results = [Trial.Result(name="obj", type="objective", value=value)]
+    trial.status = "completed"
+    trial.end_time = datetime.datetime.utcnow()
+    exp.storage.push_trial_results(trial)
+
+
+# ------------------------------------------------------------------ producer
+class TestProducer:
+    def test_produces_pool_size_new_trials(self):
+        exp = _exp(pool_size=4, algorithms={"random": {"seed": 1}})
+        n = Producer(exp).produce()
+        trials = exp.fetch_trials()
+        assert n == 4 and len(trials) == 4 and all(t.status == "new" for t in trials)
+        assert len({t.id for t in trials}) == 4
+
+    def test_lies_go_to_naive_copy_only(self):
+        exp = _exp(pool_size=2, algorithms={"random": {"seed": 2}},
+                   strategy={"MaxParallelStrategy": {}})
+        prod = Producer(exp)
+        prod.produce()
+        a, b = exp.fetch_trials()
+        _complete(exp, a, 3.0)
+        prod.update()
+        # the real algorithm saw one completed trial, the naive copy also the lie for the other
+        assert len(prod.trials_history.ids) == 1
+        assert len(prod.naive_trials_history.ids) == 2
+        lies = exp.storage.fetch_lies(exp)
+        assert len(lies) == 1 and lies[0].lie.value == 3.0   # max of the observed objectives
+        assert lies[0].params == b.params
+
+    def test_strategy_lie_values(self):
+        s = MaxParallelStrategy()
+        s.observe([(1,), (2,)], [{"objective": 4.0}, {"objective": 9.0}])
+        t = Trial(status="reserved", params=[dict(name="/x", type="real", value=1.0)])
+        assert s.lie(t).value == 9.0
+
+    def test_duplicates_are_not_registered_twice(self):
+        exp = _exp(priors={"/c": "choices(['a', 'b'])"}, pool_size=3,
+                   algorithms={"random": {"seed": 0}})
+        prod = Producer(exp, max_idle_time=2, backoff_max=0.01)
+        try:
+            prod.produce()
+        except SampleTimeout:
+            pass
+        ids = [t.id for t in exp.fetch_trials()]
+        assert len(ids) == len(set(ids)) <= 2
+
+    def test_idle_timeout_when_algorithm_opts_out(self):
+        exp = _exp(priors={"/x": "uniform(0, 1)", "/s": "fidelity(1, 4, 2)"}, pool_size=1,
+                   algorithms={"asha": {"seed": 0, "num_rungs": 2, "num_brackets": 1}})
+        prod = Producer(exp, max_idle_time=0.3, backoff_max=0.05)
+        prod.produce()       # first rung point
+        prod.algorithm.suggest = lambda num=1: None      # opts out forever
+        prod.naive_algorithm = None
+        t0 = time.time()
+        with pytest.raises(SampleTimeout):
+            prod.produce()
+        assert time.time() - t0 < 5
+
+    def test_trials_history_lineage(self):
+        h = TrialsHistory()
+        a = Trial(params=[dict(name="/x", type="real", value=1.0)])
+        b = Trial(params=[dict(name="/x", type="real", value=2.0)])
+        h.update([a])
+        assert a in h and h.children == [a.id]
+        b.parents = [a.id]
+        h.update([b])
+        assert h.children == [b.id] and b in h
+
+
+# ------------------------------------------------------------------ consumer
+BLACK_BOX = textwrap.dedent("""\
+    import json, os, sys
+    args = sys.argv[1:]
+    x = float(args[args.index('--xx') + 1])
+    env = {k: os.environ.get(k) for k in ('ORION_EXPERIMENT_NAME', 'ORION_TRIAL_ID',
+                                          'ORION_WORKING_DIR', 'MOPT_RESULTS_PATH')}
+    with open(os.path.join(os.environ['ORION_WORKING_DIR'], 'seen.json'), 'w') as f:
+        json.dump({'args': args, 'env': env}, f)
+    if x > 4:
+        sys.exit(3)
+    with open(os.environ['ORION_RESULTS_PATH'], 'w') as f:
+        json.dump([{'name': 'q', 'type': 'objective', 'value': (x - 1) ** 2}], f)
+""")
+
+
+@pytest.fixture
+def script(tmp_path):
+    p = tmp_path / "box.py"
+    p.write_text(BLACK_BOX)
+    return str(p)
+
+
+def _bb_exp(script, tmp_path, name="bb", **kw):
+    return build_experiment(name, user_args=["--xx~uniform(-5, 5)", "--wd",
+                                             "{trial.working_dir}"],
+                            storage=_storage(), working_dir=str(tmp_path / "runs"),
+                            **kw)
+
+
+def _with_script(exp, script):
+    exp.metadata["user_script"] = script
+    return exp
+
+
+class TestConsumer:
+    def test_runs_black_box_and_records_result(self, script, tmp_path):
+        exp = _with_script(_bb_exp(script, tmp_path), script)
+        t = Trial(experiment=exp.id, params=[dict(name="/xx", type="real", value=2.0)])
+        exp.register_trial(t)
+        t = exp.reserve_trial()
+        Consumer(exp, heartbeat=60).consume(t)
+        got = exp.get_trial(t)
+        assert got.status == "completed" and got.objective.value == pytest.approx(1.0)
+        wd = os.path.join(str(tmp_path / "runs"), f"bb_{t.id}")
+        seen = json.load(open(os.path.join(wd, "seen.json")))
+        assert seen["env"]["ORION_EXPERIMENT_NAME"] == "bb"
+        assert seen["env"]["ORION_TRIAL_ID"] == t.id
+        assert seen["env"]["ORION_WORKING_DIR"] == wd == seen["args"][-1]   # {trial.working_dir}
+        assert seen["env"]["MOPT_RESULTS_PATH"].startswith(wd)
+
+    def test_nonzero_exit_marks_broken(self, script, tmp_path):
+        exp = _with_script(_bb_exp(script, tmp_path, name="bb2"), script)
+        exp.register_trial(Trial(experiment=exp.id,
+                                 params=[dict(name="/xx", type="real", value=4.5)]))
+        t = exp.reserve_trial()
+        Consumer(exp, heartbeat=60).consume(t)
+        assert exp.get_trial(t).status == "broken"
+
+    def test_keyboard_interrupt_marks_interrupted(self, script, tmp_path, monkeypatch):
+        exp = _with_script(_bb_exp(script, tmp_path, name="bb3"), script)
+        exp.register_trial(Trial(experiment=exp.id,
+                                 params=[dict(name="/xx", type="real", value=0.0)]))
+        t = exp.reserve_trial()
+        cons = Consumer(exp, heartbeat=60)
+
+        def boom(*a, **k):
+            raise KeyboardInterrupt
+        monkeypatch.setattr(cons, "execute_process", boom)
+        with pytest.raises(KeyboardInterrupt):
+            cons.consume(t)
+        assert exp.get_trial(t).status == "interrupted"
+
+    def test_workon_until_done_and_max_broken(self, script, tmp_path):
+        exp = _with_script(_bb_exp(script, tmp_path, name="bb4", max_trials=4,
+                                   algorithms={"random": {"seed": 5}}), script)
+        workon(exp, consumer=Consumer(exp, heartbeat=60),
+               producer=Producer(exp, backoff_max=0.01))
+        statuses = [t.status for t in exp.fetch_trials()]
+        assert statuses.count("completed") >= 1
+        assert exp.is_done or exp.is_broken
+
+
+# ------------------------------------------------------------------ pacemaker
+class TestPacemaker:
+    def test_heartbeat_refreshes_then_stops_on_completion(self):
+        exp = _exp(name="hb")
+        exp.register_trial(Trial(experiment=exp.id,
+                                 params=[dict(name="/x", type="real", value=0.5)]))
+        t = exp.reserve_trial()
+        before = exp.get_trial(t).heartbeat
+        pm = TrialPacemaker(t, wait_time=0.05, storage=exp.storage)
+        pm.start()
+        time.sleep(0.3)
+        assert exp.get_trial(t).heartbeat > before
+        _complete(exp, t, 1.0)
+        time.sleep(0.3)
+        assert pm.stopped.is_set()
+        pm.stop()
+
+
+# ------------------------------------------------------------------ study API
+class TestStudy:
+    def test_suggest_observe_until_done(self):
+        exp = _exp(name="study", max_trials=5, algorithms={"random": {"seed": 3}})
+        study = Study(exp)
+        seen = []
+        while not study.is_done:
+            t = study.suggest()
+            assert t is not None and t.status == "reserved"
+            x = t.params[0].value
+            study.observe(t, (x - 1.0) ** 2)
+            seen.append(t.id)
+        assert len(set(seen)) == 5
+        assert study.stats["trials_completed"] == 5
+        assert study.stats["best_evaluation"] == min(
+            (t.params[0].value - 1.0) ** 2 for t in study.fetch_trials())
+
+    def test_observe_dict_results_and_release(self):
+        exp = _exp(name="study2", max_trials=3, algorithms={"random": {"seed": 4}})
+        study = Study(exp)
+        t = study.suggest()
+        study.release(t)
+        assert exp.get_trial(t).status == "interrupted"
+        t2 = study.suggest()
+        study.observe(t2, {"objective": 2.0, "statistic": 1.0})
+        got = exp.get_trial(t2)
+        assert got.objective.value == 2.0 and got.status == "completed"
+
+
+def test_report_results_writes_file_once(tmp_path, monkeypatch):
+    import importlib
+    path = tmp_path / "res.json"
+    path.write_text("")
+    monkeypatch.setenv("ORION_RESULTS_PATH", str(path))
+    import metaopt_amd.client as client
+    client = importlib.reload(client)
+    client.report_results([{"name": "o", "type": "objective", "value": 1.5}])
+    assert json.loads(path.read_text())[0]["value"] == 1.5
+    with pytest.raises(RuntimeWarning):
+        client.report_results([])
+    monkeypatch.delenv("ORION_RESULTS_PATH")
+    importlib.reload(client)
