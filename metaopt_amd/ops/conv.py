@@ -1,9 +1,12 @@
 """Convolution and BatchNorm operators of the population ResNet (north-star kernels K3, K8).
 
 A 3x3 convolution (pad 1, stride 1/2) over NHWC bf16 activations with the population folded into
-the batch dimension runs as HIP ``im2col`` + a population-batched GEMM (``torch.bmm`` on
-hipBLASLt) ``col[P, M, 9C] . W[P, 9C, Cout]``; its backward is the GEMM's autograd plus the HIP
-``col2im`` (gather form, no atomics).  BatchNorm with the residual add and ReLU fused into one
+the batch dimension is an implicit GEMM on the population MFMA kernel (``csrc/pgemm.hip``,
+``mopt_pconv``): the forward ``y = im2col(x) . W``, the input gradient (the transposed
+convolution ``dx = gather(dy) . W'``) and the weight gradient ``dW = im2col(x)^T . dy`` (split-K
+over pixels) gather their operands straight from the NHWC tensors, so no im2col / col2im matrix
+(9x the activation) is ever written to HBM; the weight gradient lands directly in the flat
+gradient buffer of the fused optimizer.  BatchNorm with the residual add and ReLU fused into one
 apply pass, per-trial batch statistics and running statistics, forward and backward, is HIP.
 
 fp32 PyTorch references of both (``conv3x3_ref``, ``bn_act_ref``) are the CPU backend and the
@@ -16,16 +19,15 @@ import ctypes
 import torch
 
 from . import _lib
-from .gemm import pbmm
+from .gemm import plan
 
 c_void_p, c_int, c_float, c_int64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_int64
 
 _lib.register_signatures({
-    "mopt_im2col": ([c_void_p, c_void_p] + [c_int] * 7 + [c_void_p], c_int),
-    "mopt_col2im": ([c_void_p, c_void_p] + [c_int] * 7 + [c_void_p], c_int),
     "mopt_bn_fwd": ([c_void_p] * 8 + [c_int, c_int64, c_int, c_float, c_float, c_int, c_int,
                                      c_void_p], c_int),
     "mopt_bn_bwd": ([c_void_p] * 8 + [c_int, c_int64, c_int, c_int, c_void_p], c_int),
+    "mopt_pconv": ([c_int] + [c_void_p] * 4 + [c_int] * 10 + [c_void_p], c_int),
 })
 
 
@@ -86,24 +88,55 @@ def bn_act_ref(x, gamma, beta, running, P, train, res=None, relu=True, eps=1e-5,
 
 
 # ------------------------------------------------------------------ HIP autograd Functions
-class _Im2Col(torch.autograd.Function):
+def _pow2(v):
+    return v >= 1 and (v & (v - 1)) == 0
+
+
+def _pconv(kind, a, b, out, P, Bn, H, W, Ci, Co, stride):
+    OH, OW = out_hw(H, stride), out_hw(W, stride)
+    M, N, K = {0: (Bn * OH * OW, Co, 9 * Ci), 1: (Bn * H * W, Ci, 9 * Co),
+               2: (9 * Ci, Co, Bn * OH * OW)}[kind]
+    cfg, splits, kps = plan(P, M, N, K)
+    if kind != 2:
+        splits, kps = 1, K
+    part = (torch.empty(splits, P, M, N, dtype=torch.float32, device=out.device)
+            if splits > 1 else None)
+    _call("mopt_pconv", kind, a.data_ptr(), b.data_ptr(), out.data_ptr(),
+          0 if part is None else part.data_ptr(), P, Bn, H, W, Ci, Co, stride, cfg, splits, kps,
+          _s(out))
+    return out
+
+
+class _Conv3x3(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, stride):
-        N, H, W, C = x.shape
-        OH, OW = out_hw(H, stride), out_hw(W, stride)
-        col = torch.empty(N * OH * OW, 9 * C, dtype=x.dtype, device=x.device)
-        _call("mopt_im2col", x.data_ptr(), col.data_ptr(), N, H, W, C, OH, OW, stride, _s(x))
-        ctx.dims = (N, H, W, C, OH, OW, stride)
-        return col
+    def forward(ctx, x, w, P, stride, grad_out):
+        N, H, W, Ci = x.shape
+        Co = w.shape[-1]
+        Bn = N // P
+        y = torch.empty(N, out_hw(H, stride), out_hw(W, stride), Co, dtype=x.dtype,
+                        device=x.device)
+        _pconv(0, x, w, y, P, Bn, H, W, Ci, Co, stride)
+        ctx.save_for_backward(x, w)
+        ctx.meta = (P, Bn, H, W, Ci, Co, stride)
+        ctx.grad_out = grad_out
+        return y
 
     @staticmethod
-    def backward(ctx, dcol):
-        N, H, W, C, OH, OW, stride = ctx.dims
-        dcol = dcol.contiguous()
-        dx = torch.empty(N, H, W, C, dtype=dcol.dtype, device=dcol.device)
-        _call("mopt_col2im", dcol.data_ptr(), dx.data_ptr(), N, H, W, C, OH, OW, stride,
-              _s(dcol))
-        return dx, None
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        P, Bn, H, W, Ci, Co, stride = ctx.meta
+        dy = dy.contiguous()
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            _pconv(1, dy, w, dx, P, Bn, H, W, Ci, Co, stride)
+        if ctx.needs_input_grad[1]:
+            if ctx.grad_out is not None:         # straight into the flat gradient buffer
+                _pconv(2, x, dy, ctx.grad_out, P, Bn, H, W, Ci, Co, stride)
+            else:
+                dw = torch.empty_like(w)
+                _pconv(2, x, dy, dw, P, Bn, H, W, Ci, Co, stride)
+        return dx, dw, None, None, None
 
 
 def conv3x3(x, w, P, stride):
@@ -111,9 +144,13 @@ def conv3x3(x, w, P, stride):
     if x.device.type != "cuda":
         return conv3x3_ref(x, w, P, stride)
     N, H, W, C = x.shape
-    col = _Im2Col.apply(x.contiguous(), stride)
-    out = pbmm(col.view(P, -1, 9 * C), w, w.grad if w.requires_grad and w.is_leaf else None)
-    return out.view(N, out_hw(H, stride), out_hw(W, stride), w.shape[-1])
+    Co = w.shape[-1]
+    if N % P or not all(_pow2(v) for v in (H, W, C, Co)) or C < 8 or Co < 8 or \
+            tuple(w.shape) != (P, 9 * C, Co):
+        raise ValueError(f"conv3x3: needs power-of-two H, W, channels (>= 8) and w [P, 9C, Co]; "
+                         f"got x {tuple(x.shape)} w {tuple(w.shape)} P {P}")
+    grad_out = w.grad if (w.requires_grad and w.is_leaf and w.grad is not None) else None
+    return _Conv3x3.apply(x.contiguous(), w.contiguous(), P, stride, grad_out)
 
 
 class _BNAct(torch.autograd.Function):

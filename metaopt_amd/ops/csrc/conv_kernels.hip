@@ -1,10 +1,8 @@
-// Convolution data movement and fused BatchNorm(+residual)(+ReLU) for the population ResNet
-// (north-star kernels K3 / K8).  Activations are NHWC bf16 with a leading population dimension
-// folded into N: x[(p * B + n)][h][w][c]; C is a multiple of 8 so every lane moves 16 bytes.
+// Fused BatchNorm(+residual)(+ReLU) for the population ResNet (north-star kernel K8; the
+// convolutions themselves are implicit GEMMs in pgemm.hip, K3).  Activations are NHWC bf16 with
+// a leading population dimension folded into N: x[(p * B + n)][h][w][c]; C is a multiple of 8 so
+// every lane moves 16 bytes.
 //
-//   im2col      x -> col[(n, oh, ow)][(kh, kw, c)]  (3x3, pad 1, stride 1 or 2, zero padding)
-//               so the convolution is a population-batched GEMM col[P, M, 9C] . W[P, 9C, Cout]
-//   col2im      dcol -> dx, in GATHER form (each input pixel sums its <= 9 taps): no atomics
 //   bn_stats    per (trial, channel) sum / sum of squares over the trial's N*H*W rows
 //   bn_finalize mean / rstd per (trial, channel), running-statistics update (momentum, unbiased)
 //   bn_apply    y = relu?(gamma (x - mean) rstd + beta + residual?)
@@ -27,62 +25,6 @@ __device__ __forceinline__ void unpack8(const uint4& u, float (&f)[8]) {
 __device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
   return make_uint4(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]),
                     pack2bf(f[6], f[7]));
-}
-
-// thread = (output pixel, tap, 8-channel chunk)
-__global__ __launch_bounds__(256) void im2col_kernel(const bf16_t* __restrict__ x,
-                                                     bf16_t* __restrict__ col, int N, int H,
-                                                     int W, int C, int OH, int OW, int stride) {
-  const int cc = C >> 3;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t total = (int64_t)N * OH * OW * 9 * cc;
-  if (i >= total) return;
-  const int ch = i % cc;
-  int64_t r = i / cc;
-  const int tap = r % 9;
-  r /= 9;                          // output pixel index (n, oh, ow)
-  const int ow = r % OW, oh = (r / OW) % OH;
-  const int64_t n = r / ((int64_t)OW * OH);
-  const int ih = oh * stride + tap / 3 - 1, iw = ow * stride + tap % 3 - 1;
-  uint4 v = make_uint4(0, 0, 0, 0);
-  if (ih >= 0 && ih < H && iw >= 0 && iw < W)
-    v = *(const uint4*)(x + (((n * H + ih) * W + iw) * C + 8 * ch));
-  *(uint4*)(col + (r * 9 + tap) * C + 8 * ch) = v;
-}
-
-// thread = (input pixel, 8-channel chunk): dx = sum over the taps that read this pixel
-__global__ __launch_bounds__(256) void col2im_kernel(const bf16_t* __restrict__ dcol,
-                                                     bf16_t* __restrict__ dx, int N, int H, int W,
-                                                     int C, int OH, int OW, int stride) {
-  const int cc = C >> 3;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t total = (int64_t)N * H * W * cc;
-  if (i >= total) return;
-  const int ch = i % cc;
-  int64_t r = i / cc;
-  const int iw = r % W, ih = (r / W) % H;
-  const int64_t n = r / ((int64_t)W * H);
-  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int kh = 0; kh < 3; ++kh) {
-    const int t = ih + 1 - kh;
-    if (t < 0 || t % stride) continue;
-    const int oh = t / stride;
-    if (oh >= OH) continue;
-#pragma unroll
-    for (int kw = 0; kw < 3; ++kw) {
-      const int u = iw + 1 - kw;
-      if (u < 0 || u % stride) continue;
-      const int ow = u / stride;
-      if (ow >= OW) continue;
-      float v[8];
-      unpack8(*(const uint4*)(dcol + ((((n * OH + oh) * OW + ow) * 9 + kh * 3 + kw) * C + 8 * ch)),
-              v);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) acc[e] += v[e];
-    }
-  }
-  *(uint4*)(dx + r * C + 8 * ch) = pack8(acc);
 }
 
 // grid (row chunks, P); thread = (row group, channel); C divides 256.
@@ -241,24 +183,6 @@ inline dim3 grid1(int64_t n) { return dim3((unsigned)((n + 255) / 256)); }
 }  // namespace
 
 extern "C" {
-
-int mopt_im2col(const void* x, void* col, int N, int H, int W, int C, int OH, int OW, int stride,
-                void* stream) {
-  if (C % 8) return 1;
-  const int64_t total = (int64_t)N * OH * OW * 9 * (C / 8);
-  hipLaunchKernelGGL(im2col_kernel, grid1(total), dim3(256), 0, (hipStream_t)stream,
-                     (const bf16_t*)x, (bf16_t*)col, N, H, W, C, OH, OW, stride);
-  return (int)hipGetLastError();
-}
-
-int mopt_col2im(const void* dcol, void* dx, int N, int H, int W, int C, int OH, int OW,
-                int stride, void* stream) {
-  if (C % 8) return 1;
-  const int64_t total = (int64_t)N * H * W * (C / 8);
-  hipLaunchKernelGGL(col2im_kernel, grid1(total), dim3(256), 0, (hipStream_t)stream,
-                     (const bf16_t*)dcol, (bf16_t*)dx, N, H, W, C, OH, OW, stride);
-  return (int)hipGetLastError();
-}
 
 // x [P][M][C] -> y; stat [P][2][C] (mean, rstd) out; running [P][2][C] in/out; sums scratch.
 int mopt_bn_fwd(const void* x, const void* gamma, const void* beta, const void* res, void* y,

@@ -28,7 +28,55 @@ namespace {
 constexpr int BK = 64;
 constexpr int LSK = BK + 8;  // row stride of k-contiguous LDS images (144 B)
 
-template <int ROWS, bool KCONTIG>
+// Operand sources.  Each operand is a stored matrix S[outer][inner] (inner contiguous) read in
+// 16-byte chunks S[o][i .. i+7]; at() returns the chunk's address, or nullptr outside the matrix
+// (the chunk is zero-filled).  Besides dense row-major storage, three gathers make a 3x3
+// convolution (pad 1, stride 1 or 2, NHWC, power-of-two spatial dims and channels) an implicit
+// GEMM -- no im2col / col2im matrix ever reaches HBM:
+//   kIm2col  S[pixel (b, oh, ow)][tap * C + c]  = x[b][oh*s + kh - 1][ow*s + kw - 1][c]
+//   kDgrad   S[pixel (b, h, w)][tap * Co + co]  = dY[b][(h + 1 - kh)/s][(w + 1 - kw)/s][co]
+//            (zero unless the division is exact: the stride-2 transposed convolution)
+//   kWdgrad  S[ci][tap * Co + co]               = W[tap * Ci + ci][co]
+enum SrcKind { kDense = 0, kIm2col = 1, kDgrad = 2, kWdgrad = 3 };
+
+struct Src {
+  const bf16_t* ptr;  // trial 0
+  int64_t batch;      // elements between trials
+  int ld;             // dense row stride
+  int n_outer, n_inner;
+  int hl2, wl2;       // log2 of the pixel grid enumerated by 'outer' (gathers)
+  int sh_l2, sw_l2;   // log2 of the gathered tensor's spatial dims
+  int cl2;            // log2 of the gathered tensor's channels
+  int stride;
+  int cin;            // kWdgrad: input channels of W
+};
+
+template <int KIND>
+__device__ __forceinline__ const bf16_t* src_at(const Src& s, const bf16_t* base, int o, int i) {
+  if (o >= s.n_outer || i >= s.n_inner) return nullptr;
+  if (KIND == kDense) return base + (int64_t)o * s.ld + i;
+  const int C = 1 << s.cl2;
+  const int tap = i >> s.cl2, c = i & (C - 1);
+  const int kh = tap / 3, kw = tap - 3 * kh;
+  if (KIND == kWdgrad) return base + ((int64_t)(tap * s.cin + o) << s.cl2) + c;
+  const int px = o & ((1 << s.wl2) - 1);
+  const int py = (o >> s.wl2) & ((1 << s.hl2) - 1);
+  const int b = o >> (s.hl2 + s.wl2);
+  int iy, ix;
+  if (KIND == kIm2col) {
+    iy = py * s.stride + kh - 1;
+    ix = px * s.stride + kw - 1;
+  } else {  // kDgrad
+    const int ny = py + 1 - kh, nx = px + 1 - kw;
+    if (s.stride == 2 && ((ny | nx) & 1)) return nullptr;
+    iy = s.stride == 2 ? ny >> 1 : ny;
+    ix = s.stride == 2 ? nx >> 1 : nx;
+  }
+  if (iy < 0 || ix < 0 || iy >= (1 << s.sh_l2) || ix >= (1 << s.sw_l2)) return nullptr;
+  return base + ((((int64_t)b << s.sh_l2 | iy) << s.sw_l2 | ix) << s.cl2) + c;
+}
+
+template <int ROWS, bool KCONTIG, int KIND>
 struct Img {
   static constexpr int LS = KCONTIG ? LSK : ROWS + 8;
   static constexpr int ELEMS = KCONTIG ? ROWS * LSK : BK * (ROWS + 8);
@@ -36,9 +84,11 @@ struct Img {
   static constexpr int NC = (CHUNKS + 255) / 256;
   static constexpr int RCH = ROWS / 8;          // chunks per k-row of a row-contiguous tile
 
-  // global -> registers: chunk c of the tile starting at (row0, k0); zero outside [R) x [k_end)
-  __device__ __forceinline__ static void load(uint4 (&r)[NC], const bf16_t* __restrict__ base,
-                                              int ld, int row0, int k0, int R, int k_end) {
+  // global -> registers: chunk c of the tile starting at (row0, k0); zero outside the matrix and
+  // past k_end (the split-K slice)
+  __device__ __forceinline__ static void load(uint4 (&r)[NC], const Src& s,
+                                              const bf16_t* __restrict__ base, int row0, int k0,
+                                              int k_end) {
 #pragma unroll
     for (int i = 0; i < NC; ++i) {
       const int c = threadIdx.x + 256 * i;
@@ -52,10 +102,10 @@ struct Img {
           gk = k0 + c / RCH;
           gr = row0 + 8 * (c % RCH);
         }
-        if (gr < R && gk < k_end) {
-          const bf16_t* src = KCONTIG ? base + (int64_t)gr * ld + gk : base + (int64_t)gk * ld + gr;
-          v = *(const uint4*)src;
-        }
+        const bf16_t* src = gk < k_end ? src_at<KIND>(s, base, KCONTIG ? gr : gk,
+                                                      KCONTIG ? gk : gr)
+                                       : nullptr;
+        if (src != nullptr) v = *(const uint4*)src;
       }
       r[i] = v;
     }
@@ -83,21 +133,20 @@ struct Img {
 };
 
 struct GemmArgs {
-  const bf16_t* A;
-  const bf16_t* B;
+  Src a, b;
   bf16_t* C;
   float* part;     // split-K partials [splits][P][M][N] (nullptr when splits == 1)
-  int64_t sA, sB, sC;
-  int P, M, N, K, lda, ldb, ldc;
+  int64_t sC;
+  int P, M, N, K, ldc;
   int tiles_m, tiles_n, splits, k_per_split, nwg;
 };
 
-template <bool TA, bool TB, int WM, int FM, int FN>
+template <int KA, int KB, bool TA, bool TB, int WM, int FM, int FN>
 __global__ __launch_bounds__(256) void pgemm_kernel(const GemmArgs g) {
   constexpr int WN = 4 / WM;
   constexpr int BM = WM * 16 * FM, BN = WN * 16 * FN;
-  using IA = Img<BM, !TA>;
-  using IB = Img<BN, TB>;
+  using IA = Img<BM, !TA, KA>;
+  using IB = Img<BN, TB, KB>;
   __shared__ __attribute__((aligned(16))) bf16_t smem[2 * (IA::ELEMS + IB::ELEMS)];
   constexpr int BUF = IA::ELEMS + IB::ELEMS;  // buffer b: A image at b*BUF, B image after it
 
@@ -109,8 +158,8 @@ __global__ __launch_bounds__(256) void pgemm_kernel(const GemmArgs g) {
   const int sp = t % g.splits;
   const int p = t / g.splits;
 
-  const bf16_t* A = g.A + p * g.sA;
-  const bf16_t* B = g.B + p * g.sB;
+  const bf16_t* A = g.a.ptr + p * g.a.batch;
+  const bf16_t* B = g.b.ptr + p * g.b.batch;
   const int m0 = tm * BM, n0 = tn * BN;
   const int kb = sp * g.k_per_split;
   const int ke = min(g.K, kb + g.k_per_split);
@@ -127,8 +176,8 @@ __global__ __launch_bounds__(256) void pgemm_kernel(const GemmArgs g) {
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   uint4 ra[IA::NC], rb[IB::NC];
-  IA::load(ra, A, g.lda, m0, kb, g.M, ke);
-  IB::load(rb, B, g.ldb, n0, kb, g.N, ke);
+  IA::load(ra, g.a, A, m0, kb, ke);
+  IB::load(rb, g.b, B, n0, kb, ke);
   IA::store(ra, smem);
   IB::store(rb, smem + IA::ELEMS);
   __syncthreads();
@@ -137,8 +186,8 @@ __global__ __launch_bounds__(256) void pgemm_kernel(const GemmArgs g) {
     const int cur = kt & 1;
     const bool more = kt + 1 < nk;
     if (more) {
-      IA::load(ra, A, g.lda, m0, kb + (kt + 1) * BK, g.M, ke);
-      IB::load(rb, B, g.ldb, n0, kb + (kt + 1) * BK, g.N, ke);
+      IA::load(ra, g.a, A, m0, kb + (kt + 1) * BK, ke);
+      IB::load(rb, g.b, B, n0, kb + (kt + 1) * BK, ke);
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -217,7 +266,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   C[p * sC + m * ldc + n] = f2bf(s);
 }
 
-template <bool TA, bool TB, int WM, int FM, int FN>
+template <int KA, int KB, bool TA, bool TB, int WM, int FM, int FN>
 int launch(GemmArgs g, hipStream_t st) {
   constexpr int BM = WM * 16 * FM, BN = (4 / WM) * 16 * FN;
   g.tiles_m = (g.M + BM - 1) / BM;
@@ -225,20 +274,54 @@ int launch(GemmArgs g, hipStream_t st) {
   const int64_t nwg = (int64_t)g.P * g.splits * g.tiles_m * g.tiles_n;
   if (nwg <= 0 || nwg > 0x7FFFFFFF) return (int)hipErrorInvalidValue;
   g.nwg = (int)nwg;
-  hipLaunchKernelGGL((pgemm_kernel<TA, TB, WM, FM, FN>), dim3(g.nwg), dim3(256), 0, st, g);
+  hipLaunchKernelGGL((pgemm_kernel<KA, KB, TA, TB, WM, FM, FN>), dim3(g.nwg), dim3(256), 0, st,
+                     g);
   return (int)hipGetLastError();
 }
 
-template <bool TA, bool TB>
+template <int KA, int KB, bool TA, bool TB>
 int dispatch_tile(const GemmArgs& g, int cfg, hipStream_t st) {
   switch (cfg) {
-    case 0: return launch<TA, TB, 2, 4, 4>(g, st);  // 128 x 128
-    case 1: return launch<TA, TB, 4, 2, 1>(g, st);  // 128 x 16
-    case 2: return launch<TA, TB, 4, 2, 2>(g, st);  // 128 x 32
-    case 3: return launch<TA, TB, 4, 1, 4>(g, st);  // 64 x 64
-    case 4: return launch<TA, TB, 2, 2, 4>(g, st);  // 64 x 128
+    case 0: return launch<KA, KB, TA, TB, 2, 4, 4>(g, st);  // 128 x 128
+    case 1: return launch<KA, KB, TA, TB, 4, 2, 1>(g, st);  // 128 x 16
+    case 2: return launch<KA, KB, TA, TB, 4, 2, 2>(g, st);  // 128 x 32
+    case 3: return launch<KA, KB, TA, TB, 4, 1, 4>(g, st);  // 64 x 64
+    case 4: return launch<KA, KB, TA, TB, 2, 2, 4>(g, st);  // 64 x 128
     default: return (int)hipErrorInvalidValue;
   }
+}
+
+template <int KA, int KB, bool TA, bool TB>
+int dispatch_conv_tile(const GemmArgs& g, int cfg, hipStream_t st) {
+  switch (cfg) {  // convolution GEMMs have N = channels <= 64
+    case 1: return launch<KA, KB, TA, TB, 4, 2, 1>(g, st);
+    case 2: return launch<KA, KB, TA, TB, 4, 2, 2>(g, st);
+    case 3: return launch<KA, KB, TA, TB, 4, 1, 4>(g, st);
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
+int finish_splitk(const GemmArgs& g, hipStream_t st) {
+  const int64_t total = (int64_t)g.P * g.M * g.N;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     st, (const float*)g.part, g.C, g.sC, g.ldc, g.P, g.M, g.N, g.splits);
+  return (int)hipGetLastError();
+}
+
+Src dense(const void* ptr, int64_t batch, int ld, int n_outer, int n_inner) {
+  Src s{};
+  s.ptr = (const bf16_t*)ptr;
+  s.batch = batch;
+  s.ld = ld;
+  s.n_outer = n_outer;
+  s.n_inner = n_inner;
+  return s;
+}
+
+int ilog2(int v) {
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  return (1 << l) == v ? l : -1;
 }
 
 }  // namespace
@@ -265,18 +348,92 @@ int mopt_pgemm(const void* A, const void* B, void* C, void* part, int P, int M, 
     return (int)hipErrorInvalidValue;
   }
   hipStream_t st = (hipStream_t)stream;
-  GemmArgs g{(const bf16_t*)A, (const bf16_t*)B, (bf16_t*)C, (float*)part, sA, sB, sC,
-             P, M, N, K, lda, ldb, ldc, 0, 0, splits, splits > 1 ? k_per_split : K, 0};
+  GemmArgs g{};
+  g.a = ta ? dense(A, sA, lda, K, M) : dense(A, sA, lda, M, K);
+  g.b = tb ? dense(B, sB, ldb, N, K) : dense(B, sB, ldb, K, N);
+  g.C = (bf16_t*)C;
+  g.part = (float*)part;
+  g.sC = sC;
+  g.P = P; g.M = M; g.N = N; g.K = K; g.ldc = ldc;
+  g.splits = splits;
+  g.k_per_split = splits > 1 ? k_per_split : K;
   int err;
-  if (!ta && !tb) err = dispatch_tile<false, false>(g, cfg, st);
-  else if (!ta && tb) err = dispatch_tile<false, true>(g, cfg, st);
-  else if (ta && !tb) err = dispatch_tile<true, false>(g, cfg, st);
-  else err = dispatch_tile<true, true>(g, cfg, st);
+  if (!ta && !tb) err = dispatch_tile<kDense, kDense, false, false>(g, cfg, st);
+  else if (!ta && tb) err = dispatch_tile<kDense, kDense, false, true>(g, cfg, st);
+  else if (ta && !tb) err = dispatch_tile<kDense, kDense, true, false>(g, cfg, st);
+  else err = dispatch_tile<kDense, kDense, true, true>(g, cfg, st);
   if (err || splits == 1) return err;
-  const int64_t total = (int64_t)P * M * N;
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                     st, (const float*)part, (bf16_t*)C, sC, ldc, P, M, N, splits);
-  return (int)hipGetLastError();
+  return finish_splitk(g, st);
+}
+
+// Implicit-GEMM 3x3 convolution (pad 1, stride 1|2) of a population, NHWC bf16:
+//   kind 0 forward  out y [P*Bn, OH, OW, Co] = conv(x [P*Bn, H, W, Ci], w [P, 9 Ci, Co])
+//   kind 1 dgrad    out dx [P*Bn, H, W, Ci]  from dy [P*Bn, OH, OW, Co] and w
+//   kind 2 wgrad    out dw [P, 9 Ci, Co]     from x and dy (split-K over pixels: ``part``)
+// a / b are (x, w), (dy, w), (x, dy).  H, W, Ci, Co powers of two, Ci >= 8, OH = H / stride.
+int mopt_pconv(int kind, const void* a, const void* b, void* out, void* part, int P, int Bn,
+               int H, int W, int Ci, int Co, int stride, int cfg, int splits, int k_per_split,
+               void* stream) {
+  const int hl = ilog2(H), wl = ilog2(W), cil = ilog2(Ci), col = ilog2(Co);
+  if (hl < 0 || wl < 0 || cil < 3 || col < 3 || (stride != 1 && stride != 2) ||
+      (stride == 2 && (hl < 1 || wl < 1)) || splits < 1 ||
+      (splits > 1 && (part == nullptr || k_per_split % BK))) {
+    return (int)hipErrorInvalidValue;
+  }
+  const int ohl = hl - (stride == 2), owl = wl - (stride == 2);
+  const int64_t x_batch = (int64_t)Bn << (hl + wl + cil);
+  const int64_t y_batch = (int64_t)Bn << (ohl + owl + col);
+  const int64_t w_batch = (int64_t)9 * Ci * Co;
+  const int out_pix = Bn << (ohl + owl), in_pix = Bn << (hl + wl);
+  hipStream_t st = (hipStream_t)stream;
+  GemmArgs g{};
+  g.C = (bf16_t*)out;
+  g.part = (float*)part;
+  g.P = P;
+  g.splits = splits;
+  Src im{};  // x gathered over the output grid
+  im.ptr = (const bf16_t*)a;
+  im.batch = x_batch;
+  im.hl2 = ohl; im.wl2 = owl; im.sh_l2 = hl; im.sw_l2 = wl; im.cl2 = cil; im.stride = stride;
+  int err;
+  if (kind == 0) {
+    g.M = out_pix; g.N = Co; g.K = 9 * Ci; g.ldc = Co; g.sC = y_batch;
+    im.n_outer = g.M; im.n_inner = g.K;
+    g.a = im;
+    g.b = dense(b, w_batch, Co, g.K, Co);
+    g.k_per_split = g.K;
+    g.splits = 1;
+    err = dispatch_conv_tile<kIm2col, kDense, false, false>(g, cfg, st);
+    return err;
+  }
+  if (kind == 1) {
+    g.M = in_pix; g.N = Ci; g.K = 9 * Co; g.ldc = Ci; g.sC = x_batch;
+    Src dg{};
+    dg.ptr = (const bf16_t*)a;
+    dg.batch = y_batch;
+    dg.n_outer = g.M; dg.n_inner = g.K;
+    dg.hl2 = hl; dg.wl2 = wl; dg.sh_l2 = ohl; dg.sw_l2 = owl; dg.cl2 = col; dg.stride = stride;
+    Src wd{};
+    wd.ptr = (const bf16_t*)b;
+    wd.batch = w_batch;
+    wd.n_outer = Ci; wd.n_inner = g.K; wd.cl2 = col; wd.cin = Ci;
+    g.a = dg;
+    g.b = wd;
+    g.k_per_split = g.K;
+    g.splits = 1;
+    return dispatch_conv_tile<kDgrad, kWdgrad, false, true>(g, cfg, st);
+  }
+  if (kind == 2) {
+    g.M = 9 * Ci; g.N = Co; g.K = out_pix; g.ldc = Co; g.sC = w_batch;
+    im.n_outer = g.K; im.n_inner = g.M;  // stored [pixel][tap * Ci + c] = [K][M]
+    g.a = im;
+    g.b = dense(b, y_batch, Co, g.K, Co);
+    g.k_per_split = splits > 1 ? k_per_split : g.K;
+    err = dispatch_conv_tile<kIm2col, kDense, true, false>(g, cfg, st);
+    if (err || splits == 1) return err;
+    return finish_splitk(g, st);
+  }
+  return (int)hipErrorInvalidValue;
 }
 
 }  // extern "C"

@@ -15,10 +15,14 @@ def _close(a, b, tol):
     assert err <= tol * (b.abs().max().item() + 1e-6), err
 
 
-@pytest.mark.parametrize("stride,C,Cout", [(1, 16, 16), (2, 16, 32), (1, 8, 16), (2, 32, 64)])
-def test_conv3x3_fwd_bwd(stride, C, Cout):
+@pytest.mark.parametrize("stride,C,Cout,B,H", [(1, 16, 16, 4, 16), (2, 16, 32, 4, 16),
+                                               (1, 8, 16, 4, 16), (2, 32, 64, 4, 16),
+                                               (1, 16, 16, 8, 32), (2, 64, 64, 2, 8)])
+def test_conv3x3_fwd_bwd(stride, C, Cout, B, H):
+    """Implicit-GEMM convolution (forward, transposed-conv input gradient, split-K weight
+    gradient) against the fp32 im2col reference."""
     torch.manual_seed(0)
-    P, B, H = 3, 4, 16
+    P = 3
     x = torch.randn(P * B, H, H, C, device=DEV).to(torch.bfloat16).requires_grad_(True)
     w = (0.1 * torch.randn(P, 9 * C, Cout, device=DEV)).to(torch.bfloat16).requires_grad_(True)
     out = cops.conv3x3(x, w, P, stride)
