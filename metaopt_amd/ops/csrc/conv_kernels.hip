@@ -3,7 +3,7 @@
 // a leading population dimension folded into N: x[(p * B + n)][h][w][c]; C is a multiple of 8 so
 // every lane moves 16 bytes.
 //
-//   bn_stats    per (trial, channel) sum / sum of squares over the trial's N*H*W rows
+//   bn_reduce   per (trial, channel) sums over the trial's N*H*W rows (statistics / backward)
 //   bn_finalize mean / rstd per (trial, channel), running-statistics update (momentum, unbiased)
 //   bn_apply    y = relu?(gamma (x - mean) rstd + beta + residual?)
 //   bn_bwd_*    dz = dy * relu'(y); sums of dz and dz * xhat; dx, dgamma, dbeta, dresidual
@@ -27,31 +27,78 @@ __device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
                     pack2bf(f[6], f[7]));
 }
 
-// grid (row chunks, P); thread = (row group, channel); C divides 256.
-__global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict__ x,
-                                                       float* __restrict__ sums, int64_t M,
-                                                       int C, int rows_per_block) {
-  __shared__ float s1[256], s2[256];
-  const int p = blockIdx.y, c = threadIdx.x % C, rg = threadIdx.x / C, ng = 256 / C;
+// Per (trial, channel) reductions over the trial's M rows, 16-byte loads: thread = (row group,
+// 8-channel chunk ch); a wave's lanes with the same ch are summed by xor-shuffles over the lane
+// bits above log2(C/8), then the 4 waves through LDS, then one atomic per (trial, channel) and
+// block.  grid (row chunks, P); C / 8 a power of two <= 64.
+//   BWD = false: sums[p][0][c] += x,  sums[p][1][c] += x^2                 (batch statistics)
+//   BWD = true:  dz = dy * relu'(y); sums[p][0][c] += dz, sums[p][1][c] += dz * xhat
+template <bool BWD>
+__global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict__ x,
+                                                        const bf16_t* __restrict__ y,
+                                                        const bf16_t* __restrict__ dy,
+                                                        const float* __restrict__ stat,
+                                                        float* __restrict__ sums, int64_t M,
+                                                        int C, int rows_per_block, int relu) {
+  __shared__ float red[4][2][64];
+  const int cc = C >> 3, p = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ch = tid & (cc - 1), rg = tid / cc, ng = 256 / cc;
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t r1 = min(r0 + rows_per_block, M);
-  const bf16_t* xp = x + (int64_t)p * M * C;
-  float a = 0.f, b = 0.f;
-  for (int64_t r = r0 + rg; r < r1; r += ng) {
-    const float v = bf2f(xp[r * C + c]);
-    a += v;
-    b += v * v;
-  }
-  s1[threadIdx.x] = a;
-  s2[threadIdx.x] = b;
-  __syncthreads();
-  if (rg == 0) {
-    for (int g = 1; g < ng; ++g) {
-      a += s1[g * C + c];
-      b += s2[g * C + c];
+  const int64_t base = (int64_t)p * M * C + 8 * ch;
+  float mean[8], rstd[8];
+  if (BWD) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      mean[e] = stat[(2 * p) * C + 8 * ch + e];
+      rstd[e] = stat[(2 * p + 1) * C + 8 * ch + e];
     }
-    atomicAdd(sums + (2 * p) * C + c, a);
-    atomicAdd(sums + (2 * p + 1) * C + c, b);
+  }
+  float a[8], b[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) a[e] = b[e] = 0.f;
+  for (int64_t r = r0 + rg; r < r1; r += ng) {
+    const int64_t o = base + r * C;
+    float xv[8];
+    unpack8(*(const uint4*)(x + o), xv);
+    if (!BWD) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        a[e] += xv[e];
+        b[e] += xv[e] * xv[e];
+      }
+    } else {
+      float dv[8], yv[8];
+      unpack8(*(const uint4*)(dy + o), dv);
+      if (relu) unpack8(*(const uint4*)(y + o), yv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float dz = (relu && yv[e] <= 0.f) ? 0.f : dv[e];
+        a[e] += dz;
+        b[e] += dz * (xv[e] - mean[e]) * rstd[e];
+      }
+    }
+  }
+  for (int off = 32; off >= cc; off >>= 1) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      a[e] += __shfl_xor(a[e], off, 64);
+      b[e] += __shfl_xor(b[e], off, 64);
+    }
+  }
+  if (lane < cc) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[wave][0][8 * lane + e] = a[e];
+      red[wave][1][8 * lane + e] = b[e];
+    }
+  }
+  __syncthreads();
+  if (tid < 2 * C) {
+    const int k = tid / C, c = tid % C;
+    const float v = red[0][k][c] + red[1][k][c] + red[2][k][c] + red[3][k][c];
+    atomicAdd(sums + (2 * p + k) * C + c, v);
   }
 }
 
@@ -108,40 +155,6 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
   *(uint4*)(y + row * C + 8 * ch) = pack8(v);
 }
 
-// dz = dy * relu'(y); per (p, c): sums[0] += dz, sums[1] += dz * xhat.  grid (row chunks, P).
-__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __restrict__ x,
-                                                            const bf16_t* __restrict__ y,
-                                                            const bf16_t* __restrict__ dy,
-                                                            const float* __restrict__ stat,
-                                                            float* __restrict__ sums, int64_t M,
-                                                            int C, int rows_per_block, int relu) {
-  __shared__ float s1[256], s2[256];
-  const int p = blockIdx.y, c = threadIdx.x % C, rg = threadIdx.x / C, ng = 256 / C;
-  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
-  const int64_t r1 = min(r0 + rows_per_block, M);
-  const int64_t base = (int64_t)p * M * C;
-  const float mean = stat[(2 * p) * C + c], rstd = stat[(2 * p + 1) * C + c];
-  float a = 0.f, b = 0.f;
-  for (int64_t r = r0 + rg; r < r1; r += ng) {
-    const int64_t o = base + r * C + c;
-    float dz = bf2f(dy[o]);
-    if (relu && bf2f(y[o]) <= 0.f) dz = 0.f;
-    a += dz;
-    b += dz * (bf2f(x[o]) - mean) * rstd;
-  }
-  s1[threadIdx.x] = a;
-  s2[threadIdx.x] = b;
-  __syncthreads();
-  if (rg == 0) {
-    for (int g = 1; g < ng; ++g) {
-      a += s1[g * C + c];
-      b += s2[g * C + c];
-    }
-    atomicAdd(sums + (2 * p) * C + c, a);
-    atomicAdd(sums + (2 * p + 1) * C + c, b);
-  }
-}
-
 // dx = gamma rstd (dz - sum(dz)/M - xhat sum(dz xhat)/M);  dres = dz.
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restrict__ x,
                                                            const bf16_t* __restrict__ y,
@@ -180,6 +193,16 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
 
 inline dim3 grid1(int64_t n) { return dim3((unsigned)((n + 255) / 256)); }
 
+// rows per reduction block: ~2048 blocks over the population, a multiple of the row groups
+inline int reduce_rows(int P, int64_t M, int C) {
+  const int ng = 256 / (C / 8);
+  int64_t rpb = ((int64_t)P * M + 2047) / 2048;
+  rpb = (rpb + ng - 1) / ng * ng;
+  return (int)(rpb > ng ? rpb : ng);
+}
+
+inline bool bn_shape_ok(int C) { return C >= 8 && C <= 512 && C % 8 == 0 && ((C / 8) & (C / 8 - 1)) == 0; }
+
 }  // namespace
 
 extern "C" {
@@ -188,13 +211,14 @@ extern "C" {
 int mopt_bn_fwd(const void* x, const void* gamma, const void* beta, const void* res, void* y,
                 void* stat, void* running, void* sums, int P, int64_t M, int C, float eps,
                 float momentum, int train, int relu, void* stream) {
-  if (C % 8 || 256 % C) return 1;
+  if (!bn_shape_ok(C)) return 1;
   hipStream_t st = (hipStream_t)stream;
   if (train) {
     (void)hipMemsetAsync(sums, 0, sizeof(float) * 2 * P * C, st);
-    const int rpb = 2048;
-    hipLaunchKernelGGL(bn_stats_kernel, dim3((unsigned)((M + rpb - 1) / rpb), P), dim3(256), 0,
-                       st, (const bf16_t*)x, (float*)sums, M, C, rpb);
+    const int rpb = reduce_rows(P, M, C);
+    hipLaunchKernelGGL(bn_reduce_kernel<false>, dim3((unsigned)((M + rpb - 1) / rpb), P),
+                       dim3(256), 0, st, (const bf16_t*)x, nullptr, nullptr, nullptr,
+                       (float*)sums, M, C, rpb, 0);
   }
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((P * C + 255) / 256), dim3(256), 0, st,
                      (const float*)sums, (float*)stat, (float*)running, P, C, M, eps, momentum,
@@ -209,12 +233,12 @@ int mopt_bn_fwd(const void* x, const void* gamma, const void* beta, const void* 
 int mopt_bn_bwd(const void* x, const void* y, const void* dy, const void* stat, const void* gamma,
                 void* dx, void* dres, void* sums, int P, int64_t M, int C, int relu,
                 void* stream) {
-  if (C % 8 || 256 % C) return 1;
+  if (!bn_shape_ok(C)) return 1;
   hipStream_t st = (hipStream_t)stream;
   (void)hipMemsetAsync(sums, 0, sizeof(float) * 2 * P * C, st);
-  const int rpb = 2048;
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3((unsigned)((M + rpb - 1) / rpb), P), dim3(256),
-                     0, st, (const bf16_t*)x, (const bf16_t*)y, (const bf16_t*)dy,
+  const int rpb = reduce_rows(P, M, C);
+  hipLaunchKernelGGL(bn_reduce_kernel<true>, dim3((unsigned)((M + rpb - 1) / rpb), P),
+                     dim3(256), 0, st, (const bf16_t*)x, (const bf16_t*)y, (const bf16_t*)dy,
                      (const float*)stat, (float*)sums, M, C, rpb, relu);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, grid1((int64_t)P * M * (C / 8)), dim3(256), 0, st,
                      (const bf16_t*)x, (const bf16_t*)y, (const bf16_t*)dy, (const float*)stat,
