@@ -83,8 +83,7 @@ class ASHA(BaseAlgorithm):
             for bracket, rungs in zip(self.brackets, state_dict["rungs"]):
                 bracket.rungs = [(b, {k: (o, tuple(p)) for k, (o, p) in r.items()})
                                  for b, r in rungs]
-                bracket._sorted = [sorted((o, k) for k, (o, _) in r.items() if o is not None)
-                                   for _, r in bracket.rungs]
+                bracket.rebuild_index()
             self.trial_info = {k: self.brackets[i] for k, i in state_dict["trial_info"].items()}
 
     def full_state(self) -> dict:
@@ -205,15 +204,31 @@ class ASHA(BaseAlgorithm):
 class Bracket:
     """Rungs ``[(budget, {id: (objective, point)})]`` of one ASHA bracket.
 
-    Each rung also keeps its completed entries sorted by objective (``bisect``), so a promotion
-    query is O(k) instead of re-sorting the rung (population sweeps put thousands of points in the
-    bottom rung)."""
+    Each rung also keeps its completed entries sorted by objective, and separately the completed
+    entries not yet present in the next rung (``bisect``): a promotion query is then the best
+    un-promoted entry, checked against the top-k rank by one binary search -- O(log n) instead of
+    re-sorting or scanning the rung (population sweeps put thousands of points in it)."""
 
     def __init__(self, asha, reduction_factor, budgets):
         self.asha = asha
         self.reduction_factor = reduction_factor
         self.rungs = [(int(b), dict()) for b in budgets]
         self._sorted = [[] for _ in budgets]
+        self._free = [[] for _ in budgets]
+
+    def rebuild_index(self):
+        """Recompute the sorted views after the rungs were replaced wholesale (set_state)."""
+        self._sorted = [sorted((o, k) for k, (o, _) in r.items() if o is not None)
+                        for _, r in self.rungs]
+        self._free = [[e for e in self._sorted[i]
+                       if i + 1 >= len(self.rungs) or e[1] not in self.rungs[i + 1][1]]
+                      for i in range(len(self.rungs))]
+
+    @staticmethod
+    def _discard(lst, entry):
+        j = bisect.bisect_left(lst, entry)
+        if j < len(lst) and lst[j] == entry:
+            del lst[j]
 
     def register(self, point, objective, overwrite=True):
         fid = point[self.asha.fidelity_index]
@@ -228,23 +243,28 @@ class Bracket:
             return
         old = rung.get(_id)
         if old is not None and old[0] is not None:
-            srt = self._sorted[i]
-            j = bisect.bisect_left(srt, (old[0], _id))
-            if j < len(srt) and srt[j] == (old[0], _id):
-                del srt[j]
+            self._discard(self._sorted[i], (old[0], _id))
+            self._discard(self._free[i], (old[0], _id))
         rung[_id] = (objective, tuple(point))
         if objective is not None:
             bisect.insort(self._sorted[i], (objective, _id))
+            if i + 1 >= len(self.rungs) or _id not in self.rungs[i + 1][1]:
+                bisect.insort(self._free[i], (objective, _id))
+        if i > 0 and old is None:   # entering rung i = promoted out of rung i - 1
+            below = self.rungs[i - 1][1].get(_id)
+            if below is not None and below[0] is not None:
+                self._discard(self._free[i - 1], (below[0], _id))
 
     def get_candidate(self, rung_id):
+        """Best completed entry of the rung's top ``len(rung) // eta`` not promoted yet."""
+        free = self._free[rung_id]
+        if not free:
+            return None
         _, rung = self.rungs[rung_id]
-        nxt = self.rungs[rung_id + 1][1]
-        srt = self._sorted[rung_id]
-        k = min(len(rung) // self.reduction_factor, len(srt))
-        for i in range(k):
-            _id = srt[i][1]
-            if _id not in nxt:
-                return rung[_id][1]
+        k = min(len(rung) // self.reduction_factor, len(self._sorted[rung_id]))
+        best = free[0]
+        if bisect.bisect_left(self._sorted[rung_id], best) < k:
+            return rung[best[1]][1]
         return None
 
     @property

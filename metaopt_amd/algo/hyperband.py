@@ -29,6 +29,8 @@ def _nonfid_key(point, fi):
 
 @ALGORITHMS.register()
 class Hyperband(BaseAlgorithm):
+    synchronous = True   # one bracket at a time: a rung advances when all its results are in
+
     def __init__(self, space, seed=None, repetitions=1):
         super().__init__(space, seed=seed, repetitions=repetitions)
         fids = [i for i, d in enumerate(self.space.values()) if _is_fidelity(d)]

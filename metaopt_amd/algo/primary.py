@@ -50,12 +50,14 @@ class PrimaryAlgo(BaseAlgorithm):
             out.append(tuple(_plain(v) for v in self.transformed_space.reverse(p)))
         return out
 
-    def observe(self, points, results):
+    def observe(self, points, results, check=True):
+        """``check=False``: the caller vouches that the points came from :meth:`suggest` (which
+        validated them) -- the device sweep observes thousands of points per sync."""
         if len(points) != len(results):
             raise ValueError("points and results differ in length")
         tpoints = []
         for p in points:
-            if p not in self.space:
+            if check and p not in self.space:
                 raise ValueError(f"Point {p} is not contained in space {self.space}")
             tpoints.append(self.transformed_space.transform(p))
         self.algorithm.observe(tpoints, results)

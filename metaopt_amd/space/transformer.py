@@ -339,11 +339,39 @@ class TransformedDimension:
 class TransformedSpace(Space):
     contains = TransformedDimension
 
+    def _is_identity(self) -> bool:
+        """True when no dimension is transformed (e.g. ASHA / random / PBT on any space): points
+        then pass through unchanged and membership is the original dimensions' -- the device
+        sweep moves thousands of points per sync through here."""
+        cache = getattr(self, "_identity_cache", None)
+        if cache is None or cache[0] != len(self):
+            ident = all(isinstance(d.transformer, Compose) and not d.transformer.transformers
+                        for d in self.values())
+            cache = (len(self), ident)
+            self._identity_cache = cache
+        return cache[1]
+
     def transform(self, point):
+        if self._is_identity():
+            return tuple(point)
         return tuple(dim.transform(point[i]) for i, dim in enumerate(self.values()))
 
     def reverse(self, transformed_point):
+        if self._is_identity():
+            return tuple(transformed_point)
         return tuple(dim.reverse(transformed_point[i]) for i, dim in enumerate(self.values()))
+
+    def __contains__(self, value):
+        if isinstance(value, str) or not self._is_identity():
+            return super().__contains__(value)
+        try:
+            n = len(value)
+        except TypeError as exc:
+            raise TypeError("Can check only for dimension names or "
+                            "for tuples with parameter values.") from exc
+        if not self or n != len(self):
+            return False
+        return all(v in d.original_dimension for v, d in zip(value, self._sorted_values()))
 
 
 def build_required_space(requirements, original_space: Space) -> TransformedSpace:

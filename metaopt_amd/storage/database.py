@@ -371,7 +371,10 @@ class _Collection:
                     raise DuplicateKeyError(f"Duplicate key error: index={name} value={v}")
                 values.add(v)
         self.indexes[name] = (fields, unique, values)
-        if len(fields) == 1 and fields[0] != "_id" and fields[0] not in self.hash_index:
+        # hash index only for scalar fields queried by equality / $in ("results" holds a list of
+        # result documents: hashing it on every update cost more than all other indexing)
+        if len(fields) == 1 and fields[0] not in ("_id", "results") and \
+                fields[0] not in self.hash_index:
             hidx: Dict[Any, set] = {}
             for hid, d in self.docs.items():
                 hidx.setdefault(self._hval(d, fields[0]), set()).add(hid)
@@ -459,9 +462,12 @@ class _Collection:
         return best
 
     def find_iter(self, query):
-        if query and set(query) == {"_id"} and not isinstance(query["_id"], dict):
+        if query and "_id" in query and not isinstance(query["_id"], dict):
+            # primary-key lookup, then the other clauses (compare-and-swap updates)
             d = self.docs.get(_hashable(query["_id"]))
-            return [d] if d is not None else []
+            if d is None or (len(query) > 1 and not match(d, query)):
+                return []
+            return [d]
         if query:
             cands = self._candidates(query)
             if cands is not None:

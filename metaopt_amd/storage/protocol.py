@@ -185,6 +185,18 @@ class DocumentStorage(BaseStorageProtocol):
         """Bulk registration (device populations register hundreds of trials per suggest)."""
         return self._db.write("trials", [t.to_dict() for t in trials])
 
+    def register_trial_docs(self, docs: List[dict]) -> int:
+        """Bulk registration of ready-made trial documents (the Trial schema, ``_id`` included):
+        the device sweep builds them without Trial objects."""
+        return self._db.write("trials", list(docs))
+
+    def update_trial_doc(self, uid, fields: dict, was: Optional[str] = None) -> int:
+        """Set ``fields`` of trial ``uid`` (compare-and-swap on the status when ``was`` is set)."""
+        where = {"_id": uid}
+        if was is not None:
+            where["status"] = was
+        return self._db.write("trials", data=fields, query=where)
+
     def register_lie(self, trial: Trial):
         return self._db.write("lying_trials", trial.to_dict())
 

@@ -27,6 +27,7 @@ from __future__ import annotations
 import collections
 import gc
 import datetime
+import hashlib
 import logging
 import math
 import time
@@ -35,11 +36,10 @@ from typing import Dict, List, Optional
 import numpy as np
 import torch
 
-from ..core.trial import Trial
+from ..algo.primary import PrimaryAlgo
 from ..ops.population import MemberConfig, PopulationMLP
 from ..parallel.comm import Comm
 from ..storage.database import DuplicateKeyError
-from ..utils import format_trials
 
 log = logging.getLogger(__name__)
 
@@ -77,8 +77,11 @@ class PopulationSweep:
         self.samples = 0
         self.done = False
         # rank-0 bookkeeping
-        self.trials: Dict[int, Trial] = {}            # key -> reserved trial
+        # in-flight trials as storage documents (the Trial schema of core/trial.py, built
+        # directly: object construction and re-hashing per trial dominated rank 0's host time)
+        self.trials: Dict[int, dict] = {}             # key -> reserved trial document
         self.key_params: Dict[int, dict] = {}
+        self.key_pkey: Dict[int, str] = {}
         self.ckpt_index: Dict[str, tuple] = {}        # param key -> (rank, trial key, steps)
         self._ckpt_pkey: Dict[tuple, str] = {}        # (rank, trial key) -> param key
         self.ckpt_fifo = [collections.deque() for _ in range(self.comm.world_size)]
@@ -113,6 +116,10 @@ class PopulationSweep:
             self.algorithm = experiment.algorithms
             self.space = experiment.space
             self._writer = _WriteBehind(experiment.storage)
+            self._dim_names = list(self.space.keys())
+            self._dim_types = [d.type for d in self.space.values()]
+            self._exp_str = str(experiment.id)
+            self._sec_name = getattr(task, "secondary_stat", "val_acc")
 
     def _gc_callback(self, phase, info):
         if phase == "start":
@@ -304,6 +311,7 @@ class PopulationSweep:
                         self._mirror_save(rank, key)
                     if bad and key in self.trials:
                         self.key_params.pop(key, None)
+                        self.key_pkey.pop(key, None)
                         self.broken += 1
                         self._set_status(self.trials.pop(key), "broken")
             # 2) the result of the member that finished in this slot (this sync or, pipelined,
@@ -311,34 +319,37 @@ class PopulationSweep:
             rkey = int(gathered[row, 4])
             if rkey < 0:
                 continue
-            trial = self.trials.pop(rkey, None)
+            doc = self.trials.pop(rkey, None)
             params = self.key_params.pop(rkey, None)
-            if trial is None:
+            pkey = self.key_pkey.pop(rkey, None)
+            if doc is None:
                 continue
             if gathered[row, 8] > 0:
                 self.broken += 1
-                self._set_status(trial, "broken")
+                self._set_status(doc, "broken")
                 continue
             vl, va, tl = float(gathered[row, 6]), float(gathered[row, 7]), float(gathered[row, 5])
-            trial.results = [Trial.Result(name="val_loss", type="objective", value=vl),
-                             Trial.Result(name=getattr(self.task, "secondary_stat", "val_acc"),
-                                          type="statistic", value=va),
-                             Trial.Result(name="train_loss", type="statistic", value=tl)]
-            trial.status = "completed"
-            trial.end_time = now
-            self._writer.put("complete_trial", trial)
+            self._writer.put_update(doc["_id"], {
+                "results": [{"name": "val_loss", "type": "objective", "value": vl},
+                            {"name": self._sec_name, "type": "statistic", "value": va},
+                            {"name": "train_loss", "type": "statistic", "value": tl}],
+                "status": "completed", "end_time": now, "heartbeat": doc["heartbeat"]})
             self.completed += 1
             budget = int(self.task.budget(params))
             self.history.append((time.time(), rkey, vl, budget))
             if vl < self.best[0]:
                 self.best = (vl, dict(params))
-            done_pts.append(format_trials.trial_to_tuple(trial, self.space))
+            done_pts.append(tuple(params[k] for k in self._dim_names))
             done_res.append({"objective": vl, "constraint": [], "gradient": None})
             if budget < max_b:
-                self._index_ckpt(self.task.key(params), rank, rkey, budget)
+                self._index_ckpt(pkey, rank, rkey, budget)
         t0 = time.perf_counter()
         if done_pts:
-            self.algorithm.observe(done_pts, done_res)
+            if isinstance(self.algorithm, PrimaryAlgo):
+                # the points came out of this algorithm's suggest(), validated there
+                self.algorithm.observe(done_pts, done_res, check=False)
+            else:
+                self.algorithm.observe(done_pts, done_res)
         t1 = time.perf_counter()
         self._heartbeat()
         self._fill(free, assign)
@@ -389,10 +400,11 @@ class PopulationSweep:
         if not points and in_flight == 0:
             self.done = True
             return
-        free_by_rank = {r: [row for row in free_rows if row // P == r] for r in range(W)}
+        free_by_rank = {r: collections.deque(row for row in free_rows if row // P == r)
+                        for r in range(W)}
         stamp = datetime.datetime.utcnow()
         parent_of = getattr(self.algorithm, "parent_of", None)
-        keys = self.space.keys()
+        keys = self._dim_names
         for point in points:
             params = dict(zip(keys, point))
             pkey = self.task.key(params)
@@ -405,48 +417,59 @@ class PopulationSweep:
             src = -1
             if owner is not None and free_by_rank[owner[0]]:
                 # resume next to the checkpoint (no copy between GPUs)
-                row = free_by_rank[owner[0]].pop(0)
+                row = free_by_rank[owner[0]].popleft()
                 action, resume, src = RESUME, owner[1], owner[0]
             else:
                 rank = max(free_by_rank, key=lambda r: len(free_by_rank[r]))
                 if not free_by_rank[rank]:
                     break
-                row = free_by_rank[rank].pop(0)
+                row = free_by_rank[rank].popleft()
                 if owner is not None:   # C4: the owner sends the checkpoint to that rank (P2P)
                     action, resume, src = RESUME, owner[1], owner[0]
                 else:
                     action, resume = NEW, -1
-            trial = format_trials.tuple_to_trial(point, self.space)
-            trial.experiment = self.experiment.id
-            if parent is not None:
-                ptrial = format_trials.tuple_to_trial(parent, self.space)
-                ptrial.experiment = self.experiment.id
-                trial.parents = [ptrial.id]
-            trial.status = "reserved"
-            trial.submit_time = trial.start_time = trial.heartbeat = stamp
-            if trial.id in self._registered:
+            tid = self._doc_id(point)
+            if tid in self._registered:
                 log.debug("duplicate point %s skipped", point)
-                free_by_rank[row // P].insert(0, row)
+                free_by_rank[row // P].appendleft(row)
                 continue
-            self._registered.add(trial.id)
-            self._writer.put("register_trial", trial)
+            self._registered.add(tid)
+            doc = {"experiment": self.experiment.id, "status": "reserved", "worker": None,
+                   "heartbeat": stamp, "submit_time": stamp, "start_time": stamp,
+                   "end_time": None, "results": [],
+                   "params": [{"name": n, "type": t, "value": v}
+                              for n, t, v in zip(keys, self._dim_types, point)],
+                   "parents": [self._doc_id(parent)] if parent is not None else [],
+                   "_id": tid}
+            self._writer.put_register(doc)
             key = self.next_key
             self.next_key += 1
-            self.trials[key] = trial
+            self.trials[key] = doc
             self.key_params[key] = params
+            self.key_pkey[key] = pkey
             cfg = self.task.member_config(params, self.task.seed_of(pkey))
             assign[row] = (action, key, cfg.width, cfg.lr, cfg.momentum, cfg.weight_decay,
                            cfg.dropout, cfg.seed, self.task.budget(params), resume, src)
 
-    def _set_status(self, trial, status):
-        self._writer.put("set_trial_status", trial, status, was="reserved")
+    def _doc_id(self, point) -> str:
+        """``Trial.id`` of ``point`` in this experiment (md5 of ``params_repr`` + experiment id,
+        core/trial.py), without building the Trial object."""
+        rep = ",".join(f"{n}:{v}" for n, v in zip(self._dim_names, point))
+        return hashlib.md5((rep + self._exp_str).encode("utf-8")).hexdigest()
+
+    def _set_status(self, doc, status):
+        self._writer.put_update(doc["_id"], {"status": status,
+                                             "heartbeat": datetime.datetime.utcnow()},
+                                was="reserved")
 
     def _heartbeat(self):
         if time.time() - self._last_hb < self.heartbeat_every:
             return
         self._last_hb = time.time()
-        for t in list(self.trials.values()):
-            self._writer.put("update_heartbeat", t)
+        now = datetime.datetime.utcnow()
+        for doc in list(self.trials.values()):
+            doc["heartbeat"] = now
+            self._writer.put_update(doc["_id"], {"heartbeat": now}, was="reserved")
 
     def flush(self) -> None:
         """Wait until every queued storage write has been applied."""
@@ -578,23 +601,16 @@ class PopulationSweep:
                                      for k, v in self.timers.items()}}
 
 
-class _Snapshot:
-    __slots__ = ("doc",)
-
-    def __init__(self, doc):
-        self.doc = doc
-
-
 class _WriteBehind:
     """Storage writes taken off the decision path (write-behind).
 
     The sweep's decisions never read back what it writes (rank 0 keeps its own bookkeeping), so
-    persisting trials -- registration, results, status changes, heartbeats -- is deferred: ``put``
-    snapshots the arguments; ``drain_while(busy)`` applies held writes in order, one unit at a
-    time, for as long as ``busy()`` says the GPU is still working on the interval just queued, so
-    the host does its bookkeeping inside the device time instead of after it (no helper thread:
-    a thread would need the GIL that the waiting thread holds).  Consecutive registrations become
-    one bulk insert.  ``flush`` applies everything.
+    persisting trials -- registration, results, status changes, heartbeats -- is deferred as
+    document operations: ``put_register`` / ``put_update`` queue them; ``drain_while(busy)``
+    applies held writes in order, one unit at a time, for as long as ``busy()`` says the GPU is
+    still working on queued work, so the host does its bookkeeping inside the device time
+    instead of after it (no helper thread: a thread would need the GIL that the waiting thread
+    holds).  Consecutive registrations become one bulk insert.  ``flush`` applies everything.
     """
 
     def __init__(self, storage):
@@ -603,11 +619,14 @@ class _WriteBehind:
         self._held: "collections.deque" = collections.deque()
         self.busy_s = 0.0             # seconds spent applying writes
 
-    def put(self, method, *args, **kwargs):
-        # snapshot trials (the sweep keeps mutating its objects after queueing them); the Trial
-        # objects are rebuilt from the snapshots when the write is applied
-        args = tuple(_Snapshot(a.to_dict()) if isinstance(a, Trial) else a for a in args)
-        self._held.append((method, args, kwargs))
+    def put_register(self, doc: dict):
+        """Register a trial document (a shallow copy: the sweep replaces, never mutates, the
+        fields it changes later)."""
+        self._held.append(("register", dict(doc)))
+
+    def put_update(self, uid, fields: dict, was=None):
+        """Set ``fields`` of trial ``uid`` (only while its status is ``was``, when given)."""
+        self._held.append(("update", (uid, fields, was)))
 
     def __len__(self):
         return len(self._held)
@@ -619,43 +638,36 @@ class _WriteBehind:
         self.busy_s += time.perf_counter() - t0
 
     def _take(self):
-        """Next unit of work: a run of registrations (one bulk insert of <= 64 documents) or a
-        single write."""
+        """Next unit of work: a run of registrations (one bulk insert of <= 256 documents) or a
+        single update."""
         first = self._held.popleft()
         item = [first]
-        if first[0] == "register_trial":
-            while self._held and len(item) < 64 and self._held[0][0] == "register_trial":
+        if first[0] == "register":
+            while self._held and len(item) < 256 and self._held[0][0] == "register":
                 item.append(self._held.popleft())
         return item
 
     def _apply_batch(self, held):
-        i = 0
-        while i < len(held):
-            method, args, kwargs = held[i]
-            if method == "register_trial":   # consecutive registrations: one bulk insert
-                j = i
-                while j < len(held) and held[j][0] == "register_trial":
-                    j += 1
-                trials = [Trial(**h[1][0].doc) for h in held[i:j]]
-                self._apply("register_trials", (trials,), {}, fallback=trials)
-                i = j
-                continue
-            args = tuple(Trial(**a.doc) if isinstance(a, _Snapshot) else a for a in args)
-            self._apply(method, args, kwargs)
-            i += 1
+        if held[0][0] == "register":
+            docs = [h[1] for h in held]
+            if not self._call("register_trial_docs", docs):
+                for d in docs:            # a bulk insert hit a duplicate: insert one by one
+                    self._call("register_trial_docs", [d])
+            return
+        for _, (uid, fields, was) in held:
+            self._call("update_trial_doc", uid, fields, was=was)
 
-    def _apply(self, method, args, kwargs, fallback=None):
+    def _call(self, method, *args, **kwargs) -> bool:
         try:
             getattr(self.storage, method)(*args, **kwargs)
+            return True
         except DuplicateKeyError:
-            if fallback is None:
-                log.debug("duplicate write skipped (%s)", method)
-                return
-            for t in fallback:           # a bulk insert hit a duplicate: insert one by one
-                self._apply("register_trial", (t,), {})
+            log.debug("duplicate write skipped (%s)", method)
+            return False
         except Exception as exc:  # pragma: no cover - storage hiccup
             self.errors += 1
             log.warning("storage write %s failed: %s", method, exc)
+            return True
 
     def flush(self):
         """Apply every held write."""

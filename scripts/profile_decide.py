@@ -1,7 +1,8 @@
 """Host cost of the sweep's rank-0 decision step (ASHA observe/suggest, trial bookkeeping) on CPU.
 
-Simulates a 256-slot population where every member reaches its budget on schedule, so the
-decision path sees the same completion/placement volume as the GPU bench, without a GPU.
+Simulates ``WORLD`` ranks x 256 slots where every member reaches its budget on schedule, so the
+decision path sees the same completion/placement volume as the GPU bench at that GPU count,
+without a GPU:  ``WORLD=8 python scripts/profile_decide.py [--profile]``.
 """
 import cProfile
 import os
@@ -30,16 +31,30 @@ class _FakePop:
         pass
 
 
-def main(n_syncs=40, P=256, profile=False):
+class _FakeComm:
+    def __init__(self, world):
+        self.world_size, self.rank, self.is_root = world, 0, True
+        self.distributed = False
+        import torch
+        self.device = torch.device("cpu")
+
+    def broadcast_object(self, obj, src=0):
+        return obj
+
+
+def main(n_syncs=40, P=256, world=1, profile=False):
     task = MLPSweepTask(priors=dict(MLP_PRIORS), max_width=1024)
     exp = build_experiment("decide-prof", priors=dict(MLP_PRIORS),
                            algorithms={"asha": {"seed": 0, "repetitions": float("inf")}},
                            storage=DocumentStorage(EphemeralDB()), pool_size=P)
-    sw = PopulationSweep(_FakePop(P), task, data=None, experiment=exp, sync_every=32)
+    sw = PopulationSweep(_FakePop(P), task, data=None, comm=_FakeComm(world), experiment=exp,
+                         sync_every=32, pipelined=False)
+    P = P * world                      # rows of the gathered status block
     rng = np.random.default_rng(0)
     steps = np.zeros(P)
-    gathered = np.zeros((P, 7))
+    gathered = np.zeros((P, 9))
     gathered[:, 0] = -1
+    gathered[:, 4] = -1
     assign = sw._decide(gathered)
     prof = cProfile.Profile() if profile else None
     t_total = t_rel = 0.0
@@ -57,8 +72,12 @@ def main(n_syncs=40, P=256, profile=False):
         gathered[:, 1] = steps
         fin = (gathered[:, 0] >= 0) & (steps >= gathered[:, 2])
         n_done += int(fin.sum())
-        gathered[:, 3] = rng.random(P)
-        gathered[:, 4] = np.where(fin, rng.random(P), 0)
+        gathered[:, 3] = 0
+        gathered[:, 4] = np.where(fin, gathered[:, 0], -1)      # synchronous: results now
+        gathered[:, 5] = rng.random(P)
+        gathered[:, 6] = np.where(fin, rng.random(P), 0)
+        gathered[:, 7] = 0.5
+        gathered[:, 8] = 0
         t0 = time.perf_counter()
         if prof:
             prof.enable()
@@ -80,4 +99,5 @@ if __name__ == "__main__":
     if "--nogc" in sys.argv:
         import gc
         gc.disable()
-    main(n_syncs=int(os.environ.get("N_SYNCS", 40)), profile="--profile" in sys.argv)
+    main(n_syncs=int(os.environ.get("N_SYNCS", 40)), world=int(os.environ.get("WORLD", 1)),
+         profile="--profile" in sys.argv)

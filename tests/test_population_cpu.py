@@ -115,6 +115,12 @@ def test_sweep_asha_end_to_end(data, pipelined):
     assert sweep.n_resumed == sum(1 for b in budgets if b > 16)
     assert sweep.n_resume_missing == 0
     assert exp.stats["best_evaluation"] == pytest.approx(summary["best_val_loss"])
+    # the sweep writes trial documents directly: their ids are the Trial schema's md5 ids
+    from metaopt_amd.core.trial import Trial
+    docs = storage.database.read("trials", {})
+    assert docs and all(Trial(**dict(d)).id == d["_id"] for d in docs)
+    promoted = [d for d in docs if d["parents"]]
+    assert all(p in {d["_id"] for d in docs} for t in promoted for p in t["parents"])
 
 
 def test_sweep_marks_diverged_members_broken(data):
