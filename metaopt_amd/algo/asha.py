@@ -41,6 +41,8 @@ def _is_fidelity(dim) -> bool:
 class ASHA(BaseAlgorithm):
     """Asynchronous Successive Halving over the space's single ``fidelity`` dimension."""
 
+    trusted_suggestions = True   # space samples and promotions of already-validated points
+
     def __init__(self, space, seed=None, grace_period=None, max_resources=None,
                  reduction_factor=None, num_rungs=None, num_brackets=1, repetitions=1):
         super().__init__(space, seed=seed, max_resources=max_resources,
@@ -165,9 +167,21 @@ class ASHA(BaseAlgorithm):
         return out
 
     def get_id(self, point) -> str:
-        p = list(point)
-        non_fid = p[:self.fidelity_index] + p[self.fidelity_index + 1:]
-        return hashlib.md5(str(non_fid).encode("utf-8")).hexdigest()
+        """md5 of the non-fidelity values (the bracket key); memoised per point -- every point is
+        looked up at suggest, registration and observation."""
+        cache = self.__dict__.setdefault("_id_cache", {})
+        key = tuple(point)
+        _id = cache.get(key)
+        if _id is None:
+            fi = self.fidelity_index
+            # python scalars: numpy 2 reprs np.float64 values as 'np.float64(..)', which would
+            # give a sampled point and the same point observed back from storage two ids
+            p = [v.item() if isinstance(v, numpy.generic) else v for v in key]
+            _id = hashlib.md5(str(p[:fi] + p[fi + 1:]).encode("utf-8")).hexdigest()
+            if len(cache) > 1 << 20:
+                cache.clear()
+            cache[key] = _id
+        return _id
 
     def observe(self, points, results):
         for point, result in zip(points, results):
@@ -192,12 +206,21 @@ class ASHA(BaseAlgorithm):
         return self._repetition >= reps and all(b.is_done for b in self.brackets)
 
     @property
+    def space(self):
+        return self._space
+
+    @space.setter
+    def space(self, space):
+        self._space = space
+        self.__dict__.pop("_fidelity_index", None)   # re-derived for the new space
+        self.__dict__.pop("_id_cache", None)
+
+    @property
     def fidelity_index(self) -> int:
-        cached = self.__dict__.get("_fidelity_index")
-        if cached is not None and cached[0] is self.space:
-            return cached[1]
-        idx = [i for i, d in enumerate(self.space.values()) if _is_fidelity(d)][0]
-        self.__dict__["_fidelity_index"] = (self.space, idx)
+        idx = self.__dict__.get("_fidelity_index")
+        if idx is None:
+            idx = [i for i, d in enumerate(self.space.values()) if _is_fidelity(d)][0]
+            self.__dict__["_fidelity_index"] = idx
         return idx
 
 
@@ -232,11 +255,17 @@ class Bracket:
 
     def register(self, point, objective, overwrite=True):
         fid = point[self.asha.fidelity_index]
-        idx = [i for i, (b, _) in enumerate(self.rungs) if b == fid]
-        if not idx:
-            raise IndexError(f"Bad fidelity level {fid}. Should be in "
-                             f"{[b for b, _ in self.rungs]}. Params: {point}")
-        i = idx[0]
+        if fid == self.rungs[0][0]:
+            i = 0
+        else:
+            idx = [i for i, (b, _) in enumerate(self.rungs) if b == fid]
+            if not idx:
+                raise IndexError(f"Bad fidelity level {fid}. Should be in "
+                                 f"{[b for b, _ in self.rungs]}. Params: {point}")
+            i = idx[0]
+        self._register_at(i, point, objective, overwrite)
+
+    def _register_at(self, i, point, objective, overwrite):
         rung = self.rungs[i][1]
         _id = self.asha.get_id(point)
         if not overwrite and _id in rung:

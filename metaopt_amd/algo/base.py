@@ -43,6 +43,9 @@ class BaseAlgorithm:
     #: sync (PBT generations); device sweeps then decide synchronously instead of one interval
     #: behind the GPU (see ``PopulationSweep``)
     synchronous: bool = False
+    #: True for built-in algorithms whose points are draws of ``space.sample`` (or earlier
+    #: points): the primary wrapper then skips re-validating every suggested point
+    trusted_suggestions: bool = False
 
     def __init__(self, space, **kwargs):
         log.debug("Creating %s with parameters %s", type(self).__name__, kwargs)

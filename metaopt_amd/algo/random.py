@@ -10,6 +10,8 @@ from .base import ALGORITHMS, BaseAlgorithm
 class Random(BaseAlgorithm):
     """Sample points from the space's priors; observations are ignored."""
 
+    trusted_suggestions = True
+
     def __init__(self, space, seed=None):
         super().__init__(space, seed=seed)
 

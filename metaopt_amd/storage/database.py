@@ -79,6 +79,10 @@ _MISSING = object()
 
 
 def _get_path(doc, key: str):
+    if "." not in key:                      # top-level field: the common case
+        if isinstance(doc, dict):
+            return doc.get(key, _MISSING)
+        return _MISSING
     cur = doc
     for part in key.split("."):
         if isinstance(cur, dict) and part in cur:
@@ -256,10 +260,17 @@ def _touched_keys(data) -> set:
 
 
 def _affected(fields, touched) -> bool:
-    return touched is None or any(f.split(".", 1)[0] in touched for f in fields)
+    if touched is None:
+        return True
+    for f in fields:
+        if (f if "." not in f else f.split(".", 1)[0]) in touched:
+            return True
+    return False
 
 
 def _hashable(v):
+    if type(v) in _ATOMIC:
+        return v
     if isinstance(v, dict):
         return tuple(sorted((k, _hashable(x)) for k, x in v.items()))
     if isinstance(v, (list, tuple)):

@@ -119,6 +119,8 @@ class PopulationSweep:
             self._dim_names = list(self.space.keys())
             self._dim_types = [d.type for d in self.space.values()]
             self._exp_str = str(experiment.id)
+            # Trial.params_repr of a point is this template filled with its values
+            self._repr_tmpl = ",".join(f"{n}:{{}}" for n in self._dim_names)
             self._sec_name = getattr(task, "secondary_stat", "val_acc")
 
     def _gc_callback(self, phase, info):
@@ -454,8 +456,8 @@ class PopulationSweep:
     def _doc_id(self, point) -> str:
         """``Trial.id`` of ``point`` in this experiment (md5 of ``params_repr`` + experiment id,
         core/trial.py), without building the Trial object."""
-        rep = ",".join(f"{n}:{v}" for n, v in zip(self._dim_names, point))
-        return hashlib.md5((rep + self._exp_str).encode("utf-8")).hexdigest()
+        return hashlib.md5((self._repr_tmpl.format(*point) + self._exp_str)
+                           .encode("utf-8")).hexdigest()
 
     def _set_status(self, doc, status):
         self._writer.put_update(doc["_id"], {"status": status,
