@@ -516,6 +516,44 @@ class _Collection:
         self._unregister(doc)
         del self.docs[_hashable(doc["_id"])]
 
+    def insert_owned(self, docs) -> int:
+        """Bulk insert of documents the caller hands over (no defensive copy)."""
+        for d in docs:
+            if "_id" not in d:
+                self.insert(d)
+                continue
+            self._check_unique(d)
+            self.docs[_hashable(d["_id"])] = d
+            self._register(d)
+        return len(docs)
+
+    def set_fields_by_id(self, items) -> int:
+        """Bulk ``$set`` of top-level fields: ``items`` = [(id, {field: value}, status or None)],
+        each applied only while the document's status equals the given one (compare-and-swap).
+        Same result as :meth:`update` per item without the generic operator machinery."""
+        uniq = {f for fields, unique, _ in self.indexes.values() if unique for f in fields}
+        n = 0
+        for uid, fields, was in items:
+            hid = _hashable(uid)
+            d = self.docs.get(hid)
+            if d is None or (was is not None and d.get("status") != was):
+                continue
+            if "_id" in fields or uniq.intersection(fields):
+                self.update(d, fields)     # unique-indexed field: the checked generic path
+                n += 1
+                continue
+            for f, hidx in self.hash_index.items():
+                if f in fields:
+                    ids = hidx.get(self._hval(d, f))
+                    if ids is not None:
+                        ids.discard(hid)
+            d.update(_copy_doc(fields))
+            for f, hidx in self.hash_index.items():
+                if f in fields:
+                    hidx.setdefault(self._hval(d, f), set()).add(hid)
+            n += 1
+        return n
+
 
 @DATABASES.register("ephemeraldb")
 class EphemeralDB(AbstractDB):
@@ -565,6 +603,14 @@ class EphemeralDB(AbstractDB):
 
     def read(self, collection_name, query=None, selection=None):
         return [project(d, selection) for d in self._col(collection_name).find_iter(query)]
+
+    def insert_owned(self, collection_name, docs) -> int:
+        """Insert documents the caller will never touch again (no copy): bulk writers."""
+        return self._col(collection_name).insert_owned(list(docs))
+
+    def set_fields_by_id(self, collection_name, items) -> int:
+        """Bulk compare-and-swap field updates by ``_id`` (see ``_Collection``)."""
+        return self._col(collection_name).set_fields_by_id(items)
 
     def read_and_write(self, collection_name, query, data, selection=None):
         col = self._col(collection_name)

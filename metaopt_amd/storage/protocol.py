@@ -185,17 +185,29 @@ class DocumentStorage(BaseStorageProtocol):
         """Bulk registration (device populations register hundreds of trials per suggest)."""
         return self._db.write("trials", [t.to_dict() for t in trials])
 
-    def register_trial_docs(self, docs: List[dict]) -> int:
+    def register_trial_docs(self, docs: List[dict], owned: bool = False) -> int:
         """Bulk registration of ready-made trial documents (the Trial schema, ``_id`` included):
-        the device sweep builds them without Trial objects."""
+        the device sweep builds them without Trial objects.  ``owned``: the caller never touches
+        them again, so an in-process backend may keep them without copying."""
+        if owned and hasattr(self._db, "insert_owned"):
+            return self._db.insert_owned("trials", docs)
         return self._db.write("trials", list(docs))
 
     def update_trial_doc(self, uid, fields: dict, was: Optional[str] = None) -> int:
         """Set ``fields`` of trial ``uid`` (compare-and-swap on the status when ``was`` is set)."""
-        where = {"_id": uid}
-        if was is not None:
-            where["status"] = was
-        return self._db.write("trials", data=fields, query=where)
+        return self.update_trial_docs([(uid, fields, was)])
+
+    def update_trial_docs(self, items) -> int:
+        """Bulk :meth:`update_trial_doc`: ``items`` = [(uid, fields, was or None)]."""
+        if hasattr(self._db, "set_fields_by_id"):
+            return self._db.set_fields_by_id("trials", items)
+        n = 0
+        for uid, fields, was in items:
+            where = {"_id": uid}
+            if was is not None:
+                where["status"] = was
+            n += self._db.write("trials", data=fields, query=where)
+        return n
 
     def register_lie(self, trial: Trial):
         return self._db.write("lying_trials", trial.to_dict())

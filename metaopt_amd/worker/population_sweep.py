@@ -640,24 +640,22 @@ class _WriteBehind:
         self.busy_s += time.perf_counter() - t0
 
     def _take(self):
-        """Next unit of work: a run of registrations (one bulk insert of <= 256 documents) or a
-        single update."""
+        """Next unit of work: a run of <= 256 registrations (one bulk insert) or of updates
+        (one bulk compare-and-swap)."""
         first = self._held.popleft()
         item = [first]
-        if first[0] == "register":
-            while self._held and len(item) < 256 and self._held[0][0] == "register":
-                item.append(self._held.popleft())
+        while self._held and len(item) < 256 and self._held[0][0] == first[0]:
+            item.append(self._held.popleft())
         return item
 
     def _apply_batch(self, held):
         if held[0][0] == "register":
             docs = [h[1] for h in held]
-            if not self._call("register_trial_docs", docs):
+            if not self._call("register_trial_docs", docs, owned=True):
                 for d in docs:            # a bulk insert hit a duplicate: insert one by one
-                    self._call("register_trial_docs", [d])
+                    self._call("register_trial_docs", [dict(d)])
             return
-        for _, (uid, fields, was) in held:
-            self._call("update_trial_doc", uid, fields, was=was)
+        self._call("update_trial_docs", [h[1] for h in held])
 
     def _call(self, method, *args, **kwargs) -> bool:
         try:

@@ -5,6 +5,7 @@ decision path sees the same completion/placement volume as the GPU bench at that
 without a GPU:  ``WORLD=8 python scripts/profile_decide.py [--profile]``.
 """
 import cProfile
+import gc
 import os
 import pstats
 import sys
@@ -88,6 +89,7 @@ def main(n_syncs=40, P=256, world=1, profile=False):
         t1 = time.perf_counter()
         sw._writer.flush()
         t_rel += time.perf_counter() - t1
+        gc.freeze()                     # as PopulationSweep._sync does after every sync
     sw.close()
     print(f"decide: {1e3 * t_total / n_syncs:.2f} ms/sync, writes {1e3 * t_rel / n_syncs:.2f} ms/sync, "
           f"{n_done / n_syncs:.1f} completions/sync")
