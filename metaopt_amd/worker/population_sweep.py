@@ -296,16 +296,18 @@ class PopulationSweep:
         done_pts, done_res = [], []
         now = datetime.datetime.utcnow()
         max_b = self._max_budget()
+        rows = gathered.tolist()          # python floats: ~10x cheaper to index than numpy
         for row in range(W * P):
             rank, slot = divmod(row, P)
-            key = int(gathered[row, 0])
+            g = rows[row]
+            key = int(g[0])
             # 1) the slot's current member: leaves when it reached its budget or diverged; the
             #    owner checkpoints it (below the top budget) -- mirrored here in FIFO order
             if key < 0:
                 free.append(row)
             else:
-                steps, budget = int(gathered[row, 1]), int(gathered[row, 2])
-                bad = gathered[row, 3] > 0
+                steps, budget = int(g[1]), int(g[2])
+                bad = g[3] > 0
                 if bad or steps >= budget:
                     free.append(row)
                     assign[row, 0] = CLEAR
@@ -318,7 +320,7 @@ class PopulationSweep:
                         self._set_status(self.trials.pop(key), "broken")
             # 2) the result of the member that finished in this slot (this sync or, pipelined,
             #    the previous one)
-            rkey = int(gathered[row, 4])
+            rkey = int(g[4])
             if rkey < 0:
                 continue
             doc = self.trials.pop(rkey, None)
@@ -326,11 +328,11 @@ class PopulationSweep:
             pkey = self.key_pkey.pop(rkey, None)
             if doc is None:
                 continue
-            if gathered[row, 8] > 0:
+            if g[8] > 0:
                 self.broken += 1
                 self._set_status(doc, "broken")
                 continue
-            vl, va, tl = float(gathered[row, 6]), float(gathered[row, 7]), float(gathered[row, 5])
+            vl, va, tl = g[6], g[7], g[5]
             self._writer.put_update(doc["_id"], {
                 "results": [{"name": "val_loss", "type": "objective", "value": vl},
                             {"name": self._sec_name, "type": "statistic", "value": va},
