@@ -105,6 +105,22 @@ class StatsSnapshot:
         return self._host.numpy().reshape(4, self.capacity)
 
 
+def _lpt_order(cost: np.ndarray, n_xcd: int = 8) -> np.ndarray:
+    """Work-list permutation: longest-first within each XCD's share.
+
+    The kernels map block b to work item ``xcd_remap(b)`` (common.h): XCD x processes the
+    contiguous positions [base(x), base(x + 1)) in order, so one trial-layer's tiles share its
+    L2.  Sorting each share by descending cost (stably, so a trial-layer's equal-cost tiles stay
+    adjacent) runs the heavy ragged trials first instead of leaving them as the launch's tail."""
+    n = len(cost)
+    if n <= n_xcd:
+        return np.arange(n)
+    q, r = divmod(n, n_xcd)
+    pos = np.arange(n)
+    share = np.where(pos < r * (q + 1), pos // (q + 1), r + (pos - r * (q + 1)) // max(q, 1))
+    return np.lexsort((-cost, share))
+
+
 def device_busy(device):
     if torch.device(device).type != "cuda":
         return lambda: True
@@ -502,8 +518,10 @@ class PopulationMLP:
                 tl["y_off"][i] = y_off
                 tl["gx_off"][i] = prev if l > 0 else -1
                 nt, nk = N // TILE, K // TILE
-                fwd.append(np.stack([np.repeat(i, nt), _ranges(nt)], 1).astype(np.int32))
-                bwd.append(np.stack([np.repeat(i, nk), _ranges(nk)], 1).astype(np.int32))
+                fo = _lpt_order(np.repeat(K, nt))     # a forward tile costs ~K
+                bo = _lpt_order(np.repeat(N, nk))     # a backward k-strip costs ~N
+                fwd.append(np.stack([np.repeat(i, nt)[fo], _ranges(nt)[fo]], 1).astype(np.int32))
+                bwd.append(np.stack([np.repeat(i, nk)[bo], _ranges(nk)[bo]], 1).astype(np.int32))
         else:
             fwd = [np.zeros((0, 2), np.int32) for _ in range(L)]
             bwd = [np.zeros((0, 2), np.int32) for _ in range(L)]
