@@ -68,8 +68,10 @@ def get_lib(build_if_missing: bool = True):
     with _LOCK:
         if _LIB is not None:
             return _LIB
-        path = _build.lib_path()
-        if build_if_missing and (os.environ.get("MOPT_REBUILD") or not path.exists()):
+        override = os.environ.get("MOPT_KERNEL_LIB")   # A/B experiments with variant builds
+        path = _build.lib_path() if not override else __import__("pathlib").Path(override)
+        if not override and build_if_missing and (os.environ.get("MOPT_REBUILD") or
+                                                  not path.exists()):
             try:
                 _build.build()
             except Exception as exc:  # pragma: no cover - exercised on hosts without hipcc
