@@ -287,6 +287,8 @@ int dispatch_tile(const GemmArgs& g, int cfg, hipStream_t st) {
     case 2: return launch<KA, KB, TA, TB, 4, 2, 2>(g, st);  // 128 x 32
     case 3: return launch<KA, KB, TA, TB, 4, 1, 4>(g, st);  // 64 x 64
     case 4: return launch<KA, KB, TA, TB, 2, 2, 4>(g, st);  // 64 x 128
+    // (256 x 128 and 128 x 256 at one workgroup per CU measured 10-35 % slower on the LM
+    //  shapes: this register-staged loop needs the second resident workgroup to hide latency)
     default: return (int)hipErrorInvalidValue;
   }
 }

@@ -50,6 +50,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--out", default=None)
     ap.add_argument("--no-torch", action="store_true")
+    ap.add_argument("--cfgs", default="", help="comma-separated tile configs to time as well")
     args = ap.parse_args()
     rows = []
     for name, P, M, N, K, ta, tb in SHAPES:
@@ -62,6 +63,9 @@ def main():
         t_ours = timeit(lambda: pgemm(a, b, ta=ta, tb=tb, out=out), args.iters)
         row = {"shape": name, "P": P, "M": M, "N": N, "K": K, "plan": plan(P, M, N, K),
                "pgemm_us": round(t_ours, 1), "pgemm_tflops": round(flops / t_ours / 1e6, 1)}
+        for c in [int(v) for v in args.cfgs.split(",") if v]:
+            t = timeit(lambda: pgemm(a, b, ta=ta, tb=tb, out=out, cfg=c), args.iters)
+            row[f"cfg{c}_tflops"] = round(flops / t / 1e6, 1)
         if not args.no_torch and not (ta and tb):
             aa = a.transpose(1, 2) if ta else a
             bb = b.transpose(1, 2) if tb else b
