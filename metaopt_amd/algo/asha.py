@@ -159,7 +159,7 @@ class ASHA(BaseAlgorithm):
                 if _id in self.trial_info:
                     continue
                 self.trial_info[_id] = current[idx]
-                current[idx].register(point, None, overwrite=False)
+                current[idx].register(point, None, overwrite=False, _id=_id)
                 out.append(point)
         else:
             if len(out) < n:
@@ -194,7 +194,7 @@ class ASHA(BaseAlgorithm):
                     raise ValueError(f"No bracket found for point {_id} with fidelity {fid}")
                 bracket = cands[0]
             try:
-                bracket.register(point, result["objective"])
+                bracket.register(point, result["objective"], _id=_id)
             except IndexError:
                 log.warning("Point registered to wrong bracket (corrupted timestamps?).")
                 continue
@@ -253,7 +253,7 @@ class Bracket:
         if j < len(lst) and lst[j] == entry:
             del lst[j]
 
-    def register(self, point, objective, overwrite=True):
+    def register(self, point, objective, overwrite=True, _id=None):
         fid = point[self.asha.fidelity_index]
         if fid == self.rungs[0][0]:
             i = 0
@@ -263,11 +263,12 @@ class Bracket:
                 raise IndexError(f"Bad fidelity level {fid}. Should be in "
                                  f"{[b for b, _ in self.rungs]}. Params: {point}")
             i = idx[0]
-        self._register_at(i, point, objective, overwrite)
+        self._register_at(i, point, objective, overwrite, _id)
 
-    def _register_at(self, i, point, objective, overwrite):
+    def _register_at(self, i, point, objective, overwrite, _id=None):
         rung = self.rungs[i][1]
-        _id = self.asha.get_id(point)
+        if _id is None:
+            _id = self.asha.get_id(point)
         if not overwrite and _id in rung:
             return
         old = rung.get(_id)
@@ -315,7 +316,7 @@ class Bracket:
         for rung_id in range(len(self.rungs) - 2, -1, -1):
             cand = self.get_candidate(rung_id)
             if cand is not None:
-                cand = list(copy.deepcopy(cand))
+                cand = list(cand)       # a tuple of scalars: a shallow copy is a full copy
                 cand[self.asha.fidelity_index] = self.rungs[rung_id + 1][0]
                 return tuple(cand)
         return None

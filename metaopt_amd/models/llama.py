@@ -26,7 +26,7 @@ from __future__ import annotations
 import dataclasses
 import math
 from dataclasses import dataclass
-from typing import Dict, Optional
+from typing import ClassVar, Dict, Optional
 
 import numpy as np
 import torch
@@ -190,6 +190,8 @@ class LMSweepTask:
     """Maps trial parameters to LM population members (AdamW lr / wd / beta1)."""
 
     priors: Dict[str, str] = dataclasses.field(default_factory=lambda: dict(LM_PBT_PRIORS))
+    # key(params) == param_key(params, fidelity): the sweep may derive it from points directly
+    key_by_params: ClassVar[bool] = True
     fidelity: str = "/steps"
     secondary_stat: str = "val_ppl"
     d_model: int = 768

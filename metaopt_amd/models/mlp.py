@@ -18,7 +18,7 @@ import hashlib
 
 import numpy as np
 from dataclasses import dataclass, field
-from typing import Dict, Optional
+from typing import ClassVar, Dict, Optional
 
 from ..ops.population import MemberConfig
 
@@ -54,6 +54,8 @@ def _plain(v):
 @dataclass
 class MLPSweepTask:
     priors: Dict[str, str] = field(default_factory=lambda: dict(MLP_PRIORS))
+    # key(params) == param_key(params, fidelity): the sweep may derive it from points directly
+    key_by_params: ClassVar[bool] = True
     fidelity: str = "/steps"
     momentum: float = 0.9
     weight_decay: float = 5e-4

@@ -13,7 +13,7 @@ from __future__ import annotations
 
 import math
 from dataclasses import dataclass, field
-from typing import Dict, Optional
+from typing import ClassVar, Dict, Optional
 
 import numpy as np
 import torch
@@ -178,6 +178,8 @@ class ResNetSweepTask:
     train a fixed budget of ``steps`` unless the space has a fidelity dimension."""
 
     priors: Dict[str, str] = field(default_factory=lambda: dict(RESNET_TPE_PRIORS))
+    # key(params) == param_key(params, fidelity): the sweep may derive it from points directly
+    key_by_params: ClassVar[bool] = True
     fidelity: str = "/steps"
     steps: int = 390
     secondary_stat: str = "val_acc"

@@ -70,9 +70,51 @@ enum Opt { kSGD = 0, kAdamW = 1 };
 
 // ----------------------------------------------------------------------------------------------
 // Forward GEMM core: acc[i][j] = X[row0 + 32*wave + 16i .., :] . W[n0 + 16j .., :]^T over all K.
-// Register-staged double buffering: the next K-step's global loads are issued before the current
-// step's MFMAs (T14), the LDS tile is written after the barrier.
+// Register-staged pipelining (T14), two K-steps deep: two register sets alternate (the loop body
+// is one even and one odd K-step, so no register is copied and the counted vmcnt wait at each
+// step leaves the other set's six loads in flight).  With one step of look-ahead a K = 1024
+// strip was a chain of 16 exposed HBM round trips and the whole forward ran at ~2 TB/s.  Loads
+// past the last K-step re-read the last tile (clamped address) instead of branching, so no
+// control flow sits around a load.
 // ----------------------------------------------------------------------------------------------
+// (the two register sets are plain scalars behind a macro: held in a struct passed by reference
+//  they were demoted to scratch)
+#define MOPT_FWD_LOAD(x0, x1, x2, x3, w0, w1, k)        \
+  do {                                                  \
+    const int kk_ = (k);                                \
+    x0 = *(const uint4*)(X + g0 + kk_);                 \
+    x1 = *(const uint4*)(X + g1 + kk_);                 \
+    x2 = *(const uint4*)(X + g2 + kk_);                 \
+    x3 = *(const uint4*)(X + g3 + kk_);                 \
+    w0 = *(const uint4*)(W + g0 + kk_);                 \
+    w1 = *(const uint4*)(W + g1 + kk_);                 \
+  } while (0)
+#define MOPT_FWD_STORE(x0, x1, x2, x3, w0, w1) \
+  do {                                         \
+    *(uint4*)as0 = x0;                         \
+    *(uint4*)as1 = x1;                         \
+    *(uint4*)as2 = x2;                         \
+    *(uint4*)as3 = x3;                         \
+    *(uint4*)bs0 = w0;                         \
+    *(uint4*)bs1 = w1;                         \
+  } while (0)
+
+__device__ __forceinline__ void fwd_step(const bf16_t* As, const bf16_t* Bs, int wave, int li,
+                                         int g, f32x4 (&acc)[2][4]) {
+#pragma unroll
+  for (int ks = 0; ks < BK / 32; ++ks) {
+    bf16x8 a[2], b[4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) a[i] = lds_frag(As + (wave * 32 + i * 16 + li) * LS + ks * 32 + g * 8);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = lds_frag(Bs + (j * 16 + li) * LS + ks * 32 + g * 8);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
+  }
+}
+
 __device__ __forceinline__ void fwd_gemm(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                          int K, bf16_t* As, bf16_t* Bs, f32x4 (&acc)[2][4]) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -82,8 +124,6 @@ __device__ __forceinline__ void fwd_gemm(const bf16_t* __restrict__ X, const bf1
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // Staging registers are plain scalars (no arrays captured by a lambda): an array captured by
-  // reference is demoted to scratch, which costs ~10x the forward's useful HBM writes.
   const int c0 = tid, c1 = tid + 256, c2 = tid + 512, c3 = tid + 768;
   const int g0 = (c0 >> 3) * K + (c0 & 7) * 8, g1 = (c1 >> 3) * K + (c1 & 7) * 8;
   const int g2 = (c2 >> 3) * K + (c2 & 7) * 8, g3 = (c3 >> 3) * K + (c3 & 7) * 8;
@@ -93,41 +133,30 @@ __device__ __forceinline__ void fwd_gemm(const bf16_t* __restrict__ X, const bf1
   bf16_t* as3 = As + (c3 >> 3) * LS + (c3 & 7) * 8;
   bf16_t* bs0 = Bs + (c0 >> 3) * LS + (c0 & 7) * 8;
   bf16_t* bs1 = Bs + (c1 >> 3) * LS + (c1 & 7) * 8;
-  uint4 ra0 = *(const uint4*)(X + g0), ra1 = *(const uint4*)(X + g1),
-        ra2 = *(const uint4*)(X + g2), ra3 = *(const uint4*)(X + g3),
-        rb0 = *(const uint4*)(W + g0), rb1 = *(const uint4*)(W + g1);
-  for (int k0 = 0; k0 < K; k0 += BK) {
-    *(uint4*)as0 = ra0;
-    *(uint4*)as1 = ra1;
-    *(uint4*)as2 = ra2;
-    *(uint4*)as3 = ra3;
-    *(uint4*)bs0 = rb0;
-    *(uint4*)bs1 = rb1;
+  const int klast = K - BK;
+  uint4 p0, p1, p2, p3, pw0, pw1;  // even K-steps
+  uint4 q0, q1, q2, q3, qw0, qw1;  // odd K-steps
+  MOPT_FWD_LOAD(p0, p1, p2, p3, pw0, pw1, 0);
+  MOPT_FWD_LOAD(q0, q1, q2, q3, qw0, qw1, min(BK, klast));
+  for (int k0 = 0;; k0 += 2 * BK) {
+    // even K-step: tile k0 from set p, which then fetches tile k0 + 2 BK
+    MOPT_FWD_STORE(p0, p1, p2, p3, pw0, pw1);
     __syncthreads();
-    if (k0 + BK < K) {
-      const int k1 = k0 + BK;
-      ra0 = *(const uint4*)(X + g0 + k1);
-      ra1 = *(const uint4*)(X + g1 + k1);
-      ra2 = *(const uint4*)(X + g2 + k1);
-      ra3 = *(const uint4*)(X + g3 + k1);
-      rb0 = *(const uint4*)(W + g0 + k1);
-      rb1 = *(const uint4*)(W + g1 + k1);
-    }
-#pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks) {
-      bf16x8 a[2], b[4];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) a[i] = lds_frag(As + (wave * 32 + i * 16 + li) * LS + ks * 32 + g * 8);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = lds_frag(Bs + (j * 16 + li) * LS + ks * 32 + g * 8);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
-    }
+    MOPT_FWD_LOAD(p0, p1, p2, p3, pw0, pw1, min(k0 + 2 * BK, klast));
+    fwd_step(As, Bs, wave, li, g, acc);
     __syncthreads();
+    if (k0 + BK >= K) break;
+    // odd K-step: tile k0 + BK from set q, which then fetches tile k0 + 3 BK
+    MOPT_FWD_STORE(q0, q1, q2, q3, qw0, qw1);
+    __syncthreads();
+    MOPT_FWD_LOAD(q0, q1, q2, q3, qw0, qw1, min(k0 + 3 * BK, klast));
+    fwd_step(As, Bs, wave, li, g, acc);
+    __syncthreads();
+    if (k0 + 2 * BK >= K) break;
   }
 }
+#undef MOPT_FWD_LOAD
+#undef MOPT_FWD_STORE
 
 // Y[rows, n0:n0+64] = dropout(relu(X W^T + b)) for one (trial-layer, n-tile, 128-row block).
 __global__ __launch_bounds__(256) void mlp_fwd_kernel(const MlpTL* __restrict__ tls,

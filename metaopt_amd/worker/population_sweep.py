@@ -122,6 +122,19 @@ class PopulationSweep:
             # Trial.params_repr of a point is this template filled with its values
             self._repr_tmpl = ",".join(f"{n}:{{}}" for n in self._dim_names)
             self._sec_name = getattr(task, "secondary_stat", "val_acc")
+            # the configuration key (ASHA promotion lookup, init seed) straight from a point:
+            # param_key's canonical string -- sorted (name, value) pairs without the fidelity --
+            # as a format template, instead of a dict, a sort and numpy checks per point
+            self._pkey_tmpl = None
+            if getattr(task, "key_by_params", False):
+                names = sorted(n for n in self._dim_names if n != task.fidelity)
+                idx = [self._dim_names.index(n) for n in names]
+                self._pkey_tmpl = "[" + ", ".join(
+                    "(" + repr(n).replace("{", "{{").replace("}", "}}") + ", {!r})"
+                    for n in names) + "]"
+                self._pkey_idx = idx
+            inner = getattr(self.algorithm, "algorithm", self.algorithm)
+            self._tracks_lineage = hasattr(inner, "parent_of")
 
     def _gc_callback(self, phase, info):
         if phase == "start":
@@ -292,32 +305,31 @@ class PopulationSweep:
     def _decide(self, gathered: np.ndarray) -> np.ndarray:
         W, P = self.comm.world_size, self.pop.capacity
         assign = np.zeros((W * P + 1, AS_COLS), dtype=np.float64)
-        free = []
         done_pts, done_res = [], []
         now = datetime.datetime.utcnow()
         max_b = self._max_budget()
-        rows = gathered.tolist()          # python floats: ~10x cheaper to index than numpy
-        for row in range(W * P):
-            rank, slot = divmod(row, P)
-            g = rows[row]
-            key = int(g[0])
+        # rows with nothing to report (a member still training, no result) are skipped in
+        # numpy; the rest are walked in row order (the checkpoint FIFO mirror depends on it)
+        cur = gathered[:, 0]
+        leaving = (cur >= 0) & ((gathered[:, 3] > 0) | (gathered[:, 1] >= gathered[:, 2]))
+        free = np.flatnonzero((cur < 0) | leaving).tolist()
+        events = np.flatnonzero(leaving | (gathered[:, 4] >= 0))
+        rows = gathered[events].tolist()   # python floats: ~10x cheaper to index than numpy
+        for row, g, left in zip(events.tolist(), rows, leaving[events].tolist()):
+            rank = row // P
             # 1) the slot's current member: leaves when it reached its budget or diverged; the
             #    owner checkpoints it (below the top budget) -- mirrored here in FIFO order
-            if key < 0:
-                free.append(row)
-            else:
-                steps, budget = int(g[1]), int(g[2])
+            if left:
+                key, budget = int(g[0]), int(g[2])
                 bad = g[3] > 0
-                if bad or steps >= budget:
-                    free.append(row)
-                    assign[row, 0] = CLEAR
-                    if not bad and budget < max_b:
-                        self._mirror_save(rank, key)
-                    if bad and key in self.trials:
-                        self.key_params.pop(key, None)
-                        self.key_pkey.pop(key, None)
-                        self.broken += 1
-                        self._set_status(self.trials.pop(key), "broken")
+                assign[row, 0] = CLEAR
+                if not bad and budget < max_b:
+                    self._mirror_save(rank, key)
+                if bad and key in self.trials:
+                    self.key_params.pop(key, None)
+                    self.key_pkey.pop(key, None)
+                    self.broken += 1
+                    self._set_status(self.trials.pop(key), "broken")
             # 2) the result of the member that finished in this slot (this sync or, pipelined,
             #    the previous one)
             rkey = int(g[4])
@@ -404,38 +416,41 @@ class PopulationSweep:
         if not points and in_flight == 0:
             self.done = True
             return
-        free_by_rank = {r: collections.deque(row for row in free_rows if row // P == r)
-                        for r in range(W)}
+        free_by_rank = [collections.deque(row for row in free_rows if row // P == r)
+                        for r in range(W)]
+        n_free = [len(q) for q in free_by_rank]
         stamp = datetime.datetime.utcnow()
-        parent_of = getattr(self.algorithm, "parent_of", None)
+        parent_of = getattr(self.algorithm, "parent_of", None) if self._tracks_lineage else None
         keys = self._dim_names
         for point in points:
             params = dict(zip(keys, point))
-            pkey = self.task.key(params)
+            pkey = self._point_key(point, params)
             # lineage-tracking algorithms (PBT exploit, Hyperband/ASHA promotion) name the point
             # whose device state the new trial continues; otherwise the same hyper-parameters at
             # a lower fidelity are looked up (ASHA promotion)
             parent = parent_of(point) if parent_of is not None else None
-            ckey = self.task.key(dict(zip(keys, parent))) if parent is not None else pkey
+            ckey = self._point_key(parent) if parent is not None else pkey
             owner = self.ckpt_index.get(ckey)
             src = -1
-            if owner is not None and free_by_rank[owner[0]]:
+            if owner is not None and n_free[owner[0]]:
                 # resume next to the checkpoint (no copy between GPUs)
-                row = free_by_rank[owner[0]].popleft()
+                rank = owner[0]
                 action, resume, src = RESUME, owner[1], owner[0]
             else:
-                rank = max(free_by_rank, key=lambda r: len(free_by_rank[r]))
-                if not free_by_rank[rank]:
+                rank = max(range(W), key=n_free.__getitem__)
+                if not n_free[rank]:
                     break
-                row = free_by_rank[rank].popleft()
                 if owner is not None:   # C4: the owner sends the checkpoint to that rank (P2P)
                     action, resume, src = RESUME, owner[1], owner[0]
                 else:
                     action, resume = NEW, -1
+            row = free_by_rank[rank].popleft()
+            n_free[rank] -= 1
             tid = self._doc_id(point)
             if tid in self._registered:
                 log.debug("duplicate point %s skipped", point)
-                free_by_rank[row // P].appendleft(row)
+                free_by_rank[rank].appendleft(row)
+                n_free[rank] += 1
                 continue
             self._registered.add(tid)
             doc = {"experiment": self.experiment.id, "status": "reserved", "worker": None,
@@ -454,6 +469,14 @@ class PopulationSweep:
             cfg = self.task.member_config(params, self.task.seed_of(pkey))
             assign[row] = (action, key, cfg.width, cfg.lr, cfg.momentum, cfg.weight_decay,
                            cfg.dropout, cfg.seed, self.task.budget(params), resume, src)
+
+    def _point_key(self, point, params=None) -> str:
+        """``task.key(params)`` of a suggested point (python scalars, space order)."""
+        if self._pkey_tmpl is None:
+            return self.task.key(params if params is not None
+                                 else dict(zip(self._dim_names, point)))
+        return hashlib.md5(self._pkey_tmpl.format(*[point[i] for i in self._pkey_idx])
+                           .encode("utf-8")).hexdigest()
 
     def _doc_id(self, point) -> str:
         """``Trial.id`` of ``point`` in this experiment (md5 of ``params_repr`` + experiment id,

@@ -159,3 +159,20 @@ def test_sweep_pbt_generations_resume_state(data):
     ids = {t.id for t in trials}
     children = [t for t in trials if t.parents]
     assert len(children) == 12 and all(t.parents[0] in ids for t in children)
+
+
+def test_sweep_point_key_matches_task_key(data):
+    """The sweep derives configuration keys from points with a format template; they must be
+    the task's ``param_key`` exactly (promotion lookup and per-configuration init seeds)."""
+    priors = {"/lr": "loguniform(1e-3, 1.0)", "/width": "loguniform(64, 128, discrete=True)",
+              "/dropout": "uniform(0, 0.5)", "/steps": "fidelity(16, 64, 2)"}
+    exp = build_experiment("key-test", priors=priors, algorithms={"random": {"seed": 2}},
+                           max_trials=4, storage=DocumentStorage(EphemeralDB()))
+    task = MLPSweepTask(priors=priors, max_width=128)
+    sweep = PopulationSweep(PopulationMLP(2, max_width=128, device="cpu"), task, data,
+                            experiment=exp, sync_every=16)
+    assert sweep._pkey_tmpl is not None
+    for point in exp.algorithms.suggest(8):
+        params = dict(zip(sweep._dim_names, point))
+        assert sweep._point_key(point) == task.key(params)
+    sweep.close()
