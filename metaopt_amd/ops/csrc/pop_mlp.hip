@@ -64,7 +64,12 @@ constexpr int BN = 64;   // output features per forward tile / per backward chun
 constexpr int BK = 64;   // reduction step of the forward, width of a backward k-strip
 constexpr int LS = kLdsStride;
 
-enum FwdFlags { kRelu = 1, kDropout = 2, kWriteGrad = 4 };
+// kStoreStats: one row block per trial -- store the trial's loss / #correct instead of
+// accumulating atomically into zeroed counters (saves the per-step zero-fill launch).
+// kCountStep: advance the trial's step counter hp.t (the hidden layers of the same step read
+// hp.t + 1; the backward, launched after, reads the new value) -- saves the per-step increment
+// launch.
+enum FwdFlags { kRelu = 1, kDropout = 2, kWriteGrad = 4, kStoreStats = 8, kCountStep = 16 };
 enum BwdFlags { kHasDx = 1, kInDropout = 2, kUpdateBias = 4 };
 enum Opt { kSGD = 0, kAdamW = 1 };
 
@@ -227,7 +232,8 @@ __global__ __launch_bounds__(256) void mlp_fwd_ce_kernel(const MlpTL* __restrict
                                                          bf16_t* __restrict__ grad,
                                                          float* __restrict__ loss_out,
                                                          float* __restrict__ correct_out,
-                                                         float inv_b, int flags) {
+                                                         TrialHP* __restrict__ hp, float inv_b,
+                                                         int flags) {
   constexpr int CS = BN + 1;  // f32 logits row stride
   constexpr int kSmemBytes = BM * CS * 4 > (BM + BN) * LS * 2 ? BM * CS * 4 : (BM + BN) * LS * 2;
   __shared__ __attribute__((aligned(16))) char smem_raw[kSmemBytes];
@@ -289,7 +295,19 @@ __global__ __launch_bounds__(256) void mlp_fwd_ce_kernel(const MlpTL* __restrict
   }
   loss = wave_sum(loss);
   corr = wave_sum(corr);
-  if (lane == 0 && wave < 2) {
+  if ((flags & kCountStep) && blockIdx.y == 0 && tid == 0) hp[tl.trial].t += 1u;
+  if (flags & kStoreStats) {
+    __shared__ float red[2][2];
+    if (lane == 0 && wave < 2) {
+      red[wave][0] = loss;
+      red[wave][1] = corr;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      loss_out[tl.trial] = red[0][0] + red[1][0];
+      correct_out[tl.trial] = red[0][1] + red[1][1];
+    }
+  } else if (lane == 0 && wave < 2) {
     atomicAdd(loss_out + tl.trial, loss);
     atomicAdd(correct_out + tl.trial, corr);
   }
@@ -592,7 +610,7 @@ __global__ __launch_bounds__(256) void mlp_init_kernel(const InitDesc* __restric
 // ------------------------------------------------------------------------------------------------
 extern "C" {
 
-int mopt_abi_version() { return 4; }
+int mopt_abi_version() { return 5; }
 
 int mopt_mlp_init(const void* descs, int n_desc, void* p32, void* p16, void* m32, void* v32,
                   int zero_v, void* stream) {
@@ -616,13 +634,14 @@ int mopt_mlp_fwd(const void* tls, const void* work, int n_work, int n_rowblocks,
 
 int mopt_mlp_fwd_ce(const void* tls, const void* work, int n_work, int n_rowblocks, const void* xb,
                     const void* p32, const void* p16, const void* labels, void* grad, void* loss,
-                    void* correct, float inv_b, int flags, void* stream) {
+                    void* correct, void* hp, float inv_b, int flags, void* stream) {
   if (n_work <= 0) return 0;
+  if ((flags & kStoreStats) && n_rowblocks != 1) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(mlp_fwd_ce_kernel, dim3(n_work, n_rowblocks), dim3(256), 0,
                      (hipStream_t)stream, (const MlpTL*)tls, (const int2*)work, n_work,
                      (const bf16_t*)xb, (const float*)p32, (const bf16_t*)p16,
-                     (const int32_t*)labels, (bf16_t*)grad, (float*)loss, (float*)correct, inv_b,
-                     flags);
+                     (const int32_t*)labels, (bf16_t*)grad, (float*)loss, (float*)correct,
+                     (TrialHP*)hp, inv_b, flags);
   return (int)hipGetLastError();
 }
 

@@ -41,7 +41,7 @@ INIT_DTYPE = np.dtype([("w_off", "<i8"), ("b_off", "<i8"), ("K", "<i4"), ("N", "
 assert TL_DTYPE.itemsize == 64 and HP_DTYPE.itemsize == 32 and INIT_DTYPE.itemsize == 48
 
 TILE = 64
-FWD_RELU, FWD_DROPOUT, FWD_WRITE_GRAD = 1, 2, 4
+FWD_RELU, FWD_DROPOUT, FWD_WRITE_GRAD, FWD_STORE_STATS, FWD_COUNT_STEP = 1, 2, 4, 8, 16
 BWD_HAS_DX, BWD_IN_DROPOUT, BWD_UPDATE_BIAS = 1, 2, 4
 OPTIMIZERS = {"sgd": 0, "adamw": 1}
 
@@ -565,31 +565,34 @@ class PopulationMLP:
             raise ValueError(f"x must be [{self.batch_size}, {self.K0}] (padded), got {tuple(x.shape)}")
         self.hp["t"][self._active_np] += 1
         if self.backend == "hip":
-            self._hp_increment()
-            self._train_step_hip(x, y)
+            self._train_step_hip(x, y)     # advances the device step counters itself
         else:
             self._train_step_torch(x, y)
-
-    def _hp_increment(self) -> None:
-        # device copy of the step counters: hp_dev viewed as int32 [capacity, 8], column 7 = t
-        self.hp_dev.view(torch.int32).view(self.capacity, 8)[:, 7].add_(self._active_t)
 
     def _train_step_hip(self, x, y) -> None:
         from ._lib import check, stream_ptr
         lib, tb, L, P = self._lib, self._tables["train"], self.L, self._ptr
         stream = stream_ptr(self.device)
-        self.stats[:2 * self.capacity].zero_()
+        # one 128-row block per trial: the loss kernel stores the statistics (no zero-fill) and
+        # advances the device step counters; the hidden layers run before it, so they key their
+        # dropout masks with t + 1 (the step being taken)
+        rb = self.batch_size // 128
+        ce_flags = FWD_WRITE_GRAD | FWD_COUNT_STEP
+        if rb == 1:
+            ce_flags |= FWD_STORE_STATS
+        else:
+            self.stats[:2 * self.capacity].zero_()
         drop = self._any_dropout
         xp = x.data_ptr() if x.is_contiguous() else x.contiguous().data_ptr()
         act, tl = P["act"], P["tl"]
         for l in range(L - 1):
-            check(lib.mopt_mlp_fwd(tl, P["fwd"][l], tb["n_fwd"][l], 1, xp if l == 0 else act,
-                                   P["p32"], P["p16"], act, P["hp"], 0, l,
+            check(lib.mopt_mlp_fwd(tl, P["fwd"][l], tb["n_fwd"][l], rb, xp if l == 0 else act,
+                                   P["p32"], P["p16"], act, P["hp"], 1, l,
                                    FWD_RELU | (FWD_DROPOUT if drop else 0), stream), "mlp_fwd")
-        check(lib.mopt_mlp_fwd_ce(tl, P["fwd"][L - 1], tb["n_fwd"][L - 1], 1,
+        check(lib.mopt_mlp_fwd_ce(tl, P["fwd"][L - 1], tb["n_fwd"][L - 1], rb,
                                   xp if L == 1 else act, P["p32"], P["p16"], y.data_ptr(),
-                                  P["grad"], P["loss"], P["correct"], 1.0 / self.batch_size,
-                                  FWD_WRITE_GRAD, stream), "mlp_fwd_ce")
+                                  P["grad"], P["loss"], P["correct"], P["hp"],
+                                  1.0 / self.batch_size, ce_flags, stream), "mlp_fwd_ce")
         opt = OPTIMIZERS[self.optimizer]
         for l in range(L - 1, -1, -1):
             flags = BWD_UPDATE_BIAS
@@ -684,8 +687,8 @@ class PopulationMLP:
             check(lib.mopt_mlp_fwd_ce(tb["tl"].data_ptr(), tb["fwd"][L - 1].data_ptr(),
                                       tb["n_fwd"][L - 1], rb, src.data_ptr(), self.p32.data_ptr(),
                                       self.p16.data_ptr(), y.data_ptr(), self.grad.data_ptr(),
-                                      self.eval_loss.data_ptr(), self.eval_correct.data_ptr(), 1.0,
-                                      0, stream), "mlp_fwd_ce(eval)")
+                                      self.eval_loss.data_ptr(), self.eval_correct.data_ptr(),
+                                      self.hp_dev.data_ptr(), 1.0, 0, stream), "mlp_fwd_ce(eval)")
         else:
             self.stats[2 * self.capacity:].zero_()
             xf = x.float()

@@ -55,7 +55,7 @@ def run_fwd(l):
         lib.mopt_mlp_fwd_ce(tb["tl"].data_ptr(), tb["fwd"][l].data_ptr(), tb["n_fwd"][l], 1,
                             src.data_ptr(), pop.p32.data_ptr(), pop.p16.data_ptr(), y.data_ptr(),
                             pop.grad.data_ptr(), pop.loss.data_ptr(), pop.correct.data_ptr(),
-                            1.0 / 128, FWD_WRITE_GRAD, stream)
+                            pop.hp_dev.data_ptr(), 1.0 / 128, FWD_WRITE_GRAD, stream)
 
 
 def run_bwd(l):

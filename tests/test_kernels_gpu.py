@@ -86,6 +86,9 @@ def test_multi_step_trajectory(data, n_hidden):
         lh.append(hip.train_loss())
         lr_.append(ref.train_loss())
     lh, lr_ = np.array(lh), np.array(lr_)
+    # the loss kernel advances the device step counters: they track the host mirror
+    dev_t = hip.hp_dev.view(torch.int32).view(hip.capacity, 8)[:, 7].cpu().numpy()
+    assert (dev_t == hip.hp["t"].astype(np.int32)).all(), (dev_t, hip.hp["t"])
     act = ref.active_slots()
     err = np.abs(lh[:, act] - lr_[:, act]).max()
     assert err < 3e-2, err
