@@ -9,6 +9,10 @@ North-star collectives:
     point over one xGMI link) and rank-0 decisions (C5).
 With ``world_size == 1`` and no process group every call is a local no-op, so the same engine code
 runs on one GPU without a rendezvous.
+
+``MOPT_COMM_BACKEND=gloo`` runs GPU ranks over gloo instead (ranks may then share a GPU: the
+device is ``LOCAL_RANK mod #GPUs``), staging GPU tensors through host memory -- a rehearsal of
+the multi-rank engine on a one-GPU machine, not a production path.
 """
 from __future__ import annotations
 
@@ -28,6 +32,12 @@ class Comm:
         self.local_rank = local_rank
         self.device = device if device is not None else torch.device("cpu")
         self.group = group
+        self.backend = dist.get_backend(group) if self.distributed else None
+
+    @property
+    def _host_staged(self) -> bool:
+        """GPU tensors over a host-only backend (gloo rehearsal): copy through host memory."""
+        return self.device.type == "cuda" and self.backend not in (None, "nccl")
 
     @property
     def distributed(self) -> bool:
@@ -80,14 +90,25 @@ class Comm:
             return
         if not self.distributed:
             raise RuntimeError("point-to-point exchange needs a process group")
+        staged = []
+        if self._host_staged:
+            host_ops = []
+            for kind, t, peer in ops:
+                h = t.detach().cpu() if kind == "send" else torch.empty(t.shape, dtype=t.dtype)
+                if kind == "recv":
+                    staged.append((t, h))
+                host_ops.append((kind, h, peer))
+            ops = host_ops
         p2p = [dist.P2POp(dist.isend if kind == "send" else dist.irecv, t, peer, group=self.group)
                for kind, t, peer in ops]
         for req in dist.batch_isend_irecv(p2p):
             req.wait()
+        for t, h in staged:
+            t.copy_(h)
 
     def barrier(self) -> None:
         if self.distributed:
-            if self.device.type == "cuda":
+            if self.device.type == "cuda" and self.backend == "nccl":
                 dist.barrier(group=self.group, device_ids=[self.device.index or 0])
             else:
                 dist.barrier(group=self.group)
@@ -108,7 +129,8 @@ class Comm:
         return float(t.item())
 
     def _coll_device(self):
-        return self.device if self.device.type == "cuda" else torch.device("cpu")
+        return self.device if self.device.type == "cuda" and not self._host_staged \
+            else torch.device("cpu")
 
 
 def init_from_env(backend: Optional[str] = None, timeout_s: int = 600) -> Comm:
@@ -120,9 +142,11 @@ def init_from_env(backend: Optional[str] = None, timeout_s: int = 600) -> Comm:
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     use_cuda = torch.cuda.is_available()
+    backend = os.environ.get("MOPT_COMM_BACKEND") or backend
     if use_cuda:
-        torch.cuda.set_device(local_rank)
-        device = torch.device("cuda", local_rank)
+        index = local_rank if backend in (None, "nccl") else local_rank % torch.cuda.device_count()
+        torch.cuda.set_device(index)
+        device = torch.device("cuda", index)
     else:
         device = torch.device("cpu")
     if world > 1 and not dist.is_initialized():
