@@ -588,10 +588,8 @@ class PopulationSweep:
         if W == 1:
             return {}
         ops, recv = [], {}
-        for row in range(W * P):
+        for row in np.flatnonzero(assign[:W * P, 0] == RESUME).tolist():
             a = assign[row]
-            if int(a[0]) != RESUME:
-                continue
             src, dst = int(a[10]), row // P
             if src == dst or src < 0:
                 continue
