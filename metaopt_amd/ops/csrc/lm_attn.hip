@@ -28,6 +28,16 @@ constexpr int BQ = 64;         // queries per workgroup
 constexpr int BKV = 64;        // keys per block
 constexpr int LS = kLdsStride;
 
+// (position of this workgroup's sequence block within its head, head index bh) for a 1-D grid of
+// nblk * n_bh workgroups.  All blocks of one (batch, head) run on ONE XCD -- they re-read the same
+// K/V (or Q/dO) tiles, which then stay in that XCD's L2; with the 2-D (T/64, BH) grid the
+// hardware's round-robin put the 8 blocks of a head on 8 different XCDs and every XCD fetched
+// every head's tiles.  XCDs get contiguous shares of heads; within a head, rank 0 first.
+__device__ __forceinline__ int2 head_block(int nblk, int n_bh) {
+  const int t = xcd_remap((int)blockIdx.x, nblk * n_bh);
+  return make_int2(t % nblk, t / nblk);
+}
+
 // Load a [64][64] bf16 tile (rows contiguous, row stride 64) into LDS [64][LS].
 __device__ __forceinline__ void tile_to_lds(const bf16_t* __restrict__ g, bf16_t* s, int tid) {
 #pragma unroll
@@ -85,12 +95,13 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
                                                        const bf16_t* __restrict__ V,
                                                        bf16_t* __restrict__ O,
                                                        float* __restrict__ LSE2, int T, int H,
-                                                       float c) {
+                                                       float c, int n_bh) {
   __shared__ __attribute__((aligned(16))) bf16_t Ks[BKV * LS];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[BKV * LS];
-  const int nqb = gridDim.x;
-  const int qb = nqb - 1 - (int)blockIdx.x;          // longest (most key blocks) first
-  const int bh = blockIdx.y;
+  const int nqb = T / BQ;
+  const int2 hb = head_block(nqb, n_bh);
+  const int qb = nqb - 1 - hb.x;                      // longest (most key blocks) first
+  const int bh = hb.y;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, g = lane >> 4, q = li >> 2, pp = li & 3;
   const size_t base = (size_t)bh * T * D;
@@ -188,12 +199,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16_t* __restri
                                                           const float* __restrict__ LSE2,
                                                           const float* __restrict__ Dsum,
                                                           bf16_t* __restrict__ dQ, int T, int H,
-                                                          float c, float scale) {
+                                                          float c, float scale, int n_bh) {
   __shared__ __attribute__((aligned(16))) bf16_t Ks[BKV * LS];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[BKV * LS];
-  const int nqb = gridDim.x;
-  const int qb = nqb - 1 - (int)blockIdx.x;
-  const int bh = blockIdx.y;
+  const int nqb = T / BQ;
+  const int2 hb = head_block(nqb, n_bh);
+  const int qb = nqb - 1 - hb.x;
+  const int bh = hb.y;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, g = lane >> 4, q = li >> 2, pp = li & 3;
   const size_t base = (size_t)bh * T * D;
@@ -256,12 +268,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16_t* __rest
                                                             const float* __restrict__ Dsum,
                                                             bf16_t* __restrict__ dK,
                                                             bf16_t* __restrict__ dV, int T, int H,
-                                                            float c, float scale) {
+                                                            float c, float scale, int n_bh) {
   __shared__ __attribute__((aligned(16))) bf16_t Qs[BQ * LS];
   __shared__ __attribute__((aligned(16))) bf16_t dOs[BQ * LS];
   __shared__ float lse_s[BQ], dsum_s[BQ];
-  const int kb = (int)blockIdx.x;                 // blocks with more query blocks are early ids
-  const int bh = blockIdx.y;
+  const int2 hb = head_block(T / BKV, n_bh);
+  const int kb = hb.x;                            // blocks with more query blocks are early ids
+  const int bh = hb.y;
   const int nqb = T / BQ;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, g = lane >> 4, q = li >> 2, pp = li & 3;
@@ -339,9 +352,9 @@ int mopt_attn_fwd(const void* q, const void* k, const void* v, void* o, void* ls
                   int H, float scale, void* stream) {
   if (T % 64 || bh <= 0) return 1;
   const float c = scale * 1.4426950408889634f;
-  hipLaunchKernelGGL(attn_fwd_kernel, dim3(T / 64, bh), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(attn_fwd_kernel, dim3((T / 64) * bh), dim3(256), 0, (hipStream_t)stream,
                      (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o,
-                     (float*)lse2, T, H, c);
+                     (float*)lse2, T, H, c, bh);
   return (int)hipGetLastError();
 }
 
@@ -354,12 +367,13 @@ int mopt_attn_bwd(const void* q, const void* k, const void* v, const void* o, co
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((rows + 255) / 256), dim3(256), 0, st,
                      (const bf16_t*)o, (const bf16_t*)dout, (float*)dsum, T, H, rows);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3(T / 64, bh), dim3(256), 0, st, (const bf16_t*)q,
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((T / 64) * bh), dim3(256), 0, st,
+                     (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout,
+                     (const float*)lse2, (const float*)dsum, (bf16_t*)dk, (bf16_t*)dv, T, H, c,
+                     scale, bh);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((T / 64) * bh), dim3(256), 0, st, (const bf16_t*)q,
                      (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, (const float*)lse2,
-                     (const float*)dsum, (bf16_t*)dk, (bf16_t*)dv, T, H, c, scale);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(T / 64, bh), dim3(256), 0, st, (const bf16_t*)q,
-                     (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, (const float*)lse2,
-                     (const float*)dsum, (bf16_t*)dq, T, H, c, scale);
+                     (const float*)dsum, (bf16_t*)dq, T, H, c, scale, bh);
   return (int)hipGetLastError();
 }
 
