@@ -47,6 +47,18 @@ __device__ __forceinline__ void tile_to_lds(const bf16_t* __restrict__ g, bf16_t
   }
 }
 
+// The same tile in two steps, so the next key block's global loads are in flight while the current
+// block is multiplied (register staging, T14): load into registers, store to LDS after the barrier.
+__device__ __forceinline__ void tile_load(const bf16_t* __restrict__ g, uint4& r0, uint4& r1,
+                                          int tid) {
+  r0 = *(const uint4*)(g + (tid >> 3) * D + (tid & 7) * 8);
+  r1 = *(const uint4*)(g + ((tid + 256) >> 3) * D + (tid & 7) * 8);
+}
+__device__ __forceinline__ void tile_store(const uint4& r0, const uint4& r1, bf16_t* s, int tid) {
+  *(uint4*)(s + (tid >> 3) * LS + (tid & 7) * 8) = r0;
+  *(uint4*)(s + ((tid + 256) >> 3) * LS + (tid & 7) * 8) = r1;
+}
+
 // Key row of the permuted K/V fragment: tile j = 2s + h, fragment row m.
 __device__ __forceinline__ int perm_row(int s, int h, int m) {
   return 32 * s + 8 * (m >> 2) + 4 * h + (m & 3);
@@ -116,11 +128,19 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
   for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m = -INFINITY, l = 0.f;
 
+  uint4 ka, kc, va, vc;   // key block kb + 1, fetched while block kb is multiplied
+  tile_load(K + base, ka, kc, tid);
+  tile_load(V + base, va, vc, tid);
   for (int kb = 0; kb <= qb; ++kb) {
     __syncthreads();
-    tile_to_lds(K + base + (size_t)kb * BKV * D, Ks, tid);
-    tile_to_lds(V + base + (size_t)kb * BKV * D, Vs, tid);
+    tile_store(ka, kc, Ks, tid);
+    tile_store(va, vc, Vs, tid);
     __syncthreads();
+    {
+      const size_t nb = (size_t)min(kb + 1, qb) * BKV * D;   // clamped: no branch around loads
+      tile_load(K + base + nb, ka, kc, tid);
+      tile_load(V + base + nb, va, vc, tid);
+    }
     f32x4 st[4];
     scores_T(Ks, qf, li, g, st);
     float mx = -INFINITY;
@@ -224,11 +244,19 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16_t* __restri
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) acc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  uint4 ka, kc, va, vc;
+  tile_load(K + base, ka, kc, tid);
+  tile_load(V + base, va, vc, tid);
   for (int kb = 0; kb <= qb; ++kb) {
     __syncthreads();
-    tile_to_lds(K + base + (size_t)kb * BKV * D, Ks, tid);
-    tile_to_lds(V + base + (size_t)kb * BKV * D, Vs, tid);
+    tile_store(ka, kc, Ks, tid);
+    tile_store(va, vc, Vs, tid);
     __syncthreads();
+    {
+      const size_t nb = (size_t)min(kb + 1, qb) * BKV * D;
+      tile_load(K + base + nb, ka, kc, tid);
+      tile_load(V + base + nb, va, vc, tid);
+    }
     f32x4 st[4], dpt[4];
     scores_T(Ks, qf, li, g, st);
     scores_T(Vs, df, li, g, dpt);     // dP^T = V dO^T, same permuted key order
@@ -292,20 +320,34 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16_t* __rest
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) dk[dt] = dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // query block qb + 1 (Q tile, dO rows in the [B'][T][H][64] layout, LSE2 / Dsum) is fetched
+  // into registers while block qb is multiplied (T14 register staging)
+  uint4 qa, qc, da, dc;
+  float lse_r = 0.f, dsum_r = 0.f;
+  const int r0 = tid >> 3, r1 = (tid + 256) >> 3, ch = tid & 7;
+#define MOPT_DKDV_LOAD(QB)                                                                   \
+  {                                                                                          \
+    const int qb_ = (QB);                                                                    \
+    tile_load(Q + base + (size_t)qb_ * BQ * D, qa, qc, tid);                                 \
+    da = *(const uint4*)(dO + (((size_t)b * T + qb_ * BQ + r0) * H + hh) * D + ch * 8);      \
+    dc = *(const uint4*)(dO + (((size_t)b * T + qb_ * BQ + r1) * H + hh) * D + ch * 8);      \
+    if (tid < BQ) {                                                                          \
+      lse_r = LSE2[(size_t)bh * T + qb_ * BQ + tid];                                         \
+      dsum_r = Dsum[(size_t)bh * T + qb_ * BQ + tid];                                        \
+    }                                                                                        \
+  }
+  MOPT_DKDV_LOAD(kb)
   for (int qb = kb; qb < nqb; ++qb) {
     __syncthreads();
-    tile_to_lds(Q + base + (size_t)qb * BQ * D, Qs, tid);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {      // dO rows of this query block: [B'][T][H][64] layout
-      const int cc = tid + 256 * i, r = cc >> 3, ch = cc & 7;
-      *(uint4*)(dOs + r * LS + ch * 8) =
-          *(const uint4*)(dO + (((size_t)b * T + qb * BQ + r) * H + hh) * D + ch * 8);
-    }
+    tile_store(qa, qc, Qs, tid);
+    *(uint4*)(dOs + r0 * LS + ch * 8) = da;
+    *(uint4*)(dOs + r1 * LS + ch * 8) = dc;
     if (tid < BQ) {
-      lse_s[tid] = LSE2[(size_t)bh * T + qb * BQ + tid];
-      dsum_s[tid] = Dsum[(size_t)bh * T + qb * BQ + tid];
+      lse_s[tid] = lse_r;
+      dsum_s[tid] = dsum_r;
     }
     __syncthreads();
+    MOPT_DKDV_LOAD(min(qb + 1, nqb - 1))
     // S and dP tiles j = 2s + h: rows = queries 32s + 8g + 4h + r (C layout), column = key li.
     f32x4 st[4], dp[4];
     scores_T(Qs, kf, li, g, st);
@@ -342,6 +384,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16_t* __rest
     *(uint2*)(ovp + 16 * dt + 4 * g) =
         make_uint2(pack2bf(dv[dt][0], dv[dt][1]), pack2bf(dv[dt][2], dv[dt][3]));
   }
+#undef MOPT_DKDV_LOAD
 }
 
 }  // namespace
