@@ -123,17 +123,19 @@ class PopulationLM(FlatPopulation):
         R = tok.numel()
         W = self.W
         x = ops.embedding(tok.reshape(-1), W["embed"], rpt)
+        # every residual add is fused into the pre-norm that follows it (ops.add_rmsnorm)
+        h = ops.rmsnorm(x, W["l0.attn_norm"], rpt, c.norm_eps)
         for l in range(c.n_layers):
-            h = ops.rmsnorm(x, W[f"l{l}.attn_norm"], rpt, c.norm_eps)
             qkv = _lin(h.view(P, rpt, d), W[f"l{l}.wqkv"]).view(R, 3 * d)
             q, k, v = ops.rope_split(qkv, self.cos, self.sin, T, H)
             o = ops.attention(q, k, v)
-            x = x + _lin(o.view(P, rpt, d), W[f"l{l}.wo"]).view(R, d)
-            h = ops.rmsnorm(x, W[f"l{l}.mlp_norm"], rpt, c.norm_eps)
+            x, h = ops.add_rmsnorm(x, _lin(o.view(P, rpt, d), W[f"l{l}.wo"]).view(R, d),
+                                   W[f"l{l}.mlp_norm"], rpt, c.norm_eps)
             gu = _lin(h.view(P, rpt, d), W[f"l{l}.wgu"])
             a = ops.swiglu(gu)
-            x = x + _lin(a, W[f"l{l}.wdown"]).view(R, d)
-        h = ops.rmsnorm(x, W["final_norm"], rpt, c.norm_eps)
+            nxt = W[f"l{l + 1}.attn_norm"] if l + 1 < c.n_layers else W["final_norm"]
+            x, h = ops.add_rmsnorm(x, _lin(a, W[f"l{l}.wdown"]).view(R, d), nxt, rpt,
+                                   c.norm_eps)
         logits = _lin(h.view(P, rpt, d), W["head"]).view(R, c.vocab)
         if train:
             return ops.cross_entropy(logits, labels.reshape(-1), rpt, grad_scale=1.0 / rpt,

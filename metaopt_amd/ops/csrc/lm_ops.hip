@@ -71,8 +71,13 @@ __device__ __forceinline__ float wave_max(float v) {
 // ---------------------------------------------------------------------------------- RMSNorm
 constexpr int kMaxChunks = 4;  // d <= 64 lanes * 8 * 4 = 2048
 
-// One wave per row, 4 rows per workgroup.
+// One wave per row, 4 rows per workgroup.  RES: the pre-norm residual add is fused in --
+// xs = x + res (rounded to bf16, as the unfused add would) is written out as the new residual
+// stream and normalised, so the transformer block's residual add costs no pass of its own.
+template <bool RES>
 __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const bf16_t* __restrict__ x,
+                                                          const bf16_t* __restrict__ res,
+                                                          bf16_t* __restrict__ xs,
                                                           const bf16_t* __restrict__ w,
                                                           bf16_t* __restrict__ y,
                                                           float* __restrict__ rstd, int rows,
@@ -88,6 +93,13 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const bf16_t* __restri
     const int c = lane + 64 * k;
     if (c < nc) {
       unpack8(*(const uint4*)(xr + 8 * c), v[k]);
+      if (RES) {
+        float rv[8];
+        unpack8(*(const uint4*)(res + (size_t)row * d + 8 * c), rv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[k][e] = bf2f(f2bf(v[k][e] + rv[e]));
+        *(uint4*)(xs + (size_t)row * d + 8 * c) = pack8(v[k]);
+      }
 #pragma unroll
       for (int e = 0; e < 8; ++e) ss += v[k][e] * v[k][e];
     }
@@ -108,10 +120,14 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const bf16_t* __restri
   if (lane == 0) rstd[row] = r;
 }
 
-// dx = r * (g - xhat * mean(g * xhat)),  g = dy * w,  xhat = x * r.
+// dx = r * (g - xhat * mean(g * xhat)) (+ dres),  g = dy * w,  xhat = x * r.  RES: the
+// gradient reaching the residual stream directly is added in the same pass (the fused
+// add + norm's backward: both summands of the residual get this dx).
+template <bool RES>
 __global__ __launch_bounds__(256) void rmsnorm_bwd_dx_kernel(const bf16_t* __restrict__ x,
                                                              const bf16_t* __restrict__ w,
                                                              const bf16_t* __restrict__ dy,
+                                                             const bf16_t* __restrict__ dres,
                                                              const float* __restrict__ rstd,
                                                              bf16_t* __restrict__ dx, int rows,
                                                              int d, int rows_per_trial) {
@@ -145,6 +161,12 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_dx_kernel(const bf16_t* __res
       float o[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = r * (gv[k][e] - xh[k][e] * mdot);
+      if (RES) {
+        float rv[8];
+        unpack8(*(const uint4*)(dres + (size_t)row * d + 8 * c), rv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += rv[e];
+      }
       *(uint4*)(dx + (size_t)row * d + 8 * c) = pack8(o);
     }
   }
@@ -528,19 +550,50 @@ extern "C" {
 int mopt_rmsnorm_fwd(const void* x, const void* w, void* y, void* rstd, int rows, int d,
                      int rows_per_trial, float eps, void* stream) {
   if (d % 8 || d > 64 * 8 * kMaxChunks) return 1;
-  hipLaunchKernelGGL(rmsnorm_fwd_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream,
-                     (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)rstd, rows, d,
+  hipLaunchKernelGGL(rmsnorm_fwd_kernel<false>, dim3((rows + 3) / 4), dim3(256), 0,
+                     (hipStream_t)stream, (const bf16_t*)x, (const bf16_t*)nullptr,
+                     (bf16_t*)nullptr, (const bf16_t*)w, (bf16_t*)y, (float*)rstd, rows, d,
                      rows_per_trial, eps);
   return (int)hipGetLastError();
 }
 
+// xs = x + res; y = rmsnorm(xs) * w   (the transformer's residual add fused into the next norm)
+int mopt_add_rmsnorm_fwd(const void* x, const void* res, void* xs, const void* w, void* y,
+                         void* rstd, int rows, int d, int rows_per_trial, float eps,
+                         void* stream) {
+  if (d % 8 || d > 64 * 8 * kMaxChunks) return 1;
+  hipLaunchKernelGGL(rmsnorm_fwd_kernel<true>, dim3((rows + 3) / 4), dim3(256), 0,
+                     (hipStream_t)stream, (const bf16_t*)x, (const bf16_t*)res, (bf16_t*)xs,
+                     (const bf16_t*)w, (bf16_t*)y, (float*)rstd, rows, d, rows_per_trial, eps);
+  return (int)hipGetLastError();
+}
+
+// dx = rmsnorm_bwd(dy) (+ dres when dres != null); dw32 += the weight gradient
+int mopt_rmsnorm_bwd_res(const void* x, const void* w, const void* dy, const void* dres,
+                         const void* rstd, void* dx, void* dw32, int rows, int d,
+                         int rows_per_trial, void* stream);
+
 int mopt_rmsnorm_bwd(const void* x, const void* w, const void* dy, const void* rstd, void* dx,
                      void* dw32, int rows, int d, int rows_per_trial, void* stream) {
+  return mopt_rmsnorm_bwd_res(x, w, dy, nullptr, rstd, dx, dw32, rows, d, rows_per_trial,
+                              stream);
+}
+
+int mopt_rmsnorm_bwd_res(const void* x, const void* w, const void* dy, const void* dres,
+                         const void* rstd, void* dx, void* dw32, int rows, int d,
+                         int rows_per_trial, void* stream) {
   if (d % 8 || d > 64 * 8 * kMaxChunks) return 1;
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(rmsnorm_bwd_dx_kernel, dim3((rows + 3) / 4), dim3(256), 0, st,
-                     (const bf16_t*)x, (const bf16_t*)w, (const bf16_t*)dy, (const float*)rstd,
-                     (bf16_t*)dx, rows, d, rows_per_trial);
+  if (dres != nullptr)
+    hipLaunchKernelGGL(rmsnorm_bwd_dx_kernel<true>, dim3((rows + 3) / 4), dim3(256), 0, st,
+                       (const bf16_t*)x, (const bf16_t*)w, (const bf16_t*)dy,
+                       (const bf16_t*)dres, (const float*)rstd, (bf16_t*)dx, rows, d,
+                       rows_per_trial);
+  else
+    hipLaunchKernelGGL(rmsnorm_bwd_dx_kernel<false>, dim3((rows + 3) / 4), dim3(256), 0, st,
+                       (const bf16_t*)x, (const bf16_t*)w, (const bf16_t*)dy,
+                       (const bf16_t*)nullptr, (const float*)rstd, (bf16_t*)dx, rows, d,
+                       rows_per_trial);
   const int P = rows / rows_per_trial;
   const int splits = max(1, min(64, rows_per_trial / 64));
   hipLaunchKernelGGL(rmsnorm_bwd_dw_kernel, dim3((d + 255) / 256, splits, P), dim3(256), 0, st,

@@ -27,6 +27,8 @@ _lib.register_signatures({
     "mopt_attn_bwd": ([c_void_p] * 10 + [c_int, c_int, c_int, c_float, c_void_p], c_int),
     "mopt_rmsnorm_fwd": ([c_void_p] * 4 + [c_int, c_int, c_int, c_float, c_void_p], c_int),
     "mopt_rmsnorm_bwd": ([c_void_p] * 6 + [c_int, c_int, c_int, c_void_p], c_int),
+    "mopt_add_rmsnorm_fwd": ([c_void_p] * 6 + [c_int, c_int, c_int, c_float, c_void_p], c_int),
+    "mopt_rmsnorm_bwd_res": ([c_void_p] * 7 + [c_int, c_int, c_int, c_void_p], c_int),
     "mopt_rope_fwd": ([c_void_p] * 6 + [c_int, c_int, c_int, c_void_p], c_int),
     "mopt_rope_bwd": ([c_void_p] * 6 + [c_int, c_int, c_int, c_void_p], c_int),
     "mopt_swiglu_fwd": ([c_void_p, c_void_p, c_int64, c_int, c_void_p], c_int),
@@ -161,6 +163,47 @@ def rmsnorm(x, w, rows_per_trial, eps=1e-5):
     if _hip(x, "rmsnorm"):
         return _RMSNorm.apply(x.contiguous(), w.contiguous(), rows_per_trial, eps)
     return rmsnorm_ref(x, w, rows_per_trial, eps)
+
+
+class _AddRMSNorm(torch.autograd.Function):
+    """(x + delta, rmsnorm(x + delta)) in one pass; the backward returns one gradient for both
+    summands: the norm's dx plus the gradient that reached the sum directly, also one pass."""
+
+    @staticmethod
+    def forward(ctx, x, delta, w, rows_per_trial, eps):
+        R, d = x.shape
+        xs = torch.empty_like(x)
+        y = torch.empty_like(x)
+        rstd = torch.empty(R, dtype=torch.float32, device=x.device)
+        _call("mopt_add_rmsnorm_fwd", _p(x), _p(delta), _p(xs), _p(w), _p(y), _p(rstd), R, d,
+              rows_per_trial, eps, _stream(x))
+        ctx.save_for_backward(xs, w, rstd)
+        ctx.rpt = rows_per_trial
+        return xs, y
+
+    @staticmethod
+    def backward(ctx, dxs, dy):
+        xs, w, rstd = ctx.saved_tensors
+        R, d = xs.shape
+        dw32 = torch.zeros(w.shape, dtype=torch.float32, device=xs.device)
+        if dy is None:
+            return dxs, dxs, None, None, None
+        dy = dy.contiguous()
+        dres = dxs.contiguous() if dxs is not None else None
+        dx = torch.empty_like(xs)
+        _call("mopt_rmsnorm_bwd_res", _p(xs), _p(w), _p(dy),
+              _p(dres) if dres is not None else None, _p(rstd), _p(dx), _p(dw32), R, d,
+              ctx.rpt, _stream(xs))
+        return dx, dx, dw32.to(w.dtype), None, None
+
+
+def add_rmsnorm(x, delta, w, rows_per_trial, eps=1e-5):
+    """Residual add fused into the following pre-norm: returns ``(x + delta, rmsnorm(x + delta))``."""
+    if _hip(x, "add_rmsnorm"):
+        return _AddRMSNorm.apply(x.contiguous(), delta.contiguous(), w.contiguous(),
+                                 rows_per_trial, eps)
+    xs = x + delta
+    return xs, rmsnorm_ref(xs, w, rows_per_trial, eps)
 
 
 class _RopeSplit(torch.autograd.Function):

@@ -52,6 +52,31 @@ def test_rmsnorm_fwd_bwd():
     _close(w.grad, wr.grad, 2e-2)
 
 
+@pytest.mark.parametrize("use_xs", [True, False])
+def test_add_rmsnorm_fwd_bwd(use_xs):
+    """Fused residual add + norm vs (x + delta, rmsnorm_ref) in fp32: outputs and the gradients
+    of both summands and the weight, with and without a gradient flowing into the sum."""
+    torch.manual_seed(4)
+    P, rpt, d = 2, 128, 768
+    x = torch.randn(P * rpt, d, device=DEV).to(torch.bfloat16).requires_grad_(True)
+    dl = torch.randn(P * rpt, d, device=DEV).to(torch.bfloat16).requires_grad_(True)
+    w = (1 + 0.1 * torch.randn(P, d, device=DEV)).to(torch.bfloat16).requires_grad_(True)
+    dy = torch.randn(P * rpt, d, device=DEV).to(torch.bfloat16)
+    dxs = torch.randn(P * rpt, d, device=DEV).to(torch.bfloat16)
+    xs, y = ops.add_rmsnorm(x, dl, w, rpt)
+    torch.autograd.backward([y, xs] if use_xs else [y], [dy, dxs] if use_xs else [dy])
+    xr, dr, wr = (t.detach().float().requires_grad_(True) for t in (x, dl, w))
+    xsr = xr + dr
+    yr = ops.rmsnorm_ref(xsr, wr, rpt)
+    torch.autograd.backward([yr, xsr] if use_xs else [yr],
+                            [dy.float(), dxs.float()] if use_xs else [dy.float()])
+    _close(xs, xsr, 1e-2)
+    _close(y, yr, 1e-2)
+    _close(x.grad, xr.grad, 2e-2)
+    _close(dl.grad, dr.grad, 2e-2)
+    _close(w.grad, wr.grad, 2e-2)
+
+
 def test_rope_split_roundtrip():
     torch.manual_seed(2)
     Bp, T, H = 2, 128, 3
