@@ -5,8 +5,10 @@ Architecture (He et al. 2016, CIFAR variant): 3x3 conv 16 -> 3 stages x 3 basic 
 64 channels; stride 2 at stages 2 and 3 with the parameter-free "option A" shortcut: subsample +
 zero-pad channels) -> global average pool -> linear 64 -> 10; ~0.27M parameters per trial.
 Activations are NHWC bf16 with the population folded into the batch; images carry 8 channels
-(3 real + 5 zero) so every kernel moves 16-byte vectors.  Convolutions: HIP im2col/col2im +
-population-batched GEMMs; BatchNorm (+ residual + ReLU) fused HIP kernels with per-trial batch
+(3 real + 5 zero) so every kernel moves 16-byte vectors.  Convolutions: implicit GEMMs on the
+population MFMA kernel (ops/conv.py -> csrc/pgemm.hip: the 3x3 taps are gathered while the
+operand tiles are staged, forward / data-gradient / weight-gradient, no im2col buffer);
+BatchNorm (+ residual + ReLU) fused HIP kernels with per-trial batch
 and running statistics; SGD-momentum with per-trial lr / momentum / weight decay (fused K5).
 """
 from __future__ import annotations
