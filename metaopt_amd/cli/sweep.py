@@ -36,6 +36,13 @@ def add_subparser(parser):
     g.add_argument("--steps", type=int, default=100000, help="max population steps")
     g.add_argument("--sync-every", type=int, default=32)
     g.add_argument("--seed", type=int, default=0)
+    g.add_argument("--event-log", default=None,
+                   help="JSONL event log path (rank r writes <path>.rank<r> when world > 1)")
+    g.add_argument("--trial-events", action="store_true",
+                   help="one event per finished trial in the event log")
+    g.add_argument("--watchdog", type=float, default=0.0,
+                   help="seconds without a sync before the rank fails the job cleanly "
+                        "(in-flight trials -> interrupted); 0 disables")
     p.set_defaults(func=main)
     return p
 
@@ -63,11 +70,25 @@ def main(args):
                                       priors=dict(task.priors), algorithms=algo,
                                       max_trials=args["max_trials"] or float("inf"),
                                       pool_size=P * comm.world_size)
+    events = watchdog = None
+    if args.get("event_log"):
+        from ..utils.events import EventLog
+        path = args["event_log"]
+        if comm.world_size > 1:
+            path = f"{path}.rank{comm.rank}"
+        events = EventLog(path, rank=comm.rank)
+    if args.get("watchdog"):
+        from ..parallel.watchdog import Watchdog
+        watchdog = Watchdog(args["watchdog"], events=events, rank=comm.rank)
     sweep = PopulationSweep(pop, task, data, comm=comm, experiment=experiment,
                             sync_every=args["sync_every"],
-                            ckpt_capacity=max(4, int(spec.ckpt_factor * P)))
+                            ckpt_capacity=max(4, int(spec.ckpt_factor * P)),
+                            events=events, trial_events=args.get("trial_events", False),
+                            watchdog=watchdog)
     summary = sweep.run(args["steps"])
     sweep.close()
+    if events is not None:
+        events.close()
     if comm.is_root:
         print(json.dumps({k: v for k, v in summary.items()}, default=str))
     shutdown()

@@ -92,9 +92,22 @@ def get_lib(build_if_missing: bool = True):
         return lib
 
 
+# Debug mode (SURVEY.md §5 "race detection / sanitizers": the HIP-side analogue of
+# HIP_LAUNCH_BLOCKING): MOPT_SYNC_CHECK=1 synchronises the device after every kernel launch
+# that is not being captured into a graph, so an asynchronous fault (out-of-bounds access,
+# illegal instruction) is reported at the launch that caused it, naming that kernel.
+SYNC_CHECK = os.environ.get("MOPT_SYNC_CHECK", "0") not in ("", "0")
+
+
 def check(err: int, what: str) -> None:
     if err != 0:
         raise RuntimeError(f"HIP launch of {what} failed with hipError_t {err}")
+    if SYNC_CHECK and torch.cuda.is_available() and not torch.cuda.is_current_stream_capturing():
+        try:
+            torch.cuda.synchronize()
+        except RuntimeError as exc:
+            raise RuntimeError(f"[MOPT_SYNC_CHECK] device fault after launching {what}: "
+                               f"{exc}") from exc
 
 
 def stream_ptr(device=None) -> int:

@@ -40,6 +40,7 @@ from ..algo.primary import PrimaryAlgo
 from ..ops.population import MemberConfig, PopulationMLP
 from ..parallel.comm import Comm
 from ..storage.database import DuplicateKeyError
+from ..utils.events import NullEventLog
 
 log = logging.getLogger(__name__)
 
@@ -53,7 +54,8 @@ class PopulationSweep:
     def __init__(self, pop: PopulationMLP, task, data, comm: Optional[Comm] = None,
                  experiment=None, sync_every: int = 16, ckpt_capacity: int = 512,
                  heartbeat_every: float = 30.0, max_trials: Optional[float] = None,
-                 pipelined: Optional[bool] = None):
+                 pipelined: Optional[bool] = None, events=None, trial_events: bool = False,
+                 watchdog=None):
         self.pop = pop
         self.task = task
         self.data = data
@@ -107,6 +109,10 @@ class PopulationSweep:
         self._bad_now = np.zeros(P, dtype=bool)
         self._busy_marker = None
         self._ctl_stream = None
+        # observability / failure detection (utils/events.py, parallel/watchdog.py)
+        self.events = events if events is not None else NullEventLog()
+        self.trial_events = bool(trial_events) and events is not None
+        self.watchdog = watchdog
         if pipelined is None:   # every rank must agree: rank 0 knows the algorithm
             sync_algo = bool(getattr(experiment.algorithms, "synchronous", False)) \
                 if self.comm.is_root else False
@@ -135,6 +141,14 @@ class PopulationSweep:
                 self._pkey_idx = idx
             inner = getattr(self.algorithm, "algorithm", self.algorithm)
             self._tracks_lineage = hasattr(inner, "parent_of")
+            if watchdog is not None:
+                watchdog.on_stall.append(self._interrupt_in_flight)
+        if watchdog is not None:
+            watchdog.events = watchdog.events or events
+            watchdog.start()
+        self.events.emit("sweep_start", world_size=self.comm.world_size, population=P,
+                         sync_every=self.sync_every, pipelined=self.pipelined,
+                         algorithm=type(getattr(self, "algorithm", None)).__name__)
 
     def _gc_callback(self, phase, info):
         if phase == "start":
@@ -278,6 +292,14 @@ class PopulationSweep:
         if self.pipelined:
             self._drain_writes()
         t5 = time.perf_counter()
+        if self.watchdog is not None:
+            self.watchdog.beat("sync")
+        if self.comm.is_root:
+            self.events.emit("sync", step=self.global_step, completed=self.completed,
+                             broken=self.broken, active=self._n_active, best=self.best[0],
+                             ms={"status": 1e3 * (t1 - t0), "c1_allgather": 1e3 * (t2 - t1),
+                                 "decide": 1e3 * (t3 - t2), "c5_broadcast": 1e3 * (t4 - t3),
+                                 "apply": 1e3 * (t5 - t4)})
         tm["status"] += t1 - t0
         tm["c1_allgather"] += t2 - t1
         tm["decide"] += t3 - t2
@@ -343,6 +365,9 @@ class PopulationSweep:
             if g[8] > 0:
                 self.broken += 1
                 self._set_status(doc, "broken")
+                if self.trial_events:
+                    self.events.emit("trial", id=doc["_id"], status="broken", objective=None,
+                                     budget=None)
                 continue
             vl, va, tl = g[6], g[7], g[5]
             self._writer.put_update(doc["_id"], {
@@ -352,6 +377,9 @@ class PopulationSweep:
                 "status": "completed", "end_time": now, "heartbeat": doc["heartbeat"]})
             self.completed += 1
             budget = int(self.task.budget(params))
+            if self.trial_events:
+                self.events.emit("trial", id=doc["_id"], status="completed", objective=vl,
+                                 budget=budget)
             self.history.append((time.time(), rkey, vl, budget))
             if vl < self.best[0]:
                 self.best = (vl, dict(params))
@@ -503,7 +531,28 @@ class PopulationSweep:
         if self._writer is not None:
             self._writer.flush()
 
+    def _interrupt_in_flight(self, stalled_s: float = 0.0, phase: str = "") -> int:
+        """Watchdog callback (rank 0): persist held writes, then mark every in-flight trial
+        ``interrupted`` so another worker or a re-run reserves it again -- the state a lost
+        heartbeat leads to in the reference (src/orion/core/worker/experiment.py:217-232)."""
+        if self._writer is None:
+            return 0
+        now = datetime.datetime.utcnow()
+        for doc in list(self.trials.values()):
+            self._writer.put_update(doc["_id"], {"status": "interrupted", "heartbeat": now},
+                                    was="reserved")
+        n = len(self.trials)
+        self._writer.flush()
+        self.events.emit("interrupted", n_trials=n)
+        self.events.flush()
+        return n
+
     def close(self) -> None:
+        if self.watchdog is not None:
+            self.watchdog.stop()
+        self.events.emit("sweep_end", **{k: v for k, v in self.summary().items()
+                                         if k != "host_ms_per_sync"})
+        self.events.flush()
         if self._gc_callback in gc.callbacks:
             gc.callbacks.remove(self._gc_callback)
         if self._writer is not None:
