@@ -162,7 +162,26 @@ class DocumentStorage(BaseStorageProtocol):
         uid = _uid(experiment, uid, "experiment")
         self._db.remove("trials", {"experiment": uid})
         self._db.remove("lying_trials", {"experiment": uid})
+        self._db.remove("algo_state", {"experiment": uid})
         return self._db.remove("experiments", {"_id": uid})
+
+    # -- algorithm state ----------------------------------------------------------------------------
+    # The reference never persists algorithm state: a worker rebuilds it by replaying every
+    # completed trial through ``observe`` (src/orion/core/worker/producer.py:103-132).  A device
+    # sweep completes thousands of trials per second, so the algorithm's ``state_dict`` is stored
+    # instead (one document per experiment, SURVEY.md §5 "Checkpoint / resume") and restored on
+    # re-run with ``set_state``.
+    def save_algorithm_state(self, experiment=None, uid=None, state=None) -> None:
+        uid = _uid(experiment, uid, "experiment")
+        doc = {"state": state, "updated": utcnow()}
+        if not self._db.write("algo_state", data=doc, query={"experiment": uid}):
+            doc["experiment"] = uid
+            self._db.write("algo_state", data=doc)
+
+    def get_algorithm_state(self, experiment=None, uid=None) -> Optional[dict]:
+        uid = _uid(experiment, uid, "experiment")
+        docs = self._db.read("algo_state", {"experiment": uid})
+        return docs[0]["state"] if docs else None
 
     # -- trials -----------------------------------------------------------------------------------
     def fetch_trials(self, experiment=None, uid=None, query=None):

@@ -55,7 +55,7 @@ class PopulationSweep:
                  experiment=None, sync_every: int = 16, ckpt_capacity: int = 512,
                  heartbeat_every: float = 30.0, max_trials: Optional[float] = None,
                  pipelined: Optional[bool] = None, events=None, trial_events: bool = False,
-                 watchdog=None):
+                 watchdog=None, restore_algorithm: bool = False):
         self.pop = pop
         self.task = task
         self.data = data
@@ -143,6 +143,11 @@ class PopulationSweep:
             self._tracks_lineage = hasattr(inner, "parent_of")
             if watchdog is not None:
                 watchdog.on_stall.append(self._interrupt_in_flight)
+            if restore_algorithm:
+                state = experiment.storage.get_algorithm_state(experiment)
+                if state is not None:
+                    self.algorithm.set_state(state)
+                    log.info("algorithm state restored from storage")
         if watchdog is not None:
             watchdog.events = watchdog.events or events
             watchdog.start()
@@ -547,9 +552,20 @@ class PopulationSweep:
         self.events.flush()
         return n
 
+    def save_algorithm_state(self) -> None:
+        """Rank 0: store the algorithm's ``state_dict`` with the experiment (resume without
+        replaying every trial through ``observe``)."""
+        if self.comm.is_root and self.experiment is not None:
+            self.experiment.storage.save_algorithm_state(self.experiment,
+                                                         state=self.algorithm.state_dict)
+
     def close(self) -> None:
         if self.watchdog is not None:
             self.watchdog.stop()
+        try:
+            self.save_algorithm_state()
+        except Exception as exc:  # pragma: no cover - storage without the collection API
+            log.warning("algorithm state not saved: %s", exc)
         self.events.emit("sweep_end", **{k: v for k, v in self.summary().items()
                                          if k != "host_ms_per_sync"})
         self.events.flush()

@@ -147,3 +147,37 @@ def test_sync_check_mode_runs_population_step(monkeypatch):
     pop.train_step(x, y)
     torch.cuda.synchronize()
     assert all(math.isfinite(v) for v in pop.train_loss()[:2])
+
+
+def _canon(v):
+    import numpy as np
+    if isinstance(v, dict):
+        return {str(k): _canon(x) for k, x in sorted(v.items(), key=lambda kv: str(kv[0]))}
+    if isinstance(v, (list, tuple)):
+        return [_canon(x) for x in v]
+    if isinstance(v, np.ndarray):
+        return v.tolist()
+    if isinstance(v, np.generic):
+        return v.item()
+    return v
+
+
+def test_sweep_persists_and_restores_algorithm_state(data):
+    """close() stores the algorithm's state_dict with the experiment; a re-run restores it
+    instead of replaying every trial through observe()."""
+    exp, sweep = _sweep(data, "state-sweep", 12)
+    sweep.run(1000)
+    sweep.close()
+    state = exp.storage.get_algorithm_state(exp)
+    assert state is not None
+    assert _canon(state) == _canon(exp.algorithms.state_dict)
+    pop = PopulationMLP(4, max_width=128, eval_batch=128, device="cpu")
+    fresh = build_experiment("state-sweep-2", priors=PRIORS,
+                             algorithms={"asha": {"seed": 9, "repetitions": float("inf")}},
+                             max_trials=12, storage=exp.storage)
+    fresh.storage.save_algorithm_state(fresh, state=state)
+    assert _canon(fresh.algorithms.state_dict) != _canon(state)
+    sweep2 = PopulationSweep(pop, MLPSweepTask(priors=PRIORS, max_width=128), data,
+                             experiment=fresh, sync_every=16, restore_algorithm=True)
+    assert _canon(fresh.algorithms.state_dict) == _canon(state)
+    sweep2.close()
