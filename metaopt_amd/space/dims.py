@@ -233,6 +233,8 @@ class Real(Dimension):
         rng = check_random_state(seed)
         draws = self._rvs(n_samples, rng).astype(float, copy=False)
         draws = self._redraw(draws, rng, lambda k: self._rvs(k, rng).astype(float, copy=False))
+        if not self.shape:
+            return draws.tolist()       # python floats in one C pass (no per-value .item())
         return [self._post(d) for d in draws]
 
     def _redraw(self, draws, rng, draw_fn):
@@ -303,7 +305,7 @@ class Integer(Real, _Discrete):
         draws = self._redraw(draws, rng,
                              lambda k: numpy.floor(self._rvs(k, rng).astype(float)))
         draws = draws.astype(int)
-        return [d if self.shape else int(d) for d in draws]
+        return list(draws) if self.shape else draws.tolist()
 
     def cast(self, point):
         out = numpy.asarray(point).astype(int)

@@ -81,7 +81,7 @@ class PopulationSweep:
         # rank-0 bookkeeping
         # in-flight trials as storage documents (the Trial schema of core/trial.py, built
         # directly: object construction and re-hashing per trial dominated rank 0's host time)
-        self.trials: Dict[int, dict] = {}             # key -> reserved trial document
+        self.trials: Dict[int, list] = {}             # key -> [trial id, heartbeat] (reserved)
         self.key_params: Dict[int, dict] = {}
         self.key_pkey: Dict[int, str] = {}
         self.ckpt_index: Dict[str, tuple] = {}        # param key -> (rank, trial key, steps)
@@ -121,7 +121,8 @@ class PopulationSweep:
         if self.comm.is_root:
             self.algorithm = experiment.algorithms
             self.space = experiment.space
-            self._writer = _WriteBehind(experiment.storage)
+            self._writer = _WriteBehind(experiment.storage, build_doc=self._build_doc,
+                                        build_fields=self._result_fields)
             self._dim_names = list(self.space.keys())
             self._dim_types = [d.type for d in self.space.values()]
             self._exp_str = str(experiment.id)
@@ -371,19 +372,15 @@ class PopulationSweep:
                 self.broken += 1
                 self._set_status(doc, "broken")
                 if self.trial_events:
-                    self.events.emit("trial", id=doc["_id"], status="broken", objective=None,
+                    self.events.emit("trial", id=doc[0], status="broken", objective=None,
                                      budget=None)
                 continue
             vl, va, tl = g[6], g[7], g[5]
-            self._writer.put_update(doc["_id"], {
-                "results": [{"name": "val_loss", "type": "objective", "value": vl},
-                            {"name": self._sec_name, "type": "statistic", "value": va},
-                            {"name": "train_loss", "type": "statistic", "value": tl}],
-                "status": "completed", "end_time": now, "heartbeat": doc["heartbeat"]})
+            self._writer.put_update_spec(doc[0], (vl, va, tl, now, doc[1]))
             self.completed += 1
             budget = int(self.task.budget(params))
             if self.trial_events:
-                self.events.emit("trial", id=doc["_id"], status="completed", objective=vl,
+                self.events.emit("trial", id=doc[0], status="completed", objective=vl,
                                  budget=budget)
             self.history.append((time.time(), rkey, vl, budget))
             if vl < self.best[0]:
@@ -486,22 +483,35 @@ class PopulationSweep:
                 n_free[rank] += 1
                 continue
             self._registered.add(tid)
-            doc = {"experiment": self.experiment.id, "status": "reserved", "worker": None,
-                   "heartbeat": stamp, "submit_time": stamp, "start_time": stamp,
-                   "end_time": None, "results": [],
-                   "params": [{"name": n, "type": t, "value": v}
-                              for n, t, v in zip(keys, self._dim_types, point)],
-                   "parents": [self._doc_id(parent)] if parent is not None else [],
-                   "_id": tid}
-            self._writer.put_register(doc)
+            self._writer.put_register_spec(
+                (tid, stamp, point, self._doc_id(parent) if parent is not None else None))
             key = self.next_key
             self.next_key += 1
-            self.trials[key] = doc
+            self.trials[key] = [tid, stamp]      # [trial id, last heartbeat]
             self.key_params[key] = params
             self.key_pkey[key] = pkey
             cfg = self.task.member_config(params, self.task.seed_of(pkey))
             assign[row] = (action, key, cfg.width, cfg.lr, cfg.momentum, cfg.weight_decay,
                            cfg.dropout, cfg.seed, self.task.budget(params), resume, src)
+
+    def _build_doc(self, spec) -> dict:
+        """Trial document (core/trial.py schema) of a registration queued by ``_fill``."""
+        tid, stamp, point, parent = spec
+        return {"experiment": self.experiment.id, "status": "reserved", "worker": None,
+                "heartbeat": stamp, "submit_time": stamp, "start_time": stamp,
+                "end_time": None, "results": [],
+                "params": [{"name": n, "type": t, "value": v}
+                           for n, t, v in zip(self._dim_names, self._dim_types, point)],
+                "parents": [parent] if parent is not None else [],
+                "_id": tid}
+
+    def _result_fields(self, spec) -> dict:
+        """Fields of a completed trial's update queued by ``_decide``."""
+        vl, va, tl, now, hb = spec
+        return {"results": [{"name": "val_loss", "type": "objective", "value": vl},
+                            {"name": self._sec_name, "type": "statistic", "value": va},
+                            {"name": "train_loss", "type": "statistic", "value": tl}],
+                "status": "completed", "end_time": now, "heartbeat": hb}
 
     def _point_key(self, point, params=None) -> str:
         """``task.key(params)`` of a suggested point (python scalars, space order)."""
@@ -518,7 +528,7 @@ class PopulationSweep:
                            .encode("utf-8")).hexdigest()
 
     def _set_status(self, doc, status):
-        self._writer.put_update(doc["_id"], {"status": status,
+        self._writer.put_update(doc[0], {"status": status,
                                              "heartbeat": datetime.datetime.utcnow()},
                                 was="reserved")
 
@@ -528,8 +538,8 @@ class PopulationSweep:
         self._last_hb = time.time()
         now = datetime.datetime.utcnow()
         for doc in list(self.trials.values()):
-            doc["heartbeat"] = now
-            self._writer.put_update(doc["_id"], {"heartbeat": now}, was="reserved")
+            doc[1] = now
+            self._writer.put_update(doc[0], {"heartbeat": now}, was="reserved")
 
     def flush(self) -> None:
         """Wait until every queued storage write has been applied."""
@@ -544,7 +554,7 @@ class PopulationSweep:
             return 0
         now = datetime.datetime.utcnow()
         for doc in list(self.trials.values()):
-            self._writer.put_update(doc["_id"], {"status": "interrupted", "heartbeat": now},
+            self._writer.put_update(doc[0], {"status": "interrupted", "heartbeat": now},
                                     was="reserved")
         n = len(self.trials)
         self._writer.flush()
@@ -703,8 +713,12 @@ class _WriteBehind:
     holds).  Consecutive registrations become one bulk insert.  ``flush`` applies everything.
     """
 
-    def __init__(self, storage):
+    def __init__(self, storage, build_doc=None, build_fields=None):
         self.storage = storage
+        # deferred construction: the decision path queues compact tuples and the documents
+        # (registrations) / field dicts (results) are built here, inside the GPU-busy window
+        self.build_doc = build_doc
+        self.build_fields = build_fields
         self.errors = 0
         self._held: "collections.deque" = collections.deque()
         self.busy_s = 0.0             # seconds spent applying writes
@@ -717,6 +731,14 @@ class _WriteBehind:
     def put_update(self, uid, fields: dict, was=None):
         """Set ``fields`` of trial ``uid`` (only while its status is ``was``, when given)."""
         self._held.append(("update", (uid, fields, was)))
+
+    def put_register_spec(self, spec: tuple):
+        """Register the trial document ``build_doc(spec)`` (built when the write is applied)."""
+        self._held.append(("register", spec))
+
+    def put_update_spec(self, uid, spec: tuple, was=None):
+        """Set the fields ``build_fields(spec)`` of trial ``uid`` (built when applied)."""
+        self._held.append(("update", (uid, spec, was)))
 
     def __len__(self):
         return len(self._held)
@@ -738,12 +760,16 @@ class _WriteBehind:
 
     def _apply_batch(self, held):
         if held[0][0] == "register":
-            docs = [h[1] for h in held]
+            build = self.build_doc
+            docs = [h[1] if type(h[1]) is dict else build(h[1]) for h in held]
             if not self._call("register_trial_docs", docs, owned=True):
                 for d in docs:            # a bulk insert hit a duplicate: insert one by one
                     self._call("register_trial_docs", [dict(d)])
             return
-        self._call("update_trial_docs", [h[1] for h in held])
+        fields = self.build_fields
+        self._call("update_trial_docs",
+                   [h[1] if type(h[1][1]) is dict else (h[1][0], fields(h[1][1]), h[1][2])
+                    for h in held])
 
     def _call(self, method, *args, **kwargs) -> bool:
         try:
