@@ -20,6 +20,8 @@ def _free_port():
 def _init(rank, world, port):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch
+    torch.set_num_threads(2)   # ranks share the host's CPUs (and pytest-xdist workers)
     from metaopt_amd.parallel.comm import init_from_env
     return init_from_env(backend="gloo")
 

@@ -181,3 +181,21 @@ def test_sweep_persists_and_restores_algorithm_state(data):
                              experiment=fresh, sync_every=16, restore_algorithm=True)
     assert _canon(fresh.algorithms.state_dict) == _canon(state)
     sweep2.close()
+
+
+@pytest.mark.parametrize("task,steps", [("logreg", 288)])
+def test_sweep_cli_event_log_and_watchdog_flags(tmp_path, capsys, task, steps):
+    """``mopt --debug sweep ... --event-log --trial-events --watchdog`` on the CPU backend."""
+    import json
+    from metaopt_amd.cli import main
+    path = str(tmp_path / "cli.jsonl")
+    rc = main(["--debug", "sweep", "--task", task, "--population", "4", "--steps", str(steps),
+               "--max-trials", "8", "--sync-every", "16", "--event-log", path,
+               "--trial-events", "--watchdog", "600"])
+    assert rc == 0
+    summary = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    kinds = [r["event"] for r in read_events(path)]
+    assert kinds[0] == "sweep_start" and kinds[-1] == "sweep_end"
+    n_trials = len(list(read_events(path, "trial")))
+    assert n_trials == summary["completed"] + summary["broken"] > 0
+    assert "watchdog" not in kinds
