@@ -164,7 +164,7 @@ __device__ __forceinline__ void fwd_gemm(const bf16_t* __restrict__ X, const bf1
 #undef MOPT_FWD_STORE
 
 // Y[rows, n0:n0+64] = dropout(relu(X W^T + b)) for one (trial-layer, n-tile, 128-row block).
-__global__ __launch_bounds__(256) void mlp_fwd_kernel(const MlpTL* __restrict__ tls,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void mlp_fwd_kernel(const MlpTL* __restrict__ tls,
                                                       const int2* __restrict__ work, int n_work,
                                                       const bf16_t* __restrict__ xb,
                                                       const float* __restrict__ p32,
