@@ -2,17 +2,27 @@
 """Headline benchmark: ASHA sweep of 4-layer MLPs, device populations, 1 process per GPU.
 
 Metric (BASELINE.json): trials/sec for the whole node + best-loss@budget, 4-layer MLP sweep.
-  * one *trial* = one epoch-equivalent (60,032 samples, 469 steps x 128) of a 4-layer MLP
-    784-w-w-w-10 (w ~ loguniform(64, 1024)), SGD-momentum, dropout, bf16 compute -- the unit of
-    the reference's MNIST tutorial sweep (5 trials in 49.75 s = 0.1005 trials/s,
-    reference docs/src/user/pytorch.rst:131-136);
-  * the timed region is the whole sweep loop: population train steps (HIP kernels), validation
-    of finished trials, C1 metric all-gather, ASHA decisions on rank 0, C5 assignment broadcast,
-    member (re)initialisation and checkpoint-resume of promoted trials;
-  * weak scaling: every GPU holds ``--population`` (256) trials.
 
-``python bench.py --gpus N --steps K --warmup W``; for N > 1 launch with torchrun (one rank per
-GPU).  Rank 0 prints one JSON line.
+* One bench **step** is one *sync interval* of the population sweep: ``--sync-every`` (32)
+  optimizer steps of every resident trial (HIP kernels), followed by the sync -- validation of the
+  trials that reached their budget, C1 metric all-gather, ASHA observe/suggest on rank 0, C5
+  assignment broadcast, (re)initialisation of new members and checkpoint-resume of promoted ones.
+  Every timed step therefore contains the whole sweep loop, whatever ``--steps`` is.
+* ``value`` counts *epoch-equivalent* trials: 60,032 samples (469 steps x 128) through a 4-layer
+  MLP 784-w-w-w-10 -- the unit of the reference's MNIST tutorial sweep (5 trials in 49.75 s =
+  0.1005 trials/s, reference docs/src/user/pytorch.rst:131-136).  The JSON also reports the
+  ASHA trials actually completed (one trial document per rung evaluation, as in the reference's
+  ASHA) per second, and the best validation loss at a fixed budget of ``--budget-intervals``
+  sync intervals from the start of the sweep (stated in the JSON).
+* ASHA fidelity is ``fidelity(32, 512, 4)`` optimizer steps (rungs 32/128/512; the top rung is
+  65,536 samples ~ one MNIST epoch), so complete ASHA ladders fit in the driver's short run.
+* Weak scaling: every GPU holds ``--population`` (256) trials.
+
+``python bench.py --gpus N --steps K --warmup W``.  Under torchrun (WORLD_SIZE set) every process
+is one rank.  Without it and ``N > 1`` this process is only a launcher: it starts N rank processes
+(RANK/LOCAL_RANK/WORLD_SIZE/MASTER_ADDR=127.0.0.1) without touching the GPU itself, and when the
+machine has fewer than N GPUs the ranks share them over gloo (a rehearsal, flagged in the JSON).
+Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
@@ -20,10 +30,10 @@ import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
-
-import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
@@ -31,24 +41,84 @@ sys.path.insert(0, HERE)
 METRIC = "trials/sec (whole node) + best-loss@budget, 4-layer MLP sweep at 1/2/4/8 MI355X"
 BASELINE_TRIALS_PER_SEC = 5.0 / 49.751548  # reference MNIST tutorial sweep
 SAMPLES_PER_TRIAL = 60032                   # one epoch-equivalent of MNIST (469 x 128)
+BENCH_PRIORS = {
+    "/lr": "loguniform(1e-3, 1.0)",
+    "/width": "loguniform(64, 1024, discrete=True)",
+    "/dropout": "uniform(0, 0.5)",
+    "/steps": "fidelity(32, 512, 4)",
+}
 
 
-def main(argv=None):
-    ap = argparse.ArgumentParser()
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=320)
-    ap.add_argument("--warmup", type=int, default=64)
-    ap.add_argument("--population", type=int, default=256)
+    ap.add_argument("--steps", type=int, default=20, help="timed sync intervals")
+    ap.add_argument("--warmup", type=int, default=5, help="untimed sync intervals")
+    ap.add_argument("--population", type=int, default=256, help="trials per GPU")
     ap.add_argument("--max-width", type=int, default=1024)
     ap.add_argument("--sync-every", type=int, default=32,
-                    help="population sync interval (steps); budgets are multiples of it")
+                    help="optimizer steps per sync interval (= one bench step)")
+    ap.add_argument("--budget-intervals", type=int, default=24,
+                    help="best-loss@budget: best validation loss of the trials finished within "
+                         "this many sync intervals from the start of the sweep")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--algo", default="asha", choices=["asha", "random", "tpe"])
-    args = ap.parse_args(argv)
+    return ap.parse_args(argv)
+
+
+# ---------------------------------------------------------------------------------- launcher
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(n: int, argv) -> int:
+    """Start ``n`` rank processes of this script and wait for them (this process never touches
+    the GPU: it only counts devices, which does not initialise HIP on this image)."""
+    import torch
+    n_dev = torch.cuda.device_count()
+    env = dict(os.environ)
+    env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE=str(n),
+               LOCAL_WORLD_SIZE=str(n))
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if 0 < n_dev < n:
+        # fewer GPUs than ranks: rehearse the multi-rank engine with ranks sharing the GPUs
+        env["MOPT_COMM_BACKEND"] = "gloo"
+        env["MOPT_BENCH_REHEARSAL"] = "1"
+    procs = []
+    for r in range(n):
+        e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=e))
+    code = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                rc = p.poll()
+                if rc is None:
+                    continue
+                pending.remove(p)
+                if rc != 0 and code == 0:
+                    code = rc
+                    for q in pending:        # one rank failed: the others would hang
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return code
+
+
+# ---------------------------------------------------------------------------------- one rank
+def run_rank(args) -> None:
+    import torch
 
     from metaopt_amd.io.experiment_builder import build_experiment
     from metaopt_amd.models.data import TeacherClassification
-    from metaopt_amd.models.mlp import MLP_PRIORS, MLPSweepTask
+    from metaopt_amd.models.mlp import MLPSweepTask
     from metaopt_amd.ops.population import PopulationMLP
     from metaopt_amd.parallel.comm import init_from_env, shutdown
     from metaopt_amd.storage.database import EphemeralDB
@@ -57,9 +127,13 @@ def main(argv=None):
 
     comm = init_from_env()
     on_gpu = comm.device.type == "cuda"
+    if not on_gpu:   # CPU ranks share the host's cores
+        torch.set_num_threads(max(1, (os.cpu_count() or 1) // comm.world_size))
     P = args.population if on_gpu else min(args.population, 8)
     max_width = args.max_width if on_gpu else min(args.max_width, 256)
-    priors = dict(MLP_PRIORS)
+    S = args.sync_every
+    priors = dict(BENCH_PRIORS)
+    priors["/steps"] = f"fidelity({S}, {16 * S}, 4)"
     if not on_gpu:  # CPU smoke configuration (the GPU path is the measured one)
         priors["/width"] = f"loguniform(64, {max_width}, discrete=True)"
     task = MLPSweepTask(priors=priors, max_width=max_width)
@@ -76,37 +150,47 @@ def main(argv=None):
                                  batch_size=128, seed=1234 + args.seed, device=comm.device)
     pop = PopulationMLP(P, max_width=max_width, eval_batch=1024, device=comm.device)
     sweep = PopulationSweep(pop, task, data, comm=comm, experiment=experiment,
-                            sync_every=args.sync_every, ckpt_capacity=4 * P)
+                            sync_every=S, ckpt_capacity=4 * P)
 
     def sync():
         if on_gpu:
             torch.cuda.synchronize()
 
+    def interval():
+        for _ in range(S):
+            sweep.step()         # the last step of the interval runs the sync
+
     sweep.start()
     for _ in range(args.warmup):
-        sweep.step()
+        interval()
+    sweep.flush()
     sync()
     comm.barrier()
     sync()
-    s0, c0 = sweep.samples, sweep.completed
+    s0, c0, n0 = sweep.samples, sweep.completed, sweep.n_syncs
     sweep.timers.clear()
     sweep.n_syncs = 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        sweep.step()
+        interval()
     sweep.flush()            # deferred storage writes belong to the timed work
     sync()
     comm.barrier()
     sync()
     elapsed = comm.max_float(time.perf_counter() - t0)
-    local_samples = torch.tensor([float(sweep.samples - s0)], dtype=torch.float64,
-                                 device=comm._coll_device())
-    comm.all_reduce_(local_samples)
-    samples = float(local_samples.item())
-    completed = sweep.completed - c0
+    local = torch.tensor([float(sweep.samples - s0)], dtype=torch.float64,
+                         device=comm._coll_device())
+    comm.all_reduce_(local)
+    samples = float(local.item())
+    n_syncs = sweep.n_syncs
+    completed = sweep.completed - c0     # rank 0 records every trial of every rank
     trials_per_sec = samples / SAMPLES_PER_TRIAL / elapsed
     if comm.is_root:
         summ = sweep.summary()
+        budget_steps = args.budget_intervals * S
+        at_budget = sweep.best_within(budget_steps)
+        reached = sweep.global_step >= budget_steps
+        rehearsal = os.environ.get("MOPT_BENCH_REHEARSAL") == "1"
         out = {
             "metric": METRIC,
             "value": round(trials_per_sec, 3),
@@ -128,21 +212,41 @@ def main(argv=None):
                 "global_batch": 128 * P * comm.world_size,
                 "seq_len": None,
                 "parallelism": f"dp{comm.world_size} (trial-parallel populations)",
-                "trial_budget": "ASHA fidelity(32, 2048, 4) steps; throughput counted in "
-                                "epoch-equivalents",
-                "sync_every": args.sync_every,
+                "search_space": priors,
+                "step": f"one sync interval = {S} optimizer steps of every trial + the sync "
+                        "(validation, C1 all-gather, decide, C5 broadcast, member init/resume)",
                 "backend": pop.backend,
+                "comm_backend": comm.backend or "none",
+                "rehearsal_ranks_share_gpus": rehearsal,
             },
-            "asha_trials_completed": completed,
-            "asha_trials_completed_per_sec": round(completed / elapsed, 2),
+            "timed_syncs": n_syncs,
+            "trials_completed": completed,
+            "trials_completed_per_sec": round(completed / elapsed, 2),
+            "trials_completed_before_timing": c0,
             "best_val_loss": None if not math.isfinite(summ["best_val_loss"])
             else round(summ["best_val_loss"], 5),
             "best_params": summ["best_params"],
+            "best_val_loss_at_budget": (round(at_budget[0], 5)
+                                        if reached and math.isfinite(at_budget[0]) else None),
+            "budget": {"sync_intervals": args.budget_intervals,
+                       "optimizer_steps_per_slot": budget_steps,
+                       "samples_per_gpu": budget_steps * 128 * P,
+                       "trials_finished_within": at_budget[1],
+                       "reached": reached},
             "samples_per_sec": round(samples / elapsed, 1),
             "host_ms_per_sync": summ["host_ms_per_sync"],
+            "warmup_syncs": n0,
         }
         print(json.dumps(out), flush=True)
     shutdown()
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse_args(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch(args.gpus, argv))
+    run_rank(args)
 
 
 if __name__ == "__main__":

@@ -120,6 +120,14 @@ class Comm:
         dist.broadcast_object_list(box, src=src, group=self.group)
         return box[0]
 
+    def all_gather_object(self, obj) -> list:
+        """Every rank's ``obj`` (rank order) on every rank (small control-plane payloads)."""
+        if not self.distributed:
+            return [obj]
+        out: List = [None] * self.world_size
+        dist.all_gather_object(out, obj, group=self.group)
+        return out
+
     def max_float(self, value: float) -> float:
         """max over ranks of a host float (used for timing: the slowest rank sets the step)."""
         if not self.distributed:

@@ -92,7 +92,9 @@ class PopulationSweep:
         self.completed = 0
         self.broken = 0
         self.best = (math.inf, None)
-        self.history: List[tuple] = []                # (time, key, val_loss, budget)
+        # (time, key, val_loss, budget, global step at which the trial finished)
+        self.history: List[tuple] = []
+        self._result_step = 0
         self._last_hb = time.time()
         self.max_trials = (max_trials if max_trials is not None else
                            (experiment.max_trials if experiment is not None else math.inf))
@@ -221,10 +223,11 @@ class PopulationSweep:
             handle = pop.evaluate_async(vx, vy, slots=finished)
         snap = pop.stats_snapshot_async() if active.any() and self.global_step > 0 else None
         if self.pipelined:
-            prev, self._pending = self._pending, (snap, handle, self.slot_key.copy(), finished)
+            prev, self._pending = self._pending, (snap, handle, self.slot_key.copy(), finished,
+                                                  self.global_step)
             self._bad_now = np.zeros(P, dtype=bool)
             if prev is not None and prev[0] is not None:
-                psnap, phandle, pkeys, pfinished = prev
+                psnap, phandle, pkeys, pfinished, self._result_step = prev
                 tl, vl, va = pop.raw_results(psnap.get(), phandle)
                 # members still training that already diverged one interval ago
                 live = active & (pkeys == self.slot_key)
@@ -235,6 +238,7 @@ class PopulationSweep:
             self._drain_writes()
         else:
             self._drain_writes()
+            self._result_step = self.global_step
             if snap is not None:
                 tl, vl, va = pop.raw_results(snap.get(), handle)
                 st[:, 3] = active & ~np.isfinite(tl)
@@ -382,7 +386,7 @@ class PopulationSweep:
             if self.trial_events:
                 self.events.emit("trial", id=doc[0], status="completed", objective=vl,
                                  budget=budget)
-            self.history.append((time.time(), rkey, vl, budget))
+            self.history.append((time.time(), rkey, vl, budget, self._result_step))
             if vl < self.best[0]:
                 self.best = (vl, dict(params))
             done_pts.append(tuple(params[k] for k in self._dim_names))
@@ -691,6 +695,12 @@ class PopulationSweep:
         return self._mb
 
     # ------------------------------------------------------------------ reporting
+    def best_within(self, steps: int):
+        """(best validation loss, #trials) over the trials that finished within the first
+        ``steps`` population steps of the sweep (rank 0) -- best-loss@budget."""
+        vals = [h[2] for h in self.history if h[4] <= steps and math.isfinite(h[2])]
+        return (min(vals) if vals else math.inf), len(vals)
+
     def summary(self) -> dict:
         self.flush()
         return {"global_step": self.global_step, "samples": self.samples,
