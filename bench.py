@@ -128,7 +128,8 @@ def run_rank(args) -> None:
     comm = init_from_env()
     on_gpu = comm.device.type == "cuda"
     if not on_gpu:   # CPU ranks share the host's cores
-        torch.set_num_threads(max(1, (os.cpu_count() or 1) // comm.world_size))
+        torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", 0))
+                              or max(1, (os.cpu_count() or 1) // comm.world_size))
     P = args.population if on_gpu else min(args.population, 8)
     max_width = args.max_width if on_gpu else min(args.max_width, 256)
     S = args.sync_every

@@ -97,6 +97,17 @@ class ASHA(BaseAlgorithm):
         st["repetition"] = self._repetition
         return copy.deepcopy(st)
 
+    def clear_pending(self) -> None:
+        """Drop the entries suggested but never reported (objective None) -- after a restore
+        the stored trials without a result (waiting or broken) are observed again as
+        pending, so only points whose trial never reached the storage disappear."""
+        for bracket in self.brackets:
+            for _, rung in bracket.rungs:
+                for k in [k for k, (o, _) in rung.items() if o is None]:
+                    del rung[k]
+            bracket.rebuild_index()
+        # ``trial_info`` keeps every id's bracket: a point observed again lands where it was
+
     def suggest(self, num=1):
         """Promotions first (one at a time, each registered as pending), then all remaining new
         points drawn in ONE vectorised ``space.sample`` call and spread over the brackets."""

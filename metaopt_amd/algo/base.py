@@ -73,6 +73,12 @@ class BaseAlgorithm:
     def set_state(self, state_dict: dict) -> None:
         pass
 
+    def full_state(self) -> dict:
+        """Everything ``set_state`` needs to continue the search itself (observations, rungs,
+        lineage) -- persisted with an experiment; ``state_dict`` may be the RNG alone (the
+        producer syncs only the RNG between its naive and real algorithm copies)."""
+        return self.state_dict
+
     def suggest(self, num=1) -> Optional[List[tuple]]:
         """Up to ``num`` new points, or None to opt out (e.g. waiting for running trials)."""
         raise NotImplementedError

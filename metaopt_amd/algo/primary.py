@@ -38,6 +38,9 @@ class PrimaryAlgo(BaseAlgorithm):
     def set_state(self, state_dict):
         self.algorithm.set_state(state_dict)
 
+    def full_state(self):
+        return self.algorithm.full_state()
+
     def suggest(self, num=1):
         points = self.algorithm.suggest(num)
         if points is None:

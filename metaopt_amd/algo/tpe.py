@@ -106,6 +106,15 @@ class TPE(BaseAlgorithm):
     def set_state(self, state_dict):
         self.seed_rng(0)
         self.rng.set_state(state_dict["rng_state"])
+        if "points" in state_dict:
+            self._points = [tuple(p) for p in state_dict["points"]]
+            self._objectives = [float(o) for o in state_dict["objectives"]]
+            self._seen = {repr(p) for p in self._points}
+
+    def full_state(self):
+        """RNG + every observation (the model TPE fits is a function of them)."""
+        return {"rng_state": self.rng.get_state(), "points": [list(p) for p in self._points],
+                "objectives": list(self._objectives)}
 
     def observe(self, points, results):
         for p, r in zip(points, results):

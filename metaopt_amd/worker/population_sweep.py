@@ -30,6 +30,8 @@ import datetime
 import hashlib
 import logging
 import math
+import os
+import threading
 import time
 from typing import Dict, List, Optional
 
@@ -44,7 +46,8 @@ from ..utils.events import NullEventLog
 
 log = logging.getLogger(__name__)
 
-NONE, NEW, RESUME, CLEAR = 0, 1, 2, 3
+NONE, NEW, RESUME, CLEAR, RESUME_FILE = 0, 1, 2, 3, 4
+SIDECAR_FILE = "device_state.pt"     # per-trial device-state sidecar inside the trial's working_dir
 # status row: key, steps, budget, nan flag | result key, train loss, val loss, val acc, broken
 ST_COLS = 9
 AS_COLS = 11    # action, key, width, lr, momentum, wd, dropout, seed, budget, resume_key, src_rank
@@ -55,7 +58,8 @@ class PopulationSweep:
                  experiment=None, sync_every: int = 16, ckpt_capacity: int = 512,
                  heartbeat_every: float = 30.0, max_trials: Optional[float] = None,
                  pipelined: Optional[bool] = None, events=None, trial_events: bool = False,
-                 watchdog=None, restore_algorithm: bool = False):
+                 watchdog=None, restore_algorithm: bool = False, resume: bool = False,
+                 ckpt_dir: Optional[str] = None):
         self.pop = pop
         self.task = task
         self.data = data
@@ -111,6 +115,7 @@ class PopulationSweep:
         self._bad_now = np.zeros(P, dtype=bool)
         self._busy_marker = None
         self._ctl_stream = None
+        self._started = False
         # observability / failure detection (utils/events.py, parallel/watchdog.py)
         self.events = events if events is not None else NullEventLog()
         self.trial_events = bool(trial_events) and events is not None
@@ -146,11 +151,27 @@ class PopulationSweep:
             self._tracks_lineage = hasattr(inner, "parent_of")
             if watchdog is not None:
                 watchdog.on_stall.append(self._interrupt_in_flight)
+        # resume bookkeeping (rank 0): stored trials waiting for a slot, device-state sidecars
+        self._requeue: "collections.deque" = collections.deque()  # (id, point, status, sidecar#)
+        self._sidecar_index: Dict[str, tuple] = {}   # param key -> (sidecar number, steps)
+        self._sidecar_paths: List[str] = []
+        self._ckpt_tid: Dict[tuple, str] = {}        # (rank, trial key) -> trial id
+        self._prior_done = 0                         # completed + broken before this run
+        self._filling = True
+        self.ckpt_dir = ckpt_dir
+        restored_step = 0
+        if self.comm.is_root:
             if restore_algorithm:
                 state = experiment.storage.get_algorithm_state(experiment)
                 if state is not None:
-                    self.algorithm.set_state(state)
+                    restored_step = self._restore_state(state)
                     log.info("algorithm state restored from storage")
+            if resume:
+                self._resume_from_storage()
+        # every rank learns which sidecar files it may be told to load, and the restored step
+        # counter (the data stream continues where the stopped run left it)
+        self._sidecar_paths, self.global_step = self.comm.broadcast_object(
+            (self._sidecar_paths, restored_step) if self.comm.is_root else None)
         if watchdog is not None:
             watchdog.events = watchdog.events or events
             watchdog.start()
@@ -167,6 +188,7 @@ class PopulationSweep:
     # ------------------------------------------------------------------ main loop
     def start(self) -> None:
         """Fill every slot of every rank (first sync with nothing running)."""
+        self._started = True
         self._sync(evaluate=False)
 
     def step(self) -> None:
@@ -184,7 +206,7 @@ class PopulationSweep:
             self._sync()
 
     def run(self, max_steps: int) -> dict:
-        if self.global_step == 0 and (self.slot_key < 0).all():
+        if not self._started:
             self.start()
         for _ in range(max_steps):
             if self.done:
@@ -328,10 +350,17 @@ class PopulationSweep:
         return torch.cuda.stream(self._ctl_stream)
 
     def drain(self) -> None:
-        """Pipelined mode: run one more sync round without training so the results of the
-        members that finished at the last sync reach the algorithm and the storage."""
-        if self.pipelined and self._pending is not None and self._pending[3]:
-            self._sync()
+        """Collective, pipelined mode: sync rounds without training so the results of the
+        members that finished at the last sync (and of any that reached their budget since)
+        reach the algorithm and the storage.  Every rank runs the same rounds: the decision
+        must not depend on one rank's local state, or the collectives would not match."""
+        if self.pipelined and self._pending is not None:
+            filling, self._filling = self._filling, False
+            try:
+                self._sync()
+                self._sync()
+            finally:
+                self._filling = filling
 
     # ------------------------------------------------------------------ rank 0
     def _decide(self, gathered: np.ndarray) -> np.ndarray:
@@ -380,7 +409,7 @@ class PopulationSweep:
                                      budget=None)
                 continue
             vl, va, tl = g[6], g[7], g[5]
-            self._writer.put_update_spec(doc[0], (vl, va, tl, now, doc[1]))
+            self._writer.put_update_spec(doc[0], (vl, va, tl, now, doc[1]), was="reserved")
             self.completed += 1
             budget = int(self.task.budget(params))
             if self.trial_events:
@@ -392,7 +421,7 @@ class PopulationSweep:
             done_pts.append(tuple(params[k] for k in self._dim_names))
             done_res.append({"objective": vl, "constraint": [], "gradient": None})
             if budget < max_b:
-                self._index_ckpt(pkey, rank, rkey, budget)
+                self._index_ckpt(pkey, rank, rkey, budget, doc[0])
         t0 = time.perf_counter()
         if done_pts:
             if isinstance(self.algorithm, PrimaryAlgo):
@@ -420,14 +449,17 @@ class PopulationSweep:
         while len(fifo) > self.ckpt_capacity:
             old = fifo.popleft()
             self._ckpt_alive.discard((rank, old))
+            self._ckpt_tid.pop((rank, old), None)
             pk = self._ckpt_pkey.pop((rank, old), None)
             if pk is not None and self.ckpt_index.get(pk, (None, None))[:2] == (rank, old):
                 del self.ckpt_index[pk]
 
-    def _index_ckpt(self, pkey, rank, key, steps):
+    def _index_ckpt(self, pkey, rank, key, steps, tid=None):
         """Make a saved checkpoint findable by its parameters once its result is known."""
         if (rank, key) not in self._ckpt_alive:
             return                   # evicted before its result arrived
+        if tid is not None:
+            self._ckpt_tid[(rank, key)] = tid
         prev = self.ckpt_index.get(pkey)
         if prev is not None:
             self._ckpt_pkey.pop((prev[0], prev[1]), None)
@@ -436,67 +468,98 @@ class PopulationSweep:
 
     def _fill(self, free_rows: List[int], assign: np.ndarray) -> None:
         W, P = self.comm.world_size, self.pop.capacity
-        if self.done or not free_rows:
+        if self.done or not free_rows or not self._filling:
             return
-        n_done = self.completed + self.broken
+        n_done = self.completed + self.broken + self._prior_done
         in_flight = len(self.trials)
         budget_left = self.max_trials - n_done - in_flight
         n = int(min(len(free_rows), budget_left)) if math.isfinite(budget_left) else len(free_rows)
-        if self.algorithm.is_done or n <= 0:
-            if in_flight == 0:
+        if n <= 0:
+            if not self.trials:
                 self.done = True
-            return
-        points = self.algorithm.suggest(n) or []
-        if not points and in_flight == 0:
-            self.done = True
             return
         free_by_rank = [collections.deque(row for row in free_rows if row // P == r)
                         for r in range(W)]
         n_free = [len(q) for q in free_by_rank]
         stamp = datetime.datetime.utcnow()
-        parent_of = getattr(self.algorithm, "parent_of", None) if self._tracks_lineage else None
-        keys = self._dim_names
+        # 1) stored trials waiting for a worker (interrupted, lost, new: a resumed experiment)
+        #    take free slots before the algorithm is asked for anything new
+        while self._requeue and n > 0 and any(n_free):
+            tid, point, was, sidecar = self._requeue.popleft()
+            self._place(point, tid, assign, free_by_rank, n_free, stamp, was=was, sidecar=sidecar)
+            n -= 1
+        if n <= 0:
+            return
+        if self.algorithm.is_done:
+            if not self.trials:
+                self.done = True
+            return
+        points = self.algorithm.suggest(n) or []
+        if not points and not self.trials:
+            self.done = True
+            return
         for point in points:
-            params = dict(zip(keys, point))
-            pkey = self._point_key(point, params)
-            # lineage-tracking algorithms (PBT exploit, Hyperband/ASHA promotion) name the point
-            # whose device state the new trial continues; otherwise the same hyper-parameters at
-            # a lower fidelity are looked up (ASHA promotion)
-            parent = parent_of(point) if parent_of is not None else None
-            ckey = self._point_key(parent) if parent is not None else pkey
-            owner = self.ckpt_index.get(ckey)
-            src = -1
-            if owner is not None and n_free[owner[0]]:
-                # resume next to the checkpoint (no copy between GPUs)
-                rank = owner[0]
-                action, resume, src = RESUME, owner[1], owner[0]
-            else:
-                rank = max(range(W), key=n_free.__getitem__)
-                if not n_free[rank]:
-                    break
-                if owner is not None:   # C4: the owner sends the checkpoint to that rank (P2P)
-                    action, resume, src = RESUME, owner[1], owner[0]
-                else:
-                    action, resume = NEW, -1
-            row = free_by_rank[rank].popleft()
-            n_free[rank] -= 1
+            if not any(n_free):
+                break
             tid = self._doc_id(point)
             if tid in self._registered:
                 log.debug("duplicate point %s skipped", point)
-                free_by_rank[rank].appendleft(row)
-                n_free[rank] += 1
                 continue
             self._registered.add(tid)
+            self._place(point, tid, assign, free_by_rank, n_free, stamp)
+
+    def _place(self, point, tid, assign, free_by_rank, n_free, stamp, was=None, sidecar=None):
+        """Reserve trial ``tid`` (``point``) and assign it to a free slot.
+
+        The slot is chosen next to the device state the trial continues from: its own sidecar
+        (an interrupted trial of a stopped run), the HBM checkpoint of its parent (lineage-
+        tracking algorithms: PBT exploit, promotions) or of the same configuration at a lower
+        fidelity (ASHA promotion) -- on the owner rank if it has room, else copied there (C4)
+        -- or the sidecar file of such a checkpoint written by a stopped run.  New trials go to
+        the least-loaded rank."""
+        W = len(n_free)
+        keys = self._dim_names
+        params = dict(zip(keys, point))
+        pkey = self._point_key(point, params)
+        parent = None
+        if self._tracks_lineage:
+            parent_of = getattr(self.algorithm, "parent_of", None)
+            parent = parent_of(point) if parent_of is not None else None
+        ckey = self._point_key(parent) if parent is not None else pkey
+        owner = self.ckpt_index.get(ckey)
+        src, resume = -1, -1
+        if sidecar is not None:
+            rank = max(range(W), key=n_free.__getitem__)
+            action, resume = RESUME_FILE, sidecar
+        elif owner is not None and n_free[owner[0]]:
+            # resume next to the checkpoint (no copy between GPUs)
+            rank = owner[0]
+            action, resume, src = RESUME, owner[1], owner[0]
+        else:
+            rank = max(range(W), key=n_free.__getitem__)
+            side = self._sidecar_index.get(ckey)
+            if owner is not None:   # C4: the owner sends the checkpoint to that rank (P2P)
+                action, resume, src = RESUME, owner[1], owner[0]
+            elif side is not None:
+                action, resume = RESUME_FILE, side[0]
+            else:
+                action = NEW
+        row = free_by_rank[rank].popleft()
+        n_free[rank] -= 1
+        if was is None:
             self._writer.put_register_spec(
                 (tid, stamp, point, self._doc_id(parent) if parent is not None else None))
-            key = self.next_key
-            self.next_key += 1
-            self.trials[key] = [tid, stamp]      # [trial id, last heartbeat]
-            self.key_params[key] = params
-            self.key_pkey[key] = pkey
-            cfg = self.task.member_config(params, self.task.seed_of(pkey))
-            assign[row] = (action, key, cfg.width, cfg.lr, cfg.momentum, cfg.weight_decay,
-                           cfg.dropout, cfg.seed, self.task.budget(params), resume, src)
+        else:
+            self._writer.put_update(tid, {"status": "reserved", "start_time": stamp,
+                                          "heartbeat": stamp}, was=was)
+        key = self.next_key
+        self.next_key += 1
+        self.trials[key] = [tid, stamp]      # [trial id, last heartbeat]
+        self.key_params[key] = params
+        self.key_pkey[key] = pkey
+        cfg = self.task.member_config(params, self.task.seed_of(pkey))
+        assign[row] = (action, key, cfg.width, cfg.lr, cfg.momentum, cfg.weight_decay,
+                       cfg.dropout, cfg.seed, self.task.budget(params), resume, src)
 
     def _build_doc(self, spec) -> dict:
         """Trial document (core/trial.py schema) of a registration queued by ``_fill``."""
@@ -553,41 +616,219 @@ class PopulationSweep:
     def _interrupt_in_flight(self, stalled_s: float = 0.0, phase: str = "") -> int:
         """Watchdog callback (rank 0): persist held writes, then mark every in-flight trial
         ``interrupted`` so another worker or a re-run reserves it again -- the state a lost
-        heartbeat leads to in the reference (src/orion/core/worker/experiment.py:217-232)."""
+        heartbeat leads to in the reference (src/orion/core/worker/experiment.py:217-232).
+        Results that arrive later are written with compare-and-swap on ``reserved`` and so
+        never overwrite a trial that was released here."""
         if self._writer is None:
             return 0
-        now = datetime.datetime.utcnow()
-        for doc in list(self.trials.values()):
-            self._writer.put_update(doc[0], {"status": "interrupted", "heartbeat": now},
-                                    was="reserved")
-        n = len(self.trials)
+        n = self._release_in_flight()
         self._writer.flush()
         self.events.emit("interrupted", n_trials=n)
         self.events.flush()
         return n
 
+    def _release_in_flight(self, fields: Optional[Dict[str, dict]] = None) -> int:
+        """Queue ``reserved -> interrupted`` for every in-flight trial (rank 0)."""
+        now = datetime.datetime.utcnow()
+        for doc in list(self.trials.values()):
+            upd = {"status": "interrupted", "heartbeat": now}
+            if fields and doc[0] in fields:
+                upd.update(fields[doc[0]])
+            self._writer.put_update(doc[0], upd, was="reserved")
+        return len(self.trials)
+
+    # ------------------------------------------------------------------ resume / persistence
+    def _restore_state(self, state: dict) -> int:
+        """Restore the algorithm (and the sweep's step counter) saved by :meth:`close`.
+        Pending entries (points suggested but not reported) are dropped: the trials still
+        waiting are re-registered as pending by :meth:`_resume_from_storage`."""
+        if "algorithm" in state and "sweep" in state:
+            algo_state, sweep_state = state["algorithm"], state["sweep"]
+        else:                       # an older record: the algorithm's state alone
+            algo_state, sweep_state = state, {}
+        self.algorithm.set_state(algo_state)
+        inner = getattr(self.algorithm, "algorithm", self.algorithm)
+        clear = getattr(inner, "clear_pending", None)
+        if clear is not None:
+            clear()
+        return int(sweep_state.get("global_step", 0))
+
+    def _resume_from_storage(self) -> None:
+        """Rank 0: continue the experiment stored so far (reference: the producer replays every
+        completed trial through ``observe``, src/orion/core/worker/producer.py:103-132, and
+        workers re-reserve interrupted/lost trials, src/orion/storage/legacy.py:253-273).
+
+        * completed trials are observed by the algorithm in completion order and counted
+          against ``max_trials``; broken ones are counted;
+        * trials waiting for a worker -- ``new``, ``suspended``, ``interrupted``, and
+          ``reserved`` ones whose heartbeat expired (lost) -- are queued to take free slots
+          before anything new is suggested, and are observed as pending (no objective);
+        * device-state sidecars named by a trial's ``working_dir`` are indexed: a completed
+          trial's sidecar seeds its promotion, an interrupted trial's resumes the trial itself
+          at the step it had reached."""
+        exp = self.experiment
+        storage = exp.storage
+        trials = storage.fetch_trials(exp)
+        lost = {t.id for t in storage.fetch_lost_trials(exp)}
+        names = self._dim_names
+        max_b = self._max_budget()
+        done_pts, done_res, pend = [], [], []
+        order = sorted(trials, key=lambda t: (t.end_time or datetime.datetime.max,
+                                              t.submit_time or datetime.datetime.min))
+        for t in order:
+            self._registered.add(t.id)
+            pdict = t.params_dict
+            if any(n not in pdict for n in names):
+                continue                      # a point of another space (EVC parent)
+            point = tuple(pdict[n] for n in names)
+            side = self._sidecar_path(t.working_dir)
+            if t.status == "completed":
+                obj = t.objective.value if t.objective is not None else None
+                done_pts.append(point)
+                done_res.append({"objective": obj, "constraint": [], "gradient": None})
+                self._prior_done += 1
+                if obj is not None and obj < self.best[0]:
+                    self.best = (obj, dict(pdict))
+                budget = int(self.task.budget(pdict)) if self.task.fidelity in pdict else max_b
+                if side is not None and budget < max_b:
+                    pkey = self._point_key(point, pdict)
+                    prev = self._sidecar_index.get(pkey)
+                    if prev is None or prev[1] < budget:
+                        self._sidecar_index[pkey] = (self._add_sidecar(side), budget)
+            elif t.status == "broken":
+                self._prior_done += 1
+                pend.append(point)            # never reported: pending, as before the stop
+            elif t.status in ("new", "suspended", "interrupted") or t.id in lost:
+                num = self._add_sidecar(side) if side is not None else None
+                pend.append(point)
+                self._requeue.append((t.id, point, t.status, num))
+            # reserved with a live heartbeat: another worker owns it
+        if done_pts:
+            self.algorithm.observe(done_pts, done_res)
+        if pend:
+            self.algorithm.observe(pend, [{"objective": None, "constraint": [], "gradient": None}
+                                          for _ in pend])
+        log.info("resumed experiment %s: %d finished trials replayed, %d trials requeued, "
+                 "%d sidecars", exp.name, self._prior_done, len(self._requeue),
+                 len(self._sidecar_paths))
+        self.events.emit("resume", replayed=self._prior_done, requeued=len(self._requeue),
+                         sidecars=len(self._sidecar_paths))
+
+    @staticmethod
+    def _sidecar_path(working_dir) -> Optional[str]:
+        if not working_dir:
+            return None
+        path = os.path.join(working_dir, SIDECAR_FILE)
+        return path if os.path.exists(path) else None
+
+    def _add_sidecar(self, path: str) -> int:
+        self._sidecar_paths.append(path)
+        return len(self._sidecar_paths) - 1
+
+    def _load_sidecar(self, num: int, width: int) -> Optional[dict]:
+        """The device state stored in sidecar ``num`` (tensors on this rank's device), or None
+        when the file is gone or belongs to another architecture."""
+        try:
+            st = torch.load(self._sidecar_paths[num], map_location=self.pop.device,
+                            weights_only=True)
+        except (OSError, IndexError, RuntimeError) as exc:
+            log.warning("sidecar %d unreadable: %s", num, exc)
+            return None
+        if int(st["config"]["width"]) != int(width) or st.get("optimizer") != self.pop.optimizer:
+            log.warning("sidecar %d does not match the member (width %s)", num, width)
+            return None
+        st["t"] = int(st["t"])
+        return st
+
+    def _write_sidecar(self, tid: str, state: dict, exp_name: str) -> str:
+        """Write a member's device state (f32 master weights, optimizer state, step count,
+        configuration) to ``<ckpt_dir>/<experiment>_<trial id>/device_state.pt``; returns the
+        directory (recorded as the trial's ``working_dir``)."""
+        d = os.path.join(self.ckpt_dir, f"{exp_name}_{tid}")
+        os.makedirs(d, exist_ok=True)
+        out = {k: (v.detach().to("cpu") if isinstance(v, torch.Tensor) else v)
+               for k, v in state.items()}
+        out["t"] = int(out["t"])
+        tmp = os.path.join(d, SIDECAR_FILE + ".tmp")
+        torch.save(out, tmp)
+        os.replace(tmp, os.path.join(d, SIDECAR_FILE))
+        return d
+
+    def spill(self) -> int:
+        """Collective: write the device state the experiment still needs to sidecar files --
+        the HBM checkpoints ASHA/PBT may resume (indexed completed trials) and every member
+        still training -- and record each file's directory as the trial's ``working_dir``.
+        Rank 0 marks the in-flight trials ``interrupted`` (a re-run resumes them from their
+        sidecar at the step they reached).  Returns the number of files this rank wrote."""
+        plan = None
+        if self.comm.is_root:
+            ck = [(r, k, self._ckpt_tid[(r, k)]) for r, k, _ in self.ckpt_index.values()
+                  if (r, k) in self._ckpt_tid]
+            fl = [(k, doc[0]) for k, doc in self.trials.items()]
+            plan = (ck, fl, self.experiment.name)
+        ck, fl, name = self.comm.broadcast_object(plan)
+        me, written = self.comm.rank, []
+        if self.ckpt_dir is not None:
+            for r, k, tid in ck:
+                meta = self.ckpts.get(k) if r == me else None
+                if meta is not None:
+                    written.append((tid, self._write_sidecar(tid, self.pop.pool_state(meta),
+                                                             name)))
+            slots = {int(k): s for s, k in enumerate(self.slot_key.tolist()) if k >= 0}
+            for k, tid in fl:
+                s = slots.get(int(k))
+                if s is not None:
+                    written.append((tid, self._write_sidecar(tid, self.pop.slot_state(s), name)))
+        everyone = self.comm.all_gather_object(written)
+        if self.comm.is_root:
+            dirs = {tid: d for part in everyone for tid, d in part}
+            in_flight = {doc[0] for doc in self.trials.values()}
+            for tid, d in dirs.items():
+                if tid not in in_flight:
+                    self._writer.put_update(tid, {"working_dir": d})
+            self._release_in_flight({tid: {"working_dir": d} for tid, d in dirs.items()
+                                     if tid in in_flight})
+            self.trials.clear()
+        return len(written)
+
     def save_algorithm_state(self) -> None:
-        """Rank 0: store the algorithm's ``state_dict`` with the experiment (resume without
-        replaying every trial through ``observe``)."""
+        """Rank 0: store the algorithm's full state (ASHA rungs, TPE observations, PBT
+        lineage, RNG) and the sweep's step counter with the experiment."""
         if self.comm.is_root and self.experiment is not None:
-            self.experiment.storage.save_algorithm_state(self.experiment,
-                                                         state=self.algorithm.state_dict)
+            algo = self.algorithm
+            full = algo.full_state() if hasattr(algo, "full_state") else algo.state_dict
+            self.experiment.storage.save_algorithm_state(
+                self.experiment, state={"algorithm": full,
+                                        "sweep": {"global_step": int(self.global_step)}})
 
     def close(self) -> None:
+        """Collective end of the sweep: the results of the last sync reach the algorithm and
+        the storage (pipelined mode), device state is spilled to sidecars (``ckpt_dir``), the
+        trials still in flight are released (``interrupted``: a re-run or another worker
+        picks them up), and the algorithm state is saved."""
         if self.watchdog is not None:
             self.watchdog.stop()
+        self._filling = False         # the final sync only collects results
         try:
-            self.save_algorithm_state()
-        except Exception as exc:  # pragma: no cover - storage without the collection API
-            log.warning("algorithm state not saved: %s", exc)
-        self.events.emit("sweep_end", **{k: v for k, v in self.summary().items()
-                                         if k != "host_ms_per_sync"})
-        self.events.flush()
-        if self._gc_callback in gc.callbacks:
-            gc.callbacks.remove(self._gc_callback)
-        if self._writer is not None:
-            self._writer.close()
-            self._writer = None
+            self.drain()
+            self.spill()
+        finally:
+            if self.comm.is_root and self._writer is not None:
+                self._release_in_flight()
+                self.trials.clear()
+                self._writer.flush()
+            try:
+                self.save_algorithm_state()
+            except Exception as exc:  # pragma: no cover - storage without the collection API
+                log.warning("algorithm state not saved: %s", exc)
+            self.events.emit("sweep_end", **{k: v for k, v in self.summary().items()
+                                             if k != "host_ms_per_sync"})
+            self.events.flush()
+            if self._gc_callback in gc.callbacks:
+                gc.callbacks.remove(self._gc_callback)
+            if self._writer is not None:
+                self._writer.close()
+                self._writer = None
 
     # ------------------------------------------------------------------ every rank
     def _apply(self, gathered: np.ndarray, assign: np.ndarray) -> None:
@@ -630,21 +871,25 @@ class PopulationSweep:
         for s in range(P):
             a = mine[s]
             act = int(a[0])
-            if act not in (NEW, RESUME):
+            if act not in (NEW, RESUME, RESUME_FILE):
                 continue
             cfg = MemberConfig(width=int(a[2]), lr=float(a[3]), momentum=float(a[4]),
                                weight_decay=float(a[5]), dropout=float(a[6]), seed=int(a[7]),
                                **getattr(self.task, "member_defaults", {}))
             # checkpoints are not consumed: a PBT winner can seed several members
             meta = self.ckpts.get(int(a[9])) if act == RESUME and s not in received else None
-            if act == RESUME and s in received:
+            state = self._load_sidecar(int(a[9]), cfg.width) if act == RESUME_FILE else None
+            if state is not None:
+                pop.load_slot_state(s, state)
+                hp_updates.append((s, cfg))
+            elif act == RESUME and s in received:
                 pop.load_slot_state(s, received[s])
                 hp_updates.append((s, cfg))
             elif meta is not None:
                 loads.append((s, meta))
                 hp_updates.append((s, cfg))
             else:
-                if act == RESUME:  # evicted checkpoint: the trial retrains from scratch
+                if act in (RESUME, RESUME_FILE):  # evicted/lost: the trial retrains from scratch
                     self.n_resume_missing += 1
                     log.warning("checkpoint of trial %d missing; trial %d starts from scratch",
                                 int(a[9]), int(a[1]))
@@ -732,6 +977,8 @@ class _WriteBehind:
         self.errors = 0
         self._held: "collections.deque" = collections.deque()
         self.busy_s = 0.0             # seconds spent applying writes
+        # the watchdog thread may flush while the main thread drains: one unit at a time
+        self._lock = threading.Lock()
 
     def put_register(self, doc: dict):
         """Register a trial document (a shallow copy: the sweep replaces, never mutates, the
@@ -756,7 +1003,10 @@ class _WriteBehind:
     def drain_while(self, busy) -> None:
         t0 = time.perf_counter()
         while self._held and busy():
-            self._apply_batch(self._take())
+            with self._lock:
+                if not self._held:
+                    break
+                self._apply_batch(self._take())
         self.busy_s += time.perf_counter() - t0
 
     def _take(self):

@@ -163,23 +163,34 @@ def _canon(v):
 
 
 def test_sweep_persists_and_restores_algorithm_state(data):
-    """close() stores the algorithm's state_dict with the experiment; a re-run restores it
-    instead of replaying every trial through observe()."""
+    """close() stores the algorithm's FULL state (ASHA rungs, not only the RNG) and the sweep's
+    step counter; a re-run restores both."""
     exp, sweep = _sweep(data, "state-sweep", 12)
     sweep.run(1000)
     sweep.close()
     state = exp.storage.get_algorithm_state(exp)
     assert state is not None
-    assert _canon(state) == _canon(exp.algorithms.state_dict)
+    assert _canon(state["algorithm"]) == _canon(exp.algorithms.full_state())
+    assert state["sweep"]["global_step"] == sweep.global_step
+    rungs = state["algorithm"]["rungs"]
+    assert sum(len(r) for br in rungs for _, r in br) >= 12     # the search itself is persisted
     pop = PopulationMLP(4, max_width=128, eval_batch=128, device="cpu")
     fresh = build_experiment("state-sweep-2", priors=PRIORS,
                              algorithms={"asha": {"seed": 9, "repetitions": float("inf")}},
                              max_trials=12, storage=exp.storage)
     fresh.storage.save_algorithm_state(fresh, state=state)
-    assert _canon(fresh.algorithms.state_dict) != _canon(state)
+    assert _canon(fresh.algorithms.full_state()) != _canon(state["algorithm"])
     sweep2 = PopulationSweep(pop, MLPSweepTask(priors=PRIORS, max_width=128), data,
                              experiment=fresh, sync_every=16, restore_algorithm=True)
-    assert _canon(fresh.algorithms.state_dict) == _canon(state)
+    restored = fresh.algorithms.full_state()
+    # completed entries come back; pending ones (never reported) are dropped
+    want = _canon(state["algorithm"])
+    for br in want["rungs"]:
+        for rung in br:
+            rung[1] = {k: v for k, v in rung[1].items() if v[0] is not None}
+    got = _canon(restored)
+    assert got["rungs"] == want["rungs"] and got["rng_state"] == want["rng_state"]
+    assert sweep2.global_step == sweep.global_step
     sweep2.close()
 
 

@@ -1,0 +1,168 @@
+"""Resuming a device sweep from the database (SURVEY.md §5 "Checkpoint / resume"; reference:
+completed trials replayed through ``observe``, src/orion/core/worker/producer.py:103-132, and
+interrupted/lost trials re-reserved, src/orion/storage/legacy.py:206-273).
+
+* a 2-rank (gloo) ASHA sweep stopped mid-run and restarted from its storage, device-state
+  sidecars and saved algorithm state ends with the same completed trials (same ids, same
+  objectives) and the same ASHA rungs as the same sweep run without interruption;
+* a crashed sweep (no close: trials left ``reserved``) is resumed: its lost trials are
+  re-reserved and finished, none is left behind;
+* promotions of a stopped run resume from the sidecar of the lower-rung trial.
+"""
+import datetime
+import math
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from metaopt_amd.io.experiment_builder import build_experiment
+from metaopt_amd.models.data import TeacherClassification
+from metaopt_amd.models.mlp import MLPSweepTask
+from metaopt_amd.ops.population import PopulationMLP
+from metaopt_amd.storage.database import EphemeralDB, PickledDB
+from metaopt_amd.storage.protocol import DocumentStorage
+from metaopt_amd.worker.population_sweep import PopulationSweep
+
+PRIORS = {"/lr": "loguniform(1e-3, 0.3)", "/width": "loguniform(64, 128, discrete=True)",
+          "/dropout": "uniform(0, 0.5)", "/steps": "fidelity(16, 64, 2)"}
+ALGO = {"asha": {"seed": 5, "repetitions": float("inf")}}
+MAX_TRIALS = 64
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _data():
+    return TeacherClassification(n_train=512, n_val=128, batch_size=128, seed=11)
+
+
+def _make(storage, data, comm=None, **kw):
+    exp = None
+    if comm is None or comm.is_root:
+        exp = build_experiment("resume-sweep", priors=PRIORS, algorithms=ALGO,
+                               max_trials=MAX_TRIALS, storage=storage)
+    pop = PopulationMLP(4, max_width=128, eval_batch=128, device="cpu")
+    return exp, PopulationSweep(pop, MLPSweepTask(priors=PRIORS, max_width=128), data,
+                                comm=comm, experiment=exp, sync_every=16,
+                                ckpt_capacity=64, **kw)
+
+
+def _phase_worker(rank, world, port, db_path, ckpt_dir, max_steps, resume, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(2)
+    from metaopt_amd.parallel.comm import init_from_env, shutdown
+    comm = init_from_env(backend="gloo")
+    storage = DocumentStorage(PickledDB(host=db_path)) if comm.is_root else None
+    _, sweep = _make(storage, _data(), comm=comm, resume=resume, restore_algorithm=resume,
+                     ckpt_dir=ckpt_dir)
+    sweep.run(max_steps)
+    sweep.close()
+    q.put((rank, sweep.done, sweep.n_resumed, sweep.n_resume_missing))
+    shutdown()
+
+
+def _run_phase(db_path, ckpt_dir, max_steps, resume, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_phase_worker,
+                         args=(r, world, port, db_path, ckpt_dir, max_steps, resume, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return out
+
+
+def _outcome(db_path):
+    storage = DocumentStorage(PickledDB(host=db_path))
+    exp = build_experiment("resume-sweep", priors=PRIORS, algorithms=ALGO,
+                           max_trials=MAX_TRIALS, storage=storage)
+    trials = storage.fetch_trials(exp)
+    done = {t.id: t.objective.value for t in trials if t.status == "completed"}
+    stati = sorted(t.status for t in trials)
+    rungs = storage.get_algorithm_state(exp)["algorithm"]["rungs"]
+    completed_rungs = [[(b, sorted((k, round(v[0], 12)) for k, v in r.items()
+                                   if v[0] is not None)) for b, r in br] for br in rungs]
+    return done, stati, completed_rungs
+
+
+def test_two_rank_sweep_stopped_and_resumed_equals_uninterrupted(tmp_path):
+    ref_db = str(tmp_path / "ref.pkl")
+    res = _run_phase(ref_db, None, 100000, resume=False)
+    assert all(r[1] for r in res)                       # ran to completion
+    ref_done, ref_stati, ref_rungs = _outcome(ref_db)
+    assert len(ref_done) == MAX_TRIALS
+
+    db = str(tmp_path / "stopped.pkl")
+    ckpt = str(tmp_path / "sidecars")
+    _run_phase(db, ckpt, 4 * 16 + 3, resume=False)     # stopped mid-interval 5
+    mid_done, mid_stati, _ = _outcome(db)
+    assert 0 < len(mid_done) < MAX_TRIALS
+    assert "reserved" not in mid_stati and "interrupted" in mid_stati
+    res = _run_phase(db, ckpt, 100000, resume=True)
+    assert all(r[1] for r in res)
+    assert sum(r[2] for r in res) > 0 and sum(r[3] for r in res) == 0   # resumed from sidecars
+    done, stati, rungs = _outcome(db)
+    assert "reserved" not in stati
+    assert set(done) == set(ref_done)
+    for tid, obj in ref_done.items():
+        assert done[tid] == pytest.approx(obj, rel=1e-6, abs=1e-9), tid
+    assert rungs == ref_rungs
+
+
+def test_crashed_sweep_requeues_lost_trials():
+    data = _data()
+    storage = DocumentStorage(EphemeralDB())
+    exp, sweep = _make(storage, data, pipelined=False)
+    sweep.run(3 * 16)
+    sweep.flush()                     # a crash: no close(), in-flight trials stay reserved
+    lost = [t for t in storage.fetch_trials(exp) if t.status == "reserved"]
+    assert lost
+    # their heartbeats expire (the reference's lost-trial rule)
+    old = datetime.datetime.utcnow() - datetime.timedelta(hours=1)
+    for t in lost:
+        storage.update_trial_doc(t.id, {"heartbeat": old})
+    n_done_before = sum(t.status == "completed" for t in storage.fetch_trials(exp))
+    exp2, sweep2 = _make(storage, data, resume=True, pipelined=False)
+    assert sweep2._prior_done >= n_done_before and len(sweep2._requeue) == len(lost)
+    sweep2.run(100000)
+    sweep2.close()
+    trials = storage.fetch_trials(exp2)
+    assert not [t for t in trials if t.status in ("reserved", "new", "interrupted")]
+    finished = {t.id for t in trials if t.status in ("completed", "broken")}
+    assert {t.id for t in lost} <= finished
+    assert sum(t.status == "completed" for t in trials) >= MAX_TRIALS - sweep2.broken
+
+
+def test_promotion_resumes_from_sidecar(tmp_path):
+    data = _data()
+    storage = DocumentStorage(EphemeralDB())
+    ckpt = str(tmp_path / "sc")
+    exp, sweep = _make(storage, data, ckpt_dir=ckpt)
+    sweep.run(2 * 16)
+    sweep.close()
+    with_state = [t for t in storage.fetch_trials(exp) if t.working_dir]
+    assert with_state and all(os.path.exists(os.path.join(t.working_dir, "device_state.pt"))
+                              for t in with_state)
+    st = torch.load(os.path.join(with_state[0].working_dir, "device_state.pt"),
+                    weights_only=True)
+    assert {"config", "t", "p32", "m32"} <= set(st)
+    exp2, sweep2 = _make(storage, data, resume=True, restore_algorithm=True, ckpt_dir=ckpt)
+    assert sweep2._sidecar_paths
+    sweep2.run(100000)
+    sweep2.close()
+    assert sweep2.n_resumed > 0 and sweep2.n_resume_missing == 0
+    assert math.isfinite(sweep2.best[0])
