@@ -40,6 +40,12 @@ def add_subparser(parser):
                    help="JSONL event log path (rank r writes <path>.rank<r> when world > 1)")
     g.add_argument("--trial-events", action="store_true",
                    help="one event per finished trial in the event log")
+    g.add_argument("--resume", action="store_true",
+                   help="continue the stored experiment: replay its finished trials, re-reserve "
+                        "interrupted/lost ones, restore the saved algorithm state")
+    g.add_argument("--ckpt-dir", default=None,
+                   help="directory for per-trial device-state sidecars written at the end of "
+                        "the sweep (promotions and interrupted trials resume from them)")
     g.add_argument("--watchdog", type=float, default=0.0,
                    help="seconds without a sync before the rank fails the job cleanly "
                         "(in-flight trials -> interrupted); 0 disables")
@@ -84,11 +90,16 @@ def main(args):
                             sync_every=args["sync_every"],
                             ckpt_capacity=max(4, int(spec.ckpt_factor * P)),
                             events=events, trial_events=args.get("trial_events", False),
-                            watchdog=watchdog)
-    summary = sweep.run(args["steps"])
-    sweep.close()
-    if events is not None:
-        events.close()
+                            watchdog=watchdog, resume=args.get("resume", False),
+                            restore_algorithm=args.get("resume", False),
+                            ckpt_dir=args.get("ckpt_dir"))
+    try:
+        summary = sweep.run(args["steps"])
+    finally:
+        # releases in-flight trials and stops the watchdog even when a collective failed
+        sweep.close()
+        if events is not None:
+            events.close()
     if comm.is_root:
         print(json.dumps({k: v for k, v in summary.items()}, default=str))
     shutdown()

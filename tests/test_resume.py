@@ -166,3 +166,27 @@ def test_promotion_resumes_from_sidecar(tmp_path):
     sweep2.close()
     assert sweep2.n_resumed > 0 and sweep2.n_resume_missing == 0
     assert math.isfinite(sweep2.best[0])
+
+
+def test_sweep_cli_resume(tmp_path, capsys):
+    """``mopt sweep --ckpt-dir D`` stopped by ``--steps``, then ``--resume``: the experiment is
+    finished without losing or duplicating trials."""
+    import json
+    from metaopt_amd.cli import main
+    from metaopt_amd.storage.protocol import get_storage
+    name = "cli-resume-logreg"
+    common = ["--debug", "sweep", "-n", name, "--task", "logreg", "--population", "4",
+              "--max-trials", "40", "--sync-every", "16", "--ckpt-dir", str(tmp_path)]
+    assert main(common + ["--steps", "300"]) == 0
+    first = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert 0 < first["completed"] < 40
+    assert main(common + ["--steps", "100000", "--resume"]) == 0
+    second = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    storage = get_storage()
+    exp = storage.fetch_experiments({"name": name})[0]
+    trials = storage.fetch_trials(uid=exp["_id"])
+    stati = [t.status for t in trials]
+    assert "reserved" not in stati and "interrupted" not in stati and "new" not in stati
+    assert stati.count("completed") + stati.count("broken") >= 40
+    assert len({t.id for t in trials}) == len(trials)
+    assert second["completed"] > 0
