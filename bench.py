@@ -63,6 +63,8 @@ def parse_args(argv=None):
                          "this many sync intervals from the start of the sweep")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--algo", default="asha", choices=["asha", "random", "tpe"])
+    ap.add_argument("--momentum-dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="SGD momentum buffer precision (weights: f32 master + bf16 copy)")
     return ap.parse_args(argv)
 
 
@@ -149,7 +151,8 @@ def run_rank(args) -> None:
                                       storage=storage, pool_size=P)
     data = TeacherClassification(n_train=SAMPLES_PER_TRIAL if on_gpu else 4096, n_val=1024,
                                  batch_size=128, seed=1234 + args.seed, device=comm.device)
-    pop = PopulationMLP(P, max_width=max_width, eval_batch=1024, device=comm.device)
+    pop = PopulationMLP(P, max_width=max_width, eval_batch=1024, device=comm.device,
+                        momentum_dtype=args.momentum_dtype)
     sweep = PopulationSweep(pop, task, data, comm=comm, experiment=experiment,
                             sync_every=S, ckpt_capacity=4 * P)
 
@@ -217,6 +220,8 @@ def run_rank(args) -> None:
                 "step": f"one sync interval = {S} optimizer steps of every trial + the sync "
                         "(validation, C1 all-gather, decide, C5 broadcast, member init/resume)",
                 "backend": pop.backend,
+                "optimizer_state": f"f32 master weights + bf16 copy, {args.momentum_dtype} "
+                                   "SGD momentum",
                 "comm_backend": comm.backend or "none",
                 "rehearsal_ranks_share_gpus": rehearsal,
             },

@@ -1,8 +1,9 @@
 """Batched device copies (``mopt_multi_copy``) used by the sweep's checkpoint pool.
 
-``multi_copy(items)`` moves every ``(src, dst, dst16)`` triple of f32 views in ONE kernel launch
-on the GPU (``dst16``: optional bf16 view that receives the rounded copy), or with plain tensor
-copies on the CPU reference backend.  Replaces the one-framework-copy-per-tensor checkpoint and
+``multi_copy(items)`` moves every ``(src, dst, dst16)`` triple in ONE kernel launch on the GPU,
+or with plain tensor copies on the CPU reference backend.  ``src`` is an f32 or bf16 view,
+``dst`` an f32 view or None, ``dst16`` an optional bf16 view that receives the rounded copy (a bf16
+momentum buffer goes into the f32 checkpoint pool widened, and comes back through ``dst16``).  Replaces the one-framework-copy-per-tensor checkpoint and
 resume path that left the GPU idle for ~0.3 ms per copy at every sync.
 """
 from __future__ import annotations
@@ -15,7 +16,9 @@ import torch
 
 from . import _lib
 
-DESC_DTYPE = np.dtype([("src", "<u8"), ("dst", "<u8"), ("dst16", "<u8"), ("n", "<i8")])
+DESC_DTYPE = np.dtype([("src", "<u8"), ("dst", "<u8"), ("dst16", "<u8"), ("n", "<i8"),
+                       ("src16", "<u8"), ("pad", "<i8")])
+assert DESC_DTYPE.itemsize == 48
 CHUNK_DTYPE = np.dtype([("desc", "<i4"), ("pad", "<i4"), ("start", "<i8")])
 CHUNK = 4096
 
@@ -29,10 +32,11 @@ def multi_copy(items: Iterable[Tuple[torch.Tensor, torch.Tensor, Optional[torch.
     items = list(items)
     if not items:
         return
-    dev = items[0][1].device
+    dev = items[0][0].device
     if dev.type != "cuda":
         for src, dst, dst16 in items:
-            dst.copy_(src)
+            if dst is not None:
+                dst.copy_(src)
             if dst16 is not None:
                 dst16.copy_(src.to(dst16.dtype))
         return
@@ -40,13 +44,19 @@ def multi_copy(items: Iterable[Tuple[torch.Tensor, torch.Tensor, Optional[torch.
     counts = []
     for i, (src, dst, dst16) in enumerate(items):
         n = src.numel()
-        if dst.numel() != n or (dst16 is not None and dst16.numel() != n):
+        if (dst is not None and dst.numel() != n) or (dst16 is not None and dst16.numel() != n):
             raise ValueError("multi_copy: size mismatch")
-        if n % 4 or not (src.is_contiguous() and dst.is_contiguous()):
+        if dst is None and dst16 is None:
+            raise ValueError("multi_copy: no destination")
+        if n % 4 or not src.is_contiguous() or (dst is not None and not dst.is_contiguous()):
             raise ValueError("multi_copy: views must be contiguous with a multiple of 4 elements")
-        if src.dtype != torch.float32 or dst.dtype != torch.float32:
-            raise TypeError("multi_copy moves f32 data")
-        descs[i] = (src.data_ptr(), dst.data_ptr(), 0 if dst16 is None else dst16.data_ptr(), n)
+        if src.dtype not in (torch.float32, torch.bfloat16) or \
+                (dst is not None and dst.dtype != torch.float32) or \
+                (dst16 is not None and dst16.dtype != torch.bfloat16):
+            raise TypeError("multi_copy moves f32/bf16 sources into f32/bf16 destinations")
+        s16 = src.dtype == torch.bfloat16
+        descs[i] = (0 if s16 else src.data_ptr(), 0 if dst is None else dst.data_ptr(),
+                    0 if dst16 is None else dst16.data_ptr(), n, src.data_ptr() if s16 else 0, 0)
         counts.append((n + CHUNK - 1) // CHUNK)
     counts = np.array(counts, dtype=np.int64)
     chunks = np.zeros(int(counts.sum()), dtype=CHUNK_DTYPE)

@@ -35,6 +35,16 @@ __device__ __forceinline__ uint32_t pack2bf(float a, float b) {
   return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
 }
 
+// 4 packed bf16 <-> 4 f32 (bf16 optimizer state moved 8 bytes per lane)
+__device__ __forceinline__ f32x4 bf4_to_f32(uint2 v) {
+  return f32x4{__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xFFFF0000u),
+               __uint_as_float(v.y << 16), __uint_as_float(v.y & 0xFFFF0000u)};
+}
+
+__device__ __forceinline__ uint2 f32_to_bf4(const f32x4& v) {
+  return make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+}
+
 __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }

@@ -1,8 +1,10 @@
 // Batched device copies for the sweep's checkpoint pool (one launch per sync instead of one
 // framework copy per tensor and member).
 //
-// A descriptor moves n f32 values src -> dst and optionally also writes their bf16 image to dst16
-// (restoring a member's bf16 working weights in the same pass that restores its f32 master copy).
+// A descriptor moves n values from an f32 (src) or bf16 (src16) source to an f32 destination
+// (dst) and/or the bf16 image of the values (dst16): restoring a member's bf16 working weights in
+// the same pass that restores its f32 master copy, and widening / narrowing a bf16 momentum
+// buffer into / out of the f32 checkpoint pool (exact: the values are bf16).
 // Work is split into 4096-element chunks listed on the host, so a launch needs no per-descriptor
 // grid sizing and stays balanced however ragged the member sizes are.
 #include "common.h"
@@ -11,11 +13,13 @@ using namespace mopt;
 
 extern "C" {
 
-struct CopyDesc {       // 32 bytes, mirrored by metaopt_amd/ops/ckpt.py
-  const float* src;
-  float* dst;
+struct CopyDesc {       // 48 bytes, mirrored by metaopt_amd/ops/ckpt.py
+  const float* src;     // f32 source, or nullptr when src16 is set
+  float* dst;           // nullptr: no f32 copy
   bf16_t* dst16;        // nullptr: no bf16 image
   int64_t n;            // multiple of 4
+  const bf16_t* src16;  // bf16 source (widened exactly)
+  int64_t pad;
 };
 
 struct CopyChunk {      // 16 bytes
@@ -36,9 +40,10 @@ __global__ __launch_bounds__(256) void multi_copy_kernel(const CopyDesc* __restr
   const CopyDesc d = descs[c.desc];
   const int64_t end = min((int64_t)kChunk, d.n - c.start);
   for (int64_t i = 4 * threadIdx.x; i < end; i += 4 * 256) {
-    const f32x4 v = *(const f32x4*)(d.src + c.start + i);
-    *(f32x4*)(d.dst + c.start + i) = v;
-    if (d.dst16) *(uint2*)(d.dst16 + c.start + i) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+    const f32x4 v = d.src16 ? bf4_to_f32(*(const uint2*)(d.src16 + c.start + i))
+                            : *(const f32x4*)(d.src + c.start + i);
+    if (d.dst) *(f32x4*)(d.dst + c.start + i) = v;
+    if (d.dst16) *(uint2*)(d.dst16 + c.start + i) = f32_to_bf4(v);
   }
 }
 

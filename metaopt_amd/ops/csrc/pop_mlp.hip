@@ -16,8 +16,9 @@
 //                      dW never touches HBM.  W is read once (f32 master) for both dX and the update.
 //
 // Memory-bound by design: per parameter and step the population moves 2 B (forward) + 18 B (fused
-// backward + SGD) through HBM; the MFMA work (6 * B FLOP per parameter) is a small fraction of the
-// chip's bf16 rate at B = 128.  See profiles/ for measured bandwidth.
+// backward + SGD; 14 B with the bf16 momentum buffer of kSGD16) through HBM; the MFMA work
+// (6 * B FLOP per parameter) is a small fraction of the chip's bf16 rate at B = 128.  See
+// profiles/ for measured bandwidth.
 #include "common.h"
 
 using namespace mopt;
@@ -71,7 +72,9 @@ constexpr int LS = kLdsStride;
 // launch.
 enum FwdFlags { kRelu = 1, kDropout = 2, kWriteGrad = 4, kStoreStats = 8, kCountStep = 16 };
 enum BwdFlags { kHasDx = 1, kInDropout = 2, kUpdateBias = 4 };
-enum Opt { kSGD = 0, kAdamW = 1 };
+// kSGD16: SGD with the momentum buffer stored as bf16 (RNE after every update; the update uses
+// the rounded value) -- 4 bytes per parameter and step less HBM traffic than kSGD.
+enum Opt { kSGD = 0, kAdamW = 1, kSGD16 = 2 };
 
 // ----------------------------------------------------------------------------------------------
 // Forward GEMM core: acc[i][j] = X[row0 + 32*wave + 16i .., :] . W[n0 + 16j .., :]^T over all K.
@@ -345,7 +348,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const bf16_t* X = xb + tl.x_off;
   const bf16_t* dZ = grad + tl.y_off;
   float* W32 = p32 + tl.w_off;
-  float* M32 = m32 + tl.w_off;
+  float* M32 = m32 + tl.w_off;                       // kSGD / kAdamW
+  bf16_t* M16 = (bf16_t*)m32 + tl.w_off;             // kSGD16
   float* V32 = v32 + tl.w_off;  // AdamW only
   bf16_t* W16 = p16 + tl.w_off;
   const TrialHP h = hp[tl.trial];
@@ -390,6 +394,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int wo = (tid >> 4) * K + k0 + 4 * (tid & 15);
   uint4 z0, z1, z2, z3;
   f32x4 w0, w1, w2, w3, m0, m1, m2, m3, v0, v1, v2, v3;
+  uint2 h0, h1, h2, h3;                               // kSGD16 momentum (4 bf16 per lane)
 #define MOPT_BWD_LOAD(NC)                                                                        \
   {                                                                                              \
     const bf16_t* zc = dZ + (NC);                                                                \
@@ -402,10 +407,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     w1 = *(const f32x4*)(W32 + ob + 16 * K);                                                     \
     w2 = *(const f32x4*)(W32 + ob + 32 * K);                                                     \
     w3 = *(const f32x4*)(W32 + ob + 48 * K);                                                     \
-    m0 = *(const f32x4*)(M32 + ob);                                                              \
-    m1 = *(const f32x4*)(M32 + ob + 16 * K);                                                     \
-    m2 = *(const f32x4*)(M32 + ob + 32 * K);                                                     \
-    m3 = *(const f32x4*)(M32 + ob + 48 * K);                                                     \
+    if (OPT == kSGD16) {                                                                         \
+      h0 = *(const uint2*)(M16 + ob);                                                            \
+      h1 = *(const uint2*)(M16 + ob + 16 * K);                                                   \
+      h2 = *(const uint2*)(M16 + ob + 32 * K);                                                   \
+      h3 = *(const uint2*)(M16 + ob + 48 * K);                                                   \
+    } else {                                                                                     \
+      m0 = *(const f32x4*)(M32 + ob);                                                            \
+      m1 = *(const f32x4*)(M32 + ob + 16 * K);                                                   \
+      m2 = *(const f32x4*)(M32 + ob + 32 * K);                                                   \
+      m3 = *(const f32x4*)(M32 + ob + 48 * K);                                                   \
+    }                                                                                            \
     if (OPT == kAdamW) {                                                                         \
       v0 = *(const f32x4*)(V32 + ob);                                                            \
       v1 = *(const f32x4*)(V32 + ob + 16 * K);                                                   \
@@ -420,6 +432,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     *(uint4*)(zs0 + 32 * LS) = z1;
     *(uint4*)(zs0 + 64 * LS) = z2;
     *(uint4*)(zs0 + 96 * LS) = z3;
+    if (OPT == kSGD16) {
+      m0 = bf4_to_f32(h0); m1 = bf4_to_f32(h1); m2 = bf4_to_f32(h2); m3 = bf4_to_f32(h3);
+    }
     const f32x4 w[4] = {w0, w1, w2, w3}, m[4] = {m0, m1, m2, m3};
     f32x4 v[4];
     if (OPT == kAdamW) {
@@ -499,10 +514,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float gr = gv[r];
-        if (OPT == kSGD) {
+        if (OPT == kSGD || OPT == kSGD16) {
           const float gg = gr + h.wd * wv[r];
-          mv[r] = h.b1 * mv[r] + gg;
-          wv[r] = wv[r] - h.lr * mv[r];
+          float mn = h.b1 * mv[r] + gg;
+          if (OPT == kSGD16) mn = bf2f(f2bf(mn));   // the stored (rounded) momentum drives W
+          mv[r] = mn;
+          wv[r] = wv[r] - h.lr * mn;
         } else {
           wv[r] = wv[r] * (1.f - h.lr * h.wd);
           mv[r] = h.b1 * mv[r] + (1.f - h.b1) * gr;
@@ -511,7 +528,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         }
       }
       *(f32x4*)(W32 + o) = wv;
-      *(f32x4*)(M32 + o) = mv;
+      if (OPT == kSGD16) *(uint2*)(M16 + o) = f32_to_bf4(mv);
+      else *(f32x4*)(M32 + o) = mv;
       if (OPT == kAdamW) *(f32x4*)(V32 + o) = vv;
       *(uint2*)(W16 + o) = make_uint2(pack2bf(wv[0], wv[1]), pack2bf(wv[2], wv[3]));
     }
@@ -527,9 +545,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         const float gb = red[tid] + red[64 + tid] + red[128 + tid] + red[192 + tid];
         float* bp = p32 + tl.b_off + nc + tid;
         float* bm = m32 + tl.b_off + nc + tid;
-        float bw = *bp, mb = *bm;
-        if (OPT == kSGD) {
+        bf16_t* bm16 = (bf16_t*)m32 + tl.b_off + nc + tid;
+        float bw = *bp, mb = OPT == kSGD16 ? bf2f(*bm16) : *bm;
+        if (OPT == kSGD || OPT == kSGD16) {
           mb = h.b1 * mb + gb;
+          if (OPT == kSGD16) mb = bf2f(f2bf(mb));
           bw = bw - h.lr * mb;
         } else {
           float* bv = v32 + tl.b_off + nc + tid;
@@ -540,7 +560,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           *bv = vb;
         }
         *bp = bw;
-        *bm = mb;
+        if (OPT == kSGD16) *bm16 = f2bf(mb);
+        else *bm = mb;
       }
     }
     __syncthreads();
@@ -577,7 +598,7 @@ __global__ __launch_bounds__(256) void mlp_init_kernel(const InitDesc* __restric
                                                        float* __restrict__ p32,
                                                        bf16_t* __restrict__ p16,
                                                        float* __restrict__ m32,
-                                                       float* __restrict__ v32, int zero_v) {
+                                                       float* __restrict__ v32, int flags) {
   const InitDesc d = descs[blockIdx.y];
   const uint32_t wkey = rng_key(d.seed, 0x1000u + (uint32_t)d.layer, 0u);
   const uint32_t bkey = rng_key(d.seed, 0x2000u + (uint32_t)d.layer, 0u);
@@ -598,8 +619,9 @@ __global__ __launch_bounds__(256) void mlp_init_kernel(const InitDesc* __restric
     }
     p32[o] = v;
     p16[o] = f2bf(v);
-    m32[o] = 0.f;
-    if (zero_v) v32[o] = 0.f;
+    if (flags & 2) ((bf16_t*)m32)[o] = 0;   // bf16 momentum (kSGD16)
+    else m32[o] = 0.f;
+    if (flags & 1) v32[o] = 0.f;
   }
 }
 
@@ -610,14 +632,15 @@ __global__ __launch_bounds__(256) void mlp_init_kernel(const InitDesc* __restric
 // ------------------------------------------------------------------------------------------------
 extern "C" {
 
-int mopt_abi_version() { return 5; }
+int mopt_abi_version() { return 6; }
 
+// flags: 1 = zero the AdamW second moment, 2 = the momentum buffer is bf16
 int mopt_mlp_init(const void* descs, int n_desc, void* p32, void* p16, void* m32, void* v32,
-                  int zero_v, void* stream) {
+                  int flags, void* stream) {
   if (n_desc <= 0) return 0;
   hipLaunchKernelGGL(mlp_init_kernel, dim3(64, n_desc), dim3(256), 0, (hipStream_t)stream,
                      (const InitDesc*)descs, (float*)p32, (bf16_t*)p16, (float*)m32, (float*)v32,
-                     zero_v);
+                     flags);
   return (int)hipGetLastError();
 }
 
@@ -651,6 +674,11 @@ int mopt_mlp_bwd(const void* tls, const void* work, int n_work, const void* xb, 
   if (n_work <= 0) return 0;
   if (opt == kAdamW) {
     hipLaunchKernelGGL(mlp_bwd_opt_kernel<kAdamW>, dim3(n_work), dim3(256), 0, (hipStream_t)stream,
+                       (const MlpTL*)tls, (const int2*)work, n_work, (const bf16_t*)xb,
+                       (bf16_t*)grad, (float*)p32, (bf16_t*)p16, (float*)m32, (float*)v32,
+                       (const TrialHP*)hp, flags);
+  } else if (opt == kSGD16) {
+    hipLaunchKernelGGL(mlp_bwd_opt_kernel<kSGD16>, dim3(n_work), dim3(256), 0, (hipStream_t)stream,
                        (const MlpTL*)tls, (const int2*)work, n_work, (const bf16_t*)xb,
                        (bf16_t*)grad, (float*)p32, (bf16_t*)p16, (float*)m32, (float*)v32,
                        (const TrialHP*)hp, flags);

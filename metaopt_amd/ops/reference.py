@@ -100,8 +100,14 @@ def softmax_ce(logits: torch.Tensor, labels: torch.Tensor, n_real: int, inv_b: f
 
 
 def sgd_update(w, m, g, lr, momentum, wd):
-    """torch.optim.SGD(momentum, weight_decay, dampening=0, nesterov=False) on one tensor."""
+    """torch.optim.SGD(momentum, weight_decay, dampening=0, nesterov=False) on one tensor.
+    A bf16 ``m`` is the kernel's bf16 momentum buffer: the f32 update is rounded once (RNE) and
+    the rounded value drives the weight update."""
     g = g + wd * w
+    if m.dtype == torch.bfloat16:
+        m.copy_(m.float() * momentum + g)
+        w.sub_(lr * m.float())
+        return
     m.mul_(momentum).add_(g)
     w.sub_(lr * m)
 

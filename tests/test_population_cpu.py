@@ -176,3 +176,35 @@ def test_sweep_point_key_matches_task_key(data):
         params = dict(zip(sweep._dim_names, point))
         assert sweep._point_key(point) == task.key(params)
     sweep.close()
+
+
+def test_bf16_momentum_reference_update():
+    """The bf16 momentum buffer: one RNE rounding of the f32 update, which then drives W."""
+    import torch
+    from metaopt_amd.ops import reference as ref
+    w = torch.tensor([1.0, -2.0, 0.5])
+    g = torch.tensor([0.3, 0.1, -0.7])
+    m16 = torch.tensor([0.2, -0.4, 1.0]).to(torch.bfloat16)
+    m_exact = m16.float() * 0.9 + (g + 1e-3 * w)
+    w_exp = w - 0.1 * m_exact.to(torch.bfloat16).float()
+    ref.sgd_update(w, m16, g, 0.1, 0.9, 1e-3)
+    assert m16.dtype == torch.bfloat16
+    assert torch.equal(m16, m_exact.to(torch.bfloat16))
+    assert torch.allclose(w, w_exp, rtol=0, atol=1e-7)
+
+
+def test_bf16_momentum_population_trains_on_cpu():
+    import numpy as np
+    from metaopt_amd.models.data import TeacherClassification
+    from metaopt_amd.ops.population import MemberConfig, PopulationMLP
+    data = TeacherClassification(n_train=1024, n_val=128, batch_size=128, seed=0)
+    pop = PopulationMLP(2, max_width=64, eval_batch=128, device="cpu", momentum_dtype="bf16")
+    assert pop.m32.dtype == __import__("torch").bfloat16
+    pop.set_member(0, MemberConfig(width=64, lr=0.1, seed=1))
+    losses = []
+    for step in range(8):
+        pop.train_step(*data.batch(step))
+        losses.append(pop.train_loss()[0])
+    assert np.isfinite(losses).all() and losses[-1] < losses[0]
+    st = pop.slot_state(0)
+    assert st["m32"].dtype == __import__("torch").bfloat16
