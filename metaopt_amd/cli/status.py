@@ -1,7 +1,19 @@
-"""``mopt status [-a] [-C] [-e]``: per-status trial counts (reference: ``cli/status.py:25-233``)."""
+"""``mopt status [-a] [-C] [-e]``: an overview of the trials of every experiment.
+
+Behaviour follows the reference's ``orion status`` (``src/orion/core/cli/status.py:25-233``):
+one block per experiment -- the tree name underlined, then either a per-status table (count and
+best objective) or, with ``--all``, one row per trial.  Experiments are shown as version trees:
+an experiment whose tree holds other names (or ``--expand-versions``) lists each node indented
+by depth; ``--collapse`` shows the latest version's view of the whole tree instead.
+
+Built differently: a pass collects :class:`Block` records (title, depth, trials) from the EVC
+tree, and one renderer turns any block into text, so the per-status and per-trial layouts share
+the indentation and table code.
+"""
 from __future__ import annotations
 
-import collections
+from dataclasses import dataclass
+from typing import Iterable, List
 
 import tabulate
 
@@ -23,99 +35,100 @@ def add_subparser(parser):
     return p
 
 
+@dataclass
+class Block:
+    """What one experiment node contributes to the report."""
+
+    title: str
+    depth: int
+    trials: list
+
+
 def main(args):
     builder = ExperimentBuilder()
-    local = builder.fetch_full_config(args, use_db=False)
-    builder.setup_storage(local)
-    args = dict(args)
-    args["all_trials"] = args.pop("all", False)
-    experiments = get_experiments(args, builder)
-    if not experiments:
-        print("No experiment found")
-        return 0
-    if args.get("name"):
-        print_evc([experiments[0]], builder, **args)
-        return 0
-    if args.get("version") and (args.get("collapse") or args.get("expand_versions")):
+    builder.setup_storage(builder.fetch_full_config(args, use_db=False))
+    name, version = args.get("name"), args.get("version")
+    per_trial = bool(args.get("all"))
+    collapse, expand = bool(args.get("collapse")), bool(args.get("expand_versions"))
+    if name is None and version and (collapse or expand):
         raise RuntimeError("Cannot fetch specific version of experiments with --collapse or "
                            "--expand-versions.")
-    print_evc([e for e in experiments if e.refers.get("parent_id") is None], builder, **args)
+    views = _experiment_views(builder, name)
+    if not views:
+        print("No experiment found")
+        return 0
+    roots = views[:1] if name else [v for v in views if v.refers.get("parent_id") is None]
+    for root in roots:
+        for block in _blocks(builder, root, version, collapse, expand):
+            print(render(block, per_trial))
     return 0
 
 
-def get_experiments(args, builder):
-    query = {"name": args["name"]} if args.get("name") else {}
-    found = get_storage().fetch_experiments(query, {"name": 1, "version": 1})
-    return [builder.build_view_from({"name": e["name"], "version": e.get("version", 1)})
-            for e in found]
+def _experiment_views(builder, name):
+    query = {"name": name} if name else {}
+    docs = get_storage().fetch_experiments(query, {"name": 1, "version": 1})
+    return [builder.build_view_from({"name": d["name"], "version": d.get("version", 1)})
+            for d in docs]
 
 
-def _has_named_children(exp):
-    return any(node.name != exp.name for node in exp.node)
+def _blocks(builder, root, version, collapse, expand) -> Iterable[Block]:
+    """Blocks of one root experiment: its tree node by node, or one collapsed block."""
+    chosen = builder.build_view_from({"name": root.name, "version": version})
+    anchor = root if version is None else chosen
+    many_names = any(node.name != anchor.name for node in anchor.node)
+    if (expand or many_names) and not collapse:
+        yield from _walk(anchor, 0)
+    else:
+        yield Block(chosen.node.tree_name, 0, chosen.fetch_trials(with_evc_tree=True))
 
 
-def print_evc(experiments, builder, version=None, all_trials=False, collapse=False,
-              expand_versions=False, **kwargs):
-    for exp in experiments:
-        experiment = builder.build_view_from({"name": exp.name, "version": version})
-        expand_exp = exp if version is None else experiment
-        expand = expand_versions or _has_named_children(expand_exp)
-        if expand and not collapse:
-            print_status_recursively(expand_exp, all_trials=all_trials)
-        else:
-            print_status(experiment, all_trials=all_trials, collapse=True)
-
-
-def print_status_recursively(exp, depth=0, **kwargs):
-    print_status(exp, offset=depth * 2, **kwargs)
+def _walk(exp, depth) -> Iterable[Block]:
+    yield Block(exp.node.tree_name, depth, exp.fetch_trials(with_evc_tree=False))
     for child in exp.node.children:
-        print_status_recursively(child.item, depth + 1, **kwargs)
+        yield from _walk(child.item, depth + 1)
 
 
-def print_status(exp, offset=0, all_trials=False, collapse=False):
-    trials = exp.fetch_trials(with_evc_tree=collapse)
-    title = exp.node.tree_name
-    print(" " * offset, title, sep="")
-    print(" " * offset, "=" * len(title), sep="")
-    if all_trials:
-        print_all_trials(trials, offset=offset)
+# ---------------------------------------------------------------------------------- rendering
+def render(block: Block, per_trial: bool = False) -> str:
+    pad = " " * (2 * block.depth)
+    out: List[str] = [pad + block.title, pad + "=" * len(block.title)]
+    if per_trial:
+        headers, rows = _trial_rows(block.trials)
+    elif block.trials:
+        headers, rows = _status_rows(block.trials)
     else:
-        print_summary(trials, offset=offset)
+        headers, rows = None, None
+    if headers is None:
+        out.append(pad + "empty")
+    else:
+        out.extend(pad + line for line in tabulate.tabulate(rows, headers=headers).split("\n"))
+    return "\n".join(out) + "\n\n"
 
 
-def print_summary(trials, offset=0):
-    by_status = collections.defaultdict(list)
+def _status_rows(trials):
+    """(status, count[, best objective]) per status, statuses in alphabetical order."""
+    groups = {}
     for t in trials:
-        by_status[t.status].append(t)
-    headers = ["status", "quantity"]
-    lines = []
-    for status, ts in sorted(by_status.items()):
-        line = [status, len(ts)]
-        if ts[0].objective:
-            headers.append(f"min {ts[0].objective.name}")
-            line.append(min(t.objective.value for t in ts if t.objective))
-        lines.append(line)
-    if trials:
-        grid = tabulate.tabulate(lines, headers=headers)
-        tab = " " * offset
-        print(tab + ("\n" + tab).join(grid.split("\n")))
-    else:
-        print(" " * offset, "empty", sep="")
-    print("\n")
+        groups.setdefault(t.status, []).append(t)
+    headers, rows = ["status", "quantity"], []
+    for status in sorted(groups):
+        members = groups[status]
+        row = [status, len(members)]
+        scored = [t.objective for t in members if t.objective]
+        if members[0].objective:   # the reference names the column after the first trial's
+            headers.append(f"min {members[0].objective.name}")
+            row.append(min(o.value for o in scored))
+        rows.append(row)
+    return headers, rows
 
 
-def print_all_trials(trials, offset=0):
+def _trial_rows(trials):
+    """(id, status[, objective]) per trial, grouped by status."""
     headers = ["id", "status", "best objective"]
-    lines = []
+    rows = []
     for t in sorted(trials, key=lambda t: t.status):
-        line = [t.id, t.status]
-        if t.objective:
-            headers[-1] = f"min {t.objective.name}"
-            line.append(t.objective.value)
-        lines.append(line)
-    if not trials:
-        lines.append(["empty", "", ""])
-    grid = tabulate.tabulate(lines, headers=headers)
-    tab = " " * offset
-    print(tab + ("\n" + tab).join(grid.split("\n")))
-    print("\n")
+        obj = t.objective
+        if obj:
+            headers[2] = f"min {obj.name}"
+        rows.append([t.id, t.status] + ([obj.value] if obj else []))
+    return headers, rows or [["empty", "", ""]]
