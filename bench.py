@@ -63,7 +63,7 @@ def parse_args(argv=None):
                          "this many sync intervals from the start of the sweep")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--algo", default="asha", choices=["asha", "random", "tpe"])
-    ap.add_argument("--momentum-dtype", default="fp32", choices=["fp32", "bf16"],
+    ap.add_argument("--momentum-dtype", default="bf16", choices=["fp32", "bf16"],
                     help="SGD momentum buffer precision (weights: f32 master + bf16 copy)")
     return ap.parse_args(argv)
 
@@ -171,6 +171,7 @@ def run_rank(args) -> None:
     sync()
     comm.barrier()
     sync()
+    sweep.gpu_timeline(clear=True)
     s0, c0, n0 = sweep.samples, sweep.completed, sweep.n_syncs
     sweep.timers.clear()
     sweep.n_syncs = 0
@@ -241,6 +242,8 @@ def run_rank(args) -> None:
                        "reached": reached},
             "samples_per_sec": round(samples / elapsed, 1),
             "host_ms_per_sync": summ["host_ms_per_sync"],
+            **({"gpu_timeline": sweep.gpu_timeline()} if os.environ.get("MOPT_GPU_TIMELINE")
+               else {}),
             "warmup_syncs": n0,
         }
         print(json.dumps(out), flush=True)

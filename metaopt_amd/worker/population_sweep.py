@@ -116,6 +116,10 @@ class PopulationSweep:
         self._busy_marker = None
         self._ctl_stream = None
         self._started = False
+        # MOPT_GPU_TIMELINE=1: GPU events at interval starts and syncs (stream time of the train
+        # steps vs the sync work, including any idle the host causes) -- see gpu_timeline()
+        self._timeline = [] if (os.environ.get("MOPT_GPU_TIMELINE") == "1"
+                                and pop.device.type == "cuda") else None
         # observability / failure detection (utils/events.py, parallel/watchdog.py)
         self.events = events if events is not None else NullEventLog()
         self.trial_events = bool(trial_events) and events is not None
@@ -193,6 +197,8 @@ class PopulationSweep:
 
     def step(self) -> None:
         t0 = time.perf_counter()
+        if self._timeline is not None and self.global_step % self.sync_every == 0:
+            self._mark("interval")
         x, y = self.data.batch(self.global_step)
         self.pop.train_step(x, y)
         self.global_step += 1
@@ -203,6 +209,8 @@ class PopulationSweep:
             self._busy_marker = self.pop.device_busy()
         self.timers["launch"] += time.perf_counter() - t0
         if self.global_step % self.sync_every == 0:
+            if self._timeline is not None:
+                self._mark("sync")
             self._sync()
 
     def run(self, max_steps: int) -> dict:
@@ -940,6 +948,27 @@ class PopulationSweep:
         return self._mb
 
     # ------------------------------------------------------------------ reporting
+    def _mark(self, kind: str) -> None:
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.current_stream(self.pop.device))
+        self._timeline.append((kind, ev, time.perf_counter()))
+
+    def gpu_timeline(self, clear: bool = True) -> dict:
+        """Mean GPU-stream ms of the train steps of an interval and of the sync work between
+        intervals (MOPT_GPU_TIMELINE=1), after a device synchronize."""
+        if not self._timeline:
+            return {}
+        torch.cuda.synchronize()
+        marks = self._timeline
+        train, between = [], []
+        for (k0, e0, _), (k1, e1, _) in zip(marks, marks[1:]):
+            (train if (k0, k1) == ("interval", "sync") else between).append(e0.elapsed_time(e1))
+        if clear:
+            self._timeline = []
+        mean = (lambda v: round(sum(v) / len(v), 3) if v else None)
+        return {"gpu_ms_train_per_interval": mean(train), "gpu_ms_sync_per_interval": mean(between),
+                "n": len(train)}
+
     def best_within(self, steps: int):
         """(best validation loss, #trials) over the trials that finished within the first
         ``steps`` population steps of the sweep (rank 0) -- best-loss@budget."""

@@ -23,13 +23,16 @@ ap.add_argument("--population", type=int, default=256)
 ap.add_argument("--iters", type=int, default=50)
 ap.add_argument("--width", type=int, default=0, help="fixed width (0: loguniform(64,1024))")
 ap.add_argument("--optimizer", default="sgd")
+ap.add_argument("--momentum-dtype", default="fp32", choices=["fp32", "bf16"])
+ap.add_argument("--streams", type=int, default=1)
 ap.add_argument("--out", default="")
 args = ap.parse_args()
 
 dev = torch.device("cuda")
 rng = np.random.RandomState(0)
 P = args.population
-pop = PopulationMLP(P, max_width=1024, device=dev, optimizer=args.optimizer)
+pop = PopulationMLP(P, max_width=1024, device=dev, optimizer=args.optimizer,
+                    momentum_dtype=args.momentum_dtype, n_streams=args.streams)
 for s in range(P):
     w = args.width or int(np.exp(rng.uniform(np.log(64), np.log(1024))))
     pop.set_member(s, MemberConfig(width=w, lr=0.01, dropout=0.1, seed=s))
@@ -41,7 +44,8 @@ torch.cuda.synchronize()
 
 lib, tb, L = pop._lib, pop._tables["train"], pop.L
 stream = _lib.stream_ptr(dev)
-opt = 0 if args.optimizer == "sgd" else 1
+opt = (2 if args.momentum_dtype == "bf16" else 0) if args.optimizer == "sgd" else 1
+BWD_BYTES = {0: 18, 1: 26, 2: 14}[opt]
 
 
 def run_fwd(l):
@@ -74,7 +78,7 @@ for l in range(L):
     layer_params.append(int((rows["K"].astype(np.int64) * rows["N"]).sum()))
 
 results = {}
-for name, fn, byte_per in [("fwd", run_fwd, 2), ("bwd", run_bwd, 18 if opt == 0 else 26)]:
+for name, fn, byte_per in [("fwd", run_fwd, 2), ("bwd", run_bwd, BWD_BYTES)]:
     for l in range(L):
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
@@ -99,7 +103,7 @@ torch.cuda.synchronize()
 step = ev0.elapsed_time(ev1) / args.iters
 total_params = sum(layer_params)
 print(f"full step: {step*1e3:.1f} us; params {total_params/1e6:.1f}M; "
-      f"{total_params*(20 if opt == 0 else 28)/(step*1e-3)/1e12:.2f} TB/s param-bytes")
+      f"{total_params*(2 + BWD_BYTES)/(step*1e-3)/1e12:.2f} TB/s param-bytes")
 results["step_ms"] = step
 if args.out:
     with open(args.out, "w") as f:
