@@ -41,8 +41,8 @@ import torch
 from ..algo.primary import PrimaryAlgo
 from ..ops.population import MemberConfig, PopulationMLP
 from ..parallel.comm import Comm
-from ..storage.database import DuplicateKeyError
 from ..utils.events import NullEventLog
+from .writer import DocBuilder, WriteBehind, WriterProcess, storage_spec
 
 log = logging.getLogger(__name__)
 
@@ -59,7 +59,7 @@ class PopulationSweep:
                  heartbeat_every: float = 30.0, max_trials: Optional[float] = None,
                  pipelined: Optional[bool] = None, events=None, trial_events: bool = False,
                  watchdog=None, restore_algorithm: bool = False, resume: bool = False,
-                 ckpt_dir: Optional[str] = None):
+                 ckpt_dir: Optional[str] = None, writer: str = "auto"):
         self.pop = pop
         self.task = task
         self.data = data
@@ -132,11 +132,10 @@ class PopulationSweep:
         if self.comm.is_root:
             self.algorithm = experiment.algorithms
             self.space = experiment.space
-            self._writer = _WriteBehind(experiment.storage, build_doc=self._build_doc,
-                                        build_fields=self._result_fields)
             self._dim_names = list(self.space.keys())
             self._dim_types = [d.type for d in self.space.values()]
             self._exp_str = str(experiment.id)
+            self._writer = self._make_writer(writer, getattr(task, "secondary_stat", "val_acc"))
             # Trial.params_repr of a point is this template filled with its values
             self._repr_tmpl = ",".join(f"{n}:{{}}" for n in self._dim_names)
             self._sec_name = getattr(task, "secondary_stat", "val_acc")
@@ -182,6 +181,19 @@ class PopulationSweep:
         self.events.emit("sweep_start", world_size=self.comm.world_size, population=P,
                          sync_every=self.sync_every, pipelined=self.pipelined,
                          algorithm=type(getattr(self, "algorithm", None)).__name__)
+
+    def _make_writer(self, kind: str, sec_name: str):
+        """Storage writes off the decision path: in this process (``inline``) or in a child
+        process (``process``; ``auto`` picks it from 2 ranks up, where rank 0 decides for every
+        rank's slots and has no idle host time to write in).  ``MOPT_WRITER`` overrides."""
+        kind = os.environ.get("MOPT_WRITER", kind)
+        builder = DocBuilder(self.experiment.id, self._dim_names, self._dim_types, sec_name)
+        spec = storage_spec(self.experiment.storage)
+        if kind == "auto":
+            kind = "process" if self.comm.world_size > 1 and spec is not None else "inline"
+        if kind == "process" and spec is not None:
+            return WriterProcess(self.experiment.storage, builder, spec)
+        return WriteBehind(self.experiment.storage, builder)
 
     def _gc_callback(self, phase, info):
         if phase == "start":
@@ -568,25 +580,6 @@ class PopulationSweep:
         cfg = self.task.member_config(params, self.task.seed_of(pkey))
         assign[row] = (action, key, cfg.width, cfg.lr, cfg.momentum, cfg.weight_decay,
                        cfg.dropout, cfg.seed, self.task.budget(params), resume, src)
-
-    def _build_doc(self, spec) -> dict:
-        """Trial document (core/trial.py schema) of a registration queued by ``_fill``."""
-        tid, stamp, point, parent = spec
-        return {"experiment": self.experiment.id, "status": "reserved", "worker": None,
-                "heartbeat": stamp, "submit_time": stamp, "start_time": stamp,
-                "end_time": None, "results": [],
-                "params": [{"name": n, "type": t, "value": v}
-                           for n, t, v in zip(self._dim_names, self._dim_types, point)],
-                "parents": [parent] if parent is not None else [],
-                "_id": tid}
-
-    def _result_fields(self, spec) -> dict:
-        """Fields of a completed trial's update queued by ``_decide``."""
-        vl, va, tl, now, hb = spec
-        return {"results": [{"name": "val_loss", "type": "objective", "value": vl},
-                            {"name": self._sec_name, "type": "statistic", "value": va},
-                            {"name": "train_loss", "type": "statistic", "value": tl}],
-                "status": "completed", "end_time": now, "heartbeat": hb}
 
     def _point_key(self, point, params=None) -> str:
         """``task.key(params)`` of a suggested point (python scalars, space order)."""
@@ -983,98 +976,3 @@ class PopulationSweep:
                 "active": int((self.slot_key >= 0).sum()),
                 "host_ms_per_sync": {k: round(1e3 * v / max(self.n_syncs, 1), 3)
                                      for k, v in self.timers.items()}}
-
-
-class _WriteBehind:
-    """Storage writes taken off the decision path (write-behind).
-
-    The sweep's decisions never read back what it writes (rank 0 keeps its own bookkeeping), so
-    persisting trials -- registration, results, status changes, heartbeats -- is deferred as
-    document operations: ``put_register`` / ``put_update`` queue them; ``drain_while(busy)``
-    applies held writes in order, one unit at a time, for as long as ``busy()`` says the GPU is
-    still working on queued work, so the host does its bookkeeping inside the device time
-    instead of after it (no helper thread: a thread would need the GIL that the waiting thread
-    holds).  Consecutive registrations become one bulk insert.  ``flush`` applies everything.
-    """
-
-    def __init__(self, storage, build_doc=None, build_fields=None):
-        self.storage = storage
-        # deferred construction: the decision path queues compact tuples and the documents
-        # (registrations) / field dicts (results) are built here, inside the GPU-busy window
-        self.build_doc = build_doc
-        self.build_fields = build_fields
-        self.errors = 0
-        self._held: "collections.deque" = collections.deque()
-        self.busy_s = 0.0             # seconds spent applying writes
-        # the watchdog thread may flush while the main thread drains: one unit at a time
-        self._lock = threading.Lock()
-
-    def put_register(self, doc: dict):
-        """Register a trial document (a shallow copy: the sweep replaces, never mutates, the
-        fields it changes later)."""
-        self._held.append(("register", dict(doc)))
-
-    def put_update(self, uid, fields: dict, was=None):
-        """Set ``fields`` of trial ``uid`` (only while its status is ``was``, when given)."""
-        self._held.append(("update", (uid, fields, was)))
-
-    def put_register_spec(self, spec: tuple):
-        """Register the trial document ``build_doc(spec)`` (built when the write is applied)."""
-        self._held.append(("register", spec))
-
-    def put_update_spec(self, uid, spec: tuple, was=None):
-        """Set the fields ``build_fields(spec)`` of trial ``uid`` (built when applied)."""
-        self._held.append(("update", (uid, spec, was)))
-
-    def __len__(self):
-        return len(self._held)
-
-    def drain_while(self, busy) -> None:
-        t0 = time.perf_counter()
-        while self._held and busy():
-            with self._lock:
-                if not self._held:
-                    break
-                self._apply_batch(self._take())
-        self.busy_s += time.perf_counter() - t0
-
-    def _take(self):
-        """Next unit of work: a run of <= 256 registrations (one bulk insert) or of updates
-        (one bulk compare-and-swap)."""
-        first = self._held.popleft()
-        item = [first]
-        while self._held and len(item) < 256 and self._held[0][0] == first[0]:
-            item.append(self._held.popleft())
-        return item
-
-    def _apply_batch(self, held):
-        if held[0][0] == "register":
-            build = self.build_doc
-            docs = [h[1] if type(h[1]) is dict else build(h[1]) for h in held]
-            if not self._call("register_trial_docs", docs, owned=True):
-                for d in docs:            # a bulk insert hit a duplicate: insert one by one
-                    self._call("register_trial_docs", [dict(d)])
-            return
-        fields = self.build_fields
-        self._call("update_trial_docs",
-                   [h[1] if type(h[1][1]) is dict else (h[1][0], fields(h[1][1]), h[1][2])
-                    for h in held])
-
-    def _call(self, method, *args, **kwargs) -> bool:
-        try:
-            getattr(self.storage, method)(*args, **kwargs)
-            return True
-        except DuplicateKeyError:
-            log.debug("duplicate write skipped (%s)", method)
-            return False
-        except Exception as exc:  # pragma: no cover - storage hiccup
-            self.errors += 1
-            log.warning("storage write %s failed: %s", method, exc)
-            return True
-
-    def flush(self):
-        """Apply every held write."""
-        self.drain_while(lambda: True)
-
-    def close(self):
-        self.flush()

@@ -42,6 +42,9 @@ class _FakeComm:
     def broadcast_object(self, obj, src=0):
         return obj
 
+    def all_gather_object(self, obj):
+        return [obj]
+
 
 def main(n_syncs=40, P=256, world=1, profile=False):
     task = MLPSweepTask(priors=dict(MLP_PRIORS), max_width=1024)
@@ -49,7 +52,8 @@ def main(n_syncs=40, P=256, world=1, profile=False):
                            algorithms={"asha": {"seed": 0, "repetitions": float("inf")}},
                            storage=DocumentStorage(EphemeralDB()), pool_size=P)
     sw = PopulationSweep(_FakePop(P), task, data=None, comm=_FakeComm(world), experiment=exp,
-                         sync_every=32, pipelined=False)
+                         sync_every=32, pipelined=False,
+                         writer=os.environ.get("WRITER", "auto"))
     P = P * world                      # rows of the gathered status block
     rng = np.random.default_rng(0)
     steps = np.zeros(P)
@@ -87,10 +91,15 @@ def main(n_syncs=40, P=256, world=1, profile=False):
             prof.disable()
         t_total += time.perf_counter() - t0
         t1 = time.perf_counter()
-        sw._writer.flush()
+        sw._writer.drain_while(lambda: True)   # rank 0's share of the writes (inline: all)
         t_rel += time.perf_counter() - t1
         gc.freeze()                     # as PopulationSweep._sync does after every sync
+    t2 = time.perf_counter()
+    sw._writer.flush()
+    t_flush = time.perf_counter() - t2
     sw.close()
+    print(f"writer {type(sw._writer).__name__ if sw._writer else ''}: final flush "
+          f"{1e3 * t_flush:.1f} ms")
     print(f"decide: {1e3 * t_total / n_syncs:.2f} ms/sync, writes {1e3 * t_rel / n_syncs:.2f} ms/sync, "
           f"{n_done / n_syncs:.1f} completions/sync")
     if prof:

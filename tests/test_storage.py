@@ -191,3 +191,28 @@ class TestStorageProtocol:
         assert len(storage.fetch_pending_trials(exp)) == 2
         assert len(storage.fetch_noncompleted_trials(exp)) == 4
         assert len(storage.fetch_trials_by_status(exp, "broken")) == 2
+
+
+def test_writer_process_mirrors_ephemeral_db():
+    """The sweep's child-process writer applies queued specs in its own copy of an in-memory
+    database and copies the final trials back at close; file databases are shared."""
+    import datetime
+    from metaopt_amd.storage.protocol import DocumentStorage
+    from metaopt_amd.worker.writer import DocBuilder, WriterProcess, storage_spec
+    storage = DocumentStorage(EphemeralDB())
+    storage.database.write("trials", {"_id": "old", "experiment": 7, "status": "interrupted",
+                                      "params": [], "results": []})
+    b = DocBuilder(7, ["/x"], ["real"])
+    w = WriterProcess(storage, b, storage_spec(storage))
+    now = datetime.datetime.utcnow()
+    for i in range(300):
+        w.put_register_spec((f"t{i}", now, (float(i),), None))
+    w.put_update("old", {"status": "reserved"}, was="interrupted")
+    w.drain_while(lambda: True)
+    w.put_update_spec("t3", (0.5, 0.9, 0.7, now, now), was="reserved")
+    w.flush()
+    w.close()
+    docs = {d["_id"]: d for d in storage.database.read("trials", {"experiment": 7})}
+    assert len(docs) == 301 and docs["old"]["status"] == "reserved"
+    assert docs["t3"]["status"] == "completed" and docs["t3"]["results"][0]["value"] == 0.5
+    assert docs["t5"]["params"][0] == {"name": "/x", "type": "real", "value": 5.0}
