@@ -228,11 +228,12 @@ class ASHA(BaseAlgorithm):
 
     @property
     def fidelity_index(self) -> int:
-        idx = self.__dict__.get("_fidelity_index")
-        if idx is None:
+        try:
+            return self.__dict__["_fidelity_index"]
+        except KeyError:
             idx = [i for i, d in enumerate(self.space.values()) if _is_fidelity(d)][0]
             self.__dict__["_fidelity_index"] = idx
-        return idx
+            return idx
 
 
 class Bracket:

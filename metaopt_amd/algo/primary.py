@@ -45,8 +45,11 @@ class PrimaryAlgo(BaseAlgorithm):
         points = self.algorithm.suggest(num)
         if points is None:
             return None
-        out = []
         check = not getattr(self.algorithm, "trusted_suggestions", False)
+        if not check and self.transformed_space._is_identity():
+            # draws of space.sample (python scalars) or earlier points: nothing to convert
+            return [p if type(p) is tuple else tuple(p) for p in points]
+        out = []
         for p in points:
             if check and p not in self.transformed_space:
                 raise ValueError(f"Point is not contained in space:\nPoint: {p}\n"

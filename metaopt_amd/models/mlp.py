@@ -75,6 +75,16 @@ class MLPSweepTask:
             seed=int(seed) & 0x7FFFFFFF,
         )
 
+    def member_row(self, params: Dict, seed: int) -> tuple:
+        """(width, lr, momentum, weight decay, dropout, seed) of :meth:`member_config` without
+        building the dataclass (the sweep places thousands of members per sync)."""
+        g = params.get
+        return (int(g("/width", self.width)), float(params["/lr"]),
+                float(g("/momentum", self.momentum)),
+                float(g("/weight_decay", self.weight_decay)),
+                float(g("/dropout", 0.0)) if self.n_hidden > 0 else 0.0,
+                int(seed) & 0x7FFFFFFF)
+
     def budget(self, params: Dict) -> int:
         return int(params[self.fidelity])
 

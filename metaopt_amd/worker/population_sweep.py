@@ -86,8 +86,8 @@ class PopulationSweep:
         # in-flight trials as storage documents (the Trial schema of core/trial.py, built
         # directly: object construction and re-hashing per trial dominated rank 0's host time)
         self.trials: Dict[int, list] = {}             # key -> [trial id, heartbeat] (reserved)
-        self.key_params: Dict[int, dict] = {}
-        self.key_pkey: Dict[int, str] = {}
+        # in-flight trial key -> (params dict, param key, point tuple, budget)
+        self.key_info: Dict[int, tuple] = {}
         self.ckpt_index: Dict[str, tuple] = {}        # param key -> (rank, trial key, steps)
         self._ckpt_pkey: Dict[tuple, str] = {}        # (rank, trial key) -> param key
         self.ckpt_fifo = [collections.deque() for _ in range(self.comm.world_size)]
@@ -150,6 +150,17 @@ class PopulationSweep:
                     "(" + repr(n).replace("{", "{{").replace("}", "}}") + ", {!r})"
                     for n in names) + "]"
                 self._pkey_idx = idx
+            # ASHA identifies a configuration by the md5 of its non-fidelity values and caches
+            # it per suggested point: the same identity serves as the sweep's key (one md5 less
+            # per placed trial)
+            inner_algo = getattr(self.algorithm, "algorithm", self.algorithm)
+            self._algo_id = None
+            if (getattr(task, "key_by_params", False) and hasattr(inner_algo, "get_id")
+                    and getattr(inner_algo, "fidelity_index", None) is not None
+                    and self._dim_names[inner_algo.fidelity_index] == task.fidelity
+                    and getattr(getattr(self.algorithm, "transformed_space", None),
+                                "_is_identity", lambda: False)()):
+                self._algo_id = inner_algo.get_id
             inner = getattr(self.algorithm, "algorithm", self.algorithm)
             self._tracks_lineage = hasattr(inner, "parent_of")
             if watchdog is not None:
@@ -407,8 +418,7 @@ class PopulationSweep:
                 if not bad and budget < max_b:
                     self._mirror_save(rank, key)
                 if bad and key in self.trials:
-                    self.key_params.pop(key, None)
-                    self.key_pkey.pop(key, None)
+                    self.key_info.pop(key, None)
                     self.broken += 1
                     self._set_status(self.trials.pop(key), "broken")
             # 2) the result of the member that finished in this slot (this sync or, pipelined,
@@ -417,10 +427,10 @@ class PopulationSweep:
             if rkey < 0:
                 continue
             doc = self.trials.pop(rkey, None)
-            params = self.key_params.pop(rkey, None)
-            pkey = self.key_pkey.pop(rkey, None)
+            info = self.key_info.pop(rkey, None)
             if doc is None:
                 continue
+            params, pkey, point, budget = info
             if g[8] > 0:
                 self.broken += 1
                 self._set_status(doc, "broken")
@@ -431,14 +441,13 @@ class PopulationSweep:
             vl, va, tl = g[6], g[7], g[5]
             self._writer.put_update_spec(doc[0], (vl, va, tl, now, doc[1]), was="reserved")
             self.completed += 1
-            budget = int(self.task.budget(params))
             if self.trial_events:
                 self.events.emit("trial", id=doc[0], status="completed", objective=vl,
                                  budget=budget)
             self.history.append((time.time(), rkey, vl, budget, self._result_step))
             if vl < self.best[0]:
                 self.best = (vl, dict(params))
-            done_pts.append(tuple(params[k] for k in self._dim_names))
+            done_pts.append(point)
             done_res.append({"objective": vl, "constraint": [], "gradient": None})
             if budget < max_b:
                 self._index_ckpt(pkey, rank, rkey, budget, doc[0])
@@ -504,12 +513,20 @@ class PopulationSweep:
         stamp = datetime.datetime.utcnow()
         # 1) stored trials waiting for a worker (interrupted, lost, new: a resumed experiment)
         #    take free slots before the algorithm is asked for anything new
+        rows, vals = [], []
         while self._requeue and n > 0 and any(n_free):
             tid, point, was, sidecar = self._requeue.popleft()
-            self._place(point, tid, assign, free_by_rank, n_free, stamp, was=was, sidecar=sidecar)
+            self._place(point, tid, rows, vals, free_by_rank, n_free, stamp, was=was,
+                        sidecar=sidecar)
             n -= 1
-        if n <= 0:
-            return
+        try:
+            if n > 0:
+                self._fill_new(n, rows, vals, free_by_rank, n_free, stamp)
+        finally:
+            if rows:
+                assign[rows] = vals
+
+    def _fill_new(self, n, rows, vals, free_by_rank, n_free, stamp) -> None:
         if self.algorithm.is_done:
             if not self.trials:
                 self.done = True
@@ -518,17 +535,21 @@ class PopulationSweep:
         if not points and not self.trials:
             self.done = True
             return
+        left = sum(n_free)
+        registered = self._registered
         for point in points:
-            if not any(n_free):
+            if not left:
                 break
             tid = self._doc_id(point)
-            if tid in self._registered:
+            if tid in registered:
                 log.debug("duplicate point %s skipped", point)
                 continue
-            self._registered.add(tid)
-            self._place(point, tid, assign, free_by_rank, n_free, stamp)
+            registered.add(tid)
+            self._place(point, tid, rows, vals, free_by_rank, n_free, stamp)
+            left -= 1
 
-    def _place(self, point, tid, assign, free_by_rank, n_free, stamp, was=None, sidecar=None):
+    def _place(self, point, tid, rows, vals, free_by_rank, n_free, stamp, was=None,
+               sidecar=None):
         """Reserve trial ``tid`` (``point``) and assign it to a free slot.
 
         The slot is chosen next to the device state the trial continues from: its own sidecar
@@ -538,8 +559,7 @@ class PopulationSweep:
         -- or the sidecar file of such a checkpoint written by a stopped run.  New trials go to
         the least-loaded rank."""
         W = len(n_free)
-        keys = self._dim_names
-        params = dict(zip(keys, point))
+        params = dict(zip(self._dim_names, point))
         pkey = self._point_key(point, params)
         parent = None
         if self._tracks_lineage:
@@ -556,7 +576,7 @@ class PopulationSweep:
             rank = owner[0]
             action, resume, src = RESUME, owner[1], owner[0]
         else:
-            rank = max(range(W), key=n_free.__getitem__)
+            rank = max(range(W), key=n_free.__getitem__) if W > 1 else 0
             side = self._sidecar_index.get(ckey)
             if owner is not None:   # C4: the owner sends the checkpoint to that rank (P2P)
                 action, resume, src = RESUME, owner[1], owner[0]
@@ -575,14 +595,23 @@ class PopulationSweep:
         key = self.next_key
         self.next_key += 1
         self.trials[key] = [tid, stamp]      # [trial id, last heartbeat]
-        self.key_params[key] = params
-        self.key_pkey[key] = pkey
-        cfg = self.task.member_config(params, self.task.seed_of(pkey))
-        assign[row] = (action, key, cfg.width, cfg.lr, cfg.momentum, cfg.weight_decay,
-                       cfg.dropout, cfg.seed, self.task.budget(params), resume, src)
+        budget = int(self.task.budget(params))
+        self.key_info[key] = (params, pkey, point, budget)
+        row_fn = getattr(self.task, "member_row", None)
+        seed = self.task.seed_of(pkey)
+        if row_fn is not None:
+            hp = row_fn(params, seed)
+        else:
+            cfg = self.task.member_config(params, seed)
+            hp = (cfg.width, cfg.lr, cfg.momentum, cfg.weight_decay, cfg.dropout, cfg.seed)
+        rows.append(row)
+        vals.append((action, key) + tuple(hp) + (budget, resume, src))
 
     def _point_key(self, point, params=None) -> str:
-        """``task.key(params)`` of a suggested point (python scalars, space order)."""
+        """Identity of a suggested point's configuration regardless of its fidelity (python
+        scalars, space order): ASHA's own id when the algorithm is ASHA, else ``task.key``."""
+        if self._algo_id is not None:
+            return self._algo_id(point)
         if self._pkey_tmpl is None:
             return self.task.key(params if params is not None
                                  else dict(zip(self._dim_names, point)))

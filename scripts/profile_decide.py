@@ -100,6 +100,8 @@ def main(n_syncs=40, P=256, world=1, profile=False):
     sw.close()
     print(f"writer {type(sw._writer).__name__ if sw._writer else ''}: final flush "
           f"{1e3 * t_flush:.1f} ms")
+    print("phases ms/sync:", {k: round(1e3 * v / n_syncs, 2) for k, v in sw.timers.items()
+                              if k.startswith("decide")})
     print(f"decide: {1e3 * t_total / n_syncs:.2f} ms/sync, writes {1e3 * t_rel / n_syncs:.2f} ms/sync, "
           f"{n_done / n_syncs:.1f} completions/sync")
     if prof:
