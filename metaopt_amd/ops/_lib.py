@@ -79,6 +79,17 @@ def get_lib(build_if_missing: bool = True):
         if not path.exists():
             raise KernelLibraryError(f"HIP kernel library not found at {path}; run "
                                      "`python -m metaopt_amd.ops.build`")
+        if not override and _build.built_digest() != _build.source_digest():
+            if build_if_missing:
+                try:
+                    _build.build()
+                except Exception as exc:  # pragma: no cover - hosts without hipcc
+                    raise KernelLibraryError(
+                        f"{path} was built from other sources and cannot be rebuilt: {exc}"
+                    ) from exc
+            if _build.built_digest() != _build.source_digest():
+                raise KernelLibraryError(f"{path} was built from other kernel sources than "
+                                         "the ones in this tree; rebuild it")
         try:
             lib = ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL)
         except OSError as exc:

@@ -7,11 +7,18 @@ cache: the ``.so`` lives in the source tree and travels with the repository snap
 
 Each ``csrc/*.hip`` file is compiled to its own object (incremental: only stale objects rebuild) and
 the objects are linked once.  ``python -m metaopt_amd.ops.build [--force]`` rebuilds by hand.
+
+Provenance: the link also writes ``libmopt_kernels.so.sha256``, the digest of every source,
+header, flag and the target arch the library was built from.  ``build()`` recompiles everything
+when the digest of the current tree differs (modification times do not survive a copy of the
+tree), and the loader (:mod:`._lib`) refuses a library whose digest does not match the sources
+next to it -- a stale ``.so`` shipped with a snapshot fails loudly instead of running old code.
 """
 from __future__ import annotations
 
 import argparse
 import concurrent.futures as cf
+import hashlib
 import os
 import shutil
 import subprocess
@@ -53,6 +60,25 @@ def _headers():
     return sorted(CSRC.glob("*.h"))
 
 
+def digest_path() -> Path:
+    return OUT_DIR / (LIB_NAME + ".sha256")
+
+
+def source_digest(extra_flags=None) -> str:
+    """sha256 of the kernel sources, headers, compiler flags and target arch."""
+    h = hashlib.sha256()
+    h.update(repr((ARCH, COMMON_FLAGS, list(extra_flags or []))).encode())
+    for f in sorted(_sources() + _headers()):
+        h.update(f.name.encode())
+        h.update(f.read_bytes())
+    return h.hexdigest()
+
+
+def built_digest() -> str:
+    p = digest_path()
+    return p.read_text().strip() if p.exists() else ""
+
+
 def _needs(obj: Path, deps) -> bool:
     if not obj.exists():
         return True
@@ -71,6 +97,9 @@ def build(force: bool = False, verbose: bool = False, extra_flags=None) -> Path:
     """Compile every ``csrc/*.hip`` for gfx950 and link ``libmopt_kernels.so``; returns its path."""
     hipcc = hipcc_path()
     OUT_DIR.mkdir(parents=True, exist_ok=True)
+    digest = source_digest(extra_flags)
+    if not force and (built_digest() != digest or not lib_path().exists()):
+        force = True                  # other sources/flags than the library's: rebuild all
     obj_dir = OUT_DIR / "obj"
     obj_dir.mkdir(exist_ok=True)
     extra = list(extra_flags or [])
@@ -98,6 +127,7 @@ def build(force: bool = False, verbose: bool = False, extra_flags=None) -> Path:
         if proc.returncode != 0:
             raise RuntimeError(f"link failed:\n{proc.stderr}")
         os.replace(tmp, lib)
+        digest_path().write_text(digest + "\n")
         if verbose:
             print(f"[mopt build] linked {lib}")
     return lib

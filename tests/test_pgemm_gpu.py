@@ -72,3 +72,16 @@ def test_pbmm_autograd_and_grad_out():
         err = (got.float() - ref).abs().max().item()
         assert err <= 1e-2 * ref.abs().max().item(), err
     assert w.grad is buf           # written in place, never re-accumulated by autograd
+
+
+@pytest.mark.parametrize("K,N", [(768, 2304), (768, 4096), (2048, 768), (768, 32000)])
+def test_library_nn_forward_lm_shapes(K, N):
+    """Regression guard of the dispatch in ops/gemm.py: the wide NN forwards that go to the
+    library (``nn_forward``, N >= LIBRARY_NN_MIN_N) are right on the installed stack for the
+    LM's projection shapes (scripts/check_bmm.py found its *transposed* batched GEMM wrong)."""
+    from metaopt_amd.ops.gemm import nn_forward
+    P, M = 2, 1024
+    g = torch.Generator(device=DEV).manual_seed(K + N)
+    x = (torch.randn(P, M, K, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
+    w = (torch.randn(P, K, N, device=DEV, generator=g) * 0.02).to(torch.bfloat16)
+    _check(nn_forward(x, w), x, w)
