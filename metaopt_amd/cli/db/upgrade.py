@@ -1,6 +1,7 @@
 """``mopt db upgrade``: migrate an old database in place (reference: ``cli/db/upgrade.py:56-183``).
 
-Drops the deprecated ``(name, metadata.user)`` indexes, adds ``version`` (default 1) and derives
+Drops the deprecated ``(name, metadata.user)`` indexes, converts a PickledDB file written in an
+older on-disk format to the current one, adds ``version`` (default 1) and derives
 ``metadata.parser``/``metadata.priors`` from ``user_args`` for old experiment documents.
 """
 from __future__ import annotations
@@ -27,6 +28,24 @@ def update_indexes(database):
     for idx in DEPRECATED_INDEXES:
         if idx in info:
             database.drop_index("experiments", idx)
+
+
+def upgrade_db_specifics(database):
+    """Backend-specific steps: deprecated indexes everywhere, the on-disk format of a PickledDB
+    file, MongoDB's index set (re-created by the storage setup that follows)."""
+    from ...storage.database import MongoDB, PickledDB
+    print("Updating indexes...")
+    update_indexes(database)
+    if isinstance(database, PickledDB):
+        print("Updating pickleddb scheme...")
+        n = database.upgrade_format()
+        print(f"  {n} collection(s) converted to format 2")
+    elif isinstance(database, MongoDB):
+        print("Updating mongodb scheme...")
+        for col in ("experiments", "trials"):
+            for name in list(database.index_information(col)):
+                if name in DEPRECATED_INDEXES:
+                    database.drop_index(col, name)
 
 
 def upgrade_documents(storage):
@@ -61,8 +80,7 @@ def main(args):
         from ...storage.database import create_database
         of_type = db.pop("type")
         storage = DocumentStorage(create_database(of_type.lower(), **db), setup=False)
-    print("Updating indexes...")
-    update_indexes(storage.database)
+    upgrade_db_specifics(storage.database)
     print("Updating documents...")
     upgrade_documents(storage)
     storage._setup_db()

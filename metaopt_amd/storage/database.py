@@ -392,6 +392,34 @@ class _Collection:
             self.hash_index[fields[0]] = hidx
         return name
 
+    # -- on-disk format (PickledDB pickles whole collections) ------------------------------------
+    FORMAT = 2
+
+    def __getstate__(self):
+        return {"format": self.FORMAT, "docs": self.docs, "indexes": self.indexes,
+                "hash_index": self.hash_index, "next_id": self._next_id}
+
+    def __setstate__(self, state):
+        """Load any layout this backend ever wrote.  Format 2 is stored as built (a load costs
+        one unpickle, no re-indexing).  Anything else -- the first release's bare ``__dict__``,
+        indexes keyed by their field tuple (the index signature the reference changed in
+        v0.1.6) or missing hash indexes -- is re-indexed from the documents and flagged
+        ``migrated`` so ``mopt db upgrade`` rewrites it."""
+        self.docs = state["docs"]
+        self._next_id = state.get("next_id", state.get("_next_id", 1))
+        self.migrated = state.get("format") != self.FORMAT
+        if not self.migrated:
+            self.indexes = state["indexes"]
+            self.hash_index = state["hash_index"]
+            return
+        self.indexes, self.hash_index = {}, {}
+        for name, spec in state.get("indexes", {}).items():
+            fields = tuple(spec[0]) if isinstance(name, str) else tuple(name)
+            unique = bool(spec[1]) if isinstance(spec, tuple) and len(spec) > 1 else True
+            self.create_index([(f, AbstractDB.ASCENDING) for f in fields], unique=unique)
+        if "_id_" not in self.indexes:
+            self.create_index("_id", unique=True)
+
     def drop_index(self, name):
         fields, _, _ = self.indexes.pop(name)
         if len(fields) == 1 and not any(f == fields for f, _, _ in self.indexes.values()):
@@ -652,7 +680,17 @@ def default_pickled_path() -> str:
 
 @DATABASES.register("pickleddb")
 class PickledDB(AbstractDB):
-    """An :class:`EphemeralDB` pickled to ``host`` (a file path), every op under a file lock."""
+    """An :class:`EphemeralDB` pickled to ``host`` (a file path), every op under a file lock.
+
+    Collections pickle as format 2 (documents + index definitions; indexes rebuilt on load);
+    older files load through ``_Collection.__setstate__`` and are rewritten in the current
+    format by the next write or by :meth:`upgrade_format` (``mopt db upgrade``)."""
+
+    def upgrade_format(self) -> int:
+        """Rewrite the file in the current format; returns how many collections were in an
+        older one."""
+        with self.locked_database() as db:
+            return sum(1 for col in (db._db or {}).values() if getattr(col, "migrated", False))
 
     LOCK_TIMEOUT = 60
 
@@ -811,6 +849,30 @@ class MongoDB(AbstractDB):
         with self._errors():
             self._db[collection_name].drop_index(name)
 
+    @staticmethod
+    def _query(query):
+        """Queries as the in-memory backends read them: a nested plain dict matches fields of a
+        sub-document (``{'meta': {'user': 'u'}}`` == ``{'meta.user': 'u'}``) instead of
+        MongoDB's whole-embedded-document equality, so every backend answers alike."""
+        if not query:
+            return {}
+        out = {}
+        for key, op, val in _flatten_query(query):
+            if op == "$eq":
+                out[key] = val
+            else:
+                out.setdefault(key, {})[op] = val
+        return out
+
+    @staticmethod
+    def _selection(selection):
+        if selection:
+            sel = {k: v for k, v in selection.items() if k != "_id"}
+            if len(set(bool(v) for v in sel.values())) > 1:
+                raise ValueError("Cannot mix selection with 1 and 0s except for _id: "
+                                 f"{selection}")
+        return selection
+
     def write(self, collection_name, data, query=None):
         col = self._db[collection_name]
         with self._errors():
@@ -819,27 +881,28 @@ class MongoDB(AbstractDB):
                 res = col.insert_many(docs)
                 return len(res.inserted_ids)
             update = data if any(k.startswith("$") for k in data) else {"$set": data}
-            return col.update_many(query, update).modified_count
+            return col.update_many(self._query(query), update).modified_count
 
     def read(self, collection_name, query=None, selection=None):
+        selection = self._selection(selection)
         with self._errors():
-            return list(self._db[collection_name].find(query or {}, selection))
+            return list(self._db[collection_name].find(self._query(query), selection))
 
     def read_and_write(self, collection_name, query, data, selection=None):
         import pymongo
         update = data if any(k.startswith("$") for k in data) else {"$set": data}
         with self._errors():
             return self._db[collection_name].find_one_and_update(
-                query, update, projection=selection,
+                self._query(query), update, projection=self._selection(selection),
                 return_document=pymongo.ReturnDocument.AFTER)
 
     def count(self, collection_name, query=None):
         with self._errors():
-            return self._db[collection_name].count_documents(query or {})
+            return self._db[collection_name].count_documents(self._query(query))
 
     def remove(self, collection_name, query):
         with self._errors():
-            return self._db[collection_name].delete_many(query).deleted_count
+            return self._db[collection_name].delete_many(self._query(query)).deleted_count
 
 
 def create_database(of_type: str = "ephemeraldb", **config) -> AbstractDB:

@@ -12,10 +12,15 @@ from metaopt_amd.storage.database import (DuplicateKeyError, EphemeralDB, Pickle
 from metaopt_amd.storage.protocol import DocumentStorage, FailedUpdate
 
 
-@pytest.fixture(params=["ephemeral", "pickled"])
-def db(request, tmp_path):
+@pytest.fixture(params=["ephemeral", "pickled", "mongodb"])
+def db(request, tmp_path, monkeypatch):
     if request.param == "ephemeral":
         return EphemeralDB()
+    if request.param == "mongodb":       # the same contract through a stand-in pymongo
+        import fake_pymongo
+        fake_pymongo.install(monkeypatch)
+        from metaopt_amd.storage.database import MongoDB
+        return MongoDB(host="mongodb://user:pass@localhost/mopt_test")
     return PickledDB(host=str(tmp_path / "db.pkl"))
 
 
@@ -119,8 +124,14 @@ class _Exp:
         self._id = _id
 
 
-@pytest.fixture
-def storage():
+@pytest.fixture(params=["ephemeral", "mongodb"])
+def storage(request, monkeypatch):
+    if request.param == "mongodb":
+        import fake_pymongo
+        fake_pymongo.install(monkeypatch)
+        from metaopt_amd.storage.database import MongoDB
+        return DocumentStorage(MongoDB(host="mongodb://user:pass@localhost/mopt_test"),
+                               heartbeat=120)
     return DocumentStorage(EphemeralDB(), heartbeat=120)
 
 
@@ -216,3 +227,57 @@ def test_writer_process_mirrors_ephemeral_db():
     assert len(docs) == 301 and docs["old"]["status"] == "reserved"
     assert docs["t3"]["status"] == "completed" and docs["t3"]["results"][0]["value"] == 0.5
     assert docs["t5"]["params"][0] == {"name": "/x", "type": "real", "value": 5.0}
+
+
+def test_mongodb_uri_and_connection_errors(monkeypatch):
+    """URI parsing (user, password, database, port) and server errors surfacing as
+    DatabaseError (reference: src/orion/core/io/database/mongodb.py:30-86,272-295)."""
+    import fake_pymongo
+    fake_pymongo.install(monkeypatch)
+    from metaopt_amd.storage.database import DatabaseError, MongoDB
+    db = MongoDB(host="mongodb://alice:s3cret@localhost:27018/studies")
+    assert (db.username, db.password, db.name, db.port) == ("alice", "s3cret", "studies", 27018)
+    with pytest.raises(DatabaseError):
+        MongoDB(host="mongodb://unreachable:1/x")
+    with pytest.raises(DatabaseError):
+        db.drop_index("trials", "no_such_index")
+
+
+def test_pickleddb_older_format_is_upgraded(tmp_path, monkeypatch, capsys):
+    """A PickledDB file in the first release's layout (indexes keyed by their field tuple, no
+    hash indexes) loads, and ``mopt db upgrade`` rewrites it in the current format with the
+    deprecated (name, metadata.user) index dropped and the unique indexes still enforced."""
+    import pickle
+    from metaopt_amd import cli
+    from metaopt_amd.storage import database as dbm
+    from metaopt_amd.storage import protocol
+    path = tmp_path / "old.pkl"
+    eph = EphemeralDB()
+    eph.write("experiments", {"name": "e", "version": 1,
+                              "metadata": {"user": "u", "user_args": ["-x~uniform(0, 1)"]}})
+    eph.ensure_index("experiments", [("name", 1), ("metadata.user", 1)], unique=True)
+
+    def legacy_state(col):          # the old layout: field-tuple keys, value sets, no hashes
+        return {"docs": col.docs, "_next_id": col._next_id,
+                "indexes": {f: (f, u, v) for _, (f, u, v) in col.indexes.items()}}
+    monkeypatch.setattr(dbm._Collection, "__getstate__", legacy_state)
+    path.write_bytes(pickle.dumps(eph))
+    monkeypatch.undo()
+    old = PickledDB(host=str(path))
+    assert old.read("experiments", {"name": "e"})[0]["version"] == 1
+    assert "name_1_metadata.user_1" in old.index_information("experiments")
+    monkeypatch.setenv("MOPT_DB_TYPE", "pickleddb")
+    monkeypatch.setenv("MOPT_DB_ADDRESS", str(path))
+    monkeypatch.setattr(protocol, "_STORAGE", None)
+    assert cli.main(["db", "upgrade", "-f"]) == 0
+    out = capsys.readouterr().out
+    assert "Updating pickleddb scheme" in out and "converted to format 2" in out
+    raw = pickle.loads(path.read_bytes())
+    assert all(col.__getstate__()["format"] == 2 and not col.migrated
+               for col in raw._db.values())
+    new = PickledDB(host=str(path))
+    assert "name_1_metadata.user_1" not in new.index_information("experiments")
+    exp = new.read("experiments", {"name": "e"})[0]
+    assert exp["metadata"]["priors"] == {"/x": "uniform(0, 1)"}
+    with pytest.raises(DuplicateKeyError):
+        new.write("experiments", {"_id": exp["_id"], "name": "other"})
