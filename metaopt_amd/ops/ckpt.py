@@ -17,8 +17,21 @@ import torch
 from . import _lib
 
 DESC_DTYPE = np.dtype([("src", "<u8"), ("dst", "<u8"), ("dst16", "<u8"), ("n", "<i8"),
-                       ("src16", "<u8"), ("pad", "<i8")])
-assert DESC_DTYPE.itemsize == 48
+                       ("src16", "<u8"), ("src_lo", "<u8"), ("dst_lo", "<u8"), ("pad", "<i8")])
+assert DESC_DTYPE.itemsize == 64
+
+
+class Split:
+    """A split f32 master (``hi`` bf16 working copy + ``lo`` int16 residual, see
+    ``csrc/common.h``) as a multi_copy source or destination."""
+
+    __slots__ = ("hi", "lo")
+
+    def __init__(self, hi: torch.Tensor, lo: torch.Tensor):
+        self.hi, self.lo = hi, lo
+
+    def numel(self):
+        return self.hi.numel()
 CHUNK_DTYPE = np.dtype([("desc", "<i4"), ("pad", "<i4"), ("start", "<i8")])
 CHUNK = 4096
 
@@ -32,12 +45,20 @@ def multi_copy(items: Iterable[Tuple[torch.Tensor, torch.Tensor, Optional[torch.
     items = list(items)
     if not items:
         return
-    dev = items[0][0].device
+    first = items[0][0]
+    dev = (first.hi if isinstance(first, Split) else first).device
     if dev.type != "cuda":
+        from .reference import join_f32, split_f32
         for src, dst, dst16 in items:
+            if isinstance(src, Split):
+                src = join_f32(src.hi, src.lo)
             if dst is not None:
                 dst.copy_(src)
-            if dst16 is not None:
+            if isinstance(dst16, Split):
+                hi, lo = split_f32(src.float())
+                dst16.hi.copy_(hi)
+                dst16.lo.copy_(lo)
+            elif dst16 is not None:
                 dst16.copy_(src.to(dst16.dtype))
         return
     descs = np.zeros(len(items), dtype=DESC_DTYPE)
@@ -48,15 +69,29 @@ def multi_copy(items: Iterable[Tuple[torch.Tensor, torch.Tensor, Optional[torch.
             raise ValueError("multi_copy: size mismatch")
         if dst is None and dst16 is None:
             raise ValueError("multi_copy: no destination")
-        if n % 4 or not src.is_contiguous() or (dst is not None and not dst.is_contiguous()):
+        views = [v for v in (src, dst, dst16) if v is not None]
+        flat = [t for v in views for t in ((v.hi, v.lo) if isinstance(v, Split) else (v,))]
+        if n % 4 or not all(t.is_contiguous() for t in flat):
             raise ValueError("multi_copy: views must be contiguous with a multiple of 4 elements")
-        if src.dtype not in (torch.float32, torch.bfloat16) or \
-                (dst is not None and dst.dtype != torch.float32) or \
-                (dst16 is not None and dst16.dtype != torch.bfloat16):
-            raise TypeError("multi_copy moves f32/bf16 sources into f32/bf16 destinations")
-        s16 = src.dtype == torch.bfloat16
-        descs[i] = (0 if s16 else src.data_ptr(), 0 if dst is None else dst.data_ptr(),
-                    0 if dst16 is None else dst16.data_ptr(), n, src.data_ptr() if s16 else 0, 0)
+        if isinstance(src, Split):
+            s32, s16, slo = 0, src.hi.data_ptr(), src.lo.data_ptr()
+        elif src.dtype == torch.bfloat16:
+            s32, s16, slo = 0, src.data_ptr(), 0
+        elif src.dtype == torch.float32:
+            s32, s16, slo = src.data_ptr(), 0, 0
+        else:
+            raise TypeError("multi_copy: source must be f32, bf16 or a split master")
+        if dst is not None and dst.dtype != torch.float32:
+            raise TypeError("multi_copy: dst must be f32")
+        if isinstance(dst16, Split):
+            d16, dlo = dst16.hi.data_ptr(), dst16.lo.data_ptr()
+        elif dst16 is not None:
+            if dst16.dtype != torch.bfloat16:
+                raise TypeError("multi_copy: dst16 must be bf16")
+            d16, dlo = dst16.data_ptr(), 0
+        else:
+            d16, dlo = 0, 0
+        descs[i] = (s32, 0 if dst is None else dst.data_ptr(), d16, n, s16, slo, dlo, 0)
         counts.append((n + CHUNK - 1) // CHUNK)
     counts = np.array(counts, dtype=np.int64)
     chunks = np.zeros(int(counts.sum()), dtype=CHUNK_DTYPE)

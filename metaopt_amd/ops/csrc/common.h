@@ -35,6 +35,38 @@ __device__ __forceinline__ uint32_t pack2bf(float a, float b) {
   return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
 }
 
+// Split f32 master weights: hi = the bf16 working copy (round to nearest, ties toward the
+// smaller magnitude), lo = a 16-bit residual such that (hi << 16) + lo - 0x7FFF is the f32 bit
+// pattern again -- exact reconstruction of the master from 4 bytes, of which the forward reads
+// only the 2 of hi.  Mirrored by metaopt_amd/ops/reference.py (split_f32 / join_f32).
+__device__ __forceinline__ float join_hilo(uint32_t hi, uint32_t lo) {
+  return __uint_as_float((hi << 16) + lo - 0x7FFFu);
+}
+
+__device__ __forceinline__ uint32_t split_hi(uint32_t u) { return (u + 0x7FFFu) >> 16; }
+
+__device__ __forceinline__ uint32_t split_lo(uint32_t u, uint32_t hi) {
+  return (u - (hi << 16) + 0x7FFFu) & 0xFFFFu;
+}
+
+// 4 (hi, lo) pairs (8 + 8 bytes) <-> 4 f32
+__device__ __forceinline__ f32x4 join4(uint2 hi, uint2 lo) {
+  return f32x4{join_hilo(hi.x & 0xFFFFu, lo.x & 0xFFFFu), join_hilo(hi.x >> 16, lo.x >> 16),
+               join_hilo(hi.y & 0xFFFFu, lo.y & 0xFFFFu), join_hilo(hi.y >> 16, lo.y >> 16)};
+}
+
+__device__ __forceinline__ void split4(const f32x4& v, uint2& hi, uint2& lo) {
+  uint32_t h[4], l[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const uint32_t u = __float_as_uint(v[r]);
+    h[r] = split_hi(u) & 0xFFFFu;
+    l[r] = split_lo(u, h[r]);
+  }
+  hi = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+  lo = make_uint2(l[0] | (l[1] << 16), l[2] | (l[3] << 16));
+}
+
 // 4 packed bf16 <-> 4 f32 (bf16 optimizer state moved 8 bytes per lane)
 __device__ __forceinline__ f32x4 bf4_to_f32(uint2 v) {
   return f32x4{__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xFFFF0000u),

@@ -4,7 +4,8 @@
 // A descriptor moves n values from an f32 (src) or bf16 (src16) source to an f32 destination
 // (dst) and/or the bf16 image of the values (dst16): restoring a member's bf16 working weights in
 // the same pass that restores its f32 master copy, and widening / narrowing a bf16 momentum
-// buffer into / out of the f32 checkpoint pool (exact: the values are bf16).
+// buffer into / out of the f32 checkpoint pool (exact: the values are bf16), and joining /
+// splitting split master weights (hi = bf16 working copy, lo = residual; common.h).
 // Work is split into 4096-element chunks listed on the host, so a launch needs no per-descriptor
 // grid sizing and stays balanced however ragged the member sizes are.
 #include "common.h"
@@ -13,12 +14,14 @@ using namespace mopt;
 
 extern "C" {
 
-struct CopyDesc {       // 48 bytes, mirrored by metaopt_amd/ops/ckpt.py
+struct CopyDesc {       // 64 bytes, mirrored by metaopt_amd/ops/ckpt.py
   const float* src;     // f32 source, or nullptr when src16 is set
   float* dst;           // nullptr: no f32 copy
-  bf16_t* dst16;        // nullptr: no bf16 image
+  bf16_t* dst16;        // nullptr: no bf16 image (with dst_lo: the hi half of a split master)
   int64_t n;            // multiple of 4
-  const bf16_t* src16;  // bf16 source (widened exactly)
+  const bf16_t* src16;  // bf16 source (widened exactly; with src_lo: hi half of a split master)
+  const bf16_t* src_lo; // lo half of a split-master source
+  bf16_t* dst_lo;       // lo half of a split-master destination
   int64_t pad;
 };
 
@@ -40,10 +43,20 @@ __global__ __launch_bounds__(256) void multi_copy_kernel(const CopyDesc* __restr
   const CopyDesc d = descs[c.desc];
   const int64_t end = min((int64_t)kChunk, d.n - c.start);
   for (int64_t i = 4 * threadIdx.x; i < end; i += 4 * 256) {
-    const f32x4 v = d.src16 ? bf4_to_f32(*(const uint2*)(d.src16 + c.start + i))
-                            : *(const f32x4*)(d.src + c.start + i);
-    if (d.dst) *(f32x4*)(d.dst + c.start + i) = v;
-    if (d.dst16) *(uint2*)(d.dst16 + c.start + i) = f32_to_bf4(v);
+    const int64_t e = c.start + i;
+    f32x4 v;
+    if (d.src_lo) v = join4(*(const uint2*)(d.src16 + e), *(const uint2*)(d.src_lo + e));
+    else if (d.src16) v = bf4_to_f32(*(const uint2*)(d.src16 + e));
+    else v = *(const f32x4*)(d.src + e);
+    if (d.dst) *(f32x4*)(d.dst + e) = v;
+    if (d.dst_lo) {
+      uint2 hi, lo;
+      split4(v, hi, lo);
+      *(uint2*)(d.dst16 + e) = hi;
+      *(uint2*)(d.dst_lo + e) = lo;
+    } else if (d.dst16) {
+      *(uint2*)(d.dst16 + e) = f32_to_bf4(v);
+    }
   }
 }
 

@@ -170,7 +170,7 @@ __device__ __forceinline__ void fwd_gemm(const bf16_t* __restrict__ X, const bf1
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void mlp_fwd_kernel(const MlpTL* __restrict__ tls,
                                                       const int2* __restrict__ work, int n_work,
                                                       const bf16_t* __restrict__ xb,
-                                                      const float* __restrict__ p32,
+                                                      const bf16_t* __restrict__ plo,
                                                       const bf16_t* __restrict__ p16,
                                                       bf16_t* __restrict__ act,
                                                       const TrialHP* __restrict__ hp,
@@ -188,7 +188,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void m
   fwd_gemm(X, W, K, As, Bs, acc);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, g = lane >> 4;
-  const float* bias = p32 + tl.b_off + n0;
+  const bf16_t* bias_hi = p16 + tl.b_off + n0;
+  const bf16_t* bias_lo = plo + tl.b_off + n0;
   const TrialHP h = hp[tl.trial];
   const bool drop = (flags & kDropout) && h.drop > 0.f;
   const float inv_keep = drop ? 1.f / (1.f - h.drop) : 1.f;
@@ -199,7 +200,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void m
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int col = j * 16 + li;
-    const float bj = bias[col];
+    const float bj = join_hilo(bias_hi[col], bias_lo[col]);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -229,7 +230,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void m
 __global__ __launch_bounds__(256) void mlp_fwd_ce_kernel(const MlpTL* __restrict__ tls,
                                                          const int2* __restrict__ work, int n_work,
                                                          const bf16_t* __restrict__ xb,
-                                                         const float* __restrict__ p32,
+                                                         const bf16_t* __restrict__ plo,
                                                          const bf16_t* __restrict__ p16,
                                                          const int32_t* __restrict__ labels,
                                                          bf16_t* __restrict__ grad,
@@ -254,11 +255,12 @@ __global__ __launch_bounds__(256) void mlp_fwd_ce_kernel(const MlpTL* __restrict
   fwd_gemm(X, W, K, As, Bs, acc);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, g = lane >> 4;
-  const float* bias = p32 + tl.b_off;
+  const bf16_t* bias_hi = p16 + tl.b_off;
+  const bf16_t* bias_lo = plo + tl.b_off;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int col = j * 16 + li;
-    const float bj = bias[col];
+    const float bj = join_hilo(bias_hi[col], bias_lo[col]);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -329,7 +331,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                                                           const int2* __restrict__ work, int n_work,
                                                           const bf16_t* __restrict__ xb,
                                                           bf16_t* __restrict__ grad,
-                                                          float* __restrict__ p32,
+                                                          bf16_t* __restrict__ plo,
                                                           bf16_t* __restrict__ p16,
                                                           float* __restrict__ m32,
                                                           float* __restrict__ v32,
@@ -347,7 +349,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int K = tl.K, N = tl.N, k0 = wi.y * BK;
   const bf16_t* X = xb + tl.x_off;
   const bf16_t* dZ = grad + tl.y_off;
-  float* W32 = p32 + tl.w_off;
+  bf16_t* WLO = plo + tl.w_off;                      // master = (hi, lo) pairs, see common.h
   float* M32 = m32 + tl.w_off;                       // kSGD / kAdamW
   bf16_t* M16 = (bf16_t*)m32 + tl.w_off;             // kSGD16
   float* V32 = v32 + tl.w_off;  // AdamW only
@@ -393,7 +395,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // every wave-instruction moves 4 rows x 256 contiguous bytes of W/M (/V), full 128-B lines.
   const int wo = (tid >> 4) * K + k0 + 4 * (tid & 15);
   uint4 z0, z1, z2, z3;
-  f32x4 w0, w1, w2, w3, m0, m1, m2, m3, v0, v1, v2, v3;
+  f32x4 m0, m1, m2, m3, v0, v1, v2, v3;
+  uint2 wh0, wh1, wh2, wh3, wl0, wl1, wl2, wl3;       // master weights: hi (bf16) and lo halves
   uint2 h0, h1, h2, h3;                               // kSGD16 momentum (4 bf16 per lane)
 #define MOPT_BWD_LOAD(NC)                                                                        \
   {                                                                                              \
@@ -403,10 +406,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     z2 = *(const uint4*)(zc + zo2);                                                              \
     z3 = *(const uint4*)(zc + zo3);                                                              \
     const size_t ob = (size_t)(NC) * K + wo;                                                     \
-    w0 = *(const f32x4*)(W32 + ob);                                                              \
-    w1 = *(const f32x4*)(W32 + ob + 16 * K);                                                     \
-    w2 = *(const f32x4*)(W32 + ob + 32 * K);                                                     \
-    w3 = *(const f32x4*)(W32 + ob + 48 * K);                                                     \
+    wh0 = *(const uint2*)(W16 + ob);                                                             \
+    wh1 = *(const uint2*)(W16 + ob + 16 * K);                                                    \
+    wh2 = *(const uint2*)(W16 + ob + 32 * K);                                                    \
+    wh3 = *(const uint2*)(W16 + ob + 48 * K);                                                    \
+    wl0 = *(const uint2*)(WLO + ob);                                                             \
+    wl1 = *(const uint2*)(WLO + ob + 16 * K);                                                    \
+    wl2 = *(const uint2*)(WLO + ob + 32 * K);                                                    \
+    wl3 = *(const uint2*)(WLO + ob + 48 * K);                                                    \
     if (OPT == kSGD16) {                                                                         \
       h0 = *(const uint2*)(M16 + ob);                                                            \
       h1 = *(const uint2*)(M16 + ob + 16 * K);                                                   \
@@ -435,16 +442,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     if (OPT == kSGD16) {
       m0 = bf4_to_f32(h0); m1 = bf4_to_f32(h1); m2 = bf4_to_f32(h2); m3 = bf4_to_f32(h3);
     }
-    const f32x4 w[4] = {w0, w1, w2, w3}, m[4] = {m0, m1, m2, m3};
+    const f32x4 w[4] = {join4(wh0, wl0), join4(wh1, wl1), join4(wh2, wl2), join4(wh3, wl3)};
+    const f32x4 m[4] = {m0, m1, m2, m3};
     f32x4 v[4];
     if (OPT == kAdamW) {
       v[0] = v0; v[1] = v1; v[2] = v2; v[3] = v3;
     }
-    if (has_dx) {
+    if (has_dx) {   // the bf16 working copy (hi) is the dX operand, as in the forward
+      const uint2 wh[4] = {wh0, wh1, wh2, wh3};
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        *(uint2*)(Ws + (16 * i + (tid >> 4)) * LS + 4 * (tid & 15)) =
-            make_uint2(pack2bf(w[i][0], w[i][1]), pack2bf(w[i][2], w[i][3]));
+      for (int i = 0; i < 4; ++i) *(uint2*)(Ws + (16 * i + (tid >> 4)) * LS + 4 * (tid & 15)) = wh[i];
     }
     __syncthreads();
 
@@ -527,11 +534,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           wv[r] = wv[r] - c1 * mv[r] / (sqrtf(vv[r]) * c2 + h.eps);
         }
       }
-      *(f32x4*)(W32 + o) = wv;
+      uint2 nh, nl;
+      split4(wv, nh, nl);
+      *(uint2*)(W16 + o) = nh;
+      *(uint2*)(WLO + o) = nl;
       if (OPT == kSGD16) *(uint2*)(M16 + o) = f32_to_bf4(mv);
       else *(f32x4*)(M32 + o) = mv;
       if (OPT == kAdamW) *(f32x4*)(V32 + o) = vv;
-      *(uint2*)(W16 + o) = make_uint2(pack2bf(wv[0], wv[1]), pack2bf(wv[2], wv[3]));
     }
 
     // ---- bias: db[n] = sum_b dZ[b][n]; only the k-strip-0 workgroup owns the bias ----
@@ -543,10 +552,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       __syncthreads();
       if (tid < 64) {
         const float gb = red[tid] + red[64 + tid] + red[128 + tid] + red[192 + tid];
-        float* bp = p32 + tl.b_off + nc + tid;
+        bf16_t* bph = p16 + tl.b_off + nc + tid;
+        bf16_t* bpl = plo + tl.b_off + nc + tid;
         float* bm = m32 + tl.b_off + nc + tid;
         bf16_t* bm16 = (bf16_t*)m32 + tl.b_off + nc + tid;
-        float bw = *bp, mb = OPT == kSGD16 ? bf2f(*bm16) : *bm;
+        float bw = join_hilo(*bph, *bpl), mb = OPT == kSGD16 ? bf2f(*bm16) : *bm;
         if (OPT == kSGD || OPT == kSGD16) {
           mb = h.b1 * mb + gb;
           if (OPT == kSGD16) mb = bf2f(f2bf(mb));
@@ -559,7 +569,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           bw = bw - c1 * mb / (sqrtf(vb) * c2 + h.eps);
           *bv = vb;
         }
-        *bp = bw;
+        const uint32_t ub = __float_as_uint(bw), hb = split_hi(ub) & 0xFFFFu;
+        *bph = (bf16_t)hb;
+        *bpl = (bf16_t)split_lo(ub, hb);
         if (OPT == kSGD16) *bm16 = f2bf(mb);
         else *bm = mb;
       }
@@ -595,7 +607,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 // the same values), zero padding, the bf16 copy, and zeroed optimizer state.  Replaces ~10 small
 // framework launches per member.
 __global__ __launch_bounds__(256) void mlp_init_kernel(const InitDesc* __restrict__ descs,
-                                                       float* __restrict__ p32,
+                                                       bf16_t* __restrict__ plo,
                                                        bf16_t* __restrict__ p16,
                                                        float* __restrict__ m32,
                                                        float* __restrict__ v32, int flags) {
@@ -617,8 +629,9 @@ __global__ __launch_bounds__(256) void mlp_init_kernel(const InitDesc* __restric
       if (n < d.n_real) v = (2.f * rng_uniform(bkey, (uint32_t)n) - 1.f) * d.bound;
       o = d.b_off + n;
     }
-    p32[o] = v;
-    p16[o] = f2bf(v);
+    const uint32_t u = __float_as_uint(v), h = split_hi(u) & 0xFFFFu;
+    p16[o] = (bf16_t)h;
+    plo[o] = (bf16_t)split_lo(u, h);
     if (flags & 2) ((bf16_t*)m32)[o] = 0;   // bf16 momentum (kSGD16)
     else m32[o] = 0.f;
     if (flags & 1) v32[o] = 0.f;
@@ -632,60 +645,60 @@ __global__ __launch_bounds__(256) void mlp_init_kernel(const InitDesc* __restric
 // ------------------------------------------------------------------------------------------------
 extern "C" {
 
-int mopt_abi_version() { return 6; }
+int mopt_abi_version() { return 7; }
 
 // flags: 1 = zero the AdamW second moment, 2 = the momentum buffer is bf16
-int mopt_mlp_init(const void* descs, int n_desc, void* p32, void* p16, void* m32, void* v32,
+int mopt_mlp_init(const void* descs, int n_desc, void* plo, void* p16, void* m32, void* v32,
                   int flags, void* stream) {
   if (n_desc <= 0) return 0;
   hipLaunchKernelGGL(mlp_init_kernel, dim3(64, n_desc), dim3(256), 0, (hipStream_t)stream,
-                     (const InitDesc*)descs, (float*)p32, (bf16_t*)p16, (float*)m32, (float*)v32,
+                     (const InitDesc*)descs, (bf16_t*)plo, (bf16_t*)p16, (float*)m32, (float*)v32,
                      flags);
   return (int)hipGetLastError();
 }
 
 int mopt_mlp_fwd(const void* tls, const void* work, int n_work, int n_rowblocks, const void* xb,
-                 const void* p32, const void* p16, void* act, const void* hp, unsigned step,
+                 const void* plo, const void* p16, void* act, const void* hp, unsigned step,
                  int layer, int flags, void* stream) {
   if (n_work <= 0) return 0;
   hipLaunchKernelGGL(mlp_fwd_kernel, dim3(n_work, n_rowblocks), dim3(256), 0, (hipStream_t)stream,
                      (const MlpTL*)tls, (const int2*)work, n_work, (const bf16_t*)xb,
-                     (const float*)p32, (const bf16_t*)p16, (bf16_t*)act, (const TrialHP*)hp, step,
+                     (const bf16_t*)plo, (const bf16_t*)p16, (bf16_t*)act, (const TrialHP*)hp, step,
                      layer, flags);
   return (int)hipGetLastError();
 }
 
 int mopt_mlp_fwd_ce(const void* tls, const void* work, int n_work, int n_rowblocks, const void* xb,
-                    const void* p32, const void* p16, const void* labels, void* grad, void* loss,
+                    const void* plo, const void* p16, const void* labels, void* grad, void* loss,
                     void* correct, void* hp, float inv_b, int flags, void* stream) {
   if (n_work <= 0) return 0;
   if ((flags & kStoreStats) && n_rowblocks != 1) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(mlp_fwd_ce_kernel, dim3(n_work, n_rowblocks), dim3(256), 0,
                      (hipStream_t)stream, (const MlpTL*)tls, (const int2*)work, n_work,
-                     (const bf16_t*)xb, (const float*)p32, (const bf16_t*)p16,
+                     (const bf16_t*)xb, (const bf16_t*)plo, (const bf16_t*)p16,
                      (const int32_t*)labels, (bf16_t*)grad, (float*)loss, (float*)correct,
                      (TrialHP*)hp, inv_b, flags);
   return (int)hipGetLastError();
 }
 
 int mopt_mlp_bwd(const void* tls, const void* work, int n_work, const void* xb, void* grad,
-                 void* p32, void* p16, void* m32, void* v32, const void* hp, int opt, int flags,
+                 void* plo, void* p16, void* m32, void* v32, const void* hp, int opt, int flags,
                  void* stream) {
   if (n_work <= 0) return 0;
   if (opt == kAdamW) {
     hipLaunchKernelGGL(mlp_bwd_opt_kernel<kAdamW>, dim3(n_work), dim3(256), 0, (hipStream_t)stream,
                        (const MlpTL*)tls, (const int2*)work, n_work, (const bf16_t*)xb,
-                       (bf16_t*)grad, (float*)p32, (bf16_t*)p16, (float*)m32, (float*)v32,
+                       (bf16_t*)grad, (bf16_t*)plo, (bf16_t*)p16, (float*)m32, (float*)v32,
                        (const TrialHP*)hp, flags);
   } else if (opt == kSGD16) {
     hipLaunchKernelGGL(mlp_bwd_opt_kernel<kSGD16>, dim3(n_work), dim3(256), 0, (hipStream_t)stream,
                        (const MlpTL*)tls, (const int2*)work, n_work, (const bf16_t*)xb,
-                       (bf16_t*)grad, (float*)p32, (bf16_t*)p16, (float*)m32, (float*)v32,
+                       (bf16_t*)grad, (bf16_t*)plo, (bf16_t*)p16, (float*)m32, (float*)v32,
                        (const TrialHP*)hp, flags);
   } else {
     hipLaunchKernelGGL(mlp_bwd_opt_kernel<kSGD>, dim3(n_work), dim3(256), 0, (hipStream_t)stream,
                        (const MlpTL*)tls, (const int2*)work, n_work, (const bf16_t*)xb,
-                       (bf16_t*)grad, (float*)p32, (bf16_t*)p16, (float*)m32, (float*)v32,
+                       (bf16_t*)grad, (bf16_t*)plo, (bf16_t*)p16, (float*)m32, (float*)v32,
                        (const TrialHP*)hp, flags);
   }
   return (int)hipGetLastError();

@@ -2,8 +2,11 @@
 
 :class:`PopulationMLP` owns flat device buffers for ``capacity`` trial *slots*:
 
-* ``p32`` f32 master weights, ``p16`` their bf16 copy (forward operand), ``m32``/``v32`` optimizer
-  state -- every slot a fixed-size region sized for ``max_width`` (288 GB of HBM makes the
+* master weights: on the HIP backend ``p16`` (the bf16 working copy the forward reads) plus
+  ``plo``, a 16-bit residual that makes (``p16``, ``plo``) an exact f32 master in 4 bytes
+  (``csrc/common.h``); on the reference backend a plain f32 ``p32`` and its ``p16`` copy;
+  ``m32``/``v32`` optimizer state -- every slot a fixed-size region sized for ``max_width``
+  (288 GB of HBM makes the
   per-slot worst case cheap, and fixed regions make slot replacement, ASHA resume and PBT exploit
   plain region copies);
 * ``act``/``grad`` bf16 activations and their gradients ([rows][N_l] per slot and layer);
@@ -122,6 +125,17 @@ def _lpt_order(cost: np.ndarray, n_xcd: int = 8) -> np.ndarray:
     return np.lexsort((-cost, share))
 
 
+class _SplitBuffer:
+    """(hi, lo) split-master buffers sliced together (``buf[a:b]`` -> ckpt.Split)."""
+
+    def __init__(self, hi, lo):
+        self.hi, self.lo = hi, lo
+
+    def __getitem__(self, sl):
+        from .ckpt import Split
+        return Split(self.hi[sl], self.lo[sl])
+
+
 def device_busy(device):
     if torch.device(device).type != "cuda":
         return lambda: True
@@ -195,7 +209,10 @@ class PopulationMLP:
         self.act_row = sum(self.nmax)
         dev = self.device
         total = self.capacity * self.slot_params
-        self.p32 = torch.zeros(total, dtype=torch.float32, device=dev)
+        # HIP: split master (hi = p16, lo = plo; no separate f32 copy to write every step)
+        self.split = backend == "hip"
+        self.p32 = None if self.split else torch.zeros(total, dtype=torch.float32, device=dev)
+        self.plo = torch.zeros(total, dtype=torch.int16, device=dev) if self.split else None
         self.p16 = torch.zeros(total, dtype=torch.bfloat16, device=dev)
         self.m32 = torch.zeros(total, dtype=torch.bfloat16 if momentum_dtype == "bf16"
                                else torch.float32, device=dev)   # momentum / AdamW first moment
@@ -268,8 +285,9 @@ class PopulationMLP:
 
     def bytes_per_step(self, slot: int) -> int:
         """HBM bytes per step for parameters/state of ``slot`` (fwd bf16 + fused bwd/update)."""
-        per = 2 + (26 if self.optimizer == "adamw" else
-                   14 if self.momentum_dtype == "bf16" else 18)
+        w = 8 if self.split else 10      # split master r+w (4+4) vs f32 r+w + bf16 copy w
+        per = 2 + w + (16 if self.optimizer == "adamw" else
+                       4 if self.momentum_dtype == "bf16" else 8)
         return per * self.padded_params(slot)
 
     # ------------------------------------------------------------------ members
@@ -351,7 +369,7 @@ class PopulationMLP:
             from ._lib import check, stream_ptr
             from ._lib import upload_bytes
             d = upload_bytes(descs, self.device)
-            check(self._lib.mopt_mlp_init(d.data_ptr(), len(descs), self.p32.data_ptr(),
+            check(self._lib.mopt_mlp_init(d.data_ptr(), len(descs), self.plo.data_ptr(),
                                           self.p16.data_ptr(), self.m32.data_ptr(),
                                           self.v32.data_ptr(),
                                           int(self.optimizer == "adamw")
@@ -367,21 +385,43 @@ class PopulationMLP:
             for s in slots:
                 b = self.slot_base(s)
                 n = self.used_params(s)
-                self.p16[b:b + n] = self.p32[b:b + n].to(torch.bfloat16)
+                self.p16[b:b + n] = ref.split_f32(self.p32[b:b + n])[0]
 
     def layer_views(self, slot: int, buf: torch.Tensor = None):
         """[(W [N,K], b [N])] views of ``buf`` (default: f32 master) for the member in ``slot``."""
         self._run_pending_init()
-        buf = self.p32 if buf is None else buf
         self._join()
         cfg = self.members[slot]
         base = self.slot_base(slot)
+        if buf is None and self.split:     # a decoded copy of the slot's f32 master
+            buf, base = self.master(slot), 0
+        buf = self.p32 if buf is None else buf
         out = []
         for (k, n), (wo, bo) in zip(self.layer_dims(cfg.width), self.param_offsets(cfg.width)):
             out.append((buf[base + wo: base + wo + n * k].view(n, k), buf[base + bo: base + bo + n]))
         return out
 
     # ------------------------------------------------------------------ checkpoints (device)
+    def master(self, slot: int) -> torch.Tensor:
+        """The f32 master weights of ``slot``'s used region (a copy on the HIP backend)."""
+        self._run_pending_init()
+        self._join()
+        b, n = self.slot_base(slot), self.used_params(slot)
+        if self.split:
+            return ref.join_f32(self.p16[b:b + n], self.plo[b:b + n])
+        return self.p32[b:b + n]
+
+    def _set_master(self, b: int, values: torch.Tensor) -> None:
+        n = values.numel()
+        values = values.to(self.device, torch.float32)
+        if self.split:
+            hi, lo = ref.split_f32(values)
+            self.p16[b:b + n] = hi
+            self.plo[b:b + n] = lo
+        else:
+            self.p32[b:b + n] = values
+            self.p16[b:b + n] = ref.split_f32(values)[0]
+
     def used_params(self, slot: int) -> int:
         """Length of the prefix of the slot region the member actually uses."""
         return self.used_params_for(self.members[slot].width)
@@ -397,7 +437,8 @@ class PopulationMLP:
                               device=self.device)
 
     def _state_tensors(self):
-        return [self.p32, self.m32] + ([self.v32] if self.optimizer == "adamw" else [])
+        w = _SplitBuffer(self.p16, self.plo) if self.split else self.p32
+        return [w, self.m32] + ([self.v32] if self.optimizer == "adamw" else [])
 
     def save_states(self, pairs) -> list:
         """Checkpoint members: ``pairs`` = [(slot, pool index)]; returns per-member metadata."""
@@ -424,7 +465,9 @@ class PopulationMLP:
             n, idx = meta["n"], meta["ck"]
             b = self.slot_base(slot)
             for j, buf in enumerate(self._state_tensors()):
-                if buf.dtype == torch.bfloat16:   # bf16 momentum: narrowed back (exact)
+                if isinstance(buf, _SplitBuffer):  # f32 pool -> split master (hi, lo)
+                    items.append((self.ck[idx, j, :n], None, buf[b:b + n]))
+                elif buf.dtype == torch.bfloat16:   # bf16 momentum: narrowed back (exact)
                     items.append((self.ck[idx, j, :n], None, buf[b:b + n]))
                 else:
                     items.append((self.ck[idx, j, :n], buf[b:b + n],
@@ -480,7 +523,8 @@ class PopulationMLP:
         reg = slice(b, b + self.used_params(slot))
         mv = (lambda t: t.detach().cpu().clone()) if to_cpu else (lambda t: t.detach().clone())
         st = {"config": self.members[slot].to_dict(), "t": int(self.hp[slot]["t"]),
-              "p32": mv(self.p32[reg]), "m32": mv(self.m32[reg]), "optimizer": self.optimizer}
+              "p32": mv(self.master(slot)), "m32": mv(self.m32[reg]),
+              "optimizer": self.optimizer}
         if self.optimizer == "adamw":
             st["v32"] = mv(self.v32[reg])
         return st
@@ -493,11 +537,10 @@ class PopulationMLP:
         self._write_hp(slot, cfg, int(state["t"]))
         b = self.slot_base(slot)
         reg = slice(b, b + state["p32"].numel())
-        self.p32[reg].copy_(state["p32"])
+        self._set_master(b, state["p32"])
         self.m32[reg].copy_(state["m32"])
         if self.optimizer == "adamw":
             self.v32[reg].copy_(state["v32"])
-        self.p16[reg] = self.p32[reg].to(torch.bfloat16)
         self._dirty = True
 
     def copy_member(self, src: int, dst: int, **hp_changes) -> None:
@@ -506,7 +549,10 @@ class PopulationMLP:
         self._join()
         self._pending_init.discard(dst)
         rs, rd = self._region(src), self._region(dst)
-        self.p32[rd].copy_(self.p32[rs])
+        if self.split:
+            self.plo[rd].copy_(self.plo[rs])
+        else:
+            self.p32[rd].copy_(self.p32[rs])
         self.p16[rd].copy_(self.p16[rs])
         self.m32[rd].copy_(self.m32[rs])
         if self.optimizer == "adamw":
@@ -587,7 +633,7 @@ class PopulationMLP:
         if self.backend == "hip":
             tb = self._tables["train"]
             self._parts = self._partition(tb)
-            self._ptr = {"p32": self.p32.data_ptr(), "p16": self.p16.data_ptr(),
+            self._ptr = {"plo": self.plo.data_ptr(), "p16": self.p16.data_ptr(),
                          "m32": self.m32.data_ptr(), "v32": self.v32.data_ptr(),
                          "act": self.act.data_ptr(), "grad": self.grad.data_ptr(),
                          "hp": self.hp_dev.data_ptr(), "loss": self.loss.data_ptr(),
@@ -690,10 +736,10 @@ class PopulationMLP:
         act, tl = P["act"], P["tl"]
         for l in range(L - 1):
             check(lib.mopt_mlp_fwd(tl, part["fwd"][l], part["n_fwd"][l], rb, xp if l == 0 else act,
-                                   P["p32"], P["p16"], act, P["hp"], 1, l,
+                                   P["plo"], P["p16"], act, P["hp"], 1, l,
                                    FWD_RELU | (FWD_DROPOUT if drop else 0), stream), "mlp_fwd")
         check(lib.mopt_mlp_fwd_ce(tl, part["fwd"][L - 1], part["n_fwd"][L - 1], rb,
-                                  xp if L == 1 else act, P["p32"], P["p16"], yp,
+                                  xp if L == 1 else act, P["plo"], P["p16"], yp,
                                   P["grad"], P["loss"], P["correct"], P["hp"],
                                   1.0 / self.batch_size, ce_flags, stream), "mlp_fwd_ce")
         opt = 2 if self.momentum_dtype == "bf16" else OPTIMIZERS[self.optimizer]
@@ -702,7 +748,7 @@ class PopulationMLP:
             if l > 0:
                 flags |= BWD_HAS_DX | (BWD_IN_DROPOUT if drop else 0)
             check(lib.mopt_mlp_bwd(tl, part["bwd"][l], part["n_bwd"][l], xp if l == 0 else act,
-                                   P["grad"], P["p32"], P["p16"], P["m32"], P["v32"], P["hp"],
+                                   P["grad"], P["plo"], P["p16"], P["m32"], P["v32"], P["hp"],
                                    opt, flags, stream), "mlp_bwd")
 
     def _train_step_torch(self, x, y) -> None:
@@ -721,7 +767,7 @@ class PopulationMLP:
                 a = ref.hidden_fwd(a, w, b, cfg.dropout, cfg.seed, l, t, emulate_bf16=em)
                 acts.append(a)
             w, b = layers[-1]
-            wq = ref.bf16_round(w) if em else w
+            wq = ref.bf16_weight(w) if em else w
             logits = a @ wq.t() + b
             ls, cs, dz = ref.softmax_ce(logits, y, self.num_classes, 1.0 / self.batch_size, em)
             self.loss[s] = ls
@@ -733,7 +779,7 @@ class PopulationMLP:
                 dw = dz.t() @ a_in
                 db = dz.sum(0)
                 if l > 0:
-                    wq = ref.bf16_round(w) if em else w
+                    wq = ref.bf16_weight(w) if em else w
                     dx = dz @ wq
                     dz_prev = torch.where(a_in > 0, dx * inv_keep, torch.zeros_like(dx))
                     dz_prev = ref.bf16_round(dz_prev) if em else dz_prev
@@ -749,7 +795,7 @@ class PopulationMLP:
                 if l > 0:
                     dz = dz_prev
             reg = self._region(s)
-            self.p16[reg] = self.p32[reg].to(torch.bfloat16)
+            self.p16[reg] = ref.split_f32(self.p32[reg])[0]
 
     # ------------------------------------------------------------------ evaluation
     @torch.no_grad()
@@ -784,12 +830,12 @@ class PopulationMLP:
             for l in range(L - 1):
                 src = xb if l == 0 else self.act_eval
                 check(lib.mopt_mlp_fwd(tb["tl"].data_ptr(), tb["fwd"][l].data_ptr(), tb["n_fwd"][l],
-                                       rb, src.data_ptr(), self.p32.data_ptr(), self.p16.data_ptr(),
+                                       rb, src.data_ptr(), self.plo.data_ptr(), self.p16.data_ptr(),
                                        self.act_eval.data_ptr(), self.hp_dev.data_ptr(), 0, l,
                                        FWD_RELU, stream), "mlp_fwd(eval)")
             src = xb if L == 1 else self.act_eval
             check(lib.mopt_mlp_fwd_ce(tb["tl"].data_ptr(), tb["fwd"][L - 1].data_ptr(),
-                                      tb["n_fwd"][L - 1], rb, src.data_ptr(), self.p32.data_ptr(),
+                                      tb["n_fwd"][L - 1], rb, src.data_ptr(), self.plo.data_ptr(),
                                       self.p16.data_ptr(), y.data_ptr(), self.grad.data_ptr(),
                                       self.eval_loss.data_ptr(), self.eval_correct.data_ptr(),
                                       self.hp_dev.data_ptr(), 1.0, 0, stream), "mlp_fwd_ce(eval)")
@@ -808,7 +854,7 @@ class PopulationMLP:
                     a = ref.hidden_fwd(a, w, b, cfg.dropout, cfg.seed, l, 0, emulate_bf16=em,
                                        train=False)
                 w, b = layers[-1]
-                wq = ref.bf16_round(w) if em else w
+                wq = ref.bf16_weight(w) if em else w
                 ls, cs, _ = ref.softmax_ce(a @ wq.t() + b, y, self.num_classes, 1.0, em)
                 self.eval_loss[s] = ls
                 self.eval_correct[s] = cs

@@ -65,6 +65,12 @@ def dropout_mask(seed: int, layer: int, step: int, rows: int, n: int, p: float,
     return u >= torch.tensor(p, dtype=torch.float32, device=device)
 
 
+def bf16_weight(w: torch.Tensor) -> torch.Tensor:
+    """The bf16 working copy the kernels read for an f32 master weight: the hi half of the
+    split master (round to nearest, ties toward the smaller magnitude; csrc/common.h)."""
+    return split_f32(w.float())[0].float()
+
+
 def bf16_round(t: torch.Tensor) -> torch.Tensor:
     return t.to(torch.bfloat16).to(torch.float32)
 
@@ -75,7 +81,7 @@ def _inv_keep(drop: float) -> float:
 
 def hidden_fwd(x, w, b, drop, seed, layer, step, emulate_bf16=True, train=True):
     """Reference of ``mlp_fwd_kernel``: dropout(relu(x w^T + b)), rounded to bf16 when emulating."""
-    wq = bf16_round(w) if emulate_bf16 else w
+    wq = bf16_weight(w) if emulate_bf16 else w
     z = torch.relu(x.float() @ wq.t() + b)
     if train and drop > 0.0:
         keep = dropout_mask(seed, layer, step, z.shape[0], z.shape[1], drop, device=z.device)
@@ -97,6 +103,25 @@ def softmax_ce(logits: torch.Tensor, labels: torch.Tensor, n_real: int, inv_b: f
     if emulate_bf16:
         g = bf16_round(g)
     return loss.sum(), correct.sum(), g
+
+
+def split_f32(t: torch.Tensor):
+    """f32 -> (hi bf16, lo int16): the split master of the HIP backend (csrc/common.h); hi is
+    round-to-nearest with ties toward the smaller magnitude, (hi << 16) + lo - 0x7FFF the
+    original bit pattern."""
+    u = t.contiguous().view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    h = ((u + 0x7FFF) >> 16) & 0xFFFF
+    lo = (u - (h << 16) + 0x7FFF) & 0xFFFF
+    to16 = lambda x: (((x + 0x8000) & 0xFFFF) - 0x8000).to(torch.int16)  # noqa: E731
+    return to16(h).view(torch.bfloat16), to16(lo)
+
+
+def join_f32(hi: torch.Tensor, lo: torch.Tensor) -> torch.Tensor:
+    """(hi bf16, lo int16) -> the exact f32 master."""
+    h = hi.contiguous().view(torch.int16).to(torch.int64) & 0xFFFF
+    l = lo.contiguous().view(torch.int16).to(torch.int64) & 0xFFFF
+    u = ((h << 16) + l - 0x7FFF) & 0xFFFFFFFF
+    return (((u + 0x80000000) & 0xFFFFFFFF) - 0x80000000).to(torch.int32).view(torch.float32)
 
 
 def sgd_update(w, m, g, lr, momentum, wd):

@@ -1,7 +1,8 @@
 """Per-kernel timing of one population step (256 members, widths ~ loguniform(64, 1024)).
 
 Reports time per launch (HIP events) and effective bandwidth against the per-parameter byte
-model of each kernel (fwd: 2 B/param bf16 weight read; bwd+SGD: 18 B/param).
+model of each kernel (fwd: 2 B/param bf16 weight read; bwd+SGD: 16 B/param, 12 with the bf16
+momentum buffer -- split f32 master read and written as hi/lo halves).
 """
 import os
 import argparse
@@ -45,19 +46,19 @@ torch.cuda.synchronize()
 lib, tb, L = pop._lib, pop._tables["train"], pop.L
 stream = _lib.stream_ptr(dev)
 opt = (2 if args.momentum_dtype == "bf16" else 0) if args.optimizer == "sgd" else 1
-BWD_BYTES = {0: 18, 1: 26, 2: 14}[opt]
+BWD_BYTES = {0: 16, 1: 24, 2: 12}[opt]     # split master r+w 8, + momentum (+ AdamW v)
 
 
 def run_fwd(l):
     src = x if l == 0 else pop.act
     if l < L - 1:
         lib.mopt_mlp_fwd(tb["tl"].data_ptr(), tb["fwd"][l].data_ptr(), tb["n_fwd"][l], 1,
-                         src.data_ptr(), pop.p32.data_ptr(), pop.p16.data_ptr(),
+                         src.data_ptr(), pop.plo.data_ptr(), pop.p16.data_ptr(),
                          pop.act.data_ptr(), pop.hp_dev.data_ptr(), 0, l, FWD_RELU | FWD_DROPOUT,
                          stream)
     else:
         lib.mopt_mlp_fwd_ce(tb["tl"].data_ptr(), tb["fwd"][l].data_ptr(), tb["n_fwd"][l], 1,
-                            src.data_ptr(), pop.p32.data_ptr(), pop.p16.data_ptr(), y.data_ptr(),
+                            src.data_ptr(), pop.plo.data_ptr(), pop.p16.data_ptr(), y.data_ptr(),
                             pop.grad.data_ptr(), pop.loss.data_ptr(), pop.correct.data_ptr(),
                             pop.hp_dev.data_ptr(), 1.0 / 128, FWD_WRITE_GRAD, stream)
 
@@ -66,7 +67,7 @@ def run_bwd(l):
     src = x if l == 0 else pop.act
     flags = BWD_UPDATE_BIAS | ((BWD_HAS_DX | BWD_IN_DROPOUT) if l > 0 else 0)
     lib.mopt_mlp_bwd(tb["tl"].data_ptr(), tb["bwd"][l].data_ptr(), tb["n_bwd"][l], src.data_ptr(),
-                     pop.grad.data_ptr(), pop.p32.data_ptr(), pop.p16.data_ptr(),
+                     pop.grad.data_ptr(), pop.plo.data_ptr(), pop.p16.data_ptr(),
                      pop.m32.data_ptr(), pop.v32.data_ptr(), pop.hp_dev.data_ptr(), opt, flags,
                      stream)
 

@@ -10,6 +10,7 @@ import torch
 
 from metaopt_amd.models.data import TeacherClassification
 from metaopt_amd.ops.population import MemberConfig, PopulationMLP
+from metaopt_amd.ops.reference import join_f32, split_f32
 
 pytestmark = pytest.mark.gpu
 
@@ -157,8 +158,7 @@ def test_copy_member_and_checkpoint(data):
         hip.train_step(*data.batch(step))
     torch.cuda.synchronize()
     hip.load_slot_state(5, st)
-    b = hip.slot_base(5)
-    assert torch.equal(hip.p32[b:b + st["p32"].numel()].cpu(), st["p32"])
+    assert torch.equal(hip.master(5).cpu(), st["p32"])
     assert hip.steps_done(5) == 3
 
 
@@ -182,6 +182,18 @@ def test_multi_copy_and_checkpoint_pool(data):
     torch.cuda.synchronize()
     for h, w, b in zip(h16, wide, back):
         assert torch.equal(w, h.float()) and torch.equal(b, h)
+    # split masters: f32 -> (hi, lo) -> f32 is exact and agrees with the torch mirror
+    from metaopt_amd.ops.ckpt import Split
+    his = [torch.empty(t.numel(), dtype=torch.bfloat16, device="cuda") for t in src]
+    los = [torch.empty(t.numel(), dtype=torch.int16, device="cuda") for t in src]
+    again = [torch.empty_like(t) for t in src]
+    multi_copy([(s, None, Split(h, l)) for s, h, l in zip(src, his, los)])
+    multi_copy([(Split(h, l), a, None) for h, l, a in zip(his, los, again)])
+    torch.cuda.synchronize()
+    for s, h, l, a in zip(src, his, los, again):
+        assert torch.equal(a, s)
+        rh, rl = split_f32(s)
+        assert torch.equal(h, rh) and torch.equal(l, rl) and torch.equal(join_f32(h, l), s)
 
 
 @pytest.mark.parametrize("mdt", ["fp32", "bf16"])
@@ -198,7 +210,8 @@ def test_checkpoint_pool_roundtrip(data, mdt):
     torch.cuda.synchronize()
     b = hip.slot_base(4)
     n = ref1["p32"].numel()
-    assert torch.equal(hip.p32[b:b + n], ref1["p32"])
+    assert torch.equal(hip.master(4), ref1["p32"])
     assert torch.equal(hip.m32[b:b + n], ref1["m32"])
-    assert torch.equal(hip.p16[b:b + n], ref1["p32"].to(torch.bfloat16))
+    # the bf16 working copy is the split master's hi half: round to nearest (ties toward zero)
+    assert torch.equal(hip.p16[b:b + n], split_f32(ref1["p32"])[0])
     assert hip.steps_done(4) == ref1["t"] and hip.members[4].width == CONFIGS[0].width
