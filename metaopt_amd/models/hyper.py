@@ -6,9 +6,13 @@ preset by default) with SGD-momentum, and propagates forward-mode tangents of th
 respect to the two hyper-parameters through every inner step (Franceschi et al., "Forward and
 Reverse Gradient-Based Hyperparameter Optimization", ICML 2017):
 
-* the inner loss is written with differentiable fp32 PyTorch ops (GEMMs on hipBLASLt), so one
-  forward-over-reverse pass (``torch.func.jvp`` of ``torch.func.grad``) yields the gradient and a
-  Hessian-vector product along each tangent, exactly (no finite differences);
+* the inner loss is written so that one forward-over-reverse pass (``torch.func.jvp`` of
+  ``torch.func.grad``) yields the gradient and a Hessian-vector product along each tangent,
+  exactly (no finite differences): every GEMM -- the projections, the attention scores and
+  values, the LM head, in the forward, the backward and the tangent propagation -- is the
+  second-order-differentiable population GEMM of ``ops/pgemm_ad.py`` on the hand-written MFMA
+  kernel (bf16 operands, f32 accumulation); norms, RoPE, softmax and the loss are elementwise
+  fp32 ops;
 * the fused update of weights, momentum and the four tangent buffers is the hand-written K11
   kernel (``mopt_hyper_sgdm``), and the final ``<grad L_val, Z>`` reductions are ``mopt_hyper_dot``;
 * ``HypergradientSweep`` runs the outer loop over ranks: every rank trains its own ``P`` inner runs
@@ -29,6 +33,7 @@ import torch
 
 from ..ops import _lib
 from ..ops import lm as ops
+from ..ops.pgemm_ad import matmul
 from .llama import PRESETS, LMConfig, SyntheticLM, param_specs
 
 _lib.register_signatures({
@@ -37,6 +42,17 @@ _lib.register_signatures({
     "mopt_hyper_dot": ([ctypes.c_void_p] * 4 + [ctypes.c_int64, ctypes.c_int, ctypes.c_void_p],
                        ctypes.c_int),
 })
+
+
+def causal_attention(q, k, v, scale):
+    """Causal softmax attention of [B', H, T, Dh] heads -> rows [B' T, H Dh]: scores and values
+    on the population GEMM (differentiable to second order), softmax in fp32."""
+    Bp, H, T, Dh = q.shape
+    s = matmul(q.reshape(Bp * H, T, Dh), k.reshape(Bp * H, T, Dh), tb=True) * scale
+    mask = torch.ones(T, T, dtype=torch.bool, device=q.device).triu(1)
+    p = s.masked_fill(mask, float("-inf")).softmax(-1)
+    o = matmul(p, v.reshape(Bp * H, T, Dh))
+    return o.view(Bp, H, T, Dh).permute(0, 2, 1, 3).reshape(Bp * T, H * Dh)
 
 
 def lm_losses(params: Dict[str, torch.Tensor], tok, tgt, cfg: LMConfig, cos, sin):
@@ -48,15 +64,15 @@ def lm_losses(params: Dict[str, torch.Tensor], tok, tgt, cfg: LMConfig, cos, sin
     x = ops.embed_ref(tok.reshape(-1), params["embed"], rpt)
     for l in range(cfg.n_layers):
         h = ops.rmsnorm_ref(x, params[f"l{l}.attn_norm"], rpt, cfg.norm_eps)
-        qkv = torch.bmm(h.view(P, rpt, d), params[f"l{l}.wqkv"]).reshape(R, 3 * d)
+        qkv = matmul(h.view(P, rpt, d), params[f"l{l}.wqkv"]).reshape(R, 3 * d)
         q, k, v = ops.rope_split_ref(qkv, cos, sin, T, H)
-        o = ops.attention_ref(q, k, v, 1.0 / math.sqrt(cfg.head_dim))
-        x = x + torch.bmm(o.view(P, rpt, d), params[f"l{l}.wo"]).reshape(R, d)
+        o = causal_attention(q, k, v, 1.0 / math.sqrt(cfg.head_dim))
+        x = x + matmul(o.view(P, rpt, d), params[f"l{l}.wo"]).reshape(R, d)
         h = ops.rmsnorm_ref(x, params[f"l{l}.mlp_norm"], rpt, cfg.norm_eps)
-        a = ops.swiglu_ref(torch.bmm(h.view(P, rpt, d), params[f"l{l}.wgu"]))
-        x = x + torch.bmm(a, params[f"l{l}.wdown"]).reshape(R, d)
+        a = ops.swiglu_ref(matmul(h.view(P, rpt, d), params[f"l{l}.wgu"]))
+        x = x + matmul(a, params[f"l{l}.wdown"]).reshape(R, d)
     h = ops.rmsnorm_ref(x, params["final_norm"], rpt, cfg.norm_eps)
-    logits = torch.bmm(h.view(P, rpt, d), params["head"]).reshape(R, cfg.vocab)
+    logits = matmul(h.view(P, rpt, d), params["head"]).reshape(R, cfg.vocab)
     lz = torch.nn.functional.cross_entropy(logits, tgt.reshape(-1).long(), reduction="none")
     return lz.view(P, rpt).mean(1)
 
@@ -77,7 +93,7 @@ def hyper_sgdm_ref(w, v, ze, zm, ye, ym, g, he, hm, eta, mu):
 
 class HypergradLM:
     def __init__(self, capacity: int, config="tiny-2layer", batch_size: int = 4,
-                 seq_len: Optional[int] = None, device="cuda"):
+                 seq_len: Optional[int] = None, device="cuda", graph: Optional[bool] = None):
         cfg = PRESETS[config] if isinstance(config, str) else config
         if seq_len is not None:
             import dataclasses
@@ -100,6 +116,16 @@ class HypergradLM:
         self.mu = torch.zeros(P, dtype=torch.float32, device=self.device)
         self.cos, self.sin = ops.rope_tables(cfg.seq_len, cfg.rope_base, device=self.device)
         self.steps = 0
+        # the inner step is thousands of small launches (forward, backward and two tangent
+        # passes through every op): on the GPU it is captured once into a HIP graph and
+        # replayed (MOPT_HYPER_GRAPH=0 runs it eagerly)
+        if graph is None:
+            import os
+            graph = os.environ.get("MOPT_HYPER_GRAPH", "1") != "0"
+        self.use_graph = bool(graph) and self.device.type == "cuda"
+        self._graph = None
+        self._static = None
+        self._eager_steps = 0
 
     def params(self, W: torch.Tensor) -> Dict[str, torch.Tensor]:
         return {name: W[:, o:o + k].view(self.P, *shape)
@@ -133,11 +159,31 @@ class HypergradLM:
     def inner_step(self, tok, tgt) -> torch.Tensor:
         """One SGD-momentum step of every run with tangent propagation; returns losses [P]."""
         tok, tgt = self._expand(tok), self._expand(tgt)
-        grad_fn = torch.func.grad_and_value(lambda W: self._loss_sum(W, tok, tgt))
-        (g, loss), (he, _) = torch.func.jvp(grad_fn, (self.w,), (self.ze,))
+        if not self.use_graph:
+            return self._step_body(tok, tgt)
+        if self._graph is None and self._eager_steps < 1:
+            self._eager_steps += 1            # first step eager: lazy initialisations run
+            return self._step_body(tok, tgt)
+        if self._graph is None:
+            self._static = (tok.clone(), tgt.clone())
+            self._graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self._graph):
+                self._graph_out = self._step_body(*self._static)
+            self.steps -= 1                    # capture recorded the step, replay runs it
+        self._static[0].copy_(tok)
+        self._static[1].copy_(tgt)
+        self._graph.replay()
+        self.steps += 1
+        return self._graph_out.clone()
+
+    def _step_body(self, tok, tgt) -> torch.Tensor:
+        def loss_fn(W):
+            per_trial = lm_losses(self.params(W), tok, tgt, self.cfg, self.cos, self.sin)
+            return per_trial.sum(), per_trial.detach()
+
+        grad_fn = torch.func.grad_and_value(loss_fn, has_aux=True)
+        (g, (_, losses)), (he, _) = torch.func.jvp(grad_fn, (self.w,), (self.ze,))
         (_, _), (hm, _) = torch.func.jvp(grad_fn, (self.w,), (self.zm,))
-        with torch.no_grad():
-            losses = lm_losses(self.params(self.w), tok, tgt, self.cfg, self.cos, self.sin)
         self._update(g.contiguous(), he.contiguous(), hm.contiguous())
         self.steps += 1
         return losses
