@@ -133,10 +133,37 @@ def build(force: bool = False, verbose: bool = False, extra_flags=None) -> Path:
     return lib
 
 
+def build_variant(name: str, extra_flags, verbose: bool = False) -> Path:
+    """Build the library with ``extra_flags`` into ``lib/variants/<name>/`` (A/B experiments:
+    load it with ``MOPT_KERNEL_LIB``; the default library is untouched)."""
+    hipcc = hipcc_path()
+    out = OUT_DIR / "variants" / name
+    (out / "obj").mkdir(parents=True, exist_ok=True)
+    objs = [out / "obj" / (src.stem + ".o") for src in _sources()]
+    with cf.ThreadPoolExecutor(max(1, min(len(objs), int(os.environ.get("MAX_JOBS", "8"))))) as ex:
+        for f in [ex.submit(_compile, src, obj, hipcc, list(extra_flags))
+                  for src, obj in zip(_sources(), objs)]:
+            f.result()
+    lib = out / LIB_NAME
+    proc = subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs),
+                           "-o", str(lib)], capture_output=True, text=True)
+    if proc.returncode != 0:
+        raise RuntimeError(f"link failed:\n{proc.stderr}")
+    if verbose:
+        print(f"[mopt build] variant {name}: {lib}")
+    return lib
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--force", action="store_true")
+    ap.add_argument("--variant", default=None, help="name of an A/B variant build")
+    ap.add_argument("-D", dest="defines", action="append", default=[],
+                    help="preprocessor define of the variant (repeatable)")
     args = ap.parse_args(argv)
+    if args.variant:
+        print(build_variant(args.variant, [f"-D{d}" for d in args.defines], verbose=True))
+        return 0
     path = build(force=args.force, verbose=True)
     print(path)
     return 0

@@ -166,6 +166,14 @@ __device__ __forceinline__ void fwd_gemm(const bf16_t* __restrict__ X, const bf1
 #undef MOPT_FWD_LOAD
 #undef MOPT_FWD_STORE
 
+// (Measured and rejected: an LDS-free variant loading every MFMA fragment -- 16 bytes of one
+// row of X or W per lane -- straight from global memory ran the forward 2.5x slower than the
+// LDS-staged tiles above; profiles/README.md.)
+__device__ __forceinline__ void fwd_core(const bf16_t* X, const bf16_t* W, int K, bf16_t* As,
+                                         bf16_t* Bs, f32x4 (&acc)[2][4]) {
+  fwd_gemm(X, W, K, As, Bs, acc);
+}
+
 // Y[rows, n0:n0+64] = dropout(relu(X W^T + b)) for one (trial-layer, n-tile, 128-row block).
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void mlp_fwd_kernel(const MlpTL* __restrict__ tls,
                                                       const int2* __restrict__ work, int n_work,
@@ -185,7 +193,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void m
   const bf16_t* W = p16 + tl.w_off + (size_t)n0 * K;
 
   f32x4 acc[2][4];
-  fwd_gemm(X, W, K, As, Bs, acc);
+  fwd_core(X, W, K, As, Bs, acc);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, g = lane >> 4;
   const bf16_t* bias_hi = p16 + tl.b_off + n0;
@@ -252,7 +260,7 @@ __global__ __launch_bounds__(256) void mlp_fwd_ce_kernel(const MlpTL* __restrict
   const bf16_t* W = p16 + tl.w_off;
 
   f32x4 acc[2][4];
-  fwd_gemm(X, W, K, As, Bs, acc);
+  fwd_core(X, W, K, As, Bs, acc);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, g = lane >> 4;
   const bf16_t* bias_hi = p16 + tl.b_off;

@@ -6,16 +6,16 @@ set -e
 OUT=${OUT:-gpurun_out/prof}
 mkdir -p "$OUT"
 ROOT=$(pwd)
-timeout -k 10 300 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
-timeout -k 10 300 python scripts/kernel_bench.py --out "$OUT/kbench.json" > "$OUT/kbench.log" 2>&1
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err"
+timeout -k 10 300 python scripts/kernel_bench.py --momentum-dtype bf16 --out "$OUT/kbench.json" > "$OUT/kbench.log" 2>&1
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$OUT/trace" -o run -- \
-    python3 "$ROOT/bench.py" --steps 64 --warmup 32 > "$ROOT/$OUT/trace.log" 2>&1
+    python3 "$ROOT/bench.py" --steps 10 --warmup 3 > "$ROOT/$OUT/trace.log" 2>&1
 # derived counters expand to many hardware counters: one derived counter per pass
 pmc() {
   local name=$1; shift
   timeout -k 10 180 rocprofv3 --output-format csv --pmc "$@" -d "$ROOT/$OUT/$name" -o run -- \
-      python3 "$ROOT/scripts/kernel_bench.py" --iters 3 > "$ROOT/$OUT/$name.log" 2>&1
+      python3 "$ROOT/scripts/kernel_bench.py" --iters 3 --momentum-dtype bf16 > "$ROOT/$OUT/$name.log" 2>&1
 }
 if [ -z "$NO_PMC" ]; then
   pmc pmc_fetch FETCH_SIZE
