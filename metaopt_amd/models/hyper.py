@@ -17,7 +17,12 @@ Reverse Gradient-Based Hyperparameter Optimization", ICML 2017):
   kernel (``mopt_hyper_sgdm``), and the final ``<grad L_val, Z>`` reductions are ``mopt_hyper_dot``;
 * ``HypergradientSweep`` runs the outer loop over ranks: every rank trains its own ``P`` inner runs
   (different seeds and data shards), the per-rank mean hypergradient is averaged with ONE
-  all-reduce (C2) per outer step, and the shared (log lr, logit momentum) take an Adam step.
+  all-reduce (C2) per outer step, and the shared (log lr, logit momentum) take an Adam step;
+* intra-trial data parallelism (C3, ``dp_comm``): the ranks of a DP group hold the SAME inner
+  runs and each differentiates its own shard of every minibatch; the gradient and both
+  Hessian-vector products are averaged with ONE all-reduce of a packed [3, P, n] buffer per
+  inner step before the K11 update, so every rank takes the identical step a single process
+  would take on the whole minibatch.
   Each outer step is recorded as a trial (objective = validation loss, ``gradient`` result =
   d L_val / d(lr, momentum)) in the experiment storage, the reference's gradient-result contract.
 """
@@ -93,7 +98,8 @@ def hyper_sgdm_ref(w, v, ze, zm, ye, ym, g, he, hm, eta, mu):
 
 class HypergradLM:
     def __init__(self, capacity: int, config="tiny-2layer", batch_size: int = 4,
-                 seq_len: Optional[int] = None, device="cuda", graph: Optional[bool] = None):
+                 seq_len: Optional[int] = None, device="cuda", graph: Optional[bool] = None,
+                 dp_comm=None):
         cfg = PRESETS[config] if isinstance(config, str) else config
         if seq_len is not None:
             import dataclasses
@@ -122,7 +128,10 @@ class HypergradLM:
         if graph is None:
             import os
             graph = os.environ.get("MOPT_HYPER_GRAPH", "1") != "0"
-        self.use_graph = bool(graph) and self.device.type == "cuda"
+        # C3: the DP group's all-reduce sits between the captured compute and the update, so
+        # the step runs eagerly when the runs are data-parallel
+        self.dp_comm = dp_comm if dp_comm is not None and dp_comm.world_size > 1 else None
+        self.use_graph = bool(graph) and self.device.type == "cuda" and self.dp_comm is None
         self._graph = None
         self._static = None
         self._eager_steps = 0
@@ -184,6 +193,14 @@ class HypergradLM:
         grad_fn = torch.func.grad_and_value(loss_fn, has_aux=True)
         (g, (_, losses)), (he, _) = torch.func.jvp(grad_fn, (self.w,), (self.ze,))
         (_, _), (hm, _) = torch.func.jvp(grad_fn, (self.w,), (self.zm,))
+        if self.dp_comm is not None:                                            # C3
+            packed = torch.stack([g, he, hm])
+            buf = packed.to(self.dp_comm._coll_device())
+            self.dp_comm.all_reduce_mean_(buf)
+            g, he, hm = buf.to(self.device).unbind(0)
+            losses = losses.to(self.dp_comm._coll_device())
+            self.dp_comm.all_reduce_mean_(losses)
+            losses = losses.to(self.device)
         self._update(g.contiguous(), he.contiguous(), hm.contiguous())
         self.steps += 1
         return losses
@@ -205,6 +222,11 @@ class HypergradLM:
         with torch.no_grad():
             losses = lm_losses(self.params(self.w), tok, tgt, self.cfg, self.cos, self.sin)
         gval = gval.contiguous()
+        if self.dp_comm is not None:      # C3: validation gradient over the DP group's shards
+            buf = torch.cat([gval, losses[:, None]], 1).to(self.dp_comm._coll_device())
+            self.dp_comm.all_reduce_mean_(buf)
+            buf = buf.to(self.device)
+            gval, losses = buf[:, :-1].contiguous(), buf[:, -1].contiguous()
         if self.device.type == "cuda":
             out = torch.empty(self.P, 2, dtype=torch.float32, device=self.device)
             lib = _lib.get_lib()
@@ -250,11 +272,19 @@ class HypergradientSweep:
         comm.broadcast_(theta, src=0)                                           # C5
         self.theta = theta.cpu().numpy()
         lr, mu = self.hparams
-        base = (self.outer * comm.world_size + comm.rank) * model.P
+        dp = model.dp_comm is not None
+        if dp:   # C3: the same runs on every rank, each rank differentiating its rows
+            base, shard = self.outer * model.P, self.outer
+        else:
+            base = (self.outer * comm.world_size + comm.rank) * model.P
+            shard = self.outer * comm.world_size + comm.rank
         model.reset([1000003 * (base + p) + 17 for p in range(model.P)], lr, mu)
-        shard = self.outer * comm.world_size + comm.rank
         for k in range(self.inner_steps):
             tok, tgt = self.data.batch(shard * self.inner_steps + k)
+            if dp:
+                rows = tok.shape[0] // comm.world_size
+                tok = tok[comm.rank * rows:(comm.rank + 1) * rows]
+                tgt = tgt[comm.rank * rows:(comm.rank + 1) * rows]
             model.inner_step(tok, tgt)
         hg, vl = model.hypergradient(*self.data.validation())
         red = torch.cat([hg.mean(0).double(), vl.mean().double().view(1)])

@@ -93,7 +93,8 @@ def run_hyper(args, comm):
     from metaopt_amd.models.hyper import HypergradientSweep, HypergradLM
     from metaopt_amd.models.llama import SyntheticLM
     P = args.population or 8
-    model = HypergradLM(P, "tiny-2layer", batch_size=4, seq_len=128, device=comm.device)
+    model = HypergradLM(P, "tiny-2layer", batch_size=4, seq_len=128, device=comm.device,
+                        dp_comm=comm if getattr(args, "dp", False) else None)
     data = SyntheticLM(4096, 128, 4, n_tokens=1 << 20, seed=args.seed, device=comm.device)
     sweep = HypergradientSweep(model, data, comm=comm, inner_steps=args.inner_steps)
     for _ in range(args.warmup):
@@ -125,6 +126,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="resnet20",
                     choices=["logreg", "mlp", "resnet20", "lm-125m", "lm-tiny", "hyper"])
+    ap.add_argument("--dp", action="store_true",
+                    help="hyper: intra-trial data parallelism (C3) instead of independent runs")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--population", type=int, default=None)
     ap.add_argument("--steps", type=int, default=60)

@@ -101,3 +101,46 @@ def test_c2_allreduce_keeps_ranks_in_lockstep_gloo():
         p.join(timeout=60)
     (_, lr0, g0, th0), (_, lr1, g1, th1) = res
     assert lr0 == lr1 and g0 == g1 and th0 == th1   # identical meta-steps on every rank
+
+
+def _dp_worker(rank, world, port, q):
+    """C3: 2 ranks, each with half of every minibatch, data-parallel over the same runs."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(2)
+    from metaopt_amd.parallel.comm import init_from_env
+    comm = init_from_env(backend="gloo")
+    data = _data(batch=4)
+    m = HypergradLM(2, "micro", batch_size=2, device="cpu", dp_comm=comm)
+    m.reset([1, 2], 0.3, 0.6)
+    for k in range(3):
+        tok, tgt = data.batch(k)
+        m.inner_step(tok[2 * rank:2 * rank + 2], tgt[2 * rank:2 * rank + 2])
+    vt, vg = data.validation()
+    hg, vl = m.hypergradient(vt, vg)
+    q.put((rank, m.w.numpy().copy(), hg.numpy().copy(), vl.numpy().copy()))  # by value
+    dist.destroy_process_group()
+
+
+def test_c3_intra_trial_data_parallel_equals_one_process():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dp_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=300) for _ in range(world)), key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    torch.set_num_threads(2)
+    data = _data(batch=4)
+    m = HypergradLM(2, "micro", batch_size=4, device="cpu")
+    m.reset([1, 2], 0.3, 0.6)
+    for k in range(3):
+        m.inner_step(*data.batch(k))
+    hg, vl = m.hypergradient(*data.validation())
+    (_, w0, hg0, vl0), (_, w1, hg1, vl1) = [(r, *map(torch.from_numpy, t)) for r, *t in res]
+    assert torch.equal(w0, w1) and torch.equal(hg0, hg1)     # the DP ranks stay identical
+    torch.testing.assert_close(w0, m.w, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(hg0, hg, rtol=1e-3, atol=1e-5)
+    torch.testing.assert_close(vl0, vl, rtol=1e-5, atol=1e-6)
