@@ -609,6 +609,7 @@ class PopulationMLP:
             fwd = [np.zeros((0, 2), np.int32) for _ in range(L)]
             bwd = [np.zeros((0, 2), np.int32) for _ in range(L)]
         out = {"tl_np": tl, "rows": rows, "fwd_np": fwd, "bwd_np": bwd}
+        self._validate_tables(tl, fwd, bwd, rows)
         if self.device.type == "cuda":
             from ._lib import upload, upload_bytes
             out["tl"] = upload_bytes(tl, self.device)
@@ -617,6 +618,49 @@ class PopulationMLP:
         out["n_fwd"] = [len(w) for w in fwd]
         out["n_bwd"] = [len(w) for w in bwd]
         return out
+
+    def _validate_tables(self, tl, fwd, bwd, rows) -> None:
+        """Bounds check of every descriptor a launch will read (SURVEY §5 "race detection /
+        sanitizers"): the kernels index memory only through these tables, so a table that
+        passes here cannot make a kernel read or write outside its buffers.  Vectorised over
+        the table (microseconds per refresh), always on."""
+        L = self.L
+        n_tl = len(tl)
+        params = self.capacity * self.slot_params
+        act = self.capacity * rows * self.act_row
+        live = tl["K"] > 0
+        t = tl[live]
+        bad = []
+        if ((t["K"] % TILE) | (t["N"] % TILE)).any():
+            bad.append("K/N not multiples of 64")
+        if (t["w_off"] < 0).any() or (t["w_off"] + t["K"].astype(np.int64) * t["N"] > params).any():
+            bad.append("weights outside the parameter buffers")
+        if (t["b_off"] < 0).any() or (t["b_off"] + t["N"] > params).any():
+            bad.append("bias outside the parameter buffers")
+        first = (np.flatnonzero(live) % L) == 0
+        xin = t[~first]
+        if (xin["x_off"] < 0).any() or (xin["x_off"] + rows * xin["K"].astype(np.int64) > act).any():
+            bad.append("layer input outside the activation buffer")
+        if (t["K"][first] != self.K0).any():
+            bad.append("first layer K differs from the input width")
+        if (t["y_off"] < 0).any() or (t["y_off"] + rows * t["N"].astype(np.int64) > act).any():
+            bad.append("layer output outside the activation buffer")
+        if (t["n_real"] > t["N"]).any() or (t["trial"] < 0).any() or \
+                (t["trial"] >= self.capacity).any():
+            bad.append("trial / class fields out of range")
+        for name, lists, per in (("fwd", fwd, "N"), ("bwd", bwd, "K")):
+            for w in lists:
+                if not len(w):
+                    continue
+                idx = w[:, 0]
+                if (idx < 0).any() or (idx >= n_tl).any() or not live[idx].all():
+                    bad.append(f"{name} work item names a missing trial-layer")
+                    break
+                if (w[:, 1] < 0).any() or (w[:, 1] >= tl[per][idx] // TILE).any():
+                    bad.append(f"{name} work item tile out of range")
+                    break
+        if bad:
+            raise ValueError("population work tables fail the bounds check: " + "; ".join(bad))
 
     def _refresh(self) -> None:
         self._run_pending_init()

@@ -208,3 +208,26 @@ def test_bf16_momentum_population_trains_on_cpu():
     assert np.isfinite(losses).all() and losses[-1] < losses[0]
     st = pop.slot_state(0)
     assert st["m32"].dtype == __import__("torch").bfloat16
+
+
+def test_work_tables_are_bounds_checked():
+    """Every table a launch reads is validated against the buffers before use; a corrupted
+    descriptor is refused on the host instead of reaching a kernel."""
+    import numpy as np
+    import pytest
+    from metaopt_amd.ops.population import MemberConfig, PopulationMLP
+    pop = PopulationMLP(3, max_width=128, eval_batch=128, device="cpu")
+    pop.set_member(1, MemberConfig(width=100, lr=0.1, seed=1))
+    tb = pop._build_tables(128)
+    tl = tb["tl_np"].copy()
+    tl["w_off"][1 * pop.L + 1] = pop.capacity * pop.slot_params        # past the end
+    with pytest.raises(ValueError, match="weights outside"):
+        pop._validate_tables(tl, tb["fwd_np"], tb["bwd_np"], 128)
+    fwd = [w.copy() for w in tb["fwd_np"]]
+    fwd[0][0, 1] = 99                                                   # tile index too large
+    with pytest.raises(ValueError, match="tile out of range"):
+        pop._validate_tables(tb["tl_np"], fwd, tb["bwd_np"], 128)
+    fwd = [w.copy() for w in tb["fwd_np"]]
+    fwd[1][0, 0] = 0                                                    # an empty slot's layer
+    with pytest.raises(ValueError, match="missing trial-layer"):
+        pop._validate_tables(tb["tl_np"], fwd, tb["bwd_np"], 128)
