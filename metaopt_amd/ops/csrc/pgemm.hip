@@ -19,6 +19,10 @@
 // Split-K (for the weight gradient's long reduction over tokens / pixels) writes f32 partial
 // tiles that a second pass sums and rounds to bf16.  Blocks are remapped XCD-aware so the tiles
 // sharing an A row panel run on one XCD (one L2).
+//
+// Large dense shapes (the LM's projections and their gradients: M, N multiples of 128/256) use a
+// second kernel, pgemm_big_kernel (below): 8 waves, 256-wide tiles, operands filled straight
+// from global memory into swizzled LDS images, persistent over the tiles.
 #include "common.h"
 
 using namespace mopt;
@@ -252,6 +256,192 @@ __global__ __launch_bounds__(256) void pgemm_kernel(const GemmArgs g) {
   }
 }
 
+// ----------------------------------------------------------------------------------------------
+// Large-tile dense GEMM (the LM's projections, head and their gradients): 512 threads = 8 waves
+// arranged WM x (8/WM), each wave a 16*FM x 16*FN sub-tile; block tile 256 x 256 (or 256 x 128 /
+// 128 x 256), BK = 64, one workgroup per CU.  Operand tiles go HBM/L2 -> LDS directly with
+// global_load_lds_dwordx4 (no VGPR staging, no ds_write pass): every wave-instruction fills 1 KB
+// of the LDS image lane-linearly, so the images are unpadded and bank conflicts are removed by
+// XOR-swizzling 16-byte chunks -- the permutation is applied to the per-lane GLOBAL source
+// address at the fill and to the ds_read address at the use (the same involution on both sides):
+//   * k-contiguous image [rows][64] (128-B rows): chunk c of row r lives at c ^ ((r >> 1) & 7),
+//     so the 16 rows of an A/B fragment read (ds_read_b128) hit 16 distinct 16-byte bank slots;
+//   * row-contiguous image [64 k][rows]: chunk c of k-row kr lives at c ^ swz(kr), swz spreading
+//     the 4 k-rows (and the two lane groups) of a ds_read_b64_tr_b16 over distinct bank slots.
+// Two LDS stages: the fills of tile t+1 are in flight while tile t is multiplied; every wave
+// waits for its own fills (vmcnt(0)) and the barrier publishes them.
+// Preconditions (checked on the host): M % BM == 0, N % BN == 0, K % 64 == 0 (per split), row
+// strides multiples of 8 elements, 16-byte aligned bases.
+// ----------------------------------------------------------------------------------------------
+#ifndef MOPT_GEMM_GROUP_M
+#define MOPT_GEMM_GROUP_M 8
+#endif
+constexpr int kGroupM = MOPT_GEMM_GROUP_M;
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glb_void;
+
+__device__ __forceinline__ int kc_swz(int row) { return (row >> 1) & 7; }
+__device__ __forceinline__ int rc_swz(int kr) { return ((kr & 3) << 1) | (((kr >> 3) & 1) << 3); }
+
+template <int ROWS, bool KCONTIG>
+struct GImg {
+  static constexpr int ELEMS = ROWS * BK;          // unpadded
+  static constexpr int BLOCKS = ELEMS * 2 / 1024;  // 1-KB wave-instruction fills
+  static constexpr int NI = BLOCKS / 8;            // fills per wave (8 waves)
+  static_assert(NI * 8 == BLOCKS, "tile must split into 8 waves of 1-KB fills");
+  static constexpr int CPR = ROWS / 8;             // 16-B chunks per k-row (row-contiguous)
+  static_assert(KCONTIG || CPR >= 16, "row-contiguous swizzle needs >= 16 chunks per k-row");
+
+  // fill this wave's share of the tile whose first row / k is (row0, k0)
+  __device__ __forceinline__ static void fill(const bf16_t* __restrict__ base, int ld, int row0,
+                                              int k0, bf16_t* img, int wave, int lane) {
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int blk = wave * NI + j;
+      const bf16_t* src;
+      if (KCONTIG) {
+        const int r = blk * 8 + (lane >> 3), c = lane & 7;
+        src = base + (int64_t)(row0 + r) * ld + k0 + 8 * (c ^ kc_swz(r));
+      } else {
+        const int kr = blk * (64 / CPR) + lane / CPR, c = lane % CPR;
+        src = base + (int64_t)(k0 + kr) * ld + row0 + 8 * (c ^ rc_swz(kr));
+      }
+      __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)(img + blk * 512), 16, 0, 0);
+    }
+  }
+
+  // fragment of rows row16 .. row16+15, k = 32 s + 8 g .. + 7 (same lane map as Img::frag)
+  __device__ __forceinline__ static bf16x8 frag(const bf16_t* img, int row16, int s, int li, int g,
+                                                int q, int pp) {
+    if (KCONTIG) {
+      const int r = row16 + li;
+      return lds_frag(img + r * BK + 8 * ((4 * s + g) ^ kc_swz(r)));
+    }
+    const int col = row16 + 4 * pp, k1 = 32 * s + 8 * g + q, k2 = k1 + 4;
+    const s16x4 lo = lds_tr4(img + k1 * ROWS + 8 * ((col >> 3) ^ rc_swz(k1)) + (col & 7));
+    const s16x4 hi = lds_tr4(img + k2 * ROWS + 8 * ((col >> 3) ^ rc_swz(k2)) + (col & 7));
+    return cat_frag(lo, hi);
+  }
+};
+
+template <bool TA, bool TB, int WM, int FM, int FN>
+__global__ __launch_bounds__(512) void pgemm_big_kernel(const GemmArgs g) {
+  constexpr int WN = 8 / WM;
+  constexpr int BM = WM * 16 * FM, BN = WN * 16 * FN;
+  static_assert(FN % 2 == 0, "the epilogue pairs n-fragments");
+  using IA = GImg<BM, !TA>;
+  using IB = GImg<BN, TB>;
+  constexpr int STAGE = IA::ELEMS + IB::ELEMS;
+  __shared__ __attribute__((aligned(1024))) bf16_t smem[2 * STAGE];  // the only __shared__ object
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int li = lane & 15, gq = lane >> 4, q = li >> 2, pp = li & 3;
+  const int wm = wave / WN, wn = wave % WN;
+  const int nk = g.K / BK;
+
+  // Persistent: workgroup b computes the tiles of virtual ids b, b + G, ... (G = grid size, a
+  // multiple of 8, so every virtual id of b maps to b's XCD under xcd_remap).
+  int vb = blockIdx.x;
+  int p = 0, m0 = 0, n0 = 0;
+  // Tile order within a trial: groups of kGroupM row panels, m fastest inside a group, so the
+  // tiles an XCD runs together share both their B column panels and a few A row panels in L2
+  // (n-fastest order re-streams every B panel from HBM once per row panel).
+  auto decode = [&](int v) {
+    const int t = xcd_remap(v, g.nwg);
+    const int per = g.tiles_m * g.tiles_n;
+    p = t / per;
+    const int idx = t - p * per, span = kGroupM * g.tiles_n;
+    const int grp = idx / span, in = idx - grp * span;
+    const int gm = min(kGroupM, g.tiles_m - grp * kGroupM);
+    m0 = (grp * kGroupM + in % gm) * BM;
+    n0 = (in / gm) * BN;
+  };
+  decode(vb);
+  IA::fill(g.a.ptr + p * g.a.batch, g.a.ld, m0, 0, smem, wave, lane);
+  IB::fill(g.b.ptr + p * g.b.batch, g.b.ld, n0, 0, smem + IA::ELEMS, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  int stage = 0;
+  while (true) {
+    const int nvb = vb + (int)gridDim.x;
+    const bool has_next = nvb < g.nwg;
+    int np = p, nm0 = m0, nn0 = n0;
+    if (has_next) {
+      const int cp = p, cm = m0, cn = n0;
+      decode(nvb);
+      np = p; nm0 = m0; nn0 = n0;
+      p = cp; m0 = cm; n0 = cn;
+    }
+    const bf16_t* A = g.a.ptr + p * g.a.batch;
+    const bf16_t* B = g.b.ptr + p * g.b.batch;
+
+    // acc holds C^T fragments (B is the MFMA's A operand): lane (li, gq), register r =
+    // C[m = 16 i + li][n = 16 j + 4 gq + r] of the wave's sub-tile -- 4 consecutive columns
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int kt = 0; kt < nk; ++kt) {
+      const bf16_t* cur = smem + stage * STAGE;
+      bf16_t* nxt = smem + (stage ^ 1) * STAGE;
+      // fill the other stage: this tile's next K-step, or the next tile's first one
+      if (kt + 1 < nk) {
+        IA::fill(A, g.a.ld, m0, (kt + 1) * BK, nxt, wave, lane);
+        IB::fill(B, g.b.ld, n0, (kt + 1) * BK, nxt + IA::ELEMS, wave, lane);
+      } else if (has_next) {
+        IA::fill(g.a.ptr + np * g.a.batch, g.a.ld, nm0, 0, nxt, wave, lane);
+        IB::fill(g.b.ptr + np * g.b.batch, g.b.ld, nn0, 0, nxt + IA::ELEMS, wave, lane);
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 a[FM], b[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) a[i] = IA::frag(cur, wm * 16 * FM + 16 * i, s, li, gq, q, pp);
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          b[j] = IB::frag(cur + IA::ELEMS, wn * 16 * FN + 16 * j, s, li, gq, q, pp);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(b[j], a[i], acc[i][j]);
+      }
+      // the fills of the other stage (and the previous tile's C stores) have landed, and every
+      // wave is done reading this stage
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      stage ^= 1;
+    }
+
+    // Epilogue without LDS: pack 4 columns per fragment to bf16, then exchange between the lane
+    // rows gq = 0|1 (and 2|3) with v_permlane16_swap so every lane holds 8 consecutive columns of
+    // one row; per fragment pair (j, j+1) each row gets 64 contiguous bytes in one dwordx4 store.
+    // The stores drain while the next tile's first K-step is multiplied.
+    bf16_t* C = g.C + p * g.sC + (int64_t)(m0 + wm * 16 * FM + li) * g.ldc + n0 + wn * 16 * FN +
+                16 * (gq & 1) + 8 * (gq >> 1);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+      for (int j = 0; j < FN; j += 2) {
+        uint32_t x0 = pack2bf(acc[i][j][0], acc[i][j][1]);
+        uint32_t x1 = pack2bf(acc[i][j][2], acc[i][j][3]);
+        uint32_t y0 = pack2bf(acc[i][j + 1][0], acc[i][j + 1][1]);
+        uint32_t y1 = pack2bf(acc[i][j + 1][2], acc[i][j + 1][3]);
+        const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+        *(uint4*)(C + (int64_t)(16 * i) * g.ldc + 16 * j) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+      }
+    }
+    if (!has_next) break;
+    vb = nvb;
+    p = np; m0 = nm0; n0 = nn0;
+  }
+}
+
 // sum of the split-K partials [splits][P][M][N] -> C[p][m][n * ldc] bf16
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part,
                                                             bf16_t* __restrict__ C, int64_t sC,
@@ -279,8 +469,32 @@ int launch(GemmArgs g, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+template <bool TA, bool TB, int WM, int FM, int FN>
+int launch_big(GemmArgs g, hipStream_t st) {
+  constexpr int BM = WM * 16 * FM, BN = (8 / WM) * 16 * FN;
+  if (g.M % BM || g.N % BN || g.K % BK || g.splits != 1) return (int)hipErrorInvalidValue;
+  g.tiles_m = g.M / BM;
+  g.tiles_n = g.N / BN;
+  const int64_t nwg = (int64_t)g.P * g.tiles_m * g.tiles_n;
+  if (nwg <= 0 || nwg > 0x7FFFFFFF) return (int)hipErrorInvalidValue;
+  g.nwg = (int)nwg;
+  // persistent: one workgroup per CU (the LDS stages allow no second one), a multiple of 8
+  constexpr int kGrid = 256;
+  const int grid = nwg < kGrid ? (int)nwg : kGrid;
+  hipLaunchKernelGGL((pgemm_big_kernel<TA, TB, WM, FM, FN>), dim3(grid), dim3(512), 0, st, g);
+  return (int)hipGetLastError();
+}
+
 template <int KA, int KB, bool TA, bool TB>
 int dispatch_tile(const GemmArgs& g, int cfg, hipStream_t st) {
+  if constexpr (KA == kDense && KB == kDense) {
+    switch (cfg) {
+      case 5: return launch_big<TA, TB, 2, 8, 4>(g, st);  // 256 x 256
+      case 6: return launch_big<TA, TB, 4, 4, 4>(g, st);  // 256 x 128
+      case 7: return launch_big<TA, TB, 2, 4, 4>(g, st);  // 128 x 256
+      default: break;
+    }
+  }
   switch (cfg) {
     case 0: return launch<KA, KB, TA, TB, 2, 4, 4>(g, st);  // 128 x 128
     case 1: return launch<KA, KB, TA, TB, 4, 2, 1>(g, st);  // 128 x 16
@@ -332,8 +546,9 @@ extern "C" {
 
 // Tile of configuration ``cfg`` (rows, cols): lets the host size grids and split-K.
 int mopt_pgemm_tile(int cfg, int* bm, int* bn) {
-  static const int t[5][2] = {{128, 128}, {128, 16}, {128, 32}, {64, 64}, {64, 128}};
-  if (cfg < 0 || cfg > 4) return (int)hipErrorInvalidValue;
+  static const int t[8][2] = {{128, 128}, {128, 16}, {128, 32}, {64, 64},
+                              {64, 128},  {256, 256}, {256, 128}, {128, 256}};
+  if (cfg < 0 || cfg > 7) return (int)hipErrorInvalidValue;
   *bm = t[cfg][0];
   *bn = t[cfg][1];
   return 0;

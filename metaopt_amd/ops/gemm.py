@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 from typing import Optional
 
 import torch
@@ -33,9 +34,17 @@ _lib.register_signatures({
                    c_int),
 })
 
-# tile configurations of csrc/pgemm.hip: cfg -> (BM, BN)
-TILES = {0: (128, 128), 1: (128, 16), 2: (128, 32), 3: (64, 64), 4: (64, 128)}
+# tile configurations of csrc/pgemm.hip: cfg -> (BM, BN).  0-4: 4-wave register-staged kernel
+# (any shape, ragged edges); 5-7: 8-wave direct-to-LDS kernel, one workgroup per CU, for shapes
+# the tile divides (M % BM == N % BN == K % 64 == 0)
+TILES = {0: (128, 128), 1: (128, 16), 2: (128, 32), 3: (64, 64), 4: (64, 128),
+         5: (256, 256), 6: (256, 128), 7: (128, 256)}
+BIG_TILES = (5, 6, 7)
 NUM_CU = 256
+#: relative speed of the big tiles at equal occupancy of the chip; the 256 x 128 / 128 x 256 tiles
+#: lose more on long reductions (less reuse per loaded byte): profiles/gemm_r2.md
+BIG_SPEED = {5: 1.0, 6: 0.85, 7: 0.85}
+LONG_K = 8192
 
 
 def pick_tile(M: int, N: int) -> int:
@@ -50,15 +59,50 @@ def pick_tile(M: int, N: int) -> int:
     return 0
 
 
-def plan(P: int, M: int, N: int, K: int, cfg: Optional[int] = None):
-    """(tile cfg, splits, k_per_split) for a [P] x (M x K) . (K x N) problem: split the K
-    reduction when the output tiles alone give fewer than ~2 workgroups per CU."""
+def big_fits(M: int, N: int, K: int, cfg: int) -> bool:
+    bm, bn = TILES[cfg]
+    return M % bm == 0 and N % bn == 0 and K % 64 == 0
+
+
+def _plan_big(P: int, M: int, N: int, K: int):
+    """Best big tile by the fraction of its last wave of 256 workgroups it fills, weighted by
+    the tile's speed; None when no big tile divides the shape or fills the chip well (the big
+    kernel is persistent and never splits K: split-K partials measured 2-3x slower)."""
+    best = None
+    for cfg in BIG_TILES:
+        if not big_fits(M, N, K, cfg):
+            continue
+        bm, bn = TILES[cfg]
+        n = P * (M // bm) * (N // bn)
+        fill = n / (math.ceil(n / NUM_CU) * NUM_CU)
+        score = fill * BIG_SPEED[cfg] * (0.8 if cfg != 5 and K > LONG_K else 1.0)
+        if best is None or score > best[0]:
+            best = (score, cfg)
+    if best is None or best[0] < 0.6:
+        return None
+    return best[1], 1, K
+
+
+def plan(P: int, M: int, N: int, K: int, cfg: Optional[int] = None,
+         splits: Optional[int] = None):
+    """(tile cfg, splits, k_per_split) for a [P] x (M x K) . (K x N) problem: a big tile when it
+    divides the shape and fills the chip, else a small one with the K reduction split when the
+    output tiles alone give fewer than ~2 workgroups per CU."""
+    if cfg is None and splits is None:
+        big = _plan_big(P, M, N, K)
+        if big is not None:
+            return big
+    if cfg in BIG_TILES:
+        if big_fits(M, N, K, cfg) and (splits or 1) == 1:
+            return cfg, 1, K
+        cfg = None                    # the tile does not divide this shape, or split-K asked
     cfg = pick_tile(M, N) if cfg is None else cfg
     bm, bn = TILES[cfg]
     blocks = P * math.ceil(M / bm) * math.ceil(N / bn)
-    splits = 1
-    if blocks < 2 * NUM_CU and K >= 512:
-        splits = min(math.ceil(2 * NUM_CU / blocks), K // 256, 32)
+    if splits is None:
+        splits = 1
+        if blocks < 2 * NUM_CU and K >= 512:
+            splits = min(math.ceil(2 * NUM_CU / blocks), K // 256, 32)
     if splits <= 1:
         return cfg, 1, K
     kps = math.ceil(K / splits / 64) * 64
@@ -76,7 +120,8 @@ def _check_operand(t: torch.Tensor, name: str) -> None:
 
 
 def pgemm(a: torch.Tensor, b: torch.Tensor, ta: bool = False, tb: bool = False,
-          out: Optional[torch.Tensor] = None, cfg: Optional[int] = None) -> torch.Tensor:
+          out: Optional[torch.Tensor] = None, cfg: Optional[int] = None,
+          splits: Optional[int] = None) -> torch.Tensor:
     """``out[p] = op(a[p]) @ op(b[p])`` in bf16 with f32 accumulation on the MFMA kernel."""
     if a.device.type != "cuda":
         aa = a.transpose(1, 2) if ta else a
@@ -101,7 +146,7 @@ def pgemm(a: torch.Tensor, b: torch.Tensor, ta: bool = False, tb: bool = False,
     elif tuple(out.shape) != (P, M, N) or out.stride(2) != 1 or out.dtype != torch.bfloat16:
         raise ValueError(f"pgemm: out must be [P, M, N] = {(P, M, N)} bf16 row-major")
     _check_operand(out, "out")
-    cfg, splits, kps = plan(P, M, N, K, cfg)
+    cfg, splits, kps = plan(P, M, N, K, cfg, splits)
     part = (torch.empty(splits, P, M, N, dtype=torch.float32, device=a.device)
             if splits > 1 else None)
     _lib.check(_lib.get_lib().mopt_pgemm(
@@ -113,9 +158,10 @@ def pgemm(a: torch.Tensor, b: torch.Tensor, ta: bool = False, tb: bool = False,
 
 
 #: wide NN products (the LM's projections, N >= 256) go to hipBLASLt, which is correct for the
-#: NN layout and currently ~1.4x faster than pgemm there (scripts/gemm_bench.py); the backward's
-#: NT / TN products and every CNN product stay on pgemm
-LIBRARY_NN_MIN_N = 256
+#: NN layout and still ~1.1-1.4x faster there than the big-tile kernel (profiles/gemm_r2.md); the
+#: backward's NT / TN products and every CNN product run on pgemm.  ``MOPT_LIBRARY_NN=0`` keeps
+#: the forward on pgemm too.
+LIBRARY_NN_MIN_N = None if os.environ.get("MOPT_LIBRARY_NN") == "0" else 256
 
 
 def nn_forward(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:

@@ -51,9 +51,12 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--no-torch", action="store_true")
     ap.add_argument("--cfgs", default="", help="comma-separated tile configs to time as well")
+    ap.add_argument("--shapes", default="", help="only shapes whose name starts with this")
     args = ap.parse_args()
     rows = []
     for name, P, M, N, K, ta, tb in SHAPES:
+        if not name.startswith(args.shapes):
+            continue
         a = torch.randn(P, K, M, device="cuda").to(torch.bfloat16) if ta else \
             torch.randn(P, M, K, device="cuda").to(torch.bfloat16)
         b = torch.randn(P, N, K, device="cuda").to(torch.bfloat16) if tb else \

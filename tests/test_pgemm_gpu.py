@@ -3,7 +3,7 @@ every tile configuration, ragged edges, split-K, and the autograd wrapper used b
 import pytest
 import torch
 
-from metaopt_amd.ops.gemm import TILES, pbmm, pgemm, plan
+from metaopt_amd.ops.gemm import BIG_TILES, TILES, pbmm, pgemm, plan
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -33,10 +33,38 @@ def test_layouts_and_edges(ta, tb, P, M, N, K):
     _check(pgemm(a, b, ta=ta, tb=tb), A, B)
 
 
-@pytest.mark.parametrize("cfg", sorted(TILES))
+@pytest.mark.parametrize("cfg", sorted(c for c in TILES if c not in BIG_TILES))
 def test_every_tile_config(cfg):
     A, B, a, b = _operands(2, 264, 200, 136, False, True, seed=cfg)
     _check(pgemm(a, b, tb=True, cfg=cfg), A, B)
+
+
+@pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("cfg", BIG_TILES)
+def test_big_tiles_every_layout(cfg, ta, tb):
+    """The 8-wave direct-to-LDS kernel (swizzled k-contiguous and row-contiguous images) in
+    every operand layout; several K tiles so both LDS stages are used, distinct trials."""
+    A, B, a, b = _operands(3, 512, 512, 320, ta, tb, seed=10 + cfg)
+    _check(pgemm(a, b, ta=ta, tb=tb, cfg=cfg), A, B)
+
+
+@pytest.mark.parametrize("cfg", BIG_TILES)
+def test_big_tiles_persistent_and_strided_output(cfg):
+    """More tiles than workgroups (the persistent loop carries the next tile's first K-step
+    across the epilogue), a C written into a wider row stride, split-K falling back."""
+    A, B, a, b = _operands(2, 256, 256, 2048, True, False, seed=20 + cfg)
+    _check(pgemm(a, b, ta=True, cfg=cfg, splits=4), A, B)
+    wide = torch.zeros(2, 256, 384, dtype=torch.bfloat16, device=DEV)
+    _check(pgemm(a, b, ta=True, cfg=cfg, out=wide[:, :, :256]), A, B)
+    assert wide[:, :, 256:].abs().max().item() == 0     # nothing written past the view
+    A, B, a, b = _operands(40, 512, 256, 128, False, True, seed=40 + cfg)   # 160-640 tiles
+    _check(pgemm(a, b, tb=True, cfg=cfg), A, B)
+
+
+def test_big_tile_shape_guard():
+    """A big tile on a shape it does not divide falls back (never launches out of bounds)."""
+    A, B, a, b = _operands(1, 200, 256, 128, False, False, seed=30)
+    _check(pgemm(a, b, cfg=5), A, B)
 
 
 def test_split_k_reduction():
