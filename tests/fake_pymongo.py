@@ -152,10 +152,15 @@ class Collection:
     def _apply(self, doc, update):
         new = copy.deepcopy(doc)
         for op, fields in update.items():
-            if op != "$set":
+            if op == "$set":
+                for k, v in fields.items():
+                    _set(new, k, v)
+            elif op == "$inc":                  # MongoDB: a missing field counts as 0
+                for k, v in fields.items():
+                    cur = _get(new, k)
+                    _set(new, k, (0 if cur is _MISSING else cur) + v)
+            else:
                 raise errors.OperationFailure(f"unsupported update operator {op}")
-            for k, v in fields.items():
-                _set(new, k, v)
         self._check(new, skip=doc)
         doc.clear()
         doc.update(new)
