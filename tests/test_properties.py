@@ -246,7 +246,8 @@ def test_addition_and_deletion_are_mirror_images(ts, default):
 
 
 @SETTINGS
-@given(st.lists(st.floats(min_value=-10, max_value=10), min_size=1, max_size=10))
+@given(st.lists(st.floats(min_value=-10, max_value=10, exclude_max=True), min_size=1,
+                max_size=10))
 def test_prior_change_filters_by_the_target_prior(values):
     ts = [Trial(experiment="e", params=[{"name": "/x", "type": "real", "value": v}])
           for v in values]
@@ -316,9 +317,13 @@ def test_observed_results_keep_suggestions_valid(name, space, seed):
         pytest.skip(f"{name} not registered")
     algo = create_algo(space, {name: {"seed": seed}})
     rng = np.random.default_rng(seed)
-    for _ in range(3):
-        pts = algo.suggest(4) or []
-        assume(pts)
-        algo.observe(pts, [{"objective": float(rng.normal())} for _ in pts])
-    more = algo.suggest(2) or []
+    try:
+        for _ in range(3):
+            pts = algo.suggest(4) or []
+            assume(pts)
+            algo.observe(pts, [{"objective": float(rng.normal())} for _ in pts])
+        more = algo.suggest(2) or []
+    except RuntimeError as exc:     # a tiny discrete space is exhausted (reference behaviour)
+        assume("already existing" not in str(exc))
+        raise
     assert all(p in space for p in more)
