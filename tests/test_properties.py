@@ -302,7 +302,11 @@ def test_sampling_algorithms_suggest_inside_the_space(name, space, seed):
     if name not in ALGORITHMS:
         pytest.skip(f"{name} not registered")
     algo = create_algo(space, {name: {"seed": seed}})
-    pts = algo.suggest(3) or []
+    try:
+        pts = algo.suggest(3) or []
+    except RuntimeError as exc:     # a tiny discrete space is exhausted (reference behaviour)
+        assume("already existing" not in str(exc))
+        raise
     assert pts, name
     assert all(p in space for p in pts)
     twin = create_algo(space, {name: {"seed": seed}})
