@@ -20,7 +20,7 @@ from . import build as _build
 
 _LOCK = threading.Lock()
 _LIB = None
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 c_void_p = ctypes.c_void_p
 c_int = ctypes.c_int
@@ -37,6 +37,7 @@ _SIGNATURES = {
                       c_int),
     "mopt_mlp_bwd": ([c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                       c_void_p, c_void_p, c_int, c_int, c_void_p], c_int),
+    "mopt_mlp_step": ([c_void_p, c_void_p, c_void_p, c_void_p], c_int),
 }
 
 _OPTIONAL_SIGNATURES: dict = {}

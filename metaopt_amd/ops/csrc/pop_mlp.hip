@@ -653,7 +653,7 @@ __global__ __launch_bounds__(256) void mlp_init_kernel(const InitDesc* __restric
 // ------------------------------------------------------------------------------------------------
 extern "C" {
 
-int mopt_abi_version() { return 7; }
+int mopt_abi_version() { return 8; }
 
 // flags: 1 = zero the AdamW second moment, 2 = the momentum buffer is bf16
 int mopt_mlp_init(const void* descs, int n_desc, void* plo, void* p16, void* m32, void* v32,
@@ -710,6 +710,46 @@ int mopt_mlp_bwd(const void* tls, const void* work, int n_work, const void* xb, 
                        (const TrialHP*)hp, flags);
   }
   return (int)hipGetLastError();
+}
+
+// One whole train step of a group of trials (forward of every layer, fused loss, fused backward
+// + optimizer of every layer, top-down) in ONE host call: the per-step host cost of the sweep is
+// one C call instead of 2L bound-method calls.  The argument block is built once per work-table
+// refresh (metaopt_amd/ops/population.py, _MlpStep mirrors it); x / y change every step.
+struct MlpStep {
+  const void* tls;
+  const void* fwd[8];
+  const void* bwd[8];
+  int32_t n_fwd[8];
+  int32_t n_bwd[8];
+  int32_t L, rb, drop, opt;
+  void *plo, *p16, *m32, *v32, *act, *grad, *hp, *loss, *correct;
+  float inv_b;
+  int32_t pad;
+};
+
+int mopt_mlp_step(const MlpStep* s, const void* x, const void* y, void* stream) {
+  if (s == nullptr || s->L < 1 || s->L > 8 || s->rb < 1) return (int)hipErrorInvalidValue;
+  const int L = s->L;
+  int err;
+  for (int l = 0; l < L - 1; ++l) {
+    err = mopt_mlp_fwd(s->tls, s->fwd[l], s->n_fwd[l], s->rb, l == 0 ? x : s->act, s->plo,
+                       s->p16, s->act, s->hp, 1u, l, kRelu | (s->drop ? kDropout : 0), stream);
+    if (err) return err;
+  }
+  const int ce = kWriteGrad | kCountStep | (s->rb == 1 ? kStoreStats : 0);
+  err = mopt_mlp_fwd_ce(s->tls, s->fwd[L - 1], s->n_fwd[L - 1], s->rb, L == 1 ? x : s->act,
+                        s->plo, s->p16, y, s->grad, s->loss, s->correct, s->hp, s->inv_b, ce,
+                        stream);
+  if (err) return err;
+  for (int l = L - 1; l >= 0; --l) {
+    int flags = kUpdateBias;
+    if (l > 0) flags |= kHasDx | (s->drop ? kInDropout : 0);
+    err = mopt_mlp_bwd(s->tls, s->bwd[l], s->n_bwd[l], l == 0 ? x : s->act, s->grad, s->plo,
+                       s->p16, s->m32, s->v32, s->hp, s->opt, flags, stream);
+    if (err) return err;
+  }
+  return 0;
 }
 
 }  // extern "C"

@@ -23,6 +23,7 @@ Backends: ``"hip"`` (gfx950 kernels, the only GPU path; never falls back silentl
 """
 from __future__ import annotations
 
+import ctypes
 import dataclasses
 import math
 import os
@@ -47,6 +48,18 @@ assert TL_DTYPE.itemsize == 64 and HP_DTYPE.itemsize == 32 and INIT_DTYPE.itemsi
 TILE = 64
 FWD_RELU, FWD_DROPOUT, FWD_WRITE_GRAD, FWD_STORE_STATS, FWD_COUNT_STEP = 1, 2, 4, 8, 16
 BWD_HAS_DX, BWD_IN_DROPOUT, BWD_UPDATE_BIAS = 1, 2, 4
+
+
+class _MlpStep(ctypes.Structure):
+    """Argument block of ``mopt_mlp_step`` (csrc/pop_mlp.hip ``MlpStep``): one host call
+    launches a group's whole train step; built once per work-table refresh."""
+    _fields_ = [("tls", ctypes.c_void_p), ("fwd", ctypes.c_void_p * 8),
+                ("bwd", ctypes.c_void_p * 8), ("n_fwd", ctypes.c_int32 * 8),
+                ("n_bwd", ctypes.c_int32 * 8), ("L", ctypes.c_int32), ("rb", ctypes.c_int32),
+                ("drop", ctypes.c_int32), ("opt", ctypes.c_int32)] + \
+               [(n, ctypes.c_void_p) for n in ("plo", "p16", "m32", "v32", "act", "grad", "hp",
+                                               "loss", "correct")] + \
+               [("inv_b", ctypes.c_float), ("pad", ctypes.c_int32)]
 OPTIMIZERS = {"sgd": 0, "adamw": 1}
 
 
@@ -123,6 +136,11 @@ def _lpt_order(cost: np.ndarray, n_xcd: int = 8) -> np.ndarray:
     pos = np.arange(n)
     share = np.where(pos < r * (q + 1), pos // (q + 1), r + (pos - r * (q + 1)) // max(q, 1))
     return np.lexsort((-cost, share))
+
+
+def _lib_sync_check() -> bool:
+    from . import _lib
+    return _lib.SYNC_CHECK
 
 
 class _SplitBuffer:
@@ -684,7 +702,25 @@ class PopulationMLP:
                          "correct": self.correct.data_ptr(), "tl": tb["tl"].data_ptr(),
                          "fwd": [w.data_ptr() for w in tb["fwd"]],
                          "bwd": [w.data_ptr() for w in tb["bwd"]]}
+            for part in self._parts:
+                part["step"] = self._step_args(part)
         self._dirty = False
+
+    def _step_args(self, part) -> "_MlpStep":
+        """``mopt_mlp_step`` argument block of one trial group (pointers of this refresh)."""
+        P, L = self._ptr, self.L
+        a = _MlpStep()
+        a.tls = P["tl"]
+        for l in range(L):
+            a.fwd[l], a.bwd[l] = part["fwd"][l], part["bwd"][l]
+            a.n_fwd[l], a.n_bwd[l] = part["n_fwd"][l], part["n_bwd"][l]
+        a.L, a.rb, a.drop = L, self.batch_size // 128, int(self._any_dropout)
+        a.opt = 2 if self.momentum_dtype == "bf16" else OPTIMIZERS[self.optimizer]
+        for n in ("plo", "p16", "m32", "v32", "act", "grad", "hp", "loss", "correct"):
+            setattr(a, n, P[n])
+        a.inv_b = 1.0 / self.batch_size
+        part["step_ptr"] = ctypes.addressof(a)
+        return a
 
     def _join(self) -> None:
         """Order the main stream after every side stream's queued work (no host wait)."""
@@ -773,7 +809,12 @@ class PopulationMLP:
             self._launch_step(lib, P, part, xp, y.data_ptr(), rb, stream.cuda_stream, check)
 
     def _launch_step(self, lib, P, part, xp, yp, rb, stream, check) -> None:
-        """The 2L launches of one train step for one group of trials on ``stream``."""
+        """The 2L launches of one train step for one group of trials on ``stream``: one host
+        call (``mopt_mlp_step``), or one call per kernel under MOPT_SYNC_CHECK (each launch
+        checked by name)."""
+        if not _lib_sync_check():
+            check(lib.mopt_mlp_step(part["step_ptr"], xp, yp, stream), "mlp_step")
+            return
         L = self.L
         ce_flags = FWD_WRITE_GRAD | FWD_COUNT_STEP | (FWD_STORE_STATS if rb == 1 else 0)
         drop = self._any_dropout

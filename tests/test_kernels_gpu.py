@@ -129,6 +129,31 @@ def test_stream_groups_equal_one_stream(data, streams):
             assert torch.equal(wa, wb)
 
 
+@pytest.mark.parametrize("mdt", ["fp32", "bf16"])
+def test_one_call_step_equals_per_kernel_launches(data, mdt, monkeypatch):
+    """``mopt_mlp_step`` (the whole step in one host call) launches exactly the per-kernel
+    sequence: bitwise-equal weights and losses after several steps, with dropout members."""
+    from metaopt_amd.ops import _lib
+    pops = []
+    for _ in range(2):
+        p = PopulationMLP(6, max_width=256, eval_batch=256, device="cuda", backend="hip",
+                          momentum_dtype=mdt)
+        for i, c in enumerate(CONFIGS):
+            p.set_member(i + 1, c)
+        pops.append(p)
+    for step in range(5):
+        monkeypatch.setattr(_lib, "SYNC_CHECK", False)
+        pops[0].train_step(*data.batch(step))
+        monkeypatch.setattr(_lib, "SYNC_CHECK", True)     # one checked launch per kernel
+        pops[1].train_step(*data.batch(step))
+    monkeypatch.setattr(_lib, "SYNC_CHECK", False)
+    a, b = pops
+    assert np.array_equal(a.train_loss(), b.train_loss(), equal_nan=True)
+    for s in a.active_slots():
+        for (wa, _), (wb, _) in zip(a.layer_views(s), b.layer_views(s)):
+            assert torch.equal(wa, wb)
+
+
 def test_population_equals_independent_runs(data):
     """A member trained inside a population equals the same trial trained alone (bitwise)."""
     full, _ = _pair()
