@@ -279,10 +279,23 @@ __global__ __launch_bounds__(256) void pgemm_kernel(const GemmArgs g) {
 constexpr int kGroupM = MOPT_GEMM_GROUP_M;
 
 typedef __attribute__((address_space(3))) void lds_void;
-typedef __attribute__((address_space(1))) void glb_void;
 
 __device__ __forceinline__ int kc_swz(int row) { return (row >> 1) & 7; }
 __device__ __forceinline__ int rc_swz(int kr) { return ((kr & 3) << 1) | (((kr >> 3) & 1) << 3); }
+
+// global_load_lds_dwordx4 as inline asm (M0 = the wave's LDS destination).  Through the builtin,
+// hipcc (ROCm 7.2) tracks the fill as an LDS DMA and, unable to separate it from the transposed
+// reads (ds_read_b64_tr_b16) of the other stage, waits vmcnt(0) before them -- draining the next
+// tile's fills at the top of every K-step, which serialised loads and MFMAs on the NN / TN
+// layouts (20-30 % slower than NT).  Issued from asm the fills are invisible to the waitcnt pass;
+// the K loop waits for them itself (vmcnt(0) before its barrier).
+__device__ __forceinline__ void glds16(const bf16_t* src, bf16_t* lds_dst) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((lds_void*)lds_dst));
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off"
+               :
+               : "v"(src), "s"(m0)
+               : "memory", "m0");
+}
 
 template <int ROWS, bool KCONTIG>
 struct GImg {
@@ -307,7 +320,7 @@ struct GImg {
         const int kr = blk * (64 / CPR) + lane / CPR, c = lane % CPR;
         src = base + (int64_t)(k0 + kr) * ld + row0 + 8 * (c ^ rc_swz(kr));
       }
-      __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)(img + blk * 512), 16, 0, 0);
+      glds16(src, img + blk * 512);
     }
   }
 

@@ -157,11 +157,10 @@ def pgemm(a: torch.Tensor, b: torch.Tensor, ta: bool = False, tb: bool = False,
     return out
 
 
-#: wide NN products (the LM's projections, N >= 256) go to hipBLASLt, which is correct for the
-#: NN layout and still ~1.1-1.4x faster there than the big-tile kernel (profiles/gemm_r2.md); the
-#: backward's NT / TN products and every CNN product run on pgemm.  ``MOPT_LIBRARY_NN=0`` keeps
-#: the forward on pgemm too.
-LIBRARY_NN_MIN_N = None if os.environ.get("MOPT_LIBRARY_NN") == "0" else 256
+#: every product runs on pgemm: the big-tile kernel is at parity with hipBLASLt on the LM's NN
+#: projections (profiles/gemm_r2.md).  ``MOPT_LIBRARY_NN=1`` sends the wide NN forwards
+#: (N >= 256) to ``torch.bmm`` instead, for A/B comparisons.
+LIBRARY_NN_MIN_N = 256 if os.environ.get("MOPT_LIBRARY_NN") == "1" else None
 
 
 def nn_forward(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:

@@ -7,7 +7,7 @@ ROOT=$(pwd)
 mkdir -p "$OUT"
 timeout -k 10 400 python -u -m pytest tests/test_lm_gpu.py tests/test_resnet_gpu.py tests/test_hyper.py tests/test_pgemm_ad.py -m gpu -x -q --timeout 120 --timeout-method thread > "$OUT/pytest.log" 2>&1
 timeout -k 10 300 python scripts/bench_configs.py --config lm-125m --steps 20 --warmup 10 > "$OUT/lm.json" 2> "$OUT/lm.err"
-MOPT_LIBRARY_NN=0 timeout -k 10 300 python scripts/bench_configs.py --config lm-125m --steps 20 --warmup 10 > "$OUT/lm_nolib.json" 2> "$OUT/lm_nolib.err"
+MOPT_LIBRARY_NN=1 timeout -k 10 300 python scripts/bench_configs.py --config lm-125m --steps 20 --warmup 10 > "$OUT/lm_lib.json" 2> "$OUT/lm_lib.err"
 timeout -k 10 300 python scripts/bench_configs.py --config resnet20 --steps 40 --warmup 10 > "$OUT/resnet.json" 2> "$OUT/resnet.err"
 timeout -k 10 300 python scripts/bench_configs.py --config hyper --steps 3 > "$OUT/hyper.json" 2> "$OUT/hyper.err"
 cd /tmp && export TMPDIR=/tmp

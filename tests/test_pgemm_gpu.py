@@ -102,12 +102,15 @@ def test_pbmm_autograd_and_grad_out():
     assert w.grad is buf           # written in place, never re-accumulated by autograd
 
 
+@pytest.mark.parametrize("library", [None, 256])
 @pytest.mark.parametrize("K,N", [(768, 2304), (768, 4096), (2048, 768), (768, 32000)])
-def test_library_nn_forward_lm_shapes(K, N):
-    """Regression guard of the dispatch in ops/gemm.py: the wide NN forwards that go to the
-    library (``nn_forward``, N >= LIBRARY_NN_MIN_N) are right on the installed stack for the
-    LM's projection shapes (scripts/check_bmm.py found its *transposed* batched GEMM wrong)."""
+def test_nn_forward_lm_shapes(K, N, library, monkeypatch):
+    """The LM's NN projection forwards (``nn_forward``) on the big-tile kernel (default) and on
+    the library (``MOPT_LIBRARY_NN=1``; scripts/check_bmm.py found the library's *transposed*
+    batched GEMM wrong, this guards its NN form on these shapes)."""
+    from metaopt_amd.ops import gemm
     from metaopt_amd.ops.gemm import nn_forward
+    monkeypatch.setattr(gemm, "LIBRARY_NN_MIN_N", library)
     P, M = 2, 1024
     g = torch.Generator(device=DEV).manual_seed(K + N)
     x = (torch.randn(P, M, K, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
