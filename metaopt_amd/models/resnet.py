@@ -5,10 +5,10 @@ Architecture (He et al. 2016, CIFAR variant): 3x3 conv 16 -> 3 stages x 3 basic 
 64 channels; stride 2 at stages 2 and 3 with the parameter-free "option A" shortcut: subsample +
 zero-pad channels) -> global average pool -> linear 64 -> 10; ~0.27M parameters per trial.
 Activations are NHWC bf16 with the population folded into the batch; images carry 8 channels
-(3 real + 5 zero) so every kernel moves 16-byte vectors.  Convolutions: implicit GEMMs on the
-population MFMA kernel (ops/conv.py -> csrc/pgemm.hip: the 3x3 taps are gathered while the
-operand tiles are staged, forward / data-gradient / weight-gradient, no im2col buffer);
-BatchNorm (+ residual + ReLU) fused HIP kernels with per-trial batch
+(3 real + 5 zero) so every kernel moves 16-byte vectors.  Convolutions: direct halo-tiled MFMA
+kernels (ops/conv.py -> csrc/conv_direct.hip: forward with the BatchNorm batch statistics in its
+epilogue, stride-1 data gradient, weight gradient), the implicit GEMM of csrc/pgemm.hip for the
+stride-2 data gradient; BatchNorm (+ residual + ReLU) fused HIP kernels with per-trial batch
 and running statistics; SGD-momentum with per-trial lr / momentum / weight decay (fused K5).
 """
 from __future__ import annotations
@@ -79,12 +79,12 @@ class PopulationResNet(FlatPopulation):
         return int(x.shape[0])
 
     # ------------------------------------------------------------------ forward
-    def _bn(self, name, x, train, res=None, relu=True):
-        P = self.capacity
-        C = x.shape[-1]
-        running = self.A[f"{name}.running"].view(P, 2, C)
-        return cops.bn_act(x, self.W[f"{name}.g"], self.W[f"{name}.b"], running, P, train,
-                           res=res, relu=relu)
+    def _conv_bn(self, name, x, stride, train, res=None, relu=True):
+        P, W = self.capacity, self.W
+        w = W[f"{name}.w"]
+        running = self.A[f"{name}.running"].view(P, 2, w.shape[-1])
+        return cops.conv_bn_act(x, w, W[f"{name}.g"], W[f"{name}.b"], running, P, stride, train,
+                                res=res, relu=relu)
 
     @staticmethod
     def _shortcut(x, cout, stride):
@@ -99,14 +99,14 @@ class PopulationResNet(FlatPopulation):
         B = x.shape[0]
         it = iter(self.layout)
         name, _, cout, stride = next(it)
-        h = self._bn(name, cops.conv3x3(h, W[f"{name}.w"], P, stride), train)
+        h = self._conv_bn(name, h, stride, train)
         for si in range(len(STAGES)):
             for b in range(self.blocks):
                 n1, _, c1, s1 = next(it)
                 n2, _, c2, _ = next(it)
                 r = self._shortcut(h, c2, s1)
-                t = self._bn(n1, cops.conv3x3(h, W[f"{n1}.w"], P, s1), train)
-                h = self._bn(n2, cops.conv3x3(t, W[f"{n2}.w"], P, 1), train, res=r)
+                t = self._conv_bn(n1, h, s1, train)
+                h = self._conv_bn(n2, t, 1, train, res=r)
         feat = h.view(P, B, -1, h.shape[-1]).float().mean(2)            # [P, B, 64]
         logits = torch.baddbmm(W["fc.b"].float()[:, None, :], feat,
                                W["fc.w"].float())[..., :NCLS]           # [P, B, 10]

@@ -15,6 +15,7 @@ numerics oracle of tests/test_resnet_gpu.py.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -25,10 +26,16 @@ c_void_p, c_int, c_float, c_int64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_floa
 
 _lib.register_signatures({
     "mopt_bn_fwd": ([c_void_p] * 8 + [c_int, c_int64, c_int, c_float, c_float, c_int, c_int,
-                                     c_void_p], c_int),
+                                     c_int, c_void_p], c_int),
     "mopt_bn_bwd": ([c_void_p] * 8 + [c_int, c_int64, c_int, c_int, c_void_p], c_int),
     "mopt_pconv": ([c_int] + [c_void_p] * 4 + [c_int] * 10 + [c_void_p], c_int),
+    "mopt_dconv": ([c_int] + [c_void_p] * 4 + [c_int] * 6 + [c_void_p], c_int),
+    "mopt_dconv_wgrad_splits": ([c_int] * 6, c_int),
 })
+
+_NOT_SUPPORTED = 801   # hipErrorNotSupported: no direct-conv instantiation for the shape
+# MOPT_CONV_IMPLICIT=1 routes every convolution through the implicit GEMM (A/B and fallback check)
+_DIRECT = os.environ.get("MOPT_CONV_IMPLICIT", "0") != "1"
 
 
 def _call(name, *args):
@@ -92,7 +99,29 @@ def _pow2(v):
     return v >= 1 and (v & (v - 1)) == 0
 
 
-def _pconv(kind, a, b, out, P, Bn, H, W, Ci, Co, stride):
+def _dconv(kind, a, b, out, P, Bn, H, W, Ci, Co, stride, sums=None):
+    """Direct (halo-tiled) convolution kernels of csrc/conv_direct.hip; False when the shape has
+    no instantiation (the caller then runs the implicit GEMM)."""
+    if not _DIRECT or H != W:
+        return False
+    lib = _lib.get_lib()
+    aux = sums
+    if kind == 2:
+        nb = lib.mopt_dconv_wgrad_splits(P, Bn, H, Ci, Co, stride)
+        if nb <= 0:
+            return False
+        aux = torch.empty(nb * P * 9 * Ci * Co, dtype=torch.float32, device=out.device)
+    rc = lib.mopt_dconv(kind, a.data_ptr(), b.data_ptr(), out.data_ptr(),
+                        0 if aux is None else aux.data_ptr(), P, Bn, H, Ci, Co, stride, _s(out))
+    if rc == _NOT_SUPPORTED:
+        return False
+    _lib.check(rc, "mopt_dconv")
+    return True
+
+
+def _pconv(kind, a, b, out, P, Bn, H, W, Ci, Co, stride, sums=None):
+    if _dconv(kind, a, b, out, P, Bn, H, W, Ci, Co, stride, sums):
+        return out, sums is not None
     OH, OW = out_hw(H, stride), out_hw(W, stride)
     M, N, K = {0: (Bn * OH * OW, Co, 9 * Ci), 1: (Bn * H * W, Ci, 9 * Co),
                2: (9 * Ci, Co, Bn * OH * OW)}[kind]
@@ -104,18 +133,23 @@ def _pconv(kind, a, b, out, P, Bn, H, W, Ci, Co, stride):
     _call("mopt_pconv", kind, a.data_ptr(), b.data_ptr(), out.data_ptr(),
           0 if part is None else part.data_ptr(), P, Bn, H, W, Ci, Co, stride, cfg, splits, kps,
           _s(out))
-    return out
+    return out, False
 
 
 class _Conv3x3(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, P, stride, grad_out):
+    def forward(ctx, x, w, P, stride, grad_out, stats=None):
         N, H, W, Ci = x.shape
         Co = w.shape[-1]
         Bn = N // P
         y = torch.empty(N, out_hw(H, stride), out_hw(W, stride), Co, dtype=x.dtype,
                         device=x.device)
-        _pconv(0, x, w, y, P, Bn, H, W, Ci, Co, stride)
+        # stats = [zeroed f32 sums [P, 2, Co], False]: the direct kernel adds the BatchNorm
+        # batch sums of y and sets the flag
+        _, done = _pconv(0, x, w, y, P, Bn, H, W, Ci, Co, stride,
+                         None if stats is None else stats[0])
+        if stats is not None:
+            stats[1] = done
         ctx.save_for_backward(x, w)
         ctx.meta = (P, Bn, H, W, Ci, Co, stride)
         ctx.grad_out = grad_out
@@ -136,11 +170,13 @@ class _Conv3x3(torch.autograd.Function):
             else:
                 dw = torch.empty_like(w)
                 _pconv(2, x, dy, dw, P, Bn, H, W, Ci, Co, stride)
-        return dx, dw, None, None, None
+        return dx, dw, None, None, None, None
 
 
-def conv3x3(x, w, P, stride):
-    """Population 3x3 convolution: x [P*B, H, W, Cin] bf16, w [P, 9 Cin, Cout]."""
+def conv3x3(x, w, P, stride, stats=None):
+    """Population 3x3 convolution: x [P*B, H, W, Cin] bf16, w [P, 9 Cin, Cout].  ``stats`` (HIP
+    only): ``[sums, False]`` with zeroed f32 sums [P, 2, Cout]; when the direct kernel ran, the
+    per-trial channel sums of the output and of its square were added and the flag is True."""
     if x.device.type != "cuda":
         return conv3x3_ref(x, w, P, stride)
     N, H, W, C = x.shape
@@ -150,21 +186,23 @@ def conv3x3(x, w, P, stride):
         raise ValueError(f"conv3x3: needs power-of-two H, W, channels (>= 8) and w [P, 9C, Co]; "
                          f"got x {tuple(x.shape)} w {tuple(w.shape)} P {P}")
     grad_out = w.grad if (w.requires_grad and w.is_leaf and w.grad is not None) else None
-    return _Conv3x3.apply(x.contiguous(), w.contiguous(), P, stride, grad_out)
+    return _Conv3x3.apply(x.contiguous(), w.contiguous(), P, stride, grad_out, stats)
 
 
 class _BNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, res, running, P, train, relu, eps, momentum):
+    def forward(ctx, x, gamma, beta, res, running, P, train, relu, eps, momentum, sums=None):
         C = x.shape[-1]
         M = x.numel() // (P * C)
         y = torch.empty_like(x)
         stat = torch.empty(P, 2, C, dtype=torch.float32, device=x.device)
-        sums = torch.empty(P, 2, C, dtype=torch.float32, device=x.device)
+        ready = sums is not None and train
+        if not ready:
+            sums = torch.empty(P, 2, C, dtype=torch.float32, device=x.device)
         _call("mopt_bn_fwd", x.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
               0 if res is None else res.data_ptr(), y.data_ptr(), stat.data_ptr(),
               running.data_ptr(), sums.data_ptr(), P, M, C, eps, momentum, int(train), int(relu),
-              _s(x))
+              int(ready), _s(x))
         ctx.save_for_backward(x, y, stat, gamma)
         ctx.meta = (P, M, C, relu, res is not None)
         return y
@@ -182,13 +220,29 @@ class _BNAct(torch.autograd.Function):
               sums.data_ptr(), P, M, C, int(relu), _s(x))
         dgamma = sums[:, 1].to(gamma.dtype)
         dbeta = sums[:, 0].to(gamma.dtype)
-        return dx, dgamma, dbeta, dres, None, None, None, None, None, None
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None
 
 
-def bn_act(x, gamma, beta, running, P, train, res=None, relu=True, eps=1e-5, momentum=0.1):
-    """y = relu?(BN(x) + res?) per trial; ``running`` [P, 2, C] f32 updated when training."""
+def bn_act(x, gamma, beta, running, P, train, res=None, relu=True, eps=1e-5, momentum=0.1,
+           sums=None):
+    """y = relu?(BN(x) + res?) per trial; ``running`` [P, 2, C] f32 updated when training.
+    ``sums``: precomputed f32 [P, 2, C] batch sums of x and x^2 (the producing convolution's
+    epilogue) -- the statistics pass is skipped."""
     if x.device.type != "cuda":
         return bn_act_ref(x, gamma, beta, running, P, train, res, relu, eps, momentum)
     return _BNAct.apply(x.contiguous(), gamma.contiguous(), beta.contiguous(),
                         None if res is None else res.contiguous(), running, P, train, relu, eps,
-                        momentum)
+                        momentum, sums)
+
+
+def conv_bn_act(x, w, gamma, beta, running, P, stride, train, res=None, relu=True):
+    """relu?(BN(conv3x3(x, w)) + res?): on the HIP path the convolution's epilogue produces the
+    BatchNorm batch statistics (no separate reduction pass over the conv output)."""
+    if x.device.type != "cuda":
+        return bn_act_ref(conv3x3_ref(x, w, P, stride), gamma, beta, running, P, train, res,
+                          relu)
+    stats = [torch.zeros(P, 2, w.shape[-1], dtype=torch.float32, device=x.device), False] \
+        if train else None
+    y = conv3x3(x, w, P, stride, stats)
+    return bn_act(y, gamma, beta, running, P, train, res=res, relu=relu,
+                  sums=stats[0] if stats is not None and stats[1] else None)

@@ -1,0 +1,409 @@
+// Direct 3x3 convolutions of the population ResNet (north-star kernel K3) for the narrow
+// channel counts of CIFAR ResNets (8..64): halo-tiled in LDS, weights register-resident.
+//
+// Why not the implicit GEMM of pgemm.hip: with C <= 64 the GEMM's K = 9 C is gathered tap by
+// tap, so every input pixel is fetched 9 times (from L2) and every workgroup re-derives its
+// addresses per 16-byte chunk; the layers ran at ~4x their HBM time.  Here a workgroup owns a
+// band of NPX output pixels (TR output rows of one image, or IMGS whole images when an image is
+// smaller than the band), stages the input halo band ((TR-1)*S + 3 rows x (OW-1)*S + 3 columns
+// x CI, zero-padded) in LDS ONCE, and runs all 9 taps against it.  Workgroups are persistent
+// over the bands of one trial, so each wave loads its slice of that trial's weights into
+// registers once (as MFMA B fragments: one 16-column slice of CO per wave) and streams bands.
+//
+//   dconv_fwd_kernel    y = conv(x, w)    (+ per (trial, channel) sum / sum^2 of the bf16 output
+//                       accumulated across bands and added once per wave: the BatchNorm batch
+//                       statistics, so the BN forward skips its reduction pass)
+//                       also the stride-1 data gradient dx = conv(dy, flip(w)^T) (DG mode: the
+//                       B fragments are the tap-flipped, channel-transposed weights)
+//   dconv_wgrad_kernel  partial dW = sum over a trial's bands of im2col(x)^T . dy, both operands
+//                       read from LDS with the transposing ds_read_b64_tr_b16, f32 partials per
+//                       persistent workgroup, summed + rounded by dconv_reduce_kernel.
+//
+// MFMA v_mfma_f32_16x16x32_bf16: lane l holds A[row l&15][k 8(l>>4)..+7], B[k ..][col l&15],
+// C[row 4(l>>4)+r][col l&15] (common.h).  Forward: rows = output pixels, k = tap*CI + c, cols =
+// output channels.  Weight gradient: rows = tap*CI + c, k = output pixels, cols = CO.
+// Preconditions (host-checked): square power-of-two images, OW <= NPX, CI in {8,16,32,64},
+// CO in {16,32,64}, stride 1 or 2.
+#include "common.h"
+
+using namespace mopt;
+
+namespace {
+
+struct Geom {
+  int Bn;          // images per trial
+  int H, OH;       // input / output side (square)
+  int owl;         // log2 OW
+  int TR, IMGS;    // output rows per band, images per band
+  int TRI, WI;     // halo rows / columns
+  int rpil;        // log2 (pixels per image in a band) = log2(TR * OW)
+  int tpi;         // bands per image
+  int tiles;       // bands per trial
+  int nb;          // persistent workgroups per trial
+};
+
+template <int CI, int S>
+__device__ __forceinline__ void load_halo(bf16_t* hs, const bf16_t* __restrict__ x,
+                                          const Geom& g, int b0, int oy0) {
+  constexpr int CC = CI / 8;
+  const int n = g.IMGS * g.TRI * g.WI * CC;
+  for (int c = threadIdx.x; c < n; c += 256) {
+    const int cc = c % CC;
+    int t = c / CC;
+    const int hc = t % g.WI;
+    t /= g.WI;
+    const int hr = t % g.TRI, img = t / g.TRI;
+    const int iy = oy0 * S - 1 + hr, ix = hc - 1, b = b0 + img;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (b < g.Bn && iy >= 0 && iy < g.H && ix >= 0 && ix < g.H)
+      v = *(const uint4*)(x + (((int64_t)b * g.H + iy) * g.H + ix) * CI + 8 * cc);
+    *(uint4*)(hs + 8 * c) = v;
+  }
+}
+
+// halo offset of output pixel pl of a band (tap (0, 0), channel 0)
+template <int CI, int S>
+__device__ __forceinline__ int pix_base(const Geom& g, int pl) {
+  const int img = pl >> g.rpil, rem = pl & ((1 << g.rpil) - 1);
+  const int ly = rem >> g.owl, ox = rem & ((1 << g.owl) - 1);
+  return ((img * g.TRI + ly * S) * g.WI + ox * S) * CI;
+}
+
+// halo offset of tap k / CI, channel k % CI (tap clamped to 8: padded k rows meet zero weights)
+template <int CI>
+__device__ __forceinline__ int tap_off(const Geom& g, int k) {
+  const int tap = min(k / CI, 8), c = k % CI;
+  const int kh = tap / 3, kw = tap - 3 * kh;
+  return (kh * g.WI + kw) * CI + c;
+}
+
+template <int CI, int CO, int NPX>
+__global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict__ x,
+                                                        const bf16_t* __restrict__ w,
+                                                        bf16_t* __restrict__ y,
+                                                        float* __restrict__ sums, const Geom g,
+                                                        int S2, int dg) {
+  constexpr int KS = (9 * CI + 31) / 32;  // 32-wide k steps (k = tap * CI + c)
+  constexpr int WN = CO / 16, WM = 4 / WN;
+  constexpr int MFW = NPX / 16 / WM;      // 16-pixel fragments per wave
+  constexpr int LSC = CO + 8;
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  const int halo = g.IMGS * g.TRI * g.WI * CI;
+  bf16_t* hs = smem;
+  bf16_t* cs = smem + halo;
+
+  const int p = blockIdx.x / g.nb, blk = blockIdx.x % g.nb;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 15, gq = lane >> 4;
+  const int wm = wave / WN, wn = wave % WN;
+  const int n = 16 * wn + li;
+  const int64_t wbatch = (int64_t)9 * CI * CO;
+  const bf16_t* wp = w + p * wbatch;
+
+  // this wave's B fragments for every k step
+  bf16x8 wr[KS];
+#pragma unroll
+  for (int j = 0; j < KS; ++j) {
+    const int k0 = 32 * j + 8 * gq;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (k0 < 9 * CI) {
+      if (dg) {  // W'[tap' CI + c][n] = W[(8 - tap') CO + n][c]  (W stored [9 CO][CI] here)
+        const int tp = k0 / CI, c = k0 % CI;
+        v = *(const uint4*)(wp + ((int64_t)(8 - tp) * CO + n) * CI + c);
+      } else {   // W[k][n], stored [9 CI][CO]
+        uint32_t e[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) e[i] = wp[(int64_t)(k0 + i) * CO + n];
+        v = make_uint4(e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16),
+                       e[6] | (e[7] << 16));
+      }
+    }
+    wr[j] = __builtin_bit_cast(bf16x8, v);
+  }
+
+  const int64_t x_batch = (int64_t)g.Bn * g.H * g.H * CI;
+  const int64_t y_batch = (int64_t)g.Bn * g.OH * (1 << g.owl) * CO;
+  const bf16_t* xp = x + p * x_batch;
+  bf16_t* yp = y + p * y_batch;
+  const int ppi = 1 << g.rpil;  // band pixels per image
+
+  float s1 = 0.f, s2 = 0.f;
+  for (int t = blk; t < g.tiles; t += g.nb) {
+    const int b0 = (t / g.tpi) * g.IMGS, oy0 = (t % g.tpi) * g.TR;
+    if (S2) load_halo<CI, 2>(hs, xp, g, b0, oy0);
+    else load_halo<CI, 1>(hs, xp, g, b0, oy0);
+    __syncthreads();
+
+    f32x4 acc[MFW];
+    int pb[MFW];
+#pragma unroll
+    for (int i = 0; i < MFW; ++i) {
+      acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int pl = (wm * MFW + i) * 16 + li;
+      pb[i] = S2 ? pix_base<CI, 2>(g, pl) : pix_base<CI, 1>(g, pl);
+    }
+#pragma unroll
+    for (int j = 0; j < KS; ++j) {
+      const int to = tap_off<CI>(g, 32 * j + 8 * gq);
+#pragma unroll
+      for (int i = 0; i < MFW; ++i) acc[i] = mfma16(lds_frag(hs + pb[i] + to), wr[j], acc[i]);
+    }
+
+    const int valid = min(NPX, (g.Bn - b0) * ppi);
+#pragma unroll
+    for (int i = 0; i < MFW; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = (wm * MFW + i) * 16 + 4 * gq + r;
+        const bf16_t v = f2bf(acc[i][r]);
+        cs[row * LSC + n] = v;
+        if (row < valid) {
+          const float f = bf2f(v);
+          s1 += f;
+          s2 += f * f;
+        }
+      }
+    __syncthreads();
+    // the band's output is contiguous: (b0, oy0 .. oy0 + TR) or whole images b0 ..
+    bf16_t* yt = yp + ((int64_t)b0 * g.OH + oy0) * (1 << g.owl) * CO;
+    constexpr int CPR = CO / 8;
+    for (int c = threadIdx.x; c < valid * CPR; c += 256) {
+      const int row = c / CPR, cc = c % CPR;
+      *(uint4*)(yt + (int64_t)row * CO + 8 * cc) = *(const uint4*)(cs + row * LSC + 8 * cc);
+    }
+  }
+  if (sums != nullptr) {
+    s1 += __shfl_xor(s1, 16, 64);
+    s1 += __shfl_xor(s1, 32, 64);
+    s2 += __shfl_xor(s2, 16, 64);
+    s2 += __shfl_xor(s2, 32, 64);
+    if (gq == 0) {
+      atomicAdd(sums + (2 * p) * CO + n, s1);
+      atomicAdd(sums + (2 * p + 1) * CO + n, s2);
+    }
+  }
+}
+
+template <int CI, int CO, int NPX>
+__global__ __launch_bounds__(256) void dconv_wgrad_kernel(const bf16_t* __restrict__ x,
+                                                          const bf16_t* __restrict__ dy,
+                                                          float* __restrict__ part,
+                                                          const Geom g, int S2, int P) {
+  constexpr int M = 9 * CI;
+  constexpr int MFT = (M + 15) / 16, NFT = CO / 16, MFW = (MFT + 3) / 4;
+  constexpr int LSD = CO + 8;
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  const int halo = g.IMGS * g.TRI * g.WI * CI;
+  bf16_t* hs = smem;
+  bf16_t* ds = smem + halo;
+  bf16_t* zs = ds + NPX * LSD;  // 8 zero bytes: source of the padded rows m >= 9 CI
+
+  const int p = blockIdx.x / g.nb, blk = blockIdx.x % g.nb;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 15, gq = lane >> 4, q = li >> 2, pp = li & 3;
+  if (threadIdx.x == 0) *(uint2*)zs = make_uint2(0, 0);
+
+  // this lane's A column chunk (m = 16 mi + 4 pp .. + 3) of each of the wave's M fragments
+  int co_off[MFW];
+  bool mvalid[MFW];
+#pragma unroll
+  for (int i = 0; i < MFW; ++i) {
+    const int m = 16 * (wave + 4 * i) + 4 * pp;
+    mvalid[i] = m < M;
+    co_off[i] = tap_off<CI>(g, m);
+  }
+  f32x4 acc[MFW][NFT];
+#pragma unroll
+  for (int i = 0; i < MFW; ++i)
+#pragma unroll
+    for (int j = 0; j < NFT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int ow = 1 << g.owl, ppi = 1 << g.rpil;
+  const bf16_t* xp = x + p * ((int64_t)g.Bn * g.H * g.H * CI);
+  const bf16_t* dyp = dy + p * ((int64_t)g.Bn * g.OH * ow * CO);
+  for (int t = blk; t < g.tiles; t += g.nb) {
+    const int b0 = (t / g.tpi) * g.IMGS, oy0 = (t % g.tpi) * g.TR;
+    if (S2) load_halo<CI, 2>(hs, xp, g, b0, oy0);
+    else load_halo<CI, 1>(hs, xp, g, b0, oy0);
+    const int valid = min(NPX, (g.Bn - b0) * ppi);
+    const bf16_t* dyt = dyp + ((int64_t)b0 * g.OH + oy0) * ow * CO;
+    constexpr int CPR = CO / 8;
+    for (int c = threadIdx.x; c < NPX * CPR; c += 256) {
+      const int row = c / CPR, cc = c % CPR;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (row < valid) v = *(const uint4*)(dyt + (int64_t)row * CO + 8 * cc);
+      *(uint4*)(ds + row * LSD + 8 * cc) = v;
+    }
+    __syncthreads();
+#pragma unroll 2
+    for (int ks = 0; ks < NPX / 32; ++ks) {
+      const int ka = 32 * ks + 8 * gq + q, kb = ka + 4;  // the lane's two pixel rows
+      const int pa = S2 ? pix_base<CI, 2>(g, ka) : pix_base<CI, 1>(g, ka);
+      const int pb = S2 ? pix_base<CI, 2>(g, kb) : pix_base<CI, 1>(g, kb);
+      bf16x8 b[NFT];
+#pragma unroll
+      for (int j = 0; j < NFT; ++j)
+        b[j] = cat_frag(lds_tr4(ds + ka * LSD + 16 * j + 4 * pp),
+                        lds_tr4(ds + kb * LSD + 16 * j + 4 * pp));
+#pragma unroll
+      for (int i = 0; i < MFW; ++i) {
+        if (wave + 4 * i >= MFT) continue;  // wave-uniform
+        const bf16x8 a = cat_frag(lds_tr4(mvalid[i] ? hs + pa + co_off[i] : zs),
+                                  lds_tr4(mvalid[i] ? hs + pb + co_off[i] : zs));
+#pragma unroll
+        for (int j = 0; j < NFT; ++j) acc[i][j] = mfma16(a, b[j], acc[i][j]);
+      }
+    }
+    __syncthreads();
+  }
+  // partial [blk][p][m][n]
+  float* out = part + ((int64_t)blk * P + p) * M * CO;
+#pragma unroll
+  for (int i = 0; i < MFW; ++i) {
+    const int mi = wave + 4 * i;
+    if (mi >= MFT) continue;
+#pragma unroll
+    for (int j = 0; j < NFT; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 16 * mi + 4 * gq + r;
+        if (m < M) out[(int64_t)m * CO + 16 * j + li] = acc[i][j][r];
+      }
+  }
+}
+
+// out[p][i] (bf16, batch stride sO) = sum over the nb partials [nb][P][MN]
+__global__ __launch_bounds__(256) void dconv_reduce_kernel(const float* __restrict__ part,
+                                                           bf16_t* __restrict__ out, int64_t sO,
+                                                           int P, int MN, int nb) {
+  const int64_t total = (int64_t)P * MN;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  float s = 0.f;
+  for (int k = 0; k < nb; ++k) s += part[k * total + i];
+  out[(i / MN) * sO + i % MN] = f2bf(s);
+}
+
+int ilog2i(int v) {
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  return (1 << l) == v ? l : -1;
+}
+
+constexpr int npx_for(int co) { return co >= 64 ? 128 : 256; }
+
+// band geometry for output side OH (power of two), stride S, NPX pixels per band
+bool make_geom(Geom& g, int Bn, int H, int S, int npx, int target_blocks, int P) {
+  const int hl = ilog2i(H);
+  if (hl < 0 || Bn < 1 || (S != 1 && S != 2) || (S == 2 && H < 2)) return false;
+  g.Bn = Bn;
+  g.H = H;
+  g.OH = H / S;
+  const int OW = g.OH;
+  g.owl = ilog2i(OW);
+  if (OW > npx) return false;
+  const int px_img = g.OH * OW;
+  g.IMGS = px_img >= npx ? 1 : npx / px_img;
+  g.TR = px_img >= npx ? npx / OW : g.OH;
+  g.rpil = ilog2i(g.TR * OW);
+  g.TRI = (g.TR - 1) * S + 3;
+  g.WI = (OW - 1) * S + 3;
+  g.tpi = g.OH / g.TR;
+  g.tiles = ((Bn + g.IMGS - 1) / g.IMGS) * g.tpi;
+  int nb = (target_blocks + P - 1) / P;
+  g.nb = nb < 1 ? 1 : (nb > g.tiles ? g.tiles : nb);
+  return true;
+}
+
+size_t halo_bytes(const Geom& g, int CI) { return (size_t)g.IMGS * g.TRI * g.WI * CI * 2; }
+
+template <int CI, int CO>
+int launch_fwd(const void* x, const void* w, void* y, void* sums, int P, int Bn, int H, int S,
+               int dg, hipStream_t st) {
+  constexpr int NPX = npx_for(CO);
+  Geom g{};
+  if (!make_geom(g, Bn, H, S, NPX, 1024, P)) return (int)hipErrorInvalidValue;
+  const size_t lds = halo_bytes(g, CI) + (size_t)NPX * (CO + 8) * 2;
+  if (lds > 64 * 1024) return (int)hipErrorNotSupported;
+  hipLaunchKernelGGL((dconv_fwd_kernel<CI, CO, NPX>), dim3(P * g.nb), dim3(256), lds, st,
+                     (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)sums, g, S == 2, dg);
+  return (int)hipGetLastError();
+}
+
+template <int CI, int CO>
+int launch_wgrad(const void* x, const void* dy, void* dw, void* part, int P, int Bn, int H, int S,
+                 hipStream_t st, int* nb_out) {
+  constexpr int NPX = npx_for(CO);
+  Geom g{};
+  if (!make_geom(g, Bn, H, S, NPX, 512, P)) return (int)hipErrorInvalidValue;
+  if (nb_out != nullptr) {  // size query
+    *nb_out = g.nb;
+    return 0;
+  }
+  const size_t lds = halo_bytes(g, CI) + (size_t)NPX * (CO + 8) * 2 + 16;
+  if (lds > 64 * 1024) return (int)hipErrorNotSupported;
+  hipLaunchKernelGGL((dconv_wgrad_kernel<CI, CO, NPX>), dim3(P * g.nb), dim3(256), lds, st,
+                     (const bf16_t*)x, (const bf16_t*)dy, (float*)part, g, S == 2, P);
+  const int MN = 9 * CI * CO;
+  const int64_t total = (int64_t)P * MN;
+  hipLaunchKernelGGL(dconv_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
+                     (const float*)part, (bf16_t*)dw, (int64_t)MN, P, MN, g.nb);
+  return (int)hipGetLastError();
+}
+
+#define MOPT_DCONV_SHAPES(X) X(8, 16) X(16, 16) X(16, 32) X(32, 32) X(32, 64) X(64, 64)
+
+}  // namespace
+
+extern "C" {
+
+// Direct 3x3 convolution (pad 1) of a population, NHWC bf16, square power-of-two images:
+//   kind 0 forward   y [P*Bn, H/S, H/S, Co] = conv(x [P*Bn, H, H, Ci], w [P, 9 Ci, Co]);
+//                    aux = f32 sums [P][2][Co] (zeroed by the caller; += sum, sum^2 of y) or 0
+//   kind 1 dgrad     dx [P*Bn, H, H, Ci] from dy [P*Bn, H, H, Co] and w (stride 1 only)
+//   kind 2 wgrad     dw [P, 9 Ci, Co] (bf16) from x and dy; aux = f32 partials
+//                    [nb][P][9 Ci][Co], nb from mopt_dconv_wgrad_splits
+// Returns hipErrorNotSupported (801) for shapes without an instantiation: the caller falls
+// back to the implicit GEMM (mopt_pconv).
+int mopt_dconv(int kind, const void* a, const void* b, void* out, void* aux, int P, int Bn, int H,
+               int Ci, int Co, int stride, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (kind == 0) {
+#define X(ci, co) \
+    if (Ci == ci && Co == co) return launch_fwd<ci, co>(a, b, out, aux, P, Bn, H, stride, 0, st);
+    MOPT_DCONV_SHAPES(X)
+#undef X
+    return (int)hipErrorNotSupported;
+  }
+  if (kind == 1) {  // the forward kernel over dy (Co channels) with flipped transposed weights
+    if (stride != 1 || Ci != Co) return (int)hipErrorNotSupported;
+#define X(ci, co) \
+    if (Co == ci && Ci == co) return launch_fwd<ci, co>(a, b, out, nullptr, P, Bn, H, 1, 1, st);
+    MOPT_DCONV_SHAPES(X)
+#undef X
+    return (int)hipErrorNotSupported;
+  }
+  if (kind == 2) {
+#define X(ci, co) \
+    if (Ci == ci && Co == co) \
+      return launch_wgrad<ci, co>(a, b, out, aux, P, Bn, H, stride, st, nullptr);
+    MOPT_DCONV_SHAPES(X)
+#undef X
+    return (int)hipErrorNotSupported;
+  }
+  return (int)hipErrorInvalidValue;
+}
+
+// number of partial slices the weight-gradient kernel writes (0 when unsupported)
+int mopt_dconv_wgrad_splits(int P, int Bn, int H, int Ci, int Co, int stride) {
+  int nb = 0;
+#define X(ci, co) \
+  if (Ci == ci && Co == co) \
+    return launch_wgrad<ci, co>(nullptr, nullptr, nullptr, nullptr, P, Bn, H, stride, 0, &nb) \
+               ? 0 : nb;
+  MOPT_DCONV_SHAPES(X)
+#undef X
+  return 0;
+}
+
+}  // extern "C"

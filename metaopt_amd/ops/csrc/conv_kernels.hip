@@ -207,13 +207,14 @@ inline bool bn_shape_ok(int C) { return C >= 8 && C <= 512 && C % 8 == 0 && ((C 
 
 extern "C" {
 
-// x [P][M][C] -> y; stat [P][2][C] (mean, rstd) out; running [P][2][C] in/out; sums scratch.
+// x [P][M][C] -> y; stat [P][2][C] (mean, rstd) out; running [P][2][C] in/out; sums scratch
+// (or, sums_ready, the batch sums of x and x^2 already accumulated by the convolution).
 int mopt_bn_fwd(const void* x, const void* gamma, const void* beta, const void* res, void* y,
                 void* stat, void* running, void* sums, int P, int64_t M, int C, float eps,
-                float momentum, int train, int relu, void* stream) {
+                float momentum, int train, int relu, int sums_ready, void* stream) {
   if (!bn_shape_ok(C)) return 1;
   hipStream_t st = (hipStream_t)stream;
-  if (train) {
+  if (train && !sums_ready) {  // else the producing convolution's epilogue summed x, x^2
     (void)hipMemsetAsync(sums, 0, sizeof(float) * 2 * P * C, st);
     const int rpb = reduce_rows(P, M, C);
     hipLaunchKernelGGL(bn_reduce_kernel<false>, dim3((unsigned)((M + rpb - 1) / rpb), P),

@@ -36,6 +36,57 @@ def test_conv3x3_fwd_bwd(stride, C, Cout, B, H):
     _close(w.grad, wr.grad, 2e-2)
 
 
+# every convolution shape of ResNet-20 on 32x32 images (and of the 16x16 test model)
+RESNET_SHAPES = [(1, 8, 16, 32), (1, 16, 16, 32), (2, 16, 32, 32), (1, 32, 32, 16),
+                 (2, 32, 64, 16), (1, 64, 64, 8), (1, 64, 64, 4), (2, 16, 32, 16)]
+
+
+@pytest.mark.parametrize("stride,C,Cout,H", RESNET_SHAPES)
+def test_direct_conv_kernels(stride, C, Cout, H):
+    """The halo-tiled direct kernels (csrc/conv_direct.hip) run for every ResNet-20 shape --
+    forward with fused BatchNorm sums, stride-1 data gradient, weight gradient -- and match the
+    fp32 reference; B = 5 leaves a partial multi-image band on the small images."""
+    torch.manual_seed(2)
+    P, B = 3, 5
+    x = torch.randn(P * B, H, H, C, device=DEV).to(torch.bfloat16)
+    w = (0.1 * torch.randn(P, 9 * C, Cout, device=DEV)).to(torch.bfloat16)
+    OH = H // stride
+    y = torch.empty(P * B, OH, OH, Cout, dtype=torch.bfloat16, device=DEV)
+    sums = torch.zeros(P, 2, Cout, device=DEV)
+    assert cops._dconv(0, x, w, y, P, B, H, H, C, Cout, stride, sums)
+    xr, wr = x.float().requires_grad_(True), w.float().requires_grad_(True)
+    ref = cops.conv3x3_ref(xr, wr, P, stride)
+    _close(y, ref, 1e-2)
+    yf = y.float().view(P, -1, Cout)
+    torch.testing.assert_close(sums[:, 0], yf.sum(1), rtol=1e-3, atol=1e-2)
+    torch.testing.assert_close(sums[:, 1], (yf * yf).sum(1), rtol=1e-3, atol=1e-2)
+    dy = torch.randn_like(y)
+    ref.backward(dy.float())
+    dw = torch.empty_like(w)
+    assert cops._dconv(2, x, dy, dw, P, B, H, H, C, Cout, stride)
+    _close(dw, wr.grad, 1e-2)
+    if stride == 1 and C == Cout:
+        dx = torch.empty_like(x)
+        assert cops._dconv(1, dy, w, dx, P, B, H, H, C, Cout, stride)
+        _close(dx, xr.grad, 1e-2)
+
+
+def test_conv_bn_act_fused_statistics():
+    """conv_bn_act (BN statistics from the convolution epilogue) equals conv3x3 + bn_act."""
+    torch.manual_seed(3)
+    P, B, H, C = 2, 4, 16, 32
+    x = torch.randn(P * B, H, H, C, device=DEV).to(torch.bfloat16)
+    w = (0.1 * torch.randn(P, 9 * C, C, device=DEV)).to(torch.bfloat16)
+    g = (1 + 0.1 * torch.randn(P, C, device=DEV)).to(torch.bfloat16)
+    b = (0.1 * torch.randn(P, C, device=DEV)).to(torch.bfloat16)
+    run_a = torch.stack([torch.zeros(P, C), torch.ones(P, C)], 1).to(DEV).contiguous()
+    run_b = run_a.clone()
+    ya = cops.conv_bn_act(x, w, g, b, run_a, P, 1, True)
+    yb = cops.bn_act(cops.conv3x3(x, w, P, 1), g, b, run_b, P, True)
+    _close(ya, yb, 1e-2)
+    torch.testing.assert_close(run_a, run_b, rtol=1e-4, atol=1e-4)
+
+
 @pytest.mark.parametrize("relu,res", [(True, False), (True, True), (False, False)])
 def test_bn_act_train_and_eval(relu, res):
     torch.manual_seed(1)
