@@ -111,6 +111,8 @@ def _dconv(kind, a, b, out, P, Bn, H, W, Ci, Co, stride, sums=None):
         if nb <= 0:
             return False
         aux = torch.empty(nb * P * 9 * Ci * Co, dtype=torch.float32, device=out.device)
+    if kind == 0:       # the forward kernel loads its B fragments from W^T [P, Co, 9 Ci]
+        b = b.transpose(1, 2).contiguous()
     rc = lib.mopt_dconv(kind, a.data_ptr(), b.data_ptr(), out.data_ptr(),
                         0 if aux is None else aux.data_ptr(), P, Bn, H, Ci, Co, stride, _s(out))
     if rc == _NOT_SUPPORTED:

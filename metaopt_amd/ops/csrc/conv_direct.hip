@@ -26,9 +26,13 @@
 // CO in {16,32,64}, stride 1 or 2.
 #include "common.h"
 
+#include <algorithm>
+
 using namespace mopt;
 
 namespace {
+
+enum Mode { kFwd = 0, kDgrad = 1, kDgrad2 = 2 };
 
 struct Geom {
   int Bn;          // images per trial
@@ -40,24 +44,43 @@ struct Geom {
   int tpi;         // bands per image
   int tiles;       // bands per trial
   int nb;          // persistent workgroups per trial
+  float inv_wi, inv_tri;  // 1 / WI, 1 / TRI: exact quotients of small integers via (t + .5) / d
 };
 
+__device__ __forceinline__ int fdiv(int t, float inv) { return (int)(((float)t + 0.5f) * inv); }
+
+// LDS pixel stride of the halo band (elements).  An A fragment's ds_read_b128 is serviced in four
+// 16-lane groups, e.g. {0-3, 12-15, 20-27}: fragment rows (pixels) li in {0-3, 12-15} at chunk
+// g and li in {4-11} at chunk g + 1.  With a = the stride between consecutive fragment pixels in
+// 16-byte bank slots, the 16 slots a li (+1) are distinct mod 16 exactly when a = 2 mod 4: so
+// a = 2 (8 <= CI <= 16), 6 (CI 32), 10 (CI 64) at stride 1 (pixels adjacent), and odd pixel
+// strides at stride 2 (fragment pixels two apart): CI + 8 for CI >= 16.
+template <int CI, int S>
+constexpr int pstride() {
+  if (S == 2) return CI >= 16 ? CI + 8 : CI;
+  // (CI = 8: the 4 chunks of a fragment row are 4 different taps -- unpadded measured best)
+  if (CI == 8) return 8;
+  return CI / 8 % 4 == 2 ? CI : CI + 16;
+}
+
+// halo band: input rows row0 .. row0 + TRI, columns -1 .. WI - 2 of images b0 .. b0 + IMGS
 template <int CI, int S>
 __device__ __forceinline__ void load_halo(bf16_t* hs, const bf16_t* __restrict__ x,
-                                          const Geom& g, int b0, int oy0) {
+                                          const Geom& g, int b0, int row0) {
   constexpr int CC = CI / 8;
   const int n = g.IMGS * g.TRI * g.WI * CC;
   for (int c = threadIdx.x; c < n; c += 256) {
     const int cc = c % CC;
-    int t = c / CC;
-    const int hc = t % g.WI;
-    t /= g.WI;
-    const int hr = t % g.TRI, img = t / g.TRI;
-    const int iy = oy0 * S - 1 + hr, ix = hc - 1, b = b0 + img;
+    const int t = c / CC;
+    const int t2 = fdiv(t, g.inv_wi);
+    const int hc = t - t2 * g.WI;
+    const int img = fdiv(t2, g.inv_tri);
+    const int hr = t2 - img * g.TRI;
+    const int iy = row0 + hr, ix = hc - 1, b = b0 + img;
     uint4 v = make_uint4(0, 0, 0, 0);
     if (b < g.Bn && iy >= 0 && iy < g.H && ix >= 0 && ix < g.H)
       v = *(const uint4*)(x + (((int64_t)b * g.H + iy) * g.H + ix) * CI + 8 * cc);
-    *(uint4*)(hs + 8 * c) = v;
+    *(uint4*)(hs + t * pstride<CI, S>() + 8 * cc) = v;
   }
 }
 
@@ -66,31 +89,31 @@ template <int CI, int S>
 __device__ __forceinline__ int pix_base(const Geom& g, int pl) {
   const int img = pl >> g.rpil, rem = pl & ((1 << g.rpil) - 1);
   const int ly = rem >> g.owl, ox = rem & ((1 << g.owl) - 1);
-  return ((img * g.TRI + ly * S) * g.WI + ox * S) * CI;
+  return ((img * g.TRI + ly * S) * g.WI + ox * S) * pstride<CI, S>();
 }
 
 // halo offset of tap k / CI, channel k % CI (tap clamped to 8: padded k rows meet zero weights)
-template <int CI>
+template <int CI, int S>
 __device__ __forceinline__ int tap_off(const Geom& g, int k) {
   const int tap = min(k / CI, 8), c = k % CI;
   const int kh = tap / 3, kw = tap - 3 * kh;
-  return (kh * g.WI + kw) * CI + c;
+  return (kh * g.WI + kw) * pstride<CI, S>() + c;
 }
 
-template <int CI, int CO, int NPX>
+template <int CI, int CO, int NPX, int MODE, int S>
 __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict__ x,
                                                         const bf16_t* __restrict__ w,
                                                         bf16_t* __restrict__ y,
-                                                        float* __restrict__ sums, const Geom g,
-                                                        int S2, int dg) {
+                                                        float* __restrict__ sums, const Geom g) {
+  constexpr int mode = MODE;
   constexpr int KS = (9 * CI + 31) / 32;  // 32-wide k steps (k = tap * CI + c)
   constexpr int WN = CO / 16, WM = 4 / WN;
   constexpr int MFW = NPX / 16 / WM;      // 16-pixel fragments per wave
   constexpr int LSC = CO + 8;
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
-  const int halo = g.IMGS * g.TRI * g.WI * CI;
+  const int halo = g.IMGS * g.TRI * g.WI * pstride<CI, S>();
   bf16_t* hs = smem;
-  bf16_t* cs = smem + halo;
+  bf16_t* cs = smem;  // the output tile is restaged over the halo band once the MFMAs are done
 
   const int p = blockIdx.x / g.nb, blk = blockIdx.x % g.nb;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -107,16 +130,12 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
     const int k0 = 32 * j + 8 * gq;
     uint4 v = make_uint4(0, 0, 0, 0);
     if (k0 < 9 * CI) {
-      if (dg) {  // W'[tap' CI + c][n] = W[(8 - tap') CO + n][c]  (W stored [9 CO][CI] here)
-        const int tp = k0 / CI, c = k0 % CI;
-        v = *(const uint4*)(wp + ((int64_t)(8 - tp) * CO + n) * CI + c);
-      } else {   // W[k][n], stored [9 CI][CO]
-        uint32_t e[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) e[i] = wp[(int64_t)(k0 + i) * CO + n];
-        v = make_uint4(e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16),
-                       e[6] | (e[7] << 16));
-      }
+      const int tp = k0 / CI, c = k0 % CI;
+      int64_t off;
+      if (mode == kFwd) off = (int64_t)n * 9 * CI + k0;       // W^T [CO][9 CI] (pre-transposed)
+      else if (mode == kDgrad) off = ((int64_t)(8 - tp) * CO + n) * CI + c;  // flip, W [9 CO][CI]
+      else off = ((int64_t)tp * CO + n) * CI + c;              // kDgrad2: taps unflipped
+      v = *(const uint4*)(wp + off);
     }
     wr[j] = __builtin_bit_cast(bf16x8, v);
   }
@@ -127,29 +146,55 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
   bf16_t* yp = y + p * y_batch;
   const int ppi = 1 << g.rpil;  // band pixels per image
 
+  // this lane's pixel of each of its fragments (the band geometry is the same for every band)
+  int pb[MFW], ply[MFW], pox[MFW];
+#pragma unroll
+  for (int i = 0; i < MFW; ++i) {
+    const int pl = (wm * MFW + i) * 16 + li;
+    pb[i] = pix_base<CI, S>(g, pl);
+    const int rem = pl & ((1 << g.rpil) - 1);
+    ply[i] = ((pl >> g.rpil) * g.TRI) * 2 + (rem >> g.owl);  // kDgrad2: 2 img TRI + ly
+    pox[i] = rem & ((1 << g.owl) - 1);
+  }
+
   float s1 = 0.f, s2 = 0.f;
   for (int t = blk; t < g.tiles; t += g.nb) {
     const int b0 = (t / g.tpi) * g.IMGS, oy0 = (t % g.tpi) * g.TR;
-    if (S2) load_halo<CI, 2>(hs, xp, g, b0, oy0);
-    else load_halo<CI, 1>(hs, xp, g, b0, oy0);
+    load_halo<CI, S>(hs, xp, g, b0, mode == kDgrad2 ? oy0 / 2 - 1 : oy0 * S - 1);
     __syncthreads();
 
     f32x4 acc[MFW];
-    int pb[MFW];
 #pragma unroll
-    for (int i = 0; i < MFW; ++i) {
-      acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const int pl = (wm * MFW + i) * 16 + li;
-      pb[i] = S2 ? pix_base<CI, 2>(g, pl) : pix_base<CI, 1>(g, pl);
-    }
+    for (int i = 0; i < MFW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (MODE != kDgrad2) {
 #pragma unroll
-    for (int j = 0; j < KS; ++j) {
-      const int to = tap_off<CI>(g, 32 * j + 8 * gq);
+      for (int j = 0; j < KS; ++j) {
+        const int to = tap_off<CI, S>(g, 32 * j + 8 * gq);
 #pragma unroll
-      for (int i = 0; i < MFW; ++i) acc[i] = mfma16(lds_frag(hs + pb[i] + to), wr[j], acc[i]);
+        for (int i = 0; i < MFW; ++i) acc[i] = mfma16(lds_frag(hs + pb[i] + to), wr[j], acc[i]);
+      }
+    } else {
+      // stride-2 data gradient (transposed convolution): output pixel (ly, ox) takes dy at
+      // ((ly + 1 - kh) / 2, (ox + 1 - kw) / 2) for the taps whose divisions are exact (oy0 even)
+#pragma unroll
+      for (int j = 0; j < KS; ++j) {
+        const int k0 = 32 * j + 8 * gq;
+        const int tap = min(k0 / CI, 8), c = k0 % CI;
+        const int kh = tap / 3, kw = tap - 3 * kh;
+#pragma unroll
+        for (int i = 0; i < MFW; ++i) {
+          // ply = 2 img TRI + ly: parity and halving act on ly alone
+          const int ny = ply[i] + 1 - kh, nx = pox[i] + 1 - kw;
+          const bf16x8 f = lds_frag(hs + (((ny >> 1) + 1) * g.WI +
+                                          (nx >> 1) + 1) * pstride<CI, S>() + c);
+          const bf16x8 z = __builtin_bit_cast(bf16x8, make_uint4(0, 0, 0, 0));
+          acc[i] = mfma16(((ny | nx) & 1) ? z : f, wr[j], acc[i]);
+        }
+      }
     }
 
     const int valid = min(NPX, (g.Bn - b0) * ppi);
+    __syncthreads();  // every wave is done with the halo band
 #pragma unroll
     for (int i = 0; i < MFW; ++i)
 #pragma unroll
@@ -171,6 +216,7 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
       const int row = c / CPR, cc = c % CPR;
       *(uint4*)(yt + (int64_t)row * CO + 8 * cc) = *(const uint4*)(cs + row * LSC + 8 * cc);
     }
+    __syncthreads();  // the next band's halo overwrites the output tile
   }
   if (sums != nullptr) {
     s1 += __shfl_xor(s1, 16, 64);
@@ -184,16 +230,16 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
   }
 }
 
-template <int CI, int CO, int NPX>
+template <int CI, int CO, int NPX, int S>
 __global__ __launch_bounds__(256) void dconv_wgrad_kernel(const bf16_t* __restrict__ x,
                                                           const bf16_t* __restrict__ dy,
                                                           float* __restrict__ part,
-                                                          const Geom g, int S2, int P) {
+                                                          const Geom g, int P) {
   constexpr int M = 9 * CI;
   constexpr int MFT = (M + 15) / 16, NFT = CO / 16, MFW = (MFT + 3) / 4;
   constexpr int LSD = CO + 8;
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
-  const int halo = g.IMGS * g.TRI * g.WI * CI;
+  const int halo = g.IMGS * g.TRI * g.WI * pstride<CI, S>();
   bf16_t* hs = smem;
   bf16_t* ds = smem + halo;
   bf16_t* zs = ds + NPX * LSD;  // 8 zero bytes: source of the padded rows m >= 9 CI
@@ -210,7 +256,7 @@ __global__ __launch_bounds__(256) void dconv_wgrad_kernel(const bf16_t* __restri
   for (int i = 0; i < MFW; ++i) {
     const int m = 16 * (wave + 4 * i) + 4 * pp;
     mvalid[i] = m < M;
-    co_off[i] = tap_off<CI>(g, m);
+    co_off[i] = tap_off<CI, S>(g, m);
   }
   f32x4 acc[MFW][NFT];
 #pragma unroll
@@ -218,13 +264,22 @@ __global__ __launch_bounds__(256) void dconv_wgrad_kernel(const bf16_t* __restri
 #pragma unroll
     for (int j = 0; j < NFT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // this lane's two pixel rows of each 32-pixel k step: halo offsets (same for every band)
+  constexpr int NKS = NPX / 32;
+  int pa[NKS], pb[NKS];
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) {
+    const int ka = 32 * ks + 8 * gq + q;
+    pa[ks] = pix_base<CI, S>(g, ka);
+    pb[ks] = pix_base<CI, S>(g, ka + 4);
+  }
+
   const int ow = 1 << g.owl, ppi = 1 << g.rpil;
   const bf16_t* xp = x + p * ((int64_t)g.Bn * g.H * g.H * CI);
   const bf16_t* dyp = dy + p * ((int64_t)g.Bn * g.OH * ow * CO);
   for (int t = blk; t < g.tiles; t += g.nb) {
     const int b0 = (t / g.tpi) * g.IMGS, oy0 = (t % g.tpi) * g.TR;
-    if (S2) load_halo<CI, 2>(hs, xp, g, b0, oy0);
-    else load_halo<CI, 1>(hs, xp, g, b0, oy0);
+    load_halo<CI, S>(hs, xp, g, b0, oy0 * S - 1);
     const int valid = min(NPX, (g.Bn - b0) * ppi);
     const bf16_t* dyt = dyp + ((int64_t)b0 * g.OH + oy0) * ow * CO;
     constexpr int CPR = CO / 8;
@@ -235,11 +290,9 @@ __global__ __launch_bounds__(256) void dconv_wgrad_kernel(const bf16_t* __restri
       *(uint4*)(ds + row * LSD + 8 * cc) = v;
     }
     __syncthreads();
-#pragma unroll 2
-    for (int ks = 0; ks < NPX / 32; ++ks) {
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
       const int ka = 32 * ks + 8 * gq + q, kb = ka + 4;  // the lane's two pixel rows
-      const int pa = S2 ? pix_base<CI, 2>(g, ka) : pix_base<CI, 1>(g, ka);
-      const int pb = S2 ? pix_base<CI, 2>(g, kb) : pix_base<CI, 1>(g, kb);
       bf16x8 b[NFT];
 #pragma unroll
       for (int j = 0; j < NFT; ++j)
@@ -248,8 +301,8 @@ __global__ __launch_bounds__(256) void dconv_wgrad_kernel(const bf16_t* __restri
 #pragma unroll
       for (int i = 0; i < MFW; ++i) {
         if (wave + 4 * i >= MFT) continue;  // wave-uniform
-        const bf16x8 a = cat_frag(lds_tr4(mvalid[i] ? hs + pa + co_off[i] : zs),
-                                  lds_tr4(mvalid[i] ? hs + pb + co_off[i] : zs));
+        const bf16x8 a = cat_frag(lds_tr4(mvalid[i] ? hs + pa[ks] + co_off[i] : zs),
+                                  lds_tr4(mvalid[i] ? hs + pb[ks] + co_off[i] : zs));
 #pragma unroll
         for (int j = 0; j < NFT; ++j) acc[i][j] = mfma16(a, b[j], acc[i][j]);
       }
@@ -291,14 +344,17 @@ int ilog2i(int v) {
 }
 
 constexpr int npx_for(int co) { return co >= 64 ? 128 : 256; }
+// weight gradient: halo and dy tile live together, so wide outputs take half bands
+constexpr int npx_wgrad(int co) { return co >= 32 ? 128 : 256; }
 
-// band geometry for output side OH (power of two), stride S, NPX pixels per band
-bool make_geom(Geom& g, int Bn, int H, int S, int npx, int target_blocks, int P) {
+// band geometry: input side H (power of two), stride S, NPX output pixels per band; kDgrad2:
+// H is the side of the (full-resolution) output, the input dy is H / 2
+bool make_geom(Geom& g, int Bn, int H, int S, int npx, int target_blocks, int P, int mode) {
   const int hl = ilog2i(H);
   if (hl < 0 || Bn < 1 || (S != 1 && S != 2) || (S == 2 && H < 2)) return false;
   g.Bn = Bn;
-  g.H = H;
-  g.OH = H / S;
+  g.H = mode == kDgrad2 ? H / 2 : H;
+  g.OH = mode == kDgrad2 ? H : H / S;
   const int OW = g.OH;
   g.owl = ilog2i(OW);
   if (OW > npx) return false;
@@ -306,8 +362,10 @@ bool make_geom(Geom& g, int Bn, int H, int S, int npx, int target_blocks, int P)
   g.IMGS = px_img >= npx ? 1 : npx / px_img;
   g.TR = px_img >= npx ? npx / OW : g.OH;
   g.rpil = ilog2i(g.TR * OW);
-  g.TRI = (g.TR - 1) * S + 3;
-  g.WI = (OW - 1) * S + 3;
+  g.TRI = mode == kDgrad2 ? g.TR / 2 + 2 : (g.TR - 1) * S + 3;
+  g.WI = mode == kDgrad2 ? OW / 2 + 2 : (OW - 1) * S + 3;
+  g.inv_wi = 1.f / (float)g.WI;
+  g.inv_tri = 1.f / (float)g.TRI;
   g.tpi = g.OH / g.TR;
   g.tiles = ((Bn + g.IMGS - 1) / g.IMGS) * g.tpi;
   int nb = (target_blocks + P - 1) / P;
@@ -315,35 +373,44 @@ bool make_geom(Geom& g, int Bn, int H, int S, int npx, int target_blocks, int P)
   return true;
 }
 
-size_t halo_bytes(const Geom& g, int CI) { return (size_t)g.IMGS * g.TRI * g.WI * CI * 2; }
+template <int CI, int S>
+size_t halo_bytes(const Geom& g) { return (size_t)g.IMGS * g.TRI * g.WI * pstride<CI, S>() * 2; }
 
-template <int CI, int CO>
-int launch_fwd(const void* x, const void* w, void* y, void* sums, int P, int Bn, int H, int S,
-               int dg, hipStream_t st) {
+// S: the stride of the halo layout (kDgrad2 reads its half-resolution dy band at layout S = 1)
+template <int CI, int CO, int MODE, int S>
+int launch_fwd(const void* x, const void* w, void* y, void* sums, int P, int Bn, int H,
+               hipStream_t st) {
   constexpr int NPX = npx_for(CO);
   Geom g{};
-  if (!make_geom(g, Bn, H, S, NPX, 1024, P)) return (int)hipErrorInvalidValue;
-  const size_t lds = halo_bytes(g, CI) + (size_t)NPX * (CO + 8) * 2;
+  if (!make_geom(g, Bn, H, MODE == kDgrad2 ? 2 : S, NPX, 1024, P, MODE))
+    return (int)hipErrorInvalidValue;
+  const size_t lds = std::max(halo_bytes<CI, S>(g), (size_t)NPX * (CO + 8) * 2);
   if (lds > 64 * 1024) return (int)hipErrorNotSupported;
-  hipLaunchKernelGGL((dconv_fwd_kernel<CI, CO, NPX>), dim3(P * g.nb), dim3(256), lds, st,
-                     (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)sums, g, S == 2, dg);
+  hipLaunchKernelGGL((dconv_fwd_kernel<CI, CO, NPX, MODE, S>), dim3(P * g.nb), dim3(256), lds, st,
+                     (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)sums, g);
   return (int)hipGetLastError();
 }
 
-template <int CI, int CO>
-int launch_wgrad(const void* x, const void* dy, void* dw, void* part, int P, int Bn, int H, int S,
+template <int CI, int CO, int S>
+int launch_wgrad(const void* x, const void* dy, void* dw, void* part, int P, int Bn, int H,
                  hipStream_t st, int* nb_out) {
-  constexpr int NPX = npx_for(CO);
+  constexpr int NPX = npx_wgrad(CO);
+  // persistent workgroups per trial: ~2048 in all (latency hiding: a workgroup does not overlap
+  // its band loads with its MFMAs), <= 64 MB of f32 partials, >= 4 bands each
+  constexpr int64_t kPartBytes = 64 << 20;
+  const int64_t per = (int64_t)P * 9 * CI * CO * 4;
+  const int by_bytes = (int)(kPartBytes / per > 0 ? kPartBytes / per : 1);
   Geom g{};
-  if (!make_geom(g, Bn, H, S, NPX, 512, P)) return (int)hipErrorInvalidValue;
+  if (!make_geom(g, Bn, H, S, NPX, 2048, P, kFwd)) return (int)hipErrorInvalidValue;
+  g.nb = min(g.nb, max(1, min(by_bytes, g.tiles / 4)));
   if (nb_out != nullptr) {  // size query
     *nb_out = g.nb;
     return 0;
   }
-  const size_t lds = halo_bytes(g, CI) + (size_t)NPX * (CO + 8) * 2 + 16;
+  const size_t lds = halo_bytes<CI, S>(g) + (size_t)NPX * (CO + 8) * 2 + 16;
   if (lds > 64 * 1024) return (int)hipErrorNotSupported;
-  hipLaunchKernelGGL((dconv_wgrad_kernel<CI, CO, NPX>), dim3(P * g.nb), dim3(256), lds, st,
-                     (const bf16_t*)x, (const bf16_t*)dy, (float*)part, g, S == 2, P);
+  hipLaunchKernelGGL((dconv_wgrad_kernel<CI, CO, NPX, S>), dim3(P * g.nb), dim3(256), lds, st,
+                     (const bf16_t*)x, (const bf16_t*)dy, (float*)part, g, P);
   const int MN = 9 * CI * CO;
   const int64_t total = (int64_t)P * MN;
   hipLaunchKernelGGL(dconv_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
@@ -352,15 +419,17 @@ int launch_wgrad(const void* x, const void* dy, void* dw, void* part, int P, int
 }
 
 #define MOPT_DCONV_SHAPES(X) X(8, 16) X(16, 16) X(16, 32) X(32, 32) X(32, 64) X(64, 64)
+// data gradients run the forward kernel with the channel counts swapped (dy -> dx)
+#define MOPT_DCONV_DGRAD_SHAPES(X) X(16, 16) X(32, 16) X(32, 32) X(64, 32) X(64, 64)
 
 }  // namespace
 
 extern "C" {
 
 // Direct 3x3 convolution (pad 1) of a population, NHWC bf16, square power-of-two images:
-//   kind 0 forward   y [P*Bn, H/S, H/S, Co] = conv(x [P*Bn, H, H, Ci], w [P, 9 Ci, Co]);
+//   kind 0 forward   y [P*Bn, H/S, H/S, Co] = conv(x [P*Bn, H, H, Ci], w^T [P, Co, 9 Ci]);
 //                    aux = f32 sums [P][2][Co] (zeroed by the caller; += sum, sum^2 of y) or 0
-//   kind 1 dgrad     dx [P*Bn, H, H, Ci] from dy [P*Bn, H, H, Co] and w (stride 1 only)
+//   kind 1 dgrad     dx [P*Bn, H, H, Ci] from dy [P*Bn, H/S, H/S, Co] and w [P, 9 Ci, Co]
 //   kind 2 wgrad     dw [P, 9 Ci, Co] (bf16) from x and dy; aux = f32 partials
 //                    [nb][P][9 Ci][Co], nb from mopt_dconv_wgrad_splits
 // Returns hipErrorNotSupported (801) for shapes without an instantiation: the caller falls
@@ -370,23 +439,27 @@ int mopt_dconv(int kind, const void* a, const void* b, void* out, void* aux, int
   hipStream_t st = (hipStream_t)stream;
   if (kind == 0) {
 #define X(ci, co) \
-    if (Ci == ci && Co == co) return launch_fwd<ci, co>(a, b, out, aux, P, Bn, H, stride, 0, st);
+    if (Ci == ci && Co == co) \
+      return stride == 1 ? launch_fwd<ci, co, kFwd, 1>(a, b, out, aux, P, Bn, H, st) \
+                         : launch_fwd<ci, co, kFwd, 2>(a, b, out, aux, P, Bn, H, st);
     MOPT_DCONV_SHAPES(X)
 #undef X
     return (int)hipErrorNotSupported;
   }
   if (kind == 1) {  // the forward kernel over dy (Co channels) with flipped transposed weights
-    if (stride != 1 || Ci != Co) return (int)hipErrorNotSupported;
 #define X(ci, co) \
-    if (Co == ci && Ci == co) return launch_fwd<ci, co>(a, b, out, nullptr, P, Bn, H, 1, 1, st);
-    MOPT_DCONV_SHAPES(X)
+    if (Co == ci && Ci == co) \
+      return stride == 1 ? launch_fwd<ci, co, kDgrad, 1>(a, b, out, nullptr, P, Bn, H, st) \
+                         : launch_fwd<ci, co, kDgrad2, 1>(a, b, out, nullptr, P, Bn, H, st);
+    MOPT_DCONV_DGRAD_SHAPES(X)
 #undef X
     return (int)hipErrorNotSupported;
   }
   if (kind == 2) {
 #define X(ci, co) \
     if (Ci == ci && Co == co) \
-      return launch_wgrad<ci, co>(a, b, out, aux, P, Bn, H, stride, st, nullptr);
+      return stride == 1 ? launch_wgrad<ci, co, 1>(a, b, out, aux, P, Bn, H, st, nullptr) \
+                         : launch_wgrad<ci, co, 2>(a, b, out, aux, P, Bn, H, st, nullptr);
     MOPT_DCONV_SHAPES(X)
 #undef X
     return (int)hipErrorNotSupported;
@@ -399,7 +472,9 @@ int mopt_dconv_wgrad_splits(int P, int Bn, int H, int Ci, int Co, int stride) {
   int nb = 0;
 #define X(ci, co) \
   if (Ci == ci && Co == co) \
-    return launch_wgrad<ci, co>(nullptr, nullptr, nullptr, nullptr, P, Bn, H, stride, 0, &nb) \
+    return (stride == 1 \
+                ? launch_wgrad<ci, co, 1>(nullptr, nullptr, nullptr, nullptr, P, Bn, H, 0, &nb) \
+                : launch_wgrad<ci, co, 2>(nullptr, nullptr, nullptr, nullptr, P, Bn, H, 0, &nb)) \
                ? 0 : nb;
   MOPT_DCONV_SHAPES(X)
 #undef X
