@@ -270,7 +270,11 @@ class Experiment:
             final["metadata"]["datetime"] = datetime.datetime.utcnow()
             self.metadata["datetime"] = final["metadata"]["datetime"]
             final.pop("_id", None)
-            self._storage.create_experiment(final)
+            try:
+                self._storage.create_experiment(final)
+            except DuplicateKeyError:
+                self._init_done = False    # lost the race: this object was never registered
+                raise
             self._id = final["_id"]
             if self.refers.get("parent_id") is None:
                 self.refers["root_id"] = self._id

@@ -79,12 +79,12 @@ class PopulationResNet(FlatPopulation):
         return int(x.shape[0])
 
     # ------------------------------------------------------------------ forward
-    def _conv_bn(self, name, x, stride, train, res=None, relu=True):
+    def _conv_bn(self, name, x, stride, train, res=None, relu=True, arena=None):
         P, W = self.capacity, self.W
         w = W[f"{name}.w"]
         running = self.A[f"{name}.running"].view(P, 2, w.shape[-1])
         return cops.conv_bn_act(x, w, W[f"{name}.g"], W[f"{name}.b"], running, P, stride, train,
-                                res=res, relu=relu)
+                                res=res, relu=relu, arena=arena)
 
     @staticmethod
     def _shortcut(x, cout, stride):
@@ -97,16 +97,19 @@ class PopulationResNet(FlatPopulation):
         P, W = self.capacity, self.W
         h = self._expand(x, torch.bfloat16).view(-1, *x.shape[1:])     # [P*B, H, W, 8]
         B = x.shape[0]
+        # one zero fill per step for every layer's BatchNorm sums (forward and backward)
+        arena = (cops.ZeroArena(sum(4 * P * c for _, _, c, _ in self.layout), x.device)
+                 if train and x.device.type == "cuda" else None)
         it = iter(self.layout)
         name, _, cout, stride = next(it)
-        h = self._conv_bn(name, h, stride, train)
+        h = self._conv_bn(name, h, stride, train, arena=arena)
         for si in range(len(STAGES)):
             for b in range(self.blocks):
                 n1, _, c1, s1 = next(it)
                 n2, _, c2, _ = next(it)
                 r = self._shortcut(h, c2, s1)
-                t = self._conv_bn(n1, h, s1, train)
-                h = self._conv_bn(n2, t, 1, train, res=r)
+                t = self._conv_bn(n1, h, s1, train, arena=arena)
+                h = self._conv_bn(n2, t, 1, train, res=r, arena=arena)
         feat = h.view(P, B, -1, h.shape[-1]).float().mean(2)            # [P, B, 64]
         logits = torch.baddbmm(W["fc.b"].float()[:, None, :], feat,
                                W["fc.w"].float())[..., :NCLS]           # [P, B, 10]

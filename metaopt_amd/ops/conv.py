@@ -27,7 +27,7 @@ c_void_p, c_int, c_float, c_int64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_floa
 _lib.register_signatures({
     "mopt_bn_fwd": ([c_void_p] * 8 + [c_int, c_int64, c_int, c_float, c_float, c_int, c_int,
                                      c_int, c_void_p], c_int),
-    "mopt_bn_bwd": ([c_void_p] * 8 + [c_int, c_int64, c_int, c_int, c_void_p], c_int),
+    "mopt_bn_bwd": ([c_void_p] * 10 + [c_int, c_int64, c_int, c_int, c_int, c_void_p], c_int),
     "mopt_pconv": ([c_int] + [c_void_p] * 4 + [c_int] * 10 + [c_void_p], c_int),
     "mopt_dconv": ([c_int] + [c_void_p] * 4 + [c_int] * 6 + [c_void_p], c_int),
     "mopt_dconv_wgrad_splits": ([c_int] * 6, c_int),
@@ -111,8 +111,6 @@ def _dconv(kind, a, b, out, P, Bn, H, W, Ci, Co, stride, sums=None):
         if nb <= 0:
             return False
         aux = torch.empty(nb * P * 9 * Ci * Co, dtype=torch.float32, device=out.device)
-    if kind == 0:       # the forward kernel loads its B fragments from W^T [P, Co, 9 Ci]
-        b = b.transpose(1, 2).contiguous()
     rc = lib.mopt_dconv(kind, a.data_ptr(), b.data_ptr(), out.data_ptr(),
                         0 if aux is None else aux.data_ptr(), P, Bn, H, Ci, Co, stride, _s(out))
     if rc == _NOT_SUPPORTED:
@@ -193,7 +191,8 @@ def conv3x3(x, w, P, stride, stats=None):
 
 class _BNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, res, running, P, train, relu, eps, momentum, sums=None):
+    def forward(ctx, x, gamma, beta, res, running, P, train, relu, eps, momentum, sums=None,
+                arena=None):
         C = x.shape[-1]
         M = x.numel() // (P * C)
         y = torch.empty_like(x)
@@ -205,8 +204,15 @@ class _BNAct(torch.autograd.Function):
               0 if res is None else res.data_ptr(), y.data_ptr(), stat.data_ptr(),
               running.data_ptr(), sums.data_ptr(), P, M, C, eps, momentum, int(train), int(relu),
               int(ready), _s(x))
+        # (recomputing relu'(y) from x, gamma, beta instead of keeping y measured slower:
+        #  187 -> 229 us for the stage-1 backward pair on one MI355X)
         ctx.save_for_backward(x, y, stat, gamma)
         ctx.meta = (P, M, C, relu, res is not None)
+        # backward: pre-zeroed sums from the step's arena; dgamma / dbeta written by the kernel
+        # straight into the flat gradient buffer when the parameters are its leaf views
+        ctx.bwd_sums = arena.take(P * 2 * C).view(P, 2, C) if arena is not None else None
+        ctx.grads = tuple(t.grad if (t.requires_grad and t.is_leaf and t.grad is not None) else None
+                          for t in (gamma, beta))
         return y
 
     @staticmethod
@@ -216,17 +222,24 @@ class _BNAct(torch.autograd.Function):
         dy = dy.contiguous()
         dx = torch.empty_like(x)
         dres = torch.empty_like(x) if has_res else None
-        sums = torch.empty(P, 2, C, dtype=torch.float32, device=x.device)
+        zeroed = ctx.bwd_sums is not None
+        sums = ctx.bwd_sums if zeroed else torch.empty(P, 2, C, dtype=torch.float32,
+                                                       device=x.device)
+        gg, gb = ctx.grads
+        direct = gg is not None and gb is not None and gg.is_contiguous() and gb.is_contiguous()
         _call("mopt_bn_bwd", x.data_ptr(), y.data_ptr(), dy.data_ptr(), stat.data_ptr(),
               gamma.data_ptr(), dx.data_ptr(), 0 if dres is None else dres.data_ptr(),
-              sums.data_ptr(), P, M, C, int(relu), _s(x))
+              sums.data_ptr(), gg.data_ptr() if direct else 0, gb.data_ptr() if direct else 0,
+              P, M, C, int(relu), int(zeroed), _s(x))
+        if direct:
+            return dx, None, None, dres, None, None, None, None, None, None, None, None
         dgamma = sums[:, 1].to(gamma.dtype)
         dbeta = sums[:, 0].to(gamma.dtype)
-        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None
 
 
 def bn_act(x, gamma, beta, running, P, train, res=None, relu=True, eps=1e-5, momentum=0.1,
-           sums=None):
+           sums=None, arena=None):
     """y = relu?(BN(x) + res?) per trial; ``running`` [P, 2, C] f32 updated when training.
     ``sums``: precomputed f32 [P, 2, C] batch sums of x and x^2 (the producing convolution's
     epilogue) -- the statistics pass is skipped."""
@@ -234,17 +247,38 @@ def bn_act(x, gamma, beta, running, P, train, res=None, relu=True, eps=1e-5, mom
         return bn_act_ref(x, gamma, beta, running, P, train, res, relu, eps, momentum)
     return _BNAct.apply(x.contiguous(), gamma.contiguous(), beta.contiguous(),
                         None if res is None else res.contiguous(), running, P, train, relu, eps,
-                        momentum, sums)
+                        momentum, sums, arena)
 
 
-def conv_bn_act(x, w, gamma, beta, running, P, stride, train, res=None, relu=True):
+class ZeroArena:
+    """One zero-filled f32 buffer per training step, carved into the convolutions' BatchNorm
+    sums and the BatchNorm backward's reductions (one fill instead of one per layer)."""
+
+    def __init__(self, n, device):
+        self.buf = torch.zeros(n, dtype=torch.float32, device=device)
+        self.pos = 0
+
+    def take(self, n):
+        if self.pos + n > self.buf.numel():
+            raise RuntimeError("ZeroArena exhausted")
+        v = self.buf[self.pos:self.pos + n]
+        self.pos += n
+        return v
+
+
+def conv_bn_act(x, w, gamma, beta, running, P, stride, train, res=None, relu=True, arena=None):
     """relu?(BN(conv3x3(x, w)) + res?): on the HIP path the convolution's epilogue produces the
     BatchNorm batch statistics (no separate reduction pass over the conv output)."""
     if x.device.type != "cuda":
         return bn_act_ref(conv3x3_ref(x, w, P, stride), gamma, beta, running, P, train, res,
                           relu)
-    stats = [torch.zeros(P, 2, w.shape[-1], dtype=torch.float32, device=x.device), False] \
-        if train else None
+    Co = w.shape[-1]
+    stats = None
+    if train:
+        z = arena.take(P * 2 * Co).view(P, 2, Co) if arena is not None else \
+            torch.zeros(P, 2, Co, dtype=torch.float32, device=x.device)
+        stats = [z, False]
     y = conv3x3(x, w, P, stride, stats)
     return bn_act(y, gamma, beta, running, P, train, res=res, relu=relu,
-                  sums=stats[0] if stats is not None and stats[1] else None)
+                  sums=stats[0] if stats is not None and stats[1] else None,
+                  arena=arena if train else None)

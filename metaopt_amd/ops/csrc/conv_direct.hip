@@ -45,6 +45,7 @@ struct Geom {
   int tiles;       // bands per trial
   int nb;          // persistent workgroups per trial
   float inv_wi, inv_tri;  // 1 / WI, 1 / TRI: exact quotients of small integers via (t + .5) / d
+  int lds_elems;          // bf16 elements of the workgroup's LDS allocation
 };
 
 __device__ __forceinline__ int fdiv(int t, float inv) { return (int)(((float)t + 0.5f) * inv); }
@@ -125,19 +126,43 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
 
   // this wave's B fragments for every k step
   bf16x8 wr[KS];
+  if constexpr (MODE == kFwd) {
+    // W [9 CI][CO] is n-contiguous: staged through LDS in k chunks and read back transposed
+    // (ds_read_b64_tr_b16), so neither a transposed copy nor 2-byte gathers are needed
+    static_assert((NPX * LSC / CO) / 32 >= 1, "weight chunk");
+    const int KCH = min(KS * 32, (g.lds_elems / CO) / 32 * 32);  // k rows per chunk
+    const int q = li >> 2, pp = li & 3;
+    for (int c0 = 0; c0 < KS * 32; c0 += KCH) {
+      for (int c = threadIdx.x; c < KCH * (CO / 8); c += 256) {
+        const int r = c / (CO / 8), cc = c % (CO / 8);
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (c0 + r < 9 * CI) v = *(const uint4*)(wp + (int64_t)(c0 + r) * CO + 8 * cc);
+        *(uint4*)(smem + r * CO + 8 * cc) = v;
+      }
+      __syncthreads();
 #pragma unroll
-  for (int j = 0; j < KS; ++j) {
-    const int k0 = 32 * j + 8 * gq;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (k0 < 9 * CI) {
-      const int tp = k0 / CI, c = k0 % CI;
-      int64_t off;
-      if (mode == kFwd) off = (int64_t)n * 9 * CI + k0;       // W^T [CO][9 CI] (pre-transposed)
-      else if (mode == kDgrad) off = ((int64_t)(8 - tp) * CO + n) * CI + c;  // flip, W [9 CO][CI]
-      else off = ((int64_t)tp * CO + n) * CI + c;              // kDgrad2: taps unflipped
-      v = *(const uint4*)(wp + off);
+      for (int j = 0; j < KS; ++j) {
+        if (32 * j < c0 || 32 * j >= c0 + KCH) continue;
+        const int r = 32 * j - c0 + 8 * gq + q;
+        wr[j] = cat_frag(lds_tr4(smem + r * CO + 16 * wn + 4 * pp),
+                         lds_tr4(smem + (r + 4) * CO + 16 * wn + 4 * pp));
+      }
+      __syncthreads();
     }
-    wr[j] = __builtin_bit_cast(bf16x8, v);
+  } else {
+#pragma unroll
+    for (int j = 0; j < KS; ++j) {
+      const int k0 = 32 * j + 8 * gq;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (k0 < 9 * CI) {
+        const int tp = k0 / CI, c = k0 % CI;
+        const int64_t off = mode == kDgrad
+                                ? ((int64_t)(8 - tp) * CO + n) * CI + c  // flip, W [9 CO][CI]
+                                : ((int64_t)tp * CO + n) * CI + c;       // kDgrad2: unflipped
+        v = *(const uint4*)(wp + off);
+      }
+      wr[j] = __builtin_bit_cast(bf16x8, v);
+    }
   }
 
   const int64_t x_batch = (int64_t)g.Bn * g.H * g.H * CI;
@@ -382,10 +407,12 @@ int launch_fwd(const void* x, const void* w, void* y, void* sums, int P, int Bn,
                hipStream_t st) {
   constexpr int NPX = npx_for(CO);
   Geom g{};
-  if (!make_geom(g, Bn, H, MODE == kDgrad2 ? 2 : S, NPX, 1024, P, MODE))
+  // (64-wide outputs: half the workgroups, twice the bands each -- their weight prologue is long)
+  if (!make_geom(g, Bn, H, MODE == kDgrad2 ? 2 : S, NPX, CO >= 64 ? 512 : 1024, P, MODE))
     return (int)hipErrorInvalidValue;
   const size_t lds = std::max(halo_bytes<CI, S>(g), (size_t)NPX * (CO + 8) * 2);
   if (lds > 64 * 1024) return (int)hipErrorNotSupported;
+  g.lds_elems = (int)(lds / 2);
   hipLaunchKernelGGL((dconv_fwd_kernel<CI, CO, NPX, MODE, S>), dim3(P * g.nb), dim3(256), lds, st,
                      (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)sums, g);
   return (int)hipGetLastError();
@@ -427,7 +454,7 @@ int launch_wgrad(const void* x, const void* dy, void* dw, void* part, int P, int
 extern "C" {
 
 // Direct 3x3 convolution (pad 1) of a population, NHWC bf16, square power-of-two images:
-//   kind 0 forward   y [P*Bn, H/S, H/S, Co] = conv(x [P*Bn, H, H, Ci], w^T [P, Co, 9 Ci]);
+//   kind 0 forward   y [P*Bn, H/S, H/S, Co] = conv(x [P*Bn, H, H, Ci], w [P, 9 Ci, Co]);
 //                    aux = f32 sums [P][2][Co] (zeroed by the caller; += sum, sum^2 of y) or 0
 //   kind 1 dgrad     dx [P*Bn, H, H, Ci] from dy [P*Bn, H/S, H/S, Co] and w [P, 9 Ci, Co]
 //   kind 2 wgrad     dw [P, 9 Ci, Co] (bf16) from x and dy; aux = f32 partials

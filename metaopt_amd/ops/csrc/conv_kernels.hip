@@ -163,9 +163,18 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
                                                            const float* __restrict__ sums,
                                                            const bf16_t* __restrict__ gamma,
                                                            bf16_t* __restrict__ dx,
-                                                           bf16_t* __restrict__ dres, int64_t M,
+                                                           bf16_t* __restrict__ dres,
+                                                           bf16_t* __restrict__ dgamma,
+                                                           bf16_t* __restrict__ dbeta, int64_t M,
                                                            int C, int P, int relu) {
   const int cc = C >> 3;
+  if (blockIdx.x == 0 && dgamma != nullptr) {  // (sum dz xhat, sum dz) straight into the grads
+    for (int k = threadIdx.x; k < P * C; k += 256) {
+      const int pk = k / C, c = k % C;
+      dgamma[k] = f2bf(sums[(2 * pk + 1) * C + c]);
+      dbeta[k] = f2bf(sums[(2 * pk) * C + c]);
+    }
+  }
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= (int64_t)P * M * cc) return;
   const int ch = i % cc;
@@ -230,21 +239,22 @@ int mopt_bn_fwd(const void* x, const void* gamma, const void* beta, const void* 
   return (int)hipGetLastError();
 }
 
-// sums [P][2][C] out: (sum dz, sum dz * xhat) = (dbeta, dgamma) in f32.
+// sums [P][2][C] out: (sum dz, sum dz * xhat) = (dbeta, dgamma) in f32 (zeroed here unless
+// sums_zeroed); dgamma / dbeta (bf16 [P][C], may be null): the gradients written directly.
 int mopt_bn_bwd(const void* x, const void* y, const void* dy, const void* stat, const void* gamma,
-                void* dx, void* dres, void* sums, int P, int64_t M, int C, int relu,
-                void* stream) {
+                void* dx, void* dres, void* sums, void* dgamma, void* dbeta, int P, int64_t M,
+                int C, int relu, int sums_zeroed, void* stream) {
   if (!bn_shape_ok(C)) return 1;
   hipStream_t st = (hipStream_t)stream;
-  (void)hipMemsetAsync(sums, 0, sizeof(float) * 2 * P * C, st);
+  if (!sums_zeroed) (void)hipMemsetAsync(sums, 0, sizeof(float) * 2 * P * C, st);
   const int rpb = reduce_rows(P, M, C);
   hipLaunchKernelGGL(bn_reduce_kernel<true>, dim3((unsigned)((M + rpb - 1) / rpb), P),
                      dim3(256), 0, st, (const bf16_t*)x, (const bf16_t*)y, (const bf16_t*)dy,
                      (const float*)stat, (float*)sums, M, C, rpb, relu);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, grid1((int64_t)P * M * (C / 8)), dim3(256), 0, st,
                      (const bf16_t*)x, (const bf16_t*)y, (const bf16_t*)dy, (const float*)stat,
-                     (const float*)sums, (const bf16_t*)gamma, (bf16_t*)dx, (bf16_t*)dres, M, C,
-                     P, relu);
+                     (const float*)sums, (const bf16_t*)gamma, (bf16_t*)dx, (bf16_t*)dres,
+                     (bf16_t*)dgamma, (bf16_t*)dbeta, M, C, P, relu);
   return (int)hipGetLastError();
 }
 
