@@ -73,6 +73,17 @@ class FlatPopulation:
             leaf.requires_grad_(True)
             leaf.grad = self.g16[o:o + P * n].view(P, *shape)
             self.W[name] = leaf
+        # gradients the HIP kernels overwrite every step (straight into the .grad views) need no
+        # zeroing; the rest (autograd-accumulated) is zeroed per step, contiguous runs merged
+        direct = self.direct_grads() if self.device.type == "cuda" else set()
+        self._zero_runs = []
+        for (name, _, _), (o, n) in zip(self.specs, self.segments):
+            if name in direct:
+                continue
+            if self._zero_runs and self._zero_runs[-1][1] == o:
+                self._zero_runs[-1][1] = o + P * n
+            else:
+                self._zero_runs.append([o, o + P * n])
         self.opt = ops.FlatOptimizer(self.segments, P, dev, kind=self.optimizer)
         self.hp = np.zeros(P, dtype=[("t", "<i4")])
         self.opt_hp = np.zeros(P, dtype=ops.LM_HP_DTYPE)
@@ -86,6 +97,11 @@ class FlatPopulation:
         """[(name, per-trial shape, init)]; init = ('normal', std) | ('ones',) | ('zeros',) |
         ('kaiming', fan_in)."""
         raise NotImplementedError
+
+    def direct_grads(self):
+        """Names of the parameters whose gradient the HIP backward writes in full every step
+        (no zeroing, no accumulation); default: none."""
+        return set()
 
     def aux_specs(self):
         """[(name, per-trial numel)] of the non-parameter state (checkpointed with the weights)."""
@@ -194,7 +210,8 @@ class FlatPopulation:
         self._body(x, y, None)
 
     def _body(self, x, y, hp_dev):
-        self.g16.zero_()
+        for a, b in self._zero_runs:
+            self.g16[a:b].zero_()
         out = self._loss(x, y, train=True)
         loss = out[0] if isinstance(out, tuple) else out
         loss.sum().backward()

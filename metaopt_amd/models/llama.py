@@ -109,6 +109,10 @@ class PopulationLM(FlatPopulation):
     def param_specs(self):
         return param_specs(self.cfg)
 
+    def direct_grads(self):
+        # projections (pgemm grad_out), norms and the embedding (cast into the .grad views)
+        return {name for name, _, _ in self.specs}
+
     def rows_per_batch(self, x) -> int:
         return int(x.numel())
 

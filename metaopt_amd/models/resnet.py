@@ -66,6 +66,11 @@ class PopulationResNet(FlatPopulation):
         specs.append(("fc.b", (NCLS_PAD,), ("zeros",)))
         return specs
 
+    def direct_grads(self):
+        # conv weights (wgrad kernels) and BatchNorm gamma / beta (BN backward); the classifier
+        # goes through autograd
+        return {f"{name}.{k}" for name, _, _, _ in self.layout for k in ("w", "g", "b")}
+
     def aux_specs(self):
         return [(f"{name}.running", 2 * cout) for name, _, cout, _ in self.layout]
 

@@ -135,6 +135,23 @@ def embed_ref(tok, table, rows_per_trial):
 
 
 # ============================================================================ autograd Functions
+def _grad_view(t):
+    """The leaf's preset ``.grad`` (a view of the flat bf16 gradient buffer) when the kernels can
+    write the gradient there directly -- autograd then has nothing to accumulate."""
+    if t.requires_grad and t.is_leaf and t.grad is not None and t.grad.is_contiguous() and \
+            t.grad.dtype == torch.bfloat16:
+        return t.grad
+    return None
+
+
+def _dw_out(dw32, gw, dtype, stream_of):
+    """f32 weight gradient -> the flat buffer (returns None) or a tensor for autograd."""
+    if gw is not None:
+        _call("mopt_cast_bf16", _p(dw32), _p(gw), dw32.numel(), _stream(stream_of))
+        return None
+    return dw32.to(dtype)
+
+
 class _RMSNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, rows_per_trial, eps):
@@ -145,6 +162,7 @@ class _RMSNorm(torch.autograd.Function):
               _stream(x))
         ctx.save_for_backward(x, w, rstd)
         ctx.rpt = rows_per_trial
+        ctx.gw = _grad_view(w)
         return y
 
     @staticmethod
@@ -156,7 +174,7 @@ class _RMSNorm(torch.autograd.Function):
         dw32 = torch.zeros(w.shape, dtype=torch.float32, device=x.device)
         _call("mopt_rmsnorm_bwd", _p(x), _p(w), _p(dy), _p(rstd), _p(dx), _p(dw32), R, d,
               ctx.rpt, _stream(x))
-        return dx, dw32.to(w.dtype), None, None
+        return dx, _dw_out(dw32, ctx.gw, w.dtype, x), None, None
 
 
 def rmsnorm(x, w, rows_per_trial, eps=1e-5):
@@ -179,6 +197,7 @@ class _AddRMSNorm(torch.autograd.Function):
               rows_per_trial, eps, _stream(x))
         ctx.save_for_backward(xs, w, rstd)
         ctx.rpt = rows_per_trial
+        ctx.gw = _grad_view(w)
         return xs, y
 
     @staticmethod
@@ -187,14 +206,14 @@ class _AddRMSNorm(torch.autograd.Function):
         R, d = xs.shape
         dw32 = torch.zeros(w.shape, dtype=torch.float32, device=xs.device)
         if dy is None:
-            return dxs, dxs, None, None, None
+            return dxs, dxs, _dw_out(dw32, ctx.gw, w.dtype, xs), None, None
         dy = dy.contiguous()
         dres = dxs.contiguous() if dxs is not None else None
         dx = torch.empty_like(xs)
         _call("mopt_rmsnorm_bwd_res", _p(xs), _p(w), _p(dy),
               _p(dres) if dres is not None else None, _p(rstd), _p(dx), _p(dw32), R, d,
               ctx.rpt, _stream(xs))
-        return dx, dx, dw32.to(w.dtype), None, None
+        return dx, dx, _dw_out(dw32, ctx.gw, w.dtype, xs), None, None
 
 
 def add_rmsnorm(x, delta, w, rows_per_trial, eps=1e-5):
@@ -364,6 +383,7 @@ class _Embedding(torch.autograd.Function):
               _stream(table))
         ctx.save_for_backward(tok)
         ctx.dims = (P, V, d, rows_per_trial, table.dtype)
+        ctx.gw = _grad_view(table)
         return out
 
     @staticmethod
@@ -373,6 +393,9 @@ class _Embedding(torch.autograd.Function):
         d32 = torch.zeros(P, V, d, dtype=torch.float32, device=dout.device)
         _call("mopt_embed_bwd", _p(tok), _p(dout.contiguous()), _p(d32), tok.numel(), d, V, rpt,
               _stream(dout))
+        if ctx.gw is not None:      # cast straight into the flat gradient buffer
+            _call("mopt_cast_bf16", _p(d32), _p(ctx.gw), d32.numel(), _stream(dout))
+            return None, None, None
         d16 = torch.empty(P, V, d, dtype=dtype, device=dout.device)
         _call("mopt_cast_bf16", _p(d32), _p(d16), d32.numel(), _stream(dout))
         return None, d16, None
