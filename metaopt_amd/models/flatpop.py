@@ -31,6 +31,7 @@ from ..ops.population import MemberConfig, device_busy
 
 class FlatPopulation:
     optimizer = "adamw"            # or "sgd"
+    moment_dtype = torch.float32   # AdamW first-moment storage (bf16: see lm_ops.hip adamw)
     secondary = "acc"              # eval_result's second array: "acc" or "ppl"
 
     def __init__(self, capacity: int, device="cuda", max_grad_norm: float = 0.0,
@@ -56,7 +57,8 @@ class FlatPopulation:
         self.p32 = torch.zeros(off, dtype=torch.float32, device=dev)
         self.p16 = torch.zeros(off, dtype=torch.bfloat16, device=dev)
         self.g16 = torch.zeros(off, dtype=torch.bfloat16, device=dev)
-        self.m = torch.zeros(off, dtype=torch.float32, device=dev)
+        self.m = torch.zeros(off, dtype=self.moment_dtype if self.optimizer == "adamw"
+                             else torch.float32, device=dev)
         self.v = (torch.zeros(off, dtype=torch.float32, device=dev) if self.optimizer == "adamw"
                   else torch.zeros(0, dtype=torch.float32, device=dev))
         # per-trial non-parameter state, segment-major like the parameters: A[name] is [P, n]
@@ -330,8 +332,10 @@ class FlatPopulation:
             for sl in self._slices(slot):
                 n = sl.stop - sl.start
                 pool = self._ck[idx, j, o:o + n]
-                if to_pool:
+                if to_pool:                      # (a bf16 moment widens to the f32 pool)
                     items.append((buf[sl], pool, None))
+                elif buf.dtype == torch.bfloat16:   # ... and narrows back on load
+                    items.append((pool, None, buf[sl]))
                 else:
                     items.append((pool, buf[sl], self.p16[sl] if j == 0 else None))
                 o += n
@@ -377,7 +381,7 @@ class FlatPopulation:
     def slot_state(self, slot: int) -> dict:
         cat = lambda buf: torch.cat([buf[sl] for sl in self._slices(slot)])  # noqa: E731
         st = {"config": self.members[slot].to_dict(), "t": int(self.hp[slot]["t"]),
-              "p32": cat(self.p32), "m32": cat(self.m), "aux": self._aux_of(slot),
+              "p32": cat(self.p32), "m32": cat(self.m).float(), "aux": self._aux_of(slot),
               "optimizer": self.optimizer}
         if self.v.numel():
             st["v32"] = cat(self.v)

@@ -109,6 +109,9 @@ class PopulationLM(FlatPopulation):
     def param_specs(self):
         return param_specs(self.cfg)
 
+    # AdamW first moment in bf16 (28 -> 24 bytes per parameter per step)
+    moment_dtype = torch.bfloat16
+
     def direct_grads(self):
         # projections (pgemm grad_out), norms and the embedding (cast into the .grad views)
         return {name for name, _, _ in self.specs}

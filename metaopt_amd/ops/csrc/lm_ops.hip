@@ -451,6 +451,10 @@ __global__ __launch_bounds__(256) void grad_sumsq_kernel(const Segment* __restri
   if (threadIdx.x == 0) atomicAdd(sumsq + trial, tot);
 }
 
+// M16: the first moment is kept in bf16 (RNE after each update; the update itself uses the f32
+// value) -- 4 of the 28 bytes per parameter the step moves.  The second moment stays f32: with
+// b2 = 0.999 its per-step change (0.1 %) is below bf16 resolution and would stall.
+template <bool M16>
 __global__ __launch_bounds__(256) void adamw_multi_kernel(const Segment* __restrict__ segs,
                                                           const SegChunk* __restrict__ chunks,
                                                           const LmHP* __restrict__ hp,
@@ -458,7 +462,7 @@ __global__ __launch_bounds__(256) void adamw_multi_kernel(const Segment* __restr
                                                           float* __restrict__ p32,
                                                           bf16_t* __restrict__ p16,
                                                           const bf16_t* __restrict__ g16,
-                                                          float* __restrict__ m32,
+                                                          void* __restrict__ mbuf,
                                                           float* __restrict__ v32) {
   const SegChunk ch = chunks[blockIdx.x];
   const Segment sg = segs[ch.seg];
@@ -479,7 +483,15 @@ __global__ __launch_bounds__(256) void adamw_multi_kernel(const Segment* __restr
   float gv[8];
   unpack8(*(const uint4*)(g16 + o), gv);
   const f32x4 w0 = *(const f32x4*)(p32 + o), w1 = *(const f32x4*)(p32 + o + 4);
-  const f32x4 m0 = *(const f32x4*)(m32 + o), m1 = *(const f32x4*)(m32 + o + 4);
+  f32x4 m0, m1;
+  if constexpr (M16) {
+    const uint4 mv = *(const uint4*)((const bf16_t*)mbuf + o);
+    m0 = bf4_to_f32(make_uint2(mv.x, mv.y));
+    m1 = bf4_to_f32(make_uint2(mv.z, mv.w));
+  } else {
+    m0 = *(const f32x4*)((const float*)mbuf + o);
+    m1 = *(const f32x4*)((const float*)mbuf + o + 4);
+  }
   const f32x4 v0 = *(const f32x4*)(v32 + o), v1 = *(const f32x4*)(v32 + o + 4);
   float we[8] = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
   float me[8] = {m0[0], m0[1], m0[2], m0[3], m1[0], m1[1], m1[2], m1[3]};
@@ -494,8 +506,12 @@ __global__ __launch_bounds__(256) void adamw_multi_kernel(const Segment* __restr
   }
   *(f32x4*)(p32 + o) = f32x4{we[0], we[1], we[2], we[3]};
   *(f32x4*)(p32 + o + 4) = f32x4{we[4], we[5], we[6], we[7]};
-  *(f32x4*)(m32 + o) = f32x4{me[0], me[1], me[2], me[3]};
-  *(f32x4*)(m32 + o + 4) = f32x4{me[4], me[5], me[6], me[7]};
+  if constexpr (M16) {
+    *(uint4*)((bf16_t*)mbuf + o) = pack8(me);
+  } else {
+    *(f32x4*)((float*)mbuf + o) = f32x4{me[0], me[1], me[2], me[3]};
+    *(f32x4*)((float*)mbuf + o + 4) = f32x4{me[4], me[5], me[6], me[7]};
+  }
   *(f32x4*)(v32 + o) = f32x4{ve[0], ve[1], ve[2], ve[3]};
   *(f32x4*)(v32 + o + 4) = f32x4{ve[4], ve[5], ve[6], ve[7]};
   *(uint4*)(p16 + o) = pack8(we);
@@ -668,9 +684,10 @@ int mopt_cast_bf16(const void* src, void* dst, int64_t n, void* stream) {
   return (int)hipGetLastError();
 }
 
+// m16: the first moment buffer is bf16 (else f32)
 int mopt_adamw_multi(const void* segs, const void* chunks, int n_chunks, const void* hp,
-                     void* sumsq, void* p32, void* p16, const void* g16, void* m32, void* v32,
-                     int P, int clip, void* stream) {
+                     void* sumsq, void* p32, void* p16, const void* g16, void* m, void* v32,
+                     int P, int clip, int m16, void* stream) {
   if (n_chunks <= 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   if (clip) {
@@ -679,9 +696,10 @@ int mopt_adamw_multi(const void* segs, const void* chunks, int n_chunks, const v
                        dim3(256), 0, st, (const Segment*)segs, (const SegChunk*)chunks, n_chunks,
                        (const bf16_t*)g16, (float*)sumsq);
   }
-  hipLaunchKernelGGL(adamw_multi_kernel, dim3(n_chunks), dim3(256), 0, st, (const Segment*)segs,
-                     (const SegChunk*)chunks, (const LmHP*)hp, (const float*)sumsq, (float*)p32,
-                     (bf16_t*)p16, (const bf16_t*)g16, (float*)m32, (float*)v32);
+  hipLaunchKernelGGL((m16 ? adamw_multi_kernel<true> : adamw_multi_kernel<false>), dim3(n_chunks),
+                     dim3(256), 0, st, (const Segment*)segs, (const SegChunk*)chunks,
+                     (const LmHP*)hp, (const float*)sumsq, (float*)p32, (bf16_t*)p16,
+                     (const bf16_t*)g16, m, (float*)v32);
   return (int)hipGetLastError();
 }
 

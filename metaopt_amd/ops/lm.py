@@ -40,7 +40,8 @@ _lib.register_signatures({
     "mopt_embed_bwd": ([c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_void_p],
                        c_int),
     "mopt_cast_bf16": ([c_void_p, c_void_p, c_int64, c_void_p], c_int),
-    "mopt_adamw_multi": ([c_void_p, c_void_p, c_int] + [c_void_p] * 7 + [c_int, c_int, c_void_p],
+    "mopt_adamw_multi": ([c_void_p, c_void_p, c_int] + [c_void_p] * 7 + [c_int, c_int, c_int,
+                                                                         c_void_p],
                          c_int),
     "mopt_sgd_multi": ([c_void_p, c_void_p, c_int] + [c_void_p] * 6 + [c_int, c_int, c_void_p],
                        c_int),
@@ -452,7 +453,7 @@ class FlatOptimizer:
             if self.kind == "adamw":
                 _call("mopt_adamw_multi", _p(self._segs), _p(self._chunks), self.n_chunks,
                       _p(hp_dev), _p(self._sumsq), _p(p32), _p(p16), _p(g16), _p(m), _p(v),
-                      self.P, clip, _lib.stream_ptr(self.device))
+                      self.P, clip, int(m.dtype == torch.bfloat16), _lib.stream_ptr(self.device))
             else:
                 _call("mopt_sgd_multi", _p(self._segs), _p(self._chunks), self.n_chunks,
                       _p(hp_dev), _p(self._sumsq), _p(p32), _p(p16), _p(g16), _p(m), self.P,
@@ -511,8 +512,9 @@ def adamw_flat_ref(segments, P, p32, p16, g16, m, v, hp):
             bc1, bc2 = 1 - float(h["b1"]) ** t, 1 - float(h["b2"]) ** t
             w = p32[lo:hi]
             w.mul_(1 - float(h["lr"]) * float(h["wd"]))
-            m[lo:hi].mul_(float(h["b1"])).add_(gr, alpha=1 - float(h["b1"]))
+            mf = m[lo:hi].float() * float(h["b1"]) + (1 - float(h["b1"])) * gr
+            m[lo:hi] = mf.to(m.dtype)          # a bf16 first moment rounds once per update
             v[lo:hi].mul_(float(h["b2"])).addcmul_(gr, gr, value=1 - float(h["b2"]))
             denom = v[lo:hi].sqrt() / math.sqrt(bc2) + float(h["eps"])
-            w.addcdiv_(m[lo:hi], denom, value=-float(h["lr"]) / bc1)
+            w.addcdiv_(mf, denom, value=-float(h["lr"]) / bc1)
         p16[sl] = p32[sl].to(p16.dtype)
