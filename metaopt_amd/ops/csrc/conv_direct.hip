@@ -289,16 +289,7 @@ __global__ __launch_bounds__(256) void dconv_wgrad_kernel(const bf16_t* __restri
 #pragma unroll
     for (int j = 0; j < NFT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // this lane's two pixel rows of each 32-pixel k step: halo offsets (same for every band)
   constexpr int NKS = NPX / 32;
-  int pa[NKS], pb[NKS];
-#pragma unroll
-  for (int ks = 0; ks < NKS; ++ks) {
-    const int ka = 32 * ks + 8 * gq + q;
-    pa[ks] = pix_base<CI, S>(g, ka);
-    pb[ks] = pix_base<CI, S>(g, ka + 4);
-  }
-
   const int ow = 1 << g.owl, ppi = 1 << g.rpil;
   const bf16_t* xp = x + p * ((int64_t)g.Bn * g.H * g.H * CI);
   const bf16_t* dyp = dy + p * ((int64_t)g.Bn * g.OH * ow * CO);
@@ -315,9 +306,12 @@ __global__ __launch_bounds__(256) void dconv_wgrad_kernel(const bf16_t* __restri
       *(uint4*)(ds + row * LSD + 8 * cc) = v;
     }
     __syncthreads();
-#pragma unroll
+    // (offsets recomputed per step: hoisting all NKS of them and unrolling fully doubled the
+    //  VGPRs of the 16-channel kernel and cost more in occupancy than the ALU saved)
+#pragma unroll 2
     for (int ks = 0; ks < NKS; ++ks) {
       const int ka = 32 * ks + 8 * gq + q, kb = ka + 4;  // the lane's two pixel rows
+      const int pa = pix_base<CI, S>(g, ka), pb = pix_base<CI, S>(g, kb);
       bf16x8 b[NFT];
 #pragma unroll
       for (int j = 0; j < NFT; ++j)
@@ -326,8 +320,8 @@ __global__ __launch_bounds__(256) void dconv_wgrad_kernel(const bf16_t* __restri
 #pragma unroll
       for (int i = 0; i < MFW; ++i) {
         if (wave + 4 * i >= MFT) continue;  // wave-uniform
-        const bf16x8 a = cat_frag(lds_tr4(mvalid[i] ? hs + pa[ks] + co_off[i] : zs),
-                                  lds_tr4(mvalid[i] ? hs + pb[ks] + co_off[i] : zs));
+        const bf16x8 a = cat_frag(lds_tr4(mvalid[i] ? hs + pa + co_off[i] : zs),
+                                  lds_tr4(mvalid[i] ? hs + pb + co_off[i] : zs));
 #pragma unroll
         for (int j = 0; j < NFT; ++j) acc[i][j] = mfma16(a, b[j], acc[i][j]);
       }
