@@ -84,12 +84,12 @@ class PopulationResNet(FlatPopulation):
         return int(x.shape[0])
 
     # ------------------------------------------------------------------ forward
-    def _conv_bn(self, name, x, stride, train, res=None, relu=True, arena=None):
+    def _conv_bn(self, name, x, stride, train, res=None, relu=True, arena=None, **mail):
         P, W = self.capacity, self.W
         w = W[f"{name}.w"]
         running = self.A[f"{name}.running"].view(P, 2, w.shape[-1])
         return cops.conv_bn_act(x, w, W[f"{name}.g"], W[f"{name}.b"], running, P, stride, train,
-                                res=res, relu=relu, arena=arena)
+                                res=res, relu=relu, arena=arena, **mail)
 
     @staticmethod
     def _shortcut(x, cout, stride):
@@ -112,6 +112,14 @@ class PopulationResNet(FlatPopulation):
             for b in range(self.blocks):
                 n1, _, c1, s1 = next(it)
                 n2, _, c2, _ = next(it)
+                if train and arena is not None and s1 == 1 and h.shape[-1] == c2:
+                    # identity shortcut: its gradient joins the first conv's data gradient in
+                    # that kernel's epilogue (no separate add over the block input)
+                    box = {}
+                    t = self._conv_bn(n1, h, s1, train, arena=arena, conv_mailbox=box)
+                    h = self._conv_bn(n2, t, 1, train, res=h.detach(), arena=arena,
+                                      bn_mailbox=box)
+                    continue
                 r = self._shortcut(h, c2, s1)
                 t = self._conv_bn(n1, h, s1, train, arena=arena)
                 h = self._conv_bn(n2, t, 1, train, res=r, arena=arena)

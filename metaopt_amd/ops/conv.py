@@ -99,13 +99,13 @@ def _pow2(v):
     return v >= 1 and (v & (v - 1)) == 0
 
 
-def _dconv(kind, a, b, out, P, Bn, H, W, Ci, Co, stride, sums=None):
+def _dconv(kind, a, b, out, P, Bn, H, W, Ci, Co, stride, sums=None, addend=None):
     """Direct (halo-tiled) convolution kernels of csrc/conv_direct.hip; False when the shape has
     no instantiation (the caller then runs the implicit GEMM)."""
     if not _DIRECT or H != W:
         return False
     lib = _lib.get_lib()
-    aux = sums
+    aux = sums if kind == 0 else addend
     if kind == 2:
         nb = lib.mopt_dconv_wgrad_splits(P, Bn, H, Ci, Co, stride)
         if nb <= 0:
@@ -119,8 +119,9 @@ def _dconv(kind, a, b, out, P, Bn, H, W, Ci, Co, stride, sums=None):
     return True
 
 
-def _pconv(kind, a, b, out, P, Bn, H, W, Ci, Co, stride, sums=None):
-    if _dconv(kind, a, b, out, P, Bn, H, W, Ci, Co, stride, sums):
+def _pconv(kind, a, b, out, P, Bn, H, W, Ci, Co, stride, sums=None, addend=None):
+    """``addend`` (kind 1): a tensor shaped like ``out`` added to the data gradient."""
+    if _dconv(kind, a, b, out, P, Bn, H, W, Ci, Co, stride, sums, addend):
         return out, sums is not None
     OH, OW = out_hw(H, stride), out_hw(W, stride)
     M, N, K = {0: (Bn * OH * OW, Co, 9 * Ci), 1: (Bn * H * W, Ci, 9 * Co),
@@ -133,12 +134,14 @@ def _pconv(kind, a, b, out, P, Bn, H, W, Ci, Co, stride, sums=None):
     _call("mopt_pconv", kind, a.data_ptr(), b.data_ptr(), out.data_ptr(),
           0 if part is None else part.data_ptr(), P, Bn, H, W, Ci, Co, stride, cfg, splits, kps,
           _s(out))
+    if addend is not None:
+        out.add_(addend)
     return out, False
 
 
 class _Conv3x3(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, P, stride, grad_out, stats=None):
+    def forward(ctx, x, w, P, stride, grad_out, stats=None, mailbox=None):
         N, H, W, Ci = x.shape
         Co = w.shape[-1]
         Bn = N // P
@@ -153,6 +156,7 @@ class _Conv3x3(torch.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.meta = (P, Bn, H, W, Ci, Co, stride)
         ctx.grad_out = grad_out
+        ctx.mailbox = mailbox
         return y
 
     @staticmethod
@@ -163,17 +167,20 @@ class _Conv3x3(torch.autograd.Function):
         dx = dw = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
-            _pconv(1, dy, w, dx, P, Bn, H, W, Ci, Co, stride)
+            # the identity shortcut's gradient (left by the block's last BatchNorm) joins here,
+            # in the data-gradient epilogue, instead of in a separate autograd add
+            addend = ctx.mailbox.pop("dres", None) if ctx.mailbox is not None else None
+            _pconv(1, dy, w, dx, P, Bn, H, W, Ci, Co, stride, addend=addend)
         if ctx.needs_input_grad[1]:
             if ctx.grad_out is not None:         # straight into the flat gradient buffer
                 _pconv(2, x, dy, ctx.grad_out, P, Bn, H, W, Ci, Co, stride)
             else:
                 dw = torch.empty_like(w)
                 _pconv(2, x, dy, dw, P, Bn, H, W, Ci, Co, stride)
-        return dx, dw, None, None, None, None
+        return dx, dw, None, None, None, None, None
 
 
-def conv3x3(x, w, P, stride, stats=None):
+def conv3x3(x, w, P, stride, stats=None, mailbox=None):
     """Population 3x3 convolution: x [P*B, H, W, Cin] bf16, w [P, 9 Cin, Cout].  ``stats`` (HIP
     only): ``[sums, False]`` with zeroed f32 sums [P, 2, Cout]; when the direct kernel ran, the
     per-trial channel sums of the output and of its square were added and the flag is True."""
@@ -186,13 +193,13 @@ def conv3x3(x, w, P, stride, stats=None):
         raise ValueError(f"conv3x3: needs power-of-two H, W, channels (>= 8) and w [P, 9C, Co]; "
                          f"got x {tuple(x.shape)} w {tuple(w.shape)} P {P}")
     grad_out = w.grad if (w.requires_grad and w.is_leaf and w.grad is not None) else None
-    return _Conv3x3.apply(x.contiguous(), w.contiguous(), P, stride, grad_out, stats)
+    return _Conv3x3.apply(x.contiguous(), w.contiguous(), P, stride, grad_out, stats, mailbox)
 
 
 class _BNAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, res, running, P, train, relu, eps, momentum, sums=None,
-                arena=None):
+                arena=None, mailbox=None):
         C = x.shape[-1]
         M = x.numel() // (P * C)
         y = torch.empty_like(x)
@@ -213,6 +220,7 @@ class _BNAct(torch.autograd.Function):
         ctx.bwd_sums = arena.take(P * 2 * C).view(P, 2, C) if arena is not None else None
         ctx.grads = tuple(t.grad if (t.requires_grad and t.is_leaf and t.grad is not None) else None
                           for t in (gamma, beta))
+        ctx.mailbox = mailbox
         return y
 
     @staticmethod
@@ -231,15 +239,18 @@ class _BNAct(torch.autograd.Function):
               gamma.data_ptr(), dx.data_ptr(), 0 if dres is None else dres.data_ptr(),
               sums.data_ptr(), gg.data_ptr() if direct else 0, gb.data_ptr() if direct else 0,
               P, M, C, int(relu), int(zeroed), _s(x))
+        if dres is not None and ctx.mailbox is not None:
+            ctx.mailbox["dres"] = dres     # picked up by the block's first convolution
+            dres = None
         if direct:
-            return dx, None, None, dres, None, None, None, None, None, None, None, None
+            return dx, None, None, dres, None, None, None, None, None, None, None, None, None
         dgamma = sums[:, 1].to(gamma.dtype)
         dbeta = sums[:, 0].to(gamma.dtype)
-        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None
 
 
 def bn_act(x, gamma, beta, running, P, train, res=None, relu=True, eps=1e-5, momentum=0.1,
-           sums=None, arena=None):
+           sums=None, arena=None, mailbox=None):
     """y = relu?(BN(x) + res?) per trial; ``running`` [P, 2, C] f32 updated when training.
     ``sums``: precomputed f32 [P, 2, C] batch sums of x and x^2 (the producing convolution's
     epilogue) -- the statistics pass is skipped."""
@@ -247,7 +258,7 @@ def bn_act(x, gamma, beta, running, P, train, res=None, relu=True, eps=1e-5, mom
         return bn_act_ref(x, gamma, beta, running, P, train, res, relu, eps, momentum)
     return _BNAct.apply(x.contiguous(), gamma.contiguous(), beta.contiguous(),
                         None if res is None else res.contiguous(), running, P, train, relu, eps,
-                        momentum, sums, arena)
+                        momentum, sums, arena, mailbox)
 
 
 class ZeroArena:
@@ -266,7 +277,12 @@ class ZeroArena:
         return v
 
 
-def conv_bn_act(x, w, gamma, beta, running, P, stride, train, res=None, relu=True, arena=None):
+def conv_bn_act(x, w, gamma, beta, running, P, stride, train, res=None, relu=True, arena=None,
+                conv_mailbox=None, bn_mailbox=None):
+    """``bn_mailbox`` / ``conv_mailbox`` (one dict per residual block, HIP path): the block's last
+    BatchNorm leaves the identity shortcut's gradient there and the block's first convolution
+    adds it in its data-gradient epilogue -- pass ``res`` detached so autograd does not add it
+    a second time."""
     """relu?(BN(conv3x3(x, w)) + res?): on the HIP path the convolution's epilogue produces the
     BatchNorm batch statistics (no separate reduction pass over the conv output)."""
     if x.device.type != "cuda":
@@ -278,7 +294,7 @@ def conv_bn_act(x, w, gamma, beta, running, P, stride, train, res=None, relu=Tru
         z = arena.take(P * 2 * Co).view(P, 2, Co) if arena is not None else \
             torch.zeros(P, 2, Co, dtype=torch.float32, device=x.device)
         stats = [z, False]
-    y = conv3x3(x, w, P, stride, stats)
+    y = conv3x3(x, w, P, stride, stats, mailbox=conv_mailbox)
     return bn_act(y, gamma, beta, running, P, train, res=res, relu=relu,
                   sums=stats[0] if stats is not None and stats[1] else None,
-                  arena=arena if train else None)
+                  arena=arena if train else None, mailbox=bn_mailbox)

@@ -105,7 +105,9 @@ template <int CI, int CO, int NPX, int MODE, int S>
 __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict__ x,
                                                         const bf16_t* __restrict__ w,
                                                         bf16_t* __restrict__ y,
-                                                        float* __restrict__ sums, const Geom g) {
+                                                        float* __restrict__ sums,
+                                                        const bf16_t* __restrict__ addend,
+                                                        const Geom g) {
   constexpr int mode = MODE;
   constexpr int KS = (9 * CI + 31) / 32;  // 32-wide k steps (k = tap * CI + c)
   constexpr int WN = CO / 16, WM = 4 / WN;
@@ -237,9 +239,21 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
     // the band's output is contiguous: (b0, oy0 .. oy0 + TR) or whole images b0 ..
     bf16_t* yt = yp + ((int64_t)b0 * g.OH + oy0) * (1 << g.owl) * CO;
     constexpr int CPR = CO / 8;
+    const bf16_t* at = addend == nullptr ? nullptr : addend + (yt - y);
     for (int c = threadIdx.x; c < valid * CPR; c += 256) {
       const int row = c / CPR, cc = c % CPR;
-      *(uint4*)(yt + (int64_t)row * CO + 8 * cc) = *(const uint4*)(cs + row * LSC + 8 * cc);
+      uint4 v = *(const uint4*)(cs + row * LSC + 8 * cc);
+      if (at != nullptr) {  // data gradient + the residual branch's gradient (identity shortcut)
+        const uint4 a = *(const uint4*)(at + (int64_t)row * CO + 8 * cc);
+        const uint32_t vw[4] = {v.x, v.y, v.z, v.w}, aw[4] = {a.x, a.y, a.z, a.w};
+        uint32_t o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          o[e] = pack2bf(bf2f(vw[e] & 0xFFFF) + bf2f(aw[e] & 0xFFFF),
+                         bf2f(vw[e] >> 16) + bf2f(aw[e] >> 16));
+        v = make_uint4(o[0], o[1], o[2], o[3]);
+      }
+      *(uint4*)(yt + (int64_t)row * CO + 8 * cc) = v;
     }
     __syncthreads();  // the next band's halo overwrites the output tile
   }
@@ -344,16 +358,26 @@ __global__ __launch_bounds__(256) void dconv_wgrad_kernel(const bf16_t* __restri
   }
 }
 
-// out[p][i] (bf16, batch stride sO) = sum over the nb partials [nb][P][MN]
+// out[p][i] (bf16, batch stride sO) = sum over the nb partials [nb][P][MN]; 4 elements per
+// thread (16-byte partial loads, MN % 4 == 0), the nb loads of a thread issued 4 at a time
 __global__ __launch_bounds__(256) void dconv_reduce_kernel(const float* __restrict__ part,
                                                            bf16_t* __restrict__ out, int64_t sO,
                                                            int P, int MN, int nb) {
   const int64_t total = (int64_t)P * MN;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t i = 4 * ((int64_t)blockIdx.x * 256 + threadIdx.x);
   if (i >= total) return;
-  float s = 0.f;
-  for (int k = 0; k < nb; ++k) s += part[k * total + i];
-  out[(i / MN) * sO + i % MN] = f2bf(s);
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  int k = 0;
+  for (; k + 4 <= nb; k += 4) {
+    const f32x4 a = *(const f32x4*)(part + k * total + i);
+    const f32x4 b = *(const f32x4*)(part + (k + 1) * total + i);
+    const f32x4 c = *(const f32x4*)(part + (k + 2) * total + i);
+    const f32x4 d = *(const f32x4*)(part + (k + 3) * total + i);
+    s += (a + b) + (c + d);
+  }
+  for (; k < nb; ++k) s += *(const f32x4*)(part + k * total + i);
+  bf16_t* o = out + (i / MN) * sO + i % MN;  // 4 | MN: the 4 elements share a trial
+  *(uint2*)o = f32_to_bf4(s);
 }
 
 int ilog2i(int v) {
@@ -398,7 +422,7 @@ size_t halo_bytes(const Geom& g) { return (size_t)g.IMGS * g.TRI * g.WI * pstrid
 // S: the stride of the halo layout (kDgrad2 reads its half-resolution dy band at layout S = 1)
 template <int CI, int CO, int MODE, int S>
 int launch_fwd(const void* x, const void* w, void* y, void* sums, int P, int Bn, int H,
-               hipStream_t st) {
+               hipStream_t st, const void* addend = nullptr) {
   constexpr int NPX = npx_for(CO);
   Geom g{};
   // (64-wide outputs: half the workgroups, twice the bands each -- their weight prologue is long)
@@ -408,7 +432,8 @@ int launch_fwd(const void* x, const void* w, void* y, void* sums, int P, int Bn,
   if (lds > 64 * 1024) return (int)hipErrorNotSupported;
   g.lds_elems = (int)(lds / 2);
   hipLaunchKernelGGL((dconv_fwd_kernel<CI, CO, NPX, MODE, S>), dim3(P * g.nb), dim3(256), lds, st,
-                     (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)sums, g);
+                     (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)sums,
+                     (const bf16_t*)addend, g);
   return (int)hipGetLastError();
 }
 
@@ -434,7 +459,7 @@ int launch_wgrad(const void* x, const void* dy, void* dw, void* part, int P, int
                      (const bf16_t*)x, (const bf16_t*)dy, (float*)part, g, P);
   const int MN = 9 * CI * CO;
   const int64_t total = (int64_t)P * MN;
-  hipLaunchKernelGGL(dconv_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
+  hipLaunchKernelGGL(dconv_reduce_kernel, dim3((unsigned)((total / 4 + 255) / 256)), dim3(256), 0, st,
                      (const float*)part, (bf16_t*)dw, (int64_t)MN, P, MN, g.nb);
   return (int)hipGetLastError();
 }
@@ -450,7 +475,8 @@ extern "C" {
 // Direct 3x3 convolution (pad 1) of a population, NHWC bf16, square power-of-two images:
 //   kind 0 forward   y [P*Bn, H/S, H/S, Co] = conv(x [P*Bn, H, H, Ci], w [P, 9 Ci, Co]);
 //                    aux = f32 sums [P][2][Co] (zeroed by the caller; += sum, sum^2 of y) or 0
-//   kind 1 dgrad     dx [P*Bn, H, H, Ci] from dy [P*Bn, H/S, H/S, Co] and w [P, 9 Ci, Co]
+//   kind 1 dgrad     dx [P*Bn, H, H, Ci] from dy [P*Bn, H/S, H/S, Co] and w [P, 9 Ci, Co];
+//                    aux = bf16 addend shaped like dx (added in the epilogue) or 0
 //   kind 2 wgrad     dw [P, 9 Ci, Co] (bf16) from x and dy; aux = f32 partials
 //                    [nb][P][9 Ci][Co], nb from mopt_dconv_wgrad_splits
 // Returns hipErrorNotSupported (801) for shapes without an instantiation: the caller falls
@@ -470,8 +496,8 @@ int mopt_dconv(int kind, const void* a, const void* b, void* out, void* aux, int
   if (kind == 1) {  // the forward kernel over dy (Co channels) with flipped transposed weights
 #define X(ci, co) \
     if (Co == ci && Ci == co) \
-      return stride == 1 ? launch_fwd<ci, co, kDgrad, 1>(a, b, out, nullptr, P, Bn, H, st) \
-                         : launch_fwd<ci, co, kDgrad2, 1>(a, b, out, nullptr, P, Bn, H, st);
+      return stride == 1 ? launch_fwd<ci, co, kDgrad, 1>(a, b, out, nullptr, P, Bn, H, st, aux) \
+                         : launch_fwd<ci, co, kDgrad2, 1>(a, b, out, nullptr, P, Bn, H, st, aux);
     MOPT_DCONV_DGRAD_SHAPES(X)
 #undef X
     return (int)hipErrorNotSupported;

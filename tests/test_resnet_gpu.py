@@ -70,6 +70,9 @@ def test_direct_conv_kernels(stride, C, Cout, H):
         dx = torch.empty_like(x)
         assert cops._dconv(1, dy, w, dx, P, B, H, H, C, Cout, stride)
         _close(dx, xr.grad, 1e-2)
+        addend = torch.randn_like(x)          # residual-branch gradient fused in the epilogue
+        assert cops._dconv(1, dy, w, dx, P, B, H, H, C, Cout, stride, addend=addend)
+        _close(dx, xr.grad + addend.float(), 1e-2)
 
 
 def test_conv_bn_act_fused_statistics():
