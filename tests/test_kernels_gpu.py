@@ -240,3 +240,30 @@ def test_checkpoint_pool_roundtrip(data, mdt):
     # the bf16 working copy is the split master's hi half: round to nearest (ties toward zero)
     assert torch.equal(hip.p16[b:b + n], split_f32(ref1["p32"])[0])
     assert hip.steps_done(4) == ref1["t"] and hip.members[4].width == CONFIGS[0].width
+
+
+@pytest.mark.parametrize("mdt", ["fp32", "bf16"])
+def test_sidecar_resume_equals_in_hbm_resume_and_uninterrupted(data, tmp_path, mdt):
+    """A promoted trial resumed from its on-disk sidecar (slot_state -> torch.save -> load with
+    weights_only -> load_slot_state), one resumed from the in-HBM checkpoint pool and the same
+    trial trained without interruption take bitwise identical steps afterwards."""
+    hip, _ = _pair(momentum_dtype=mdt)
+    for step in range(3):
+        hip.train_step(*data.batch(step))
+    hip.alloc_ckpt_pool(2)
+    meta = hip.save_states([(2, 1)])[0]
+    path = tmp_path / "device_state.pt"
+    torch.save(hip.slot_state(2, to_cpu=True), path)
+    hip.load_states([(5, meta)])                                  # in-HBM resume
+    hip.load_slot_state(0, torch.load(path, weights_only=True))   # sidecar resume
+    assert hip.steps_done(0) == hip.steps_done(5) == hip.steps_done(2) == 3
+    for step in range(3, 7):
+        hip.train_step(*data.batch(step))
+    torch.cuda.synchronize()
+    for (a, ab), (b, bb), (c, cb) in zip(hip.layer_views(2), hip.layer_views(5),
+                                         hip.layer_views(0)):
+        assert torch.equal(a, b) and torch.equal(a, c)
+        assert torch.equal(ab, bb) and torch.equal(ab, cb)
+    assert torch.equal(hip.master(2), hip.master(5)) and torch.equal(hip.master(2), hip.master(0))
+    loss = hip.train_loss()
+    assert loss[2] == loss[5] == loss[0]

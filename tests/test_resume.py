@@ -44,38 +44,38 @@ def _data():
     return TeacherClassification(n_train=512, n_val=128, batch_size=128, seed=11)
 
 
-def _make(storage, data, comm=None, **kw):
+def _make(storage, data, comm=None, cap=4, **kw):
     exp = None
     if comm is None or comm.is_root:
         exp = build_experiment("resume-sweep", priors=PRIORS, algorithms=ALGO,
                                max_trials=MAX_TRIALS, storage=storage)
-    pop = PopulationMLP(4, max_width=128, eval_batch=128, device="cpu")
+    pop = PopulationMLP(cap, max_width=128, eval_batch=128, device="cpu")
     return exp, PopulationSweep(pop, MLPSweepTask(priors=PRIORS, max_width=128), data,
                                 comm=comm, experiment=exp, sync_every=16,
                                 ckpt_capacity=64, **kw)
 
 
-def _phase_worker(rank, world, port, db_path, ckpt_dir, max_steps, resume, q):
+def _phase_worker(rank, world, port, db_path, ckpt_dir, max_steps, resume, q, cap=4):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     torch.set_num_threads(2)
     from metaopt_amd.parallel.comm import init_from_env, shutdown
     comm = init_from_env(backend="gloo")
     storage = DocumentStorage(PickledDB(host=db_path)) if comm.is_root else None
-    _, sweep = _make(storage, _data(), comm=comm, resume=resume, restore_algorithm=resume,
-                     ckpt_dir=ckpt_dir)
+    _, sweep = _make(storage, _data(), comm=comm, cap=cap, resume=resume,
+                     restore_algorithm=resume, ckpt_dir=ckpt_dir)
     sweep.run(max_steps)
     sweep.close()
     q.put((rank, sweep.done, sweep.n_resumed, sweep.n_resume_missing))
     shutdown()
 
 
-def _run_phase(db_path, ckpt_dir, max_steps, resume, world=2):
+def _run_phase(db_path, ckpt_dir, max_steps, resume, world=2, cap=4):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_phase_worker,
-                         args=(r, world, port, db_path, ckpt_dir, max_steps, resume, q))
+                         args=(r, world, port, db_path, ckpt_dir, max_steps, resume, q, cap))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -190,3 +190,18 @@ def test_sweep_cli_resume(tmp_path, capsys):
     assert stati.count("completed") + stati.count("broken") >= 40
     assert len({t.id for t in trials}) == len(trials)
     assert second["completed"] > 0
+
+
+def test_two_rank_sweep_equals_one_rank_with_the_same_slots(tmp_path):
+    """The trial-parallel engine is placement-invariant: 2 ranks x 4 slots (gloo) and 1 rank x
+    8 slots finish the same trials with the same objectives and build the same ASHA rungs."""
+    one = str(tmp_path / "one.pkl")
+    two = str(tmp_path / "two.pkl")
+    assert all(r[1] for r in _run_phase(one, None, 100000, resume=False, world=1, cap=8))
+    assert all(r[1] for r in _run_phase(two, None, 100000, resume=False, world=2, cap=4))
+    done1, _, rungs1 = _outcome(one)
+    done2, _, rungs2 = _outcome(two)
+    assert len(done1) == MAX_TRIALS and set(done1) == set(done2)
+    for tid, obj in done1.items():
+        assert done2[tid] == pytest.approx(obj, rel=1e-6, abs=1e-9), tid
+    assert rungs1 == rungs2
