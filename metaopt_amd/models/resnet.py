@@ -95,8 +95,7 @@ class PopulationResNet(FlatPopulation):
     def _shortcut(x, cout, stride):
         if stride == 1 and x.shape[-1] == cout:
             return x
-        y = x[:, ::stride, ::stride, :]
-        return torch.nn.functional.pad(y, (0, cout - x.shape[-1])).contiguous()
+        return cops.option_a_shortcut(x, cout)
 
     def _loss(self, x, y, train: bool):
         P, W = self.capacity, self.W
@@ -112,13 +111,15 @@ class PopulationResNet(FlatPopulation):
             for b in range(self.blocks):
                 n1, _, c1, s1 = next(it)
                 n2, _, c2, _ = next(it)
-                if train and arena is not None and s1 == 1 and h.shape[-1] == c2:
-                    # identity shortcut: its gradient joins the first conv's data gradient in
-                    # that kernel's epilogue (no separate add over the block input)
+                identity = s1 == 1 and h.shape[-1] == c2
+                if train and arena is not None and (identity or s1 == 2):
+                    # the shortcut's gradient joins the first conv's data gradient in that
+                    # kernel's epilogue (no separate add over the block input); an option-A
+                    # shortcut is also read in place by the BatchNorm (no padded copy)
                     box = {}
                     t = self._conv_bn(n1, h, s1, train, arena=arena, conv_mailbox=box)
                     h = self._conv_bn(n2, t, 1, train, res=h.detach(), arena=arena,
-                                      bn_mailbox=box)
+                                      bn_mailbox=box, res_sub2=not identity)
                     continue
                 r = self._shortcut(h, c2, s1)
                 t = self._conv_bn(n1, h, s1, train, arena=arena)

@@ -26,10 +26,10 @@ c_void_p, c_int, c_float, c_int64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_floa
 
 _lib.register_signatures({
     "mopt_bn_fwd": ([c_void_p] * 8 + [c_int, c_int64, c_int, c_float, c_float, c_int, c_int,
-                                     c_int, c_void_p], c_int),
+                                     c_int, c_int, c_int, c_void_p], c_int),
     "mopt_bn_bwd": ([c_void_p] * 10 + [c_int, c_int64, c_int, c_int, c_int, c_void_p], c_int),
     "mopt_pconv": ([c_int] + [c_void_p] * 4 + [c_int] * 10 + [c_void_p], c_int),
-    "mopt_dconv": ([c_int] + [c_void_p] * 4 + [c_int] * 6 + [c_void_p], c_int),
+    "mopt_dconv": ([c_int] + [c_void_p] * 4 + [c_int] * 7 + [c_void_p], c_int),
     "mopt_dconv_wgrad_splits": ([c_int] * 6, c_int),
 })
 
@@ -99,7 +99,7 @@ def _pow2(v):
     return v >= 1 and (v & (v - 1)) == 0
 
 
-def _dconv(kind, a, b, out, P, Bn, H, W, Ci, Co, stride, sums=None, addend=None):
+def _dconv(kind, a, b, out, P, Bn, H, W, Ci, Co, stride, sums=None, addend=None, addend_c=0):
     """Direct (halo-tiled) convolution kernels of csrc/conv_direct.hip; False when the shape has
     no instantiation (the caller then runs the implicit GEMM)."""
     if not _DIRECT or H != W:
@@ -112,16 +112,18 @@ def _dconv(kind, a, b, out, P, Bn, H, W, Ci, Co, stride, sums=None, addend=None)
             return False
         aux = torch.empty(nb * P * 9 * Ci * Co, dtype=torch.float32, device=out.device)
     rc = lib.mopt_dconv(kind, a.data_ptr(), b.data_ptr(), out.data_ptr(),
-                        0 if aux is None else aux.data_ptr(), P, Bn, H, Ci, Co, stride, _s(out))
+                        0 if aux is None else aux.data_ptr(), P, Bn, H, Ci, Co, stride,
+                        addend_c if kind == 1 else 0, _s(out))
     if rc == _NOT_SUPPORTED:
         return False
     _lib.check(rc, "mopt_dconv")
     return True
 
 
-def _pconv(kind, a, b, out, P, Bn, H, W, Ci, Co, stride, sums=None, addend=None):
-    """``addend`` (kind 1): a tensor shaped like ``out`` added to the data gradient."""
-    if _dconv(kind, a, b, out, P, Bn, H, W, Ci, Co, stride, sums, addend):
+def _pconv(kind, a, b, out, P, Bn, H, W, Ci, Co, stride, sums=None, addend=None, addend_c=0):
+    """``addend`` (kind 1): added to the data gradient -- shaped like ``out``, or (``addend_c``
+    > 0) the half-resolution gradient of an option-A shortcut, added at the even pixels."""
+    if _dconv(kind, a, b, out, P, Bn, H, W, Ci, Co, stride, sums, addend, addend_c):
         return out, sums is not None
     OH, OW = out_hw(H, stride), out_hw(W, stride)
     M, N, K = {0: (Bn * OH * OW, Co, 9 * Ci), 1: (Bn * H * W, Ci, 9 * Co),
@@ -134,7 +136,9 @@ def _pconv(kind, a, b, out, P, Bn, H, W, Ci, Co, stride, sums=None, addend=None)
     _call("mopt_pconv", kind, a.data_ptr(), b.data_ptr(), out.data_ptr(),
           0 if part is None else part.data_ptr(), P, Bn, H, W, Ci, Co, stride, cfg, splits, kps,
           _s(out))
-    if addend is not None:
+    if addend is not None and addend_c:
+        out[:, ::2, ::2, :] += addend[..., :out.shape[-1]]
+    elif addend is not None:
         out.add_(addend)
     return out, False
 
@@ -170,7 +174,9 @@ class _Conv3x3(torch.autograd.Function):
             # the identity shortcut's gradient (left by the block's last BatchNorm) joins here,
             # in the data-gradient epilogue, instead of in a separate autograd add
             addend = ctx.mailbox.pop("dres", None) if ctx.mailbox is not None else None
-            _pconv(1, dy, w, dx, P, Bn, H, W, Ci, Co, stride, addend=addend)
+            sub2 = addend is not None and ctx.mailbox.pop("sub2", False)
+            _pconv(1, dy, w, dx, P, Bn, H, W, Ci, Co, stride, addend=addend,
+                   addend_c=addend.shape[-1] if sub2 else 0)
         if ctx.needs_input_grad[1]:
             if ctx.grad_out is not None:         # straight into the flat gradient buffer
                 _pconv(2, x, dy, ctx.grad_out, P, Bn, H, W, Ci, Co, stride)
@@ -199,7 +205,7 @@ def conv3x3(x, w, P, stride, stats=None, mailbox=None):
 class _BNAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, res, running, P, train, relu, eps, momentum, sums=None,
-                arena=None, mailbox=None):
+                arena=None, mailbox=None, res_sub2=False):
         C = x.shape[-1]
         M = x.numel() // (P * C)
         y = torch.empty_like(x)
@@ -210,7 +216,8 @@ class _BNAct(torch.autograd.Function):
         _call("mopt_bn_fwd", x.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
               0 if res is None else res.data_ptr(), y.data_ptr(), stat.data_ptr(),
               running.data_ptr(), sums.data_ptr(), P, M, C, eps, momentum, int(train), int(relu),
-              int(ready), _s(x))
+              int(ready), res.shape[-1] if res_sub2 else 0,
+              (x.shape[1].bit_length() - 1) if res_sub2 else 0, _s(x))
         # (recomputing relu'(y) from x, gamma, beta instead of keeping y measured slower:
         #  187 -> 229 us for the stage-1 backward pair on one MI355X)
         ctx.save_for_backward(x, y, stat, gamma)
@@ -221,6 +228,7 @@ class _BNAct(torch.autograd.Function):
         ctx.grads = tuple(t.grad if (t.requires_grad and t.is_leaf and t.grad is not None) else None
                           for t in (gamma, beta))
         ctx.mailbox = mailbox
+        ctx.res_sub2 = res_sub2
         return y
 
     @staticmethod
@@ -241,24 +249,37 @@ class _BNAct(torch.autograd.Function):
               P, M, C, int(relu), int(zeroed), _s(x))
         if dres is not None and ctx.mailbox is not None:
             ctx.mailbox["dres"] = dres     # picked up by the block's first convolution
+            ctx.mailbox["sub2"] = ctx.res_sub2
             dres = None
         if direct:
-            return dx, None, None, dres, None, None, None, None, None, None, None, None, None
+            return dx, None, None, dres, None, None, None, None, None, None, None, None, None, None
         dgamma = sums[:, 1].to(gamma.dtype)
         dbeta = sums[:, 0].to(gamma.dtype)
-        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None
+
+
+def option_a_shortcut(h, cout):
+    """ResNet option-A shortcut: stride-2 subsample, zero-pad channels to ``cout`` (NHWC)."""
+    y = h[:, ::2, ::2, :]
+    return torch.nn.functional.pad(y, (0, cout - h.shape[-1])).contiguous()
 
 
 def bn_act(x, gamma, beta, running, P, train, res=None, relu=True, eps=1e-5, momentum=0.1,
-           sums=None, arena=None, mailbox=None):
+           sums=None, arena=None, mailbox=None, res_sub2=False):
+    """``res_sub2``: ``res`` is the full-resolution block input and the residual its option-A
+    shortcut, read in place by the kernel (no subsampled / padded copy)."""
     """y = relu?(BN(x) + res?) per trial; ``running`` [P, 2, C] f32 updated when training.
     ``sums``: precomputed f32 [P, 2, C] batch sums of x and x^2 (the producing convolution's
     epilogue) -- the statistics pass is skipped."""
-    if x.device.type != "cuda":
-        return bn_act_ref(x, gamma, beta, running, P, train, res, relu, eps, momentum)
+    if x.device.type != "cuda" or (res_sub2 and x.shape[1] & (x.shape[1] - 1)):
+        if res_sub2:
+            res = option_a_shortcut(res, x.shape[-1])
+        if x.device.type != "cuda":
+            return bn_act_ref(x, gamma, beta, running, P, train, res, relu, eps, momentum)
+        res_sub2 = False
     return _BNAct.apply(x.contiguous(), gamma.contiguous(), beta.contiguous(),
                         None if res is None else res.contiguous(), running, P, train, relu, eps,
-                        momentum, sums, arena, mailbox)
+                        momentum, sums, arena, mailbox, res_sub2)
 
 
 class ZeroArena:
@@ -278,7 +299,7 @@ class ZeroArena:
 
 
 def conv_bn_act(x, w, gamma, beta, running, P, stride, train, res=None, relu=True, arena=None,
-                conv_mailbox=None, bn_mailbox=None):
+                conv_mailbox=None, bn_mailbox=None, res_sub2=False):
     """``bn_mailbox`` / ``conv_mailbox`` (one dict per residual block, HIP path): the block's last
     BatchNorm leaves the identity shortcut's gradient there and the block's first convolution
     adds it in its data-gradient epilogue -- pass ``res`` detached so autograd does not add it
@@ -286,6 +307,8 @@ def conv_bn_act(x, w, gamma, beta, running, P, stride, train, res=None, relu=Tru
     """relu?(BN(conv3x3(x, w)) + res?): on the HIP path the convolution's epilogue produces the
     BatchNorm batch statistics (no separate reduction pass over the conv output)."""
     if x.device.type != "cuda":
+        if res_sub2:
+            res = option_a_shortcut(res, w.shape[-1])
         return bn_act_ref(conv3x3_ref(x, w, P, stride), gamma, beta, running, P, train, res,
                           relu)
     Co = w.shape[-1]
@@ -297,4 +320,4 @@ def conv_bn_act(x, w, gamma, beta, running, P, stride, train, res=None, relu=Tru
     y = conv3x3(x, w, P, stride, stats, mailbox=conv_mailbox)
     return bn_act(y, gamma, beta, running, P, train, res=res, relu=relu,
                   sums=stats[0] if stats is not None and stats[1] else None,
-                  arena=arena if train else None, mailbox=bn_mailbox)
+                  arena=arena if train else None, mailbox=bn_mailbox, res_sub2=res_sub2)

@@ -101,13 +101,16 @@ __device__ __forceinline__ int tap_off(const Geom& g, int k) {
   return (kh * g.WI + kw) * pstride<CI, S>() + c;
 }
 
-template <int CI, int CO, int NPX, int MODE, int S>
+// ADD: data-gradient epilogue addend -- 0 none, 1 same layout as the output (identity shortcut),
+// 2 half-resolution option-A shortcut gradient (compile-time: the epilogue code otherwise costs
+// the forward kernels registers and a wave per SIMD)
+template <int CI, int CO, int NPX, int MODE, int S, int ADD>
 __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict__ x,
                                                         const bf16_t* __restrict__ w,
                                                         bf16_t* __restrict__ y,
                                                         float* __restrict__ sums,
                                                         const bf16_t* __restrict__ addend,
-                                                        const Geom g) {
+                                                        const Geom g, int addend_c) {
   constexpr int mode = MODE;
   constexpr int KS = (9 * CI + 31) / 32;  // 32-wide k steps (k = tap * CI + c)
   constexpr int WN = CO / 16, WM = 4 / WN;
@@ -239,12 +242,24 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
     // the band's output is contiguous: (b0, oy0 .. oy0 + TR) or whole images b0 ..
     bf16_t* yt = yp + ((int64_t)b0 * g.OH + oy0) * (1 << g.owl) * CO;
     constexpr int CPR = CO / 8;
-    const bf16_t* at = addend == nullptr ? nullptr : addend + (yt - y);
+    const bf16_t* at = ADD == 1 ? addend + (yt - y) : nullptr;
     for (int c = threadIdx.x; c < valid * CPR; c += 256) {
       const int row = c / CPR, cc = c % CPR;
       uint4 v = *(const uint4*)(cs + row * LSC + 8 * cc);
-      if (at != nullptr) {  // data gradient + the residual branch's gradient (identity shortcut)
-        const uint4 a = *(const uint4*)(at + (int64_t)row * CO + 8 * cc);
+      const bf16_t* ap = nullptr;
+      if constexpr (ADD == 1) {  // identity shortcut: same layout as the output
+        ap = at + (int64_t)row * CO + 8 * cc;
+      } else if constexpr (ADD == 2) {  // option-A shortcut: its gradient lands on even pixels
+        const int b = b0 + (row >> g.rpil), rem = row & ((1 << g.rpil) - 1);
+        const int oy = oy0 + (rem >> g.owl), ox = rem & ((1 << g.owl) - 1);
+        if (((oy | ox) & 1) == 0) {
+          const int hs2 = g.OH >> 1;
+          ap = addend + ((((int64_t)p * g.Bn + b) * hs2 + (oy >> 1)) * hs2 + (ox >> 1)) *
+                            addend_c + 8 * cc;
+        }
+      }
+      if (ADD != 0 && ap != nullptr) {  // data gradient + the shortcut branch's gradient
+        const uint4 a = *(const uint4*)ap;
         const uint32_t vw[4] = {v.x, v.y, v.z, v.w}, aw[4] = {a.x, a.y, a.z, a.w};
         uint32_t o[4];
 #pragma unroll
@@ -420,9 +435,9 @@ template <int CI, int S>
 size_t halo_bytes(const Geom& g) { return (size_t)g.IMGS * g.TRI * g.WI * pstride<CI, S>() * 2; }
 
 // S: the stride of the halo layout (kDgrad2 reads its half-resolution dy band at layout S = 1)
-template <int CI, int CO, int MODE, int S>
+template <int CI, int CO, int MODE, int S, int ADD = 0>
 int launch_fwd(const void* x, const void* w, void* y, void* sums, int P, int Bn, int H,
-               hipStream_t st, const void* addend = nullptr) {
+               hipStream_t st, const void* addend = nullptr, int addend_c = 0) {
   constexpr int NPX = npx_for(CO);
   Geom g{};
   // (64-wide outputs: half the workgroups, twice the bands each -- their weight prologue is long)
@@ -431,9 +446,10 @@ int launch_fwd(const void* x, const void* w, void* y, void* sums, int P, int Bn,
   const size_t lds = std::max(halo_bytes<CI, S>(g), (size_t)NPX * (CO + 8) * 2);
   if (lds > 64 * 1024) return (int)hipErrorNotSupported;
   g.lds_elems = (int)(lds / 2);
-  hipLaunchKernelGGL((dconv_fwd_kernel<CI, CO, NPX, MODE, S>), dim3(P * g.nb), dim3(256), lds, st,
+  hipLaunchKernelGGL((dconv_fwd_kernel<CI, CO, NPX, MODE, S, ADD>), dim3(P * g.nb), dim3(256), lds,
+                     st,
                      (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)sums,
-                     (const bf16_t*)addend, g);
+                     (const bf16_t*)addend, g, addend_c);
   return (int)hipGetLastError();
 }
 
@@ -476,13 +492,15 @@ extern "C" {
 //   kind 0 forward   y [P*Bn, H/S, H/S, Co] = conv(x [P*Bn, H, H, Ci], w [P, 9 Ci, Co]);
 //                    aux = f32 sums [P][2][Co] (zeroed by the caller; += sum, sum^2 of y) or 0
 //   kind 1 dgrad     dx [P*Bn, H, H, Ci] from dy [P*Bn, H/S, H/S, Co] and w [P, 9 Ci, Co];
-//                    aux = bf16 addend shaped like dx (added in the epilogue) or 0
+//                    aux = bf16 addend (added in the epilogue) or 0: shaped like dx (aux_c = 0)
+//                    or, aux_c > 0, [P*Bn, H/2, H/2, aux_c] added at dx's even pixels to
+//                    channels < Ci (the gradient of an option-A shortcut)
 //   kind 2 wgrad     dw [P, 9 Ci, Co] (bf16) from x and dy; aux = f32 partials
 //                    [nb][P][9 Ci][Co], nb from mopt_dconv_wgrad_splits
 // Returns hipErrorNotSupported (801) for shapes without an instantiation: the caller falls
 // back to the implicit GEMM (mopt_pconv).
 int mopt_dconv(int kind, const void* a, const void* b, void* out, void* aux, int P, int Bn, int H,
-               int Ci, int Co, int stride, void* stream) {
+               int Ci, int Co, int stride, int aux_c, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (kind == 0) {
 #define X(ci, co) \
@@ -496,8 +514,12 @@ int mopt_dconv(int kind, const void* a, const void* b, void* out, void* aux, int
   if (kind == 1) {  // the forward kernel over dy (Co channels) with flipped transposed weights
 #define X(ci, co) \
     if (Co == ci && Ci == co) \
-      return stride == 1 ? launch_fwd<ci, co, kDgrad, 1>(a, b, out, nullptr, P, Bn, H, st, aux) \
-                         : launch_fwd<ci, co, kDgrad2, 1>(a, b, out, nullptr, P, Bn, H, st, aux);
+      return stride == 1 \
+          ? (aux ? launch_fwd<ci, co, kDgrad, 1, 1>(a, b, out, nullptr, P, Bn, H, st, aux) \
+                 : launch_fwd<ci, co, kDgrad, 1, 0>(a, b, out, nullptr, P, Bn, H, st)) \
+          : (aux ? launch_fwd<ci, co, kDgrad2, 1, 2>(a, b, out, nullptr, P, Bn, H, st, aux, \
+                                                     aux_c) \
+                 : launch_fwd<ci, co, kDgrad2, 1, 0>(a, b, out, nullptr, P, Bn, H, st));
     MOPT_DCONV_DGRAD_SHAPES(X)
 #undef X
     return (int)hipErrorNotSupported;

@@ -131,7 +131,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
                                                        const bf16_t* __restrict__ beta,
                                                        const bf16_t* __restrict__ res,
                                                        bf16_t* __restrict__ y, int64_t M, int C,
-                                                       int P, int relu) {
+                                                       int P, int relu, int res_c, int res_ohl) {
   const int cc = C >> 3;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= (int64_t)P * M * cc) return;
@@ -143,7 +143,19 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
   unpack8(*(const uint4*)(gamma + (int64_t)p * C + 8 * ch), g);
   unpack8(*(const uint4*)(beta + (int64_t)p * C + 8 * ch), b);
   float rr[8];
-  if (res) unpack8(*(const uint4*)(res + row * C + 8 * ch), rr);
+  if (res && res_c == 0) {
+    unpack8(*(const uint4*)(res + row * C + 8 * ch), rr);
+  } else if (res) {  // option-A shortcut of the full-resolution block input: x[2i][2j][c < res_c]
+    const int64_t img = row >> (2 * res_ohl);
+    const int pix = (int)(row & ((1 << (2 * res_ohl)) - 1));
+    const int i2 = 2 * (pix >> res_ohl), j2 = 2 * (pix & ((1 << res_ohl) - 1));
+    const int hin = 2 << res_ohl;
+    if (8 * ch < res_c)
+      unpack8(*(const uint4*)(res + ((img * hin + i2) * hin + j2) * res_c + 8 * ch), rr);
+    else
+#pragma unroll
+      for (int e = 0; e < 8; ++e) rr[e] = 0.f;
+  }
   const float* mean = stat + (2 * p) * C + 8 * ch;
   const float* rstd = stat + (2 * p + 1) * C + 8 * ch;
 #pragma unroll
@@ -218,9 +230,13 @@ extern "C" {
 
 // x [P][M][C] -> y; stat [P][2][C] (mean, rstd) out; running [P][2][C] in/out; sums scratch
 // (or, sums_ready, the batch sums of x and x^2 already accumulated by the convolution).
+// res_c > 0: res is the block input at twice the resolution with res_c channels and the
+// residual is its option-A shortcut (stride-2 subsample, zero channels >= res_c); the output
+// side is 1 << res_ohl.
 int mopt_bn_fwd(const void* x, const void* gamma, const void* beta, const void* res, void* y,
                 void* stat, void* running, void* sums, int P, int64_t M, int C, float eps,
-                float momentum, int train, int relu, int sums_ready, void* stream) {
+                float momentum, int train, int relu, int sums_ready, int res_c, int res_ohl,
+                void* stream) {
   if (!bn_shape_ok(C)) return 1;
   hipStream_t st = (hipStream_t)stream;
   if (train && !sums_ready) {  // else the producing convolution's epilogue summed x, x^2
@@ -235,7 +251,8 @@ int mopt_bn_fwd(const void* x, const void* gamma, const void* beta, const void* 
                      train);
   hipLaunchKernelGGL(bn_apply_kernel, grid1((int64_t)P * M * (C / 8)), dim3(256), 0, st,
                      (const bf16_t*)x, (const float*)stat, (const bf16_t*)gamma,
-                     (const bf16_t*)beta, (const bf16_t*)res, (bf16_t*)y, M, C, P, relu);
+                     (const bf16_t*)beta, (const bf16_t*)res, (bf16_t*)y, M, C, P, relu, res_c,
+                     res_ohl);
   return (int)hipGetLastError();
 }
 

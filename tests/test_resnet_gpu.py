@@ -70,9 +70,17 @@ def test_direct_conv_kernels(stride, C, Cout, H):
         dx = torch.empty_like(x)
         assert cops._dconv(1, dy, w, dx, P, B, H, H, C, Cout, stride)
         _close(dx, xr.grad, 1e-2)
-        addend = torch.randn_like(x)          # residual-branch gradient fused in the epilogue
-        assert cops._dconv(1, dy, w, dx, P, B, H, H, C, Cout, stride, addend=addend)
-        _close(dx, xr.grad + addend.float(), 1e-2)
+        if stride == 1:                       # identity shortcut's gradient in the epilogue
+            addend = torch.randn_like(x)
+            assert cops._dconv(1, dy, w, dx, P, B, H, H, C, Cout, stride, addend=addend)
+            _close(dx, xr.grad + addend.float(), 1e-2)
+        else:                                 # option-A shortcut: even pixels, channels < C
+            addend = torch.randn_like(y)
+            assert cops._dconv(1, dy, w, dx, P, B, H, H, C, Cout, stride, addend=addend,
+                               addend_c=Cout)
+            want = xr.grad.clone()
+            want[:, ::2, ::2, :] += addend[..., :C].float()
+            _close(dx, want, 1e-2)
 
 
 def test_conv_bn_act_fused_statistics():
@@ -89,6 +97,21 @@ def test_conv_bn_act_fused_statistics():
     yb = cops.bn_act(cops.conv3x3(x, w, P, 1), g, b, run_b, P, True)
     _close(ya, yb, 1e-2)
     torch.testing.assert_close(run_a, run_b, rtol=1e-4, atol=1e-4)
+
+
+def test_bn_option_a_residual_read_in_place():
+    """BN with the option-A shortcut of the full-resolution block input read in place equals
+    BN with the materialised subsampled / zero-padded residual."""
+    torch.manual_seed(4)
+    P, B, H, Ci, C = 2, 4, 16, 16, 32
+    x = torch.randn(P * B, H // 2, H // 2, C, device=DEV).to(torch.bfloat16)
+    h = torch.randn(P * B, H, H, Ci, device=DEV).to(torch.bfloat16)
+    g = (1 + 0.1 * torch.randn(P, C, device=DEV)).to(torch.bfloat16)
+    b = (0.1 * torch.randn(P, C, device=DEV)).to(torch.bfloat16)
+    run = torch.stack([torch.zeros(P, C), torch.ones(P, C)], 1).to(DEV).contiguous()
+    ya = cops.bn_act(x, g, b, run.clone(), P, True, res=h, res_sub2=True)
+    yb = cops.bn_act(x, g, b, run.clone(), P, True, res=cops.option_a_shortcut(h, C))
+    assert torch.equal(ya, yb)
 
 
 @pytest.mark.parametrize("relu,res", [(True, False), (True, True), (False, False)])
