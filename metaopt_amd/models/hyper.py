@@ -7,8 +7,8 @@ respect to the two hyper-parameters through every inner step (Franceschi et al.,
 Reverse Gradient-Based Hyperparameter Optimization", ICML 2017):
 
 * the inner loss is written so that one forward-over-reverse pass (``torch.func.jvp`` of
-  ``torch.func.grad``) yields the gradient and a Hessian-vector product along each tangent,
-  exactly (no finite differences): every GEMM -- the projections, the attention scores and
+  ``torch.func.grad``, vmapped over the two tangents) yields the gradient and a Hessian-vector
+  product along each tangent, exactly (no finite differences): every GEMM -- the projections, the attention scores and
   values, the LM head, in the forward, the backward and the tangent propagation -- is the
   second-order-differentiable population GEMM of ``ops/pgemm_ad.py`` on the hand-written MFMA
   kernel (bf16 operands, f32 accumulation); norms, RoPE, softmax and the loss are elementwise
@@ -191,8 +191,18 @@ class HypergradLM:
             return per_trial.sum(), per_trial.detach()
 
         grad_fn = torch.func.grad_and_value(loss_fn, has_aux=True)
-        (g, (_, losses)), (he, _) = torch.func.jvp(grad_fn, (self.w,), (self.ze,))
-        (_, _), (hm, _) = torch.func.jvp(grad_fn, (self.w,), (self.zm,))
+
+        def along(tangent):
+            (g, (_, losses)), (h, _) = torch.func.jvp(grad_fn, (self.w,), (tangent,))
+            return g, losses, h
+
+        # both tangents in ONE forward-over-reverse pass: vmapped over the tangent, the primal
+        # forward / backward run once and every tangent op is batched (the population GEMM's
+        # batching rule folds the two tangents into its trial dimension) -- half the passes of
+        # one jvp per hyper-parameter, same numbers
+        g, losses, h = torch.func.vmap(along, out_dims=(None, None, 0))(
+            torch.stack([self.ze, self.zm]))
+        he, hm = h[0], h[1]
         if self.dp_comm is not None:                                            # C3
             packed = torch.stack([g, he, hm])
             buf = packed.to(self.dp_comm._coll_device())

@@ -57,6 +57,19 @@ class _MatmulPG(torch.autograd.Function):
         return ga, gb, None, None
 
     @staticmethod
+    def vmap(info, in_dims, a, b, ta, tb):
+        """Batching rule: the vmapped dimension folds into the population dimension, so a
+        batch of tangents (K11: one per hyper-parameter) is ONE population GEMM."""
+        B = info.batch_size
+
+        def fold(x, d):
+            x = x.unsqueeze(0).expand(B, *x.shape) if d is None else x.movedim(d, 0)
+            return x.reshape(B * x.shape[1], *x.shape[2:])
+
+        out = matmul(fold(a, in_dims[0]), fold(b, in_dims[1]), ta, tb)
+        return out.view(B, -1, *out.shape[1:]), 0
+
+    @staticmethod
     def jvp(ctx, da, db, _ta, _tb):
         a, b = ctx.saved_tensors
         out = None
