@@ -41,7 +41,9 @@ constexpr int LSK = BK + 8;  // row stride of k-contiguous LDS images (144 B)
 //   kDgrad   S[pixel (b, h, w)][tap * Co + co]  = dY[b][(h + 1 - kh)/s][(w + 1 - kw)/s][co]
 //            (zero unless the division is exact: the stride-2 transposed convolution)
 //   kWdgrad  S[ci][tap * Co + co]               = W[tap * Ci + ci][co]
-enum SrcKind { kDense = 0, kIm2col = 1, kDgrad = 2, kWdgrad = 3 };
+//   kDenseF32 dense f32 storage, rounded to bf16 (RNE) as it is staged (the fp32 tensors of the
+//            forward-over-reverse hypergradient step need no separate cast kernels)
+enum SrcKind { kDense = 0, kIm2col = 1, kDgrad = 2, kWdgrad = 3, kDenseF32 = 4 };
 
 struct Src {
   const bf16_t* ptr;  // trial 0
@@ -106,10 +108,20 @@ struct Img {
           gk = k0 + c / RCH;
           gr = row0 + 8 * (c % RCH);
         }
-        const bf16_t* src = gk < k_end ? src_at<KIND>(s, base, KCONTIG ? gr : gk,
-                                                      KCONTIG ? gk : gr)
-                                       : nullptr;
-        if (src != nullptr) v = *(const uint4*)src;
+        if constexpr (KIND == kDenseF32) {
+          const int o = KCONTIG ? gr : gk, in = KCONTIG ? gk : gr;
+          if (gk < k_end && o < s.n_outer && in < s.n_inner) {
+            const float* f = (const float*)base + (int64_t)o * s.ld + in;
+            const float4 x0 = *(const float4*)f, x1 = *(const float4*)(f + 4);
+            v = make_uint4(pack2bf(x0.x, x0.y), pack2bf(x0.z, x0.w), pack2bf(x1.x, x1.y),
+                           pack2bf(x1.z, x1.w));
+          }
+        } else {
+          const bf16_t* src = gk < k_end ? src_at<KIND == kDenseF32 ? kDense : KIND>(
+                                               s, base, KCONTIG ? gr : gk, KCONTIG ? gk : gr)
+                                         : nullptr;
+          if (src != nullptr) v = *(const uint4*)src;
+        }
       }
       r[i] = v;
     }
@@ -139,6 +151,7 @@ struct Img {
 struct GemmArgs {
   Src a, b;
   bf16_t* C;
+  float* C32;      // f32 output instead of C (register-staged kernel only), else nullptr
   float* part;     // split-K partials [splits][P][M][N] (nullptr when splits == 1)
   int64_t sC;
   int P, M, N, K, ldc;
@@ -162,8 +175,11 @@ __global__ __launch_bounds__(256) void pgemm_kernel(const GemmArgs g) {
   const int sp = t % g.splits;
   const int p = t / g.splits;
 
-  const bf16_t* A = g.a.ptr + p * g.a.batch;
-  const bf16_t* B = g.b.ptr + p * g.b.batch;
+  // (f32 operands: the trial stride counts f32 elements)
+  const bf16_t* A = KA == kDenseF32 ? (const bf16_t*)((const float*)g.a.ptr + p * g.a.batch)
+                                    : g.a.ptr + p * g.a.batch;
+  const bf16_t* B = KB == kDenseF32 ? (const bf16_t*)((const float*)g.b.ptr + p * g.b.batch)
+                                    : g.b.ptr + p * g.b.batch;
   const int m0 = tm * BM, n0 = tn * BN;
   const int kb = sp * g.k_per_split;
   const int ke = min(g.K, kb + g.k_per_split);
@@ -217,7 +233,21 @@ __global__ __launch_bounds__(256) void pgemm_kernel(const GemmArgs g) {
   // epilogue: lane holds C[row 4 gq + r][col li] of every fragment.  bf16 output is restaged
   // through LDS (the operand buffers are free after the loop's last barrier) so every lane
   // stores whole 16-byte row segments instead of scattered 2-byte elements.
-  if (g.splits == 1) {
+  if (g.splits == 1 && g.C32 != nullptr) {  // f32 output: fragments stored as they are
+    float* C = g.C32 + p * g.sC;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = n0 + wn * 16 * FN + 16 * j + li;
+        if (n >= g.N) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * 16 * FM + 16 * i + 4 * gq + r;
+          if (m < g.M) C[(int64_t)m * g.ldc + n] = acc[i][j][r];
+        }
+      }
+  } else if (g.splits == 1) {
     constexpr int LSC = BN + 8;
     static_assert(BM * LSC <= 2 * BUF, "C tile must fit in the operand buffers");
     bf16_t* Cs = smem;
@@ -457,7 +487,8 @@ __global__ __launch_bounds__(512) void pgemm_big_kernel(const GemmArgs g) {
 
 // sum of the split-K partials [splits][P][M][N] -> C[p][m][n * ldc] bf16
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part,
-                                                            bf16_t* __restrict__ C, int64_t sC,
+                                                            bf16_t* __restrict__ C,
+                                                            float* __restrict__ C32, int64_t sC,
                                                             int ldc, int P, int M, int N,
                                                             int splits) {
   const int64_t total = (int64_t)P * M * N;
@@ -466,7 +497,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   float s = 0.f;
   for (int k = 0; k < splits; ++k) s += part[k * total + i];
   const int64_t n = i % N, m = (i / N) % M, p = i / ((int64_t)M * N);
-  C[p * sC + m * ldc + n] = f2bf(s);
+  if (C32 != nullptr) C32[p * sC + m * ldc + n] = s;
+  else C[p * sC + m * ldc + n] = f2bf(s);
 }
 
 template <int KA, int KB, bool TA, bool TB, int WM, int FM, int FN>
@@ -533,7 +565,7 @@ int dispatch_conv_tile(const GemmArgs& g, int cfg, hipStream_t st) {
 int finish_splitk(const GemmArgs& g, hipStream_t st) {
   const int64_t total = (int64_t)g.P * g.M * g.N;
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                     st, (const float*)g.part, g.C, g.sC, g.ldc, g.P, g.M, g.N, g.splits);
+                     st, (const float*)g.part, g.C, g.C32, g.sC, g.ldc, g.P, g.M, g.N, g.splits);
   return (int)hipGetLastError();
 }
 
@@ -592,6 +624,35 @@ int mopt_pgemm(const void* A, const void* B, void* C, void* part, int P, int M, 
   else if (!ta && tb) err = dispatch_tile<kDense, kDense, false, true>(g, cfg, st);
   else if (ta && !tb) err = dispatch_tile<kDense, kDense, true, false>(g, cfg, st);
   else err = dispatch_tile<kDense, kDense, true, true>(g, cfg, st);
+  if (err || splits == 1) return err;
+  return finish_splitk(g, st);
+}
+
+// mopt_pgemm with f32 operands and f32 output (a32/b32/c32 all 1; the register-staged tiles
+// only, cfg 0..4): operands are rounded to bf16 as they are staged, accumulation f32.
+int mopt_pgemm_f32(const void* A, const void* B, void* C, void* part, int P, int M, int N, int K,
+                   int lda, int ldb, int ldc, int64_t sA, int64_t sB, int64_t sC, int ta, int tb,
+                   int cfg, int splits, int k_per_split, void* stream) {
+  if (P <= 0 || M <= 0 || N <= 0 || K <= 0) return 0;
+  if (cfg < 0 || cfg > 4 || splits < 1 ||
+      (splits > 1 && (part == nullptr || k_per_split % BK))) {
+    return (int)hipErrorInvalidValue;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  GemmArgs g{};
+  g.a = ta ? dense(A, sA, lda, K, M) : dense(A, sA, lda, M, K);
+  g.b = tb ? dense(B, sB, ldb, N, K) : dense(B, sB, ldb, K, N);
+  g.C32 = (float*)C;
+  g.part = (float*)part;
+  g.sC = sC;
+  g.P = P; g.M = M; g.N = N; g.K = K; g.ldc = ldc;
+  g.splits = splits;
+  g.k_per_split = splits > 1 ? k_per_split : K;
+  int err;
+  if (!ta && !tb) err = dispatch_tile<kDenseF32, kDenseF32, false, false>(g, cfg, st);
+  else if (!ta && tb) err = dispatch_tile<kDenseF32, kDenseF32, false, true>(g, cfg, st);
+  else if (ta && !tb) err = dispatch_tile<kDenseF32, kDenseF32, true, false>(g, cfg, st);
+  else err = dispatch_tile<kDenseF32, kDenseF32, true, true>(g, cfg, st);
   if (err || splits == 1) return err;
   return finish_splitk(g, st);
 }

@@ -32,6 +32,8 @@ c_void_p, c_int, c_int64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
 _lib.register_signatures({
     "mopt_pgemm": ([c_void_p] * 4 + [c_int] * 7 + [c_int64] * 3 + [c_int] * 5 + [c_void_p],
                    c_int),
+    "mopt_pgemm_f32": ([c_void_p] * 4 + [c_int] * 7 + [c_int64] * 3 + [c_int] * 5 + [c_void_p],
+                       c_int),
 })
 
 # tile configurations of csrc/pgemm.hip: cfg -> (BM, BN).  0-4: 4-wave register-staged kernel
@@ -109,10 +111,10 @@ def plan(P: int, M: int, N: int, K: int, cfg: Optional[int] = None,
     return cfg, math.ceil(K / kps), kps
 
 
-def _check_operand(t: torch.Tensor, name: str) -> None:
-    if t.dtype != torch.bfloat16 or t.dim() != 3 or t.stride(2) != 1:
-        raise ValueError(f"pgemm: {name} must be a [P, rows, cols] bf16 tensor with unit column "
-                         f"stride, got {t.dtype} {tuple(t.shape)} strides {t.stride()}")
+def _check_operand(t: torch.Tensor, name: str, dtype=torch.bfloat16) -> None:
+    if t.dtype != dtype or t.dim() != 3 or t.stride(2) != 1:
+        raise ValueError(f"pgemm: {name} must be a [P, rows, cols] {dtype} tensor with unit "
+                         f"column stride, got {t.dtype} {tuple(t.shape)} strides {t.stride()}")
     if t.shape[2] % 8 or t.stride(1) % 8 or (t.shape[0] > 1 and t.stride(0) % 8) or \
             t.data_ptr() % 16:
         raise ValueError(f"pgemm: {name} rows must be 16-byte aligned multiples of 8 elements "
@@ -122,7 +124,9 @@ def _check_operand(t: torch.Tensor, name: str) -> None:
 def pgemm(a: torch.Tensor, b: torch.Tensor, ta: bool = False, tb: bool = False,
           out: Optional[torch.Tensor] = None, cfg: Optional[int] = None,
           splits: Optional[int] = None) -> torch.Tensor:
-    """``out[p] = op(a[p]) @ op(b[p])`` in bf16 with f32 accumulation on the MFMA kernel."""
+    """``out[p] = op(a[p]) @ op(b[p])`` in bf16 with f32 accumulation on the MFMA kernel.  f32
+    operands give an f32 product: they are rounded to bf16 while the kernel stages them (no cast
+    kernels) and the f32 accumulators are stored as they are."""
     if a.device.type != "cuda":
         aa = a.transpose(1, 2) if ta else a
         bb = b.transpose(1, 2) if tb else b
@@ -131,8 +135,12 @@ def pgemm(a: torch.Tensor, b: torch.Tensor, ta: bool = False, tb: bool = False,
             out.copy_(r)
             return out
         return r
-    _check_operand(a, "a")
-    _check_operand(b, "b")
+    f32 = a.dtype == torch.float32 or b.dtype == torch.float32
+    dt = torch.float32 if f32 else torch.bfloat16
+    if f32:
+        a, b = a.float(), b.float()
+    _check_operand(a, "a", dt)
+    _check_operand(b, "b", dt)
     P = a.shape[0]
     K, M = (a.shape[1], a.shape[2]) if ta else (a.shape[2], a.shape[1])
     N, Kb = (b.shape[1], b.shape[2]) if tb else (b.shape[2], b.shape[1])
@@ -142,14 +150,17 @@ def pgemm(a: torch.Tensor, b: torch.Tensor, ta: bool = False, tb: bool = False,
     if N % 8:
         raise ValueError(f"pgemm: N = {N} must be a multiple of 8 (16-byte output rows)")
     if out is None:
-        out = torch.empty(P, M, N, dtype=torch.bfloat16, device=a.device)
-    elif tuple(out.shape) != (P, M, N) or out.stride(2) != 1 or out.dtype != torch.bfloat16:
-        raise ValueError(f"pgemm: out must be [P, M, N] = {(P, M, N)} bf16 row-major")
-    _check_operand(out, "out")
+        out = torch.empty(P, M, N, dtype=dt, device=a.device)
+    elif tuple(out.shape) != (P, M, N) or out.stride(2) != 1 or out.dtype != dt:
+        raise ValueError(f"pgemm: out must be [P, M, N] = {(P, M, N)} {dt} row-major")
+    _check_operand(out, "out", dt)
+    if f32 and (cfg is None or cfg in BIG_TILES):
+        cfg = pick_tile(M, N)          # f32 operands: the register-staged tiles only
     cfg, splits, kps = plan(P, M, N, K, cfg, splits)
     part = (torch.empty(splits, P, M, N, dtype=torch.float32, device=a.device)
             if splits > 1 else None)
-    _lib.check(_lib.get_lib().mopt_pgemm(
+    fn = _lib.get_lib().mopt_pgemm_f32 if f32 else _lib.get_lib().mopt_pgemm
+    _lib.check(fn(
         a.data_ptr(), b.data_ptr(), out.data_ptr(), 0 if part is None else part.data_ptr(),
         P, M, N, K, a.stride(1), b.stride(1), out.stride(1), a.stride(0), b.stride(0),
         out.stride(0), int(ta), int(tb), cfg, splits, kps, _lib.stream_ptr(a.device)),

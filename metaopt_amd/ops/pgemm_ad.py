@@ -8,7 +8,8 @@ unrolled hypergradient (K11, ``models/hyper.py``) -- runs every GEMM of the forw
 backward AND the tangent propagation on the hand-written MFMA kernel (``csrc/pgemm.hip``),
 operands read in their stored layout (no transposed copies).
 
-On the GPU the operands are rounded to bf16 and accumulated in f32 (the kernel's contract); on
+On the GPU the operands are rounded to bf16 and accumulated in f32 (the kernel's contract; f32
+operands are rounded as the kernel stages them and the f32 result is returned unrounded); on
 CPU the same Function computes in fp32 with ``torch.bmm`` (the exact reference of the tests).
 
 Derivatives of ``C = A B`` (``A = op(a)``, ``B = op(b)``):
@@ -23,6 +24,10 @@ import torch
 def _mm(a: torch.Tensor, b: torch.Tensor, ta: bool, tb: bool) -> torch.Tensor:
     if a.device.type == "cuda":
         from .gemm import pgemm
+        if a.dtype == torch.float32 and b.dtype == torch.float32:
+            # f32 operands are rounded to bf16 inside the kernel and the f32 accumulators come
+            # back as they are: no cast kernels around the GEMM
+            return pgemm(a.contiguous(), b.contiguous(), ta=ta, tb=tb)
         a16 = a.to(torch.bfloat16).contiguous()
         b16 = b.to(torch.bfloat16).contiguous()
         return pgemm(a16, b16, ta=ta, tb=tb).to(a.dtype)

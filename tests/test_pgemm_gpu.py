@@ -116,3 +116,18 @@ def test_nn_forward_lm_shapes(K, N, library, monkeypatch):
     x = (torch.randn(P, M, K, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
     w = (torch.randn(P, K, N, device=DEV, generator=g) * 0.02).to(torch.bfloat16)
     _check(nn_forward(x, w), x, w)
+
+
+@pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("P,M,N,K,splits", [(3, 200, 136, 72, 1), (2, 64, 40, 1000, None)])
+def test_f32_operands_and_output(ta, tb, P, M, N, K, splits):
+    """f32 operands are rounded to bf16 while staged (bitwise the same products as casting
+    first) and the f32 accumulators come back unrounded, also through split-K."""
+    A, B, a, b = _operands(P, M, N, K, ta, tb, seed=7)
+    a32, b32 = a.float(), b.float()
+    got = pgemm(a32, b32, ta=ta, tb=tb, splits=splits)
+    assert got.dtype == torch.float32
+    _check(got, A, B)
+    ref16 = pgemm(a, b, ta=ta, tb=tb, cfg=pgemm.__globals__["pick_tile"](M, N), splits=splits)
+    # same inputs after rounding, same tile order: the bf16 path is the f32 result rounded
+    assert torch.equal(got.to(torch.bfloat16), ref16)
