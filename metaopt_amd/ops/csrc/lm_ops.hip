@@ -402,6 +402,46 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const int32_t* __restric
   for (int e = 0; e < 8; ++e) atomicAdd(dst + e, v[e]);
 }
 
+// Embedding gradient from the (trial, token) keys sorted stably: one wave per sorted position;
+// the wave at the start of each run of equal keys sums the run's dout rows in f32 (in token
+// order: deterministic) and writes the bf16 row of the table gradient -- no atomics, no f32
+// table.  The caller zeroes the table gradient first (rows no token touched stay zero).
+__global__ __launch_bounds__(256) void embed_bwd_sorted_kernel(const int64_t* __restrict__ keys,
+                                                               const int64_t* __restrict__ order,
+                                                               const bf16_t* __restrict__ dout,
+                                                               bf16_t* __restrict__ dtable,
+                                                               int64_t rows, int d) {
+  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (w >= rows) return;
+  const int64_t key = keys[w];
+  if (w > 0 && keys[w - 1] == key) return;  // not the first of its run
+  const int nc = d >> 3;
+  float acc[kMaxChunks][8];
+#pragma unroll
+  for (int k = 0; k < kMaxChunks; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[k][e] = 0.f;
+  for (int64_t j = w; j < rows && keys[j] == key; ++j) {
+    const bf16_t* src = dout + order[j] * (int64_t)d;
+#pragma unroll
+    for (int k = 0; k < kMaxChunks; ++k) {
+      const int c = lane + 64 * k;
+      if (c < nc) {
+        float v[8];
+        unpack8(*(const uint4*)(src + 8 * c), v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[k][e] += v[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kMaxChunks; ++k) {
+    const int c = lane + 64 * k;
+    if (c < nc) *(uint4*)(dtable + key * (int64_t)d + 8 * c) = pack8(acc[k]);
+  }
+}
+
 // f32 -> bf16 (n multiple of 8).
 __global__ __launch_bounds__(256) void cast_bf16_kernel(const float* __restrict__ src,
                                                         bf16_t* __restrict__ dst, int64_t n) {
@@ -674,6 +714,17 @@ int mopt_embed_bwd(const void* tok, const void* dout, void* dtable32, int64_t ro
   hipLaunchKernelGGL(embed_bwd_kernel, grid1(rows * (d / 8)), dim3(256), 0, (hipStream_t)stream,
                      (const int32_t*)tok, (const bf16_t*)dout, (float*)dtable32, rows, d, V,
                      rows_per_trial);
+  return (int)hipGetLastError();
+}
+
+// keys [rows] = trial * V + token sorted ascending (stably), order [rows] the dout row of each;
+// dtable bf16 [P][V][d] zeroed by the caller.
+int mopt_embed_bwd_sorted(const void* keys, const void* order, const void* dout, void* dtable,
+                          int64_t rows, int d, void* stream) {
+  if (d % 8 || d > 64 * 8 * kMaxChunks) return 1;
+  hipLaunchKernelGGL(embed_bwd_sorted_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0,
+                     (hipStream_t)stream, (const int64_t*)keys, (const int64_t*)order,
+                     (const bf16_t*)dout, (bf16_t*)dtable, rows, d);
   return (int)hipGetLastError();
 }
 

@@ -40,6 +40,7 @@ _lib.register_signatures({
     "mopt_embed_bwd": ([c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_void_p],
                        c_int),
     "mopt_cast_bf16": ([c_void_p, c_void_p, c_int64, c_void_p], c_int),
+    "mopt_embed_bwd_sorted": ([c_void_p] * 4 + [c_int64, c_int, c_void_p], c_int),
     "mopt_adamw_multi": ([c_void_p, c_void_p, c_int] + [c_void_p] * 7 + [c_int, c_int, c_int,
                                                                          c_void_p],
                          c_int),
@@ -391,12 +392,21 @@ class _Embedding(torch.autograd.Function):
     def backward(ctx, dout):
         (tok,) = ctx.saved_tensors
         P, V, d, rpt, dtype = ctx.dims
+        dout = dout.contiguous()
+        if ctx.gw is not None:
+            # sort the (trial, token) keys once (stable: deterministic sums), zero the table
+            # gradient and let one wave per run of equal keys write its row -- no f32 table,
+            # no atomics, no cast pass
+            R = tok.numel()
+            trial = torch.arange(R, device=tok.device, dtype=torch.int64) // rpt
+            keys, order = torch.sort(trial * V + tok.long(), stable=True)
+            ctx.gw.zero_()
+            _call("mopt_embed_bwd_sorted", _p(keys), _p(order), _p(dout), _p(ctx.gw), R, d,
+                  _stream(dout))
+            return None, None, None
         d32 = torch.zeros(P, V, d, dtype=torch.float32, device=dout.device)
         _call("mopt_embed_bwd", _p(tok), _p(dout.contiguous()), _p(d32), tok.numel(), d, V, rpt,
               _stream(dout))
-        if ctx.gw is not None:      # cast straight into the flat gradient buffer
-            _call("mopt_cast_bf16", _p(d32), _p(ctx.gw), d32.numel(), _stream(dout))
-            return None, None, None
         d16 = torch.empty(P, V, d, dtype=dtype, device=dout.device)
         _call("mopt_cast_bf16", _p(d32), _p(d16), d32.numel(), _stream(dout))
         return None, d16, None
