@@ -442,6 +442,65 @@ __global__ __launch_bounds__(256) void embed_bwd_sorted_kernel(const int64_t* __
   }
 }
 
+// RMSNorm weight gradient straight into a bf16 gradient view, two passes without atomics.
+// Pass 1: thread (column group cg of 8, slice s, trial p) sums dy * x * rstd over its slice of
+// the trial's rows with 16-byte loads and writes 8 floats to part[(p * G + cg) * S + s]
+// (G = d / 8: the S partials of one column group are contiguous).  grid (ceil(G/bx), S, P),
+// bx = G rounded up to whole waves (<= 256).
+// Pass 2: one wave per (p, cg) reads its S partials coalesced (32 B per lane), reduces them
+// across the wave and writes the 8 bf16 gradients.
+__global__ __launch_bounds__(256) void rmsnorm_dw_partial_kernel(const bf16_t* __restrict__ x,
+                                                                 const bf16_t* __restrict__ dy,
+                                                                 const float* __restrict__ rstd,
+                                                                 float* __restrict__ part, int d,
+                                                                 int rows_per_trial) {
+  const int cg = blockIdx.x * blockDim.x + threadIdx.x, G = d / 8;
+  if (cg >= G) return;
+  const int p = blockIdx.z, s = blockIdx.y, S = gridDim.y;
+  const int per = (rows_per_trial + S - 1) / S;
+  const int r0 = p * rows_per_trial + s * per;
+  const int r1 = min(r0 + per, (p + 1) * rows_per_trial);
+  float acc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+#pragma unroll 4
+  for (int r = r0; r < r1; ++r) {
+    float xv[8], dv[8];
+    unpack8(*(const uint4*)(x + (size_t)r * d + 8 * cg), xv);
+    unpack8(*(const uint4*)(dy + (size_t)r * d + 8 * cg), dv);
+    const float rs = rstd[r];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] += dv[e] * xv[e] * rs;
+  }
+  float* o = part + (((size_t)p * G + cg) * S + s) * 8;
+  *(f32x4*)o = f32x4{acc[0], acc[1], acc[2], acc[3]};
+  *(f32x4*)(o + 4) = f32x4{acc[4], acc[5], acc[6], acc[7]};
+}
+
+__global__ __launch_bounds__(256) void rmsnorm_dw_reduce_kernel(const float* __restrict__ part,
+                                                                bf16_t* __restrict__ dw16,
+                                                                int groups, int S) {
+  const int w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (w >= groups) return;
+  float acc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+  const float* q = part + (size_t)w * S * 8;
+  for (int s = lane; s < S; s += 64) {
+    const f32x4 a = *(const f32x4*)(q + 8 * s), b = *(const f32x4*)(q + 8 * s + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      acc[e] += a[e];
+      acc[4 + e] += b[e];
+    }
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] += __shfl_xor(acc[e], m, 64);
+  if (lane == 0) *(uint4*)(dw16 + (size_t)w * 8) = pack8(acc);
+}
+
 // f32 -> bf16 (n multiple of 8).
 __global__ __launch_bounds__(256) void cast_bf16_kernel(const float* __restrict__ src,
                                                         bf16_t* __restrict__ dst, int64_t n) {
@@ -650,6 +709,7 @@ int mopt_rmsnorm_bwd_res(const void* x, const void* w, const void* dy, const voi
                        (const bf16_t*)x, (const bf16_t*)w, (const bf16_t*)dy,
                        (const bf16_t*)nullptr, (const float*)rstd, (bf16_t*)dx, rows, d,
                        rows_per_trial);
+  if (dw32 == nullptr) return (int)hipGetLastError();  // weight gradient via mopt_rmsnorm_dw16
   const int P = rows / rows_per_trial;
   const int splits = max(1, min(64, rows_per_trial / 64));
   hipLaunchKernelGGL(rmsnorm_bwd_dw_kernel, dim3((d + 255) / 256, splits, P), dim3(256), 0, st,
@@ -725,6 +785,24 @@ int mopt_embed_bwd_sorted(const void* keys, const void* order, const void* dout,
   hipLaunchKernelGGL(embed_bwd_sorted_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0,
                      (hipStream_t)stream, (const int64_t*)keys, (const int64_t*)order,
                      (const bf16_t*)dout, (bf16_t*)dtable, rows, d);
+  return (int)hipGetLastError();
+}
+
+// dw16 (bf16 [P][d], a gradient view) = the RMSNorm weight gradient; part: f32 scratch of
+// mopt_rmsnorm_dw_splits(rows_per_trial) * P * d elements (fully overwritten, no zeroing).
+int mopt_rmsnorm_dw_splits(int rows_per_trial) { return max(1, min(256, rows_per_trial / 16)); }
+
+int mopt_rmsnorm_dw16(const void* x, const void* dy, const void* rstd, void* part, void* dw16,
+                      int rows, int d, int rows_per_trial, void* stream) {
+  if (d % 8 || rows % rows_per_trial) return 1;
+  hipStream_t st = (hipStream_t)stream;
+  const int P = rows / rows_per_trial, S = mopt_rmsnorm_dw_splits(rows_per_trial), G = d / 8;
+  const int bx = min(256, (G + 63) / 64 * 64);
+  hipLaunchKernelGGL(rmsnorm_dw_partial_kernel, dim3((G + bx - 1) / bx, S, P), dim3(bx), 0, st,
+                     (const bf16_t*)x, (const bf16_t*)dy, (const float*)rstd, (float*)part, d,
+                     rows_per_trial);
+  hipLaunchKernelGGL(rmsnorm_dw_reduce_kernel, dim3((P * G + 3) / 4), dim3(256), 0, st,
+                     (const float*)part, (bf16_t*)dw16, P * G, S);
   return (int)hipGetLastError();
 }
 

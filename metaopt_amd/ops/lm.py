@@ -29,6 +29,8 @@ _lib.register_signatures({
     "mopt_rmsnorm_bwd": ([c_void_p] * 6 + [c_int, c_int, c_int, c_void_p], c_int),
     "mopt_add_rmsnorm_fwd": ([c_void_p] * 6 + [c_int, c_int, c_int, c_float, c_void_p], c_int),
     "mopt_rmsnorm_bwd_res": ([c_void_p] * 7 + [c_int, c_int, c_int, c_void_p], c_int),
+    "mopt_rmsnorm_dw_splits": ([c_int], c_int),
+    "mopt_rmsnorm_dw16": ([c_void_p] * 5 + [c_int, c_int, c_int, c_void_p], c_int),
     "mopt_rope_fwd": ([c_void_p] * 6 + [c_int, c_int, c_int, c_void_p], c_int),
     "mopt_rope_bwd": ([c_void_p] * 6 + [c_int, c_int, c_int, c_void_p], c_int),
     "mopt_swiglu_fwd": ([c_void_p, c_void_p, c_int64, c_int, c_void_p], c_int),
@@ -154,6 +156,18 @@ def _dw_out(dw32, gw, dtype, stream_of):
     return dw32.to(dtype)
 
 
+def _norm_dw(x, dy, rstd, gw, rows_per_trial):
+    """RMSNorm weight gradient written into the flat bf16 gradient view ``gw``: per-slice f32
+    partials, then one reduce that writes bf16 (no zero fill, no atomics, no cast kernel).
+    ``x`` is the norm's input.  Returns None (autograd has nothing to accumulate)."""
+    R, d = x.shape
+    S = _lib.get_lib().mopt_rmsnorm_dw_splits(rows_per_trial)
+    part = torch.empty(S * (R // rows_per_trial) * d, dtype=torch.float32, device=x.device)
+    _call("mopt_rmsnorm_dw16", _p(x), _p(dy), _p(rstd), _p(part), _p(gw), R, d,
+          rows_per_trial, _stream(x))
+    return None
+
+
 class _RMSNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, rows_per_trial, eps):
@@ -173,6 +187,10 @@ class _RMSNorm(torch.autograd.Function):
         dy = dy.contiguous()
         R, d = x.shape
         dx = torch.empty_like(x)
+        if ctx.gw is not None:
+            _call("mopt_rmsnorm_bwd", _p(x), _p(w), _p(dy), _p(rstd), _p(dx), None, R, d,
+                  ctx.rpt, _stream(x))
+            return dx, _norm_dw(x, dy, rstd, ctx.gw, ctx.rpt), None, None
         dw32 = torch.zeros(w.shape, dtype=torch.float32, device=x.device)
         _call("mopt_rmsnorm_bwd", _p(x), _p(w), _p(dy), _p(rstd), _p(dx), _p(dw32), R, d,
               ctx.rpt, _stream(x))
@@ -206,16 +224,22 @@ class _AddRMSNorm(torch.autograd.Function):
     def backward(ctx, dxs, dy):
         xs, w, rstd = ctx.saved_tensors
         R, d = xs.shape
-        dw32 = torch.zeros(w.shape, dtype=torch.float32, device=xs.device)
         if dy is None:
-            return dxs, dxs, _dw_out(dw32, ctx.gw, w.dtype, xs), None, None
+            if ctx.gw is not None:
+                ctx.gw.zero_()
+                return dxs, dxs, None, None, None
+            return dxs, dxs, torch.zeros_like(w), None, None
         dy = dy.contiguous()
         dres = dxs.contiguous() if dxs is not None else None
         dx = torch.empty_like(xs)
+        dw32 = None if ctx.gw is not None else \
+            torch.zeros(w.shape, dtype=torch.float32, device=xs.device)
         _call("mopt_rmsnorm_bwd_res", _p(xs), _p(w), _p(dy),
-              _p(dres) if dres is not None else None, _p(rstd), _p(dx), _p(dw32), R, d,
-              ctx.rpt, _stream(xs))
-        return dx, dx, _dw_out(dw32, ctx.gw, w.dtype, xs), None, None
+              _p(dres) if dres is not None else None, _p(rstd), _p(dx),
+              _p(dw32) if dw32 is not None else None, R, d, ctx.rpt, _stream(xs))
+        if ctx.gw is not None:
+            return dx, dx, _norm_dw(xs, dy, rstd, ctx.gw, ctx.rpt), None, None
+        return dx, dx, dw32.to(w.dtype), None, None
 
 
 def add_rmsnorm(x, delta, w, rows_per_trial, eps=1e-5):

@@ -77,6 +77,30 @@ def test_add_rmsnorm_fwd_bwd(use_xs):
     _close(w.grad, wr.grad, 2e-2)
 
 
+@pytest.mark.parametrize("fused", [False, True])
+@pytest.mark.parametrize("P,rpt,d", [(3, 1000, 768), (2, 48, 200)])
+def test_rmsnorm_weight_grad_into_flat_view(fused, P, rpt, d):
+    """Weight .grad preset to a bf16 view (the flat gradient buffer): the two-pass kernel
+    (per-slice partials + reduce, no atomics) overwrites stale values with the gradient; row
+    counts that do not divide into the slices and d not a multiple of the wave width."""
+    torch.manual_seed(5)
+    x = torch.randn(P * rpt, d, device=DEV).to(torch.bfloat16)
+    dl = torch.randn(P * rpt, d, device=DEV).to(torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(P, d, device=DEV)).to(torch.bfloat16).requires_grad_(True)
+    w.grad = torch.full_like(w, 5.0)
+    dy = torch.randn(P * rpt, d, device=DEV).to(torch.bfloat16)
+    wr = w.detach().float().requires_grad_(True)
+    if fused:
+        _, y = ops.add_rmsnorm(x, dl, w, rpt)
+        yr = ops.rmsnorm_ref(x.float() + dl.float(), wr, rpt)
+    else:
+        y = ops.rmsnorm(x, w, rpt)
+        yr = ops.rmsnorm_ref(x.float(), wr, rpt)
+    y.backward(dy)
+    yr.backward(dy.float())
+    _close(w.grad, wr.grad, 2e-2)
+
+
 def test_rope_split_roundtrip():
     torch.manual_seed(2)
     Bp, T, H = 2, 128, 3
