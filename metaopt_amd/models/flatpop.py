@@ -206,7 +206,9 @@ class FlatPopulation:
         active = np.array([m is not None for m in self.members])
         self.hp["t"][active] += 1
         self.opt_hp["t"] = self.hp["t"]
-        if self.use_graph and self.device.type == "cuda":
+        from ..ops import _lib
+        # under MOPT_SYNC_CHECK / MOPT_KERNEL_CHECKED every launch is checked eagerly
+        if self.use_graph and self.device.type == "cuda" and not _lib.SYNC_CHECK:
             self._graph_step(x, y)
             return
         self._body(x, y, None)

@@ -70,6 +70,8 @@ def get_lib(build_if_missing: bool = True):
         if _LIB is not None:
             return _LIB
         override = os.environ.get("MOPT_KERNEL_LIB")   # A/B experiments with variant builds
+        if CHECKED and not override:
+            return _load_checked()
         path = _build.lib_path() if not override else __import__("pathlib").Path(override)
         if not override and build_if_missing and (os.environ.get("MOPT_REBUILD") or
                                                   not path.exists()):
@@ -104,11 +106,56 @@ def get_lib(build_if_missing: bool = True):
         return lib
 
 
+def _load_checked():
+    """The bounds-checked variant (MOPT_KERNEL_CHECKED=1), built in-tree when missing/stale."""
+    global _LIB
+    path = _build.variant_path(_build.CHECKED)
+    digest = _build.source_digest(_build.CHECKED_FLAGS)
+    if not path.exists() or _build.variant_digest(_build.CHECKED) != digest:
+        try:
+            _build.build_variant(_build.CHECKED, _build.CHECKED_FLAGS, force=False)
+        except Exception as exc:  # pragma: no cover - hosts without hipcc
+            raise KernelLibraryError(f"cannot build the checked library {path}: {exc}") from exc
+    try:
+        lib = ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL)
+    except OSError as exc:
+        raise KernelLibraryError(f"failed to load {path}: {exc}") from exc
+    _bind(lib, _SIGNATURES)
+    _bind(lib, _OPTIONAL_SIGNATURES)
+    if lib.mopt_abi_version() != ABI_VERSION or lib.mopt_checked_build() != 1:
+        raise KernelLibraryError(f"{path} is not the checked build of ABI {ABI_VERSION}")
+    _LIB = lib
+    return lib
+
+
+# Bounds-checked debug build: MOPT_KERNEL_CHECKED=1 loads lib/variants/checked/ (compiled with
+# -DMOPT_BOUNDS_CHECK: the kernels verify token ids, labels and gather indices on the device)
+# and check() synchronises after every launch, reads the per-module violation counters and
+# raises naming the launch.  Implies the synchronous launch checking below.
+CHECKED = os.environ.get("MOPT_KERNEL_CHECKED", "0") not in ("", "0")
+_CHECKED_MODULES = ("lm_ops", "pop_mlp")
+
+
+class BoundsViolation(RuntimeError):
+    pass
+
+
+def violations() -> int:
+    """Device-side index violations since the last call (0 outside the checked build)."""
+    lib = get_lib()
+    total = 0
+    for mod in _CHECKED_MODULES:
+        fn = getattr(lib, "mopt_violations_" + mod)
+        fn.restype = c_uint
+        total += fn()
+    return total
+
+
 # Debug mode (SURVEY.md §5 "race detection / sanitizers": the HIP-side analogue of
 # HIP_LAUNCH_BLOCKING): MOPT_SYNC_CHECK=1 synchronises the device after every kernel launch
 # that is not being captured into a graph, so an asynchronous fault (out-of-bounds access,
 # illegal instruction) is reported at the launch that caused it, naming that kernel.
-SYNC_CHECK = os.environ.get("MOPT_SYNC_CHECK", "0") not in ("", "0")
+SYNC_CHECK = CHECKED or os.environ.get("MOPT_SYNC_CHECK", "0") not in ("", "0")
 
 
 def check(err: int, what: str) -> None:
@@ -120,6 +167,12 @@ def check(err: int, what: str) -> None:
         except RuntimeError as exc:
             raise RuntimeError(f"[MOPT_SYNC_CHECK] device fault after launching {what}: "
                                f"{exc}") from exc
+        if CHECKED:
+            n = violations()
+            if n:
+                raise BoundsViolation(f"[MOPT_KERNEL_CHECKED] {what}: {n} out-of-range "
+                                      "device index access(es) skipped (see the "
+                                      "'[mopt bounds]' line on stdout)")
 
 
 def stream_ptr(device=None) -> int:

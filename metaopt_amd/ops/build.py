@@ -133,9 +133,30 @@ def build(force: bool = False, verbose: bool = False, extra_flags=None) -> Path:
     return lib
 
 
-def build_variant(name: str, extra_flags, verbose: bool = False) -> Path:
-    """Build the library with ``extra_flags`` into ``lib/variants/<name>/`` (A/B experiments:
-    load it with ``MOPT_KERNEL_LIB``; the default library is untouched)."""
+# The bounds-checked debug build (SURVEY.md §5 "race detection / sanitizers"): every kernel
+# verifies its data-dependent indices on the device (csrc/common.h, MOPT_IN_RANGE) and the host
+# raises on a violation after each launch.  Loaded instead of the default library with
+# MOPT_KERNEL_CHECKED=1 (metaopt_amd/ops/_lib.py).
+CHECKED = "checked"
+CHECKED_FLAGS = ["-DMOPT_BOUNDS_CHECK"]
+
+
+def variant_path(name: str) -> Path:
+    return OUT_DIR / "variants" / name / LIB_NAME
+
+
+def variant_digest(name: str) -> str:
+    p = variant_path(name).with_suffix(".so.sha256")
+    return p.read_text().strip() if p.exists() else ""
+
+
+def build_variant(name: str, extra_flags, verbose: bool = False, force: bool = True) -> Path:
+    """Build the library with ``extra_flags`` into ``lib/variants/<name>/`` (the checked debug
+    build; A/B experiments: load it with ``MOPT_KERNEL_LIB``; the default library is
+    untouched).  With ``force=False`` an up-to-date variant (same source digest) is kept."""
+    digest = source_digest(extra_flags)
+    if not force and variant_path(name).exists() and variant_digest(name) == digest:
+        return variant_path(name)
     hipcc = hipcc_path()
     out = OUT_DIR / "variants" / name
     (out / "obj").mkdir(parents=True, exist_ok=True)
@@ -149,6 +170,7 @@ def build_variant(name: str, extra_flags, verbose: bool = False) -> Path:
                            "-o", str(lib)], capture_output=True, text=True)
     if proc.returncode != 0:
         raise RuntimeError(f"link failed:\n{proc.stderr}")
+    lib.with_suffix(".so.sha256").write_text(digest + "\n")
     if verbose:
         print(f"[mopt build] variant {name}: {lib}")
     return lib
@@ -158,6 +180,8 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--variant", default=None, help="name of an A/B variant build")
+    ap.add_argument("--checked", action="store_true",
+                    help="also build the bounds-checked debug variant")
     ap.add_argument("-D", dest="defines", action="append", default=[],
                     help="preprocessor define of the variant (repeatable)")
     args = ap.parse_args(argv)
@@ -166,6 +190,8 @@ def main(argv=None) -> int:
         return 0
     path = build(force=args.force, verbose=True)
     print(path)
+    if args.checked:
+        print(build_variant(CHECKED, CHECKED_FLAGS, verbose=True, force=args.force))
     return 0
 
 

@@ -131,4 +131,46 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// -------------------------------------------------------------- bounds-checked debug build
+// Compiled with -DMOPT_BOUNDS_CHECK (the "checked" library variant, lib/variants/checked/,
+// loaded with MOPT_KERNEL_CHECKED=1), the kernels verify on the device the data-dependent
+// indices that no host-side check can see -- token ids, class labels, sorted gather indices --
+// before using them (the shapes and work tables are checked on the host before every launch).
+// A violation increments this code object's counter, the first one prints the check, value
+// and bound, and the offending access is skipped: a bad index is reported, never turned into
+// a memory fault.  The host reads and clears the counters after each launch
+// (metaopt_amd/ops/_lib.py) and raises naming the launch.  In the default build MOPT_IN_RANGE
+// is the constant `true` and costs nothing.
+#ifdef MOPT_BOUNDS_CHECK
+static __device__ unsigned int g_violations;  // one per code object (internal linkage)
+
+__device__ __noinline__ bool report_out_of_range(int64_t v, int64_t hi, const char* what) {
+  if (atomicAdd(&g_violations, 1u) == 0)
+    printf("[mopt bounds] %s: index %lld outside [0, %lld) (block %u thread %u)\n", what,
+           (long long)v, (long long)hi, blockIdx.x, threadIdx.x);
+  return false;
+}
+
+__device__ __forceinline__ bool in_range(int64_t v, int64_t hi, const char* what) {
+  return (v >= 0 && v < hi) ? true : report_out_of_range(v, hi, what);
+}
+#define MOPT_IN_RANGE(v, hi, what) ::mopt::in_range((int64_t)(v), (int64_t)(hi), what)
+// extern "C" reader of this code object's counter (reads and clears it; synchronises)
+#define MOPT_VIOLATIONS_READER(name)                                                  \
+  extern "C" unsigned int mopt_violations_##name() {                                  \
+    unsigned int h = 0, z = 0;                                                        \
+    if (hipDeviceSynchronize() != hipSuccess) return 0xFFFFFFFFu;                     \
+    if (hipMemcpyFromSymbol(&h, HIP_SYMBOL(::mopt::g_violations), sizeof h) != hipSuccess) \
+      return 0xFFFFFFFFu;                                                             \
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(::mopt::g_violations), &z, sizeof z);          \
+    return h;                                                                         \
+  }
+#define MOPT_CHECKED_BUILD 1
+#else
+#define MOPT_IN_RANGE(v, hi, what) true
+#define MOPT_VIOLATIONS_READER(name) \
+  extern "C" unsigned int mopt_violations_##name() { return 0; }
+#define MOPT_CHECKED_BUILD 0
+#endif
+
 }  // namespace mopt

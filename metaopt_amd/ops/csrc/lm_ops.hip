@@ -350,8 +350,9 @@ __global__ __launch_bounds__(256) void ce_fwd_bwd_kernel(bf16_t* __restrict__ lo
 #pragma unroll
   for (int w = 0; w < 4; ++w)
     if (red[w] != -INFINITY) S += red[4 + w] * __expf(red[w] - M);
-  const int y = labels[row];
-  if (threadIdx.x == 0) {
+  int y = labels[row];
+  if (!MOPT_IN_RANGE(y, V, "ce_fwd_bwd label")) y = -1;  // checked build: no loss, no one-hot
+  if (threadIdx.x == 0 && y >= 0) {
     const float zy = bf2f(z[y]);
     atomicAdd(loss_sum + row / rows_per_trial, M + __logf(S) - zy);
   }
@@ -381,7 +382,12 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int32_t* __restric
   const int64_t r = i / per;
   const int c = (int)(i % per) * 8;
   const int64_t p = r / rows_per_trial;
-  *(uint4*)(out + r * d + c) = *(const uint4*)(table + (p * V + tok[r]) * (int64_t)d + c);
+  const int t = tok[r];
+  if (!MOPT_IN_RANGE(t, V, "embedding token")) {
+    *(uint4*)(out + r * d + c) = make_uint4(0, 0, 0, 0);
+    return;
+  }
+  *(uint4*)(out + r * d + c) = *(const uint4*)(table + (p * V + t) * (int64_t)d + c);
 }
 
 __global__ __launch_bounds__(256) void embed_bwd_kernel(const int32_t* __restrict__ tok,
@@ -397,6 +403,7 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const int32_t* __restric
   const int64_t p = r / rows_per_trial;
   float v[8];
   unpack8(*(const uint4*)(dout + r * d + c), v);
+  if (!MOPT_IN_RANGE(tok[r], V, "embedding backward token")) return;
   float* dst = dtable32 + (p * V + tok[r]) * (int64_t)d + c;
 #pragma unroll
   for (int e = 0; e < 8; ++e) atomicAdd(dst + e, v[e]);
@@ -423,6 +430,7 @@ __global__ __launch_bounds__(256) void embed_bwd_sorted_kernel(const int64_t* __
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[k][e] = 0.f;
   for (int64_t j = w; j < rows && keys[j] == key; ++j) {
+    if (!MOPT_IN_RANGE(order[j], rows, "embedding backward sorted order")) continue;
     const bf16_t* src = dout + order[j] * (int64_t)d;
 #pragma unroll
     for (int k = 0; k < kMaxChunks; ++k) {
@@ -850,3 +858,6 @@ int mopt_sgd_multi(const void* segs, const void* chunks, int n_chunks, const voi
 }
 
 }  // extern "C"
+
+// device-side index checks of the checked build (common.h)
+MOPT_VIOLATIONS_READER(lm_ops)

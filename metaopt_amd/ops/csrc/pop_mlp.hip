@@ -279,7 +279,9 @@ __global__ __launch_bounds__(256) void mlp_fwd_ce_kernel(const MlpTL* __restrict
   float loss = 0.f, corr = 0.f;
   if (tid < BM) {
     const float* z = Ls + tid * CS;
-    const int y = labels[row0 + tid];
+    int y = labels[row0 + tid];
+    const bool y_ok = MOPT_IN_RANGE(y, C, "mlp cross-entropy label");
+    if (!y_ok) y = -1;                // checked build: no loss, no one-hot
     float m = -INFINITY;
     int am = 0;
     for (int c = 0; c < C; ++c)
@@ -287,7 +289,7 @@ __global__ __launch_bounds__(256) void mlp_fwd_ce_kernel(const MlpTL* __restrict
     float s = 0.f;
     for (int c = 0; c < C; ++c) s += __expf(z[c] - m);
     const float lse = m + __logf(s);
-    loss = lse - z[y];
+    loss = y_ok ? lse - z[y] : 0.f;
     corr = (am == y) ? 1.f : 0.f;
     if (flags & kWriteGrad) {
       const float rs = 1.f / s;
@@ -655,6 +657,9 @@ extern "C" {
 
 int mopt_abi_version() { return 8; }
 
+// 1 when this library is the bounds-checked variant (-DMOPT_BOUNDS_CHECK)
+int mopt_checked_build() { return MOPT_CHECKED_BUILD; }
+
 // flags: 1 = zero the AdamW second moment, 2 = the momentum buffer is bf16
 int mopt_mlp_init(const void* descs, int n_desc, void* plo, void* p16, void* m32, void* v32,
                   int flags, void* stream) {
@@ -753,3 +758,6 @@ int mopt_mlp_step(const MlpStep* s, const void* x, const void* y, void* stream) 
 }
 
 }  // extern "C"
+
+// device-side index checks of the checked build (common.h)
+MOPT_VIOLATIONS_READER(pop_mlp)

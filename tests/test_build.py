@@ -24,3 +24,19 @@ def test_built_library_matches_tree():
     if not build.lib_path().exists():
         pytest.skip("kernel library not built")
     assert build.built_digest() == build.source_digest()
+
+
+def test_checked_variant_is_the_bounds_checked_build():
+    """The debug variant (MOPT_KERNEL_CHECKED=1) is built from this tree with
+    -DMOPT_BOUNDS_CHECK and says so; the default library says it is not."""
+    import ctypes
+    path = build.variant_path(build.CHECKED)
+    if not path.exists():
+        pytest.skip("checked variant not built")
+    assert build.variant_digest(build.CHECKED) == build.source_digest(build.CHECKED_FLAGS)
+    chk = ctypes.CDLL(str(path))
+    assert chk.mopt_checked_build() == 1
+    for mod in _lib._CHECKED_MODULES:
+        assert hasattr(chk, "mopt_violations_" + mod)
+    if build.lib_path().exists():
+        assert ctypes.CDLL(str(build.lib_path())).mopt_checked_build() == 0
