@@ -96,6 +96,40 @@ def hyper_sgdm_ref(w, v, ze, zm, ye, ym, g, he, hm, eta, mu):
     ym.copy_(ymn)
 
 
+class _Unflatten(torch.autograd.Function):
+    """The parameter tensors of the flat run state ``W [P, n]`` (slices, reshaped).
+
+    Differentiating through plain slices of one flat tensor makes autograd build, for EVERY
+    parameter, a zero-filled [P, n] gradient holding its slice and then add them all up (and,
+    forward-over-reverse, the same again for the batched tangents): ~17 full-size fills + adds
+    per gradient.  Here the backward is one ``cat`` of the parameter gradients and the tangent
+    of each output is the matching slice of the input tangent -- still composable with
+    ``torch.func`` (jvp of the backward = cat of the tangents; vmap rule generated)."""
+    generate_vmap_rule = True
+
+    @staticmethod
+    def forward(W, layout):
+        return tuple(W[:, o:o + k].reshape(W.shape[0], *shape) for o, k, shape in layout)
+
+    @staticmethod
+    def setup_context(ctx, inputs, output):
+        ctx.layout = inputs[1]
+
+    @staticmethod
+    def backward(ctx, *grads):
+        parts = []
+        for g, (o, k, shape) in zip(grads, ctx.layout):
+            if g is None:
+                g = torch.zeros(grads[0].shape[0], k, dtype=grads[0].dtype,
+                                device=grads[0].device)
+            parts.append(g.reshape(g.shape[0], k))
+        return torch.cat(parts, 1), None
+
+    @staticmethod
+    def jvp(ctx, dW, _):
+        return tuple(dW[:, o:o + k].reshape(dW.shape[0], *shape) for o, k, shape in ctx.layout)
+
+
 class HypergradLM:
     def __init__(self, capacity: int, config="tiny-2layer", batch_size: int = 4,
                  seq_len: Optional[int] = None, device="cuda", graph: Optional[bool] = None,
@@ -137,8 +171,9 @@ class HypergradLM:
         self._eager_steps = 0
 
     def params(self, W: torch.Tensor) -> Dict[str, torch.Tensor]:
-        return {name: W[:, o:o + k].view(self.P, *shape)
-                for (name, shape, _), (o, k) in zip(self.specs, self.offsets)}
+        layout = tuple((o, k, tuple(shape)) for (_, shape, _), (o, k) in
+                       zip(self.specs, self.offsets))
+        return dict(zip((name for name, _, _ in self.specs), _Unflatten.apply(W, layout)))
 
     def reset(self, seeds: List[int], eta, mu) -> None:
         """Fresh inner runs: weights from per-run seeds, zero momentum and tangents."""
