@@ -49,13 +49,81 @@ _lib.register_signatures({
 })
 
 
+class _CausalSoftmax(torch.autograd.Function):
+    """p = softmax(causal_mask(scale * s)) over the last dim, with analytic derivatives:
+    backward gs = scale p (g - <p, g>), tangent dp = scale p (ds - <p, ds>) -- a handful of
+    fused-size ops instead of the scale / masked_fill / softmax chain differentiated op by op
+    (masked entries have p = 0, so no mask is needed after the forward).  The backward is
+    written in differentiable ops, so forward-over-reverse (jvp of grad) composes; vmap rule
+    generated."""
+    generate_vmap_rule = True
+
+    @staticmethod
+    def forward(s, scale):
+        T = s.shape[-1]
+        mask = torch.ones(T, T, dtype=torch.bool, device=s.device).triu(1)
+        return (s * scale).masked_fill(mask, float("-inf")).softmax(-1)
+
+    @staticmethod
+    def setup_context(ctx, inputs, output):
+        ctx.save_for_backward(output)
+        ctx.save_for_forward(output)
+        ctx.scale = inputs[1]
+
+    @staticmethod
+    def backward(ctx, g):
+        p, = ctx.saved_tensors
+        pg = p * g
+        return (pg - p * pg.sum(-1, keepdim=True)) * ctx.scale, None
+
+    @staticmethod
+    def jvp(ctx, ds, _):
+        p, = ctx.saved_tensors
+        pd = p * ds
+        return (pd - p * pd.sum(-1, keepdim=True)) * ctx.scale
+
+
+class _Rotary(torch.autograd.Function):
+    """RoPE rotation of [..., T, 64] by (cos, sin) [T, 32].  The rotation is linear and
+    orthogonal: its tangent is the same rotation of the input tangent and its adjoint the
+    rotation by -sin, both computed by this Function again -- so every derivative order stays a
+    handful of elementwise ops (no slice-gradient zero fills or cat-backward copies)."""
+    generate_vmap_rule = True
+
+    @staticmethod
+    def forward(t, cos, sin):
+        t1, t2 = t[..., :32], t[..., 32:]
+        return torch.cat([t1 * cos - t2 * sin, t2 * cos + t1 * sin], -1)
+
+    @staticmethod
+    def setup_context(ctx, inputs, output):
+        ctx.cs = (inputs[1], inputs[2])
+
+    @staticmethod
+    def backward(ctx, g):
+        cos, sin = ctx.cs
+        return _Rotary.apply(g, cos, -sin), None, None
+
+    @staticmethod
+    def jvp(ctx, dt, _c, _s):
+        cos, sin = ctx.cs
+        return _Rotary.apply(dt, cos, sin)
+
+
+def rope_split(qkv, cos, sin, T, H):
+    """(q, k, v) [B', H, T, 64] of the fused projection rows [B' T, 3 H 64], q and k rotated
+    (fp32 twin of ``ops.rope_split_ref`` with the rotation as one differentiable Function)."""
+    Bp = qkv.shape[0] // T
+    x = qkv.view(Bp, T, 3, H, 64).permute(2, 0, 3, 1, 4)      # [3, B', H, T, 64]
+    return _Rotary.apply(x[0], cos, sin), _Rotary.apply(x[1], cos, sin), x[2].contiguous()
+
+
 def causal_attention(q, k, v, scale):
     """Causal softmax attention of [B', H, T, Dh] heads -> rows [B' T, H Dh]: scores and values
     on the population GEMM (differentiable to second order), softmax in fp32."""
     Bp, H, T, Dh = q.shape
-    s = matmul(q.reshape(Bp * H, T, Dh), k.reshape(Bp * H, T, Dh), tb=True) * scale
-    mask = torch.ones(T, T, dtype=torch.bool, device=q.device).triu(1)
-    p = s.masked_fill(mask, float("-inf")).softmax(-1)
+    s = matmul(q.reshape(Bp * H, T, Dh), k.reshape(Bp * H, T, Dh), tb=True)
+    p = _CausalSoftmax.apply(s, scale)
     o = matmul(p, v.reshape(Bp * H, T, Dh))
     return o.view(Bp, H, T, Dh).permute(0, 2, 1, 3).reshape(Bp * T, H * Dh)
 
@@ -70,7 +138,7 @@ def lm_losses(params: Dict[str, torch.Tensor], tok, tgt, cfg: LMConfig, cos, sin
     for l in range(cfg.n_layers):
         h = ops.rmsnorm_ref(x, params[f"l{l}.attn_norm"], rpt, cfg.norm_eps)
         qkv = matmul(h.view(P, rpt, d), params[f"l{l}.wqkv"]).reshape(R, 3 * d)
-        q, k, v = ops.rope_split_ref(qkv, cos, sin, T, H)
+        q, k, v = rope_split(qkv, cos, sin, T, H)
         o = causal_attention(q, k, v, 1.0 / math.sqrt(cfg.head_dim))
         x = x + matmul(o.view(P, rpt, d), params[f"l{l}.wo"]).reshape(R, d)
         h = ops.rmsnorm_ref(x, params[f"l{l}.mlp_norm"], rpt, cfg.norm_eps)
