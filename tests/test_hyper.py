@@ -144,3 +144,44 @@ def test_c3_intra_trial_data_parallel_equals_one_process():
     torch.testing.assert_close(w0, m.w, rtol=1e-4, atol=1e-6)
     torch.testing.assert_close(hg0, hg, rtol=1e-3, atol=1e-5)
     torch.testing.assert_close(vl0, vl, rtol=1e-5, atol=1e-6)
+
+
+def test_analytic_functions_match_op_by_op_second_order():
+    """The K11 graph's hand-derived Functions (parameter unflatten, RoPE, causal softmax) give
+    the same values, gradients and Hessian-vector products (jvp of grad, vmapped over two
+    tangents) as the op-by-op expressions they replace."""
+    import math
+    from metaopt_amd.models.hyper import _CausalSoftmax, rope_split
+    from metaopt_amd.ops import lm as lmops
+    torch.manual_seed(0)
+    T, H, Bp = 16, 2, 3
+    qkv = torch.randn(Bp * T, 3 * H * 64, dtype=torch.float32)
+    cos, sin = lmops.rope_tables(T)
+    scale = 1.0 / math.sqrt(64)
+
+    def attn(q, k, v, soft):
+        s = q @ k.transpose(-1, -2)
+        return soft(s) @ v
+
+    def soft_ref(s):
+        mask = torch.ones(T, T, dtype=torch.bool).triu(1)
+        return (s * scale).masked_fill(mask, float("-inf")).softmax(-1)
+
+    def f_new(z):
+        q, k, v = rope_split(z, cos, sin, T, H)
+        return (attn(q, k, v, lambda s: _CausalSoftmax.apply(s, scale)) ** 2).sum()
+
+    def f_ref(z):
+        q, k, v = lmops.rope_split_ref(z, cos, sin, T, H)
+        return (attn(q, k, v, soft_ref) ** 2).sum()
+
+    assert torch.allclose(f_new(qkv), f_ref(qkv), rtol=1e-5)
+    tangents = torch.randn(2, *qkv.shape, dtype=torch.float32)
+
+    def hvp(f):
+        along = lambda t: torch.func.jvp(torch.func.grad(f), (qkv,), (t,))
+        return torch.func.vmap(along)(tangents)
+
+    (g1, h1), (g2, h2) = hvp(f_new), hvp(f_ref)
+    assert torch.allclose(g1, g2, rtol=1e-4, atol=1e-4)
+    assert torch.allclose(h1, h2, rtol=1e-4, atol=1e-4)
