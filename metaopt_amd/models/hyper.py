@@ -118,6 +118,47 @@ def rope_split(qkv, cos, sin, T, H):
     return _Rotary.apply(x[0], cos, sin), _Rotary.apply(x[1], cos, sin), x[2].contiguous()
 
 
+def rmsnorm(x, w, rows_per_trial, eps):
+    """fp32 RMSNorm of rows [P rpt, d] with per-trial weights [P, d] broadcast over the trial's
+    rows (``ops.rmsnorm_ref`` materialises them with repeat_interleave; same arithmetic)."""
+    r = torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + eps)
+    return ((x * r).view(w.shape[0], rows_per_trial, -1) * w[:, None, :]).view(x.shape)
+
+
+class _SwiGLU(torch.autograd.Function):
+    """silu(g) * u of gu = [g | u] with analytic derivatives (slicing gu op by op makes the
+    backward zero-fill and add two full-size gradients per pass):
+    adjoint [gy u silu'(g) | gy silu(g)], tangent silu'(g) u dg + silu(g) du,
+    silu'(g) = s (1 + g (1 - s)), s = sigmoid(g)."""
+    generate_vmap_rule = True
+
+    @staticmethod
+    def forward(gu):
+        F = gu.shape[-1] // 2
+        return torch.nn.functional.silu(gu[..., :F]) * gu[..., F:]
+
+    @staticmethod
+    def setup_context(ctx, inputs, output):
+        ctx.save_for_backward(inputs[0])
+        ctx.save_for_forward(inputs[0])
+
+    @staticmethod
+    def backward(ctx, gy):
+        gu, = ctx.saved_tensors
+        F = gu.shape[-1] // 2
+        g, u = gu[..., :F], gu[..., F:]
+        s = torch.sigmoid(g)
+        return torch.cat([gy * u * (s * (1 + g * (1 - s))), gy * (g * s)], -1)
+
+    @staticmethod
+    def jvp(ctx, dgu):
+        gu, = ctx.saved_tensors
+        F = gu.shape[-1] // 2
+        g, u = gu[..., :F], gu[..., F:]
+        s = torch.sigmoid(g)
+        return dgu[..., :F] * u * (s * (1 + g * (1 - s))) + (g * s) * dgu[..., F:]
+
+
 def causal_attention(q, k, v, scale):
     """Causal softmax attention of [B', H, T, Dh] heads -> rows [B' T, H Dh]: scores and values
     on the population GEMM (differentiable to second order), softmax in fp32."""
@@ -136,15 +177,15 @@ def lm_losses(params: Dict[str, torch.Tensor], tok, tgt, cfg: LMConfig, cos, sin
     R = P * rpt
     x = ops.embed_ref(tok.reshape(-1), params["embed"], rpt)
     for l in range(cfg.n_layers):
-        h = ops.rmsnorm_ref(x, params[f"l{l}.attn_norm"], rpt, cfg.norm_eps)
+        h = rmsnorm(x, params[f"l{l}.attn_norm"], rpt, cfg.norm_eps)
         qkv = matmul(h.view(P, rpt, d), params[f"l{l}.wqkv"]).reshape(R, 3 * d)
         q, k, v = rope_split(qkv, cos, sin, T, H)
         o = causal_attention(q, k, v, 1.0 / math.sqrt(cfg.head_dim))
         x = x + matmul(o.view(P, rpt, d), params[f"l{l}.wo"]).reshape(R, d)
-        h = ops.rmsnorm_ref(x, params[f"l{l}.mlp_norm"], rpt, cfg.norm_eps)
-        a = ops.swiglu_ref(matmul(h.view(P, rpt, d), params[f"l{l}.wgu"]))
+        h = rmsnorm(x, params[f"l{l}.mlp_norm"], rpt, cfg.norm_eps)
+        a = _SwiGLU.apply(matmul(h.view(P, rpt, d), params[f"l{l}.wgu"]))
         x = x + matmul(a, params[f"l{l}.wdown"]).reshape(R, d)
-    h = ops.rmsnorm_ref(x, params["final_norm"], rpt, cfg.norm_eps)
+    h = rmsnorm(x, params["final_norm"], rpt, cfg.norm_eps)
     logits = matmul(h.view(P, rpt, d), params["head"]).reshape(R, cfg.vocab)
     lz = torch.nn.functional.cross_entropy(logits, tgt.reshape(-1).long(), reduction="none")
     return lz.view(P, rpt).mean(1)

@@ -185,3 +185,23 @@ def test_analytic_functions_match_op_by_op_second_order():
     (g1, h1), (g2, h2) = hvp(f_new), hvp(f_ref)
     assert torch.allclose(g1, g2, rtol=1e-4, atol=1e-4)
     assert torch.allclose(h1, h2, rtol=1e-4, atol=1e-4)
+
+
+def test_swiglu_and_rmsnorm_match_reference_second_order():
+    from metaopt_amd.models.hyper import _SwiGLU, rmsnorm
+    from metaopt_amd.ops import lm as lmops
+    torch.manual_seed(1)
+    P, rpt, d = 2, 8, 32
+    gu = torch.randn(P, rpt, 2 * d)
+    x = torch.randn(P * rpt, d)
+    w = 1 + 0.1 * torch.randn(P, d)
+    assert torch.equal(rmsnorm(x, w, rpt, 1e-5), lmops.rmsnorm_ref(x, w, rpt, 1e-5))
+    f_new = lambda z: (_SwiGLU.apply(z) ** 2).sum()
+    f_ref = lambda z: (lmops.swiglu_ref(z) ** 2).sum()
+    assert torch.allclose(f_new(gu), f_ref(gu), rtol=1e-6)
+    tangents = torch.randn(2, *gu.shape)
+    hvp = lambda f: torch.func.vmap(
+        lambda t: torch.func.jvp(torch.func.grad(f), (gu,), (t,)))(tangents)
+    (g1, h1), (g2, h2) = hvp(f_new), hvp(f_ref)
+    assert torch.allclose(g1, g2, rtol=1e-5, atol=1e-5)
+    assert torch.allclose(h1, h2, rtol=1e-5, atol=1e-5)
