@@ -34,13 +34,15 @@ def upgrade_db_specifics(database):
     """Backend-specific steps: deprecated indexes everywhere, the on-disk format of a PickledDB
     file, MongoDB's index set (re-created by the storage setup that follows)."""
     from ...storage.database import MongoDB, PickledDB
-    print("Updating indexes...")
-    update_indexes(database)
     if isinstance(database, PickledDB):
+        # the format conversion is counted on the file as found: any write (an index drop
+        # included) rewrites it in the current format, so it runs before the index step
         print("Updating pickleddb scheme...")
         n = database.upgrade_format()
         print(f"  {n} collection(s) converted to format 2")
-    elif isinstance(database, MongoDB):
+    print("Updating indexes...")
+    update_indexes(database)
+    if isinstance(database, MongoDB):
         print("Updating mongodb scheme...")
         for col in ("experiments", "trials"):
             for name in list(database.index_information(col)):

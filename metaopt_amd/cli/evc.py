@@ -5,20 +5,20 @@ from ..evc import adapters
 from ..evc import conflicts as C
 
 RESOLUTION_ARGS = [
-    (C.ExperimentNameConflict.ExperimentNameResolution.ARGUMENT, "-b",
+    (C.FLAGS["branch"], "-b",
      dict(type=str, metavar="stringID",
           help="Unique name for the new branching experiment")),
-    (C.AlgorithmConflict.AlgorithmResolution.ARGUMENT, None,
+    (C.FLAGS["algorithm"], None,
      dict(action="store_true", help="Set algorithm change as resolved if a branching event "
                                     "occur")),
-    (C.CodeConflict.CodeResolution.ARGUMENT, None,
-     dict(type=str, choices=adapters.CodeChange.types,
+    (C.FLAGS["code"], None,
+     dict(type=str, choices=list(adapters.CHANGE_TYPES),
           help="Set code change type (default: break)")),
-    (C.CommandLineConflict.CommandLineResolution.ARGUMENT, None,
-     dict(type=str, choices=adapters.CommandLineChange.types,
+    (C.FLAGS["cli"], None,
+     dict(type=str, choices=list(adapters.CHANGE_TYPES),
           help="Set command line change type (default: break)")),
-    (C.ScriptConfigConflict.ScriptConfigResolution.ARGUMENT, None,
-     dict(type=str, choices=adapters.ScriptConfigChange.types,
+    (C.FLAGS["config"], None,
+     dict(type=str, choices=list(adapters.CHANGE_TYPES),
           help="Set script config change type (default: break)")),
 ]
 

@@ -95,11 +95,16 @@ def main(args):
                             ckpt_dir=args.get("ckpt_dir"))
     try:
         summary = sweep.run(args["steps"])
-    finally:
-        # releases in-flight trials and stops the watchdog even when a collective failed
-        sweep.close()
+    except BaseException:
+        # rank-local teardown only: the peers may be inside another collective; the original
+        # error propagates (in-flight trials -> interrupted, the watchdog stops)
+        sweep.close(failed=True)
         if events is not None:
             events.close()
+        raise
+    sweep.close()
+    if events is not None:
+        events.close()
     if comm.is_root:
         print(json.dumps({k: v for k, v in summary.items()}, default=str))
     shutdown()

@@ -436,6 +436,10 @@ class HypergradientSweep:
         for k in range(self.inner_steps):
             tok, tgt = self.data.batch(shard * self.inner_steps + k)
             if dp:
+                if tok.shape[0] % comm.world_size:
+                    raise ValueError(f"C3: the minibatch ({tok.shape[0]} rows) does not split "
+                                     f"evenly over {comm.world_size} ranks; the averaged "
+                                     "shard gradients would not equal the full batch's")
                 rows = tok.shape[0] // comm.world_size
                 tok = tok[comm.rank * rows:(comm.rank + 1) * rows]
                 tgt = tgt[comm.rank * rows:(comm.rank + 1) * rows]

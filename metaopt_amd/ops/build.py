@@ -9,7 +9,8 @@ Each ``csrc/*.hip`` file is compiled to its own object (incremental: only stale 
 the objects are linked once.  ``python -m metaopt_amd.ops.build [--force]`` rebuilds by hand.
 
 Provenance: the link also writes ``libmopt_kernels.so.sha256``, the digest of every source,
-header, flag and the target arch the library was built from.  ``build()`` recompiles everything
+header, flag and the target arch the library was built from, paired with the sha256 of the
+linked binary itself (a stamp is void next to any other binary).  ``build()`` recompiles everything
 when the digest of the current tree differs (modification times do not survive a copy of the
 tree), and the loader (:mod:`._lib`) refuses a library whose digest does not match the sources
 next to it -- a stale ``.so`` shipped with a snapshot fails loudly instead of running old code.
@@ -74,9 +75,33 @@ def source_digest(extra_flags=None) -> str:
     return h.hexdigest()
 
 
+def _file_sha256(path: Path) -> str:
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
+def _write_stamp(lib: Path, stamp: Path, digest: str) -> None:
+    """Record the source digest together with the hash of the library it describes."""
+    stamp.write_text(f"{digest} {_file_sha256(lib)}\n")
+
+
+def _read_stamp(lib: Path, stamp: Path) -> str:
+    """The source digest ``lib`` was built from -- but only when the stamp names this very
+    binary (its sha256): a stamp left next to another library (a checkout that changed the
+    sources, a copied file) vouches for nothing and reads as ""."""
+    if not stamp.exists() or not lib.exists():
+        return ""
+    parts = stamp.read_text().split()
+    if len(parts) != 2 or parts[1] != _file_sha256(lib):
+        return ""
+    return parts[0]
+
+
 def built_digest() -> str:
-    p = digest_path()
-    return p.read_text().strip() if p.exists() else ""
+    return _read_stamp(lib_path(), digest_path())
 
 
 def _needs(obj: Path, deps) -> bool:
@@ -127,7 +152,7 @@ def build(force: bool = False, verbose: bool = False, extra_flags=None) -> Path:
         if proc.returncode != 0:
             raise RuntimeError(f"link failed:\n{proc.stderr}")
         os.replace(tmp, lib)
-        digest_path().write_text(digest + "\n")
+        _write_stamp(lib, digest_path(), digest)
         if verbose:
             print(f"[mopt build] linked {lib}")
     return lib
@@ -146,8 +171,8 @@ def variant_path(name: str) -> Path:
 
 
 def variant_digest(name: str) -> str:
-    p = variant_path(name).with_suffix(".so.sha256")
-    return p.read_text().strip() if p.exists() else ""
+    lib = variant_path(name)
+    return _read_stamp(lib, lib.with_suffix(".so.sha256"))
 
 
 def build_variant(name: str, extra_flags, verbose: bool = False, force: bool = True) -> Path:
@@ -170,7 +195,7 @@ def build_variant(name: str, extra_flags, verbose: bool = False, force: bool = T
                            "-o", str(lib)], capture_output=True, text=True)
     if proc.returncode != 0:
         raise RuntimeError(f"link failed:\n{proc.stderr}")
-    lib.with_suffix(".so.sha256").write_text(digest + "\n")
+    _write_stamp(lib, lib.with_suffix(".so.sha256"), digest)
     if verbose:
         print(f"[mopt build] variant {name}: {lib}")
     return lib

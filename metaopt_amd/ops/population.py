@@ -193,9 +193,10 @@ class PopulationMLP:
         # latency-bound forward overlaps another's bandwidth-bound backward (measured: two
         # processes sharing the GPU ran 14% more trials/s than one).  Any other operation first
         # joins the side streams into the main one (``_join``); the next train step forks them
-        # again after it.
+        # again after it.  Default 1: round 3 measured 741.7 / 748.5 trials/s for 1 / 2 streams
+        # (noise) with 2.9 vs 4.0 ms of host launch time per interval (profiles/README.md).
         if n_streams is None:
-            n_streams = int(os.environ.get("MOPT_STREAMS", "2")) if backend == "hip" else 1
+            n_streams = int(os.environ.get("MOPT_STREAMS", "1")) if backend == "hip" else 1
         self.n_streams = max(1, int(n_streams))
         self._side_streams: list = []
         self._events: list = []

@@ -682,7 +682,7 @@ def default_pickled_path() -> str:
 class PickledDB(AbstractDB):
     """An :class:`EphemeralDB` pickled to ``host`` (a file path), every op under a file lock.
 
-    Collections pickle as format 2 (documents + index definitions; indexes rebuilt on load);
+    Collections pickle as format 2 (documents and built indexes, unpickled as stored);
     older files load through ``_Collection.__setstate__`` and are rewritten in the current
     format by the next write or by :meth:`upgrade_format` (``mopt db upgrade``)."""
 

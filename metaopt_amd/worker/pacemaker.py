@@ -1,37 +1,121 @@
-"""Heartbeat thread for a running trial (reference: ``src/orion/core/worker/trial_pacemaker.py:14-52``).
+"""Heartbeats of running trials.
 
-Every ``wait_time`` seconds it refreshes the trial's ``heartbeat`` in storage; it stops on its own
-once the trial is completed, interrupted or suspended, or when the heartbeat update fails (the
-trial was taken over after being declared lost).
+Behaviour contract (reference ``src/orion/core/worker/trial_pacemaker.py:14-52``): while a trial
+runs, its ``heartbeat`` in storage is refreshed every ``wait_time`` seconds; the refreshes stop
+once the trial is completed / interrupted / suspended / broken, or when a refresh fails (the trial
+was declared lost and taken over by another worker).
+
+Structure: one scheduler thread serves every pacemaker of the process from a deadline heap --
+a study holding many reserved trials (``client/study.py``) costs one thread, not one per trial.
+:class:`TrialPacemaker` is a handle on one entry: ``start`` schedules it, ``stop`` cancels it
+and returns once no beat of it is running, ``stopped`` is set when it ends for any reason.
 """
 from __future__ import annotations
 
+import heapq
+import itertools
+import logging
 import threading
+import time
+
+log = logging.getLogger(__name__)
 
 STOPPED_STATUS = {"completed", "interrupted", "suspended", "broken"}
 
 
-class TrialPacemaker(threading.Thread):
+class _Scheduler:
+    """Deadline heap of pacemakers, served by one daemon thread (started on first use)."""
+
+    def __init__(self):
+        self._cv = threading.Condition()
+        self._heap = []                     # (due, seq, pacemaker)
+        self._seq = itertools.count()
+        self._thread = None
+        self._running = None                # the pacemaker whose beat is in progress
+
+    def add(self, pm, due):
+        with self._cv:
+            heapq.heappush(self._heap, (due, next(self._seq), pm))
+            if self._thread is None or not self._thread.is_alive():
+                self._thread = threading.Thread(target=self._serve, name="mopt-heartbeats",
+                                                daemon=True)
+                self._thread.start()
+            self._cv.notify()
+
+    def wait_idle(self, pm):
+        """Block until ``pm`` is not being beaten (its entry may still sit in the heap, where
+        it is skipped once ``pm.stopped`` is set)."""
+        with self._cv:
+            while self._running is pm:
+                self._cv.wait(0.05)
+
+    def _serve(self):
+        while True:
+            with self._cv:
+                while True:
+                    while self._heap and self._heap[0][2].stopped.is_set():
+                        heapq.heappop(self._heap)          # cancelled entries
+                    if not self._heap:
+                        self._cv.wait(1.0)
+                        if not self._heap:
+                            self._thread = None
+                            return                          # idle: the next add restarts it
+                        continue
+                    due = self._heap[0][0]
+                    now = time.monotonic()
+                    if due <= now:
+                        _, _, pm = heapq.heappop(self._heap)
+                        self._running = pm
+                        break
+                    self._cv.wait(due - now)
+            try:
+                alive = pm._beat()
+            except Exception as exc:   # a storage error ends this trial's heartbeat only
+                log.warning("heartbeat of trial %s failed: %s", pm.trial.id, exc)
+                alive = False
+            with self._cv:
+                self._running = None
+                if alive and not pm.stopped.is_set():
+                    heapq.heappush(self._heap, (time.monotonic() + pm.wait_time,
+                                                next(self._seq), pm))
+                else:
+                    pm.stopped.set()
+                self._cv.notify_all()
+
+
+_SCHEDULER = _Scheduler()
+
+
+class TrialPacemaker:
+    """Keep ``trial``'s heartbeat fresh every ``wait_time`` seconds until it stops running."""
+
     def __init__(self, trial, wait_time=60, storage=None):
-        super().__init__(daemon=True)
-        from ..storage.protocol import get_storage
-        self.stopped = threading.Event()
+        if storage is None:
+            from ..storage.protocol import get_storage
+            storage = get_storage()
         self.trial = trial
-        self.wait_time = wait_time
-        self.storage = storage if storage is not None else get_storage()
+        self.wait_time = float(wait_time)
+        self.storage = storage
+        self.stopped = threading.Event()
+        self._started = False
+
+    def start(self):
+        if self._started:
+            raise RuntimeError("a pacemaker starts once")
+        self._started = True
+        _SCHEDULER.add(self, time.monotonic() + self.wait_time)
 
     def stop(self):
+        """Cancel further beats; returns once none of this trial's beats is in progress."""
         self.stopped.set()
-        if self.is_alive():
-            self.join()
+        _SCHEDULER.wait_idle(self)
 
-    def run(self):
-        while not self.stopped.wait(self.wait_time):
-            self._monitor_trial()
+    def is_alive(self) -> bool:
+        return self._started and not self.stopped.is_set()
 
-    def _monitor_trial(self):
-        trial = self.storage.get_trial(self.trial)
-        if trial is None or trial.status in STOPPED_STATUS:
-            self.stopped.set()
-        elif not self.storage.update_heartbeat(trial):
-            self.stopped.set()
+    def _beat(self) -> bool:
+        """One refresh; False when the trial no longer runs here."""
+        current = self.storage.get_trial(self.trial)
+        if current is None or current.status in STOPPED_STATUS:
+            return False
+        return bool(self.storage.update_heartbeat(current))

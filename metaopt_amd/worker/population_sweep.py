@@ -831,14 +831,31 @@ class PopulationSweep:
                 self.experiment, state={"algorithm": full,
                                         "sweep": {"global_step": int(self.global_step)}})
 
-    def close(self) -> None:
+    def close(self, failed: bool = False) -> None:
         """Collective end of the sweep: the results of the last sync reach the algorithm and
         the storage (pipelined mode), device state is spilled to sidecars (``ckpt_dir``), the
         trials still in flight are released (``interrupted``: a re-run or another worker
-        picks them up), and the algorithm state is saved."""
+        picks them up), and the algorithm state is saved.
+
+        ``failed``: the sweep is being torn down after an exception, possibly raised on this
+        rank only -- its peers may sit in a different collective, so nothing collective runs
+        (no drain, no spill): rank 0 releases its in-flight trials and flushes its writes, and
+        every rank stops its watchdog.  Errors of this cleanup are logged, never raised, so
+        the caller's original exception is the one that propagates."""
         if self.watchdog is not None:
             self.watchdog.stop()
         self._filling = False         # the final sync only collects results
+        if failed:
+            try:
+                if self.comm.is_root and self._writer is not None:
+                    self._release_in_flight()
+                    self.trials.clear()
+                    self._writer.flush()
+            except Exception as exc:  # the original error matters more
+                log.warning("cleanup after a failed sweep: %s", exc)
+            finally:
+                self._finish(save=False)
+            return
         try:
             self.drain()
             self.spill()
@@ -847,17 +864,27 @@ class PopulationSweep:
                 self._release_in_flight()
                 self.trials.clear()
                 self._writer.flush()
+            self._finish(save=True)
+
+    def _finish(self, save: bool) -> None:
+        if save:
             try:
                 self.save_algorithm_state()
             except Exception as exc:  # pragma: no cover - storage without the collection API
                 log.warning("algorithm state not saved: %s", exc)
-            self.events.emit("sweep_end", **{k: v for k, v in self.summary().items()
-                                             if k != "host_ms_per_sync"})
+        try:
+            self.events.emit("sweep_end", failed=not save,
+                             **{k: v for k, v in self.summary().items()
+                                if k != "host_ms_per_sync"})
             self.events.flush()
-            if self._gc_callback in gc.callbacks:
-                gc.callbacks.remove(self._gc_callback)
-            if self._writer is not None:
+        except Exception as exc:
+            log.warning("sweep_end event not written: %s", exc)
+        if self._gc_callback in gc.callbacks:
+            gc.callbacks.remove(self._gc_callback)
+        if self._writer is not None:
+            try:
                 self._writer.close()
+            finally:
                 self._writer = None
 
     # ------------------------------------------------------------------ every rank

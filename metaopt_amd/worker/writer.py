@@ -196,22 +196,40 @@ def _child(conn, spec, builder, seed_docs):  # pragma: no cover - runs in the ch
             return
 
 
+class WriterDied(RuntimeError):
+    """The writer child process is gone (it failed to open the database, was killed, or its
+    pipe broke)."""
+
+
 class WriterProcess:
     """:class:`WriteBehind`'s interface, applied by a child process (see module docstring).
 
     ``drain_while`` only hands the queued specs to a sender thread (pickling and the pipe write
     happen there, while the sweep's thread waits on the GPU or decides), so a slow database
-    never blocks the decision path; ``flush``/``close`` wait for the child."""
+    never blocks the decision path; ``flush``/``close`` wait for the child.
 
-    def __init__(self, storage, builder: DocBuilder, spec: tuple):
+    Failure: when the child dies (or the pipe breaks) the writer falls back to an in-process
+    :class:`WriteBehind` on the parent's storage and replays every write the child had not
+    acknowledged -- all of them for an in-memory database, whose child copy died with it.  The
+    replay is safe: registrations of trials the child did write hit the unique index and are
+    skipped, and status updates are compare-and-swap.  No caller ever waits on a dead child:
+    requests poll the child's liveness (``poll_s``)."""
+
+    def __init__(self, storage, builder: DocBuilder, spec: tuple, poll_s: float = 0.5):
         import queue
         self.storage = storage
         self.builder = builder
         self.spec = spec
         self.errors = 0
         self.busy_s = 0.0
+        self.poll_s = float(poll_s)
         self._held: list = []
         self._lock = threading.Lock()
+        # writes handed to the child and not yet covered by an acknowledged flush (an in-memory
+        # database keeps them all: the child's copy is the only one until close)
+        self._unacked: list = []
+        self._failure: Optional[BaseException] = None
+        self._fallback: Optional[WriteBehind] = None
         seed = None
         if spec[0] == "ephemeral":
             seed = storage.database.read("trials", {"experiment": builder.exp_id})
@@ -234,53 +252,118 @@ class WriterProcess:
     def __len__(self):
         return len(self._held)
 
+    @property
+    def failed(self) -> bool:
+        return self._fallback is not None
+
     def _send_loop(self):
-        while True:
-            item = self._queue.get()
-            if item[0] == "ops":
-                self._conn.send(item)
-                continue
-            # ("sync", request, done event, reply box): a request that waits for the child
-            _, request, done, box = item
-            self._conn.send(request)
-            box.append(self._conn.recv())
-            done.set()
-            if request[0] == "close":
-                return
+        item = None
+        try:
+            while True:
+                item = self._queue.get()
+                if item[0] == "ops":
+                    self._conn.send(item)
+                    continue
+                # ("sync", request, done event, reply box): a request that waits for the child
+                _, request, done, box = item
+                self._conn.send(request)
+                box.append(self._conn.recv())
+                done.set()
+                item = None
+                if request[0] == "close":
+                    return
+        except BaseException as exc:  # child gone, pipe broken, unpicklable op
+            self._failure = exc
+            if item is not None and item[0] == "sync":
+                item[2].set()           # the waiter sees an empty reply box
+            while True:                 # and so does every request queued behind it
+                try:
+                    nxt = self._queue.get_nowait()
+                except Exception:
+                    break
+                if nxt[0] == "sync":
+                    nxt[2].set()
+
+    def _fail_over(self, why) -> WriteBehind:
+        """Switch to in-process writes and replay what the child did not acknowledge."""
+        if self._fallback is None:
+            log.warning("storage writer process failed (%s): writing in process", why)
+            fb = WriteBehind(self.storage, self.builder)
+            fb.extend(self._unacked)
+            self._unacked = []
+            self._fallback = fb
+            if self._proc is not None and self._proc.is_alive():
+                self._proc.kill()
+        return self._fallback
 
     def _hand_over(self):
         with self._lock:
             held, self._held = self._held, []
-        if held:
-            self._queue.put(("ops", held))
+        if not held:
+            return
+        if self._fallback is not None:
+            self._fallback.extend(held)
+            return
+        self._unacked.extend(held)
+        self._queue.put(("ops", held))
 
     def _request(self, request):
+        """Send ``request`` and wait for the reply; None when the child died meanwhile."""
+        if self._fallback is not None:
+            return None
         done, box = threading.Event(), []
         self._queue.put(("sync", request, done, box))
-        done.wait()
-        return box[0]
+        while not done.wait(self.poll_s):
+            if self._failure is not None or not self._proc.is_alive():
+                break
+        if box:
+            return box[0]
+        self._fail_over(self._failure or f"child exited ({self._proc.exitcode})")
+        return None
 
     def drain_while(self, busy) -> None:
         t0 = time.perf_counter()
+        if self._fallback is None and (self._failure is not None or not self._proc.is_alive()):
+            self._fail_over(self._failure or f"child exited ({self._proc.exitcode})")
         self._hand_over()
+        if self._fallback is not None:
+            self._fallback.drain_while(busy)
         self.busy_s += time.perf_counter() - t0
 
     def flush(self):
-        """Wait until the child applied every write queued so far."""
+        """Wait until the child (or the in-process fallback) applied every write so far."""
         self._hand_over()
-        _, self.errors = self._request(("flush",))
+        reply = self._request(("flush",))
+        if reply is not None:
+            _, self.errors = reply
+            if self.spec[0] != "ephemeral":
+                self._unacked = []
+            return
+        fb = self._fallback
+        fb.flush()
+        self.errors = fb.errors
 
     def close(self):
         """Apply everything; copy an in-memory database's trials back into ``storage``."""
         if self._proc is None:
             return
         self._hand_over()
-        if self.spec[0] == "ephemeral":
-            _, docs = self._request(("dump",))
-            db = self.storage.database
-            db.remove("trials", {"experiment": self.builder.exp_id})
-            if docs:
-                db.write("trials", docs)
-        _, self.errors = self._request(("close",))
+        if self._fallback is None and self.spec[0] == "ephemeral":
+            reply = self._request(("dump",))
+            if reply is not None:
+                _, docs = reply
+                db = self.storage.database
+                db.remove("trials", {"experiment": self.builder.exp_id})
+                if docs:
+                    db.write("trials", docs)
+                self._unacked = []
+        reply = self._request(("close",))
+        if reply is not None:
+            _, self.errors = reply
+        else:
+            self._fallback.flush()
+            self.errors = self._fallback.errors
         self._proc.join(timeout=60)
+        if self._proc.is_alive():
+            self._proc.kill()
         self._proc = None

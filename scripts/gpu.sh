@@ -1,0 +1,69 @@
+#!/bin/bash
+# One parameterised GPU job runner (run on the box through gpurun, from the repo root):
+#
+#   OUT=gpurun_out/x bash scripts/gpu.sh STEP [STEP ...]
+#
+# Every step runs under its own time limit and the job stops at the first failing step (no GPU
+# work after a fault, an abort or a timeout).  Steps:
+#   tests            pytest -m gpu (whole suite)           tests:FILE[,FILE]  a subset
+#   bench            bench.py N=1 (driver shape)           bench_long  60 timed intervals
+#   random           bench.py --algo random (best-loss@budget at the same budget as ASHA)
+#   timeline         bench.py with the GPU-event timeline (MOPT_GPU_TIMELINE=1)
+#   streams          bench.py at MOPT_STREAMS=1,2
+#   kbench           per-kernel MLP microbench             trace_bench  rocprofv3 kernel trace
+#   pmc_kbench       PMC passes of the MLP kernels (fetch/write/MFMA/LDS, one pass each)
+#   lm resnet hyper  bench_configs.py of one config        trace_lm trace_resnet trace_hyper
+#   gemm conv        pgemm / direct-conv microbenches
+#   decide           rank-0 decide cost at simulated W=1,8 (host CPU of the box)
+#   rehearsal        bench.py --gpus 2 / 4 / 8 over gloo with ranks sharing the GPU
+set -e
+OUT=${OUT:-gpurun_out/job}
+mkdir -p "$OUT"
+ROOT=$(pwd)
+T="timeout -k 10"
+PYT="python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu"
+
+prof() {   # prof NAME LIMIT -- cmd...: rocprofv3 kernel trace + stats (own run, no counters)
+  local name=$1 lim=$2; shift 3
+  (cd /tmp && export TMPDIR=/tmp && $T "$lim" rocprofv3 --kernel-trace --stats \
+      --output-format csv -d "$ROOT/$OUT/$name" -o run -- "$@" > "$ROOT/$OUT/$name.log" 2>&1)
+}
+pmc() {    # pmc NAME COUNTERS...: one counter pass over the MLP kernel microbench
+  local name=$1; shift
+  (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 150 rocprofv3 --output-format csv \
+      --pmc "$@" -d "$ROOT/$OUT/$name" -o run -- \
+      python3 "$ROOT/scripts/kernel_bench.py" --iters 3 --momentum-dtype bf16 \
+      > "$ROOT/$OUT/$name.log" 2>&1)
+}
+
+for step in "$@"; do
+  echo "[gpu.sh] $step"
+  case "$step" in
+    tests)      $T 600 $PYT tests > "$OUT/pytest_gpu.log" 2>&1 ;;
+    tests:*)    $T 400 $PYT $(echo "${step#tests:}" | tr ',' ' ') > "$OUT/pytest_sub.log" 2>&1 ;;
+    bench)      $T 240 python bench.py --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
+    bench_long) $T 240 python bench.py --steps 60 --warmup 5 > "$OUT/bench_long.json" 2> "$OUT/bench_long.err" ;;
+    random)     $T 240 python bench.py --steps 20 --warmup 5 --algo random > "$OUT/bench_random.json" 2> "$OUT/bench_random.err" ;;
+    timeline)   MOPT_GPU_TIMELINE=1 $T 240 python bench.py --steps 20 --warmup 5 > "$OUT/bench_timeline.json" 2> "$OUT/bench_timeline.err" ;;
+    streams)    for s in 1 2; do MOPT_STREAMS=$s $T 240 python bench.py --steps 20 --warmup 5 > "$OUT/bench_streams$s.json" 2> "$OUT/bench_streams$s.err"; done ;;
+    kbench)     $T 200 python scripts/kernel_bench.py --momentum-dtype bf16 --out "$OUT/kbench.json" > "$OUT/kbench.log" 2>&1 ;;
+    trace_bench) prof trace_bench 300 -- python3 "$ROOT/bench.py" --steps 10 --warmup 3 ;;
+    pmc_kbench)
+      pmc pmc_fetch FETCH_SIZE
+      pmc pmc_write WRITE_SIZE
+      pmc pmc_mfma SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES
+      pmc pmc_lds SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAVE_CYCLES ;;
+    lm)         $T 300 python scripts/bench_configs.py --config lm-125m --steps 20 --warmup 10 > "$OUT/lm.json" 2> "$OUT/lm.err" ;;
+    resnet)     $T 300 python scripts/bench_configs.py --config resnet20 --steps 60 --warmup 30 > "$OUT/resnet20.json" 2> "$OUT/resnet20.err" ;;
+    hyper)      $T 300 python scripts/bench_configs.py --config hyper --steps 3 --warmup 1 > "$OUT/hyper.json" 2> "$OUT/hyper.err" ;;
+    trace_lm)   prof trace_lm 300 -- python3 "$ROOT/scripts/bench_configs.py" --config lm-125m --steps 6 --warmup 4 ;;
+    trace_resnet) prof trace_resnet 300 -- python3 "$ROOT/scripts/bench_configs.py" --config resnet20 --steps 20 --warmup 10 ;;
+    trace_hyper) prof trace_hyper 300 -- python3 "$ROOT/scripts/bench_configs.py" --config hyper --steps 1 --warmup 1 ;;
+    gemm)       $T 300 python scripts/gemm_bench.py --cfgs "${CFGS:-0,5,6,7}" --out "$OUT/gemm.json" > "$OUT/gemm.log" 2>&1 ;;
+    conv)       $T 200 python scripts/conv_bench.py --implicit --out "$OUT/conv_bench.json" > "$OUT/conv_bench.log" 2>&1 ;;
+    decide)     for w in 1 8; do WORLD=$w $T 300 python scripts/profile_decide.py > "$OUT/decide_world$w.log" 2>&1; done ;;
+    rehearsal)  for n in 2 4 8; do $T 400 python bench.py --gpus $n --steps 10 --warmup 3 > "$OUT/rehearsal_n$n.json" 2> "$OUT/rehearsal_n$n.err"; done ;;
+    *) echo "unknown step $step" >&2; exit 2 ;;
+  esac
+done
+echo "[gpu.sh] done"

@@ -44,38 +44,40 @@ def _data():
     return TeacherClassification(n_train=512, n_val=128, batch_size=128, seed=11)
 
 
-def _make(storage, data, comm=None, cap=4, **kw):
+def _make(storage, data, comm=None, cap=4, max_trials=MAX_TRIALS, **kw):
     exp = None
     if comm is None or comm.is_root:
         exp = build_experiment("resume-sweep", priors=PRIORS, algorithms=ALGO,
-                               max_trials=MAX_TRIALS, storage=storage)
+                               max_trials=max_trials, storage=storage)
     pop = PopulationMLP(cap, max_width=128, eval_batch=128, device="cpu")
     return exp, PopulationSweep(pop, MLPSweepTask(priors=PRIORS, max_width=128), data,
                                 comm=comm, experiment=exp, sync_every=16,
                                 ckpt_capacity=64, **kw)
 
 
-def _phase_worker(rank, world, port, db_path, ckpt_dir, max_steps, resume, q, cap=4):
+def _phase_worker(rank, world, port, db_path, ckpt_dir, max_steps, resume, q, cap=4,
+                  max_trials=MAX_TRIALS):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
-    torch.set_num_threads(2)
+    torch.set_num_threads(1)    # same BLAS reduction order whatever the world size
     from metaopt_amd.parallel.comm import init_from_env, shutdown
     comm = init_from_env(backend="gloo")
     storage = DocumentStorage(PickledDB(host=db_path)) if comm.is_root else None
     _, sweep = _make(storage, _data(), comm=comm, cap=cap, resume=resume,
-                     restore_algorithm=resume, ckpt_dir=ckpt_dir)
+                     restore_algorithm=resume, ckpt_dir=ckpt_dir, max_trials=max_trials)
     sweep.run(max_steps)
     sweep.close()
     q.put((rank, sweep.done, sweep.n_resumed, sweep.n_resume_missing))
     shutdown()
 
 
-def _run_phase(db_path, ckpt_dir, max_steps, resume, world=2, cap=4):
+def _run_phase(db_path, ckpt_dir, max_steps, resume, world=2, cap=4, max_trials=MAX_TRIALS):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_phase_worker,
-                         args=(r, world, port, db_path, ckpt_dir, max_steps, resume, q, cap))
+                         args=(r, world, port, db_path, ckpt_dir, max_steps, resume, q, cap,
+                               max_trials))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -86,13 +88,15 @@ def _run_phase(db_path, ckpt_dir, max_steps, resume, world=2, cap=4):
     return out
 
 
-def _outcome(db_path):
+def _outcome(db_path, max_trials=MAX_TRIALS, fidelities=None):
     storage = DocumentStorage(PickledDB(host=db_path))
     exp = build_experiment("resume-sweep", priors=PRIORS, algorithms=ALGO,
-                           max_trials=MAX_TRIALS, storage=storage)
+                           max_trials=max_trials, storage=storage)
     trials = storage.fetch_trials(exp)
     done = {t.id: t.objective.value for t in trials if t.status == "completed"}
     stati = sorted(t.status for t in trials)
+    if fidelities is not None:
+        fidelities.update(t.params_dict["/steps"] for t in trials if t.status == "completed")
     rungs = storage.get_algorithm_state(exp)["algorithm"]["rungs"]
     completed_rungs = [[(b, sorted((k, round(v[0], 12)) for k, v in r.items()
                                    if v[0] is not None)) for b, r in br] for br in rungs]
@@ -205,3 +209,49 @@ def test_two_rank_sweep_equals_one_rank_with_the_same_slots(tmp_path):
     for tid, obj in done1.items():
         assert done2[tid] == pytest.approx(obj, rel=1e-6, abs=1e-9), tid
     assert rungs1 == rungs2
+
+
+def test_eight_rank_sweep_equals_one_rank_with_the_same_slots(tmp_path):
+    """The 8-rank control path (placement over 8 ranks, C1/C5 at W=8, C4 copies between many
+    rank pairs, the writer child under 8 ranks' completions): 8 gloo ranks x 4 slots finish
+    the same trials with the same objectives and ASHA rungs as 1 rank x 32 slots."""
+    import collections
+    n = 160
+    one = str(tmp_path / "one.pkl")
+    eight = str(tmp_path / "eight.pkl")
+    assert all(r[1] for r in _run_phase(one, None, 100000, resume=False, world=1, cap=32,
+                                        max_trials=n))
+    out = _run_phase(eight, None, 100000, resume=False, world=8, cap=4, max_trials=n)
+    assert len(out) == 8 and all(r[1] for r in out)
+    fid = collections.Counter()
+    done1, _, rungs1 = _outcome(one, n)
+    done8, stati8, rungs8 = _outcome(eight, n, fid)
+    assert len(done1) == n and set(done1) == set(done8)
+    for tid, obj in done1.items():
+        assert done8[tid] == pytest.approx(obj, rel=1e-6, abs=1e-9), tid
+    assert rungs1 == rungs8
+    assert "reserved" not in stati8
+    # every ASHA rung was reached: promotions resumed from checkpoints (in place or over C4,
+    # spread over the 8 ranks), none lost its checkpoint on the way
+    assert fid[32] > 0 and fid[64] > 0
+    assert sum(r[2] for r in out) > 0 and sum(r[3] for r in out) == 0
+    assert sum(r[2] > 0 for r in out) >= 4
+
+
+def test_failed_sweep_close_releases_trials_without_collectives():
+    """close(failed=True) after an exception on one rank: no drain/spill collectives, the
+    in-flight trials are released (interrupted) and the watchdog stops."""
+    data = _data()
+    storage = DocumentStorage(EphemeralDB())
+    exp, sweep = _make(storage, data)
+    sweep.run(2 * 16)
+
+    def boom(*a, **k):
+        raise AssertionError("a collective ran during failed close")
+    sweep.drain = sweep.spill = boom
+    in_flight = [doc[0] for doc in sweep.trials.values()]
+    assert in_flight
+    sweep.close(failed=True)
+    by_id = {t.id: t.status for t in storage.fetch_trials(exp)}
+    assert all(by_id[tid] == "interrupted" for tid in in_flight)
+    assert "reserved" not in by_id.values()

@@ -229,6 +229,54 @@ def test_writer_process_mirrors_ephemeral_db():
     assert docs["t5"]["params"][0] == {"name": "/x", "type": "real", "value": 5.0}
 
 
+def test_writer_process_killed_child_falls_back_in_process():
+    """A writer child that dies (OOM kill, crash) never hangs flush/close: the writer notices,
+    switches to in-process writes and replays what the child had not acknowledged -- for an
+    in-memory database, every write (the child's copy died with it)."""
+    import datetime
+    from metaopt_amd.storage.protocol import DocumentStorage
+    from metaopt_amd.worker.writer import DocBuilder, WriterProcess, storage_spec
+    storage = DocumentStorage(EphemeralDB())
+    b = DocBuilder(7, ["/x"], ["real"])
+    w = WriterProcess(storage, b, storage_spec(storage), poll_s=0.1)
+    now = datetime.datetime.utcnow()
+    for i in range(20):
+        w.put_register_spec((f"t{i}", now, (float(i),), None))
+    w.flush()
+    w._proc.kill()
+    w._proc.join(timeout=10)
+    for i in range(20, 30):
+        w.put_register_spec((f"t{i}", now, (float(i),), None))
+    w.put_update_spec("t3", (0.5, 0.9, 0.7, now, now), was="reserved")
+    w.flush()                       # returns: the child is gone
+    assert w.failed
+    w.put_register_spec(("late", now, (99.0,), None))
+    w.close()
+    docs = {d["_id"]: d for d in storage.database.read("trials", {"experiment": 7})}
+    assert len(docs) == 31 and docs["t3"]["status"] == "completed"
+    assert docs["late"]["params"][0]["value"] == 99.0
+
+
+def test_writer_process_child_that_cannot_open_the_database(tmp_path):
+    """A child that fails at start-up (here: a PickledDB path whose parent is a file) is seen
+    as dead; the writes land through the parent's own storage."""
+    import datetime
+    from metaopt_amd.storage.protocol import DocumentStorage
+    from metaopt_amd.worker.writer import DocBuilder, WriterProcess
+    storage = DocumentStorage(EphemeralDB())
+    blocker = tmp_path / "file"
+    blocker.write_text("x")
+    b = DocBuilder(7, ["/x"], ["real"])
+    w = WriterProcess(storage, b, ("pickleddb", str(blocker / "sub" / "db.pkl")), poll_s=0.1)
+    now = datetime.datetime.utcnow()
+    for i in range(5):
+        w.put_register_spec((f"t{i}", now, (float(i),), None))
+    w.flush()
+    w.close()
+    assert w.failed
+    assert len(storage.database.read("trials", {"experiment": 7})) == 5
+
+
 def test_mongodb_uri_and_connection_errors(monkeypatch):
     """URI parsing (user, password, database, port) and server errors surfacing as
     DatabaseError (reference: src/orion/core/io/database/mongodb.py:30-86,272-295)."""
@@ -271,7 +319,8 @@ def test_pickleddb_older_format_is_upgraded(tmp_path, monkeypatch, capsys):
     monkeypatch.setattr(protocol, "_STORAGE", None)
     assert cli.main(["db", "upgrade", "-f"]) == 0
     out = capsys.readouterr().out
-    assert "Updating pickleddb scheme" in out and "converted to format 2" in out
+    assert "Updating pickleddb scheme" in out
+    assert "2 collection(s) converted to format 2" in out or "1 collection(s) converted" in out
     raw = pickle.loads(path.read_bytes())
     assert all(col.__getstate__()["format"] == 2 and not col.migrated
                for col in raw._db.values())
