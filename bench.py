@@ -30,8 +30,6 @@ import argparse
 import json
 import math
 import os
-import socket
-import subprocess
 import sys
 import time
 
@@ -69,49 +67,11 @@ def parse_args(argv=None):
 
 
 # ---------------------------------------------------------------------------------- launcher
-def _free_port() -> int:
-    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
 def launch(n: int, argv) -> int:
     """Start ``n`` rank processes of this script and wait for them (this process never touches
-    the GPU: it only counts devices, which does not initialise HIP on this image)."""
-    import torch
-    n_dev = torch.cuda.device_count()
-    env = dict(os.environ)
-    env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE=str(n),
-               LOCAL_WORLD_SIZE=str(n))
-    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    if 0 < n_dev < n:
-        # fewer GPUs than ranks: rehearse the multi-rank engine with ranks sharing the GPUs
-        env["MOPT_COMM_BACKEND"] = "gloo"
-        env["MOPT_BENCH_REHEARSAL"] = "1"
-    procs = []
-    for r in range(n):
-        e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=e))
-    code = 0
-    try:
-        pending = list(procs)
-        while pending:
-            for p in list(pending):
-                rc = p.poll()
-                if rc is None:
-                    continue
-                pending.remove(p)
-                if rc != 0 and code == 0:
-                    code = rc
-                    for q in pending:        # one rank failed: the others would hang
-                        q.terminate()
-            time.sleep(0.05)
-    finally:
-        for p in procs:
-            if p.poll() is None:
-                p.kill()
-                p.wait()
-    return code
+    the GPU; see metaopt_amd/parallel/launch.py)."""
+    from metaopt_amd.parallel.launch import spawn
+    return spawn(n, [os.path.abspath(__file__), *argv])
 
 
 # ---------------------------------------------------------------------------------- one rank

@@ -9,6 +9,7 @@ from __future__ import annotations
 import importlib
 import logging
 import pkgutil
+import re
 import sys
 
 from .base import ArgsParser
@@ -27,10 +28,35 @@ def load_modules_parser(parser: ArgsParser):
             mod.add_subparser(parser.get_subparsers())
 
 
+_ARGV: list = []
+_PRIOR_ARG = re.compile(r"^--?[^=~\s]+~")
+
+
+def current_argv() -> list:
+    """The argument list of the running ``main`` call (launchers re-run it per rank)."""
+    return [*_ARGV]     # (``list`` here is the cli.list sub-module once it is imported)
+
+
+def _space_after_options(argv):
+    """``mopt sweep ... --lr~'loguniform(..)'``: a sweep has no script, so its space starts at
+    the first ``--name~prior`` argument; a ``--`` there hands the rest to the user arguments."""
+    if "sweep" not in argv:
+        return argv
+    start = argv.index("sweep") + 1
+    for i in range(start, len(argv)):
+        if argv[i] == "--":
+            return argv
+        if _PRIOR_ARG.match(argv[i]):
+            return argv[:i] + ["--"] + argv[i:]
+    return argv
+
+
 def main(argv=None):
+    argv = [*(sys.argv[1:] if argv is None else argv)]
+    _ARGV[:] = argv
     parser = ArgsParser()
     load_modules_parser(parser)
-    rc = parser.execute(sys.argv[1:] if argv is None else argv)
+    rc = parser.execute(_space_after_options(argv))
     return rc or 0
 
 

@@ -1,18 +1,34 @@
 """``mopt sweep``: run an experiment's trials as device populations (one process per GPU).
 
-    mopt sweep -n mlp-asha --algo asha --population 256 --max-trials 2000
+    mopt sweep -n mlp-asha --task mlp --gpus 8 --max-trials 20000 \\
+        --lr~'loguniform(1e-4, 1)' --width~'loguniform(64, 512, discrete=True)' \\
+        --dropout~'uniform(0, 0.3)' --steps~'fidelity(32, 512, 4)'
+    mopt sweep -n mlp-asha --task mlp -c sweep.yaml        # algorithms / max_trials from a file
     torchrun --nproc-per-node 8 -m metaopt_amd sweep -n mlp-asha ...
 
-The experiment (space, algorithm, trials) lives in the configured database exactly like a
-``hunt`` experiment -- ``status``/``info``/``list`` work on it -- but trials are trained in-process
-on the GPU by :class:`~metaopt_amd.worker.population_sweep.PopulationSweep`.
+The search space is the user's, in the prior grammar of ``hunt`` (``--name~prior(...)`` after
+the options, or the task's default space when none is given): it is parsed by the same
+command-line parser, validated against the task's tunable hyper-parameters, stored with the
+experiment (so ``status`` / ``info`` / ``list`` and EVC branching work on it) and sampled by
+the algorithm.  The experiment configuration is resolved with the reference's precedence
+(defaults < environment < stored experiment < ``--config`` file < command line,
+``src/orion/core/io/experiment_builder.py:175-185``): a file's ``algorithms`` / ``max_trials``
+/ ``pool_size`` apply unless the command line sets them (``--algo`` / ``--max-trials``).
+
+``--gpus N`` (N > 1, outside torchrun) makes this process a launcher of N rank processes
+(``parallel/launch.py``, the launcher ``bench.py`` uses); ``--dtype`` picks the storage
+precision of the optimizer state (``bf16``: bf16 momentum / AdamW first moment; ``fp32``).
+Compute is bf16 MFMA with fp32 accumulation and an exact fp32 master either way.
 """
 from __future__ import annotations
 
 import json
 import logging
+import os
+import sys
 
-from .base import get_basic_args_group
+from .base import get_basic_args_group, get_user_args_group
+from .evc import get_branching_args_group
 
 log = logging.getLogger(__name__)
 
@@ -23,6 +39,8 @@ ALGOS = {"asha": lambda seed, n: {"asha": {"seed": seed, "repetitions": float("i
          "hyperband": lambda seed, n: {"hyperband": {"seed": seed}},
          "gridsearch": lambda seed, n: {"gridsearch": {"n_values": 4}}}
 
+DEFAULT_POPULATION = {"logreg": 64, "mlp": 256, "resnet20": 32, "lm-125m": 8, "lm-tiny": 16}
+
 
 def add_subparser(parser):
     from ..worker.tasks import TASKS
@@ -30,7 +48,11 @@ def add_subparser(parser):
     g = get_basic_args_group(p)
     g.add_argument("--task", default="mlp", choices=sorted(TASKS))
     g.add_argument("--algo", default=None, choices=sorted(ALGOS),
-                   help="search algorithm (default: the task's)")
+                   help="search algorithm (default: the --config file's, else the task's)")
+    g.add_argument("--gpus", type=int, default=1,
+                   help="ranks to launch, one per GPU (ignored under torchrun)")
+    g.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
+                   help="optimizer-state storage precision (compute: bf16 MFMA, fp32 accum)")
     g.add_argument("--population", type=int, default=None, help="trials per GPU")
     g.add_argument("--max-trials", type=int, default=None)
     g.add_argument("--steps", type=int, default=100000, help="max population steps")
@@ -49,15 +71,80 @@ def add_subparser(parser):
     g.add_argument("--watchdog", type=float, default=0.0,
                    help="seconds without a sync before the rank fails the job cleanly "
                         "(in-flight trials -> interrupted); 0 disables")
+    get_branching_args_group(p)
+    get_user_args_group(p)
     p.set_defaults(func=main)
     return p
 
 
-DEFAULT_POPULATION = {"logreg": 64, "mlp": 256, "resnet20": 32, "lm-125m": 8, "lm-tiny": 16}
+def _user_priors(user_args):
+    """The space of ``--name~prior`` user arguments (sweeps have no script: a leading token
+    that is not an option is refused)."""
+    from ..io.space_parser import SpaceCmdlineParser
+    args = list(user_args or [])
+    if args and args[0] == "--":
+        args = args[1:]
+    if not args:
+        return None, []
+    if not args[0].startswith("-"):
+        raise ValueError(f"mopt sweep trains in-process: no script expected, got '{args[0]}' "
+                         "(give the search space as --name~prior(...))")
+    parser = SpaceCmdlineParser()
+    parser.parse(args)
+    return dict(parser.priors), args
+
+
+def resolve(args: dict, world_size: int, population: int):
+    """(full experiment configuration, priors, user args): the reference's precedence, the
+    user's space or the task's, validated against the task."""
+    from ..io.experiment_builder import ExperimentBuilder
+    from ..space.builder import SpaceBuilder
+    from ..worker.tasks import get
+    spec = get(args["task"])
+    priors, user_args = _user_priors(args.get("user_args"))
+    if priors is None:
+        priors = dict(spec.priors)
+        user_args = [f"--{k.lstrip('/')}~{v}" for k, v in priors.items()]
+    space = SpaceBuilder().build(priors)
+    spec.check_space(space)
+    cmd = {k: args.get(k) for k in ("name", "user", "version", "config", "debug",
+                                    "manual_resolution", "auto_resolution", "branch",
+                                    "algorithm_change", "code_change_type", "cli_change_type",
+                                    "config_change_type")}
+    if args.get("max_trials") is not None:
+        cmd["max_trials"] = args["max_trials"]
+    if args.get("algo"):
+        cmd["algorithms"] = ALGOS[args["algo"]](args.get("seed", 0), population * world_size)
+    cmd["name"] = args.get("name")
+    builder = ExperimentBuilder()
+    full = builder.fetch_full_config(cmd, use_db=False)
+    file_algos = (builder.fetch_file_config(cmd) or {}).get("algorithms")
+    if args.get("algo"):          # an algorithm replaces, never merges with, the file's
+        full["algorithms"] = cmd["algorithms"]
+    elif not file_algos:
+        full["algorithms"] = spec.algorithm(args.get("seed", 0), population * world_size)
+    if full.get("name") is None:
+        full["name"] = f"sweep-{args['task']}"
+    full["pool_size"] = population * world_size
+    full.setdefault("metadata", {})["user_args"] = user_args
+    full["metadata"].pop("user_script", None)
+    return full, priors, builder
 
 
 def main(args):
-    from ..io.experiment_builder import ExperimentBuilder, build_experiment
+    if int(args.get("gpus") or 1) > 1 and "WORLD_SIZE" not in os.environ:
+        from ..parallel.launch import spawn
+        return spawn(int(args["gpus"]), ["-m", "metaopt_amd", *_argv()])
+    return run(args)
+
+
+def _argv():
+    """This invocation's command line (``mopt ...`` / ``python -m metaopt_amd ...``)."""
+    from . import current_argv
+    return current_argv()
+
+
+def run(args):
     from ..parallel.comm import init_from_env, shutdown
     from ..worker.population_sweep import PopulationSweep
     from ..worker.tasks import get
@@ -65,17 +152,19 @@ def main(args):
     comm = init_from_env()
     spec = get(args["task"])
     P = args["population"] or DEFAULT_POPULATION.get(args["task"], 64)
-    algo = (ALGOS[args["algo"]](args["seed"], P * comm.world_size) if args["algo"]
-            else spec.algorithm(args["seed"], P * comm.world_size))
-    task, pop, data = spec.build(P, comm.device, args["seed"])
     experiment = None
+    priors = None
     if comm.is_root:
-        builder = ExperimentBuilder()
-        builder.setup_storage({"debug": args.get("debug"), "database": {}})
-        experiment = build_experiment(args["name"] or f"sweep-{args['task']}",
-                                      priors=dict(task.priors), algorithms=algo,
-                                      max_trials=args["max_trials"] or float("inf"),
-                                      pool_size=P * comm.world_size)
+        full, priors, builder = resolve(args, comm.world_size, P)
+        if args.get("debug"):
+            full["debug"] = True
+        builder.setup_storage(full)
+        experiment = builder.build_from_config(full)
+        priors = dict(experiment.configuration["metadata"]["priors"])
+    # every rank builds its population for the same (stored) space
+    priors = comm.broadcast_object(priors)
+    task, pop, data = spec.build(P, comm.device, args["seed"], priors=priors,
+                                 state_dtype=args.get("dtype", "bf16"))
     events = watchdog = None
     if args.get("event_log"):
         from ..utils.events import EventLog
@@ -106,6 +195,9 @@ def main(args):
     if events is not None:
         events.close()
     if comm.is_root:
-        print(json.dumps({k: v for k, v in summary.items()}, default=str))
+        summary["experiment"] = {"name": experiment.name, "version": experiment.version,
+                                 "space": priors, "algorithms": experiment.configuration[
+                                     "algorithms"], "world_size": comm.world_size}
+        print(json.dumps(summary, default=str), flush=True)
     shutdown()
     return 0

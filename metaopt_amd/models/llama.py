@@ -92,7 +92,10 @@ class PopulationLM(FlatPopulation):
 
     def __init__(self, capacity: int, config="tiny-2layer", batch_size: int = 8,
                  seq_len: Optional[int] = None, device="cuda", max_grad_norm: float = 1.0,
-                 eval_batch: Optional[int] = None, use_graph: bool = True):
+                 eval_batch: Optional[int] = None, use_graph: bool = True,
+                 moment_dtype: Optional[torch.dtype] = None):
+        if moment_dtype is not None:       # AdamW first-moment storage (mopt sweep --dtype)
+            self.moment_dtype = moment_dtype
         self.cfg = PRESETS[config] if isinstance(config, str) else config
         if seq_len is not None:
             self.cfg = dataclasses.replace(self.cfg, seq_len=seq_len)

@@ -64,6 +64,7 @@ class MLPSweepTask:
     in_features: int = 784
     num_classes: int = 10
     max_width: int = 1024
+    steps: int = 256          # budget of every trial when the space has no /steps fidelity
 
     def member_config(self, params: Dict, seed: int) -> MemberConfig:
         return MemberConfig(
@@ -86,7 +87,7 @@ class MLPSweepTask:
                 int(seed) & 0x7FFFFFFF)
 
     def budget(self, params: Dict) -> int:
-        return int(params[self.fidelity])
+        return int(params.get(self.fidelity, self.steps))
 
     def key(self, params: Dict) -> str:
         return param_key(params, self.fidelity)
