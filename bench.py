@@ -121,8 +121,7 @@ def run_rank(args) -> None:
             torch.cuda.synchronize()
 
     def interval():
-        for _ in range(S):
-            sweep.step()         # the last step of the interval runs the sync
+        sweep.run_interval()     # S optimizer steps queued in one host call, then the sync
 
     sweep.start()
     for _ in range(args.warmup):

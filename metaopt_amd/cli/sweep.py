@@ -95,18 +95,13 @@ def _user_priors(user_args):
 
 
 def resolve(args: dict, world_size: int, population: int):
-    """(full experiment configuration, priors, user args): the reference's precedence, the
-    user's space or the task's, validated against the task."""
+    """(full experiment configuration, priors, builder): the reference's precedence (the
+    stored experiment of that name included), the user's space -- else the stored one, else
+    the task's -- validated against the task."""
     from ..io.experiment_builder import ExperimentBuilder
     from ..space.builder import SpaceBuilder
     from ..worker.tasks import get
     spec = get(args["task"])
-    priors, user_args = _user_priors(args.get("user_args"))
-    if priors is None:
-        priors = dict(spec.priors)
-        user_args = [f"--{k.lstrip('/')}~{v}" for k, v in priors.items()]
-    space = SpaceBuilder().build(priors)
-    spec.check_space(space)
     cmd = {k: args.get(k) for k in ("name", "user", "version", "config", "debug",
                                     "manual_resolution", "auto_resolution", "branch",
                                     "algorithm_change", "code_change_type", "cli_change_type",
@@ -115,16 +110,29 @@ def resolve(args: dict, world_size: int, population: int):
         cmd["max_trials"] = args["max_trials"]
     if args.get("algo"):
         cmd["algorithms"] = ALGOS[args["algo"]](args.get("seed", 0), population * world_size)
-    cmd["name"] = args.get("name")
+    if cmd["name"] is None:
+        cmd["name"] = f"sweep-{args['task']}"
     builder = ExperimentBuilder()
-    full = builder.fetch_full_config(cmd, use_db=False)
+    if args.get("debug"):
+        builder.setup_storage({"debug": True})
+    full = builder.fetch_full_config(cmd)
+    stored = builder.fetch_config_from_db(cmd) or {}
+    priors, user_args = _user_priors(args.get("user_args"))
+    if priors is None:
+        md = stored.get("metadata", {}) or {}
+        if md.get("user_args") is not None and md.get("priors"):
+            priors, user_args = dict(md["priors"]), list(md["user_args"])
+        else:
+            priors = dict(spec.priors)
+            user_args = [f"--{k.lstrip('/')}~{v}" for k, v in priors.items()]
+    spec.check_space(SpaceBuilder().build(priors))
     file_algos = (builder.fetch_file_config(cmd) or {}).get("algorithms")
     if args.get("algo"):          # an algorithm replaces, never merges with, the file's
         full["algorithms"] = cmd["algorithms"]
-    elif not file_algos:
+    elif file_algos:
+        full["algorithms"] = file_algos
+    elif not stored.get("algorithms"):
         full["algorithms"] = spec.algorithm(args.get("seed", 0), population * world_size)
-    if full.get("name") is None:
-        full["name"] = f"sweep-{args['task']}"
     full["pool_size"] = population * world_size
     full.setdefault("metadata", {})["user_args"] = user_args
     full["metadata"].pop("user_script", None)
@@ -156,9 +164,6 @@ def run(args):
     priors = None
     if comm.is_root:
         full, priors, builder = resolve(args, comm.world_size, P)
-        if args.get("debug"):
-            full["debug"] = True
-        builder.setup_storage(full)
         experiment = builder.build_from_config(full)
         priors = dict(experiment.configuration["metadata"]["priors"])
     # every rank builds its population for the same (stored) space

@@ -38,6 +38,8 @@ _SIGNATURES = {
     "mopt_mlp_bwd": ([c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                       c_void_p, c_void_p, c_int, c_int, c_void_p], c_int),
     "mopt_mlp_step": ([c_void_p, c_void_p, c_void_p, c_void_p], c_int),
+    "mopt_mlp_steps": ([c_void_p, c_void_p, c_void_p, c_int, c_void_p], c_int),
+    "mopt_mlp_set_bwd_prefetch": ([c_int], c_int),
 }
 
 _OPTIONAL_SIGNATURES: dict = {}

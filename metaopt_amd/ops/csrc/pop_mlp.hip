@@ -336,7 +336,7 @@ __global__ __launch_bounds__(256) void mlp_fwd_ce_kernel(const MlpTL* __restrict
 //   W, M (, V) <- optimizer(W, M, dW)                       (dW^T C-layout = 4 consecutive k/lane)
 // One LDS image per operand serves both row reads and ds_read_b64_tr_b16 transposed reads.
 // ----------------------------------------------------------------------------------------------
-template <int OPT>
+template <int OPT, bool PF>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void mlp_bwd_opt_kernel(const MlpTL* __restrict__ tls,
                                                           const int2* __restrict__ work, int n_work,
                                                           const bf16_t* __restrict__ xb,
@@ -394,72 +394,87 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
     for (int j = 0; j < 4; ++j) dx[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // Chunk operands are loaded at the top of each chunk (a one-chunk-ahead register prefetch
-  // measured no faster and pushes the kernel to one wave per SIMD); latency is hidden by the
-  // second workgroup per CU.  Staging lives in named registers, never in arrays captured by a
-  // lambda (see fwd_gemm).
+  // Chunk operands (dZ rows, W hi/lo, momentum) live in named registers, never in arrays
+  // captured by a lambda (see fwd_gemm).  PF (prefetch): the operands of chunk c+1 are loaded
+  // into a second register set right after chunk c's operands reached LDS / f32 registers, so
+  // every workgroup keeps two chunks of HBM traffic in flight across its MFMA + update phase
+  // (without it the loads of a chunk are exposed at the top of the chunk and only the second
+  // workgroup per CU hides them).
   const int zo0 = (tid >> 3) * N + (tid & 7) * 8, zo1 = ((tid + 256) >> 3) * N + (tid & 7) * 8;
   const int zo2 = ((tid + 512) >> 3) * N + (tid & 7) * 8, zo3 = ((tid + 768) >> 3) * N + (tid & 7) * 8;
   bf16_t* zs0 = Zs + (tid >> 3) * LS + (tid & 7) * 8;
   // Optimizer-state layout: thread -> rows 16i + tid/16 (i < 4), 4 consecutive k at 4 * (tid % 16):
   // every wave-instruction moves 4 rows x 256 contiguous bytes of W/M (/V), full 128-B lines.
   const int wo = (tid >> 4) * K + k0 + 4 * (tid & 15);
-  uint4 z0, z1, z2, z3;
-  f32x4 m0, m1, m2, m3, v0, v1, v2, v3;
-  uint2 wh0, wh1, wh2, wh3, wl0, wl1, wl2, wl3;       // master weights: hi (bf16) and lo halves
-  uint2 h0, h1, h2, h3;                               // kSGD16 momentum (4 bf16 per lane)
-#define MOPT_BWD_LOAD(NC)                                                                        \
+  uint4 cz0, cz1, cz2, cz3, nz0, nz1, nz2, nz3;
+  f32x4 cm0, cm1, cm2, cm3, cv0, cv1, cv2, cv3, nm0, nm1, nm2, nm3, nv0, nv1, nv2, nv3;
+  uint2 cwh0, cwh1, cwh2, cwh3, cwl0, cwl1, cwl2, cwl3;   // master weights: hi (bf16), lo halves
+  uint2 nwh0, nwh1, nwh2, nwh3, nwl0, nwl1, nwl2, nwl3;
+  uint2 ch0, ch1, ch2, ch3, nh0, nh1, nh2, nh3;           // kSGD16 momentum (4 bf16 per lane)
+#define MOPT_BWD_LOAD(NC, P)                                                                     \
   {                                                                                              \
-    const bf16_t* zc = dZ + (NC);                                                                \
-    z0 = *(const uint4*)(zc + zo0);                                                              \
-    z1 = *(const uint4*)(zc + zo1);                                                              \
-    z2 = *(const uint4*)(zc + zo2);                                                              \
-    z3 = *(const uint4*)(zc + zo3);                                                              \
+    const bf16_t* zc_ = dZ + (NC);                                                               \
+    P##z0 = *(const uint4*)(zc_ + zo0);                                                          \
+    P##z1 = *(const uint4*)(zc_ + zo1);                                                          \
+    P##z2 = *(const uint4*)(zc_ + zo2);                                                          \
+    P##z3 = *(const uint4*)(zc_ + zo3);                                                          \
     const size_t ob = (size_t)(NC) * K + wo;                                                     \
-    wh0 = *(const uint2*)(W16 + ob);                                                             \
-    wh1 = *(const uint2*)(W16 + ob + 16 * K);                                                    \
-    wh2 = *(const uint2*)(W16 + ob + 32 * K);                                                    \
-    wh3 = *(const uint2*)(W16 + ob + 48 * K);                                                    \
-    wl0 = *(const uint2*)(WLO + ob);                                                             \
-    wl1 = *(const uint2*)(WLO + ob + 16 * K);                                                    \
-    wl2 = *(const uint2*)(WLO + ob + 32 * K);                                                    \
-    wl3 = *(const uint2*)(WLO + ob + 48 * K);                                                    \
+    P##wh0 = *(const uint2*)(W16 + ob);                                                          \
+    P##wh1 = *(const uint2*)(W16 + ob + 16 * K);                                                 \
+    P##wh2 = *(const uint2*)(W16 + ob + 32 * K);                                                 \
+    P##wh3 = *(const uint2*)(W16 + ob + 48 * K);                                                 \
+    P##wl0 = *(const uint2*)(WLO + ob);                                                          \
+    P##wl1 = *(const uint2*)(WLO + ob + 16 * K);                                                 \
+    P##wl2 = *(const uint2*)(WLO + ob + 32 * K);                                                 \
+    P##wl3 = *(const uint2*)(WLO + ob + 48 * K);                                                 \
     if (OPT == kSGD16) {                                                                         \
-      h0 = *(const uint2*)(M16 + ob);                                                            \
-      h1 = *(const uint2*)(M16 + ob + 16 * K);                                                   \
-      h2 = *(const uint2*)(M16 + ob + 32 * K);                                                   \
-      h3 = *(const uint2*)(M16 + ob + 48 * K);                                                   \
+      P##h0 = *(const uint2*)(M16 + ob);                                                         \
+      P##h1 = *(const uint2*)(M16 + ob + 16 * K);                                                \
+      P##h2 = *(const uint2*)(M16 + ob + 32 * K);                                                \
+      P##h3 = *(const uint2*)(M16 + ob + 48 * K);                                                \
     } else {                                                                                     \
-      m0 = *(const f32x4*)(M32 + ob);                                                            \
-      m1 = *(const f32x4*)(M32 + ob + 16 * K);                                                   \
-      m2 = *(const f32x4*)(M32 + ob + 32 * K);                                                   \
-      m3 = *(const f32x4*)(M32 + ob + 48 * K);                                                   \
+      P##m0 = *(const f32x4*)(M32 + ob);                                                         \
+      P##m1 = *(const f32x4*)(M32 + ob + 16 * K);                                                \
+      P##m2 = *(const f32x4*)(M32 + ob + 32 * K);                                                \
+      P##m3 = *(const f32x4*)(M32 + ob + 48 * K);                                                \
     }                                                                                            \
     if (OPT == kAdamW) {                                                                         \
-      v0 = *(const f32x4*)(V32 + ob);                                                            \
-      v1 = *(const f32x4*)(V32 + ob + 16 * K);                                                   \
-      v2 = *(const f32x4*)(V32 + ob + 32 * K);                                                   \
-      v3 = *(const f32x4*)(V32 + ob + 48 * K);                                                   \
+      P##v0 = *(const f32x4*)(V32 + ob);                                                         \
+      P##v1 = *(const f32x4*)(V32 + ob + 16 * K);                                                \
+      P##v2 = *(const f32x4*)(V32 + ob + 32 * K);                                                \
+      P##v3 = *(const f32x4*)(V32 + ob + 48 * K);                                                \
     }                                                                                            \
   }
+#define MOPT_BWD_ADVANCE()                                                                       \
+  {                                                                                              \
+    cz0 = nz0; cz1 = nz1; cz2 = nz2; cz3 = nz3;                                                  \
+    cwh0 = nwh0; cwh1 = nwh1; cwh2 = nwh2; cwh3 = nwh3;                                          \
+    cwl0 = nwl0; cwl1 = nwl1; cwl2 = nwl2; cwl3 = nwl3;                                          \
+    if (OPT == kSGD16) { ch0 = nh0; ch1 = nh1; ch2 = nh2; ch3 = nh3; }                           \
+    else { cm0 = nm0; cm1 = nm1; cm2 = nm2; cm3 = nm3; }                                         \
+    if (OPT == kAdamW) { cv0 = nv0; cv1 = nv1; cv2 = nv2; cv3 = nv3; }                           \
+  }
+  MOPT_BWD_LOAD(0, c)
   for (int nc = 0; nc < N; nc += BN) {
-    MOPT_BWD_LOAD(nc)
     // ---- this chunk's operands -> LDS (dZ row-major; W^T image as bf16 for the dX MFMAs) ----
-    *(uint4*)(zs0) = z0;
-    *(uint4*)(zs0 + 32 * LS) = z1;
-    *(uint4*)(zs0 + 64 * LS) = z2;
-    *(uint4*)(zs0 + 96 * LS) = z3;
+    *(uint4*)(zs0) = cz0;
+    *(uint4*)(zs0 + 32 * LS) = cz1;
+    *(uint4*)(zs0 + 64 * LS) = cz2;
+    *(uint4*)(zs0 + 96 * LS) = cz3;
     if (OPT == kSGD16) {
-      m0 = bf4_to_f32(h0); m1 = bf4_to_f32(h1); m2 = bf4_to_f32(h2); m3 = bf4_to_f32(h3);
+      cm0 = bf4_to_f32(ch0); cm1 = bf4_to_f32(ch1); cm2 = bf4_to_f32(ch2); cm3 = bf4_to_f32(ch3);
     }
-    const f32x4 w[4] = {join4(wh0, wl0), join4(wh1, wl1), join4(wh2, wl2), join4(wh3, wl3)};
-    const f32x4 m[4] = {m0, m1, m2, m3};
+    const f32x4 w[4] = {join4(cwh0, cwl0), join4(cwh1, cwl1), join4(cwh2, cwl2),
+                        join4(cwh3, cwl3)};
+    const f32x4 m[4] = {cm0, cm1, cm2, cm3};
     f32x4 v[4];
     if (OPT == kAdamW) {
-      v[0] = v0; v[1] = v1; v[2] = v2; v[3] = v3;
+      v[0] = cv0; v[1] = cv1; v[2] = cv2; v[3] = cv3;
     }
+    const uint2 wh[4] = {cwh0, cwh1, cwh2, cwh3};
+    const bool more = nc + BN < N;
+    if (PF && more) MOPT_BWD_LOAD(nc + BN, n)
     if (has_dx) {   // the bf16 working copy (hi) is the dX operand, as in the forward
-      const uint2 wh[4] = {wh0, wh1, wh2, wh3};
 #pragma unroll
       for (int i = 0; i < 4; ++i) *(uint2*)(Ws + (16 * i + (tid >> 4)) * LS + 4 * (tid & 15)) = wh[i];
     }
@@ -587,8 +602,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       }
     }
     __syncthreads();
+    if (more) {
+      if (PF) MOPT_BWD_ADVANCE()
+      else MOPT_BWD_LOAD(nc + BN, c)
+    }
   }
 #undef MOPT_BWD_LOAD
+#undef MOPT_BWD_ADVANCE
 
   if (!has_dx) return;
   // ---- dZ of the layer below: dX * relu'(.) * dropout mask, both read off X (X > 0) ----
@@ -648,6 +668,30 @@ __global__ __launch_bounds__(256) void mlp_init_kernel(const InitDesc* __restric
   }
 }
 
+// Backward chunk prefetch (PF) on/off: A/B switch of the fused backward, on by default
+// (mopt_mlp_set_bwd_prefetch; MOPT_BWD_PREFETCH=0 in metaopt_amd/ops/population.py).
+static int g_bwd_prefetch = 1;
+
+template <int OPT, bool PF>
+static void launch_bwd(int n_work, hipStream_t stream, const void* tls, const void* work,
+                       const void* xb, void* grad, void* plo, void* p16, void* m32, void* v32,
+                       const void* hp, int flags) {
+  hipLaunchKernelGGL((mlp_bwd_opt_kernel<OPT, PF>), dim3(n_work), dim3(256), 0, stream,
+                     (const MlpTL*)tls, (const int2*)work, n_work, (const bf16_t*)xb,
+                     (bf16_t*)grad, (bf16_t*)plo, (bf16_t*)p16, (float*)m32, (float*)v32,
+                     (const TrialHP*)hp, flags);
+}
+
+template <int OPT>
+static void launch_bwd_pf(int n_work, hipStream_t stream, const void* tls, const void* work,
+                          const void* xb, void* grad, void* plo, void* p16, void* m32, void* v32,
+                          const void* hp, int flags) {
+  if (g_bwd_prefetch)
+    launch_bwd<OPT, true>(n_work, stream, tls, work, xb, grad, plo, p16, m32, v32, hp, flags);
+  else
+    launch_bwd<OPT, false>(n_work, stream, tls, work, xb, grad, plo, p16, m32, v32, hp, flags);
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------------------------
@@ -694,26 +738,22 @@ int mopt_mlp_fwd_ce(const void* tls, const void* work, int n_work, int n_rowbloc
   return (int)hipGetLastError();
 }
 
+int mopt_mlp_set_bwd_prefetch(int on) {
+  g_bwd_prefetch = on ? 1 : 0;
+  return 0;
+}
+
 int mopt_mlp_bwd(const void* tls, const void* work, int n_work, const void* xb, void* grad,
                  void* plo, void* p16, void* m32, void* v32, const void* hp, int opt, int flags,
                  void* stream) {
   if (n_work <= 0) return 0;
-  if (opt == kAdamW) {
-    hipLaunchKernelGGL(mlp_bwd_opt_kernel<kAdamW>, dim3(n_work), dim3(256), 0, (hipStream_t)stream,
-                       (const MlpTL*)tls, (const int2*)work, n_work, (const bf16_t*)xb,
-                       (bf16_t*)grad, (bf16_t*)plo, (bf16_t*)p16, (float*)m32, (float*)v32,
-                       (const TrialHP*)hp, flags);
-  } else if (opt == kSGD16) {
-    hipLaunchKernelGGL(mlp_bwd_opt_kernel<kSGD16>, dim3(n_work), dim3(256), 0, (hipStream_t)stream,
-                       (const MlpTL*)tls, (const int2*)work, n_work, (const bf16_t*)xb,
-                       (bf16_t*)grad, (bf16_t*)plo, (bf16_t*)p16, (float*)m32, (float*)v32,
-                       (const TrialHP*)hp, flags);
-  } else {
-    hipLaunchKernelGGL(mlp_bwd_opt_kernel<kSGD>, dim3(n_work), dim3(256), 0, (hipStream_t)stream,
-                       (const MlpTL*)tls, (const int2*)work, n_work, (const bf16_t*)xb,
-                       (bf16_t*)grad, (bf16_t*)plo, (bf16_t*)p16, (float*)m32, (float*)v32,
-                       (const TrialHP*)hp, flags);
-  }
+  hipStream_t st = (hipStream_t)stream;
+  if (opt == kAdamW)
+    launch_bwd_pf<kAdamW>(n_work, st, tls, work, xb, grad, plo, p16, m32, v32, hp, flags);
+  else if (opt == kSGD16)
+    launch_bwd_pf<kSGD16>(n_work, st, tls, work, xb, grad, plo, p16, m32, v32, hp, flags);
+  else
+    launch_bwd_pf<kSGD>(n_work, st, tls, work, xb, grad, plo, p16, m32, v32, hp, flags);
   return (int)hipGetLastError();
 }
 
@@ -752,6 +792,18 @@ int mopt_mlp_step(const MlpStep* s, const void* x, const void* y, void* stream) 
     if (l > 0) flags |= kHasDx | (s->drop ? kInDropout : 0);
     err = mopt_mlp_bwd(s->tls, s->bwd[l], s->n_bwd[l], l == 0 ? x : s->act, s->grad, s->plo,
                        s->p16, s->m32, s->v32, s->hp, s->opt, flags, stream);
+    if (err) return err;
+  }
+  return 0;
+}
+
+// ``n`` consecutive train steps of a group in ONE host call (step i reads batch xs[i] / ys[i]):
+// the sweep queues a whole sync interval with it, so the per-step host cost is the launches alone.
+int mopt_mlp_steps(const MlpStep* s, const void* const* xs, const void* const* ys, int n,
+                   void* stream) {
+  if (n < 0 || (n > 0 && (xs == nullptr || ys == nullptr))) return (int)hipErrorInvalidValue;
+  for (int i = 0; i < n; ++i) {
+    const int err = mopt_mlp_step(s, xs[i], ys[i], stream);
     if (err) return err;
   }
   return 0;

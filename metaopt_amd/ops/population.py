@@ -187,6 +187,8 @@ class PopulationMLP:
                 raise ValueError("the hip backend needs a GPU device")
             from . import _lib
             self._lib = _lib.get_lib()  # raises loudly: no silent fallback on a GPU box
+            # backward chunk prefetch (csrc/pop_mlp.hip PF): on unless MOPT_BWD_PREFETCH=0
+            self._lib.mopt_mlp_set_bwd_prefetch(int(os.environ.get("MOPT_BWD_PREFETCH", "1")))
         self.backend = backend
         # the population's trials are split into ``n_streams`` groups of equal cost whose train
         # steps run on their own HIP streams, unsynchronised between syncs: one group's
@@ -783,6 +785,46 @@ class PopulationMLP:
             self._train_step_hip(x, y)     # advances the device step counters itself
         else:
             self._train_step_torch(x, y)
+
+    def train_steps(self, batches) -> None:
+        """``len(batches)`` consecutive steps (``batches`` = [(x, y)] of the interval): on the
+        HIP backend one host call per trial group queues them all (``mopt_mlp_steps``), so the
+        per-step host cost is the kernel launches alone; otherwise :meth:`train_step` each."""
+        if self.backend != "hip" or _lib_sync_check() or len(batches) <= 1:
+            for x, y in batches:
+                self.train_step(x, y)
+            return
+        self._refresh()
+        n = len(batches)
+        xs = np.empty(n, dtype=np.uint64)
+        ys = np.empty(n, dtype=np.uint64)
+        keep = []
+        for i, (x, y) in enumerate(batches):
+            if x.shape != (self.batch_size, self.K0):
+                raise ValueError(f"x must be [{self.batch_size}, {self.K0}] (padded), got "
+                                 f"{tuple(x.shape)}")
+            if not x.is_contiguous():
+                x = x.contiguous()
+                keep.append(x)
+            xs[i], ys[i] = x.data_ptr(), y.data_ptr()
+        self.hp["t"][self._active_np] += n
+        from ._lib import check
+        lib, main = self._lib, torch.cuda.current_stream(self.device)
+        if self.batch_size // 128 != 1:
+            raise ValueError("train_steps needs 128-row batches")
+        parts = self._parts
+        if len(parts) > 1:
+            if self._fork_needed:
+                ev = self._events[0]
+                ev.record(main)
+                for side in self._side_streams[:len(parts) - 1]:
+                    side.wait_event(ev)
+                self._fork_needed = False
+            self._side_pending = True
+        for i, part in enumerate(parts):
+            stream = main if i == 0 else self._side_streams[i - 1]
+            check(lib.mopt_mlp_steps(part["step_ptr"], xs.ctypes.data, ys.ctypes.data, n,
+                                     stream.cuda_stream), "mlp_steps")
 
     def _train_step_hip(self, x, y) -> None:
         from ._lib import check

@@ -236,13 +236,51 @@ class PopulationSweep:
                 self._mark("sync")
             self._sync()
 
+    def run_interval(self, max_steps: Optional[int] = None) -> int:
+        """Train up to the next sync boundary (at most ``max_steps`` steps) with the steps
+        queued in one host call per trial group where the population supports it, then sync
+        if the boundary was reached.  Returns the number of steps taken."""
+        if not self._started:
+            self.start()
+        if self.done:
+            return 0
+        S = self.sync_every
+        left = S - self.global_step % S
+        n = left if max_steps is None else min(left, int(max_steps))
+        if n <= 0:
+            return 0
+        multi = getattr(self.pop, "train_steps", None)
+        if multi is None:
+            for _ in range(n):
+                self.step()
+            return n
+        t0 = time.perf_counter()
+        if self._timeline is not None and self.global_step % S == 0:
+            self._mark("interval")
+        # the writes drained at the sync stop once the GPU gets this close to the boundary
+        tail = min(2, S - 1) if (self.pipelined and n == left) else 0
+        head = n - tail
+        for count in (head, tail):
+            if count <= 0:
+                continue
+            multi([self.data.batch(self.global_step + i) for i in range(count)])
+            self.global_step += count
+            self.samples += self.pop.batch_size * self._n_active * count
+            if count == head and tail:
+                self._busy_marker = self.pop.device_busy()
+        self.timers["launch"] += time.perf_counter() - t0
+        if self.global_step % S == 0:
+            if self._timeline is not None:
+                self._mark("sync")
+            self._sync()
+        return n
+
     def run(self, max_steps: int) -> dict:
         if not self._started:
             self.start()
-        for _ in range(max_steps):
-            if self.done:
-                break
-            self.step()
+        taken = 0
+        while taken < max_steps and not self.done:
+            taken += self.run_interval(max_steps - taken)
         return self.summary()
 
     # ------------------------------------------------------------------ sync

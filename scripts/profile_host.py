@@ -10,7 +10,7 @@ import bench  # noqa: E402
 out = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/host_profile.txt"
 prof = cProfile.Profile()
 prof.enable()
-bench.main(["--steps", "320", "--warmup", "64"])
+bench.main(["--steps", "60", "--warmup", "10"])
 prof.disable()
 with open(out, "w") as f:
     st = pstats.Stats(prof, stream=f)
