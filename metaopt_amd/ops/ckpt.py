@@ -93,9 +93,17 @@ def multi_copy(items: Iterable[Tuple[torch.Tensor, torch.Tensor, Optional[torch.
             d16, dlo = 0, 0
         descs[i] = (s32, 0 if dst is None else dst.data_ptr(), d16, n, s16, slo, dlo, 0)
         counts.append((n + CHUNK - 1) // CHUNK)
-    counts = np.array(counts, dtype=np.int64)
+    launch_descs(descs, dev)
+
+
+def launch_descs(descs: np.ndarray, dev) -> None:
+    """One ``mopt_multi_copy`` launch over a prebuilt DESC_DTYPE array (raw device pointers;
+    the callers build it with numpy -- no per-item tensor views)."""
+    if not len(descs):
+        return
+    counts = (descs["n"].astype(np.int64) + CHUNK - 1) // CHUNK
     chunks = np.zeros(int(counts.sum()), dtype=CHUNK_DTYPE)
-    chunks["desc"] = np.repeat(np.arange(len(items), dtype=np.int32), counts)
+    chunks["desc"] = np.repeat(np.arange(len(descs), dtype=np.int32), counts)
     first = np.concatenate([[0], np.cumsum(counts)[:-1]])
     chunks["start"] = (np.arange(len(chunks)) - np.repeat(first, counts)) * CHUNK
     d = _lib.upload_bytes(descs, dev)

@@ -22,6 +22,26 @@ typedef uint16_t bf16_t;  // storage type of a bf16 element
 
 constexpr int kLdsStride = 72;  // bf16 elements per LDS tile row (64 + 8 pad)
 
+// 64-column bf16 LDS tiles with 128-B rows whose 16-B chunks are XOR-swizzled by row:
+// chunk' = chunk ^ swz_row(row), swz_row = (r0^r1^r2^r3^r4, r0^r1^r2^r3, r0^r3) over the row's
+// low 5 bits.  Found by scripts/lds_banks.py: conflict-free for every LDS access of the
+// population-MLP kernels -- 16-B staging stores, ds_read_b128 fragment reads (4 non-contiguous
+// 16-lane groups), ds_read_b64_tr_b16 transposed reads (32-lane halves) and the 2-B epilogue
+// stores -- where the 8-element row pad cost 2-4 extra cycles per fragment / transposed read.
+__device__ __forceinline__ int swz_row(int r) {
+  const int p = (r ^ (r >> 1) ^ (r >> 2) ^ (r >> 3)) & 1;
+  return (p ^ ((r >> 4) & 1)) | (p << 1) | (((r ^ (r >> 3)) & 1) << 2);
+}
+// element offset of (row, col) in a swizzled 64-column tile
+__device__ __forceinline__ int tile_off(int r, int c) {
+  return r * 64 + ((((c >> 3) ^ swz_row(r)) & 7) << 3) + (c & 7);
+}
+// 64-column f32 tile, 256-B rows, 16-B chunks XOR-swizzled by (row & 15): conflict-free for
+// column-fragment stores (rows = lanes) and row-contiguous reads
+__device__ __forceinline__ int ftile_off(int r, int c) {
+  return r * 64 + ((((c >> 2) ^ r) & 15) << 2) + (c & 3);
+}
+
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 __device__ __forceinline__ float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }

@@ -63,7 +63,20 @@ namespace {
 constexpr int BM = 128;  // rows (batch) per workgroup
 constexpr int BN = 64;   // output features per forward tile / per backward chunk
 constexpr int BK = 64;   // reduction step of the forward, width of a backward k-strip
-constexpr int LS = kLdsStride;
+// LDS tile layout (A/B switch, -DMOPT_MLP_SWZ=0|1): 1 = 128-B rows with the row-XOR chunk
+// swizzle of common.h (bank-conflict free, scripts/lds_banks.py); 0 = rows padded to 72 bf16.
+#ifndef MOPT_MLP_SWZ
+#define MOPT_MLP_SWZ 0
+#endif
+#if MOPT_MLP_SWZ
+constexpr int TS = 64;
+#define TOFF(r, c) tile_off((r), (c))
+#define FOFF(r, c) ftile_off((r), (c))
+#else
+constexpr int TS = kLdsStride;
+#define TOFF(r, c) ((r) * TS + (c))
+#define FOFF(r, c) ((r) * (BN + 4) + (c))
+#endif
 
 // kStoreStats: one row block per trial -- store the trial's loss / #correct instead of
 // accumulating atomically into zeroed counters (saves the per-step zero-fill launch).
@@ -113,9 +126,9 @@ __device__ __forceinline__ void fwd_step(const bf16_t* As, const bf16_t* Bs, int
   for (int ks = 0; ks < BK / 32; ++ks) {
     bf16x8 a[2], b[4];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) a[i] = lds_frag(As + (wave * 32 + i * 16 + li) * LS + ks * 32 + g * 8);
+    for (int i = 0; i < 2; ++i) a[i] = lds_frag(As + TOFF(wave * 32 + i * 16 + li, ks * 32 + g * 8));
 #pragma unroll
-    for (int j = 0; j < 4; ++j) b[j] = lds_frag(Bs + (j * 16 + li) * LS + ks * 32 + g * 8);
+    for (int j = 0; j < 4; ++j) b[j] = lds_frag(Bs + TOFF(j * 16 + li, ks * 32 + g * 8));
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -135,12 +148,12 @@ __device__ __forceinline__ void fwd_gemm(const bf16_t* __restrict__ X, const bf1
   const int c0 = tid, c1 = tid + 256, c2 = tid + 512, c3 = tid + 768;
   const int g0 = (c0 >> 3) * K + (c0 & 7) * 8, g1 = (c1 >> 3) * K + (c1 & 7) * 8;
   const int g2 = (c2 >> 3) * K + (c2 & 7) * 8, g3 = (c3 >> 3) * K + (c3 & 7) * 8;
-  bf16_t* as0 = As + (c0 >> 3) * LS + (c0 & 7) * 8;
-  bf16_t* as1 = As + (c1 >> 3) * LS + (c1 & 7) * 8;
-  bf16_t* as2 = As + (c2 >> 3) * LS + (c2 & 7) * 8;
-  bf16_t* as3 = As + (c3 >> 3) * LS + (c3 & 7) * 8;
-  bf16_t* bs0 = Bs + (c0 >> 3) * LS + (c0 & 7) * 8;
-  bf16_t* bs1 = Bs + (c1 >> 3) * LS + (c1 & 7) * 8;
+  bf16_t* as0 = As + TOFF(c0 >> 3, (c0 & 7) * 8);
+  bf16_t* as1 = As + TOFF(c1 >> 3, (c1 & 7) * 8);
+  bf16_t* as2 = As + TOFF(c2 >> 3, (c2 & 7) * 8);
+  bf16_t* as3 = As + TOFF(c3 >> 3, (c3 & 7) * 8);
+  bf16_t* bs0 = Bs + TOFF(c0 >> 3, (c0 & 7) * 8);
+  bf16_t* bs1 = Bs + TOFF(c1 >> 3, (c1 & 7) * 8);
   const int klast = K - BK;
   uint4 p0, p1, p2, p3, pw0, pw1;  // even K-steps
   uint4 q0, q1, q2, q3, qw0, qw1;  // odd K-steps
@@ -183,9 +196,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void m
                                                       bf16_t* __restrict__ act,
                                                       const TrialHP* __restrict__ hp,
                                                       uint32_t step, int layer, int flags) {
-  __shared__ __attribute__((aligned(16))) bf16_t smem[(BM + BN) * LS];
+  __shared__ __attribute__((aligned(16))) bf16_t smem[(BM + BN) * TS];
   bf16_t* As = smem;
-  bf16_t* Bs = smem + BM * LS;
+  bf16_t* Bs = smem + BM * TS;
   const int2 wi = work[xcd_remap(blockIdx.x, n_work)];
   const MlpTL tl = tls[wi.x];
   const int K = tl.K, N = tl.N, n0 = wi.y * BN, row0 = blockIdx.y * BM;
@@ -220,7 +233,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void m
           const uint32_t idx = (uint32_t)((row0 + row) * N + n0 + col);
           v = rng_uniform(key, idx) >= h.drop ? v * inv_keep : 0.f;
         }
-        Cs[row * LS + col] = f2bf(v);
+        Cs[TOFF(row, col)] = f2bf(v);
       }
   }
   __syncthreads();
@@ -228,7 +241,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void m
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
-    *(uint4*)(Y + (size_t)r * N + ch * 8) = *(const uint4*)(Cs + r * LS + ch * 8);
+    *(uint4*)(Y + (size_t)r * N + ch * 8) = *(const uint4*)(Cs + TOFF(r, ch * 8));
   }
 }
 
@@ -247,10 +260,10 @@ __global__ __launch_bounds__(256) void mlp_fwd_ce_kernel(const MlpTL* __restrict
                                                          TrialHP* __restrict__ hp, float inv_b,
                                                          int flags) {
   constexpr int CS = BN + 1;  // f32 logits row stride
-  constexpr int kSmemBytes = BM * CS * 4 > (BM + BN) * LS * 2 ? BM * CS * 4 : (BM + BN) * LS * 2;
+  constexpr int kSmemBytes = BM * CS * 4 > (BM + BN) * TS * 2 ? BM * CS * 4 : (BM + BN) * TS * 2;
   __shared__ __attribute__((aligned(16))) char smem_raw[kSmemBytes];
   bf16_t* As = (bf16_t*)smem_raw;
-  bf16_t* Bs = As + BM * LS;
+  bf16_t* Bs = As + BM * TS;
   float* Ls = (float*)smem_raw;
 
   const int2 wi = work[xcd_remap(blockIdx.x, n_work)];
@@ -346,12 +359,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                                                           float* __restrict__ m32,
                                                           float* __restrict__ v32,
                                                           const TrialHP* __restrict__ hp, int flags) {
-  constexpr int DS = BN + 4;  // f32 row stride of the dW staging tile
-  __shared__ __attribute__((aligned(16))) bf16_t smem[(2 * BM + BN) * LS + 2 * 4 * BN + 2 * BN * DS];
+  constexpr int DS = BN + 4;  // f32 row stride bound of the dW staging tile (FOFF)
+  __shared__ __attribute__((aligned(16))) bf16_t smem[(2 * BM + BN) * TS + 2 * 4 * BN + 2 * BN * DS];
   bf16_t* Xs = smem;
-  bf16_t* Zs = smem + BM * LS;
-  bf16_t* Ws = smem + 2 * BM * LS;
-  float* red = (float*)(smem + (2 * BM + BN) * LS);  // [4][64] bias partial sums
+  bf16_t* Zs = smem + BM * TS;
+  bf16_t* Ws = smem + 2 * BM * TS;
+  float* red = (float*)(smem + (2 * BM + BN) * TS);  // [4][64] bias partial sums
   float* Dw = red + 4 * BN;                           // [64 n][DS] dW of the current chunk
 
   const int2 wi = work[xcd_remap(blockIdx.x, n_work)];
@@ -384,7 +397,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
-    *(uint4*)(Xs + r * LS + ch * 8) = *(const uint4*)(X + (size_t)r * K + k0 + ch * 8);
+    *(uint4*)(Xs + TOFF(r, ch * 8)) = *(const uint4*)(X + (size_t)r * K + k0 + ch * 8);
   }
   __syncthreads();
 
@@ -402,7 +415,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // workgroup per CU hides them).
   const int zo0 = (tid >> 3) * N + (tid & 7) * 8, zo1 = ((tid + 256) >> 3) * N + (tid & 7) * 8;
   const int zo2 = ((tid + 512) >> 3) * N + (tid & 7) * 8, zo3 = ((tid + 768) >> 3) * N + (tid & 7) * 8;
-  bf16_t* zs0 = Zs + (tid >> 3) * LS + (tid & 7) * 8;
+  bf16_t* zs0 = Zs + TOFF(tid >> 3, (tid & 7) * 8);     // rows +32 i keep the swizzle
   // Optimizer-state layout: thread -> rows 16i + tid/16 (i < 4), 4 consecutive k at 4 * (tid % 16):
   // every wave-instruction moves 4 rows x 256 contiguous bytes of W/M (/V), full 128-B lines.
   const int wo = (tid >> 4) * K + k0 + 4 * (tid & 15);
@@ -458,9 +471,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   for (int nc = 0; nc < N; nc += BN) {
     // ---- this chunk's operands -> LDS (dZ row-major; W^T image as bf16 for the dX MFMAs) ----
     *(uint4*)(zs0) = cz0;
-    *(uint4*)(zs0 + 32 * LS) = cz1;
-    *(uint4*)(zs0 + 64 * LS) = cz2;
-    *(uint4*)(zs0 + 96 * LS) = cz3;
+    *(uint4*)(zs0 + 32 * TS) = cz1;
+    *(uint4*)(zs0 + 64 * TS) = cz2;
+    *(uint4*)(zs0 + 96 * TS) = cz3;
     if (OPT == kSGD16) {
       cm0 = bf4_to_f32(ch0); cm1 = bf4_to_f32(ch1); cm2 = bf4_to_f32(ch2); cm3 = bf4_to_f32(ch3);
     }
@@ -476,7 +489,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     if (PF && more) MOPT_BWD_LOAD(nc + BN, n)
     if (has_dx) {   // the bf16 working copy (hi) is the dX operand, as in the forward
 #pragma unroll
-      for (int i = 0; i < 4; ++i) *(uint2*)(Ws + (16 * i + (tid >> 4)) * LS + 4 * (tid & 15)) = wh[i];
+      for (int i = 0; i < 4; ++i) *(uint2*)(Ws + TOFF(16 * i + (tid >> 4), 4 * (tid & 15))) = wh[i];
     }
     __syncthreads();
 
@@ -486,11 +499,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       for (int s = 0; s < 2; ++s) {
         bf16x8 a[2], b[4];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) a[i] = lds_frag(Zs + (32 * wave + 16 * i + li) * LS + 32 * s + 8 * g);
+        for (int i = 0; i < 2; ++i) a[i] = lds_frag(Zs + TOFF(32 * wave + 16 * i + li, 32 * s + 8 * g));
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const s16x4 lo = lds_tr4(Ws + (32 * s + 8 * g + q) * LS + 16 * j + 4 * pp);
-          const s16x4 hi = lds_tr4(Ws + (32 * s + 8 * g + 4 + q) * LS + 16 * j + 4 * pp);
+          const s16x4 lo = lds_tr4(Ws + TOFF(32 * s + 8 * g + q, 16 * j + 4 * pp));
+          const s16x4 hi = lds_tr4(Ws + TOFF(32 * s + 8 * g + 4 + q, 16 * j + 4 * pp));
           b[j] = cat_frag(lo, hi);
         }
 #pragma unroll
@@ -512,15 +525,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         const int c0 = 32 * wk + 16 * t + 4 * pp;
-        const s16x4 lo = lds_tr4(Xs + (32 * s + 8 * g + q) * LS + c0);
-        const s16x4 hi = lds_tr4(Xs + (32 * s + 8 * g + 4 + q) * LS + c0);
+        const s16x4 lo = lds_tr4(Xs + TOFF(32 * s + 8 * g + q, c0));
+        const s16x4 hi = lds_tr4(Xs + TOFF(32 * s + 8 * g + 4 + q, c0));
         xa[t] = cat_frag(lo, hi);
       }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int c0 = 32 * wn + 16 * u + 4 * pp;
-        const s16x4 lo = lds_tr4(Zs + (32 * s + 8 * g + q) * LS + c0);
-        const s16x4 hi = lds_tr4(Zs + (32 * s + 8 * g + 4 + q) * LS + c0);
+        const s16x4 lo = lds_tr4(Zs + TOFF(32 * s + 8 * g + q, c0));
+        const s16x4 hi = lds_tr4(Zs + TOFF(32 * s + 8 * g + 4 + q, c0));
         bz[u] = cat_frag(lo, hi);
       }
 #pragma unroll
@@ -535,11 +548,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int u = 0; u < 2; ++u)
-        *(f32x4*)(Dw + (32 * wn + 16 * u + li) * DS + 32 * wk + 16 * t + 4 * g) = dw[t][u];
+        *(f32x4*)(Dw + FOFF(32 * wn + 16 * u + li, 32 * wk + 16 * t + 4 * g)) = dw[t][u];
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const f32x4 gv = *(const f32x4*)(Dw + (16 * i + (tid >> 4)) * DS + 4 * (tid & 15));
+      const f32x4 gv = *(const f32x4*)(Dw + FOFF(16 * i + (tid >> 4), 4 * (tid & 15)));
       const size_t o = (size_t)nc * K + wo + (size_t)(16 * i) * K;
       f32x4 wv = w[i], mv = m[i], vv;
       if (OPT == kAdamW) vv = v[i];
@@ -572,7 +585,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     if (do_bias) {
       const int col = tid & 63, part = tid >> 6;
       float s = 0.f;
-      for (int r = part * 32; r < part * 32 + 32; ++r) s += bf2f(Zs[r * LS + col]);
+      for (int r = part * 32; r < part * 32 + 32; ++r) s += bf2f(Zs[TOFF(r, col)]);
       red[part * 64 + col] = s;
       __syncthreads();
       if (tid < 64) {
@@ -620,15 +633,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = 32 * wave + 16 * i + 4 * g + r, col = 16 * j + li;
-        const float xv = bf2f(Xs[row * LS + col]);
-        Zs[row * LS + col] = f2bf(xv > 0.f ? dx[i][j][r] * inv_keep : 0.f);
+        const float xv = bf2f(Xs[TOFF(row, col)]);
+        Zs[TOFF(row, col)] = f2bf(xv > 0.f ? dx[i][j][r] * inv_keep : 0.f);
       }
   __syncthreads();
   bf16_t* GX = grad + tl.gx_off + k0;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
-    *(uint4*)(GX + (size_t)r * K + ch * 8) = *(const uint4*)(Zs + r * LS + ch * 8);
+    *(uint4*)(GX + (size_t)r * K + ch * 8) = *(const uint4*)(Zs + TOFF(r, ch * 8));
   }
 }
 

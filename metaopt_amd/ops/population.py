@@ -91,7 +91,12 @@ class MemberConfig:
     eps: float = 1e-8
 
     def to_dict(self) -> dict:
-        return dataclasses.asdict(self)
+        # field by field (dataclasses.asdict deep-copies recursively: a visible cost when the
+        # sweep checkpoints a hundred members per sync)
+        return {f: getattr(self, f) for f in _MEMBER_FIELDS}
+
+
+_MEMBER_FIELDS = tuple(f.name for f in dataclasses.fields(MemberConfig))
 
 
 class StatsSnapshot:
@@ -366,16 +371,35 @@ class PopulationMLP:
         return slice(b, b + self.slot_params)
 
     def _init_descs(self, slots) -> np.ndarray:
-        rows = []
-        for slot in slots:
-            cfg = self.members[slot]
-            base = self.slot_base(slot)
-            for l, ((k, n), (kr, nr), (wo, bo)) in enumerate(zip(
-                    self.layer_dims(cfg.width), self.real_dims(cfg.width),
-                    self.param_offsets(cfg.width))):
-                bound = float(np.float32(1.0) / np.sqrt(np.float32(kr)))
-                rows.append((base + wo, base + bo, k, n, kr, nr, cfg.seed & 0xFFFFFFFF, l, bound, 0))
-        return np.array(rows, dtype=INIT_DTYPE)
+        """One InitDesc per (member, layer), vectorised over the members."""
+        slots = np.asarray(list(slots), dtype=np.int64)
+        L = self.L
+        out = np.zeros((len(slots), L), dtype=INIT_DTYPE)
+        if not len(slots):
+            return out.reshape(-1)
+        widths = np.array([self.members[s].width for s in slots], dtype=np.int64)
+        seeds = np.array([self.members[s].seed & 0xFFFFFFFF for s in slots], dtype=np.uint32)
+        wp = (widths + TILE - 1) // TILE * TILE
+        base = slots * self.slot_params
+        off = np.zeros_like(base)
+        for l in range(L):
+            if self.n_hidden == 0:
+                K, N = np.full_like(wp, self.K0), np.full_like(wp, TILE)
+                kr, nr = np.full_like(wp, self.in_features), np.full_like(wp, self.num_classes)
+            else:
+                K = np.full_like(wp, self.K0) if l == 0 else wp
+                N = np.full_like(wp, TILE) if l == L - 1 else wp
+                kr = np.full_like(wp, self.in_features) if l == 0 else widths
+                nr = np.full_like(wp, self.num_classes) if l == L - 1 else widths
+            wsz = (K * N + TILE - 1) // TILE * TILE
+            r = out[:, l]
+            r["w_off"] = base + off
+            r["b_off"] = base + off + wsz
+            r["K"], r["N"], r["k_real"], r["n_real"] = K, N, kr, nr
+            r["seed"], r["layer"] = seeds, l
+            r["bound"] = (np.float32(1.0) / np.sqrt(kr.astype(np.float32))).astype(np.float32)
+            off = off + wsz + (N + TILE - 1) // TILE * TILE
+        return out.reshape(-1)
 
     def _run_pending_init(self) -> None:
         if not self._pending_init:
@@ -448,7 +472,11 @@ class PopulationMLP:
         return self.used_params_for(self.members[slot].width)
 
     def used_params_for(self, width: int) -> int:
-        return sum(pad64(k * n) + pad64(n) for k, n in self.layer_dims(width))
+        cache = self.__dict__.setdefault("_used_cache", {})
+        n = cache.get(width)
+        if n is None:
+            n = cache[width] = sum(pad64(k * n) + pad64(n) for k, n in self.layer_dims(width))
+        return n
 
     # -- checkpoint pool: batched save / restore of members (one kernel launch each) ------------
     def alloc_ckpt_pool(self, n: int) -> None:
@@ -461,11 +489,55 @@ class PopulationMLP:
         w = _SplitBuffer(self.p16, self.plo) if self.split else self.p32
         return [w, self.m32] + ([self.v32] if self.optimizer == "adamw" else [])
 
+    def _state_descs(self, slots, idxs, ns, save: bool) -> np.ndarray:
+        """multi_copy descriptors between slot regions and checkpoint-pool entries, built with
+        numpy from raw pointers (one row per member and state buffer)."""
+        from .ckpt import DESC_DTYPE
+        slots = np.asarray(slots, dtype=np.uint64)
+        idxs = np.asarray(idxs, dtype=np.uint64)
+        ns = np.asarray(ns, dtype=np.int64)
+        SP = np.uint64(self.slot_params)
+        nb = self._n_state_buffers()
+        base = slots * SP
+        ck0 = np.uint64(self.ck.data_ptr()) + np.uint64(4) * idxs * np.uint64(nb) * SP
+        out = np.zeros((nb, len(slots)), dtype=DESC_DTYPE)
+        out["n"] = ns
+        m16 = self.m32.dtype == torch.bfloat16
+        p16, plo = np.uint64(self.p16.data_ptr()), np.uint64(self.plo.data_ptr())
+        m_ptr, v_ptr = np.uint64(self.m32.data_ptr()), np.uint64(self.v32.data_ptr())
+        two, four = np.uint64(2), np.uint64(4)
+        for j in range(nb):
+            ckj = ck0 + four * np.uint64(j) * SP
+            r = out[j]
+            if save:
+                r["dst"] = ckj
+                if j == 0:
+                    r["src16"], r["src_lo"] = p16 + two * base, plo + two * base
+                elif j == 1 and m16:
+                    r["src16"] = m_ptr + two * base
+                else:
+                    r["src"] = (m_ptr if j == 1 else v_ptr) + four * base
+            else:
+                r["src"] = ckj
+                if j == 0:
+                    r["dst16"], r["dst_lo"] = p16 + two * base, plo + two * base
+                elif j == 1 and m16:
+                    r["dst16"] = m_ptr + two * base
+                else:
+                    r["dst"] = (m_ptr if j == 1 else v_ptr) + four * base
+        return out.reshape(-1)
+
     def save_states(self, pairs) -> list:
         """Checkpoint members: ``pairs`` = [(slot, pool index)]; returns per-member metadata."""
-        from .ckpt import multi_copy
+        from .ckpt import launch_descs, multi_copy
         self._run_pending_init()
         self._join()
+        if self.split and self.device.type == "cuda":
+            ns = [self.used_params(s) for s, _ in pairs]
+            launch_descs(self._state_descs([s for s, _ in pairs], [i for _, i in pairs], ns,
+                                           save=True), self.device)
+            return [{"config": self.members[s].to_dict(), "t": int(self.hp[s]["t"]),
+                     "ck": int(i), "n": n} for (s, i), n in zip(pairs, ns)]
         items, metas = [], []
         for slot, idx in pairs:
             n = self.used_params(slot)
@@ -479,8 +551,18 @@ class PopulationMLP:
 
     def load_states(self, pairs) -> None:
         """Restore members from the pool: ``pairs`` = [(slot, metadata)] (bf16 copy included)."""
-        from .ckpt import multi_copy
+        from .ckpt import launch_descs, multi_copy
         self._join()
+        if self.split and self.device.type == "cuda":
+            launch_descs(self._state_descs([s for s, _ in pairs], [m["ck"] for _, m in pairs],
+                                           [m["n"] for _, m in pairs], save=False), self.device)
+            for slot, meta in pairs:
+                self._pending_init.discard(slot)
+                cfg = MemberConfig(**meta["config"])
+                self.members[slot] = cfg
+                self._write_hp(slot, cfg, int(meta["t"]))
+            self._dirty = True
+            return
         items = []
         for slot, meta in pairs:
             n, idx = meta["n"], meta["ck"]

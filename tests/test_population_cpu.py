@@ -231,3 +231,29 @@ def test_work_tables_are_bounds_checked():
     fwd[1][0, 0] = 0                                                    # an empty slot's layer
     with pytest.raises(ValueError, match="missing trial-layer"):
         pop._validate_tables(tb["tl_np"], fwd, tb["bwd_np"], 128)
+
+
+def test_init_descriptors_match_the_layer_layout():
+    """The vectorised member-initialisation descriptors equal the per-layer layout
+    (layer_dims / real_dims / param_offsets) row for row, logistic regression included."""
+    import numpy as np
+    from metaopt_amd.ops.population import MemberConfig, PopulationMLP
+    for n_hidden, widths in ((3, (64, 100, 1, 257)), (0, (64,))):
+        pop = PopulationMLP(6, in_features=784 if n_hidden else 2,
+                            num_classes=10 if n_hidden else 2, n_hidden=n_hidden,
+                            max_width=320, device="cpu")
+        slots = [1, 3, 4, 5][:len(widths)]
+        for s, w in zip(slots, widths):
+            pop.set_member(s, MemberConfig(width=w, lr=0.1, seed=1000 + s), init=False)
+        got = pop._init_descs(slots)
+        rows = []
+        for s in slots:
+            cfg = pop.members[s]
+            base = pop.slot_base(s)
+            for l, ((k, n), (kr, nr), (wo, bo)) in enumerate(zip(
+                    pop.layer_dims(cfg.width), pop.real_dims(cfg.width),
+                    pop.param_offsets(cfg.width))):
+                rows.append((base + wo, base + bo, k, n, kr, nr, cfg.seed, l,
+                             np.float32(1.0) / np.sqrt(np.float32(kr)), 0))
+        want = np.array(rows, dtype=got.dtype)
+        assert (got == want).all()
