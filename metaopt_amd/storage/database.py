@@ -76,6 +76,7 @@ DATABASES = Registry("Database")
 # Query / projection engine on nested documents
 # ----------------------------------------------------------------------------------------------
 _MISSING = object()
+_NO_HASH_INDEX = ("_id", "results", "start_time", "end_time", "submit_time", "heartbeat")
 
 
 def _get_path(doc, key: str):
@@ -383,8 +384,11 @@ class _Collection:
                 values.add(v)
         self.indexes[name] = (fields, unique, values)
         # hash index only for scalar fields queried by equality / $in ("results" holds a list of
-        # result documents: hashing it on every update cost more than all other indexing)
-        if len(fields) == 1 and fields[0] not in ("_id", "results") and \
+        # result documents: hashing it on every update cost more than all other indexing; the
+        # timestamps are only ever range-queried or sorted -- lost trials, stats -- which an
+        # equality index never serves, while a device sweep rewrites them thousands of times per
+        # second)
+        if len(fields) == 1 and fields[0] not in _NO_HASH_INDEX and \
                 fields[0] not in self.hash_index:
             hidx: Dict[Any, set] = {}
             for hid, d in self.docs.items():
@@ -555,10 +559,11 @@ class _Collection:
             self._register(d)
         return len(docs)
 
-    def set_fields_by_id(self, items) -> int:
+    def set_fields_by_id(self, items, owned: bool = False) -> int:
         """Bulk ``$set`` of top-level fields: ``items`` = [(id, {field: value}, status or None)],
         each applied only while the document's status equals the given one (compare-and-swap).
-        Same result as :meth:`update` per item without the generic operator machinery."""
+        Same result as :meth:`update` per item without the generic operator machinery.
+        ``owned``: the caller never touches the field values again (no defensive copy)."""
         uniq = {f for fields, unique, _ in self.indexes.values() if unique for f in fields}
         n = 0
         for uid, fields, was in items:
@@ -575,7 +580,7 @@ class _Collection:
                     ids = hidx.get(self._hval(d, f))
                     if ids is not None:
                         ids.discard(hid)
-            d.update(_copy_doc(fields))
+            d.update(fields if owned else _copy_doc(fields))
             for f, hidx in self.hash_index.items():
                 if f in fields:
                     hidx.setdefault(self._hval(d, f), set()).add(hid)
@@ -636,9 +641,9 @@ class EphemeralDB(AbstractDB):
         """Insert documents the caller will never touch again (no copy): bulk writers."""
         return self._col(collection_name).insert_owned(list(docs))
 
-    def set_fields_by_id(self, collection_name, items) -> int:
+    def set_fields_by_id(self, collection_name, items, owned: bool = False) -> int:
         """Bulk compare-and-swap field updates by ``_id`` (see ``_Collection``)."""
-        return self._col(collection_name).set_fields_by_id(items)
+        return self._col(collection_name).set_fields_by_id(items, owned)
 
     def read_and_write(self, collection_name, query, data, selection=None):
         col = self._col(collection_name)

@@ -216,10 +216,11 @@ class DocumentStorage(BaseStorageProtocol):
         """Set ``fields`` of trial ``uid`` (compare-and-swap on the status when ``was`` is set)."""
         return self.update_trial_docs([(uid, fields, was)])
 
-    def update_trial_docs(self, items) -> int:
-        """Bulk :meth:`update_trial_doc`: ``items`` = [(uid, fields, was or None)]."""
+    def update_trial_docs(self, items, owned: bool = False) -> int:
+        """Bulk :meth:`update_trial_doc`: ``items`` = [(uid, fields, was or None)]; ``owned``:
+        the caller hands the field values over (an in-process backend keeps them uncopied)."""
         if hasattr(self._db, "set_fields_by_id"):
-            return self._db.set_fields_by_id("trials", items)
+            return self._db.set_fields_by_id("trials", items, owned=owned)
         n = 0
         for uid, fields, was in items:
             where = {"_id": uid}

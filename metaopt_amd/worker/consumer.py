@@ -1,12 +1,18 @@
-"""Consumer: evaluates one trial by running the user's script as a subprocess
-(reference: ``src/orion/core/worker/consumer.py:37-199``).
+"""Consumer: evaluates one trial by running the user's script as a black-box subprocess.
 
-Per trial: a working directory ``<working_dir>/<exp>_<trial.id>`` (temporary unless the
-experiment sets ``working_dir``), a rendered config file and a results file, environment variables
-``ORION_EXPERIMENT_ID/_NAME/_VERSION``, ``ORION_TRIAL_ID``, ``ORION_WORKING_DIR``,
-``ORION_RESULTS_PATH`` (plus ``MOPT_*`` aliases), the heartbeat thread, then
-``Popen([script] + args)``.  Exit code != 0 -> ``broken``; SIGTERM or Ctrl-C -> ``interrupted``
-(re-raised).  The SIGTERM handler is installed once per consumer (reference quirk 11).
+Behaviour contract (reference ``src/orion/core/worker/consumer.py:37-199``): each trial runs in
+a working directory ``<working_dir>/<experiment>_<trial id>`` (temporary unless the experiment
+sets ``working_dir``) holding the trial's rendered configuration file and the results file the
+script writes through ``report_results``; the script sees ``ORION_EXPERIMENT_ID / _NAME /
+_VERSION``, ``ORION_TRIAL_ID``, ``ORION_WORKING_DIR`` and ``ORION_RESULTS_PATH`` (plus
+``MOPT_*`` twins); the trial's heartbeat is kept while it runs.  Outcome: exit code 0 -> the
+results are recorded (``completed``); non-zero -> ``broken``; SIGTERM or Ctrl-C ->
+``interrupted`` and the interruption propagates.
+
+Structure: :class:`TrialFiles` lays out one trial's directory and files, :func:`trial_env`
+builds its environment, and :meth:`Consumer.consume` maps the run's outcome onto the trial's
+status.  The SIGTERM -> KeyboardInterrupt handler is installed once per consumer (not once per
+trial, reference quirk 11).
 """
 from __future__ import annotations
 
@@ -14,8 +20,10 @@ import logging
 import os
 import signal
 import subprocess
+import sys
 import tempfile
 import threading
+from dataclasses import dataclass
 
 from ..core.config import config as global_config
 from ..io.space_parser import SpaceCmdlineParser
@@ -26,69 +34,84 @@ log = logging.getLogger(__name__)
 
 
 class ExecutionError(Exception):
-    pass
+    """The user's script exited with a non-zero code."""
 
 
-def _sigterm_handler(signum, frame):
-    log.error("The worker has been interrupted (SIGTERM).")
+def _raise_interrupt(signum, frame):
+    log.error("worker interrupted (SIGTERM)")
     raise KeyboardInterrupt
+
+
+@dataclass
+class TrialFiles:
+    """The rendered configuration and the (empty) results file of one trial, in ``root``."""
+    root: str
+    config: str
+    results: str
+
+    @classmethod
+    def create(cls, root: str) -> "TrialFiles":
+        paths = []
+        for prefix, suffix in (("trial_", ".conf"), ("results_", ".log")):
+            fd, path = tempfile.mkstemp(prefix=prefix, suffix=suffix, dir=root)
+            os.close(fd)
+            paths.append(path)
+        return cls(root, *paths)
+
+
+def trial_env(experiment, trial, results_path, base=None) -> dict:
+    """The script's environment: ``base`` (default: this process's) plus the trial variables
+    under both the ``ORION_`` and ``MOPT_`` prefixes."""
+    env = dict(os.environ if base is None else base)
+    values = {"EXPERIMENT_ID": experiment.id, "EXPERIMENT_NAME": experiment.name,
+              "EXPERIMENT_VERSION": experiment.version, "TRIAL_ID": trial.id,
+              "WORKING_DIR": trial.working_dir, "RESULTS_PATH": results_path}
+    for prefix in ("ORION", "MOPT"):
+        env.update({f"{prefix}_{k}": str(v) for k, v in values.items()})
+    return env
 
 
 class Consumer:
     def __init__(self, experiment, heartbeat=None):
+        if experiment.space is None:
+            raise RuntimeError("the experiment is not configured yet (no space): the Consumer "
+                               "needs a built experiment")
         self.experiment = experiment
         self.space = experiment.space
-        if self.space is None:
-            raise RuntimeError("Experiment object provided to Consumer has not yet completed"
-                               " initialization.")
         self.template_builder = SpaceCmdlineParser(global_config.user_script_config)
         self.template_builder.set_state_dict(experiment.metadata["parser"])
-        if experiment.working_dir:
-            self.working_dir = os.path.abspath(experiment.working_dir)
-        else:
-            self.working_dir = os.path.join(tempfile.gettempdir(), "mopt")
+        self.working_dir = (os.path.abspath(experiment.working_dir) if experiment.working_dir
+                            else os.path.join(tempfile.gettempdir(), "mopt"))
         self.script_path = experiment.metadata["user_script"]
-        self.pacemaker = None
         self.heartbeat = (global_config.worker.pacemaker_interval if heartbeat is None
                           else heartbeat)
+        self.pacemaker = None
         if threading.current_thread() is threading.main_thread():
-            signal.signal(signal.SIGTERM, _sigterm_handler)
+            signal.signal(signal.SIGTERM, _raise_interrupt)
 
-    def consume(self, trial):
-        temp = self.experiment.working_dir is None
+    def consume(self, trial) -> None:
+        """Run ``trial`` and record its outcome in the experiment's storage."""
+        exp = self.experiment
         try:
-            with WorkingDir(self.working_dir, temp, prefix=self.experiment.name + "_",
-                            suffix=trial.id) as wd:
+            with WorkingDir(self.working_dir, exp.working_dir is None,
+                            prefix=exp.name + "_", suffix=trial.id) as wd:
                 trial.working_dir = wd
-                results_file = self._consume(trial, wd)
-                self.experiment.update_completed_trial(trial, results_file)
+                files = TrialFiles.create(wd)
+                self._run(trial, files)
+                exp.update_completed_trial(trial, files.results)
         except KeyboardInterrupt:
-            self.experiment.set_trial_status(trial, status="interrupted")
+            exp.set_trial_status(trial, status="interrupted")
             raise
         except (ExecutionError, ValueError) as exc:
-            log.warning("Trial %s broke: %s", trial.id, exc)
-            self.experiment.set_trial_status(trial, status="broken")
+            log.warning("trial %s broke: %s", trial.id, exc)
+            exp.set_trial_status(trial, status="broken")
 
-    def get_execution_environment(self, trial, results_file="results.log"):
-        env = dict(os.environ)
-        for prefix in ("ORION", "MOPT"):
-            env[f"{prefix}_EXPERIMENT_ID"] = str(self.experiment.id)
-            env[f"{prefix}_EXPERIMENT_NAME"] = str(self.experiment.name)
-            env[f"{prefix}_EXPERIMENT_VERSION"] = str(self.experiment.version)
-            env[f"{prefix}_TRIAL_ID"] = str(trial.id)
-            env[f"{prefix}_WORKING_DIR"] = str(trial.working_dir)
-            env[f"{prefix}_RESULTS_PATH"] = str(results_file)
-        return env
+    def get_execution_environment(self, trial, results_file="results.log") -> dict:
+        return trial_env(self.experiment, trial, results_file)
 
-    def _consume(self, trial, wd):
-        cfg = tempfile.NamedTemporaryFile(mode="w", prefix="trial_", suffix=".conf", dir=wd,
-                                          delete=False)
-        cfg.close()
-        res = tempfile.NamedTemporaryFile(mode="w", prefix="results_", suffix=".log", dir=wd,
-                                          delete=False)
-        res.close()
-        env = self.get_execution_environment(trial, res.name)
-        args = self.template_builder.format(cfg.name, trial, self.experiment)
+    def _run(self, trial, files: TrialFiles) -> None:
+        args = self.template_builder.format(files.config, trial, self.experiment)
+        env = self.get_execution_environment(trial, files.results)
         self.pacemaker = TrialPacemaker(trial, wait_time=self.heartbeat,
                                         storage=getattr(self.experiment, "storage", None))
         self.pacemaker.start()
@@ -96,23 +119,25 @@ class Consumer:
             self.execute_process(args, env)
         finally:
             self.pacemaker.stop()
-        return res.name
 
-    def execute_process(self, cmd_args, environ):
-        command = [self.script_path] + list(cmd_args)
-        if not os.access(self.script_path, os.X_OK) and self.script_path.endswith(".py"):
-            import sys
-            command = [sys.executable] + command
-        process = subprocess.Popen(command, env=environ)
+    def command(self, cmd_args) -> list:
+        """``[script] + args``; a non-executable ``.py`` script runs under this interpreter."""
+        script = self.script_path
+        head = [script]
+        if script.endswith(".py") and not os.access(script, os.X_OK):
+            head = [sys.executable, script]
+        return head + list(cmd_args)
+
+    def execute_process(self, cmd_args, environ) -> None:
+        proc = subprocess.Popen(self.command(cmd_args), env=environ)
         try:
-            rc = process.wait()
+            code = proc.wait()
         except KeyboardInterrupt:
-            process.terminate()
+            proc.terminate()
             try:
-                process.wait(timeout=10)
+                proc.wait(timeout=10)
             except subprocess.TimeoutExpired:
-                process.kill()
+                proc.kill()
             raise
-        if rc != 0:
-            raise ExecutionError(f"Something went wrong. Check logs. Process returned with code "
-                                 f"{rc} !")
+        if code != 0:
+            raise ExecutionError(f"the script exited with code {code}; see its output")

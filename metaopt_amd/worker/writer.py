@@ -125,9 +125,11 @@ class WriteBehind:
                     self._call("register_trial_docs", [dict(d)])
             return
         fields = self.builder.result_fields if self.builder is not None else None
+        # every queued update carries dicts built for it (the sweep's literals, result_fields):
+        # the storage may keep them as they are
         self._call("update_trial_docs",
                    [h[1] if type(h[1][1]) is dict else (h[1][0], fields(h[1][1]), h[1][2])
-                    for h in held])
+                    for h in held], owned=True)
 
     def _call(self, method, *args, **kwargs) -> bool:
         try:
@@ -173,7 +175,7 @@ def _open(spec):
     return DocumentStorage(MongoDB(**spec[1]))
 
 
-def _child(conn, spec, builder, seed_docs):  # pragma: no cover - runs in the child process
+def _child(conn, spec, builder, seed_docs, applied=None):  # pragma: no cover - child process
     storage = _open(spec)
     if seed_docs:
         storage.database.write("trials", seed_docs)
@@ -184,6 +186,8 @@ def _child(conn, spec, builder, seed_docs):  # pragma: no cover - runs in the ch
         if kind == "ops":
             wb.extend(msg[1])
             wb.flush()
+            if applied is not None:         # the parent's view of the child's backlog
+                applied.value += len(msg[1])
         elif kind == "flush":
             wb.flush()
             conn.send(("flushed", wb.errors))
@@ -235,7 +239,11 @@ class WriterProcess:
             seed = storage.database.read("trials", {"experiment": builder.exp_id})
         ctx = mp.get_context("spawn")
         self._conn, child = ctx.Pipe()
-        self._proc = ctx.Process(target=_child, args=(child, spec, builder, seed),
+        # ops applied by the child (shared counter, no pipe traffic): len(writer) counts the
+        # child's backlog too, so the sweep's backlog bound also holds when the child lags
+        self._applied = ctx.Value("q", 0, lock=False)
+        self._handed = 0
+        self._proc = ctx.Process(target=_child, args=(child, spec, builder, seed, self._applied),
                                  name="mopt-writer", daemon=True)
         self._proc.start()
         child.close()
@@ -250,7 +258,8 @@ class WriterProcess:
     put_update_spec = WriteBehind.put_update_spec
 
     def __len__(self):
-        return len(self._held)
+        lag = 0 if self._fallback is not None else max(0, self._handed - self._applied.value)
+        return len(self._held) + lag
 
     @property
     def failed(self) -> bool:
@@ -305,6 +314,7 @@ class WriterProcess:
             self._fallback.extend(held)
             return
         self._unacked.extend(held)
+        self._handed += len(held)
         self._queue.put(("ops", held))
 
     def _request(self, request):

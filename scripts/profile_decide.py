@@ -105,7 +105,7 @@ def main(n_syncs=40, P=256, world=1, profile=False):
     print(f"decide: {1e3 * t_total / n_syncs:.2f} ms/sync, writes {1e3 * t_rel / n_syncs:.2f} ms/sync, "
           f"{n_done / n_syncs:.1f} completions/sync")
     if prof:
-        pstats.Stats(prof).sort_stats("cumulative").print_stats(30)
+        pstats.Stats(prof).sort_stats(os.environ.get("SORT", "cumulative")).print_stats(30)
 
 
 if __name__ == "__main__":
