@@ -283,7 +283,7 @@ class FlatPopulation:
         from ..ops.population import StatsSnapshot
         return StatsSnapshot(self.stats, self.capacity)
 
-    def raw_results(self, snap, handle):
+    def raw_results(self, snap, handle, rows=None):
         """(train loss, eval loss, eval secondary) per slot from a snapshot, unmasked."""
         tl = snap[0].astype(np.float64) / self.train_rows()
         if handle is None:

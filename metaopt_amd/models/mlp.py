@@ -7,7 +7,10 @@ population, and names the search space the benchmark sweeps:
 * ``/width ~ loguniform(64, 1024, discrete=True)`` -- hidden width of the 3 ReLU layers;
 * ``/dropout ~ uniform(0, 0.5)`` -- dropout after each hidden layer;
 * ``/steps ~ fidelity(32, 2048, 4)`` -- training budget in optimizer steps (ASHA rungs 32, 128, 512,
-  2048).
+  2048);
+* optional ``/batch_size`` (e.g. ``choices([128, 256, 512])``) -- rows per step of the trial, a
+  multiple of 128; the population is sized for the largest value the prior can take and a trial
+  trains on the first rows of each minibatch (``MemberConfig.batch_size``).
 
 Config 1 (logistic regression, CPU) is the same task with ``n_hidden=0`` and a 2-HP space
 (``/lr``, ``/weight_decay``).
@@ -74,7 +77,12 @@ class MLPSweepTask:
             weight_decay=float(params.get("/weight_decay", self.weight_decay)),
             dropout=float(params.get("/dropout", 0.0)) if self.n_hidden > 0 else 0.0,
             seed=int(seed) & 0x7FFFFFFF,
+            batch_size=self.batch_rows(params),
         )
+
+    def batch_rows(self, params: Dict) -> int:
+        """Rows per step of the trial (0: the population's batch size)."""
+        return int(params.get("/batch_size", 0))
 
     def member_row(self, params: Dict, seed: int) -> tuple:
         """(width, lr, momentum, weight decay, dropout, seed) of :meth:`member_config` without

@@ -36,7 +36,8 @@ struct MlpTL {
   int64_t x_off;   // layer input  [rows][K] bf16: offset into the x buffer of the launch
   int64_t y_off;   // layer output [rows][N] bf16: offset into act (forward) / grad (backward)
   int64_t gx_off;  // dZ of the layer below [rows][K] bf16 in grad (backward), -1 if none
-  int64_t pad;
+  int64_t rows;    // rows this trial uses in the launch (its batch size; <= the launch's rows):
+                   // row blocks at or past it are skipped, the loss is normalised by it
 };
 
 // One (member, layer) to initialise; 48 bytes, mirrored by metaopt_amd/ops/population.py.
@@ -202,6 +203,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void m
   const int2 wi = work[xcd_remap(blockIdx.x, n_work)];
   const MlpTL tl = tls[wi.x];
   const int K = tl.K, N = tl.N, n0 = wi.y * BN, row0 = blockIdx.y * BM;
+  if (row0 >= tl.rows) return;           // a smaller batch than the launch's: uniform exit
   const bf16_t* X = xb + tl.x_off + (size_t)row0 * K;
   const bf16_t* W = p16 + tl.w_off + (size_t)n0 * K;
 
@@ -269,6 +271,9 @@ __global__ __launch_bounds__(256) void mlp_fwd_ce_kernel(const MlpTL* __restrict
   const int2 wi = work[xcd_remap(blockIdx.x, n_work)];
   const MlpTL tl = tls[wi.x];
   const int K = tl.K, N = tl.N, row0 = blockIdx.y * BM, C = tl.n_real;
+  if (row0 >= tl.rows) return;           // a smaller batch than the launch's: uniform exit
+  // inv_b <= 0: the mean over the trial's own batch (per-trial batch sizes)
+  const float ib = inv_b > 0.f ? inv_b : 1.f / (float)tl.rows;
   const bf16_t* X = xb + tl.x_off + (size_t)row0 * K;
   const bf16_t* W = p16 + tl.w_off;
 
@@ -313,8 +318,8 @@ __global__ __launch_bounds__(256) void mlp_fwd_ce_kernel(const MlpTL* __restrict
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int c0 = ch * 8 + 2 * e, c1 = c0 + 1;
-          const float g0 = c0 < C ? (__expf(z[c0] - m) * rs - (c0 == y ? 1.f : 0.f)) * inv_b : 0.f;
-          const float g1 = c1 < C ? (__expf(z[c1] - m) * rs - (c1 == y ? 1.f : 0.f)) * inv_b : 0.f;
+          const float g0 = c0 < C ? (__expf(z[c0] - m) * rs - (c0 == y ? 1.f : 0.f)) * ib : 0.f;
+          const float g1 = c1 < C ? (__expf(z[c1] - m) * rs - (c1 == y ? 1.f : 0.f)) * ib : 0.f;
           w4[e] = pack2bf(g0, g1);
         }
         *(uint4*)(dz + ch * 8) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
@@ -349,7 +354,13 @@ __global__ __launch_bounds__(256) void mlp_fwd_ce_kernel(const MlpTL* __restrict
 //   W, M (, V) <- optimizer(W, M, dW)                       (dW^T C-layout = 4 consecutive k/lane)
 // One LDS image per operand serves both row reads and ds_read_b64_tr_b16 transposed reads.
 // ----------------------------------------------------------------------------------------------
-template <int OPT, bool PF>
+//
+// Batches of R = rows / 128 row blocks (per-trial batch sizes): MODE 0 is the one-block kernel
+// above; MODE 2 computes only dX of row block 1 + blockIdx.y (W hi and dZ read, no update) and is
+// launched first; MODE 1 then does the fused pass -- dX of row block 0, dW summed over all R
+// blocks (the X strip and dZ chunk of blocks 1.. restaged through the same LDS tiles), the
+// update, the bias over all rows.  Trials with fewer rows than the launch skip the extra blocks.
+template <int OPT, bool PF, int MODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void mlp_bwd_opt_kernel(const MlpTL* __restrict__ tls,
                                                           const int2* __restrict__ work, int n_work,
                                                           const bf16_t* __restrict__ xb,
@@ -370,8 +381,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int2 wi = work[xcd_remap(blockIdx.x, n_work)];
   const MlpTL tl = tls[wi.x];
   const int K = tl.K, N = tl.N, k0 = wi.y * BK;
-  const bf16_t* X = xb + tl.x_off;
-  const bf16_t* dZ = grad + tl.y_off;
+  const int R = MODE == 0 ? 1 : (int)(tl.rows / BM);       // the trial's row blocks
+  const int rbx = MODE == 2 ? 1 + (int)blockIdx.y : 0;      // this launch's row block
+  if (MODE == 2 && rbx >= R) return;                         // uniform per workgroup
+  const bf16_t* X = xb + tl.x_off + (size_t)rbx * BM * K;
+  const bf16_t* dZ = grad + tl.y_off + (size_t)rbx * BM * N;
   bf16_t* WLO = plo + tl.w_off;                      // master = (hi, lo) pairs, see common.h
   float* M32 = m32 + tl.w_off;                       // kSGD / kAdamW
   bf16_t* M16 = (bf16_t*)m32 + tl.w_off;             // kSGD16
@@ -379,7 +393,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   bf16_t* W16 = p16 + tl.w_off;
   const TrialHP h = hp[tl.trial];
   const bool has_dx = flags & kHasDx;
-  const bool do_bias = (flags & kUpdateBias) && wi.y == 0;
+  const bool do_bias = (flags & kUpdateBias) && wi.y == 0 && MODE != 2;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, g = lane >> 4, q = li >> 2, pp = li & 3;
@@ -419,11 +433,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // Optimizer-state layout: thread -> rows 16i + tid/16 (i < 4), 4 consecutive k at 4 * (tid % 16):
   // every wave-instruction moves 4 rows x 256 contiguous bytes of W/M (/V), full 128-B lines.
   const int wo = (tid >> 4) * K + k0 + 4 * (tid & 15);
-  uint4 cz0, cz1, cz2, cz3, nz0, nz1, nz2, nz3;
-  f32x4 cm0, cm1, cm2, cm3, cv0, cv1, cv2, cv3, nm0, nm1, nm2, nm3, nv0, nv1, nv2, nv3;
-  uint2 cwh0, cwh1, cwh2, cwh3, cwl0, cwl1, cwl2, cwl3;   // master weights: hi (bf16), lo halves
-  uint2 nwh0, nwh1, nwh2, nwh3, nwl0, nwl1, nwl2, nwl3;
-  uint2 ch0, ch1, ch2, ch3, nh0, nh1, nh2, nh3;           // kSGD16 momentum (4 bf16 per lane)
+  // (zero-initialised: MODE 2 loads only the hi halves and dZ; the rest stays unused)
+  uint4 cz0{}, cz1{}, cz2{}, cz3{}, nz0{}, nz1{}, nz2{}, nz3{};
+  f32x4 cm0{}, cm1{}, cm2{}, cm3{}, cv0{}, cv1{}, cv2{}, cv3{};
+  f32x4 nm0{}, nm1{}, nm2{}, nm3{}, nv0{}, nv1{}, nv2{}, nv3{};
+  uint2 cwh0{}, cwh1{}, cwh2{}, cwh3{}, cwl0{}, cwl1{}, cwl2{}, cwl3{};   // master: hi, lo halves
+  uint2 nwh0{}, nwh1{}, nwh2{}, nwh3{}, nwl0{}, nwl1{}, nwl2{}, nwl3{};
+  uint2 ch0{}, ch1{}, ch2{}, ch3{}, nh0{}, nh1{}, nh2{}, nh3{};   // kSGD16 momentum (4 bf16)
 #define MOPT_BWD_LOAD(NC, P)                                                                     \
   {                                                                                              \
     const bf16_t* zc_ = dZ + (NC);                                                               \
@@ -436,6 +452,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     P##wh1 = *(const uint2*)(W16 + ob + 16 * K);                                                 \
     P##wh2 = *(const uint2*)(W16 + ob + 32 * K);                                                 \
     P##wh3 = *(const uint2*)(W16 + ob + 48 * K);                                                 \
+    if (MODE != 2) {                                                                             \
     P##wl0 = *(const uint2*)(WLO + ob);                                                          \
     P##wl1 = *(const uint2*)(WLO + ob + 16 * K);                                                 \
     P##wl2 = *(const uint2*)(WLO + ob + 32 * K);                                                 \
@@ -456,6 +473,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       P##v1 = *(const f32x4*)(V32 + ob + 16 * K);                                                \
       P##v2 = *(const f32x4*)(V32 + ob + 32 * K);                                                \
       P##v3 = *(const f32x4*)(V32 + ob + 48 * K);                                                \
+    }                                                                                            \
     }                                                                                            \
   }
 #define MOPT_BWD_ADVANCE()                                                                       \
@@ -513,37 +531,68 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       }
     }
 
-    // ---- dW^T[strip, chunk] = X^T dZ ----
+    // ---- dW^T[strip, chunk] = X^T dZ, summed over the trial's row blocks ----
     f32x4 dw[2][2];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int u = 0; u < 2; ++u) dw[t][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#define MOPT_BWD_DW()                                                                            \
+  _Pragma("unroll") for (int s = 0; s < 4; ++s) {                                                \
+    bf16x8 xa[2], bz[2];                                                                         \
+    _Pragma("unroll") for (int t = 0; t < 2; ++t) {                                              \
+      const int c0 = 32 * wk + 16 * t + 4 * pp;                                                  \
+      const s16x4 lo = lds_tr4(Xs + TOFF(32 * s + 8 * g + q, c0));                               \
+      const s16x4 hi = lds_tr4(Xs + TOFF(32 * s + 8 * g + 4 + q, c0));                           \
+      xa[t] = cat_frag(lo, hi);                                                                  \
+    }                                                                                            \
+    _Pragma("unroll") for (int u = 0; u < 2; ++u) {                                              \
+      const int c0 = 32 * wn + 16 * u + 4 * pp;                                                  \
+      const s16x4 lo = lds_tr4(Zs + TOFF(32 * s + 8 * g + q, c0));                               \
+      const s16x4 hi = lds_tr4(Zs + TOFF(32 * s + 8 * g + 4 + q, c0));                           \
+      bz[u] = cat_frag(lo, hi);                                                                  \
+    }                                                                                            \
+    _Pragma("unroll") for (int t = 0; t < 2; ++t)                                                \
+      _Pragma("unroll") for (int u = 0; u < 2; ++u) dw[t][u] = mfma16(xa[t], bz[u], dw[t][u]);  \
+  }
+    // bias partial sums of this thread's (row quarter, column), over every row block
+    const int bcol = tid & 63, bpart = tid >> 6;
+    float bsum = 0.f;
+    if (MODE != 2) {
+      MOPT_BWD_DW()
+      if (do_bias)
+        for (int r = bpart * 32; r < bpart * 32 + 32; ++r) bsum += bf2f(Zs[TOFF(r, bcol)]);
+      if (MODE == 1) {
+        for (int rb = 1; rb < R; ++rb) {      // R is uniform per workgroup
+          __syncthreads();                    // every wave is done with the previous block
+          const bf16_t* Xr = X + (size_t)rb * BM * K + k0;
+          const bf16_t* Zr = dZ + (size_t)rb * BM * N + nc;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      bf16x8 xa[2], bz[2];
+          for (int i = 0; i < 4; ++i) {
+            const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
+            *(uint4*)(Xs + TOFF(r, ch * 8)) = *(const uint4*)(Xr + (size_t)r * K + ch * 8);
+            *(uint4*)(Zs + TOFF(r, ch * 8)) = *(const uint4*)(Zr + (size_t)r * N + ch * 8);
+          }
+          __syncthreads();
+          MOPT_BWD_DW()
+          if (do_bias)
+            for (int r = bpart * 32; r < bpart * 32 + 32; ++r) bsum += bf2f(Zs[TOFF(r, bcol)]);
+        }
+        if (R > 1) {                          // row block 0's X strip back (next chunk, dX mask)
+          __syncthreads();
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int c0 = 32 * wk + 16 * t + 4 * pp;
-        const s16x4 lo = lds_tr4(Xs + TOFF(32 * s + 8 * g + q, c0));
-        const s16x4 hi = lds_tr4(Xs + TOFF(32 * s + 8 * g + 4 + q, c0));
-        xa[t] = cat_frag(lo, hi);
+          for (int i = 0; i < 4; ++i) {
+            const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
+            *(uint4*)(Xs + TOFF(r, ch * 8)) = *(const uint4*)(X + (size_t)r * K + k0 + ch * 8);
+          }
+        }
       }
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int c0 = 32 * wn + 16 * u + 4 * pp;
-        const s16x4 lo = lds_tr4(Zs + TOFF(32 * s + 8 * g + q, c0));
-        const s16x4 hi = lds_tr4(Zs + TOFF(32 * s + 8 * g + 4 + q, c0));
-        bz[u] = cat_frag(lo, hi);
-      }
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int u = 0; u < 2; ++u) dw[t][u] = mfma16(xa[t], bz[u], dw[t][u]);
     }
+#undef MOPT_BWD_DW
 
     // ---- optimizer epilogue: dW^T C-fragments (register r of dw[t][u] = dW[n][k + r]) are
     //      restaged through LDS into the row-contiguous layout of W/M (/V) ----
+    if (MODE != 2) {
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -583,10 +632,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
     // ---- bias: db[n] = sum_b dZ[b][n]; only the k-strip-0 workgroup owns the bias ----
     if (do_bias) {
-      const int col = tid & 63, part = tid >> 6;
-      float s = 0.f;
-      for (int r = part * 32; r < part * 32 + 32; ++r) s += bf2f(Zs[TOFF(r, col)]);
-      red[part * 64 + col] = s;
+      red[bpart * 64 + bcol] = bsum;
       __syncthreads();
       if (tid < 64) {
         const float gb = red[tid] + red[64 + tid] + red[128 + tid] + red[192 + tid];
@@ -614,6 +660,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         else *bm = mb;
       }
     }
+    }  // MODE != 2
     __syncthreads();
     if (more) {
       if (PF) MOPT_BWD_ADVANCE()
@@ -637,7 +684,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         Zs[TOFF(row, col)] = f2bf(xv > 0.f ? dx[i][j][r] * inv_keep : 0.f);
       }
   __syncthreads();
-  bf16_t* GX = grad + tl.gx_off + k0;
+  bf16_t* GX = grad + tl.gx_off + (size_t)rbx * BM * K + k0;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
@@ -685,24 +732,37 @@ __global__ __launch_bounds__(256) void mlp_init_kernel(const InitDesc* __restric
 // (mopt_mlp_set_bwd_prefetch; MOPT_BWD_PREFETCH=0 in metaopt_amd/ops/population.py).
 static int g_bwd_prefetch = 1;
 
-template <int OPT, bool PF>
-static void launch_bwd(int n_work, hipStream_t stream, const void* tls, const void* work,
-                       const void* xb, void* grad, void* plo, void* p16, void* m32, void* v32,
-                       const void* hp, int flags) {
-  hipLaunchKernelGGL((mlp_bwd_opt_kernel<OPT, PF>), dim3(n_work), dim3(256), 0, stream,
-                     (const MlpTL*)tls, (const int2*)work, n_work, (const bf16_t*)xb,
+template <int OPT, bool PF, int MODE>
+static void launch_bwd(int n_work, int grid_y, hipStream_t stream, const void* tls,
+                       const void* work, const void* xb, void* grad, void* plo, void* p16,
+                       void* m32, void* v32, const void* hp, int flags) {
+  hipLaunchKernelGGL((mlp_bwd_opt_kernel<OPT, PF, MODE>), dim3(n_work, grid_y), dim3(256), 0,
+                     stream, (const MlpTL*)tls, (const int2*)work, n_work, (const bf16_t*)xb,
                      (bf16_t*)grad, (bf16_t*)plo, (bf16_t*)p16, (float*)m32, (float*)v32,
                      (const TrialHP*)hp, flags);
 }
 
+// one layer's backward: 128-row batches -> the fused MODE 0 kernel (prefetch per the switch);
+// R > 1 row blocks -> MODE 2 (dX of blocks 1..R-1, before W changes) then the fused MODE 1
 template <int OPT>
-static void launch_bwd_pf(int n_work, hipStream_t stream, const void* tls, const void* work,
-                          const void* xb, void* grad, void* plo, void* p16, void* m32, void* v32,
-                          const void* hp, int flags) {
-  if (g_bwd_prefetch)
-    launch_bwd<OPT, true>(n_work, stream, tls, work, xb, grad, plo, p16, m32, v32, hp, flags);
-  else
-    launch_bwd<OPT, false>(n_work, stream, tls, work, xb, grad, plo, p16, m32, v32, hp, flags);
+static void launch_bwd_rows(int n_work, int n_rowblocks, hipStream_t stream, const void* tls,
+                            const void* work, const void* xb, void* grad, void* plo, void* p16,
+                            void* m32, void* v32, const void* hp, int flags) {
+  if (n_rowblocks <= 1) {
+    // AdamW's second register set (M and V in f32) does not fit next to the MFMA operands: the
+    // prefetch variant spills (256 VGPRs + scratch), so AdamW always runs the plain one
+    if (g_bwd_prefetch && OPT != kAdamW)
+      launch_bwd<OPT, true, 0>(n_work, 1, stream, tls, work, xb, grad, plo, p16, m32, v32, hp,
+                               flags);
+    else
+      launch_bwd<OPT, false, 0>(n_work, 1, stream, tls, work, xb, grad, plo, p16, m32, v32, hp,
+                                flags);
+    return;
+  }
+  if (flags & kHasDx)
+    launch_bwd<OPT, false, 2>(n_work, n_rowblocks - 1, stream, tls, work, xb, grad, plo, p16,
+                              m32, v32, hp, flags);
+  launch_bwd<OPT, false, 1>(n_work, 1, stream, tls, work, xb, grad, plo, p16, m32, v32, hp, flags);
 }
 
 }  // namespace
@@ -712,7 +772,7 @@ static void launch_bwd_pf(int n_work, hipStream_t stream, const void* tls, const
 // ------------------------------------------------------------------------------------------------
 extern "C" {
 
-int mopt_abi_version() { return 8; }
+int mopt_abi_version() { return 9; }
 
 // 1 when this library is the bounds-checked variant (-DMOPT_BOUNDS_CHECK)
 int mopt_checked_build() { return MOPT_CHECKED_BUILD; }
@@ -758,15 +818,19 @@ int mopt_mlp_set_bwd_prefetch(int on) {
 
 int mopt_mlp_bwd(const void* tls, const void* work, int n_work, const void* xb, void* grad,
                  void* plo, void* p16, void* m32, void* v32, const void* hp, int opt, int flags,
-                 void* stream) {
+                 int n_rowblocks, void* stream) {
   if (n_work <= 0) return 0;
+  if (n_rowblocks < 1 || n_rowblocks > 64) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   if (opt == kAdamW)
-    launch_bwd_pf<kAdamW>(n_work, st, tls, work, xb, grad, plo, p16, m32, v32, hp, flags);
+    launch_bwd_rows<kAdamW>(n_work, n_rowblocks, st, tls, work, xb, grad, plo, p16, m32, v32, hp,
+                            flags);
   else if (opt == kSGD16)
-    launch_bwd_pf<kSGD16>(n_work, st, tls, work, xb, grad, plo, p16, m32, v32, hp, flags);
+    launch_bwd_rows<kSGD16>(n_work, n_rowblocks, st, tls, work, xb, grad, plo, p16, m32, v32, hp,
+                            flags);
   else
-    launch_bwd_pf<kSGD>(n_work, st, tls, work, xb, grad, plo, p16, m32, v32, hp, flags);
+    launch_bwd_rows<kSGD>(n_work, n_rowblocks, st, tls, work, xb, grad, plo, p16, m32, v32, hp,
+                          flags);
   return (int)hipGetLastError();
 }
 
@@ -782,14 +846,20 @@ struct MlpStep {
   int32_t n_bwd[8];
   int32_t L, rb, drop, opt;
   void *plo, *p16, *m32, *v32, *act, *grad, *hp, *loss, *correct;
-  float inv_b;
-  int32_t pad;
+  float inv_b;      // <= 0: each trial's mean over its own rows (MlpTL::rows)
+  int32_t n_stats;  // entries of loss / correct (the population's capacity)
 };
 
 int mopt_mlp_step(const MlpStep* s, const void* x, const void* y, void* stream) {
   if (s == nullptr || s->L < 1 || s->L > 8 || s->rb < 1) return (int)hipErrorInvalidValue;
   const int L = s->L;
   int err;
+  if (s->rb > 1) {   // several row blocks add into the statistics (one stream per population)
+    if (s->n_stats < 1) return (int)hipErrorInvalidValue;
+    err = (int)hipMemsetAsync(s->loss, 0, sizeof(float) * s->n_stats, (hipStream_t)stream);
+    if (!err) err = (int)hipMemsetAsync(s->correct, 0, sizeof(float) * s->n_stats, (hipStream_t)stream);
+    if (err) return err;
+  }
   for (int l = 0; l < L - 1; ++l) {
     err = mopt_mlp_fwd(s->tls, s->fwd[l], s->n_fwd[l], s->rb, l == 0 ? x : s->act, s->plo,
                        s->p16, s->act, s->hp, 1u, l, kRelu | (s->drop ? kDropout : 0), stream);
@@ -804,7 +874,7 @@ int mopt_mlp_step(const MlpStep* s, const void* x, const void* y, void* stream) 
     int flags = kUpdateBias;
     if (l > 0) flags |= kHasDx | (s->drop ? kInDropout : 0);
     err = mopt_mlp_bwd(s->tls, s->bwd[l], s->n_bwd[l], l == 0 ? x : s->act, s->grad, s->plo,
-                       s->p16, s->m32, s->v32, s->hp, s->opt, flags, stream);
+                       s->p16, s->m32, s->v32, s->hp, s->opt, flags, s->rb, stream);
     if (err) return err;
   }
   return 0;

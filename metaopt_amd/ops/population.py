@@ -37,7 +37,7 @@ from . import reference as ref
 
 TL_DTYPE = np.dtype([("K", "<i4"), ("N", "<i4"), ("trial", "<i4"), ("n_real", "<i4"),
                      ("w_off", "<i8"), ("b_off", "<i8"), ("x_off", "<i8"), ("y_off", "<i8"),
-                     ("gx_off", "<i8"), ("pad", "<i8")])
+                     ("gx_off", "<i8"), ("rows", "<i8")])
 HP_DTYPE = np.dtype([("lr", "<f4"), ("b1", "<f4"), ("wd", "<f4"), ("drop", "<f4"),
                      ("b2", "<f4"), ("eps", "<f4"), ("seed", "<u4"), ("t", "<u4")])
 INIT_DTYPE = np.dtype([("w_off", "<i8"), ("b_off", "<i8"), ("K", "<i4"), ("N", "<i4"),
@@ -46,6 +46,7 @@ INIT_DTYPE = np.dtype([("w_off", "<i8"), ("b_off", "<i8"), ("K", "<i4"), ("N", "
 assert TL_DTYPE.itemsize == 64 and HP_DTYPE.itemsize == 32 and INIT_DTYPE.itemsize == 48
 
 TILE = 64
+MAX_ROWS = 64 * 128     # csrc/pop_mlp.hip mopt_mlp_bwd: at most 64 row blocks per launch
 FWD_RELU, FWD_DROPOUT, FWD_WRITE_GRAD, FWD_STORE_STATS, FWD_COUNT_STEP = 1, 2, 4, 8, 16
 BWD_HAS_DX, BWD_IN_DROPOUT, BWD_UPDATE_BIAS = 1, 2, 4
 
@@ -59,7 +60,7 @@ class _MlpStep(ctypes.Structure):
                 ("drop", ctypes.c_int32), ("opt", ctypes.c_int32)] + \
                [(n, ctypes.c_void_p) for n in ("plo", "p16", "m32", "v32", "act", "grad", "hp",
                                                "loss", "correct")] + \
-               [("inv_b", ctypes.c_float), ("pad", ctypes.c_int32)]
+               [("inv_b", ctypes.c_float), ("n_stats", ctypes.c_int32)]
 OPTIMIZERS = {"sgd": 0, "adamw": 1}
 
 
@@ -89,6 +90,7 @@ class MemberConfig:
     seed: int = 0
     beta2: float = 0.999
     eps: float = 1e-8
+    batch_size: int = 0            # rows per step (a multiple of 128); 0 = the population's batch
 
     def to_dict(self) -> dict:
         # field by field (dataclasses.asdict deep-copies recursively: a visible cost when the
@@ -104,10 +106,11 @@ class StatsSnapshot:
     stream (pinned, non-blocking): :meth:`get` waits for that copy only, so the host can read
     the statistics of an earlier sync while the GPU already trains the next interval."""
 
-    __slots__ = ("capacity", "_host", "_ev")
+    __slots__ = ("capacity", "rows", "_host", "_ev")
 
-    def __init__(self, stats: torch.Tensor, capacity: int):
+    def __init__(self, stats: torch.Tensor, capacity: int, rows=None):
         self.capacity = capacity
+        self.rows = rows          # per-slot train rows when the copy was queued (or None)
         if stats.device.type == "cuda":
             self._host = torch.empty(stats.shape, dtype=stats.dtype, pin_memory=True)
             self._host.copy_(stats, non_blocking=True)
@@ -210,10 +213,10 @@ class PopulationMLP:
         self._parts: list = []
         self._side_pending = False    # side streams hold work the main stream has not joined
         self._fork_needed = True      # the main stream holds work the side streams must follow
-        if backend == "hip" and batch_size != 128:
-            raise ValueError("the fused backward kernel is tiled for 128-row batches")
-        if batch_size % 128 or eval_batch % 128:
+        if batch_size % 128 or eval_batch % 128 or batch_size < 128:
             raise ValueError("batch sizes must be multiples of 128")
+        if batch_size > MAX_ROWS:
+            raise ValueError(f"batch_size above {MAX_ROWS} (64 row blocks of 128)")
         self.capacity = int(capacity)
         self.in_features = int(in_features)
         self.num_classes = int(num_classes)
@@ -258,6 +261,7 @@ class PopulationMLP:
         self.hp = np.zeros(self.capacity, dtype=HP_DTYPE)
         self.hp_dev = torch.zeros(self.capacity * HP_DTYPE.itemsize, dtype=torch.uint8, device=dev)
         self.members: List[Optional[MemberConfig]] = [None] * self.capacity
+        self._rows_np = np.full(self.capacity, self.batch_size, dtype=np.float64)
         self._pending_init = set()
         self._dirty = True
         self._tables: Dict[str, dict] = {}
@@ -304,9 +308,9 @@ class PopulationMLP:
     def flops_per_step(self, slot: int) -> int:
         """Padded MFMA FLOPs of one train step (fwd + dX + dW) of the member in ``slot``."""
         cfg = self.members[slot]
-        f = 0
+        f, rows = 0, self.member_rows(cfg)
         for l, (k, n) in enumerate(self.layer_dims(cfg.width)):
-            f += 2 * self.batch_size * k * n * (3 if l > 0 else 2)
+            f += 2 * rows * k * n * (3 if l > 0 else 2)
         return f
 
     def bytes_per_step(self, slot: int) -> int:
@@ -317,6 +321,22 @@ class PopulationMLP:
         return per * self.padded_params(slot)
 
     # ------------------------------------------------------------------ members
+    def member_rows(self, cfg: MemberConfig) -> int:
+        """Rows per train step of a member: its own batch size, or the population's.  A member
+        with a smaller batch trains on the first rows of each (population-sized) minibatch; its
+        loss and gradient are means over its own rows (TL ``rows``, csrc/pop_mlp.hip)."""
+        return int(cfg.batch_size) or self.batch_size
+
+    def _check_member(self, cfg: MemberConfig) -> None:
+        if cfg.width > self.max_width or cfg.width < 1:
+            raise ValueError(f"width {cfg.width} outside [1, {self.max_width}]")
+        if not (0.0 <= cfg.dropout < 1.0):
+            raise ValueError("dropout must be in [0, 1)")
+        b = int(cfg.batch_size)
+        if b and (b % 128 or b < 0 or b > self.batch_size):
+            raise ValueError(f"member batch_size {b} must be a multiple of 128 and <= the "
+                             f"population's {self.batch_size}")
+
     def active_slots(self) -> List[int]:
         return [i for i, m in enumerate(self.members) if m is not None]
 
@@ -337,10 +357,7 @@ class PopulationMLP:
 
         Initialisation is deferred and batched: every member set before the next train/eval call
         is initialised by one kernel launch."""
-        if cfg.width > self.max_width or cfg.width < 1:
-            raise ValueError(f"width {cfg.width} outside [1, {self.max_width}]")
-        if not (0.0 <= cfg.dropout < 1.0):
-            raise ValueError("dropout must be in [0, 1)")
+        self._check_member(cfg)
         self.members[slot] = cfg
         self._write_hp(slot, cfg, 0)
         if init:
@@ -352,6 +369,7 @@ class PopulationMLP:
         cfg = dataclasses.replace(self.members[slot], **changes)
         if cfg.width != self.members[slot].width:
             raise ValueError("width cannot change in place")
+        self._check_member(cfg)
         t = int(self.hp[slot]["t"])
         self.members[slot] = cfg
         self._write_hp(slot, cfg, t)
@@ -661,13 +679,16 @@ class PopulationMLP:
         if self.optimizer == "adamw":
             self.v32[rd].copy_(self.v32[rs])
         cfg = dataclasses.replace(self.members[src], **hp_changes)
+        self._check_member(cfg)
         self.members[dst] = cfg
         self._write_hp(dst, cfg, int(self.hp[src]["t"]))
         self._dirty = True
 
     # ------------------------------------------------------------------ tables
-    def _build_tables(self, rows: int) -> dict:
-        """Trial-layer descriptors + per-layer work lists, built with numpy (no per-item loops)."""
+    def _build_tables(self, rows: int, member_rows: bool = False) -> dict:
+        """Trial-layer descriptors + per-layer work lists, built with numpy (no per-item loops).
+        ``rows``: the launch's rows (buffer layout); with ``member_rows`` each trial-layer uses
+        its member's own batch (train), else all ``rows`` (evaluation)."""
         L = self.L
         tl = np.zeros(self.capacity * L, dtype=TL_DTYPE)
         act_slot = rows * self.act_row
@@ -677,6 +698,8 @@ class PopulationMLP:
         bwd: List[np.ndarray] = []
         if len(slots):
             widths = np.array([self.members[s].width for s in slots])
+            used = (np.array([self.member_rows(self.members[s]) for s in slots], dtype=np.int64)
+                    if member_rows else np.full(len(slots), rows, dtype=np.int64))
             # per-slot layer dims / offsets (vectorised over slots, looped over the few layers)
             wp = (widths + TILE - 1) // TILE * TILE
             Ks, Ns = [], []
@@ -703,6 +726,7 @@ class PopulationMLP:
                 tl["x_off"][i] = prev
                 tl["y_off"][i] = y_off
                 tl["gx_off"][i] = prev if l > 0 else -1
+                tl["rows"][i] = used
                 nt, nk = N // TILE, K // TILE
                 fo = _lpt_order(np.repeat(K, nt))     # a forward tile costs ~K
                 bo = _lpt_order(np.repeat(N, nk))     # a backward k-strip costs ~N
@@ -748,6 +772,8 @@ class PopulationMLP:
             bad.append("first layer K differs from the input width")
         if (t["y_off"] < 0).any() or (t["y_off"] + rows * t["N"].astype(np.int64) > act).any():
             bad.append("layer output outside the activation buffer")
+        if (t["rows"] < 128).any() or (t["rows"] % 128).any() or (t["rows"] > rows).any():
+            bad.append("trial rows outside the launch's row blocks")
         if (t["n_real"] > t["N"]).any() or (t["trial"] < 0).any() or \
                 (t["trial"] >= self.capacity).any():
             bad.append("trial / class fields out of range")
@@ -770,7 +796,10 @@ class PopulationMLP:
         if not self._dirty:
             return
         self._join()
-        self._tables = {"train": self._build_tables(self.batch_size)}  # eval: built lazily
+        self._tables = {"train": self._build_tables(self.batch_size, member_rows=True)}
+        # per-slot train rows (the loss statistics are sums over them); eval: built lazily
+        self._rows_np = np.array([self.member_rows(m) if m is not None else self.batch_size
+                                  for m in self.members], dtype=np.float64)
         if self.device.type == "cuda":
             self._upload_hp()
         self._active_np = np.array([m is not None for m in self.members])
@@ -800,10 +829,11 @@ class PopulationMLP:
             a.fwd[l], a.bwd[l] = part["fwd"][l], part["bwd"][l]
             a.n_fwd[l], a.n_bwd[l] = part["n_fwd"][l], part["n_bwd"][l]
         a.L, a.rb, a.drop = L, self.batch_size // 128, int(self._any_dropout)
+        a.n_stats = self.capacity      # > 1 row block: the step zeroes loss/correct first
         a.opt = 2 if self.momentum_dtype == "bf16" else OPTIMIZERS[self.optimizer]
         for n in ("plo", "p16", "m32", "v32", "act", "grad", "hp", "loss", "correct"):
             setattr(a, n, P[n])
-        a.inv_b = 1.0 / self.batch_size
+        a.inv_b = -1.0                 # the mean over each trial's own rows
         part["step_ptr"] = ctypes.addressof(a)
         return a
 
@@ -825,6 +855,8 @@ class PopulationMLP:
         ``{"fwd": [ptr per layer], "bwd": [...], "n_fwd": [...], "n_bwd": [...]}`` per group."""
         slots = self.active_slots()
         n = min(self.n_streams, max(1, len(slots)))
+        if self.batch_size > 128:
+            n = 1   # the step's stats zeroing covers every trial: one stream orders it
         if n <= 1:
             return [{"fwd": [w.data_ptr() for w in tb["fwd"]],
                      "bwd": [w.data_ptr() for w in tb["bwd"]],
@@ -892,8 +924,6 @@ class PopulationMLP:
         self.hp["t"][self._active_np] += n
         from ._lib import check
         lib, main = self._lib, torch.cuda.current_stream(self.device)
-        if self.batch_size // 128 != 1:
-            raise ValueError("train_steps needs 128-row batches")
         parts = self._parts
         if len(parts) > 1:
             if self._fork_needed:
@@ -914,10 +944,9 @@ class PopulationMLP:
         main = torch.cuda.current_stream(self.device)
         # one 128-row block per trial: the loss kernel stores the statistics (no zero-fill) and
         # advances the device step counters; the hidden layers run before it, so they key their
-        # dropout masks with t + 1 (the step being taken)
+        # dropout masks with t + 1 (the step being taken).  More row blocks: the step zeroes the
+        # statistics and the loss kernel adds into them.
         rb = self.batch_size // 128
-        if rb != 1:
-            self.stats[:2 * self.capacity].zero_()
         xp = x.data_ptr() if x.is_contiguous() else x.contiguous().data_ptr()
         parts = self._parts
         if len(parts) > 1:
@@ -942,6 +971,8 @@ class PopulationMLP:
             return
         L = self.L
         ce_flags = FWD_WRITE_GRAD | FWD_COUNT_STEP | (FWD_STORE_STATS if rb == 1 else 0)
+        if rb != 1:
+            self.stats[:2 * self.capacity].zero_()
         drop = self._any_dropout
         act, tl = P["act"], P["tl"]
         for l in range(L - 1):
@@ -951,7 +982,7 @@ class PopulationMLP:
         check(lib.mopt_mlp_fwd_ce(tl, part["fwd"][L - 1], part["n_fwd"][L - 1], rb,
                                   xp if L == 1 else act, P["plo"], P["p16"], yp,
                                   P["grad"], P["loss"], P["correct"], P["hp"],
-                                  1.0 / self.batch_size, ce_flags, stream), "mlp_fwd_ce")
+                                  -1.0, ce_flags, stream), "mlp_fwd_ce")
         opt = 2 if self.momentum_dtype == "bf16" else OPTIMIZERS[self.optimizer]
         for l in range(L - 1, -1, -1):
             flags = BWD_UPDATE_BIAS
@@ -959,14 +990,15 @@ class PopulationMLP:
                 flags |= BWD_HAS_DX | (BWD_IN_DROPOUT if drop else 0)
             check(lib.mopt_mlp_bwd(tl, part["bwd"][l], part["n_bwd"][l], xp if l == 0 else act,
                                    P["grad"], P["plo"], P["p16"], P["m32"], P["v32"], P["hp"],
-                                   opt, flags, stream), "mlp_bwd")
+                                   opt, flags, rb, stream), "mlp_bwd")
 
     def _train_step_torch(self, x, y) -> None:
         self.stats.zero_()
         em = self.emulate_bf16
-        xf = x.float()
         for s in self.active_slots():
             cfg = self.members[s]
+            rows = self.member_rows(cfg)
+            xf, ys = x[:rows].float(), y[:rows]
             t = int(self.hp[s]["t"])
             layers = self.layer_views(s)
             mom = self.layer_views(s, self.m32)
@@ -979,7 +1011,7 @@ class PopulationMLP:
             w, b = layers[-1]
             wq = ref.bf16_weight(w) if em else w
             logits = a @ wq.t() + b
-            ls, cs, dz = ref.softmax_ce(logits, y, self.num_classes, 1.0 / self.batch_size, em)
+            ls, cs, dz = ref.softmax_ce(logits, ys, self.num_classes, 1.0 / rows, em)
             self.loss[s] = ls
             self.correct[s] = cs
             inv_keep = ref._inv_keep(cfg.dropout) if cfg.dropout > 0 else 1.0
@@ -1083,12 +1115,13 @@ class PopulationMLP:
 
     def stats_snapshot_async(self) -> StatsSnapshot:
         self._join()
-        return StatsSnapshot(self.stats, self.capacity)
+        return StatsSnapshot(self.stats, self.capacity, self._rows_np.copy())
 
-    def raw_results(self, snap: np.ndarray, handle):
+    def raw_results(self, snap: np.ndarray, handle, rows=None):
         """(train loss, eval loss, eval accuracy) per slot from a snapshot, unmasked: the slots
-        may have been re-assigned since the snapshot was queued."""
-        tl = snap[0].astype(np.float64) / self.batch_size
+        may have been re-assigned since the snapshot was queued (``rows``: the per-slot train
+        rows of that time, ``StatsSnapshot.rows``; default the current ones)."""
+        tl = snap[0].astype(np.float64) / (self._rows_np if rows is None else rows)
         if handle is None:
             nan = np.full(self.capacity, np.nan)
             return tl, nan, nan
@@ -1108,7 +1141,7 @@ class PopulationMLP:
     def train_loss(self, snap: Optional[np.ndarray] = None) -> np.ndarray:
         """Mean training loss of the last step per slot."""
         snap = self.stats_snapshot() if snap is None else snap
-        out = snap[0].astype(np.float64) / self.batch_size
+        out = snap[0].astype(np.float64) / self._rows_np
         out[~np.array([m is not None for m in self.members])] = np.nan
         return out
 

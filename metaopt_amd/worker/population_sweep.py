@@ -50,7 +50,8 @@ NONE, NEW, RESUME, CLEAR, RESUME_FILE = 0, 1, 2, 3, 4
 SIDECAR_FILE = "device_state.pt"     # per-trial device-state sidecar inside the trial's working_dir
 # status row: key, steps, budget, nan flag | result key, train loss, val loss, val acc, broken
 ST_COLS = 9
-AS_COLS = 11    # action, key, width, lr, momentum, wd, dropout, seed, budget, resume_key, src_rank
+# action, key, width, lr, momentum, wd, dropout, seed, budget, resume_key, src_rank, batch rows
+AS_COLS = 12
 
 
 class PopulationSweep:
@@ -319,7 +320,7 @@ class PopulationSweep:
             self._bad_now = np.zeros(P, dtype=bool)
             if prev is not None and prev[0] is not None:
                 psnap, phandle, pkeys, pfinished, self._result_step = prev
-                tl, vl, va = pop.raw_results(psnap.get(), phandle)
+                tl, vl, va = pop.raw_results(psnap.get(), phandle, getattr(psnap, "rows", None))
                 # members still training that already diverged one interval ago
                 live = active & (pkeys == self.slot_key)
                 bad = live & ~np.isfinite(tl)
@@ -331,7 +332,7 @@ class PopulationSweep:
             self._drain_writes()
             self._result_step = self.global_step
             if snap is not None:
-                tl, vl, va = pop.raw_results(snap.get(), handle)
+                tl, vl, va = pop.raw_results(snap.get(), handle, getattr(snap, "rows", None))
                 st[:, 3] = active & ~np.isfinite(tl)
                 self._fill_results(st, finished, self.slot_key, tl, vl, va, handle)
             self._bad_now = st[:, 3] > 0
@@ -642,8 +643,10 @@ class PopulationSweep:
         else:
             cfg = self.task.member_config(params, seed)
             hp = (cfg.width, cfg.lr, cfg.momentum, cfg.weight_decay, cfg.dropout, cfg.seed)
+        batch_fn = getattr(self.task, "batch_rows", None)
         rows.append(row)
-        vals.append((action, key) + tuple(hp) + (budget, resume, src))
+        vals.append((action, key) + tuple(hp) + (budget, resume, src,
+                                                 batch_fn(params) if batch_fn else 0))
 
     def _point_key(self, point, params=None) -> str:
         """Identity of a suggested point's configuration regardless of its fidelity (python
@@ -971,6 +974,8 @@ class PopulationSweep:
             cfg = MemberConfig(width=int(a[2]), lr=float(a[3]), momentum=float(a[4]),
                                weight_decay=float(a[5]), dropout=float(a[6]), seed=int(a[7]),
                                **getattr(self.task, "member_defaults", {}))
+            if a[11]:
+                cfg.batch_size = int(a[11])
             # checkpoints are not consumed: a PBT winner can seed several members
             meta = self.ckpts.get(int(a[9])) if act == RESUME and s not in received else None
             state = self._load_sidecar(int(a[9]), cfg.width) if act == RESUME_FILE else None
@@ -994,8 +999,9 @@ class PopulationSweep:
         if loads:
             pop.load_states(loads)
         for s, cfg in hp_updates:
+            extra = {"batch_size": cfg.batch_size} if cfg.batch_size else {}
             pop.update_hparams(s, lr=cfg.lr, momentum=cfg.momentum,
-                               weight_decay=cfg.weight_decay, dropout=cfg.dropout)
+                               weight_decay=cfg.weight_decay, dropout=cfg.dropout, **extra)
             self.n_resumed += 1
         self.done = bool(assign[-1, 0])
         self._n_active = int((self.slot_key >= 0).sum())

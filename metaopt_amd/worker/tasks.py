@@ -15,6 +15,8 @@ lm-tiny    2-layer LM (d 256), same data (config 4's model)                  pbt
 """
 from __future__ import annotations
 
+import numbers
+
 from dataclasses import dataclass, field
 from typing import Callable, Dict, Tuple
 
@@ -62,23 +64,45 @@ def _max_width(priors, default):
     return max(64, width)
 
 
+def _max_batch(priors, default=128):
+    """Population batch rows: the largest ``/batch_size`` the prior can draw (a categorical of
+    multiples of 128, e.g. ``choices([128, 256, 512])``); members use their own first rows."""
+    if "/batch_size" not in priors:
+        return default
+    from ..space.builder import DimensionBuilder
+    dim = DimensionBuilder().build("/batch_size", priors["/batch_size"])
+    values = getattr(dim, "categories", None)
+    if dim.type != "categorical" or not values:
+        raise ValueError("/batch_size must be a choices([...]) prior of multiples of 128")
+    bad = [v for v in values if not isinstance(v, numbers.Real) or int(v) != v or int(v) % 128
+           or int(v) < 128]
+    if bad:
+        raise ValueError(f"/batch_size choices must be multiples of 128, got {bad}")
+    from ..ops.population import MAX_ROWS
+    top = max(int(v) for v in values)
+    if top > MAX_ROWS:
+        raise ValueError(f"/batch_size up to {top}: the population kernels take <= {MAX_ROWS}")
+    return top
+
+
 def _mlp(population, device, seed, logreg=False, priors=None, state_dtype="bf16", **kw):
     from ..models.data import TeacherClassification
     from ..models.mlp import LOGREG_PRIORS, MLP_PRIORS, MLPSweepTask
     from ..ops.population import PopulationMLP
     priors = dict(priors or (LOGREG_PRIORS if logreg else MLP_PRIORS))
     max_width = 64 if logreg else _max_width(priors, 1024)
+    batch = _max_batch(priors)
     task = MLPSweepTask(priors=priors, n_hidden=0 if logreg else 3,
                         in_features=2 if logreg else 784, num_classes=2 if logreg else 10,
                         width=64 if logreg else min(256, max_width), max_width=max_width)
     data = TeacherClassification(n_train=8192 if logreg else 60032, n_val=1024,
                                  in_features=task.in_features, num_classes=task.num_classes,
                                  teacher_hidden=4 if logreg else 128, seed=1234 + seed,
-                                 device=device)
+                                 batch_size=batch, device=device)
     on_gpu = str(device).startswith("cuda")
     pop = PopulationMLP(population, in_features=task.in_features, num_classes=task.num_classes,
                         n_hidden=task.n_hidden, max_width=task.max_width,
-                        eval_batch=1024, device=device,
+                        batch_size=batch, eval_batch=1024, device=device,
                         momentum_dtype="bf16" if (state_dtype == "bf16" and on_gpu) else "fp32")
     return task, pop, data
 
@@ -122,14 +146,14 @@ TASKS: Dict[str, TaskSpec] = {
                        lambda seed, n: {"random": {"seed": seed}},
                        lambda p, d, s, **kw: _mlp(p, d, s, logreg=True, **kw), 8192,
                        "trials/s (1 trial = one pass over 8,192 samples)",
-                       tunable=("/lr", "/weight_decay", "/momentum", "/steps")),
+                       tunable=("/lr", "/weight_decay", "/momentum", "/steps", "/batch_size")),
     "mlp": TaskSpec({"/lr": "loguniform(1e-3, 1.0)",
                      "/width": "loguniform(64, 1024, discrete=True)",
                      "/dropout": "uniform(0, 0.5)", "/steps": "fidelity(32, 2048, 4)"},
                     lambda seed, n: {"asha": {"seed": seed, "repetitions": float("inf")}},
                     _mlp, 60032, "trials/s (1 trial = 60,032 samples)",
                     tunable=("/lr", "/width", "/dropout", "/momentum", "/weight_decay",
-                             "/steps")),
+                             "/steps", "/batch_size")),
     "resnet20": TaskSpec({"/lr": "loguniform(0.01, 0.5)", "/momentum": "uniform(0.5, 0.99)",
                           "/weight_decay": "loguniform(1e-5, 1e-2)"},
                          lambda seed, n: {"tpe": {"seed": seed, "n_initial_points": n}},

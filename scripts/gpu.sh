@@ -11,6 +11,7 @@
 #   timeline         bench.py with the GPU-event timeline (MOPT_GPU_TIMELINE=1)
 #   streams          bench.py at MOPT_STREAMS=1,2
 #   kbench           per-kernel MLP microbench             trace_bench  rocprofv3 kernel trace
+#   kbench_rows      the microbench at 128 / 256 / 512 rows per step (multi-row-block kernels)
 #   pmc_kbench       PMC passes of the MLP kernels (fetch/write/MFMA/LDS, one pass each)
 #   lm resnet hyper  bench_configs.py of one config        trace_lm trace_resnet trace_hyper
 #   gemm conv        pgemm / direct-conv microbenches
@@ -47,6 +48,7 @@ for step in "$@"; do
     timeline)   MOPT_GPU_TIMELINE=1 $T 240 python bench.py --steps 20 --warmup 5 > "$OUT/bench_timeline.json" 2> "$OUT/bench_timeline.err" ;;
     streams)    for s in 1 2; do MOPT_STREAMS=$s $T 240 python bench.py --steps 20 --warmup 5 > "$OUT/bench_streams$s.json" 2> "$OUT/bench_streams$s.err"; done ;;
     kbench)     $T 200 python scripts/kernel_bench.py --momentum-dtype bf16 --out "$OUT/kbench.json" > "$OUT/kbench.log" 2>&1 ;;
+    kbench_rows) for b in 128 256 512; do $T 200 python scripts/kernel_bench.py --momentum-dtype bf16 --batch $b --iters 20 --out "$OUT/kbench_b$b.json" > "$OUT/kbench_b$b.log" 2>&1; done ;;
     trace_bench) prof trace_bench 300 -- python3 "$ROOT/bench.py" --steps 10 --warmup 3 ;;
     pmc_kbench)
       pmc pmc_fetch FETCH_SIZE

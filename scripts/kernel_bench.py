@@ -26,18 +26,20 @@ ap.add_argument("--width", type=int, default=0, help="fixed width (0: loguniform
 ap.add_argument("--optimizer", default="sgd")
 ap.add_argument("--momentum-dtype", default="fp32", choices=["fp32", "bf16"])
 ap.add_argument("--streams", type=int, default=1)
+ap.add_argument("--batch", type=int, default=128, help="rows per step (multiple of 128)")
 ap.add_argument("--out", default="")
 args = ap.parse_args()
 
 dev = torch.device("cuda")
 rng = np.random.RandomState(0)
 P = args.population
-pop = PopulationMLP(P, max_width=1024, device=dev, optimizer=args.optimizer,
+B, RB = args.batch, args.batch // 128
+pop = PopulationMLP(P, max_width=1024, device=dev, optimizer=args.optimizer, batch_size=B,
                     momentum_dtype=args.momentum_dtype, n_streams=args.streams)
 for s in range(P):
     w = args.width or int(np.exp(rng.uniform(np.log(64), np.log(1024))))
     pop.set_member(s, MemberConfig(width=w, lr=0.01, dropout=0.1, seed=s))
-data = TeacherClassification(n_train=128 * 8, n_val=128, batch_size=128, seed=0, device=dev)
+data = TeacherClassification(n_train=B * 8, n_val=128, batch_size=B, seed=0, device=dev)
 x, y = data.batch(0)
 for _ in range(5):
     pop.train_step(x, y)
@@ -52,15 +54,15 @@ BWD_BYTES = {0: 16, 1: 24, 2: 12}[opt]     # split master r+w 8, + momentum (+ A
 def run_fwd(l):
     src = x if l == 0 else pop.act
     if l < L - 1:
-        lib.mopt_mlp_fwd(tb["tl"].data_ptr(), tb["fwd"][l].data_ptr(), tb["n_fwd"][l], 1,
+        lib.mopt_mlp_fwd(tb["tl"].data_ptr(), tb["fwd"][l].data_ptr(), tb["n_fwd"][l], RB,
                          src.data_ptr(), pop.plo.data_ptr(), pop.p16.data_ptr(),
                          pop.act.data_ptr(), pop.hp_dev.data_ptr(), 0, l, FWD_RELU | FWD_DROPOUT,
                          stream)
     else:
-        lib.mopt_mlp_fwd_ce(tb["tl"].data_ptr(), tb["fwd"][l].data_ptr(), tb["n_fwd"][l], 1,
+        lib.mopt_mlp_fwd_ce(tb["tl"].data_ptr(), tb["fwd"][l].data_ptr(), tb["n_fwd"][l], RB,
                             src.data_ptr(), pop.plo.data_ptr(), pop.p16.data_ptr(), y.data_ptr(),
                             pop.grad.data_ptr(), pop.loss.data_ptr(), pop.correct.data_ptr(),
-                            pop.hp_dev.data_ptr(), 1.0 / 128, FWD_WRITE_GRAD, stream)
+                            pop.hp_dev.data_ptr(), -1.0, FWD_WRITE_GRAD, stream)
 
 
 def run_bwd(l):
@@ -69,7 +71,7 @@ def run_bwd(l):
     lib.mopt_mlp_bwd(tb["tl"].data_ptr(), tb["bwd"][l].data_ptr(), tb["n_bwd"][l], src.data_ptr(),
                      pop.grad.data_ptr(), pop.plo.data_ptr(), pop.p16.data_ptr(),
                      pop.m32.data_ptr(), pop.v32.data_ptr(), pop.hp_dev.data_ptr(), opt, flags,
-                     stream)
+                     pop.batch_size // 128, stream)
 
 
 tl = tb["tl_np"]
@@ -90,7 +92,7 @@ for name, fn, byte_per in [("fwd", run_fwd, 2), ("bwd", run_bwd, BWD_BYTES)]:
         ms = ev0.elapsed_time(ev1) / args.iters
         n = tb["n_fwd"][l] if name == "fwd" else tb["n_bwd"][l]
         gbps = layer_params[l] * byte_per / (ms * 1e-3) / 1e9
-        flops = 2 * 128 * layer_params[l] * (1 if name == "fwd" else (2 if l > 0 else 1))
+        flops = 2 * B * layer_params[l] * (1 if name == "fwd" else (2 if l > 0 else 1))
         results[f"{name}{l}"] = dict(ms=round(ms, 4), workgroups=n, params=layer_params[l],
                                      GBps=round(gbps, 1), TFLOPs=round(flops / ms / 1e9, 1))
         print(f"{name}{l}: {ms*1e3:8.1f} us  WG={n:6d}  params={layer_params[l]/1e6:7.2f}M "

@@ -133,7 +133,7 @@ def _pbt_worker(rank, world, port, q):
     st = pop.slot_state(0)
     sweep.ckpts[999] = pop.save_states([(0, sweep._free_ck.pop())])[0]
     assign = np.zeros((2 * 3 + 1, AS_COLS))
-    assign[3 + 2] = (RESUME, 0, 64, 0.1, 0.9, 0, 0, 7, 16, 999, 0)
+    assign[3 + 2] = (RESUME, 0, 64, 0.1, 0.9, 0, 0, 7, 16, 999, 0, 0)
     got = sweep._exchange_checkpoints(assign)
     c4 = None
     if rank == 1:

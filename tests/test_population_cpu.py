@@ -257,3 +257,80 @@ def test_init_descriptors_match_the_layer_layout():
                              np.float32(1.0) / np.sqrt(np.float32(kr)), 0))
         want = np.array(rows, dtype=got.dtype)
         assert (got == want).all()
+
+
+def test_per_member_batch_size_trains_on_its_own_rows():
+    """A member with ``batch_size`` 128 inside a 256-row population follows exactly the member
+    of a 128-row population fed the first 128 rows (reference backend); the loss statistics are
+    means over each member's own rows, also for a snapshot taken before its slot was reused."""
+    data = TeacherClassification(n_train=2048, n_val=256, batch_size=256, seed=8)
+    big = PopulationMLP(3, max_width=128, batch_size=256, device="cpu")
+    small = PopulationMLP(1, max_width=128, batch_size=128, device="cpu")
+    cfg = MemberConfig(width=96, lr=0.1, seed=4, dropout=0.2)
+    big.set_member(0, MemberConfig(**dict(cfg.to_dict(), batch_size=128)))
+    big.set_member(2, MemberConfig(width=64, lr=0.1, seed=5))          # 0: the population's 256
+    small.set_member(0, cfg)
+    for step in range(4):
+        x, y = data.batch(step)
+        big.train_step(x, y)
+        small.train_step(x[:128], y[:128])
+    assert big.train_loss()[0] == pytest.approx(small.train_loss()[0], rel=1e-6)
+    for (wa, ba), (wb, bb) in zip(big.layer_views(0), small.layer_views(0)):
+        assert torch.allclose(wa, wb, atol=1e-7) and torch.allclose(ba, bb, atol=1e-7)
+    # snapshot rows survive a slot reuse with another batch size
+    snap = big.stats_snapshot_async()
+    raw = snap.get().copy()
+    big.remove_member(0)
+    big.set_member(0, MemberConfig(width=64, lr=0.1, seed=6, batch_size=256))
+    big._refresh()
+    then, _, _ = big.raw_results(raw, None, snap.rows)
+    now, _, _ = big.raw_results(raw, None)
+    assert then[0] == pytest.approx(2 * now[0])
+
+
+def test_member_batch_size_is_validated():
+    pop = PopulationMLP(2, max_width=128, batch_size=256, device="cpu")
+    for bad in (64, 200, 384):
+        with pytest.raises(ValueError, match="batch_size"):
+            pop.set_member(0, MemberConfig(width=64, lr=0.1, batch_size=bad))
+    pop.set_member(0, MemberConfig(width=64, lr=0.1, batch_size=128))
+    with pytest.raises(ValueError, match="batch_size"):
+        pop.update_hparams(0, batch_size=512)
+    pop.update_hparams(0, batch_size=256)
+    tb = pop._build_tables(256, member_rows=True)
+    assert (tb["tl_np"]["rows"][:pop.L] == 256).all()
+    with pytest.raises(ValueError, match="multiples of 128"):
+        PopulationMLP(2, batch_size=100, device="cpu")
+    tl = tb["tl_np"].copy()
+    tl["rows"][0] = 384                                 # more rows than the launch holds
+    with pytest.raises(ValueError, match="trial rows"):
+        pop._validate_tables(tl, tb["fwd_np"], tb["bwd_np"], 256)
+
+
+def test_sweep_tunes_the_batch_size():
+    """``/batch_size`` as a searched hyper-parameter: the mlp task sizes the population for the
+    largest choice, each trial trains on its own rows, promotions keep the batch size."""
+    from metaopt_amd.worker import tasks
+    priors = {"/lr": "loguniform(1e-3, 1.0)", "/width": "loguniform(64, 128, discrete=True)",
+              "/batch_size": "choices([128, 256])", "/steps": "fidelity(16, 32, 2)"}
+    task, pop, data = tasks.get("mlp").build(4, "cpu", 0, priors=priors, state_dtype="fp32")
+    assert pop.batch_size == 256 and data.batch_size == 256
+    storage = DocumentStorage(EphemeralDB())
+    exp = build_experiment("sweep-batch", priors=priors,
+                           algorithms={"asha": {"seed": 2, "repetitions": float("inf")}},
+                           max_trials=10, storage=storage)
+    seen = set()
+    real = pop.set_member
+
+    def spy(slot, cfg, init=True):
+        seen.add(pop.member_rows(cfg))
+        return real(slot, cfg, init)
+    pop.set_member = spy
+    sweep = PopulationSweep(pop, task, data, experiment=exp, sync_every=16)
+    summary = sweep.run(1000)
+    sweep.close()
+    assert summary["completed"] == 10
+    assert seen == {128, 256}
+    for bad in ("choices([100, 256])", "uniform(128, 256)"):
+        with pytest.raises(ValueError, match="batch_size"):
+            tasks._max_batch({"/batch_size": bad})
