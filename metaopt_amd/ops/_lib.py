@@ -20,7 +20,7 @@ from . import build as _build
 
 _LOCK = threading.Lock()
 _LIB = None
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 c_void_p = ctypes.c_void_p
 c_int = ctypes.c_int
@@ -38,6 +38,7 @@ _SIGNATURES = {
     "mopt_mlp_bwd": ([c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                       c_void_p, c_void_p, c_int, c_int, c_int, c_void_p], c_int),
     "mopt_mlp_step": ([c_void_p, c_void_p, c_void_p, c_void_p], c_int),
+    "mopt_mlp_w_layout": ([], c_int),
     "mopt_mlp_steps": ([c_void_p, c_void_p, c_void_p, c_int, c_void_p], c_int),
     "mopt_mlp_set_bwd_prefetch": ([c_int], c_int),
 }

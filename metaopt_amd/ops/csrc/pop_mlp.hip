@@ -31,7 +31,7 @@ struct MlpTL {
   int32_t N;       // padded output features (multiple of 64)
   int32_t trial;   // population slot (index into the hyper-parameter table)
   int32_t n_real;  // real outputs (classes of the CE layer)
-  int64_t w_off;   // W [N][K] row-major: offset into the f32 master / bf16 / optimizer buffers
+  int64_t w_off;   // W [N][K] (layout: MOPT_W_STRIP below): offset into the parameter buffers
   int64_t b_off;   // bias [N]: offset into the f32 master / optimizer buffers
   int64_t x_off;   // layer input  [rows][K] bf16: offset into the x buffer of the launch
   int64_t y_off;   // layer output [rows][N] bf16: offset into act (forward) / grad (backward)
@@ -79,6 +79,31 @@ constexpr int TS = kLdsStride;
 #define FOFF(r, c) ((r) * (BN + 4) + (c))
 #endif
 
+// Weight layout in HBM (A/B switch, -DMOPT_W_STRIP=0|1).  1 (default): k-strip-major
+// [K/64][N][64] -- W[n][k] at (k / 64) N 64 + n 64 + k % 64, so the backward's k-strip is one
+// contiguous N x 128-B block and every 64 x 64 tile the forward or the backward touches is 8 KB
+// contiguous (a micro-benchmark of the backward's three-array read-modify-write by 64 x 64 tiles
+// measured 5.4 TB/s contiguous vs 4.65 TB/s with 128-B rows K * 2 bytes apart:
+// scripts/dev/tile_layout_bench.*).  0: row-major [N][K].  Same element set, same offsets of
+// the bias and of the optimizer state (which share the layout); metaopt_amd/ops/population.py
+// asks the library (mopt_mlp_w_layout) to view the weights row-major.
+#ifndef MOPT_W_STRIP
+#define MOPT_W_STRIP 1
+#endif
+__device__ __forceinline__ int w_row_stride(int K) { return MOPT_W_STRIP ? BK : K; }
+__device__ __forceinline__ int w_kstep(int N) { return MOPT_W_STRIP ? N : 1; }
+// stored index e -> (n, k)
+__device__ __forceinline__ void w_coords(int64_t e, int N, int K, int& n, int& k) {
+  if (MOPT_W_STRIP) {
+    const int64_t strip = e / ((int64_t)N * BK), r = e - strip * (int64_t)N * BK;
+    n = (int)(r / BK);
+    k = (int)(strip * BK + (r % BK));
+  } else {
+    n = (int)(e / K);
+    k = (int)(e - (int64_t)n * K);
+  }
+}
+
 // kStoreStats: one row block per trial -- store the trial's loss / #correct instead of
 // accumulating atomically into zeroed counters (saves the per-step zero-fill launch).
 // kCountStep: advance the trial's step counter hp.t (the hidden layers of the same step read
@@ -108,8 +133,8 @@ enum Opt { kSGD = 0, kAdamW = 1, kSGD16 = 2 };
     x1 = *(const uint4*)(X + g1 + kk_);                 \
     x2 = *(const uint4*)(X + g2 + kk_);                 \
     x3 = *(const uint4*)(X + g3 + kk_);                 \
-    w0 = *(const uint4*)(W + g0 + kk_);                 \
-    w1 = *(const uint4*)(W + g1 + kk_);                 \
+    w0 = *(const uint4*)(W + gw0 + (size_t)kk_ * WKS);  \
+    w1 = *(const uint4*)(W + gw1 + (size_t)kk_ * WKS);  \
   } while (0)
 #define MOPT_FWD_STORE(x0, x1, x2, x3, w0, w1) \
   do {                                         \
@@ -137,8 +162,10 @@ __device__ __forceinline__ void fwd_step(const bf16_t* As, const bf16_t* Bs, int
   }
 }
 
+// W: the tile's first row (w_off + w_tile_off(n0, N, K)); N: rows of the layer's weight matrix
 __device__ __forceinline__ void fwd_gemm(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
-                                         int K, bf16_t* As, bf16_t* Bs, f32x4 (&acc)[2][4]) {
+                                         int K, int N, bf16_t* As, bf16_t* Bs,
+                                         f32x4 (&acc)[2][4]) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, g = lane >> 4;
 #pragma unroll
@@ -149,6 +176,9 @@ __device__ __forceinline__ void fwd_gemm(const bf16_t* __restrict__ X, const bf1
   const int c0 = tid, c1 = tid + 256, c2 = tid + 512, c3 = tid + 768;
   const int g0 = (c0 >> 3) * K + (c0 & 7) * 8, g1 = (c1 >> 3) * K + (c1 & 7) * 8;
   const int g2 = (c2 >> 3) * K + (c2 & 7) * 8, g3 = (c3 >> 3) * K + (c3 & 7) * 8;
+  // W rows are WRS apart; a K-step of kk columns moves kk * WKS elements (w_row_stride / w_kstep)
+  const int WRS = w_row_stride(K), WKS = w_kstep(N);
+  const int gw0 = (c0 >> 3) * WRS + (c0 & 7) * 8, gw1 = (c1 >> 3) * WRS + (c1 & 7) * 8;
   bf16_t* as0 = As + TOFF(c0 >> 3, (c0 & 7) * 8);
   bf16_t* as1 = As + TOFF(c1 >> 3, (c1 & 7) * 8);
   bf16_t* as2 = As + TOFF(c2 >> 3, (c2 & 7) * 8);
@@ -183,9 +213,9 @@ __device__ __forceinline__ void fwd_gemm(const bf16_t* __restrict__ X, const bf1
 // (Measured and rejected: an LDS-free variant loading every MFMA fragment -- 16 bytes of one
 // row of X or W per lane -- straight from global memory ran the forward 2.5x slower than the
 // LDS-staged tiles above; profiles/README.md.)
-__device__ __forceinline__ void fwd_core(const bf16_t* X, const bf16_t* W, int K, bf16_t* As,
-                                         bf16_t* Bs, f32x4 (&acc)[2][4]) {
-  fwd_gemm(X, W, K, As, Bs, acc);
+__device__ __forceinline__ void fwd_core(const bf16_t* X, const bf16_t* W, int K, int N,
+                                         bf16_t* As, bf16_t* Bs, f32x4 (&acc)[2][4]) {
+  fwd_gemm(X, W, K, N, As, Bs, acc);
 }
 
 // Y[rows, n0:n0+64] = dropout(relu(X W^T + b)) for one (trial-layer, n-tile, 128-row block).
@@ -205,10 +235,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void m
   const int K = tl.K, N = tl.N, n0 = wi.y * BN, row0 = blockIdx.y * BM;
   if (row0 >= tl.rows) return;           // a smaller batch than the launch's: uniform exit
   const bf16_t* X = xb + tl.x_off + (size_t)row0 * K;
-  const bf16_t* W = p16 + tl.w_off + (size_t)n0 * K;
+  const bf16_t* W = p16 + tl.w_off + (size_t)n0 * w_row_stride(K);
 
   f32x4 acc[2][4];
-  fwd_core(X, W, K, As, Bs, acc);
+  fwd_core(X, W, K, N, As, Bs, acc);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, g = lane >> 4;
   const bf16_t* bias_hi = p16 + tl.b_off + n0;
@@ -278,7 +308,7 @@ __global__ __launch_bounds__(256) void mlp_fwd_ce_kernel(const MlpTL* __restrict
   const bf16_t* W = p16 + tl.w_off;
 
   f32x4 acc[2][4];
-  fwd_core(X, W, K, As, Bs, acc);
+  fwd_core(X, W, K, N, As, Bs, acc);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, g = lane >> 4;
   const bf16_t* bias_hi = p16 + tl.b_off;
@@ -360,8 +390,21 @@ __global__ __launch_bounds__(256) void mlp_fwd_ce_kernel(const MlpTL* __restrict
 // launched first; MODE 1 then does the fused pass -- dX of row block 0, dW summed over all R
 // blocks (the X strip and dZ chunk of blocks 1.. restaged through the same LDS tiles), the
 // update, the bias over all rows.  Trials with fewer rows than the launch skip the extra blocks.
+//
+// LDS (MOPT_BWD_ALIAS=1, default): the f32 dW staging tile aliases the dZ chunk tile (one more
+// barrier per chunk), 47 KB per workgroup instead of 64.5 KB, so three workgroups fit a CU's
+// 160 KB; the variant without the prefetch register set (<= 168 VGPRs) then runs 3 waves per
+// SIMD.  The prefetch variant needs more VGPRs and stays at 2.
+#ifndef MOPT_BWD_ALIAS
+#define MOPT_BWD_ALIAS 1
+#endif
+constexpr int bwd_waves(int opt, bool pf, int mode) {
+  // AdamW and the multi-row-block pass spill at 168 VGPRs: they keep 2 waves per SIMD
+  return (MOPT_BWD_ALIAS && !pf && opt != kAdamW && mode != 1) ? 3 : 2;
+}
 template <int OPT, bool PF, int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void mlp_bwd_opt_kernel(const MlpTL* __restrict__ tls,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
+    bwd_waves(OPT, PF, MODE), bwd_waves(OPT, PF, MODE)))) void mlp_bwd_opt_kernel(const MlpTL* __restrict__ tls,
                                                           const int2* __restrict__ work, int n_work,
                                                           const bf16_t* __restrict__ xb,
                                                           bf16_t* __restrict__ grad,
@@ -371,12 +414,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                                                           float* __restrict__ v32,
                                                           const TrialHP* __restrict__ hp, int flags) {
   constexpr int DS = BN + 4;  // f32 row stride bound of the dW staging tile (FOFF)
-  __shared__ __attribute__((aligned(16))) bf16_t smem[(2 * BM + BN) * TS + 2 * 4 * BN + 2 * BN * DS];
+  static_assert(BN * DS * 4 <= BM * TS * 2, "dW staging tile must fit the dZ tile");
+  __shared__ __attribute__((aligned(16)))
+      bf16_t smem[(2 * BM + BN) * TS + 2 * 4 * BN + (MOPT_BWD_ALIAS ? 0 : 2 * BN * DS)];
   bf16_t* Xs = smem;
   bf16_t* Zs = smem + BM * TS;
   bf16_t* Ws = smem + 2 * BM * TS;
   float* red = (float*)(smem + (2 * BM + BN) * TS);  // [4][64] bias partial sums
-  float* Dw = red + 4 * BN;                           // [64 n][DS] dW of the current chunk
+  // [64 n][DS] dW of the current chunk
+  float* Dw = MOPT_BWD_ALIAS ? (float*)Zs : red + 4 * BN;
 
   const int2 wi = work[xcd_remap(blockIdx.x, n_work)];
   const MlpTL tl = tls[wi.x];
@@ -432,7 +478,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   bf16_t* zs0 = Zs + TOFF(tid >> 3, (tid & 7) * 8);     // rows +32 i keep the swizzle
   // Optimizer-state layout: thread -> rows 16i + tid/16 (i < 4), 4 consecutive k at 4 * (tid % 16):
   // every wave-instruction moves 4 rows x 256 contiguous bytes of W/M (/V), full 128-B lines.
-  const int wo = (tid >> 4) * K + k0 + 4 * (tid & 15);
+  // (strip layout: the k-strip is one contiguous [N][64] block, rows 64 apart)
+  const int WRS = w_row_stride(K);
+  const size_t wo = (size_t)k0 * w_kstep(N) + (size_t)(tid >> 4) * WRS + 4 * (tid & 15);
   // (zero-initialised: MODE 2 loads only the hi halves and dZ; the rest stays unused)
   uint4 cz0{}, cz1{}, cz2{}, cz3{}, nz0{}, nz1{}, nz2{}, nz3{};
   f32x4 cm0{}, cm1{}, cm2{}, cm3{}, cv0{}, cv1{}, cv2{}, cv3{};
@@ -447,32 +495,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     P##z1 = *(const uint4*)(zc_ + zo1);                                                          \
     P##z2 = *(const uint4*)(zc_ + zo2);                                                          \
     P##z3 = *(const uint4*)(zc_ + zo3);                                                          \
-    const size_t ob = (size_t)(NC) * K + wo;                                                     \
+    const size_t ob = (size_t)(NC) * WRS + wo;                                                   \
     P##wh0 = *(const uint2*)(W16 + ob);                                                          \
-    P##wh1 = *(const uint2*)(W16 + ob + 16 * K);                                                 \
-    P##wh2 = *(const uint2*)(W16 + ob + 32 * K);                                                 \
-    P##wh3 = *(const uint2*)(W16 + ob + 48 * K);                                                 \
+    P##wh1 = *(const uint2*)(W16 + ob + 16 * WRS);                                                 \
+    P##wh2 = *(const uint2*)(W16 + ob + 32 * WRS);                                                 \
+    P##wh3 = *(const uint2*)(W16 + ob + 48 * WRS);                                                 \
     if (MODE != 2) {                                                                             \
     P##wl0 = *(const uint2*)(WLO + ob);                                                          \
-    P##wl1 = *(const uint2*)(WLO + ob + 16 * K);                                                 \
-    P##wl2 = *(const uint2*)(WLO + ob + 32 * K);                                                 \
-    P##wl3 = *(const uint2*)(WLO + ob + 48 * K);                                                 \
+    P##wl1 = *(const uint2*)(WLO + ob + 16 * WRS);                                                 \
+    P##wl2 = *(const uint2*)(WLO + ob + 32 * WRS);                                                 \
+    P##wl3 = *(const uint2*)(WLO + ob + 48 * WRS);                                                 \
     if (OPT == kSGD16) {                                                                         \
       P##h0 = *(const uint2*)(M16 + ob);                                                         \
-      P##h1 = *(const uint2*)(M16 + ob + 16 * K);                                                \
-      P##h2 = *(const uint2*)(M16 + ob + 32 * K);                                                \
-      P##h3 = *(const uint2*)(M16 + ob + 48 * K);                                                \
+      P##h1 = *(const uint2*)(M16 + ob + 16 * WRS);                                                \
+      P##h2 = *(const uint2*)(M16 + ob + 32 * WRS);                                                \
+      P##h3 = *(const uint2*)(M16 + ob + 48 * WRS);                                                \
     } else {                                                                                     \
       P##m0 = *(const f32x4*)(M32 + ob);                                                         \
-      P##m1 = *(const f32x4*)(M32 + ob + 16 * K);                                                \
-      P##m2 = *(const f32x4*)(M32 + ob + 32 * K);                                                \
-      P##m3 = *(const f32x4*)(M32 + ob + 48 * K);                                                \
+      P##m1 = *(const f32x4*)(M32 + ob + 16 * WRS);                                                \
+      P##m2 = *(const f32x4*)(M32 + ob + 32 * WRS);                                                \
+      P##m3 = *(const f32x4*)(M32 + ob + 48 * WRS);                                                \
     }                                                                                            \
     if (OPT == kAdamW) {                                                                         \
       P##v0 = *(const f32x4*)(V32 + ob);                                                         \
-      P##v1 = *(const f32x4*)(V32 + ob + 16 * K);                                                \
-      P##v2 = *(const f32x4*)(V32 + ob + 32 * K);                                                \
-      P##v3 = *(const f32x4*)(V32 + ob + 48 * K);                                                \
+      P##v1 = *(const f32x4*)(V32 + ob + 16 * WRS);                                                \
+      P##v2 = *(const f32x4*)(V32 + ob + 32 * WRS);                                                \
+      P##v3 = *(const f32x4*)(V32 + ob + 48 * WRS);                                                \
     }                                                                                            \
     }                                                                                            \
   }
@@ -593,6 +641,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // ---- optimizer epilogue: dW^T C-fragments (register r of dw[t][u] = dW[n][k + r]) are
     //      restaged through LDS into the row-contiguous layout of W/M (/V) ----
     if (MODE != 2) {
+    if (MOPT_BWD_ALIAS) __syncthreads();   // every wave is done reading Zs (dX, dW, bias)
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -602,7 +651,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const f32x4 gv = *(const f32x4*)(Dw + FOFF(16 * i + (tid >> 4), 4 * (tid & 15)));
-      const size_t o = (size_t)nc * K + wo + (size_t)(16 * i) * K;
+      const size_t o = (size_t)nc * WRS + wo + (size_t)(16 * i) * WRS;
       f32x4 wv = w[i], mv = m[i], vv;
       if (OPT == kAdamW) vv = v[i];
 #pragma unroll
@@ -710,9 +759,11 @@ __global__ __launch_bounds__(256) void mlp_init_kernel(const InitDesc* __restric
        e += (int64_t)gridDim.x * blockDim.x) {
     float v = 0.f;
     int64_t o;
-    if (e < nw) {
-      const int n = (int)(e / d.K), k = (int)(e - (int64_t)n * d.K);
-      if (n < d.n_real && k < d.k_real) v = (2.f * rng_uniform(wkey, (uint32_t)e) - 1.f) * d.bound;
+    if (e < nw) {   // e walks the stored layout; the RNG counter is the row-major index n K + k
+      int n, k;
+      w_coords(e, d.N, d.K, n, k);
+      if (n < d.n_real && k < d.k_real)
+        v = (2.f * rng_uniform(wkey, (uint32_t)((int64_t)n * d.K + k)) - 1.f) * d.bound;
       o = d.w_off + e;
     } else {
       const int n = (int)(e - nw);
@@ -772,7 +823,10 @@ static void launch_bwd_rows(int n_work, int n_rowblocks, hipStream_t stream, con
 // ------------------------------------------------------------------------------------------------
 extern "C" {
 
-int mopt_abi_version() { return 9; }
+int mopt_abi_version() { return 10; }
+
+// weight layout of this build: 1 = k-strip-major [K/64][N][64], 0 = row-major [N][K]
+int mopt_mlp_w_layout() { return MOPT_W_STRIP; }
 
 // 1 when this library is the bounds-checked variant (-DMOPT_BOUNDS_CHECK)
 int mopt_checked_build() { return MOPT_CHECKED_BUILD; }

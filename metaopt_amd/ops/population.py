@@ -197,6 +197,9 @@ class PopulationMLP:
             self._lib = _lib.get_lib()  # raises loudly: no silent fallback on a GPU box
             # backward chunk prefetch (csrc/pop_mlp.hip PF): on unless MOPT_BWD_PREFETCH=0
             self._lib.mopt_mlp_set_bwd_prefetch(int(os.environ.get("MOPT_BWD_PREFETCH", "1")))
+        # HIP weight layout: k-strip-major [K/64][N][64] (csrc/pop_mlp.hip MOPT_W_STRIP) -- the
+        # optimizer state shares it; layer_views() returns row-major copies
+        self.w_strip = backend == "hip" and self._lib.mopt_mlp_w_layout() == 1
         self.backend = backend
         # the population's trials are split into ``n_streams`` groups of equal cost whose train
         # steps run on their own HIP streams, unsynchronised between syncs: one group's
@@ -451,7 +454,8 @@ class PopulationMLP:
                 self.p16[b:b + n] = ref.split_f32(self.p32[b:b + n])[0]
 
     def layer_views(self, slot: int, buf: torch.Tensor = None):
-        """[(W [N,K], b [N])] views of ``buf`` (default: f32 master) for the member in ``slot``."""
+        """[(W [N,K], b [N])] views of ``buf`` (default: f32 master) for the member in ``slot``
+        (row-major copies of the weights when the HIP layout is k-strip-major)."""
         self._run_pending_init()
         self._join()
         cfg = self.members[slot]
@@ -461,7 +465,10 @@ class PopulationMLP:
         buf = self.p32 if buf is None else buf
         out = []
         for (k, n), (wo, bo) in zip(self.layer_dims(cfg.width), self.param_offsets(cfg.width)):
-            out.append((buf[base + wo: base + wo + n * k].view(n, k), buf[base + bo: base + bo + n]))
+            w = buf[base + wo: base + wo + n * k]
+            w = (w.view(k // TILE, n, TILE).permute(1, 0, 2).reshape(n, k) if self.w_strip
+                 else w.view(n, k))
+            out.append((w, buf[base + bo: base + bo + n]))
         return out
 
     # ------------------------------------------------------------------ checkpoints (device)
