@@ -20,7 +20,7 @@ from . import build as _build
 
 _LOCK = threading.Lock()
 _LIB = None
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 c_void_p = ctypes.c_void_p
 c_int = ctypes.c_int
@@ -30,7 +30,7 @@ c_float = ctypes.c_float
 _SIGNATURES = {
     "mopt_abi_version": ([], c_int),
     "mopt_mlp_fwd": ([c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
-                      c_void_p, c_uint, c_int, c_int, c_void_p], c_int),
+                      c_void_p, c_uint, c_int, c_int, c_int, c_void_p], c_int),
     "mopt_mlp_fwd_ce": ([c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int, c_void_p], c_int),
     "mopt_mlp_init": ([c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p],

@@ -134,7 +134,11 @@ enum Opt { kSGD = 0, kAdamW = 1, kSGD16 = 2 };
     x2 = *(const uint4*)(X + g2 + kk_);                 \
     x3 = *(const uint4*)(X + g3 + kk_);                 \
     w0 = *(const uint4*)(W + gw0 + (size_t)kk_ * WKS);  \
-    w1 = *(const uint4*)(W + gw1 + (size_t)kk_ * WKS);  \
+    if (TN >= 64) w1 = *(const uint4*)(W + gw1 + (size_t)kk_ * WKS); \
+    if (TN >= 128) {                                    \
+      w1##b = *(const uint4*)(W + gw2 + (size_t)kk_ * WKS); \
+      w1##c = *(const uint4*)(W + gw3 + (size_t)kk_ * WKS); \
+    }                                                   \
   } while (0)
 #define MOPT_FWD_STORE(x0, x1, x2, x3, w0, w1) \
   do {                                         \
@@ -143,35 +147,43 @@ enum Opt { kSGD = 0, kAdamW = 1, kSGD16 = 2 };
     *(uint4*)as2 = x2;                         \
     *(uint4*)as3 = x3;                         \
     *(uint4*)bs0 = w0;                         \
-    *(uint4*)bs1 = w1;                         \
+    if (TN >= 64) *(uint4*)bs1 = w1;           \
+    if (TN >= 128) {                           \
+      *(uint4*)bs2 = w1##b;                    \
+      *(uint4*)bs3 = w1##c;                    \
+    }                                          \
   } while (0)
 
+// TN: output features per tile (64, or 32 for twice the workgroups: the hidden layers' launches
+// hold ~1.5 workgroups per slot of the chip at 64, a tail of half-empty CUs)
+template <int TN>
 __device__ __forceinline__ void fwd_step(const bf16_t* As, const bf16_t* Bs, int wave, int li,
-                                         int g, f32x4 (&acc)[2][4]) {
+                                         int g, f32x4 (&acc)[2][TN / 16]) {
 #pragma unroll
   for (int ks = 0; ks < BK / 32; ++ks) {
-    bf16x8 a[2], b[4];
+    bf16x8 a[2], b[TN / 16];
 #pragma unroll
     for (int i = 0; i < 2; ++i) a[i] = lds_frag(As + TOFF(wave * 32 + i * 16 + li, ks * 32 + g * 8));
 #pragma unroll
-    for (int j = 0; j < 4; ++j) b[j] = lds_frag(Bs + TOFF(j * 16 + li, ks * 32 + g * 8));
+    for (int j = 0; j < TN / 16; ++j) b[j] = lds_frag(Bs + TOFF(j * 16 + li, ks * 32 + g * 8));
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
+      for (int j = 0; j < TN / 16; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
   }
 }
 
-// W: the tile's first row (w_off + w_tile_off(n0, N, K)); N: rows of the layer's weight matrix
+// W: the tile's first row (w_off + n0 * w_row_stride(K)); N: rows of the layer's weight matrix
+template <int TN>
 __device__ __forceinline__ void fwd_gemm(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                          int K, int N, bf16_t* As, bf16_t* Bs,
-                                         f32x4 (&acc)[2][4]) {
+                                         f32x4 (&acc)[2][TN / 16]) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, g = lane >> 4;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TN / 16; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int c0 = tid, c1 = tid + 256, c2 = tid + 512, c3 = tid + 768;
   const int g0 = (c0 >> 3) * K + (c0 & 7) * 8, g1 = (c1 >> 3) * K + (c1 & 7) * 8;
@@ -179,15 +191,18 @@ __device__ __forceinline__ void fwd_gemm(const bf16_t* __restrict__ X, const bf1
   // W rows are WRS apart; a K-step of kk columns moves kk * WKS elements (w_row_stride / w_kstep)
   const int WRS = w_row_stride(K), WKS = w_kstep(N);
   const int gw0 = (c0 >> 3) * WRS + (c0 & 7) * 8, gw1 = (c1 >> 3) * WRS + (c1 & 7) * 8;
+  const int gw2 = (c2 >> 3) * WRS + (c2 & 7) * 8, gw3 = (c3 >> 3) * WRS + (c3 & 7) * 8;
   bf16_t* as0 = As + TOFF(c0 >> 3, (c0 & 7) * 8);
   bf16_t* as1 = As + TOFF(c1 >> 3, (c1 & 7) * 8);
   bf16_t* as2 = As + TOFF(c2 >> 3, (c2 & 7) * 8);
   bf16_t* as3 = As + TOFF(c3 >> 3, (c3 & 7) * 8);
   bf16_t* bs0 = Bs + TOFF(c0 >> 3, (c0 & 7) * 8);
   bf16_t* bs1 = Bs + TOFF(c1 >> 3, (c1 & 7) * 8);
+  bf16_t* bs2 = Bs + TOFF(c2 >> 3, (c2 & 7) * 8);
+  bf16_t* bs3 = Bs + TOFF(c3 >> 3, (c3 & 7) * 8);
   const int klast = K - BK;
-  uint4 p0, p1, p2, p3, pw0, pw1;  // even K-steps
-  uint4 q0, q1, q2, q3, qw0, qw1;  // odd K-steps
+  uint4 p0, p1, p2, p3, pw0, pw1{}, pw1b{}, pw1c{};  // even K-steps
+  uint4 q0, q1, q2, q3, qw0, qw1{}, qw1b{}, qw1c{};  // odd K-steps
   MOPT_FWD_LOAD(p0, p1, p2, p3, pw0, pw1, 0);
   MOPT_FWD_LOAD(q0, q1, q2, q3, qw0, qw1, min(BK, klast));
   for (int k0 = 0;; k0 += 2 * BK) {
@@ -195,14 +210,14 @@ __device__ __forceinline__ void fwd_gemm(const bf16_t* __restrict__ X, const bf1
     MOPT_FWD_STORE(p0, p1, p2, p3, pw0, pw1);
     __syncthreads();
     MOPT_FWD_LOAD(p0, p1, p2, p3, pw0, pw1, min(k0 + 2 * BK, klast));
-    fwd_step(As, Bs, wave, li, g, acc);
+    fwd_step<TN>(As, Bs, wave, li, g, acc);
     __syncthreads();
     if (k0 + BK >= K) break;
     // odd K-step: tile k0 + BK from set q, which then fetches tile k0 + 3 BK
     MOPT_FWD_STORE(q0, q1, q2, q3, qw0, qw1);
     __syncthreads();
     MOPT_FWD_LOAD(q0, q1, q2, q3, qw0, qw1, min(k0 + 3 * BK, klast));
-    fwd_step(As, Bs, wave, li, g, acc);
+    fwd_step<TN>(As, Bs, wave, li, g, acc);
     __syncthreads();
     if (k0 + 2 * BK >= K) break;
   }
@@ -213,13 +228,15 @@ __device__ __forceinline__ void fwd_gemm(const bf16_t* __restrict__ X, const bf1
 // (Measured and rejected: an LDS-free variant loading every MFMA fragment -- 16 bytes of one
 // row of X or W per lane -- straight from global memory ran the forward 2.5x slower than the
 // LDS-staged tiles above; profiles/README.md.)
+template <int TN>
 __device__ __forceinline__ void fwd_core(const bf16_t* X, const bf16_t* W, int K, int N,
-                                         bf16_t* As, bf16_t* Bs, f32x4 (&acc)[2][4]) {
-  fwd_gemm(X, W, K, N, As, Bs, acc);
+                                         bf16_t* As, bf16_t* Bs, f32x4 (&acc)[2][TN / 16]) {
+  fwd_gemm<TN>(X, W, K, N, As, Bs, acc);
 }
 
-// Y[rows, n0:n0+64] = dropout(relu(X W^T + b)) for one (trial-layer, n-tile, 128-row block).
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void mlp_fwd_kernel(const MlpTL* __restrict__ tls,
+// Y[rows, n0:n0+TN] = dropout(relu(X W^T + b)) for one (trial-layer, n-tile, 128-row block).
+template <int TN>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TN == 128 ? 3 : 4))) void mlp_fwd_kernel(const MlpTL* __restrict__ tls,
                                                       const int2* __restrict__ work, int n_work,
                                                       const bf16_t* __restrict__ xb,
                                                       const bf16_t* __restrict__ plo,
@@ -227,18 +244,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void m
                                                       bf16_t* __restrict__ act,
                                                       const TrialHP* __restrict__ hp,
                                                       uint32_t step, int layer, int flags) {
-  __shared__ __attribute__((aligned(16))) bf16_t smem[(BM + BN) * TS];
+  __shared__ __attribute__((aligned(16))) bf16_t smem[(BM + TN) * TS];
   bf16_t* As = smem;
   bf16_t* Bs = smem + BM * TS;
   const int2 wi = work[xcd_remap(blockIdx.x, n_work)];
   const MlpTL tl = tls[wi.x];
-  const int K = tl.K, N = tl.N, n0 = wi.y * BN, row0 = blockIdx.y * BM;
+  const int K = tl.K, N = tl.N, n0 = wi.y * TN, row0 = blockIdx.y * BM;
   if (row0 >= tl.rows) return;           // a smaller batch than the launch's: uniform exit
   const bf16_t* X = xb + tl.x_off + (size_t)row0 * K;
   const bf16_t* W = p16 + tl.w_off + (size_t)n0 * w_row_stride(K);
 
-  f32x4 acc[2][4];
-  fwd_core(X, W, K, N, As, Bs, acc);
+  f32x4 acc[2][TN / 16];
+  fwd_core<TN>(X, W, K, N, As, Bs, acc);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, g = lane >> 4;
   const bf16_t* bias_hi = p16 + tl.b_off + n0;
@@ -251,7 +268,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void m
   const uint32_t key = rng_key(h.seed, (uint32_t)layer, h.t + step);
   bf16_t* Cs = smem;  // reuse As (the last K-step ended with a barrier)
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < TN / 16; ++j) {
     const int col = j * 16 + li;
     const float bj = join_hilo(bias_hi[col], bias_lo[col]);
 #pragma unroll
@@ -270,9 +287,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void m
   }
   __syncthreads();
   bf16_t* Y = act + tl.y_off + (size_t)row0 * N + n0;
+  constexpr int CPR = TN / 8;   // 16-byte chunks per row
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
+  for (int i = 0; i < TN / 16; ++i) {
+    const int c = tid + 256 * i, r = c / CPR, ch = c % CPR;
     *(uint4*)(Y + (size_t)r * N + ch * 8) = *(const uint4*)(Cs + TOFF(r, ch * 8));
   }
 }
@@ -308,7 +326,7 @@ __global__ __launch_bounds__(256) void mlp_fwd_ce_kernel(const MlpTL* __restrict
   const bf16_t* W = p16 + tl.w_off;
 
   f32x4 acc[2][4];
-  fwd_core(X, W, K, N, As, Bs, acc);
+  fwd_core<64>(X, W, K, N, As, Bs, acc);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, g = lane >> 4;
   const bf16_t* bias_hi = p16 + tl.b_off;
@@ -823,7 +841,7 @@ static void launch_bwd_rows(int n_work, int n_rowblocks, hipStream_t stream, con
 // ------------------------------------------------------------------------------------------------
 extern "C" {
 
-int mopt_abi_version() { return 10; }
+int mopt_abi_version() { return 11; }
 
 // weight layout of this build: 1 = k-strip-major [K/64][N][64], 0 = row-major [N][K]
 int mopt_mlp_w_layout() { return MOPT_W_STRIP; }
@@ -841,14 +859,27 @@ int mopt_mlp_init(const void* descs, int n_desc, void* plo, void* p16, void* m32
   return (int)hipGetLastError();
 }
 
+// tile_n: output features per work item (64 or 32; the work list was built for it)
 int mopt_mlp_fwd(const void* tls, const void* work, int n_work, int n_rowblocks, const void* xb,
                  const void* plo, const void* p16, void* act, const void* hp, unsigned step,
-                 int layer, int flags, void* stream) {
+                 int layer, int flags, int tile_n, void* stream) {
   if (n_work <= 0) return 0;
-  hipLaunchKernelGGL(mlp_fwd_kernel, dim3(n_work, n_rowblocks), dim3(256), 0, (hipStream_t)stream,
-                     (const MlpTL*)tls, (const int2*)work, n_work, (const bf16_t*)xb,
-                     (const bf16_t*)plo, (const bf16_t*)p16, (bf16_t*)act, (const TrialHP*)hp, step,
-                     layer, flags);
+  if (tile_n != 32 && tile_n != 64 && tile_n != 128) return (int)hipErrorInvalidValue;
+  if (tile_n == 128)
+    hipLaunchKernelGGL(mlp_fwd_kernel<128>, dim3(n_work, n_rowblocks), dim3(256), 0,
+                       (hipStream_t)stream, (const MlpTL*)tls, (const int2*)work, n_work,
+                       (const bf16_t*)xb, (const bf16_t*)plo, (const bf16_t*)p16, (bf16_t*)act,
+                       (const TrialHP*)hp, step, layer, flags);
+  else if (tile_n == 32)
+    hipLaunchKernelGGL(mlp_fwd_kernel<32>, dim3(n_work, n_rowblocks), dim3(256), 0,
+                       (hipStream_t)stream, (const MlpTL*)tls, (const int2*)work, n_work,
+                       (const bf16_t*)xb, (const bf16_t*)plo, (const bf16_t*)p16, (bf16_t*)act,
+                       (const TrialHP*)hp, step, layer, flags);
+  else
+    hipLaunchKernelGGL(mlp_fwd_kernel<64>, dim3(n_work, n_rowblocks), dim3(256), 0,
+                       (hipStream_t)stream, (const MlpTL*)tls, (const int2*)work, n_work,
+                       (const bf16_t*)xb, (const bf16_t*)plo, (const bf16_t*)p16, (bf16_t*)act,
+                       (const TrialHP*)hp, step, layer, flags);
   return (int)hipGetLastError();
 }
 
@@ -902,6 +933,8 @@ struct MlpStep {
   void *plo, *p16, *m32, *v32, *act, *grad, *hp, *loss, *correct;
   float inv_b;      // <= 0: each trial's mean over its own rows (MlpTL::rows)
   int32_t n_stats;  // entries of loss / correct (the population's capacity)
+  int32_t fwd_tn;   // hidden-layer forward tile width of the work lists (32 / 64)
+  int32_t pad;
 };
 
 int mopt_mlp_step(const MlpStep* s, const void* x, const void* y, void* stream) {
@@ -916,7 +949,8 @@ int mopt_mlp_step(const MlpStep* s, const void* x, const void* y, void* stream) 
   }
   for (int l = 0; l < L - 1; ++l) {
     err = mopt_mlp_fwd(s->tls, s->fwd[l], s->n_fwd[l], s->rb, l == 0 ? x : s->act, s->plo,
-                       s->p16, s->act, s->hp, 1u, l, kRelu | (s->drop ? kDropout : 0), stream);
+                       s->p16, s->act, s->hp, 1u, l, kRelu | (s->drop ? kDropout : 0), s->fwd_tn,
+                       stream);
     if (err) return err;
   }
   const int ce = kWriteGrad | kCountStep | (s->rb == 1 ? kStoreStats : 0);

@@ -46,6 +46,7 @@ INIT_DTYPE = np.dtype([("w_off", "<i8"), ("b_off", "<i8"), ("K", "<i4"), ("N", "
 assert TL_DTYPE.itemsize == 64 and HP_DTYPE.itemsize == 32 and INIT_DTYPE.itemsize == 48
 
 TILE = 64
+FWD_TN = 64             # default hidden-layer forward tile width (MOPT_FWD_TN)
 MAX_ROWS = 64 * 128     # csrc/pop_mlp.hip mopt_mlp_bwd: at most 64 row blocks per launch
 FWD_RELU, FWD_DROPOUT, FWD_WRITE_GRAD, FWD_STORE_STATS, FWD_COUNT_STEP = 1, 2, 4, 8, 16
 BWD_HAS_DX, BWD_IN_DROPOUT, BWD_UPDATE_BIAS = 1, 2, 4
@@ -60,7 +61,8 @@ class _MlpStep(ctypes.Structure):
                 ("drop", ctypes.c_int32), ("opt", ctypes.c_int32)] + \
                [(n, ctypes.c_void_p) for n in ("plo", "p16", "m32", "v32", "act", "grad", "hp",
                                                "loss", "correct")] + \
-               [("inv_b", ctypes.c_float), ("n_stats", ctypes.c_int32)]
+               [("inv_b", ctypes.c_float), ("n_stats", ctypes.c_int32),
+                ("fwd_tn", ctypes.c_int32), ("pad", ctypes.c_int32)]
 OPTIMIZERS = {"sgd": 0, "adamw": 1}
 
 
@@ -200,6 +202,11 @@ class PopulationMLP:
         # HIP weight layout: k-strip-major [K/64][N][64] (csrc/pop_mlp.hip MOPT_W_STRIP) -- the
         # optimizer state shares it; layer_views() returns row-major copies
         self.w_strip = backend == "hip" and self._lib.mopt_mlp_w_layout() == 1
+        # output features per hidden-layer forward work item (csrc/pop_mlp.hip mlp_fwd_kernel
+        # TN): 32 gives the launches twice the workgroups (less of a tail at ~1.5 per slot)
+        self.fwd_tn = int(os.environ.get("MOPT_FWD_TN", str(FWD_TN)))
+        if self.fwd_tn not in (32, 64, 128):
+            raise ValueError("MOPT_FWD_TN must be 32, 64 or 128")
         self.backend = backend
         # the population's trials are split into ``n_streams`` groups of equal cost whose train
         # steps run on their own HIP streams, unsynchronised between syncs: one group's
@@ -331,6 +338,8 @@ class PopulationMLP:
         return int(cfg.batch_size) or self.batch_size
 
     def _check_member(self, cfg: MemberConfig) -> None:
+        if self.fwd_tn == 128 and pad64(cfg.width) % 128:
+            raise ValueError("MOPT_FWD_TN=128 (experiment) needs widths padded to 128")
         if cfg.width > self.max_width or cfg.width < 1:
             raise ValueError(f"width {cfg.width} outside [1, {self.max_width}]")
         if not (0.0 <= cfg.dropout < 1.0):
@@ -734,7 +743,8 @@ class PopulationMLP:
                 tl["y_off"][i] = y_off
                 tl["gx_off"][i] = prev if l > 0 else -1
                 tl["rows"][i] = used
-                nt, nk = N // TILE, K // TILE
+                tn = self.fwd_tn if l < L - 1 else TILE   # the loss layer: one 64-wide tile
+                nt, nk = N // tn, K // TILE
                 fo = _lpt_order(np.repeat(K, nt))     # a forward tile costs ~K
                 bo = _lpt_order(np.repeat(N, nk))     # a backward k-strip costs ~N
                 fwd.append(np.stack([np.repeat(i, nt)[fo], _ranges(nt)[fo]], 1).astype(np.int32))
@@ -742,7 +752,7 @@ class PopulationMLP:
         else:
             fwd = [np.zeros((0, 2), np.int32) for _ in range(L)]
             bwd = [np.zeros((0, 2), np.int32) for _ in range(L)]
-        out = {"tl_np": tl, "rows": rows, "fwd_np": fwd, "bwd_np": bwd}
+        out = {"tl_np": tl, "rows": rows, "fwd_np": fwd, "bwd_np": bwd, "fwd_tn": self.fwd_tn}
         self._validate_tables(tl, fwd, bwd, rows)
         if self.device.type == "cuda":
             from ._lib import upload, upload_bytes
@@ -785,14 +795,15 @@ class PopulationMLP:
                 (t["trial"] >= self.capacity).any():
             bad.append("trial / class fields out of range")
         for name, lists, per in (("fwd", fwd, "N"), ("bwd", bwd, "K")):
-            for w in lists:
+            for l, w in enumerate(lists):
                 if not len(w):
                     continue
                 idx = w[:, 0]
                 if (idx < 0).any() or (idx >= n_tl).any() or not live[idx].all():
                     bad.append(f"{name} work item names a missing trial-layer")
                     break
-                if (w[:, 1] < 0).any() or (w[:, 1] >= tl[per][idx] // TILE).any():
+                tile = self.fwd_tn if (name == "fwd" and l < L - 1) else TILE
+                if (w[:, 1] < 0).any() or (w[:, 1] >= tl[per][idx] // tile).any():
                     bad.append(f"{name} work item tile out of range")
                     break
         if bad:
@@ -837,6 +848,7 @@ class PopulationMLP:
             a.n_fwd[l], a.n_bwd[l] = part["n_fwd"][l], part["n_bwd"][l]
         a.L, a.rb, a.drop = L, self.batch_size // 128, int(self._any_dropout)
         a.n_stats = self.capacity      # > 1 row block: the step zeroes loss/correct first
+        a.fwd_tn = self.fwd_tn
         a.opt = 2 if self.momentum_dtype == "bf16" else OPTIMIZERS[self.optimizer]
         for n in ("plo", "p16", "m32", "v32", "act", "grad", "hp", "loss", "correct"):
             setattr(a, n, P[n])
@@ -985,7 +997,8 @@ class PopulationMLP:
         for l in range(L - 1):
             check(lib.mopt_mlp_fwd(tl, part["fwd"][l], part["n_fwd"][l], rb, xp if l == 0 else act,
                                    P["plo"], P["p16"], act, P["hp"], 1, l,
-                                   FWD_RELU | (FWD_DROPOUT if drop else 0), stream), "mlp_fwd")
+                                   FWD_RELU | (FWD_DROPOUT if drop else 0), self.fwd_tn, stream),
+                  "mlp_fwd")
         check(lib.mopt_mlp_fwd_ce(tl, part["fwd"][L - 1], part["n_fwd"][L - 1], rb,
                                   xp if L == 1 else act, P["plo"], P["p16"], yp,
                                   P["grad"], P["loss"], P["correct"], P["hp"],
@@ -1081,7 +1094,7 @@ class PopulationMLP:
                 check(lib.mopt_mlp_fwd(tb["tl"].data_ptr(), tb["fwd"][l].data_ptr(), tb["n_fwd"][l],
                                        rb, src.data_ptr(), self.plo.data_ptr(), self.p16.data_ptr(),
                                        self.act_eval.data_ptr(), self.hp_dev.data_ptr(), 0, l,
-                                       FWD_RELU, stream), "mlp_fwd(eval)")
+                                       FWD_RELU, tb["fwd_tn"], stream), "mlp_fwd(eval)")
             src = xb if L == 1 else self.act_eval
             check(lib.mopt_mlp_fwd_ce(tb["tl"].data_ptr(), tb["fwd"][L - 1].data_ptr(),
                                       tb["n_fwd"][L - 1], rb, src.data_ptr(), self.plo.data_ptr(),

@@ -57,7 +57,7 @@ def run_fwd(l):
         lib.mopt_mlp_fwd(tb["tl"].data_ptr(), tb["fwd"][l].data_ptr(), tb["n_fwd"][l], RB,
                          src.data_ptr(), pop.plo.data_ptr(), pop.p16.data_ptr(),
                          pop.act.data_ptr(), pop.hp_dev.data_ptr(), 0, l, FWD_RELU | FWD_DROPOUT,
-                         stream)
+                         pop.fwd_tn, stream)
     else:
         lib.mopt_mlp_fwd_ce(tb["tl"].data_ptr(), tb["fwd"][l].data_ptr(), tb["n_fwd"][l], RB,
                             src.data_ptr(), pop.plo.data_ptr(), pop.p16.data_ptr(), y.data_ptr(),
