@@ -170,7 +170,7 @@ class ASHA(BaseAlgorithm):
                 if _id in self.trial_info:
                     continue
                 self.trial_info[_id] = current[idx]
-                current[idx].register(point, None, overwrite=False, _id=_id)
+                current[idx]._register_at(0, point, None, False, _id)   # fidelity = rung 0's
                 out.append(point)
         else:
             if len(out) < n:
@@ -180,8 +180,11 @@ class ASHA(BaseAlgorithm):
     def get_id(self, point) -> str:
         """md5 of the non-fidelity values (the bracket key); memoised per point -- every point is
         looked up at suggest, registration and observation."""
-        cache = self.__dict__.setdefault("_id_cache", {})
-        key = tuple(point)
+        try:
+            cache = self.__dict__["_id_cache"]
+        except KeyError:
+            cache = self.__dict__["_id_cache"] = {}
+        key = point if type(point) is tuple else tuple(point)
         _id = cache.get(key)
         if _id is None:
             fi = self.fidelity_index
@@ -242,7 +245,9 @@ class Bracket:
     Each rung also keeps its completed entries sorted by objective, and separately the completed
     entries not yet present in the next rung (``bisect``): a promotion query is then the best
     un-promoted entry, checked against the top-k rank by one binary search -- O(log n) instead of
-    re-sorting or scanning the rung (population sweeps put thousands of points in it)."""
+    re-sorting or scanning the rung.  (Plain lists: a bracket's rungs stay small -- with
+    ``repetitions`` a filled bracket is followed by a new one -- and ``sortedcontainers`` was
+    measured slower at these sizes.)"""
 
     def __init__(self, asha, reduction_factor, budgets):
         self.asha = asha

@@ -164,6 +164,10 @@ class PopulationSweep:
                 self._algo_id = inner_algo.get_id
             inner = getattr(self.algorithm, "algorithm", self.algorithm)
             self._tracks_lineage = hasattr(inner, "parent_of")
+            # per-placement callables, looked up once (thousands of placements per sync at W=8)
+            self._parent_of = getattr(self.algorithm, "parent_of", None)
+            self._row_fn = getattr(task, "member_row", None)
+            self._batch_fn = getattr(task, "batch_rows", None)
             if watchdog is not None:
                 watchdog.on_stall.append(self._interrupt_in_flight)
         # resume bookkeeping (rank 0): stored trials waiting for a slot, device-state sidecars
@@ -599,11 +603,11 @@ class PopulationSweep:
         the least-loaded rank."""
         W = len(n_free)
         params = dict(zip(self._dim_names, point))
-        pkey = self._point_key(point, params)
+        pkey = self._algo_id(point) if self._algo_id is not None else \
+            self._point_key(point, params)
         parent = None
-        if self._tracks_lineage:
-            parent_of = getattr(self.algorithm, "parent_of", None)
-            parent = parent_of(point) if parent_of is not None else None
+        if self._tracks_lineage and self._parent_of is not None:
+            parent = self._parent_of(point)
         ckey = self._point_key(parent) if parent is not None else pkey
         owner = self.ckpt_index.get(ckey)
         src, resume = -1, -1
@@ -636,17 +640,15 @@ class PopulationSweep:
         self.trials[key] = [tid, stamp]      # [trial id, last heartbeat]
         budget = int(self.task.budget(params))
         self.key_info[key] = (params, pkey, point, budget)
-        row_fn = getattr(self.task, "member_row", None)
         seed = self.task.seed_of(pkey)
-        if row_fn is not None:
-            hp = row_fn(params, seed)
+        if self._row_fn is not None:
+            hp = self._row_fn(params, seed)
         else:
             cfg = self.task.member_config(params, seed)
             hp = (cfg.width, cfg.lr, cfg.momentum, cfg.weight_decay, cfg.dropout, cfg.seed)
-        batch_fn = getattr(self.task, "batch_rows", None)
         rows.append(row)
-        vals.append((action, key) + tuple(hp) + (budget, resume, src,
-                                                 batch_fn(params) if batch_fn else 0))
+        vals.append((action, key, *hp, budget, resume, src,
+                     self._batch_fn(params) if self._batch_fn is not None else 0))
 
     def _point_key(self, point, params=None) -> str:
         """Identity of a suggested point's configuration regardless of its fidelity (python
