@@ -27,7 +27,7 @@ c_void_p, c_int, c_float, c_int64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_floa
 _lib.register_signatures({
     "mopt_bn_fwd": ([c_void_p] * 8 + [c_int, c_int64, c_int, c_float, c_float, c_int, c_int,
                                      c_int, c_int, c_int, c_void_p], c_int),
-    "mopt_bn_bwd": ([c_void_p] * 10 + [c_int, c_int64, c_int, c_int, c_int, c_void_p], c_int),
+    "mopt_bn_bwd": ([c_void_p] * 11 + [c_int, c_int64, c_int, c_int, c_int, c_void_p], c_int),
     "mopt_pconv": ([c_int] + [c_void_p] * 4 + [c_int] * 10 + [c_void_p], c_int),
     "mopt_dconv": ([c_int] + [c_void_p] * 4 + [c_int] * 7 + [c_void_p], c_int),
     "mopt_dconv_wgrad_splits": ([c_int] * 6, c_int),
@@ -218,9 +218,7 @@ class _BNAct(torch.autograd.Function):
               running.data_ptr(), sums.data_ptr(), P, M, C, eps, momentum, int(train), int(relu),
               int(ready), res.shape[-1] if res_sub2 else 0,
               (x.shape[1].bit_length() - 1) if res_sub2 else 0, _s(x))
-        # (recomputing relu'(y) from x, gamma, beta instead of keeping y measured slower:
-        #  187 -> 229 us for the stage-1 backward pair on one MI355X)
-        ctx.save_for_backward(x, y, stat, gamma)
+        ctx.save_for_backward(x, y, stat, gamma, beta)
         ctx.meta = (P, M, C, relu, res is not None)
         # backward: pre-zeroed sums from the step's arena; dgamma / dbeta written by the kernel
         # straight into the flat gradient buffer when the parameters are its leaf views
@@ -233,8 +231,11 @@ class _BNAct(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, stat, gamma = ctx.saved_tensors
+        x, y, stat, gamma, beta = ctx.saved_tensors
         P, M, C, relu, has_res = ctx.meta
+        # without a residual relu'(.) is recomputed from x, gamma, beta (y is not read): one
+        # activation tensor less through both backward kernels
+        mode = 0 if not relu else (1 if has_res else 2)
         dy = dy.contiguous()
         dx = torch.empty_like(x)
         dres = torch.empty_like(x) if has_res else None
@@ -244,9 +245,10 @@ class _BNAct(torch.autograd.Function):
         gg, gb = ctx.grads
         direct = gg is not None and gb is not None and gg.is_contiguous() and gb.is_contiguous()
         _call("mopt_bn_bwd", x.data_ptr(), y.data_ptr(), dy.data_ptr(), stat.data_ptr(),
-              gamma.data_ptr(), dx.data_ptr(), 0 if dres is None else dres.data_ptr(),
-              sums.data_ptr(), gg.data_ptr() if direct else 0, gb.data_ptr() if direct else 0,
-              P, M, C, int(relu), int(zeroed), _s(x))
+              gamma.data_ptr(), beta.data_ptr(), dx.data_ptr(),
+              0 if dres is None else dres.data_ptr(), sums.data_ptr(),
+              gg.data_ptr() if direct else 0, gb.data_ptr() if direct else 0,
+              P, M, C, mode, int(zeroed), _s(x))
         if dres is not None and ctx.mailbox is not None:
             ctx.mailbox["dres"] = dres     # picked up by the block's first convolution
             ctx.mailbox["sub2"] = ctx.res_sub2

@@ -7,6 +7,10 @@
 //   bn_finalize mean / rstd per (trial, channel), running-statistics update (momentum, unbiased)
 //   bn_apply    y = relu?(gamma (x - mean) rstd + beta + residual?)
 //   bn_bwd_*    dz = dy * relu'(y); sums of dz and dz * xhat; dx, dgamma, dbeta, dresidual
+//
+// relu mode of the backward: 0 none, 1 relu'(y) read off the stored output y, 2 relu'(.)
+// recomputed from x (x sc + sh > 0, the forward's own arithmetic) -- for a BatchNorm without a
+// residual, which then never reads y: one tensor less through both backward passes.
 #include "common.h"
 
 using namespace mopt;
@@ -44,6 +48,8 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
                                                         const bf16_t* __restrict__ y,
                                                         const bf16_t* __restrict__ dy,
                                                         const float* __restrict__ stat,
+                                                        const bf16_t* __restrict__ gamma,
+                                                        const bf16_t* __restrict__ beta,
                                                         float* __restrict__ sums, int64_t M,
                                                         int C, int rows_per_block, int relu) {
   __shared__ float red[4][2][64];
@@ -53,12 +59,22 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t r1 = min(r0 + rows_per_block, M);
   const int64_t base = (int64_t)p * M * C + 8 * ch;
-  float mean[8], rstd[8];
+  float mean[8], rstd[8], sc[8], sh[8];
   if (BWD) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       mean[e] = stat[(2 * p) * C + 8 * ch + e];
       rstd[e] = stat[(2 * p + 1) * C + 8 * ch + e];
+    }
+    if (relu == 2) {
+      float g[8], b[8];
+      unpack8(*(const uint4*)(gamma + (int64_t)p * C + 8 * ch), g);
+      unpack8(*(const uint4*)(beta + (int64_t)p * C + 8 * ch), b);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        sc[e] = g[e] * rstd[e];
+        sh[e] = b[e] - mean[e] * sc[e];
+      }
     }
   }
   float a[8], b[8];
@@ -73,7 +89,7 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
       xr[u] = *(const uint4*)(x + o);
       if (BWD) {
         dr[u] = *(const uint4*)(dy + o);
-        if (relu) yr[u] = *(const uint4*)(y + o);
+        if (relu == 1) yr[u] = *(const uint4*)(y + o);
       }
     }
 #pragma unroll
@@ -90,10 +106,12 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
       } else {
         float dv[8], yv[8];
         unpack8(dr[u], dv);
-        if (relu) unpack8(yr[u], yv);
+        if (relu == 1) unpack8(yr[u], yv);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const float dz = (relu && yv[e] <= 0.f) ? 0.f : dv[e];
+          const bool off = relu == 1 ? yv[e] <= 0.f
+                                     : (relu == 2 && xv[e] * sc[e] + sh[e] + 0.f <= 0.f);
+          const float dz = off ? 0.f : dv[e];
           a[e] += dz;
           b[e] += dz * (xv[e] - mean[e]) * rstd[e];
         }
@@ -220,6 +238,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
                                                            const float* __restrict__ stat,
                                                            const float* __restrict__ sums,
                                                            const bf16_t* __restrict__ gamma,
+                                                           const bf16_t* __restrict__ beta,
                                                            bf16_t* __restrict__ dx,
                                                            bf16_t* __restrict__ dres,
                                                            bf16_t* __restrict__ dgamma,
@@ -237,19 +256,21 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
   }
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t r1 = min(r0 + rows_per_block, M);
-  float k1[8], k2[8], k3[8];
+  float k1[8], k2[8], k3[8], sh[8];
   {
-    float g[8];
+    float g[8], b[8];
     unpack8(*(const uint4*)(gamma + (int64_t)p * C + 8 * ch), g);
+    if (relu == 2) unpack8(*(const uint4*)(beta + (int64_t)p * C + 8 * ch), b);
     const float invM = 1.f / (float)M;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int c = 8 * ch + e;
       const float mean = stat[(2 * p) * C + c], rstd = stat[(2 * p + 1) * C + c];
       const float A = sums[(2 * p) * C + c] * invM, B = sums[(2 * p + 1) * C + c] * invM;
-      k1[e] = g[e] * rstd;
+      k1[e] = g[e] * rstd;                 // = the forward's scale sc
       k2[e] = -k1[e] * rstd * B;
       k3[e] = -k1[e] * A - k2[e] * mean;
+      sh[e] = relu == 2 ? b[e] - mean * k1[e] : 0.f;
     }
   }
   const int64_t base = (int64_t)p * M * C + 8 * ch;
@@ -261,7 +282,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
       const int64_t o = base + (ru < r1 ? ru : r) * C;
       xr[u] = *(const uint4*)(x + o);
       dr[u] = *(const uint4*)(dy + o);
-      if (relu) yr[u] = *(const uint4*)(y + o);
+      if (relu == 1) yr[u] = *(const uint4*)(y + o);
     }
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
@@ -270,10 +291,12 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
       float xv[8], yv[8], dv[8], o[8];
       unpack8(xr[u], xv);
       unpack8(dr[u], dv);
-      if (relu) unpack8(yr[u], yv);
+      if (relu == 1) unpack8(yr[u], yv);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float dz = (relu && yv[e] <= 0.f) ? 0.f : dv[e];
+        const bool off = relu == 1 ? yv[e] <= 0.f
+                                   : (relu == 2 && xv[e] * k1[e] + sh[e] + 0.f <= 0.f);
+        const float dz = off ? 0.f : dv[e];
         o[e] = k1[e] * dz + k2[e] * xv[e] + k3[e];
         dv[e] = dz;
       }
@@ -314,8 +337,8 @@ int mopt_bn_fwd(const void* x, const void* gamma, const void* beta, const void* 
     (void)hipMemsetAsync(sums, 0, sizeof(float) * 2 * P * C, st);
     const int rpb = reduce_rows(P, M, C);
     hipLaunchKernelGGL(bn_reduce_kernel<false>, dim3((unsigned)((M + rpb - 1) / rpb), P),
-                       dim3(256), 0, st, (const bf16_t*)x, nullptr, nullptr, nullptr,
-                       (float*)sums, M, C, rpb, 0);
+                       dim3(256), 0, st, (const bf16_t*)x, nullptr, nullptr, nullptr, nullptr,
+                       nullptr, (float*)sums, M, C, rpb, 0);
   }
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((P * C + 255) / 256), dim3(256), 0, st,
                      (const float*)sums, (float*)stat, (float*)running, P, C, M, eps, momentum,
@@ -330,19 +353,24 @@ int mopt_bn_fwd(const void* x, const void* gamma, const void* beta, const void* 
 
 // sums [P][2][C] out: (sum dz, sum dz * xhat) = (dbeta, dgamma) in f32 (zeroed here unless
 // sums_zeroed); dgamma / dbeta (bf16 [P][C], may be null): the gradients written directly.
+// relu: 0 none, 1 mask from y, 2 mask recomputed from x with gamma / beta (y may be null)
 int mopt_bn_bwd(const void* x, const void* y, const void* dy, const void* stat, const void* gamma,
-                void* dx, void* dres, void* sums, void* dgamma, void* dbeta, int P, int64_t M,
-                int C, int relu, int sums_zeroed, void* stream) {
+                const void* beta, void* dx, void* dres, void* sums, void* dgamma, void* dbeta,
+                int P, int64_t M, int C, int relu, int sums_zeroed, void* stream) {
+  if (relu < 0 || relu > 2 || (relu == 1 && y == nullptr) || (relu == 2 && beta == nullptr))
+    return (int)hipErrorInvalidValue;
   if (!bn_shape_ok(C)) return 1;
   hipStream_t st = (hipStream_t)stream;
   if (!sums_zeroed) (void)hipMemsetAsync(sums, 0, sizeof(float) * 2 * P * C, st);
   const int rpb = reduce_rows(P, M, C);
   hipLaunchKernelGGL(bn_reduce_kernel<true>, dim3((unsigned)((M + rpb - 1) / rpb), P),
                      dim3(256), 0, st, (const bf16_t*)x, (const bf16_t*)y, (const bf16_t*)dy,
-                     (const float*)stat, (float*)sums, M, C, rpb, relu);
+                     (const float*)stat, (const bf16_t*)gamma, (const bf16_t*)beta, (float*)sums,
+                     M, C, rpb, relu);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3((unsigned)((M + rpb - 1) / rpb), P), dim3(256), 0,
                      st, (const bf16_t*)x, (const bf16_t*)y, (const bf16_t*)dy, (const float*)stat,
-                     (const float*)sums, (const bf16_t*)gamma, (bf16_t*)dx, (bf16_t*)dres,
+                     (const float*)sums, (const bf16_t*)gamma, (const bf16_t*)beta, (bf16_t*)dx,
+                     (bf16_t*)dres,
                      (bf16_t*)dgamma, (bf16_t*)dbeta, M, C, P, rpb, relu);
   return (int)hipGetLastError();
 }
