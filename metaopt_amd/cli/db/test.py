@@ -49,8 +49,14 @@ class PresenceStage:
             cfg = yaml.safe_load(f) or {}
         if "database" not in cfg:
             return "Skipping", "No database found in configuration file."
-        self.db_config.update(cfg["database"])
+        section = cfg["database"] or {}
+        if not any(k in section for k in ("type", "name", "host", "port")):
+            return "Skipping", "No configuration value found inside `database`."
+        self.db_config.update(section)
         return "Success", ""
+
+    def post_stage(self):
+        print(f"Using configuration: {self.db_config}")
 
 
 class CreationStage:
@@ -111,7 +117,6 @@ def main(args):
     presence = PresenceStage(args)
     creation = CreationStage(presence)
     operations = OperationsStage(creation)
-    ok = True
     for stage in (presence, creation, operations):
         for check in stage.checks():
             name = check.__name__.replace("check_", "").replace("_", " ")
@@ -120,6 +125,8 @@ def main(args):
                 print(f"{name}... {status}" + (f" ({msg})" if msg else ""))
             except CheckError as exc:
                 print(f"{name}... Failure\n{exc}")
-                ok = False
                 return 1
-    return 0 if ok else 1
+        post = getattr(stage, "post_stage", None)
+        if post is not None:
+            post()
+    return 0
