@@ -242,7 +242,7 @@ class _Unflatten(torch.autograd.Function):
 class HypergradLM:
     def __init__(self, capacity: int, config="tiny-2layer", batch_size: int = 4,
                  seq_len: Optional[int] = None, device="cuda", graph: Optional[bool] = None,
-                 dp_comm=None):
+                 dp_comm=None, mode: Optional[str] = None):
         cfg = PRESETS[config] if isinstance(config, str) else config
         if seq_len is not None:
             import dataclasses
@@ -258,13 +258,33 @@ class HypergradLM:
             k = int(np.prod(shape))
             self.offsets.append((n, k))
             n += k
-        self.n = n = (n + 3) // 4 * 4
+        self.n = n = (n + 7) // 8 * 8
         z = lambda: torch.zeros(P, n, dtype=torch.float32, device=self.device)  # noqa: E731
-        self.w, self.v, self.ze, self.zm, self.ye, self.ym = z(), z(), z(), z(), z(), z()
+        self.w, self.v, self.ye, self.ym = z(), z(), z(), z()
+        # the two weight tangents are one [2, P, n] tensor (and the explicit step's gradient
+        # outputs one [3, P, n]): a parameter's tangent slices are then one strided operand of
+        # the two-level-batched GEMMs (models/hyper_step.py)
+        self.Z = torch.zeros(2, P, n, dtype=torch.float32, device=self.device)
+        self.ze, self.zm = self.Z[0], self.Z[1]
         self.eta = torch.zeros(P, dtype=torch.float32, device=self.device)
         self.mu = torch.zeros(P, dtype=torch.float32, device=self.device)
         self.cos, self.sin = ops.rope_tables(cfg.seq_len, cfg.rope_base, device=self.device)
         self.steps = 0
+        # "explicit" (default): the hand-derived stacked forward-over-reverse step of
+        # models/hyper_step.py (HIP kernels on the GPU); "func": torch.func jvp-of-grad over the
+        # op-by-op graph of lm_losses (the executable specification the explicit step is tested
+        # against)
+        if mode is None:
+            import os
+            mode = os.environ.get("MOPT_HYPER_MODE", "explicit")
+        if mode not in ("explicit", "func"):
+            raise ValueError(f"HypergradLM: mode must be 'explicit' or 'func', got {mode!r}")
+        self.mode = mode
+        self._steppers = {}
+        self.g = self.he = self.hm = None
+        if mode == "explicit":
+            self.G = torch.zeros(3, P, n, dtype=torch.float32, device=self.device)
+            self.g, self.he, self.hm = self.G[0], self.G[1], self.G[2]
         # the inner step is thousands of small launches (forward, backward and two tangent
         # passes through every op): on the GPU it is captured once into a HIP graph and
         # replayed (MOPT_HYPER_GRAPH=0 runs it eagerly)
@@ -329,7 +349,33 @@ class HypergradLM:
         self.steps += 1
         return self._graph_out.clone()
 
+    def _stepper(self, S: int, B: int):
+        from .hyper_step import SecondOrderStep
+        key = (S, B)
+        if key not in self._steppers:
+            self._steppers[key] = SecondOrderStep(self.cfg, self.specs, self.offsets, self.P, B,
+                                                  S, self.device, self.cos, self.sin)
+        return self._steppers[key]
+
     def _step_body(self, tok, tgt) -> torch.Tensor:
+        if self.mode == "explicit":
+            losses = self._stepper(3, tok.shape[1]).run(self.w, self.Z, tok, tgt, self.G)
+            g, he, hm = self.g, self.he, self.hm
+        else:
+            g, he, hm, losses = self._func_grads(tok, tgt)
+        if self.dp_comm is not None:                                            # C3
+            packed = torch.stack([g, he, hm])
+            buf = packed.to(self.dp_comm._coll_device())
+            self.dp_comm.all_reduce_mean_(buf)
+            g, he, hm = buf.to(self.device).unbind(0)
+            losses = losses.to(self.dp_comm._coll_device())
+            self.dp_comm.all_reduce_mean_(losses)
+            losses = losses.to(self.device)
+        self._update(g.contiguous(), he.contiguous(), hm.contiguous())
+        self.steps += 1
+        return losses.clone() if self.mode == "explicit" else losses
+
+    def _func_grads(self, tok, tgt):
         def loss_fn(W):
             per_trial = lm_losses(self.params(W), tok, tgt, self.cfg, self.cos, self.sin)
             return per_trial.sum(), per_trial.detach()
@@ -345,19 +391,8 @@ class HypergradLM:
         # batching rule folds the two tangents into its trial dimension) -- half the passes of
         # one jvp per hyper-parameter, same numbers
         g, losses, h = torch.func.vmap(along, out_dims=(None, None, 0))(
-            torch.stack([self.ze, self.zm]))
-        he, hm = h[0], h[1]
-        if self.dp_comm is not None:                                            # C3
-            packed = torch.stack([g, he, hm])
-            buf = packed.to(self.dp_comm._coll_device())
-            self.dp_comm.all_reduce_mean_(buf)
-            g, he, hm = buf.to(self.device).unbind(0)
-            losses = losses.to(self.dp_comm._coll_device())
-            self.dp_comm.all_reduce_mean_(losses)
-            losses = losses.to(self.device)
-        self._update(g.contiguous(), he.contiguous(), hm.contiguous())
-        self.steps += 1
-        return losses
+            self.Z)
+        return g, h[0], h[1], losses
 
     def _update(self, g, he, hm):
         if self.device.type == "cuda":
@@ -372,9 +407,14 @@ class HypergradLM:
     def hypergradient(self, tok, tgt):
         """(d L_val / d eta, d L_val / d mu) per run [P, 2] and the validation losses [P]."""
         tok, tgt = self._expand(tok), self._expand(tgt)
-        gval, lval = torch.func.grad_and_value(lambda W: self._loss_sum(W, tok, tgt))(self.w)
-        with torch.no_grad():
-            losses = lm_losses(self.params(self.w), tok, tgt, self.cfg, self.cos, self.sin)
+        if self.mode == "explicit":
+            gval = self.w.new_empty(1, *self.w.shape)
+            losses = self._stepper(1, tok.shape[1]).run(self.w, [], tok, tgt, gval).clone()
+            gval = gval[0]
+        else:
+            gval, lval = torch.func.grad_and_value(lambda W: self._loss_sum(W, tok, tgt))(self.w)
+            with torch.no_grad():
+                losses = lm_losses(self.params(self.w), tok, tgt, self.cfg, self.cos, self.sin)
         gval = gval.contiguous()
         if self.dp_comm is not None:      # C3: validation gradient over the DP group's shards
             buf = torch.cat([gval, losses[:, None]], 1).to(self.dp_comm._coll_device())

@@ -152,11 +152,23 @@ struct GemmArgs {
   Src a, b;
   bf16_t* C;
   float* C32;      // f32 output instead of C (register-staged kernel only), else nullptr
+  const float* R32;  // f32 output only: C32 = product + R32 (same layout as C32; may BE C32 --
+                     // accumulate in place), nullptr: C32 = product
   float* part;     // split-K partials [splits][P][M][N] (nullptr when splits == 1)
   int64_t sC;
+  // two-level batch of the register-staged kernel: batch index p = po * nin + pi, operand X at
+  // X + po * X.batch + pi * x_in (nin <= 1: one level, the *_in strides unused)
+  int nin;
+  int64_t a_in, b_in, c_in;
   int P, M, N, K, ldc;
   int tiles_m, tiles_n, splits, k_per_split, nwg;
 };
+
+__device__ __forceinline__ int64_t boff(int p, int nin, int64_t so, int64_t si) {
+  if (nin <= 1) return (int64_t)p * so;
+  const int po = p / nin;
+  return (int64_t)po * so + (int64_t)(p - po * nin) * si;
+}
 
 template <int KA, int KB, bool TA, bool TB, int WM, int FM, int FN>
 __global__ __launch_bounds__(256) void pgemm_kernel(const GemmArgs g) {
@@ -176,10 +188,13 @@ __global__ __launch_bounds__(256) void pgemm_kernel(const GemmArgs g) {
   const int p = t / g.splits;
 
   // (f32 operands: the trial stride counts f32 elements)
-  const bf16_t* A = KA == kDenseF32 ? (const bf16_t*)((const float*)g.a.ptr + p * g.a.batch)
-                                    : g.a.ptr + p * g.a.batch;
-  const bf16_t* B = KB == kDenseF32 ? (const bf16_t*)((const float*)g.b.ptr + p * g.b.batch)
-                                    : g.b.ptr + p * g.b.batch;
+  const int64_t offA = boff(p, g.nin, g.a.batch, g.a_in);
+  const int64_t offB = boff(p, g.nin, g.b.batch, g.b_in);
+  const int64_t offC = boff(p, g.nin, g.sC, g.c_in);
+  const bf16_t* A = KA == kDenseF32 ? (const bf16_t*)((const float*)g.a.ptr + offA)
+                                    : g.a.ptr + offA;
+  const bf16_t* B = KB == kDenseF32 ? (const bf16_t*)((const float*)g.b.ptr + offB)
+                                    : g.b.ptr + offB;
   const int m0 = tm * BM, n0 = tn * BN;
   const int kb = sp * g.k_per_split;
   const int ke = min(g.K, kb + g.k_per_split);
@@ -234,7 +249,8 @@ __global__ __launch_bounds__(256) void pgemm_kernel(const GemmArgs g) {
   // through LDS (the operand buffers are free after the loop's last barrier) so every lane
   // stores whole 16-byte row segments instead of scattered 2-byte elements.
   if (g.splits == 1 && g.C32 != nullptr) {  // f32 output: fragments stored as they are
-    float* C = g.C32 + p * g.sC;
+    float* C = g.C32 + offC;
+    const float* R = g.R32 == nullptr ? nullptr : g.R32 + offC;
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -244,7 +260,10 @@ __global__ __launch_bounds__(256) void pgemm_kernel(const GemmArgs g) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int m = m0 + wm * 16 * FM + 16 * i + 4 * gq + r;
-          if (m < g.M) C[(int64_t)m * g.ldc + n] = acc[i][j][r];
+          if (m < g.M) {
+            const int64_t o = (int64_t)m * g.ldc + n;
+            C[o] = R == nullptr ? acc[i][j][r] : acc[i][j][r] + R[o];
+          }
         }
       }
   } else if (g.splits == 1) {
@@ -260,7 +279,7 @@ __global__ __launch_bounds__(256) void pgemm_kernel(const GemmArgs g) {
           Cs[(wm * 16 * FM + 16 * i + 4 * gq + r) * LSC + wn * 16 * FN + 16 * j + li] =
               f2bf(acc[i][j][r]);
     __syncthreads();
-    bf16_t* C = g.C + p * g.sC;
+    bf16_t* C = g.C + offC;
     constexpr int CPR = BN / 8;  // 16-byte chunks per tile row
 #pragma unroll
     for (int c = threadIdx.x; c < BM * CPR; c += 256) {
@@ -488,17 +507,19 @@ __global__ __launch_bounds__(512) void pgemm_big_kernel(const GemmArgs g) {
 // sum of the split-K partials [splits][P][M][N] -> C[p][m][n * ldc] bf16
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part,
                                                             bf16_t* __restrict__ C,
-                                                            float* __restrict__ C32, int64_t sC,
-                                                            int ldc, int P, int M, int N,
-                                                            int splits) {
+                                                            float* C32, const float* R32,
+                                                            int64_t sC, int ldc, int P, int M,
+                                                            int N, int splits, int nin,
+                                                            int64_t c_in) {
   const int64_t total = (int64_t)P * M * N;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= total) return;
   float s = 0.f;
   for (int k = 0; k < splits; ++k) s += part[k * total + i];
   const int64_t n = i % N, m = (i / N) % M, p = i / ((int64_t)M * N);
-  if (C32 != nullptr) C32[p * sC + m * ldc + n] = s;
-  else C[p * sC + m * ldc + n] = f2bf(s);
+  const int64_t o = boff((int)p, nin, sC, c_in) + m * ldc + n;
+  if (C32 != nullptr) C32[o] = R32 == nullptr ? s : s + R32[o];
+  else C[o] = f2bf(s);
 }
 
 template <int KA, int KB, bool TA, bool TB, int WM, int FM, int FN>
@@ -565,7 +586,8 @@ int dispatch_conv_tile(const GemmArgs& g, int cfg, hipStream_t st) {
 int finish_splitk(const GemmArgs& g, hipStream_t st) {
   const int64_t total = (int64_t)g.P * g.M * g.N;
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                     st, (const float*)g.part, g.C, g.C32, g.sC, g.ldc, g.P, g.M, g.N, g.splits);
+                     st, (const float*)g.part, g.C, g.C32, g.R32, g.sC, g.ldc, g.P, g.M, g.N,
+                     g.splits, g.nin, g.c_in);
   return (int)hipGetLastError();
 }
 
@@ -630,9 +652,13 @@ int mopt_pgemm(const void* A, const void* B, void* C, void* part, int P, int M, 
 
 // mopt_pgemm with f32 operands and f32 output (a32/b32/c32 all 1; the register-staged tiles
 // only, cfg 0..4): operands are rounded to bf16 as they are staged, accumulation f32.
-int mopt_pgemm_f32(const void* A, const void* B, void* C, void* part, int P, int M, int N, int K,
-                   int lda, int ldb, int ldc, int64_t sA, int64_t sB, int64_t sC, int ta, int tb,
-                   int cfg, int splits, int k_per_split, void* stream) {
+// ``res``: C = product + res (res laid out as C; res == C accumulates in place), or nullptr.
+// Two-level batch (nin > 1): P counts outer x inner problems, problem p = po * nin + pi reads
+// A + po * sA + pi * sA_in (likewise B, C / res); strides may be 0 (a broadcast operand).
+int mopt_pgemm_f32b(const void* A, const void* B, void* C, const void* res, void* part, int P,
+                    int M, int N, int K, int lda, int ldb, int ldc, int64_t sA, int64_t sB,
+                    int64_t sC, int ta, int tb, int cfg, int splits, int k_per_split, int nin,
+                    int64_t sA_in, int64_t sB_in, int64_t sC_in, void* stream) {
   if (P <= 0 || M <= 0 || N <= 0 || K <= 0) return 0;
   if (cfg < 0 || cfg > 4 || splits < 1 ||
       (splits > 1 && (part == nullptr || k_per_split % BK))) {
@@ -643,6 +669,11 @@ int mopt_pgemm_f32(const void* A, const void* B, void* C, void* part, int P, int
   g.a = ta ? dense(A, sA, lda, K, M) : dense(A, sA, lda, M, K);
   g.b = tb ? dense(B, sB, ldb, N, K) : dense(B, sB, ldb, K, N);
   g.C32 = (float*)C;
+  g.R32 = (const float*)res;
+  g.nin = nin;
+  g.a_in = sA_in;
+  g.b_in = sB_in;
+  g.c_in = sC_in;
   g.part = (float*)part;
   g.sC = sC;
   g.P = P; g.M = M; g.N = N; g.K = K; g.ldc = ldc;
@@ -655,6 +686,21 @@ int mopt_pgemm_f32(const void* A, const void* B, void* C, void* part, int P, int
   else err = dispatch_tile<kDenseF32, kDenseF32, true, true>(g, cfg, st);
   if (err || splits == 1) return err;
   return finish_splitk(g, st);
+}
+
+int mopt_pgemm_f32r(const void* A, const void* B, void* C, const void* res, void* part, int P,
+                    int M, int N, int K, int lda, int ldb, int ldc, int64_t sA, int64_t sB,
+                    int64_t sC, int ta, int tb, int cfg, int splits, int k_per_split,
+                    void* stream) {
+  return mopt_pgemm_f32b(A, B, C, res, part, P, M, N, K, lda, ldb, ldc, sA, sB, sC, ta, tb, cfg,
+                         splits, k_per_split, 1, 0, 0, 0, stream);
+}
+
+int mopt_pgemm_f32(const void* A, const void* B, void* C, void* part, int P, int M, int N, int K,
+                   int lda, int ldb, int ldc, int64_t sA, int64_t sB, int64_t sC, int ta, int tb,
+                   int cfg, int splits, int k_per_split, void* stream) {
+  return mopt_pgemm_f32r(A, B, C, nullptr, part, P, M, N, K, lda, ldb, ldc, sA, sB, sC, ta, tb,
+                         cfg, splits, k_per_split, stream);
 }
 
 // Implicit-GEMM 3x3 convolution (pad 1, stride 1|2) of a population, NHWC bf16:

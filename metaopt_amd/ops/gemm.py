@@ -34,6 +34,10 @@ _lib.register_signatures({
                    c_int),
     "mopt_pgemm_f32": ([c_void_p] * 4 + [c_int] * 7 + [c_int64] * 3 + [c_int] * 5 + [c_void_p],
                        c_int),
+    "mopt_pgemm_f32r": ([c_void_p] * 5 + [c_int] * 7 + [c_int64] * 3 + [c_int] * 5 + [c_void_p],
+                        c_int),
+    "mopt_pgemm_f32b": ([c_void_p] * 5 + [c_int] * 7 + [c_int64] * 3 + [c_int] * 6 +
+                        [c_int64] * 3 + [c_void_p], c_int),
 })
 
 # tile configurations of csrc/pgemm.hip: cfg -> (BM, BN).  0-4: 4-wave register-staged kernel
@@ -112,10 +116,11 @@ def plan(P: int, M: int, N: int, K: int, cfg: Optional[int] = None,
 
 
 def _check_operand(t: torch.Tensor, name: str, dtype=torch.bfloat16) -> None:
-    if t.dtype != dtype or t.dim() != 3 or t.stride(2) != 1:
+    if t.dtype != dtype or t.dim() not in (3, 4) or t.stride(-1) != 1:
         raise ValueError(f"pgemm: {name} must be a [P, rows, cols] {dtype} tensor with unit "
                          f"column stride, got {t.dtype} {tuple(t.shape)} strides {t.stride()}")
-    if t.shape[2] % 8 or t.stride(1) % 8 or (t.shape[0] > 1 and t.stride(0) % 8) or \
+    if t.shape[-1] % 8 or t.stride(-2) % 8 or \
+            any(t.shape[i] > 1 and t.stride(i) % 8 for i in range(t.dim() - 2)) or \
             t.data_ptr() % 16:
         raise ValueError(f"pgemm: {name} rows must be 16-byte aligned multiples of 8 elements "
                          f"(shape {tuple(t.shape)}, strides {t.stride()})")
@@ -123,14 +128,19 @@ def _check_operand(t: torch.Tensor, name: str, dtype=torch.bfloat16) -> None:
 
 def pgemm(a: torch.Tensor, b: torch.Tensor, ta: bool = False, tb: bool = False,
           out: Optional[torch.Tensor] = None, cfg: Optional[int] = None,
-          splits: Optional[int] = None) -> torch.Tensor:
+          splits: Optional[int] = None, res: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``out[p] = op(a[p]) @ op(b[p])`` in bf16 with f32 accumulation on the MFMA kernel.  f32
     operands give an f32 product: they are rounded to bf16 while the kernel stages them (no cast
-    kernels) and the f32 accumulators are stored as they are."""
+    kernels) and the f32 accumulators are stored as they are.  ``res`` (f32 only, same shape and
+    strides as ``out``, may be ``out`` itself): ``out = product + res`` in the epilogue -- a
+    residual add or an in-place accumulation without a separate elementwise pass."""
     if a.device.type != "cuda":
-        aa = a.transpose(1, 2) if ta else a
-        bb = b.transpose(1, 2) if tb else b
-        r = torch.bmm(aa.float(), bb.float()).to(a.dtype)
+        aa = a.transpose(-1, -2) if ta else a
+        bb = b.transpose(-1, -2) if tb else b
+        r = torch.matmul(aa.float(), bb.float())
+        if res is not None:
+            r = r + res
+        r = r.to(out.dtype if out is not None else a.dtype)
         if out is not None:
             out.copy_(r)
             return out
@@ -141,30 +151,52 @@ def pgemm(a: torch.Tensor, b: torch.Tensor, ta: bool = False, tb: bool = False,
         a, b = a.float(), b.float()
     _check_operand(a, "a", dt)
     _check_operand(b, "b", dt)
-    P = a.shape[0]
-    K, M = (a.shape[1], a.shape[2]) if ta else (a.shape[2], a.shape[1])
-    N, Kb = (b.shape[1], b.shape[2]) if tb else (b.shape[2], b.shape[1])
-    if K != Kb or b.shape[0] != P:
+    # 4-D operands [Po, I, rows, cols]: a two-level batch (any dim-0/1 strides, 0 = broadcast;
+    # f32 only), flattened to P = Po * I problems
+    four = a.dim() == 4
+    if four != (b.dim() == 4) or (four and not f32):
+        raise ValueError("pgemm: 4-D (two-level batch) operands must both be 4-D f32")
+    lead = tuple(a.shape[:-2])
+    K, M = (a.shape[-2], a.shape[-1]) if ta else (a.shape[-1], a.shape[-2])
+    N, Kb = (b.shape[-2], b.shape[-1]) if tb else (b.shape[-1], b.shape[-2])
+    if K != Kb or tuple(b.shape[:-2]) != lead:
         raise ValueError(f"pgemm: shape mismatch a {tuple(a.shape)} (ta={ta}) b "
                          f"{tuple(b.shape)} (tb={tb})")
+    P = a.shape[0] * (a.shape[1] if four else 1)
     if N % 8:
         raise ValueError(f"pgemm: N = {N} must be a multiple of 8 (16-byte output rows)")
     if out is None:
-        out = torch.empty(P, M, N, dtype=dt, device=a.device)
-    elif tuple(out.shape) != (P, M, N) or out.stride(2) != 1 or out.dtype != dt:
-        raise ValueError(f"pgemm: out must be [P, M, N] = {(P, M, N)} {dt} row-major")
+        out = torch.empty(*lead, M, N, dtype=dt, device=a.device)
+    elif tuple(out.shape) != (*lead, M, N) or out.stride(-1) != 1 or out.dtype != dt:
+        raise ValueError(f"pgemm: out must be {(*lead, M, N)} {dt} row-major")
     _check_operand(out, "out", dt)
+    if res is not None:
+        if not f32 or res.dtype != torch.float32 or res.shape != out.shape or \
+                res.stride() != out.stride():
+            raise ValueError("pgemm: res must be an f32 tensor laid out exactly like out "
+                             "(f32 operands only)")
     if f32 and (cfg is None or cfg in BIG_TILES):
         cfg = pick_tile(M, N)          # f32 operands: the register-staged tiles only
     cfg, splits, kps = plan(P, M, N, K, cfg, splits)
     part = (torch.empty(splits, P, M, N, dtype=torch.float32, device=a.device)
             if splits > 1 else None)
-    fn = _lib.get_lib().mopt_pgemm_f32 if f32 else _lib.get_lib().mopt_pgemm
-    _lib.check(fn(
-        a.data_ptr(), b.data_ptr(), out.data_ptr(), 0 if part is None else part.data_ptr(),
-        P, M, N, K, a.stride(1), b.stride(1), out.stride(1), a.stride(0), b.stride(0),
-        out.stride(0), int(ta), int(tb), cfg, splits, kps, _lib.stream_ptr(a.device)),
-        "pgemm")
+    pp = 0 if part is None else part.data_ptr()
+    lib = _lib.get_lib()
+    if four:
+        _lib.check(lib.mopt_pgemm_f32b(
+            a.data_ptr(), b.data_ptr(), out.data_ptr(), 0 if res is None else res.data_ptr(),
+            pp, P, M, N, K, a.stride(2), b.stride(2), out.stride(2), a.stride(0), b.stride(0),
+            out.stride(0), int(ta), int(tb), cfg, splits, kps, a.shape[1], a.stride(1),
+            b.stride(1), out.stride(1), _lib.stream_ptr(a.device)), "pgemm")
+        return out
+    tail = (P, M, N, K, a.stride(1), b.stride(1), out.stride(1), a.stride(0), b.stride(0),
+            out.stride(0), int(ta), int(tb), cfg, splits, kps, _lib.stream_ptr(a.device))
+    if res is not None:
+        _lib.check(lib.mopt_pgemm_f32r(a.data_ptr(), b.data_ptr(), out.data_ptr(),
+                                       res.data_ptr(), pp, *tail), "pgemm")
+    else:
+        fn = lib.mopt_pgemm_f32 if f32 else lib.mopt_pgemm
+        _lib.check(fn(a.data_ptr(), b.data_ptr(), out.data_ptr(), pp, *tail), "pgemm")
     return out
 
 
