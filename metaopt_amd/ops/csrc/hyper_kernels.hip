@@ -221,7 +221,7 @@ __global__ __launch_bounds__(256) void hy_norm_fwd_kernel(const float* __restric
 // Adjoint (and its tangents) of the RMSNorm stack; GX (+)= the input adjoints, the weight
 // gradients G_s are summed over the block's rows in registers and LDS, then added atomically.
 // Block: 4 waves x RPW rows of one trial.
-constexpr int kNormRPW = 8;
+constexpr int kNormRPW = 2;  // 8 rows per block: >= 2 blocks per CU at 4096 rows
 template <int NK>
 __global__ __launch_bounds__(256) void hy_norm_bwd_kernel(const float* __restrict__ X,
                                                           const float* __restrict__ GY, Ptr3 a,
@@ -526,12 +526,14 @@ __device__ __forceinline__ float block_max(float v, float* red) {
 }
 
 // In place over the logits stack Z [P][S R][V]: slice 0 -> (pi - onehot) / R, slice t ->
-// pi (z_t - <pi, z_t>) / R; losses[p] += nll / R.  One workgroup per (p, r).
+// pi (z_t - <pi, z_t>) / R; losses[p] += nll / R.  One workgroup per (p, r); the primal row is
+// read from HBM once and kept in LDS (V floats of dynamic shared memory) for every later pass.
 __global__ __launch_bounds__(256) void hy_ce_kernel(float* __restrict__ Z,
                                                     const int* __restrict__ tgt,
                                                     int64_t tgt_stride,
                                                     float* __restrict__ losses, int P, int R,
                                                     int V, int S) {
+  extern __shared__ float zrow[];
   __shared__ float red[4];
   const int row = blockIdx.x;
   const int p = row / R, r = row - p * R;
@@ -540,15 +542,22 @@ __global__ __launch_bounds__(256) void hy_ce_kernel(float* __restrict__ Z,
   float mx = -INFINITY;
   for (int c = 4 * threadIdx.x; c < V; c += 1024) {
     const f32x4 v = *(const f32x4*)(z + c);
+    *(f32x4*)(zrow + c) = v;
     mx = fmaxf(fmaxf(mx, fmaxf(v[0], v[1])), fmaxf(v[2], v[3]));
   }
-  mx = block_max(mx, red);
+  mx = block_max(mx, red);  // (its barriers also publish zrow)
   float se = 0.f;
   for (int c = 4 * threadIdx.x; c < V; c += 1024) {
-    const f32x4 v = *(const f32x4*)(z + c);
-    se += __expf(v[0] - mx) + __expf(v[1] - mx) + __expf(v[2] - mx) + __expf(v[3] - mx);
+    f32x4 v = *(const f32x4*)(zrow + c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[e] = __expf(v[e] - mx);
+      se += v[e];
+    }
+    *(f32x4*)(zrow + c) = v;  // unnormalised softmax, own chunk
   }
-  const float lse = mx + __logf(block_sum(se, red));
+  const float sum = block_sum(se, red);
+  const float lse = mx + __logf(sum), inv = 1.f / sum;
   const float invR = 1.f / R;
   const bool ok = MOPT_IN_RANGE(y, V, "hyper target id");
   if (threadIdx.x == 0 && ok) atomicAdd(losses + p, (lse - z[y]) * invR);
@@ -556,24 +565,23 @@ __global__ __launch_bounds__(256) void hy_ce_kernel(float* __restrict__ Z,
     float* zt = z + (int64_t)t * R * V;
     float m = 0.f;
     for (int c = 4 * threadIdx.x; c < V; c += 1024) {
-      const f32x4 v = *(const f32x4*)(z + c), w = *(const f32x4*)(zt + c);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) m += __expf(v[e] - lse) * w[e];
+      const f32x4 e = *(const f32x4*)(zrow + c), w = *(const f32x4*)(zt + c);
+      m += e[0] * w[0] + e[1] * w[1] + e[2] * w[2] + e[3] * w[3];
     }
-    m = block_sum(m, red);
+    m = block_sum(m, red) * inv;
     for (int c = 4 * threadIdx.x; c < V; c += 1024) {
-      const f32x4 v = *(const f32x4*)(z + c);
+      const f32x4 e = *(const f32x4*)(zrow + c);
       f32x4 w = *(const f32x4*)(zt + c);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) w[e] = __expf(v[e] - lse) * (w[e] - m) * invR;
+      for (int k = 0; k < 4; ++k) w[k] = e[k] * inv * (w[k] - m) * invR;
       *(f32x4*)(zt + c) = w;
     }
   }
-  __syncthreads();  // every read of the primal row is done before it is overwritten
+  __syncthreads();  // the read of z[y] above is done before the row is overwritten
   for (int c = 4 * threadIdx.x; c < V; c += 1024) {
-    f32x4 v = *(const f32x4*)(z + c);
+    f32x4 v = *(const f32x4*)(zrow + c);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = (__expf(v[e] - lse) - (c + e == y ? 1.f : 0.f)) * invR;
+    for (int e = 0; e < 4; ++e) v[e] = (v[e] * inv - (c + e == y ? 1.f : 0.f)) * invR;
     *(f32x4*)(z + c) = v;
   }
 }
@@ -732,10 +740,11 @@ int mopt_hy_swiglu(const void* GU, void* A_or_GA, void* GGU, int P, int R, int F
 
 int mopt_hy_ce(void* Z, const void* tgt, int64_t tgt_stride, void* losses, int P, int R, int V,
                int S, void* stream) {
-  if (V % 4) return (int)hipErrorInvalidValue;
+  if (V % 4 || V > 16384) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   (void)hipMemsetAsync(losses, 0, sizeof(float) * P, st);
-  hipLaunchKernelGGL(hy_ce_kernel, dim3(P * R), dim3(256), 0, st, (float*)Z, (const int*)tgt,
+  hipLaunchKernelGGL(hy_ce_kernel, dim3(P * R), dim3(256), sizeof(float) * V, st, (float*)Z,
+                     (const int*)tgt,
                      tgt_stride, (float*)losses, P, R, V, S);
   return (int)hipGetLastError();
 }

@@ -65,6 +65,19 @@ def pick_tile(M: int, N: int) -> int:
     return 0
 
 
+def f32_plan(M: int, N: int, ta: bool):
+    """(tile cfg, splits) of an f32-operand GEMM (the K11 second-order step's shapes,
+    profiles/r3/gemm32_k11.json): never split K -- the f32 partial tiles and the reduce pass
+    cost more than the parallelism they add at these sizes (1.3-3.5x slower) -- and use the
+    64-row tiles, whose 2-4x more workgroups fill the chip at P = 8..24 problems: 64 x 128 for
+    weight gradients (TN) and wide outputs, 64 x 64 otherwise."""
+    if N < 64:
+        return pick_tile(M, N), 1
+    if (ta and N >= 128) or N >= 2048:
+        return 4, 1
+    return 3, 1
+
+
 def big_fits(M: int, N: int, K: int, cfg: int) -> bool:
     bm, bn = TILES[cfg]
     return M % bm == 0 and N % bn == 0 and K % 64 == 0
@@ -175,7 +188,9 @@ def pgemm(a: torch.Tensor, b: torch.Tensor, ta: bool = False, tb: bool = False,
                 res.stride() != out.stride():
             raise ValueError("pgemm: res must be an f32 tensor laid out exactly like out "
                              "(f32 operands only)")
-    if f32 and (cfg is None or cfg in BIG_TILES):
+    if f32 and cfg is None and splits is None:
+        cfg, splits = f32_plan(M, N, ta)
+    elif f32 and (cfg is None or cfg in BIG_TILES):
         cfg = pick_tile(M, N)          # f32 operands: the register-staged tiles only
     cfg, splits, kps = plan(P, M, N, K, cfg, splits)
     part = (torch.empty(splits, P, M, N, dtype=torch.float32, device=a.device)

@@ -14,7 +14,7 @@
 #   kbench_rows      the microbench at 128 / 256 / 512 rows per step (multi-row-block kernels)
 #   pmc_kbench       PMC passes of the MLP kernels (fetch/write/MFMA/LDS, one pass each)
 #   lm resnet hyper  bench_configs.py of one config        trace_lm trace_resnet trace_hyper
-#   gemm conv        pgemm / direct-conv microbenches
+#   gemm conv        pgemm / direct-conv microbenches      gemm32  f32-operand (K11) GEMM plans
 #   decide           rank-0 decide cost at simulated W=1,8 (host CPU of the box)
 #   rehearsal        bench.py --gpus 2 / 4 / 8 over gloo with ranks sharing the GPU
 set -e
@@ -62,6 +62,7 @@ for step in "$@"; do
     trace_resnet) prof trace_resnet 300 -- python3 "$ROOT/scripts/bench_configs.py" --config resnet20 --steps 20 --warmup 10 ;;
     trace_hyper) prof trace_hyper 300 -- python3 "$ROOT/scripts/bench_configs.py" --config hyper --steps 1 --warmup 1 ;;
     gemm)       $T 300 python scripts/gemm_bench.py --cfgs "${CFGS:-0,5,6,7}" --out "$OUT/gemm.json" > "$OUT/gemm.log" 2>&1 ;;
+    gemm32)     $T 300 python scripts/gemm_f32_bench.py --out "$OUT/gemm32.json" > "$OUT/gemm32.log" 2>&1 ;;
     conv)       $T 200 python scripts/conv_bench.py --implicit --out "$OUT/conv_bench.json" > "$OUT/conv_bench.log" 2>&1 ;;
     decide)     for w in 1 8; do WORLD=$w $T 300 python scripts/profile_decide.py > "$OUT/decide_world$w.log" 2>&1; done ;;
     rehearsal)  for n in 2 4 8; do $T 400 python bench.py --gpus $n --steps 10 --warmup 3 --population 64 > "$OUT/rehearsal_n$n.json" 2> "$OUT/rehearsal_n$n.err"; done ;;

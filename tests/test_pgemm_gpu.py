@@ -131,3 +131,44 @@ def test_f32_operands_and_output(ta, tb, P, M, N, K, splits):
     ref16 = pgemm(a, b, ta=ta, tb=tb, cfg=pgemm.__globals__["pick_tile"](M, N), splits=splits)
     # same inputs after rounding, same tile order: the bf16 path is the f32 result rounded
     assert torch.equal(got.to(torch.bfloat16), ref16)
+
+
+def _bf(x):
+    return x.to(torch.bfloat16).float()
+
+
+@pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False)])
+@pytest.mark.parametrize("splits", [None, 1, 2])
+def test_f32_two_level_batch_broadcast_and_accumulate(ta, tb, splits):
+    """4-D operands [Po, I, ., .] with a broadcast (stride-0) inner dim and strided slices, the
+    f32 epilogue residual / in-place accumulation (res), with and without split-K -- the
+    patterns of the K11 second-order step (models/hyper_step.py)."""
+    g = torch.Generator(device=DEV).manual_seed(3)
+    Po, I, M, N, K = 3, 2, 72, 136, 256
+    base_a = torch.randn(Po, 3, *((K, M) if ta else (M, K)), device=DEV, generator=g)
+    a = base_a[:, :1].expand(-1, I, -1, -1)             # inner dim broadcast
+    bb = torch.randn(I, Po, *((N, K) if tb else (K, N)), device=DEV, generator=g)
+    b = bb.permute(1, 0, 2, 3)                           # inner stride = Po * K * N
+    outbuf = torch.randn(Po, I + 1, M, N, device=DEV, generator=g)
+    out = outbuf[:, 1:]                                  # strided output slices
+    before = out.clone()
+    pgemm(a, b, ta=ta, tb=tb, out=out, res=out, splits=splits)
+    A = _bf(a.transpose(-1, -2) if ta else a)
+    B = _bf(b.transpose(-1, -2) if tb else b)
+    ref = before + torch.matmul(A, B)
+    assert (out - ref).abs().max().item() <= 1e-3 * ref.abs().max().item()
+    # a separate residual (out = product + res), 3-D
+    r = torch.randn(Po, M, N, device=DEV, generator=g)
+    o3 = pgemm(base_a[:, 0], bb[0], ta=ta, tb=tb, out=torch.empty(Po, M, N, device=DEV),
+               res=r, splits=splits)
+    ref3 = r + torch.matmul(_bf(base_a[:, 0].transpose(-1, -2) if ta else base_a[:, 0]),
+                            _bf(bb[0].transpose(-1, -2) if tb else bb[0]))
+    assert (o3 - ref3).abs().max().item() <= 1e-3 * ref3.abs().max().item()
+    assert torch.equal(outbuf[:, 0], outbuf[:, 0])      # untouched slice stays finite
+
+
+def test_res_requires_matching_layout():
+    a = torch.randn(2, 64, 64, device=DEV)
+    out = torch.empty(2, 64, 64, device=DEV)
+    with pytest.raises(ValueError, match="res"):
+        pgemm(a, a, out=out, res=torch.empty(2, 64, 64, device=DEV).transpose(1, 2))
