@@ -151,8 +151,9 @@ def test_f32_two_level_batch_broadcast_and_accumulate(ta, tb, splits):
     b = bb.permute(1, 0, 2, 3)                           # inner stride = Po * K * N
     outbuf = torch.randn(Po, I + 1, M, N, device=DEV, generator=g)
     out = outbuf[:, 1:]                                  # strided output slices
-    before = out.clone()
+    before, keep = out.clone(), outbuf[:, 0].clone()
     pgemm(a, b, ta=ta, tb=tb, out=out, res=out, splits=splits)
+    assert torch.equal(outbuf[:, 0], keep)              # the slice outside out is untouched
     A = _bf(a.transpose(-1, -2) if ta else a)
     B = _bf(b.transpose(-1, -2) if tb else b)
     ref = before + torch.matmul(A, B)
@@ -164,7 +165,6 @@ def test_f32_two_level_batch_broadcast_and_accumulate(ta, tb, splits):
     ref3 = r + torch.matmul(_bf(base_a[:, 0].transpose(-1, -2) if ta else base_a[:, 0]),
                             _bf(bb[0].transpose(-1, -2) if tb else bb[0]))
     assert (o3 - ref3).abs().max().item() <= 1e-3 * ref3.abs().max().item()
-    assert torch.equal(outbuf[:, 0], outbuf[:, 0])      # untouched slice stays finite
 
 
 def test_res_requires_matching_layout():
