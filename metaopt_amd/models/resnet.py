@@ -91,6 +91,27 @@ class PopulationResNet(FlatPopulation):
         return cops.conv_bn_act(x, w, W[f"{name}.g"], W[f"{name}.b"], running, P, stride, train,
                                 res=res, relu=relu, arena=arena, **mail)
 
+    def _block_fused(self, n1, n2, h, s1, identity, arena, box):
+        """One training basic block on the HIP path: conv1 (+ its BatchNorm's batch sums),
+        BatchNorm 1 + ReLU applied inside conv2 (``bn_relu_conv3x3``: its output never reaches
+        HBM) when the shapes allow, BatchNorm 2 + shortcut + ReLU; the shortcut's gradient joins
+        conv1's data gradient in its epilogue (``box``)."""
+        P, W = self.capacity, self.W
+        w1, w2 = W[f"{n1}.w"], W[f"{n2}.w"]
+        c1, c2 = w1.shape[-1], w2.shape[-1]
+        run1 = self.A[f"{n1}.running"].view(P, 2, c1)
+        run2 = self.A[f"{n2}.running"].view(P, 2, c2)
+        y1, st1 = cops.conv_stats(h, w1, P, s1, True, arena=arena, mailbox=box)
+        if cops.bn_into_conv_ok(y1, w2, P, 1, True, arena, st1 is not None):
+            y2, st2 = cops.bn_relu_conv3x3(y1, W[f"{n1}.g"], W[f"{n1}.b"], run1, w2, P, st1,
+                                           arena)
+        else:
+            t = cops.bn_act(y1, W[f"{n1}.g"], W[f"{n1}.b"], run1, P, True, sums=st1,
+                            arena=arena)
+            y2, st2 = cops.conv_stats(t, w2, P, 1, True, arena=arena)
+        return cops.bn_act(y2, W[f"{n2}.g"], W[f"{n2}.b"], run2, P, True, res=h.detach(),
+                           sums=st2, arena=arena, mailbox=box, res_sub2=not identity)
+
     @staticmethod
     def _shortcut(x, cout, stride):
         if stride == 1 and x.shape[-1] == cout:
@@ -117,9 +138,7 @@ class PopulationResNet(FlatPopulation):
                     # kernel's epilogue (no separate add over the block input); an option-A
                     # shortcut is also read in place by the BatchNorm (no padded copy)
                     box = {}
-                    t = self._conv_bn(n1, h, s1, train, arena=arena, conv_mailbox=box)
-                    h = self._conv_bn(n2, t, 1, train, res=h.detach(), arena=arena,
-                                      bn_mailbox=box, res_sub2=not identity)
+                    h = self._block_fused(n1, n2, h, s1, identity, arena, box)
                     continue
                 r = self._shortcut(h, c2, s1)
                 t = self._conv_bn(n1, h, s1, train, arena=arena)

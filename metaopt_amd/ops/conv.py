@@ -31,7 +31,10 @@ _lib.register_signatures({
     "mopt_pconv": ([c_int] + [c_void_p] * 4 + [c_int] * 10 + [c_void_p], c_int),
     "mopt_dconv": ([c_int] + [c_void_p] * 4 + [c_int] * 7 + [c_void_p], c_int),
     "mopt_dconv_wgrad_splits": ([c_int] * 6, c_int),
+    "mopt_dconv_bnin": ([c_int] + [c_void_p] * 4 + [c_int] * 5 + [c_void_p] * 4, c_int),
 })
+# MOPT_BN_INTO_CONV=0: materialise every BatchNorm output (A/B switch of bn_relu_conv3x3)
+_BN_INTO_CONV = os.environ.get("MOPT_BN_INTO_CONV", "1") != "0"
 
 _NOT_SUPPORTED = 801   # hipErrorNotSupported: no direct-conv instantiation for the shape
 # MOPT_CONV_IMPLICIT=1 routes every convolution through the implicit GEMM (A/B and fallback check)
@@ -258,6 +261,111 @@ class _BNAct(torch.autograd.Function):
         dgamma = sums[:, 1].to(gamma.dtype)
         dbeta = sums[:, 0].to(gamma.dtype)
         return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None
+
+
+class _BNReluConv3x3(torch.autograd.Function):
+    """``conv3x3(relu(BN(x)), w)`` of a stride-1 convolution over a training-mode BatchNorm
+    whose output has no other consumer (the second convolution of a ResNet basic block): the
+    BatchNorm computes its statistics only (batch sums from the producing convolution's
+    epilogue) and the convolution applies ``relu(x sc + sh)`` while staging its halo bands, in
+    the forward and again in the weight gradient -- the BatchNorm output (one activation tensor
+    written and read back per layer) never reaches HBM.  Backward: data gradient of the
+    convolution, the BatchNorm backward with relu' recomputed from x (mode 2), weight gradient
+    with the BatchNorm re-applied on the fly."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, w, running, P, eps, momentum, sums, out_sums, arena,
+                grad_w):
+        N, H, W, C = x.shape
+        Co = w.shape[-1]
+        M = x.numel() // (P * C)
+        stat = torch.empty(P, 2, C, dtype=torch.float32, device=x.device)
+        _call("mopt_bn_fwd", x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), 0, 0,
+              stat.data_ptr(), running.data_ptr(), sums.data_ptr(), P, M, C, eps, momentum, 1, 1,
+              1, 0, 0, _s(x))
+        y = torch.empty(N, H, W, Co, dtype=x.dtype, device=x.device)
+        _call("mopt_dconv_bnin", 0, x.data_ptr(), w.data_ptr(), y.data_ptr(),
+              out_sums.data_ptr(), P, N // P, H, C, Co, stat.data_ptr(), gamma.data_ptr(),
+              beta.data_ptr(), _s(x))
+        ctx.save_for_backward(x, gamma, beta, w, stat)
+        ctx.meta = (P, M, C, Co)
+        ctx.bwd_sums = arena.take(P * 2 * C).view(P, 2, C) if arena is not None else None
+        ctx.grads = tuple(t.grad if (t.requires_grad and t.is_leaf and t.grad is not None) else None
+                          for t in (gamma, beta))
+        ctx.grad_w = grad_w
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, gamma, beta, w, stat = ctx.saved_tensors
+        P, M, C, Co = ctx.meta
+        N, H, W, _ = x.shape
+        Bn = N // P
+        dy = dy.contiguous()
+        # data gradient of the convolution = the BatchNorm output's gradient
+        dbn = torch.empty_like(x)
+        _pconv(1, dy, w, dbn, P, Bn, H, W, C, Co, 1)
+        dx = torch.empty_like(x)
+        zeroed = ctx.bwd_sums is not None
+        sums = ctx.bwd_sums if zeroed else torch.empty(P, 2, C, dtype=torch.float32,
+                                                       device=x.device)
+        gg, gb = ctx.grads
+        direct = gg is not None and gb is not None and gg.is_contiguous() and gb.is_contiguous()
+        _call("mopt_bn_bwd", x.data_ptr(), 0, dbn.data_ptr(), stat.data_ptr(), gamma.data_ptr(),
+              beta.data_ptr(), dx.data_ptr(), 0, sums.data_ptr(),
+              gg.data_ptr() if direct else 0, gb.data_ptr() if direct else 0,
+              P, M, C, 2, int(zeroed), _s(x))
+        # weight gradient over relu(BN(x)), applied again while staging
+        dw = ctx.grad_w if ctx.grad_w is not None else torch.empty_like(w)
+        lib = _lib.get_lib()
+        nb = lib.mopt_dconv_wgrad_splits(P, Bn, H, C, Co, 1)
+        part = torch.empty(max(nb, 1) * P * 9 * C * Co, dtype=torch.float32, device=x.device)
+        _call("mopt_dconv_bnin", 2, x.data_ptr(), dy.data_ptr(), dw.data_ptr(), part.data_ptr(),
+              P, Bn, H, C, Co, stat.data_ptr(), gamma.data_ptr(), beta.data_ptr(), _s(x))
+        dgamma = dbeta = None
+        if not direct:
+            dgamma = sums[:, 1].to(gamma.dtype)
+            dbeta = sums[:, 0].to(gamma.dtype)
+        return (dx, dgamma, dbeta, None if ctx.grad_w is not None else dw) + (None,) * 8
+
+
+def bn_into_conv_ok(x, w, P, stride, train, arena, sums_ready) -> bool:
+    """Whether ``bn_relu_conv3x3`` can run: training with the step's zero arena and the batch
+    sums of x from its producing convolution, a stride-1 square convolution with Ci == Co in
+    {16, 32, 64} on the direct kernels."""
+    if not (_BN_INTO_CONV and _DIRECT and train and arena is not None and sums_ready):
+        return False
+    if x.device.type != "cuda" or stride != 1:
+        return False
+    N, H, W, C = x.shape
+    return H == W and _pow2(H) and C in (16, 32, 64) and tuple(w.shape) == (P, 9 * C, C) and \
+        N % P == 0 and _lib.get_lib().mopt_dconv_wgrad_splits(P, N // P, H, C, C, 1) > 0
+
+
+def bn_relu_conv3x3(x, gamma, beta, running, w, P, sums, arena, eps=1e-5, momentum=0.1):
+    """``(conv3x3(relu(BN(x)), w), batch sums of that output)`` with the BatchNorm applied inside
+    the convolution (``_BNReluConv3x3``); ``sums``: x's batch sums from its producing
+    convolution.  Check ``bn_into_conv_ok`` first."""
+    Co = w.shape[-1]
+    out_sums = arena.take(P * 2 * Co).view(P, 2, Co)
+    grad_w = w.grad if (w.requires_grad and w.is_leaf and w.grad is not None) else None
+    y = _BNReluConv3x3.apply(x.contiguous(), gamma.contiguous(), beta.contiguous(),
+                             w.contiguous(), running, P, eps, momentum, sums, out_sums, arena,
+                             grad_w)
+    return y, out_sums
+
+
+def conv_stats(x, w, P, stride, train, arena=None, mailbox=None):
+    """``(conv3x3(x, w), batch sums of the output or None)``: the first half of ``conv_bn_act``
+    (HIP path; the sums come from the direct kernel's epilogue when it ran)."""
+    Co = w.shape[-1]
+    stats = None
+    if train:
+        z = arena.take(P * 2 * Co).view(P, 2, Co) if arena is not None else \
+            torch.zeros(P, 2, Co, dtype=torch.float32, device=x.device)
+        stats = [z, False]
+    y = conv3x3(x, w, P, stride, stats, mailbox=mailbox)
+    return y, (stats[0] if stats is not None and stats[1] else None)
 
 
 def option_a_shortcut(h, cout):

@@ -64,10 +64,14 @@ constexpr int pstride() {
   return CI / 8 % 4 == 2 ? CI : CI + 16;
 }
 
-// halo band: input rows row0 .. row0 + TRI, columns -1 .. WI - 2 of images b0 .. b0 + IMGS
-template <int CI, int S>
+// halo band: input rows row0 .. row0 + TRI, columns -1 .. WI - 2 of images b0 .. b0 + IMGS.
+// BNIN: x is a BatchNorm's raw input and the convolution's operand is relu(x sc + sh) -- applied
+// here as the band is staged (bn_apply_kernel's arithmetic, rounded to bf16), so the BatchNorm
+// output is never written to HBM; tab = LDS [2][CI] f32 (scale, shift); the zero padding stays 0.
+template <int CI, int S, int BNIN = 0>
 __device__ __forceinline__ void load_halo(bf16_t* hs, const bf16_t* __restrict__ x,
-                                          const Geom& g, int b0, int row0) {
+                                          const Geom& g, int b0, int row0,
+                                          const float* tab = nullptr) {
   constexpr int CC = CI / 8;
   const int n = g.IMGS * g.TRI * g.WI * CC;
   for (int c = threadIdx.x; c < n; c += 256) {
@@ -79,9 +83,39 @@ __device__ __forceinline__ void load_halo(bf16_t* hs, const bf16_t* __restrict__
     const int hr = t2 - img * g.TRI;
     const int iy = row0 + hr, ix = hc - 1, b = b0 + img;
     uint4 v = make_uint4(0, 0, 0, 0);
-    if (b < g.Bn && iy >= 0 && iy < g.H && ix >= 0 && ix < g.H)
+    if (b < g.Bn && iy >= 0 && iy < g.H && ix >= 0 && ix < g.H) {
       v = *(const uint4*)(x + (((int64_t)b * g.H + iy) * g.H + ix) * CI + 8 * cc);
+      if constexpr (BNIN != 0) {
+        uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int ch = 8 * cc + 2 * e;
+          const float lo = fmaxf(bf2f(w[e] & 0xFFFF) * tab[ch] + tab[CI + ch] + 0.f, 0.f);
+          const float hi = fmaxf(bf2f(w[e] >> 16) * tab[ch + 1] + tab[CI + ch + 1] + 0.f, 0.f);
+          w[e] = pack2bf(lo, hi);
+        }
+        v = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+    }
     *(uint4*)(hs + t * pstride<CI, S>() + 8 * cc) = v;
+  }
+}
+
+// BNIN prologue: the workgroup's trial's (scale, shift) = (gamma rstd, beta - mean scale) into
+// the LDS table (published by the caller's next barrier)
+struct BnIn {
+  const float* stat;     // [P][2][C] mean, rstd
+  const bf16_t* gamma;   // [P][C]
+  const bf16_t* beta;    // [P][C]
+};
+
+template <int CI>
+__device__ __forceinline__ void bnin_table(float* tab, const BnIn& bn, int p) {
+  for (int i = threadIdx.x; i < CI; i += 256) {
+    const float mean = bn.stat[(2 * p) * CI + i], rstd = bn.stat[(2 * p + 1) * CI + i];
+    const float sc = bf2f(bn.gamma[(int64_t)p * CI + i]) * rstd;
+    tab[i] = sc;
+    tab[CI + i] = bf2f(bn.beta[(int64_t)p * CI + i]) - mean * sc;
   }
 }
 
@@ -104,13 +138,15 @@ __device__ __forceinline__ int tap_off(const Geom& g, int k) {
 // ADD: data-gradient epilogue addend -- 0 none, 1 same layout as the output (identity shortcut),
 // 2 half-resolution option-A shortcut gradient (compile-time: the epilogue code otherwise costs
 // the forward kernels registers and a wave per SIMD)
-template <int CI, int CO, int NPX, int MODE, int S, int ADD>
+template <int CI, int CO, int NPX, int MODE, int S, int ADD, int BNIN = 0>
 __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict__ x,
                                                         const bf16_t* __restrict__ w,
                                                         bf16_t* __restrict__ y,
                                                         float* __restrict__ sums,
                                                         const bf16_t* __restrict__ addend,
-                                                        const Geom g, int addend_c) {
+                                                        const Geom g, int addend_c,
+                                                        const BnIn bn) {
+  static_assert(BNIN == 0 || MODE == kFwd, "the BatchNorm input is applied by forwards only");
   constexpr int mode = MODE;
   constexpr int KS = (9 * CI + 31) / 32;  // 32-wide k steps (k = tap * CI + c)
   constexpr int WN = CO / 16, WM = 4 / WN;
@@ -188,9 +224,14 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
   }
 
   float s1 = 0.f, s2 = 0.f;
+  float* bntab = (float*)(smem + g.lds_elems);  // BNIN: [2][CI] past the halo / output tile
+  if constexpr (BNIN != 0) {
+    bnin_table<CI>(bntab, bn, p);
+    __syncthreads();
+  }
   for (int t = blk; t < g.tiles; t += g.nb) {
     const int b0 = (t / g.tpi) * g.IMGS, oy0 = (t % g.tpi) * g.TR;
-    load_halo<CI, S>(hs, xp, g, b0, mode == kDgrad2 ? oy0 / 2 - 1 : oy0 * S - 1);
+    load_halo<CI, S, BNIN>(hs, xp, g, b0, mode == kDgrad2 ? oy0 / 2 - 1 : oy0 * S - 1, bntab);
     __syncthreads();
 
     f32x4 acc[MFW];
@@ -284,11 +325,11 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
   }
 }
 
-template <int CI, int CO, int NPX, int S>
+template <int CI, int CO, int NPX, int S, int BNIN = 0>
 __global__ __launch_bounds__(256) void dconv_wgrad_kernel(const bf16_t* __restrict__ x,
                                                           const bf16_t* __restrict__ dy,
                                                           float* __restrict__ part,
-                                                          const Geom g, int P) {
+                                                          const Geom g, int P, const BnIn bn) {
   constexpr int M = 9 * CI;
   constexpr int MFT = (M + 15) / 16, NFT = CO / 16, MFW = (MFT + 3) / 4;
   constexpr int LSD = CO + 8;
@@ -297,11 +338,16 @@ __global__ __launch_bounds__(256) void dconv_wgrad_kernel(const bf16_t* __restri
   bf16_t* hs = smem;
   bf16_t* ds = smem + halo;
   bf16_t* zs = ds + NPX * LSD;  // 8 zero bytes: source of the padded rows m >= 9 CI
+  float* bntab = (float*)(zs + 8);  // BNIN: [2][CI] (scale, shift)
 
   const int p = blockIdx.x / g.nb, blk = blockIdx.x % g.nb;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int li = lane & 15, gq = lane >> 4, q = li >> 2, pp = li & 3;
   if (threadIdx.x == 0) *(uint2*)zs = make_uint2(0, 0);
+  if constexpr (BNIN != 0) {
+    bnin_table<CI>(bntab, bn, p);
+    __syncthreads();
+  }
 
   // this lane's A column chunk (m = 16 mi + 4 pp .. + 3) of each of the wave's M fragments
   int co_off[MFW];
@@ -324,7 +370,7 @@ __global__ __launch_bounds__(256) void dconv_wgrad_kernel(const bf16_t* __restri
   const bf16_t* dyp = dy + p * ((int64_t)g.Bn * g.OH * ow * CO);
   for (int t = blk; t < g.tiles; t += g.nb) {
     const int b0 = (t / g.tpi) * g.IMGS, oy0 = (t % g.tpi) * g.TR;
-    load_halo<CI, S>(hs, xp, g, b0, oy0 * S - 1);
+    load_halo<CI, S, BNIN>(hs, xp, g, b0, oy0 * S - 1, bntab);
     const int valid = min(NPX, (g.Bn - b0) * ppi);
     const bf16_t* dyt = dyp + ((int64_t)b0 * g.OH + oy0) * ow * CO;
     constexpr int CPR = CO / 8;
@@ -435,27 +481,29 @@ template <int CI, int S>
 size_t halo_bytes(const Geom& g) { return (size_t)g.IMGS * g.TRI * g.WI * pstride<CI, S>() * 2; }
 
 // S: the stride of the halo layout (kDgrad2 reads its half-resolution dy band at layout S = 1)
-template <int CI, int CO, int MODE, int S, int ADD = 0>
+template <int CI, int CO, int MODE, int S, int ADD = 0, int BNIN = 0>
 int launch_fwd(const void* x, const void* w, void* y, void* sums, int P, int Bn, int H,
-               hipStream_t st, const void* addend = nullptr, int addend_c = 0) {
+               hipStream_t st, const void* addend = nullptr, int addend_c = 0,
+               const BnIn& bn = BnIn{}) {
   constexpr int NPX = npx_for(CO);
   Geom g{};
   // (64-wide outputs: half the workgroups, twice the bands each -- their weight prologue is long)
   if (!make_geom(g, Bn, H, MODE == kDgrad2 ? 2 : S, NPX, CO >= 64 ? 512 : 1024, P, MODE))
     return (int)hipErrorInvalidValue;
   const size_t lds = std::max(halo_bytes<CI, S>(g), (size_t)NPX * (CO + 8) * 2);
-  if (lds > 64 * 1024) return (int)hipErrorNotSupported;
+  const size_t lds_all = lds + (BNIN ? (size_t)2 * CI * sizeof(float) : 0);
+  if (lds_all > 64 * 1024) return (int)hipErrorNotSupported;
   g.lds_elems = (int)(lds / 2);
-  hipLaunchKernelGGL((dconv_fwd_kernel<CI, CO, NPX, MODE, S, ADD>), dim3(P * g.nb), dim3(256), lds,
-                     st,
+  hipLaunchKernelGGL((dconv_fwd_kernel<CI, CO, NPX, MODE, S, ADD, BNIN>), dim3(P * g.nb),
+                     dim3(256), lds_all, st,
                      (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)sums,
-                     (const bf16_t*)addend, g, addend_c);
+                     (const bf16_t*)addend, g, addend_c, bn);
   return (int)hipGetLastError();
 }
 
-template <int CI, int CO, int S>
+template <int CI, int CO, int S, int BNIN = 0>
 int launch_wgrad(const void* x, const void* dy, void* dw, void* part, int P, int Bn, int H,
-                 hipStream_t st, int* nb_out) {
+                 hipStream_t st, int* nb_out, const BnIn& bn = BnIn{}) {
   constexpr int NPX = npx_wgrad(CO);
   // persistent workgroups per trial: ~2048 in all (latency hiding: a workgroup does not overlap
   // its band loads with its MFMAs), <= 64 MB of f32 partials, >= 4 bands each
@@ -469,10 +517,11 @@ int launch_wgrad(const void* x, const void* dy, void* dw, void* part, int P, int
     *nb_out = g.nb;
     return 0;
   }
-  const size_t lds = halo_bytes<CI, S>(g) + (size_t)NPX * (CO + 8) * 2 + 16;
+  const size_t lds = halo_bytes<CI, S>(g) + (size_t)NPX * (CO + 8) * 2 + 16 +
+                     (BNIN ? (size_t)2 * CI * sizeof(float) : 0);
   if (lds > 64 * 1024) return (int)hipErrorNotSupported;
-  hipLaunchKernelGGL((dconv_wgrad_kernel<CI, CO, NPX, S>), dim3(P * g.nb), dim3(256), lds, st,
-                     (const bf16_t*)x, (const bf16_t*)dy, (float*)part, g, P);
+  hipLaunchKernelGGL((dconv_wgrad_kernel<CI, CO, NPX, S, BNIN>), dim3(P * g.nb), dim3(256), lds,
+                     st, (const bf16_t*)x, (const bf16_t*)dy, (float*)part, g, P, bn);
   const int MN = 9 * CI * CO;
   const int64_t total = (int64_t)P * MN;
   hipLaunchKernelGGL(dconv_reduce_kernel, dim3((unsigned)((total / 4 + 255) / 256)), dim3(256), 0, st,
@@ -534,6 +583,26 @@ int mopt_dconv(int kind, const void* a, const void* b, void* out, void* aux, int
     return (int)hipErrorNotSupported;
   }
   return (int)hipErrorInvalidValue;
+}
+
+// mopt_dconv kinds 0 (forward) and 2 (weight gradient) of a stride-1 convolution whose operand
+// is relu(BatchNorm(x)) of the raw BatchNorm input x, applied while the halo bands are staged
+// (stat [P][2][Ci] mean / rstd, gamma / beta [P][Ci] bf16): the BatchNorm output is never
+// materialised.  Ci == Co in {16, 32, 64} (the second convolution of a ResNet basic block).
+int mopt_dconv_bnin(int kind, const void* a, const void* b, void* out, void* aux, int P, int Bn,
+                    int H, int Ci, int Co, const void* stat, const void* gamma, const void* beta,
+                    void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (stat == nullptr || gamma == nullptr || beta == nullptr) return (int)hipErrorInvalidValue;
+  const BnIn bn{(const float*)stat, (const bf16_t*)gamma, (const bf16_t*)beta};
+#define X(c) \
+  if (Ci == c && Co == c) \
+    return kind == 0 ? launch_fwd<c, c, kFwd, 1, 0, 1>(a, b, out, aux, P, Bn, H, st, nullptr, 0, bn) \
+         : kind == 2 ? launch_wgrad<c, c, 1, 1>(a, b, out, aux, P, Bn, H, st, nullptr, bn) \
+                     : (int)hipErrorInvalidValue;
+  X(16) X(32) X(64)
+#undef X
+  return (int)hipErrorNotSupported;
 }
 
 // number of partial slices the weight-gradient kernel writes (0 when unsupported)

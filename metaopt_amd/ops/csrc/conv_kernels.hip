@@ -343,6 +343,7 @@ int mopt_bn_fwd(const void* x, const void* gamma, const void* beta, const void* 
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((P * C + 255) / 256), dim3(256), 0, st,
                      (const float*)sums, (float*)stat, (float*)running, P, C, M, eps, momentum,
                      train);
+  if (y == nullptr) return (int)hipGetLastError();  // statistics only: the consumer applies
   const int rpa = reduce_rows(P, M, C);
   hipLaunchKernelGGL(bn_apply_kernel, dim3((unsigned)((M + rpa - 1) / rpa), P), dim3(256), 0, st,
                      (const bf16_t*)x, (const float*)stat, (const bf16_t*)gamma,

@@ -167,3 +167,35 @@ def test_population_resnet_step_matches_cpu():
             losses[i].append(pop.train_loss())
     a, b = np.array(losses[0]), np.array(losses[1])
     assert np.allclose(a, b, rtol=3e-2, atol=3e-2), (a, b)
+
+
+@pytest.mark.parametrize("C,H", [(16, 32), (32, 16), (64, 8)])
+def test_bn_relu_conv_fused_matches_materialised(C, H):
+    """bn_relu_conv3x3 (BatchNorm + ReLU applied while the convolution stages its input, in the
+    forward and in the weight gradient) equals bn_act followed by the convolution: output, the
+    output's batch sums, running statistics, and the gradients of x, gamma, beta and w."""
+    torch.manual_seed(6)
+    P, B = 2, 4
+    x0 = (0.5 + torch.randn(P * B, H, H, C, device=DEV)).to(torch.bfloat16)
+    g0 = (1 + 0.1 * torch.randn(P, C, device=DEV)).to(torch.bfloat16)
+    b0 = (0.1 * torch.randn(P, C, device=DEV)).to(torch.bfloat16)
+    w0 = (0.1 * torch.randn(P, 9 * C, C, device=DEV)).to(torch.bfloat16)
+    xf = x0.float().view(P, -1, C)
+    sums = torch.stack([xf.sum(1), (xf * xf).sum(1)], 1).contiguous()
+    res = {}
+    for fused in (True, False):
+        x, g, b, w = (t.clone().requires_grad_(True) for t in (x0, g0, b0, w0))
+        run = torch.stack([torch.zeros(P, C), torch.ones(P, C)], 1).to(DEV).contiguous()
+        arena = cops.ZeroArena(16 * P * C, DEV)
+        if fused:
+            assert cops.bn_into_conv_ok(x, w, P, 1, True, arena, True)
+            y, st = cops.bn_relu_conv3x3(x, g, b, run, w, P, sums.clone(), arena)
+        else:
+            t = cops.bn_act(x, g, b, run, P, True, sums=sums.clone(), arena=arena)
+            y, st = cops.conv_stats(t, w, P, 1, True, arena=arena)
+        wt = torch.linspace(-1, 1, y.numel(), device=DEV).view(y.shape)
+        (y.float() * wt).sum().backward()
+        res[fused] = (y.detach(), st.clone(), run, x.grad, g.grad, b.grad, w.grad)
+    for a, r in zip(res[True], res[False]):
+        _close(a, r, 2e-2)
+    assert torch.equal(res[True][0], res[False][0])      # same bf16 operand, same kernel math
