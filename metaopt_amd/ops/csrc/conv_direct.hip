@@ -85,13 +85,17 @@ __device__ __forceinline__ void load_halo(bf16_t* hs, const bf16_t* __restrict__
     uint4 v = make_uint4(0, 0, 0, 0);
     if (b < g.Bn && iy >= 0 && iy < g.H && ix >= 0 && ix < g.H) {
       v = *(const uint4*)(x + (((int64_t)b * g.H + iy) * g.H + ix) * CI + 8 * cc);
-      if constexpr (BNIN != 0) {
+      if constexpr (BNIN != 0) {  // the chunk's 8 (scale, shift) pairs: 4 ds_read_b128
+        const f32x4 sa = *(const f32x4*)(tab + 8 * cc), sb = *(const f32x4*)(tab + 8 * cc + 4);
+        const f32x4 ha = *(const f32x4*)(tab + CI + 8 * cc);
+        const f32x4 hb = *(const f32x4*)(tab + CI + 8 * cc + 4);
+        const float sc[8] = {sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3]};
+        const float sh[8] = {ha[0], ha[1], ha[2], ha[3], hb[0], hb[1], hb[2], hb[3]};
         uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int ch = 8 * cc + 2 * e;
-          const float lo = fmaxf(bf2f(w[e] & 0xFFFF) * tab[ch] + tab[CI + ch] + 0.f, 0.f);
-          const float hi = fmaxf(bf2f(w[e] >> 16) * tab[ch + 1] + tab[CI + ch + 1] + 0.f, 0.f);
+          const float lo = fmaxf(bf2f(w[e] & 0xFFFF) * sc[2 * e] + sh[2 * e] + 0.f, 0.f);
+          const float hi = fmaxf(bf2f(w[e] >> 16) * sc[2 * e + 1] + sh[2 * e + 1] + 0.f, 0.f);
           w[e] = pack2bf(lo, hi);
         }
         v = make_uint4(w[0], w[1], w[2], w[3]);
