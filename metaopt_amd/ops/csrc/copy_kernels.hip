@@ -37,26 +37,43 @@ namespace {
 
 constexpr int kChunk = 4096;
 
+__device__ __forceinline__ f32x4 copy_load(const CopyDesc& d, int64_t e) {
+  if (d.src_lo) return join4(*(const uint2*)(d.src16 + e), *(const uint2*)(d.src_lo + e));
+  if (d.src16) return bf4_to_f32(*(const uint2*)(d.src16 + e));
+  return *(const f32x4*)(d.src + e);
+}
+
+__device__ __forceinline__ void copy_store(const CopyDesc& d, int64_t e, const f32x4& v) {
+  if (d.dst) *(f32x4*)(d.dst + e) = v;
+  if (d.dst_lo) {
+    uint2 hi, lo;
+    split4(v, hi, lo);
+    *(uint2*)(d.dst16 + e) = hi;
+    *(uint2*)(d.dst_lo + e) = lo;
+  } else if (d.dst16) {
+    *(uint2*)(d.dst16 + e) = f32_to_bf4(v);
+  }
+}
+
+// A chunk is kChunk / 1024 = 4 vectors per thread: all four loads are issued before the first
+// store (the compiler cannot reorder them itself -- source and destination pointers may alias
+// as far as it knows), so every thread keeps 4 loads in flight instead of one.
 __global__ __launch_bounds__(256) void multi_copy_kernel(const CopyDesc* __restrict__ descs,
                                                          const CopyChunk* __restrict__ chunks) {
+  constexpr int kPer = kChunk / 1024;
   const CopyChunk c = chunks[blockIdx.x];
   const CopyDesc d = descs[c.desc];
   const int64_t end = min((int64_t)kChunk, d.n - c.start);
-  for (int64_t i = 4 * threadIdx.x; i < end; i += 4 * 256) {
-    const int64_t e = c.start + i;
-    f32x4 v;
-    if (d.src_lo) v = join4(*(const uint2*)(d.src16 + e), *(const uint2*)(d.src_lo + e));
-    else if (d.src16) v = bf4_to_f32(*(const uint2*)(d.src16 + e));
-    else v = *(const f32x4*)(d.src + e);
-    if (d.dst) *(f32x4*)(d.dst + e) = v;
-    if (d.dst_lo) {
-      uint2 hi, lo;
-      split4(v, hi, lo);
-      *(uint2*)(d.dst16 + e) = hi;
-      *(uint2*)(d.dst_lo + e) = lo;
-    } else if (d.dst16) {
-      *(uint2*)(d.dst16 + e) = f32_to_bf4(v);
-    }
+  f32x4 v[kPer];
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int64_t i = 4 * threadIdx.x + 1024 * u;
+    if (i < end) v[u] = copy_load(d, c.start + i);
+  }
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int64_t i = 4 * threadIdx.x + 1024 * u;
+    if (i < end) copy_store(d, c.start + i, v[u]);
   }
 }
 
