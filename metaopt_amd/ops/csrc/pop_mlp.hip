@@ -416,6 +416,11 @@ __global__ __launch_bounds__(256) void mlp_fwd_ce_kernel(const MlpTL* __restrict
 #ifndef MOPT_BWD_ALIAS
 #define MOPT_BWD_ALIAS 1
 #endif
+// 16-byte optimizer-state accesses (2 rows x 8 k per thread) instead of 8-byte ones (4 x 4):
+// A/B switch, -DMOPT_BWD_V16=0|1
+#ifndef MOPT_BWD_V16
+#define MOPT_BWD_V16 1
+#endif
 constexpr int bwd_waves(int opt, bool pf, int mode) {
   // AdamW and the multi-row-block pass spill at 168 VGPRs: they keep 2 waves per SIMD
   return (MOPT_BWD_ALIAS && !pf && opt != kAdamW && mode != 1) ? 3 : 2;
@@ -494,10 +499,59 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
   const int zo0 = (tid >> 3) * N + (tid & 7) * 8, zo1 = ((tid + 256) >> 3) * N + (tid & 7) * 8;
   const int zo2 = ((tid + 512) >> 3) * N + (tid & 7) * 8, zo3 = ((tid + 768) >> 3) * N + (tid & 7) * 8;
   bf16_t* zs0 = Zs + TOFF(tid >> 3, (tid & 7) * 8);     // rows +32 i keep the swizzle
+  const int WRS = w_row_stride(K);
+#if MOPT_BWD_V16
+  // Optimizer-state layout: thread -> rows 32 i + tid / 8 (i < 2), 8 consecutive k at 8 (tid % 8):
+  // every W / M (/ V) access is 16 bytes per lane and a wave-instruction moves 8 rows x 128 B
+  // (1 KB) -- half the memory instructions of the 8-byte layout below.
+  const size_t wo = (size_t)k0 * w_kstep(N) + (size_t)(tid >> 3) * WRS + 8 * (tid & 7);
+  uint4 cz0{}, cz1{}, cz2{}, cz3{}, nz0{}, nz1{}, nz2{}, nz3{};
+  f32x4 cm0{}, cm1{}, cm2{}, cm3{}, cv0{}, cv1{}, cv2{}, cv3{};   // rows i = 0,1: (lo4, hi4)
+  f32x4 nm0{}, nm1{}, nm2{}, nm3{}, nv0{}, nv1{}, nv2{}, nv3{};
+  uint4 cwh0{}, cwh1{}, cwl0{}, cwl1{}, nwh0{}, nwh1{}, nwl0{}, nwl1{};  // master hi, lo halves
+  uint4 ch0{}, ch1{}, nh0{}, nh1{};                                    // kSGD16 momentum
+#define MOPT_BWD_LOAD(NC, P)                                                                     \
+  {                                                                                              \
+    const bf16_t* zc_ = dZ + (NC);                                                               \
+    P##z0 = *(const uint4*)(zc_ + zo0);                                                          \
+    P##z1 = *(const uint4*)(zc_ + zo1);                                                          \
+    P##z2 = *(const uint4*)(zc_ + zo2);                                                          \
+    P##z3 = *(const uint4*)(zc_ + zo3);                                                          \
+    const size_t ob = (size_t)(NC) * WRS + wo;                                                   \
+    P##wh0 = *(const uint4*)(W16 + ob);                                                          \
+    P##wh1 = *(const uint4*)(W16 + ob + 32 * WRS);                                               \
+    if (MODE != 2) {                                                                             \
+    P##wl0 = *(const uint4*)(WLO + ob);                                                          \
+    P##wl1 = *(const uint4*)(WLO + ob + 32 * WRS);                                               \
+    if (OPT == kSGD16) {                                                                         \
+      P##h0 = *(const uint4*)(M16 + ob);                                                         \
+      P##h1 = *(const uint4*)(M16 + ob + 32 * WRS);                                              \
+    } else {                                                                                     \
+      P##m0 = *(const f32x4*)(M32 + ob);                                                         \
+      P##m1 = *(const f32x4*)(M32 + ob + 4);                                                     \
+      P##m2 = *(const f32x4*)(M32 + ob + 32 * WRS);                                              \
+      P##m3 = *(const f32x4*)(M32 + ob + 32 * WRS + 4);                                          \
+    }                                                                                            \
+    if (OPT == kAdamW) {                                                                         \
+      P##v0 = *(const f32x4*)(V32 + ob);                                                         \
+      P##v1 = *(const f32x4*)(V32 + ob + 4);                                                     \
+      P##v2 = *(const f32x4*)(V32 + ob + 32 * WRS);                                              \
+      P##v3 = *(const f32x4*)(V32 + ob + 32 * WRS + 4);                                          \
+    }                                                                                            \
+    }                                                                                            \
+  }
+#define MOPT_BWD_ADVANCE()                                                                       \
+  {                                                                                              \
+    cz0 = nz0; cz1 = nz1; cz2 = nz2; cz3 = nz3;                                                  \
+    cwh0 = nwh0; cwh1 = nwh1; cwl0 = nwl0; cwl1 = nwl1;                                          \
+    if (OPT == kSGD16) { ch0 = nh0; ch1 = nh1; }                                                 \
+    else { cm0 = nm0; cm1 = nm1; cm2 = nm2; cm3 = nm3; }                                         \
+    if (OPT == kAdamW) { cv0 = nv0; cv1 = nv1; cv2 = nv2; cv3 = nv3; }                           \
+  }
+#else
   // Optimizer-state layout: thread -> rows 16i + tid/16 (i < 4), 4 consecutive k at 4 * (tid % 16):
   // every wave-instruction moves 4 rows x 256 contiguous bytes of W/M (/V), full 128-B lines.
   // (strip layout: the k-strip is one contiguous [N][64] block, rows 64 apart)
-  const int WRS = w_row_stride(K);
   const size_t wo = (size_t)k0 * w_kstep(N) + (size_t)(tid >> 4) * WRS + 4 * (tid & 15);
   // (zero-initialised: MODE 2 loads only the hi halves and dZ; the rest stays unused)
   uint4 cz0{}, cz1{}, cz2{}, cz3{}, nz0{}, nz1{}, nz2{}, nz3{};
@@ -551,6 +605,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     else { cm0 = nm0; cm1 = nm1; cm2 = nm2; cm3 = nm3; }                                         \
     if (OPT == kAdamW) { cv0 = nv0; cv1 = nv1; cv2 = nv2; cv3 = nv3; }                           \
   }
+#endif  // MOPT_BWD_V16
   MOPT_BWD_LOAD(0, c)
   for (int nc = 0; nc < N; nc += BN) {
     // ---- this chunk's operands -> LDS (dZ row-major; W^T image as bf16 for the dX MFMAs) ----
@@ -558,6 +613,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     *(uint4*)(zs0 + 32 * TS) = cz1;
     *(uint4*)(zs0 + 64 * TS) = cz2;
     *(uint4*)(zs0 + 96 * TS) = cz3;
+#if MOPT_BWD_V16
+    // per thread: 2 rows x 8 k = 4 groups of 4 (row 0 k 0-3, row 0 k 4-7, row 1 k 0-3, 4-7)
+    if (OPT == kSGD16) {
+      cm0 = bf4_to_f32(make_uint2(ch0.x, ch0.y)); cm1 = bf4_to_f32(make_uint2(ch0.z, ch0.w));
+      cm2 = bf4_to_f32(make_uint2(ch1.x, ch1.y)); cm3 = bf4_to_f32(make_uint2(ch1.z, ch1.w));
+    }
+    const f32x4 w[4] = {join4(make_uint2(cwh0.x, cwh0.y), make_uint2(cwl0.x, cwl0.y)),
+                        join4(make_uint2(cwh0.z, cwh0.w), make_uint2(cwl0.z, cwl0.w)),
+                        join4(make_uint2(cwh1.x, cwh1.y), make_uint2(cwl1.x, cwl1.y)),
+                        join4(make_uint2(cwh1.z, cwh1.w), make_uint2(cwl1.z, cwl1.w))};
+    const f32x4 m[4] = {cm0, cm1, cm2, cm3};
+    f32x4 v[4];
+    if (OPT == kAdamW) {
+      v[0] = cv0; v[1] = cv1; v[2] = cv2; v[3] = cv3;
+    }
+    const uint4 wh[2] = {cwh0, cwh1};
+    const bool more = nc + BN < N;
+    if (PF && more) MOPT_BWD_LOAD(nc + BN, n)
+    if (has_dx) {   // the bf16 working copy (hi) is the dX operand, as in the forward
+#pragma unroll
+      for (int i = 0; i < 2; ++i) *(uint4*)(Ws + TOFF(32 * i + (tid >> 3), 8 * (tid & 7))) = wh[i];
+    }
+#else
     if (OPT == kSGD16) {
       cm0 = bf4_to_f32(ch0); cm1 = bf4_to_f32(ch1); cm2 = bf4_to_f32(ch2); cm3 = bf4_to_f32(ch3);
     }
@@ -575,6 +653,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
       for (int i = 0; i < 4; ++i) *(uint2*)(Ws + TOFF(16 * i + (tid >> 4), 4 * (tid & 15))) = wh[i];
     }
+#endif
     __syncthreads();
 
     // ---- dX[:, strip] += dZ[:, chunk] . W[chunk, strip] ----
@@ -666,10 +745,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
       for (int u = 0; u < 2; ++u)
         *(f32x4*)(Dw + FOFF(32 * wn + 16 * u + li, 32 * wk + 16 * t + 4 * g)) = dw[t][u];
     __syncthreads();
+#if MOPT_BWD_V16
+    uint2 ph{}, pl{}, pm{};   // the row's first group, stored with the second
+#endif
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
+#if MOPT_BWD_V16
+      // group i: row 32 (i / 2) + tid / 8, k 8 (tid % 8) + 4 (i % 2) .. + 3
+      const int gr = 32 * (i >> 1) + (tid >> 3), gk = 8 * (tid & 7) + 4 * (i & 1);
+      const f32x4 gv = *(const f32x4*)(Dw + FOFF(gr, gk));
+      const size_t o = (size_t)nc * WRS + wo + (size_t)(32 * (i >> 1)) * WRS + 4 * (i & 1);
+#else
       const f32x4 gv = *(const f32x4*)(Dw + FOFF(16 * i + (tid >> 4), 4 * (tid & 15)));
       const size_t o = (size_t)nc * WRS + wo + (size_t)(16 * i) * WRS;
+#endif
       f32x4 wv = w[i], mv = m[i], vv;
       if (OPT == kAdamW) vv = v[i];
 #pragma unroll
@@ -690,10 +779,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
       }
       uint2 nh, nl;
       split4(wv, nh, nl);
+#if MOPT_BWD_V16
+      // the two groups of a row (k 0-3, 4-7) leave as one 16-byte store per array
+      if ((i & 1) == 0) {
+        ph = nh;
+        pl = nl;
+        pm = f32_to_bf4(mv);
+      } else {
+        *(uint4*)(W16 + o - 4) = make_uint4(ph.x, ph.y, nh.x, nh.y);
+        *(uint4*)(WLO + o - 4) = make_uint4(pl.x, pl.y, nl.x, nl.y);
+        if (OPT == kSGD16) {
+          const uint2 mb = f32_to_bf4(mv);
+          *(uint4*)(M16 + o - 4) = make_uint4(pm.x, pm.y, mb.x, mb.y);
+        }
+      }
+      if (OPT != kSGD16) *(f32x4*)(M32 + o) = mv;
+#else
       *(uint2*)(W16 + o) = nh;
       *(uint2*)(WLO + o) = nl;
       if (OPT == kSGD16) *(uint2*)(M16 + o) = f32_to_bf4(mv);
       else *(f32x4*)(M32 + o) = mv;
+#endif
       if (OPT == kAdamW) *(f32x4*)(V32 + o) = vv;
     }
 
