@@ -108,6 +108,15 @@ class PopulationSweep:
         self._gc_t0 = 0.0
         self.max_write_backlog = 4 * pop.capacity * self.comm.world_size
         gc.callbacks.append(self._gc_callback)   # host GC pauses show up in the phase timers
+        # Every sync allocates thousands of long-lived objects (trial records, algorithm
+        # entries) and ends with gc.freeze(); with the default gen-0 threshold (700) the young
+        # generations were collected -- and, the frozen objects being out of the heuristics,
+        # fully collected -- several times per sync: 5-13 ms of rank 0's ~30 ms decide at 8
+        # simulated ranks vs 0.5 ms at 20000 (scripts/profile_decide.py, GC_T0).  Restored by
+        # close().
+        self._gc_threshold = gc.get_threshold()
+        if self._gc_threshold[0] < 20000:
+            gc.set_threshold(20000, *self._gc_threshold[1:])
         self.n_resumed = 0            # members resumed from a device checkpoint (this rank)
         self.n_resume_missing = 0
         self.n_syncs = 0
@@ -924,6 +933,9 @@ class PopulationSweep:
             log.warning("sweep_end event not written: %s", exc)
         if self._gc_callback in gc.callbacks:
             gc.callbacks.remove(self._gc_callback)
+        if getattr(self, "_gc_threshold", None) is not None:
+            gc.set_threshold(*self._gc_threshold)
+            self._gc_threshold = None
         if self._writer is not None:
             try:
                 self._writer.close()

@@ -101,7 +101,7 @@ def main(n_syncs=40, P=256, world=1, profile=False):
     print(f"writer {type(sw._writer).__name__ if sw._writer else ''}: final flush "
           f"{1e3 * t_flush:.1f} ms")
     print("phases ms/sync:", {k: round(1e3 * v / n_syncs, 2) for k, v in sw.timers.items()
-                              if k.startswith("decide")})
+                              if k.startswith("decide") or k.startswith("gc")})
     print(f"decide: {1e3 * t_total / n_syncs:.2f} ms/sync, writes {1e3 * t_rel / n_syncs:.2f} ms/sync, "
           f"{n_done / n_syncs:.1f} completions/sync")
     if prof:
@@ -112,5 +112,7 @@ if __name__ == "__main__":
     if "--nogc" in sys.argv:
         import gc
         gc.disable()
+    if os.environ.get("GC_T0"):
+        gc.set_threshold(int(os.environ["GC_T0"]), 10, 10)
     main(n_syncs=int(os.environ.get("N_SYNCS", 40)), world=int(os.environ.get("WORLD", 1)),
          profile="--profile" in sys.argv)
