@@ -19,14 +19,28 @@ sums, optionally per-trial #correct).  The member interface -- ``set_member``,
 """
 from __future__ import annotations
 
+import ctypes
 import dataclasses
 from typing import Dict, List, Optional
 
 import numpy as np
 import torch
 
+from ..ops import _lib
 from ..ops import lm as ops
 from ..ops.population import MemberConfig, device_busy
+
+
+INIT_SEG_DTYPE = np.dtype([("p32", "<u8"), ("p16", "<u8"), ("m", "<u8"), ("v", "<u8"),
+                           ("n", "<i8"), ("kind", "<i4"), ("val", "<f4"), ("seed", "<u4"),
+                           ("tag", "<u4"), ("m16", "<i4"), ("pad", "<i4")])
+assert INIT_SEG_DTYPE.itemsize == 64
+_CHUNK = 4096
+_CHUNK_DTYPE = np.dtype([("desc", "<i4"), ("pad", "<i4"), ("start", "<i8")])
+_lib.register_signatures({
+    "mopt_flat_init": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p],
+                       ctypes.c_int),
+})
 
 
 class FlatPopulation:
@@ -155,6 +169,9 @@ class FlatPopulation:
         self._write_hp(slot, cfg, 0)
         if not init:
             return
+        if self.device.type == "cuda" and _lib.available():
+            self._init_member_hip(slot, int(cfg.seed) & 0x7FFFFFFF)
+            return
         gen = torch.Generator(device=self.device)
         gen.manual_seed(int(cfg.seed) & 0x7FFFFFFF)
         for (name, shape, init_), sl in zip(self.specs, self._slices(slot)):
@@ -175,6 +192,57 @@ class FlatPopulation:
             if self.v.numel():
                 self.v[sl].zero_()
         self.init_aux(slot)
+
+    def aux_fill_specs(self):
+        """[(aux name, offset, length, value)] constant fills that initialise a member's
+        non-parameter state on the GPU path (one launch with the parameters); None: call
+        ``init_aux`` instead."""
+        return None
+
+    def _init_member_hip(self, slot: int, seed: int) -> None:
+        """Parameters (constant / N(0, std) from the counter-based RNG, tag = tensor index),
+        bf16 copies, zeroed moments and the constant fills of the non-parameter state in ONE
+        ``mopt_flat_init`` launch (csrc/copy_kernels.hip)."""
+        segs = []
+        m16 = self.m.dtype == torch.bfloat16
+        p32, p16, mm = self.p32.data_ptr(), self.p16.data_ptr(), self.m.data_ptr()
+        v = self.v.data_ptr() if self.v.numel() else 0
+        e32, e16, em = self.p32.element_size(), self.p16.element_size(), self.m.element_size()
+        for i, ((name, shape, init_), (o, n)) in enumerate(zip(self.specs, self.segments)):
+            start = o + slot * n
+            kind = init_[0]
+            if kind == "ones":
+                k, val = 0, 1.0
+            elif kind == "zeros":
+                k, val = 0, 0.0
+            elif kind == "normal":
+                k, val = 1, float(init_[1])
+            elif kind == "kaiming":
+                k, val = 1, float((2.0 / init_[1]) ** 0.5)
+            else:
+                raise ValueError(f"unknown init {init_}")
+            segs.append((p32 + start * e32, p16 + start * e16, mm + start * em,
+                         v + start * 4 if v else 0, n, k, val, seed, 0x3000 + i, int(m16), 0))
+        fills = self.aux_fill_specs()
+        if fills is not None:
+            a32 = self.aux.data_ptr()
+            offs = {name: (o, n) for name, o, n in self.aux_segments}
+            for name, off, length, val in fills:
+                o, n = offs[name]
+                segs.append((a32 + (o + slot * n + off) * 4, 0, 0, 0, length, 0, float(val), 0,
+                             0, 0, 0))
+        arr = np.array(segs, dtype=INIT_SEG_DTYPE)
+        counts = (arr["n"] + _CHUNK - 1) // _CHUNK
+        chunks = np.zeros(int(counts.sum()), dtype=_CHUNK_DTYPE)
+        chunks["desc"] = np.repeat(np.arange(len(arr), dtype=np.int32), counts)
+        first = np.concatenate([[0], np.cumsum(counts)[:-1]])
+        chunks["start"] = (np.arange(len(chunks)) - np.repeat(first, counts)) * _CHUNK
+        d = _lib.upload_bytes(arr, self.device)
+        c = _lib.upload_bytes(chunks, self.device)
+        _lib.check(_lib.get_lib().mopt_flat_init(d.data_ptr(), c.data_ptr(), len(chunks),
+                                                 _lib.stream_ptr(self.device)), "flat_init")
+        if fills is None:
+            self.init_aux(slot)
 
     def update_hparams(self, slot: int, **changes) -> None:
         cfg = dataclasses.replace(self.members[slot], **changes)

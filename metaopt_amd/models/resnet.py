@@ -74,6 +74,13 @@ class PopulationResNet(FlatPopulation):
     def aux_specs(self):
         return [(f"{name}.running", 2 * cout) for name, _, cout, _ in self.layout]
 
+    def aux_fill_specs(self):
+        # running mean 0, running var 1 of every BatchNorm (one launch with the parameters)
+        out = []
+        for name, _, cout, _ in self.layout:
+            out += [(f"{name}.running", 0, cout, 0.0), (f"{name}.running", cout, cout, 1.0)]
+        return out
+
     def init_aux(self, slot: int) -> None:
         for name, _, cout, _ in self.layout:
             r = self.A[f"{name}.running"][slot].view(2, cout)

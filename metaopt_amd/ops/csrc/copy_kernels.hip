@@ -89,3 +89,69 @@ int mopt_multi_copy(const void* descs, const void* chunks, int n_chunks, void* s
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------------------------------
+// Member initialisation of a flat population (models/flatpop.py) in ONE launch: every
+// parameter tensor of the member gets its f32 master (p32) and bf16 copy (p16) -- a constant or
+// N(0, std) drawn from the counter-based RNG of common.h (Box-Muller over two uniforms keyed by
+// (seed, tag, element)) -- and zeroed optimizer moments (m: f32 or bf16, v: f32 or absent);
+// non-parameter state (running statistics) is filled by constant segments with only p32 set.
+// Replaces 4 framework launches per tensor (~240 per ResNet-20 member).
+extern "C" {
+
+struct InitSeg {        // 64 bytes, mirrored by metaopt_amd/models/flatpop.py
+  float* p32;
+  bf16_t* p16;          // nullptr: no bf16 copy
+  void* m;              // nullptr: no first moment
+  float* v;             // nullptr: no second moment
+  int64_t n;            // multiple of 4
+  int32_t kind;         // 0: constant val, 1: N(0, val)
+  float val;
+  uint32_t seed, tag;
+  int32_t m16;          // m is bf16
+  int32_t pad;
+};
+
+}  // extern "C"
+
+namespace {
+
+__device__ __forceinline__ float normal_draw(uint32_t key, int64_t e) {
+  const float u1 = fmaxf(rng_uniform(key, (uint32_t)(2 * e)), 1.0f / 16777216.0f);
+  const float u2 = rng_uniform(key, (uint32_t)(2 * e + 1));
+  return sqrtf(-2.f * __logf(u1)) * __cosf(6.283185307179586f * u2);
+}
+
+__global__ __launch_bounds__(256) void flat_init_kernel(const InitSeg* __restrict__ segs,
+                                                        const CopyChunk* __restrict__ chunks) {
+  const CopyChunk c = chunks[blockIdx.x];
+  const InitSeg d = segs[c.desc];
+  const int64_t end = min((int64_t)kChunk, d.n - c.start);
+  const uint32_t key = rng_key(d.seed, d.tag, 0u);
+  for (int64_t i = 4 * threadIdx.x; i < end; i += 1024) {
+    const int64_t e = c.start + i;
+    f32x4 v;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = d.kind == 1 ? d.val * normal_draw(key, e + r) : d.val;
+    *(f32x4*)(d.p32 + e) = v;
+    if (d.p16) *(uint2*)(d.p16 + e) = f32_to_bf4(v);
+    if (d.m) {
+      if (d.m16) *(uint2*)((bf16_t*)d.m + e) = make_uint2(0u, 0u);
+      else *(f32x4*)((float*)d.m + e) = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    if (d.v) *(f32x4*)(d.v + e) = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int mopt_flat_init(const void* segs, const void* chunks, int n_chunks, void* stream) {
+  if (n_chunks <= 0) return 0;
+  hipLaunchKernelGGL(flat_init_kernel, dim3(n_chunks), dim3(256), 0, (hipStream_t)stream,
+                     (const InitSeg*)segs, (const CopyChunk*)chunks);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

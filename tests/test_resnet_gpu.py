@@ -199,3 +199,43 @@ def test_bn_relu_conv_fused_matches_materialised(C, H):
     for a, r in zip(res[True], res[False]):
         _close(a, r, 2e-2)
     assert torch.equal(res[True][0], res[False][0])      # same bf16 operand, same kernel math
+
+
+def test_one_launch_member_init():
+    """FlatPopulation.set_member on the GPU (one mopt_flat_init launch): constants exact, normal
+    tensors with the requested std, bf16 copy = rounded master, zeroed moments, BatchNorm running
+    statistics (0, 1), other slots untouched, same seed -> same weights."""
+    from metaopt_amd.models.resnet import PopulationResNet
+    from metaopt_amd.ops.population import MemberConfig
+    pop = PopulationResNet(3, batch_size=16, device=DEV, blocks_per_stage=1, image_size=16)
+    with torch.no_grad():
+        pop.p32.fill_(7.0)
+        pop.m.fill_(7.0)
+        pop.aux.fill_(7.0)
+    cfg = MemberConfig(width=0, lr=0.05, momentum=0.9, seed=11)
+    pop.set_member(1, cfg)
+    torch.cuda.synchronize()
+    for (name, shape, init), sl in zip(pop.specs, pop._slices(1)):
+        w = pop.p32[sl]
+        assert torch.equal(pop.p16[sl], w.to(torch.bfloat16)), name
+        assert torch.all(pop.m[sl] == 0), name
+        if init[0] == "ones":
+            assert torch.all(w == 1), name
+        elif init[0] == "zeros":
+            assert torch.all(w == 0), name
+        else:
+            std = init[1] if init[0] == "normal" else (2.0 / init[1]) ** 0.5
+            if w.numel() >= 2048:
+                assert abs(w.std().item() / std - 1) < 0.1, (name, w.std().item(), std)
+                assert abs(w.mean().item()) < 0.1 * std, name
+    for (name, _, cout, _) in pop.layout:
+        r = pop.A[f"{name}.running"][1].view(2, cout)
+        assert torch.all(r[0] == 0) and torch.all(r[1] == 1), name
+    for slot in (0, 2):                                   # untouched
+        for sl in pop._slices(slot):
+            assert torch.all(pop.p32[sl] == 7.0)
+    first = pop.p32[pop._slices(1)[0]].clone()
+    pop.set_member(1, cfg)
+    assert torch.equal(pop.p32[pop._slices(1)[0]], first)
+    pop.set_member(1, MemberConfig(width=0, lr=0.05, momentum=0.9, seed=12))
+    assert not torch.equal(pop.p32[pop._slices(1)[0]], first)
