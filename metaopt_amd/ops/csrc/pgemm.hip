@@ -307,7 +307,7 @@ __global__ __launch_bounds__(256) void pgemm_kernel(const GemmArgs g) {
 
 // ----------------------------------------------------------------------------------------------
 // Large-tile dense GEMM (the LM's projections, head and their gradients): 512 threads = 8 waves
-// arranged WM x (8/WM), each wave a 16*FM x 16*FN sub-tile; block tile 256 x 256 (or 256 x 128 /
+// arranged WM x (8/WM), each wave a 16*FM x 16*FN sub-tile; block tile 256 x 256 (or 256 x 192 / 256 x 128 /
 // 128 x 256), BK = 64, one workgroup per CU.  Operand tiles go HBM/L2 -> LDS directly with
 // global_load_lds_dwordx4 (no VGPR staging, no ds_write pass): every wave-instruction fills 1 KB
 // of the LDS image lane-linearly, so the images are unpadded and bank conflicts are removed by
@@ -346,14 +346,29 @@ __device__ __forceinline__ void glds16(const bf16_t* src, bf16_t* lds_dst) {
                : "memory", "m0");
 }
 
-template <int ROWS, bool KCONTIG>
+// k-contiguous image with 32-element (64-B) rows: 4 chunks per row; the swizzle keeps the 16
+// rows of a fragment read on 16 distinct 16-byte slots of the 256-B bank line (and each 8-row
+// half on 8 distinct slots of a 128-B line)
+__device__ __forceinline__ int kc_swz32(int row) { return ((row >> 1) ^ (row >> 3)) & 3; }
+
+template <int ROWS, bool KCONTIG, int KD = BK>
 struct GImg {
-  static constexpr int ELEMS = ROWS * BK;          // unpadded
+  static_assert(KD == 64 || KD == 32, "image depth");
+  static constexpr int ELEMS = ROWS * KD;          // unpadded
   static constexpr int BLOCKS = ELEMS * 2 / 1024;  // 1-KB wave-instruction fills
   static constexpr int NI = BLOCKS / 8;            // fills per wave (8 waves)
   static_assert(NI * 8 == BLOCKS, "tile must split into 8 waves of 1-KB fills");
   static constexpr int CPR = ROWS / 8;             // 16-B chunks per k-row (row-contiguous)
-  static_assert(KCONTIG || CPR >= 16, "row-contiguous swizzle needs >= 16 chunks per k-row");
+  static_assert(KCONTIG || (CPR >= 16 && CPR % 8 == 0),
+                "row-contiguous swizzle needs >= 16 chunks per k-row, whole 8-chunk groups");
+  static constexpr int KCH = KD / 8;               // 16-B chunks per row (k-contiguous)
+
+  __device__ __forceinline__ static int kswz(int r) { return KD == 64 ? kc_swz(r) : kc_swz32(r); }
+  // row-contiguous swizzle, kept inside the k-row: a 192-wide image (24 chunks, not a multiple
+  // of 16) drops the bit that pairs 8-chunk groups
+  __device__ __forceinline__ static int rswz(int kr) {
+    return CPR % 16 == 0 ? rc_swz(kr) : (rc_swz(kr) & 7);
+  }
 
   // fill this wave's share of the tile whose first row / k is (row0, k0)
   __device__ __forceinline__ static void fill(const bf16_t* __restrict__ base, int ld, int row0,
@@ -363,11 +378,11 @@ struct GImg {
       const int blk = wave * NI + j;
       const bf16_t* src;
       if (KCONTIG) {
-        const int r = blk * 8 + (lane >> 3), c = lane & 7;
-        src = base + (int64_t)(row0 + r) * ld + k0 + 8 * (c ^ kc_swz(r));
+        const int r = blk * (64 / KCH) + lane / KCH, c = lane % KCH;
+        src = base + (int64_t)(row0 + r) * ld + k0 + 8 * (c ^ kswz(r));
       } else {
-        const int kr = blk * (64 / CPR) + lane / CPR, c = lane % CPR;
-        src = base + (int64_t)(k0 + kr) * ld + row0 + 8 * (c ^ rc_swz(kr));
+        const int lin = blk * 64 + lane, kr = lin / CPR, c = lin % CPR;  // lane-linear image
+        src = base + (int64_t)(k0 + kr) * ld + row0 + 8 * (c ^ rswz(kr));
       }
       glds16(src, img + blk * 512);
     }
@@ -378,11 +393,11 @@ struct GImg {
                                                 int q, int pp) {
     if (KCONTIG) {
       const int r = row16 + li;
-      return lds_frag(img + r * BK + 8 * ((4 * s + g) ^ kc_swz(r)));
+      return lds_frag(img + r * KD + 8 * ((4 * s + g) ^ kswz(r)));
     }
     const int col = row16 + 4 * pp, k1 = 32 * s + 8 * g + q, k2 = k1 + 4;
-    const s16x4 lo = lds_tr4(img + k1 * ROWS + 8 * ((col >> 3) ^ rc_swz(k1)) + (col & 7));
-    const s16x4 hi = lds_tr4(img + k2 * ROWS + 8 * ((col >> 3) ^ rc_swz(k2)) + (col & 7));
+    const s16x4 lo = lds_tr4(img + k1 * ROWS + 8 * ((col >> 3) ^ rswz(k1)) + (col & 7));
+    const s16x4 hi = lds_tr4(img + k2 * ROWS + 8 * ((col >> 3) ^ rswz(k2)) + (col & 7));
     return cat_frag(lo, hi);
   }
 };
@@ -401,28 +416,30 @@ __global__ __launch_bounds__(512) void pgemm_big_kernel(const GemmArgs g) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int li = lane & 15, gq = lane >> 4, q = li >> 2, pp = li & 3;
   const int wm = wave / WN, wn = wave % WN;
-  const int nk = g.K / BK;
+  const int nk = g.k_per_split / BK;
 
   // Persistent: workgroup b computes the tiles of virtual ids b, b + G, ... (G = grid size, a
   // multiple of 8, so every virtual id of b maps to b's XCD under xcd_remap).
   int vb = blockIdx.x;
-  int p = 0, m0 = 0, n0 = 0;
+  int p = 0, m0 = 0, n0 = 0, k0 = 0;
   // Tile order within a trial: groups of kGroupM row panels, m fastest inside a group, so the
   // tiles an XCD runs together share both their B column panels and a few A row panels in L2
   // (n-fastest order re-streams every B panel from HBM once per row panel).
   auto decode = [&](int v) {
     const int t = xcd_remap(v, g.nwg);
     const int per = g.tiles_m * g.tiles_n;
-    p = t / per;
-    const int idx = t - p * per, span = kGroupM * g.tiles_n;
+    const int pq = t / per;           // p * splits + K-split
+    p = pq / g.splits;
+    k0 = (pq - p * g.splits) * g.k_per_split;
+    const int idx = t - pq * per, span = kGroupM * g.tiles_n;
     const int grp = idx / span, in = idx - grp * span;
     const int gm = min(kGroupM, g.tiles_m - grp * kGroupM);
     m0 = (grp * kGroupM + in % gm) * BM;
     n0 = (in / gm) * BN;
   };
   decode(vb);
-  IA::fill(g.a.ptr + p * g.a.batch, g.a.ld, m0, 0, smem, wave, lane);
-  IB::fill(g.b.ptr + p * g.b.batch, g.b.ld, n0, 0, smem + IA::ELEMS, wave, lane);
+  IA::fill(g.a.ptr + p * g.a.batch, g.a.ld, m0, k0, smem, wave, lane);
+  IB::fill(g.b.ptr + p * g.b.batch, g.b.ld, n0, k0, smem + IA::ELEMS, wave, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -430,12 +447,12 @@ __global__ __launch_bounds__(512) void pgemm_big_kernel(const GemmArgs g) {
   while (true) {
     const int nvb = vb + (int)gridDim.x;
     const bool has_next = nvb < g.nwg;
-    int np = p, nm0 = m0, nn0 = n0;
+    int np = p, nm0 = m0, nn0 = n0, nk0 = k0;
     if (has_next) {
-      const int cp = p, cm = m0, cn = n0;
+      const int cp = p, cm = m0, cn = n0, ck = k0;
       decode(nvb);
-      np = p; nm0 = m0; nn0 = n0;
-      p = cp; m0 = cm; n0 = cn;
+      np = p; nm0 = m0; nn0 = n0; nk0 = k0;
+      p = cp; m0 = cm; n0 = cn; k0 = ck;
     }
     const bf16_t* A = g.a.ptr + p * g.a.batch;
     const bf16_t* B = g.b.ptr + p * g.b.batch;
@@ -453,11 +470,11 @@ __global__ __launch_bounds__(512) void pgemm_big_kernel(const GemmArgs g) {
       bf16_t* nxt = smem + (stage ^ 1) * STAGE;
       // fill the other stage: this tile's next K-step, or the next tile's first one
       if (kt + 1 < nk) {
-        IA::fill(A, g.a.ld, m0, (kt + 1) * BK, nxt, wave, lane);
-        IB::fill(B, g.b.ld, n0, (kt + 1) * BK, nxt + IA::ELEMS, wave, lane);
+        IA::fill(A, g.a.ld, m0, k0 + (kt + 1) * BK, nxt, wave, lane);
+        IB::fill(B, g.b.ld, n0, k0 + (kt + 1) * BK, nxt + IA::ELEMS, wave, lane);
       } else if (has_next) {
-        IA::fill(g.a.ptr + np * g.a.batch, g.a.ld, nm0, 0, nxt, wave, lane);
-        IB::fill(g.b.ptr + np * g.b.batch, g.b.ld, nn0, 0, nxt + IA::ELEMS, wave, lane);
+        IA::fill(g.a.ptr + np * g.a.batch, g.a.ld, nm0, nk0, nxt, wave, lane);
+        IB::fill(g.b.ptr + np * g.b.batch, g.b.ld, nn0, nk0, nxt + IA::ELEMS, wave, lane);
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -479,6 +496,20 @@ __global__ __launch_bounds__(512) void pgemm_big_kernel(const GemmArgs g) {
       stage ^= 1;
     }
 
+    if (g.part != nullptr) {
+      // K-split partial: f32 [splits][P][M][N], lane (li, gq) holds 4 consecutive columns
+      const int64_t total = (int64_t)g.P * g.M * g.N;
+      float* part = g.part + (k0 / g.k_per_split) * total + (int64_t)p * g.M * g.N +
+                    (int64_t)(m0 + wm * 16 * FM + li) * g.N + n0 + wn * 16 * FN + 4 * gq;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) *(f32x4*)(part + (int64_t)(16 * i) * g.N + 16 * j) = acc[i][j];
+      if (!has_next) break;
+      vb = nvb;
+      p = np; m0 = nm0; n0 = nn0; k0 = nk0;
+      continue;
+    }
     // Epilogue without LDS: pack 4 columns per fragment to bf16, then exchange between the lane
     // rows gq = 0|1 (and 2|3) with v_permlane16_swap so every lane holds 8 consecutive columns of
     // one row; per fragment pair (j, j+1) each row gets 64 contiguous bytes in one dwordx4 store.
@@ -500,7 +531,122 @@ __global__ __launch_bounds__(512) void pgemm_big_kernel(const GemmArgs g) {
     }
     if (!has_next) break;
     vb = nvb;
-    p = np; m0 = nm0; n0 = nn0;
+    p = np; m0 = nm0; n0 = nn0; k0 = nk0;
+  }
+}
+
+// Multi-stage variant of pgemm_big_kernel: BK = 32 images in NS LDS stages (NS x 32 KB for
+// 256 x 256), the fills running NS - 1 K-steps ahead of the MFMAs instead of one -- 1.5x (NS = 4)
+// / 2x (NS = 5) the time to cover HBM latency at the same tile and LDS budget.  The fill stream
+// is its own cursor over this workgroup's (tile, K-step) sequence, so it runs ahead across tile
+// boundaries; each K-step waits only for the fill of the NEXT step (vmcnt counts the fill groups
+// issued after it; vector memory operations retire in order, so epilogue stores in between only
+// make that wait stricter).
+template <int NIF>
+__device__ __forceinline__ void wait_fills_newer(int newer) {
+  if (newer >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NIF) : "memory");
+  else if (newer == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NIF) : "memory");
+  else if (newer == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NIF) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <bool TA, bool TB, int WM, int FM, int FN, int NS>
+__global__ __launch_bounds__(512) void pgemm_pipe_kernel(const GemmArgs g) {
+  constexpr int KD = 32;
+  constexpr int WN = 8 / WM;
+  constexpr int BM = WM * 16 * FM, BN = WN * 16 * FN;
+  static_assert(FN % 2 == 0, "the epilogue pairs n-fragments");
+  static_assert(NS >= 3 && NS <= 5, "wait_fills_newer covers up to 3 newer fill groups");
+  using IA = GImg<BM, !TA, KD>;
+  using IB = GImg<BN, TB, KD>;
+  constexpr int STAGE = IA::ELEMS + IB::ELEMS;
+  constexpr int NIF = IA::NI + IB::NI;               // fill instructions per wave per K-step
+  __shared__ __attribute__((aligned(1024))) bf16_t smem[NS * STAGE];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int li = lane & 15, gq = lane >> 4, q = li >> 2, pp = li & 3;
+  const int wm = wave / WN, wn = wave % WN;
+  const int nk = g.K / KD;
+
+  auto decode = [&](int v, int& p, int& m0, int& n0) {
+    const int t = xcd_remap(v, g.nwg);
+    const int per = g.tiles_m * g.tiles_n;
+    p = t / per;
+    const int idx = t - p * per, span = kGroupM * g.tiles_n;
+    const int grp = idx / span, in = idx - grp * span;
+    const int gm = min(kGroupM, g.tiles_m - grp * kGroupM);
+    m0 = (grp * kGroupM + in % gm) * BM;
+    n0 = (in / gm) * BN;
+  };
+
+  // fill cursor
+  int fvb = blockIdx.x, fp, fm0, fn0, fkt = 0, nfill = 0;
+  bool fvalid = true;
+  decode(fvb, fp, fm0, fn0);
+  auto fill_next = [&]() {
+    if (!fvalid) return;
+    bf16_t* dst = smem + (nfill % NS) * STAGE;
+    IA::fill(g.a.ptr + fp * g.a.batch, g.a.ld, fm0, fkt * KD, dst, wave, lane);
+    IB::fill(g.b.ptr + fp * g.b.batch, g.b.ld, fn0, fkt * KD, dst + IA::ELEMS, wave, lane);
+    ++nfill;
+    if (++fkt == nk) {
+      fkt = 0;
+      fvb += (int)gridDim.x;
+      if (fvb < g.nwg) decode(fvb, fp, fm0, fn0);
+      else fvalid = false;
+    }
+  };
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s) fill_next();
+  wait_fills_newer<NIF>(nfill - 1);
+  __syncthreads();
+
+  int vb = blockIdx.x, p, m0, n0, f = 0;
+  decode(vb, p, m0, n0);
+  while (true) {
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int kt = 0; kt < nk; ++kt, ++f) {
+      fill_next();                                   // into the stage step f - 1 read
+      const bf16_t* cur = smem + (f % NS) * STAGE;
+      bf16x8 a[FM], b[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) a[i] = IA::frag(cur, wm * 16 * FM + 16 * i, 0, li, gq, q, pp);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        b[j] = IB::frag(cur + IA::ELEMS, wn * 16 * FN + 16 * j, 0, li, gq, q, pp);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(b[j], a[i], acc[i][j]);
+      wait_fills_newer<NIF>(nfill - 2 - f);          // fill f + 1 has landed
+      __syncthreads();
+    }
+
+    // epilogue: as pgemm_big_kernel (transposed accumulators, permlane16 pairing, 64-B rows)
+    bf16_t* C = g.C + p * g.sC + (int64_t)(m0 + wm * 16 * FM + li) * g.ldc + n0 + wn * 16 * FN +
+                16 * (gq & 1) + 8 * (gq >> 1);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+      for (int j = 0; j < FN; j += 2) {
+        uint32_t x0 = pack2bf(acc[i][j][0], acc[i][j][1]);
+        uint32_t x1 = pack2bf(acc[i][j][2], acc[i][j][3]);
+        uint32_t y0 = pack2bf(acc[i][j + 1][0], acc[i][j + 1][1]);
+        uint32_t y1 = pack2bf(acc[i][j + 1][2], acc[i][j + 1][3]);
+        const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+        *(uint4*)(C + (int64_t)(16 * i) * g.ldc + 16 * j) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+      }
+    }
+    vb += (int)gridDim.x;
+    if (vb >= g.nwg) break;
+    decode(vb, p, m0, n0);
   }
 }
 
@@ -538,16 +684,35 @@ int launch(GemmArgs g, hipStream_t st) {
 template <bool TA, bool TB, int WM, int FM, int FN>
 int launch_big(GemmArgs g, hipStream_t st) {
   constexpr int BM = WM * 16 * FM, BN = (8 / WM) * 16 * FN;
-  if (g.M % BM || g.N % BN || g.K % BK || g.splits != 1) return (int)hipErrorInvalidValue;
+  if (g.M % BM || g.N % BN || g.k_per_split % BK || g.k_per_split < BK ||
+      (int64_t)g.k_per_split * g.splits != g.K || (g.splits > 1 && g.part == nullptr) ||
+      g.nin > 1)
+    return (int)hipErrorInvalidValue;
   g.tiles_m = g.M / BM;
   g.tiles_n = g.N / BN;
-  const int64_t nwg = (int64_t)g.P * g.tiles_m * g.tiles_n;
+  const int64_t nwg = (int64_t)g.P * g.splits * g.tiles_m * g.tiles_n;
   if (nwg <= 0 || nwg > 0x7FFFFFFF) return (int)hipErrorInvalidValue;
   g.nwg = (int)nwg;
   // persistent: one workgroup per CU (the LDS stages allow no second one), a multiple of 8
   constexpr int kGrid = 256;
   const int grid = nwg < kGrid ? (int)nwg : kGrid;
   hipLaunchKernelGGL((pgemm_big_kernel<TA, TB, WM, FM, FN>), dim3(grid), dim3(512), 0, st, g);
+  return (int)hipGetLastError();
+}
+
+template <bool TA, bool TB, int WM, int FM, int FN, int NS>
+int launch_pipe(GemmArgs g, hipStream_t st) {
+  constexpr int BM = WM * 16 * FM, BN = (8 / WM) * 16 * FN;
+  if (g.M % BM || g.N % BN || g.K % 32 || g.K < 32 || g.splits != 1 || g.nin > 1)
+    return (int)hipErrorInvalidValue;
+  g.tiles_m = g.M / BM;
+  g.tiles_n = g.N / BN;
+  const int64_t nwg = (int64_t)g.P * g.tiles_m * g.tiles_n;
+  if (nwg <= 0 || nwg > 0x7FFFFFFF) return (int)hipErrorInvalidValue;
+  g.nwg = (int)nwg;
+  constexpr int kGrid = 256;                 // persistent, one workgroup per CU
+  const int grid = nwg < kGrid ? (int)nwg : kGrid;
+  hipLaunchKernelGGL((pgemm_pipe_kernel<TA, TB, WM, FM, FN, NS>), dim3(grid), dim3(512), 0, st, g);
   return (int)hipGetLastError();
 }
 
@@ -558,6 +723,10 @@ int dispatch_tile(const GemmArgs& g, int cfg, hipStream_t st) {
       case 5: return launch_big<TA, TB, 2, 8, 4>(g, st);  // 256 x 256
       case 6: return launch_big<TA, TB, 4, 4, 4>(g, st);  // 256 x 128
       case 7: return launch_big<TA, TB, 2, 4, 4>(g, st);  // 128 x 256
+      case 8: return launch_pipe<TA, TB, 2, 8, 4, 4>(g, st);  // 256 x 256, BK 32, 4 stages
+      case 9: return launch_pipe<TA, TB, 2, 8, 4, 5>(g, st);  // 256 x 256, BK 32, 5 stages
+      case 10: return launch_pipe<TA, TB, 4, 4, 4, 5>(g, st); // 256 x 128, BK 32, 5 stages
+      case 11: return launch_big<TA, TB, 4, 4, 6>(g, st);     // 256 x 192
       default: break;
     }
   }
@@ -613,9 +782,10 @@ extern "C" {
 
 // Tile of configuration ``cfg`` (rows, cols): lets the host size grids and split-K.
 int mopt_pgemm_tile(int cfg, int* bm, int* bn) {
-  static const int t[8][2] = {{128, 128}, {128, 16}, {128, 32}, {64, 64},
-                              {64, 128},  {256, 256}, {256, 128}, {128, 256}};
-  if (cfg < 0 || cfg > 7) return (int)hipErrorInvalidValue;
+  static const int t[12][2] = {{128, 128}, {128, 16},  {128, 32},  {64, 64},
+                               {64, 128},  {256, 256}, {256, 128}, {128, 256},
+                               {256, 256}, {256, 256}, {256, 128}, {256, 192}};
+  if (cfg < 0 || cfg > 11) return (int)hipErrorInvalidValue;
   *bm = t[cfg][0];
   *bn = t[cfg][1];
   return 0;

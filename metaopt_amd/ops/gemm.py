@@ -44,12 +44,21 @@ _lib.register_signatures({
 # (any shape, ragged edges); 5-7: 8-wave direct-to-LDS kernel, one workgroup per CU, for shapes
 # the tile divides (M % BM == N % BN == K % 64 == 0)
 TILES = {0: (128, 128), 1: (128, 16), 2: (128, 32), 3: (64, 64), 4: (64, 128),
-         5: (256, 256), 6: (256, 128), 7: (128, 256)}
-BIG_TILES = (5, 6, 7)
+         5: (256, 256), 6: (256, 128), 7: (128, 256),
+         8: (256, 256), 9: (256, 256), 10: (256, 128), 11: (256, 192)}
+#: 256 x 192 (cfg 11): N = 768 outputs in 4 column panels, so the LM's N = 768 products fill
+#: whole waves of 256 CUs (512 tiles for M = 4096, 256 for M = 2048) where 256 x 256 leaves a
+#: 75 %-full last wave
+BIG_TILES = (5, 6, 7, 11)
+#: the multi-stage big-tile kernel (BK 32, 4 / 5 / 5 LDS stages, fills 3-4 K-steps ahead):
+#: cfg 8 / 9 = 256 x 256, 10 = 256 x 128.  ``MOPT_GEMM_PIPE=<8|9>`` makes the planner use it in
+#: place of cfg 5 (and 10 in place of 6) for A/B
+PIPE_TILES = (8, 9, 10)
+LARGE_TILES = BIG_TILES + PIPE_TILES
 NUM_CU = 256
 #: relative speed of the big tiles at equal occupancy of the chip; the 256 x 128 / 128 x 256 tiles
 #: lose more on long reductions (less reuse per loaded byte): profiles/gemm_r2.md
-BIG_SPEED = {5: 1.0, 6: 0.85, 7: 0.85}
+BIG_SPEED = {5: 1.0, 6: 0.85, 7: 0.85, 11: 0.95}
 LONG_K = 8192
 
 
@@ -83,23 +92,51 @@ def big_fits(M: int, N: int, K: int, cfg: int) -> bool:
     return M % bm == 0 and N % bn == 0 and K % 64 == 0
 
 
+#: model of the big kernel for the planner: sustained MFMA rate (FLOP/s at a full last wave) and
+#: the HBM rate of the K-split partials (f32 written + read by the reduce pass, bf16 out)
+BIG_RATE = 1.0e15
+PART_BW = 4.0e12
+MAX_BIG_SPLITS = 4
+MIN_SPLIT_K = 1024
+
+
 def _plan_big(P: int, M: int, N: int, K: int):
-    """Best big tile by the fraction of its last wave of 256 workgroups it fills, weighted by
-    the tile's speed; None when no big tile divides the shape or fills the chip well (the big
-    kernel is persistent and never splits K: split-K partials measured 2-3x slower)."""
+    """Best big tile and K-split by a time model: MFMA time at the tile's speed, scaled by the
+    fraction of its last wave of 256 workgroups that is filled, plus the traffic of the f32
+    partials when K is split (a split pays where few, long tiles leave CUs idle in the last
+    wave, e.g. the LM head's dX: 384 tiles of K = 32000 on 256 CUs); None when no big tile
+    divides the shape or fills the chip well."""
     best = None
     for cfg in BIG_TILES:
         if not big_fits(M, N, K, cfg):
             continue
         bm, bn = TILES[cfg]
-        n = P * (M // bm) * (N // bn)
-        fill = n / (math.ceil(n / NUM_CU) * NUM_CU)
-        score = fill * BIG_SPEED[cfg] * (0.8 if cfg != 5 and K > LONG_K else 1.0)
-        if best is None or score > best[0]:
-            best = (score, cfg)
-    if best is None or best[0] < 0.6:
+        tiles = P * (M // bm) * (N // bn)
+        speed = BIG_SPEED[cfg] * (0.8 if cfg in (6, 7) and K > LONG_K else 1.0)
+        s = 1
+        while s <= MAX_BIG_SPLITS:
+            if K % (64 * s) or (s > 1 and K // s < MIN_SPLIT_K):
+                break
+            n = tiles * s
+            fill = n / (math.ceil(n / NUM_CU) * NUM_CU)
+            t = 2.0 * P * M * N * K / (BIG_RATE * speed * fill)
+            if s > 1:
+                t += P * M * N * (8.0 * s + 2.0) / PART_BW
+            if best is None or t < best[0]:
+                best = (t, cfg, s, fill)
+            s *= 2
+    if best is None or best[3] < 0.6:
         return None
-    return best[1], 1, K
+    _, cfg, s, _ = best
+    return _PIPE_MAP.get(cfg, cfg) if s == 1 else cfg, s, K // s
+
+
+def _pipe_map():
+    v = os.environ.get("MOPT_GEMM_PIPE", "")
+    return {5: int(v), 6: 10} if v in ("8", "9") else {}
+
+
+_PIPE_MAP = _pipe_map()
 
 
 def plan(P: int, M: int, N: int, K: int, cfg: Optional[int] = None,
@@ -111,10 +148,11 @@ def plan(P: int, M: int, N: int, K: int, cfg: Optional[int] = None,
         big = _plan_big(P, M, N, K)
         if big is not None:
             return big
-    if cfg in BIG_TILES:
-        if big_fits(M, N, K, cfg) and (splits or 1) == 1:
-            return cfg, 1, K
-        cfg = None                    # the tile does not divide this shape, or split-K asked
+    if cfg in LARGE_TILES:
+        sp = splits or 1
+        if big_fits(M, N, K, cfg) and K % (64 * sp) == 0 and (sp == 1 or cfg in BIG_TILES):
+            return cfg, sp, K // sp
+        cfg = None                    # the tile does not divide this shape / this K-split
     cfg = pick_tile(M, N) if cfg is None else cfg
     bm, bn = TILES[cfg]
     blocks = P * math.ceil(M / bm) * math.ceil(N / bn)
@@ -190,7 +228,7 @@ def pgemm(a: torch.Tensor, b: torch.Tensor, ta: bool = False, tb: bool = False,
                              "(f32 operands only)")
     if f32 and cfg is None and splits is None:
         cfg, splits = f32_plan(M, N, ta)
-    elif f32 and (cfg is None or cfg in BIG_TILES):
+    elif f32 and (cfg is None or cfg in LARGE_TILES):
         cfg = pick_tile(M, N)          # f32 operands: the register-staged tiles only
     cfg, splits, kps = plan(P, M, N, K, cfg, splits)
     part = (torch.empty(splits, P, M, N, dtype=torch.float32, device=a.device)

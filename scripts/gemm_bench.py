@@ -52,6 +52,7 @@ def main():
     ap.add_argument("--no-torch", action="store_true")
     ap.add_argument("--cfgs", default="", help="comma-separated tile configs to time as well")
     ap.add_argument("--shapes", default="", help="only shapes whose name starts with this")
+    ap.add_argument("--splits", default="", help="cfg:splits pairs to time, e.g. 5:2,5:4,6:2")
     args = ap.parse_args()
     rows = []
     for name, P, M, N, K, ta, tb in SHAPES:
@@ -69,6 +70,12 @@ def main():
         for c in [int(v) for v in args.cfgs.split(",") if v]:
             t = timeit(lambda: pgemm(a, b, ta=ta, tb=tb, out=out, cfg=c), args.iters)
             row[f"cfg{c}_tflops"] = round(flops / t / 1e6, 1)
+        for pair in [v for v in args.splits.split(",") if v]:
+            c, sp = (int(x) for x in pair.split(":"))
+            if K % (64 * sp) == 0 and plan(P, M, N, K, c, sp)[:2] == (c, sp):
+                t = timeit(lambda: pgemm(a, b, ta=ta, tb=tb, out=out, cfg=c, splits=sp),
+                           args.iters)
+                row[f"cfg{c}s{sp}_tflops"] = round(flops / t / 1e6, 1)
         if not args.no_torch and not (ta and tb):
             aa = a.transpose(1, 2) if ta else a
             bb = b.transpose(1, 2) if tb else b

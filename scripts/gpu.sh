@@ -61,7 +61,7 @@ for step in "$@"; do
     trace_lm)   prof trace_lm 300 -- python3 "$ROOT/scripts/bench_configs.py" --config lm-125m --steps 6 --warmup 4 ;;
     trace_resnet) prof trace_resnet 300 -- python3 "$ROOT/scripts/bench_configs.py" --config resnet20 --steps 20 --warmup 10 ;;
     trace_hyper) prof trace_hyper 300 -- python3 "$ROOT/scripts/bench_configs.py" --config hyper --steps 1 --warmup 1 ;;
-    gemm)       $T 300 python scripts/gemm_bench.py --cfgs "${CFGS:-0,5,6,7}" --out "$OUT/gemm.json" > "$OUT/gemm.log" 2>&1 ;;
+    gemm)       $T 300 python scripts/gemm_bench.py --cfgs "${CFGS:-0,5,6,7}" --splits "${SPLITS:-}" --out "$OUT/gemm.json" > "$OUT/gemm.log" 2>&1 ;;
     gemm32)     $T 300 python scripts/gemm_f32_bench.py --out "$OUT/gemm32.json" > "$OUT/gemm32.log" 2>&1 ;;
     conv)       $T 200 python scripts/conv_bench.py --implicit --out "$OUT/conv_bench.json" > "$OUT/conv_bench.log" 2>&1 ;;
     decide)     for w in 1 8; do WORLD=$w $T 300 python scripts/profile_decide.py > "$OUT/decide_world$w.log" 2>&1; done ;;

@@ -17,11 +17,28 @@ def test_f32_plan_uses_64_row_tiles_without_split(M, N, ta, want):
     assert cfg not in BIG_TILES
 
 
-def test_plan_splits_short_grids_and_never_splits_big_tiles():
+def test_plan_splits_short_grids_and_big_tiles_only_for_a_ragged_last_wave():
     cfg, splits, kps = plan(2, 64, 64, 8192)        # 2 output tiles: split the reduction
     assert splits > 1 and kps % 64 == 0 and splits * kps >= 8192
     cfg, splits, kps = plan(8, 4096, 4096, 1024)    # a big tile fills the chip: one K pass
     assert cfg in BIG_TILES and splits == 1 and kps == 1024
+    # LM head dX: 384 long 256 x 256 tiles leave half the CUs idle in the second wave ->
+    # 256 x 192 tiles (512 = 2 whole waves), or 2 K-splits when that tile is not available
+    cfg, splits, kps = plan(8, 4096, 768, 32000)
+    assert cfg == 11 and splits == 1
+    from metaopt_amd.ops import gemm
+    saved = gemm.BIG_TILES
+    try:
+        gemm.BIG_TILES = (5, 6, 7)
+        assert plan(8, 4096, 768, 32000) == (5, 2, 16000)
+    finally:
+        gemm.BIG_TILES = saved
+    # the other LM projections keep one K pass (the partials would cost more than the fill)
+    for M, N, K in [(4096, 2304, 768), (768, 2304, 4096), (2048, 768, 4096), (768, 32000, 4096)]:
+        assert plan(8, M, N, K)[1] == 1
+    # an explicit K-split is honoured on the big tiles, not on the pipelined ones
+    assert plan(8, 512, 512, 1024, 5, 4) == (5, 4, 256)
+    assert plan(8, 512, 512, 1024, 8, 2)[0] not in (5, 6, 7, 8, 9, 10)
     for c in TILES:
         bm, bn = TILES[c]
         assert bm % 16 == 0 and bn % 16 == 0

@@ -3,7 +3,7 @@ every tile configuration, ragged edges, split-K, and the autograd wrapper used b
 import pytest
 import torch
 
-from metaopt_amd.ops.gemm import BIG_TILES, TILES, pbmm, pgemm, plan
+from metaopt_amd.ops.gemm import LARGE_TILES, TILES, pbmm, pgemm, plan
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -33,14 +33,14 @@ def test_layouts_and_edges(ta, tb, P, M, N, K):
     _check(pgemm(a, b, ta=ta, tb=tb), A, B)
 
 
-@pytest.mark.parametrize("cfg", sorted(c for c in TILES if c not in BIG_TILES))
+@pytest.mark.parametrize("cfg", sorted(c for c in TILES if c not in LARGE_TILES))
 def test_every_tile_config(cfg):
     A, B, a, b = _operands(2, 264, 200, 136, False, True, seed=cfg)
     _check(pgemm(a, b, tb=True, cfg=cfg), A, B)
 
 
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
-@pytest.mark.parametrize("cfg", BIG_TILES)
+@pytest.mark.parametrize("cfg", LARGE_TILES)
 def test_big_tiles_every_layout(cfg, ta, tb):
     """The 8-wave direct-to-LDS kernel (swizzled k-contiguous and row-contiguous images) in
     every operand layout; several K tiles so both LDS stages are used, distinct trials."""
@@ -48,10 +48,11 @@ def test_big_tiles_every_layout(cfg, ta, tb):
     _check(pgemm(a, b, ta=ta, tb=tb, cfg=cfg), A, B)
 
 
-@pytest.mark.parametrize("cfg", BIG_TILES)
+@pytest.mark.parametrize("cfg", LARGE_TILES)
 def test_big_tiles_persistent_and_strided_output(cfg):
     """More tiles than workgroups (the persistent loop carries the next tile's first K-step
-    across the epilogue), a C written into a wider row stride, split-K falling back."""
+    across the epilogue), a C written into a wider row stride, split-K (f32 partials of the big
+    tiles; the pipelined tiles fall back to a small tile)."""
     A, B, a, b = _operands(2, 256, 256, 2048, True, False, seed=20 + cfg)
     _check(pgemm(a, b, ta=True, cfg=cfg, splits=4), A, B)
     wide = torch.zeros(2, 256, 384, dtype=torch.bfloat16, device=DEV)
@@ -59,6 +60,39 @@ def test_big_tiles_persistent_and_strided_output(cfg):
     assert wide[:, :, 256:].abs().max().item() == 0     # nothing written past the view
     A, B, a, b = _operands(40, 512, 256, 128, False, True, seed=40 + cfg)   # 160-640 tiles
     _check(pgemm(a, b, tb=True, cfg=cfg), A, B)
+
+
+@pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("cfg,splits", [(5, 2), (5, 4), (6, 2), (7, 4)])
+def test_big_tiles_split_k(cfg, splits, ta, tb):
+    """K-split big tiles: every split starts its fills at its own K offset, writes f32 partials,
+    the reduce pass sums them -- with more (tile, split) pairs than workgroups (persistent
+    loop crossing split boundaries), into a wider output row stride."""
+    A, B, a, b = _operands(24, 512, 512, 1024, ta, tb, seed=50 + cfg + splits)
+    assert plan(24, 512, 512, 1024, cfg, splits)[:2] == (cfg, splits)
+    wide = torch.zeros(24, 512, 640, dtype=torch.bfloat16, device=DEV)
+    _check(pgemm(a, b, ta=ta, tb=tb, cfg=cfg, splits=splits, out=wide[:, :, :512]), A, B)
+    assert wide[:, :, 512:].abs().max().item() == 0
+
+
+@pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("splits", [1, 2])
+def test_256x192_tile(ta, tb, splits):
+    """The 256 x 192 big tile: 24-chunk row-contiguous images (lane-linear fills across k-rows,
+    the 3-bit swizzle), 6 n-fragments per wave, persistent over 300 tiles, with and without a
+    K-split."""
+    A, B, a, b = _operands(25, 512, 1152, 256, ta, tb, seed=60 + splits)
+    assert plan(25, 512, 1152, 256, 11, splits)[:2] == (11, splits)
+    _check(pgemm(a, b, ta=ta, tb=tb, cfg=11, splits=splits), A, B)
+
+
+def test_lm_head_dx_plan_splits_k():
+    """The LM head's dX (K = 32000, 384 256 x 256 tiles on 256 CUs): the planner fills whole
+    waves (256 x 192 tiles, or a K-split) and the split product matches."""
+    cfg, splits, kps = plan(8, 4096, 768, 32000)
+    assert cfg == 11 or splits == 2
+    A, B, a, b = _operands(2, 512, 256, 32000, False, True, seed=77)
+    _check(pgemm(a, b, tb=True, cfg=5, splits=2), A, B)
 
 
 def test_big_tile_shape_guard():
