@@ -364,10 +364,12 @@ struct GImg {
   static constexpr int KCH = KD / 8;               // 16-B chunks per row (k-contiguous)
 
   __device__ __forceinline__ static int kswz(int r) { return KD == 64 ? kc_swz(r) : kc_swz32(r); }
-  // row-contiguous swizzle, kept inside the k-row: a 192-wide image (24 chunks, not a multiple
-  // of 16) drops the bit that pairs 8-chunk groups
+  // row-contiguous swizzle for a 192-wide image (24 chunks: the XOR must stay inside an 8-chunk
+  // group).  Its 384-B k-rows shift odd rows by half a 256-B bank line, which already separates
+  // k1 & 1; bits 1-2 of the slot then take k1 bit 1 and k1 bit 3, so the 32 lanes of each half
+  // of a ds_read_b64_tr_b16 (4 k-rows x 2 lane groups x 2 chunks) hit 16 distinct 16-B slots
   __device__ __forceinline__ static int rswz(int kr) {
-    return CPR % 16 == 0 ? rc_swz(kr) : (rc_swz(kr) & 7);
+    return CPR % 16 == 0 ? rc_swz(kr) : ((((kr >> 1) & 1) << 1) | (((kr >> 3) & 1) << 2));
   }
 
   // fill this wave's share of the tile whose first row / k is (row0, k0)
