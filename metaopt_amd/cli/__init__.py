@@ -37,12 +37,24 @@ def current_argv() -> list:
     return [*_ARGV]     # (``list`` here is the cli.list sub-module once it is imported)
 
 
+def _subcommand_index(argv) -> int:
+    """Position of the sub-command: the first argument that is not a global option (the global
+    flags -V/-v/-d take no value), or -1."""
+    for i, a in enumerate(argv):
+        if not a.startswith("-"):
+            return i
+    return -1
+
+
 def _space_after_options(argv):
     """``mopt sweep ... --lr~'loguniform(..)'``: a sweep has no script, so its space starts at
-    the first ``--name~prior`` argument; a ``--`` there hands the rest to the user arguments."""
-    if "sweep" not in argv:
+    the first ``--name~prior`` argument; a ``--`` there hands the rest to the user arguments.
+    Only the ``sweep`` sub-command is rewritten: a ``sweep`` token elsewhere (an experiment name,
+    a user argument's value) leaves the command line as typed."""
+    sub = _subcommand_index(argv)
+    if sub < 0 or argv[sub] != "sweep":
         return argv
-    start = argv.index("sweep") + 1
+    start = sub + 1
     for i in range(start, len(argv)):
         if argv[i] == "--":
             return argv

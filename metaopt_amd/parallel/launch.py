@@ -1,7 +1,8 @@
 """Single-node launcher: one rank process per GPU (``mopt sweep --gpus N``, ``bench.py --gpus N``).
 
-The launching process never initialises HIP (it only counts devices, which does not on this
-image) and starts the ranks as child processes -- it never ``exec``s into one.  Ranks get
+The launching process never touches HIP: it counts the GPUs from the kernel driver's KFD topology
+in sysfs and the visible-devices variables (:func:`visible_gpu_count`), and starts the ranks as
+child processes -- it never ``exec``s into one.  Ranks get
 ``RANK / LOCAL_RANK / WORLD_SIZE / LOCAL_WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT`` and
 rendezvous through :func:`metaopt_amd.parallel.comm.init_from_env` (RCCL on GPUs).  When the
 host has fewer GPUs than ranks (a rehearsal on a one-GPU box) or none (CPU tests) the ranks use
@@ -24,14 +25,53 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
+KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
+_VISIBLE_VARS = ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")
+
+
+def _kfd_gpu_count(root: str = KFD_NODES) -> int:
+    """GPU agents in the KFD topology: nodes whose ``properties`` report SIMDs (CPU nodes have
+    ``simd_count 0``).  0 when the driver is absent."""
+    try:
+        nodes = os.listdir(root)
+    except OSError:
+        return 0
+    n = 0
+    for node in nodes:
+        try:
+            with open(os.path.join(root, node, "properties")) as f:
+                props = dict(line.split(None, 1) for line in f if line.strip())
+        except (OSError, ValueError):
+            continue
+        if int(props.get("simd_count", "0")) > 0:
+            n += 1
+    return n
+
+
+def visible_gpu_count(env: Optional[dict] = None, root: str = KFD_NODES) -> int:
+    """GPUs a child process will see, without initialising HIP in this one: the KFD topology's
+    GPU count, narrowed by ``ROCR_VISIBLE_DEVICES`` / ``HIP_VISIBLE_DEVICES`` /
+    ``CUDA_VISIBLE_DEVICES`` (each applied in that order, as the runtime does)."""
+    env = os.environ if env is None else env
+    n = _kfd_gpu_count(root)
+    for var in _VISIBLE_VARS:
+        val = env.get(var)
+        if val is None:
+            continue
+        ids = [v for v in val.split(",") if v.strip()]
+        if not ids or ids[0].strip() == "-1":
+            return 0
+        n = min(n, len(ids))
+    return n
+
+
 def rank_env(n: int, base: Optional[dict] = None, port: Optional[int] = None) -> dict:
     """Environment shared by the ``n`` ranks (RANK / LOCAL_RANK are added per rank)."""
-    import torch
     env = dict(os.environ if base is None else base)
     env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port or free_port()),
                WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n))
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    n_dev = torch.cuda.device_count()
+    n_dev = visible_gpu_count(env)
     if n_dev < n:
         env["MOPT_COMM_BACKEND"] = "gloo"
         if n_dev > 0:

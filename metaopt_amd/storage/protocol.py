@@ -23,6 +23,7 @@ import logging
 from typing import List, Optional
 
 from ..core.trial import Trial
+from ..utils.registry import Registry
 from .database import (AbstractDB, DatabaseError, EphemeralDB, OutdatedDatabaseError, ReadOnlyDB,
                        create_database)
 
@@ -48,6 +49,11 @@ def db_is_outdated(db: AbstractDB) -> bool:
     except Exception:  # pragma: no cover - backend without the collection
         return False
     return "name_1_metadata.user_1" in info
+
+
+# storage protocols by name (``storage: {type: legacy}``); plugins through the ``Storage`` entry
+# point group, as the reference declares its own (reference setup.py:48-50)
+STORAGES = Registry("Storage", groups=("metaopt_amd.storages", "Storage"))
 
 
 class BaseStorageProtocol:
@@ -118,6 +124,7 @@ def _uid(obj, uid, what):
     return uid
 
 
+@STORAGES.register("legacy")
 class DocumentStorage(BaseStorageProtocol):
     """The reference's ``Legacy`` protocol: everything in one document database."""
 
@@ -364,7 +371,7 @@ def setup_storage(config: Optional[dict] = None, debug: bool = False,
         from ..core.config import config as global_config
         heartbeat = global_config.worker.heartbeat
     db = create_database(of_type, **db_cfg)
-    _STORAGE = DocumentStorage(db, heartbeat=heartbeat)
+    _STORAGE = STORAGES.get(config.get("type", "legacy"))(db, heartbeat=heartbeat)
     return _STORAGE
 
 

@@ -59,10 +59,29 @@ class TrialFiles:
         return cls(root, *paths)
 
 
+# the directory holding the ``metaopt_amd`` and ``orion`` packages of this worker
+_PACKAGE_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def _client_importable(env: dict) -> dict:
+    """Make the worker's own client library importable by the script (``from orion.client
+    import report_results``), as an installed distribution would: the package root is appended
+    to ``PYTHONPATH`` unless the packages are already importable from site-packages or the path
+    already holds it."""
+    import importlib.util
+    spec = importlib.util.find_spec("orion")
+    installed = spec is not None and spec.origin is not None and "site-packages" in spec.origin
+    paths = [p for p in env.get("PYTHONPATH", "").split(os.pathsep) if p]
+    if not installed and _PACKAGE_ROOT not in paths and \
+            os.path.isdir(os.path.join(_PACKAGE_ROOT, "orion")):
+        env["PYTHONPATH"] = os.pathsep.join(paths + [_PACKAGE_ROOT])
+    return env
+
+
 def trial_env(experiment, trial, results_path, base=None) -> dict:
     """The script's environment: ``base`` (default: this process's) plus the trial variables
-    under both the ``ORION_`` and ``MOPT_`` prefixes."""
-    env = dict(os.environ if base is None else base)
+    under both the ``ORION_`` and ``MOPT_`` prefixes, with the client library importable."""
+    env = _client_importable(dict(os.environ if base is None else base))
     values = {"EXPERIMENT_ID": experiment.id, "EXPERIMENT_NAME": experiment.name,
               "EXPERIMENT_VERSION": experiment.version, "TRIAL_ID": trial.id,
               "WORKING_DIR": trial.working_dir, "RESULTS_PATH": results_path}

@@ -5,13 +5,16 @@ runs, its ``heartbeat`` in storage is refreshed every ``wait_time`` seconds; the
 once the trial is completed / interrupted / suspended / broken, or when a refresh fails (the trial
 was declared lost and taken over by another worker).
 
-Structure: one scheduler thread serves every pacemaker of the process from a deadline heap --
-a study holding many reserved trials (``client/study.py``) costs one thread, not one per trial.
+Structure: one dispatcher thread serves every pacemaker of the process from a deadline heap and
+hands due beats to a few worker threads -- a study holding many reserved trials
+(``client/study.py``) costs at most five threads, not one per trial, and one stalled storage call
+holds up only its own trial's heartbeat.
 :class:`TrialPacemaker` is a handle on one entry: ``start`` schedules it, ``stop`` cancels it
 and returns once no beat of it is running, ``stopped`` is set when it ends for any reason.
 """
 from __future__ import annotations
 
+import collections
 import heapq
 import itertools
 import logging
@@ -24,57 +27,89 @@ STOPPED_STATUS = {"completed", "interrupted", "suspended", "broken"}
 
 
 class _Scheduler:
-    """Deadline heap of pacemakers, served by one daemon thread (started on first use)."""
+    """Deadline heap of pacemakers.  One daemon dispatcher thread pops due entries; the beats
+    themselves (storage round trips) run on a few daemon worker threads, so one slow or stalled
+    storage call (a contended PickledDB lock, a slow MongoDB) delays only its own trial's beat,
+    never the other trials' -- their heartbeats stay fresh.  Threads start on first use and end
+    when idle."""
+
+    MAX_WORKERS = 4
+    IDLE_EXIT_S = 1.0
 
     def __init__(self):
         self._cv = threading.Condition()
         self._heap = []                     # (due, seq, pacemaker)
         self._seq = itertools.count()
-        self._thread = None
-        self._running = None                # the pacemaker whose beat is in progress
+        self._thread = None                 # dispatcher
+        self._ready = collections.deque()   # due pacemakers waiting for a worker
+        self._running = set()               # pacemakers whose beat is in progress
+        self._workers = 0
+        self._idle = 0
 
     def add(self, pm, due):
         with self._cv:
             heapq.heappush(self._heap, (due, next(self._seq), pm))
             if self._thread is None or not self._thread.is_alive():
-                self._thread = threading.Thread(target=self._serve, name="mopt-heartbeats",
+                self._thread = threading.Thread(target=self._dispatch, name="mopt-heartbeats",
                                                 daemon=True)
                 self._thread.start()
-            self._cv.notify()
+            self._cv.notify_all()
 
     def wait_idle(self, pm):
-        """Block until ``pm`` is not being beaten (its entry may still sit in the heap, where
-        it is skipped once ``pm.stopped`` is set)."""
+        """Block until ``pm`` is not being beaten (its entry may still sit in the heap or the
+        ready queue, where it is skipped once ``pm.stopped`` is set)."""
         with self._cv:
-            while self._running is pm:
+            while pm in self._running:
                 self._cv.wait(0.05)
 
-    def _serve(self):
+    def _dispatch(self):
         while True:
             with self._cv:
-                while True:
-                    while self._heap and self._heap[0][2].stopped.is_set():
-                        heapq.heappop(self._heap)          # cancelled entries
+                while self._heap and self._heap[0][2].stopped.is_set():
+                    heapq.heappop(self._heap)              # cancelled entries
+                if not self._heap:
+                    self._cv.wait(self.IDLE_EXIT_S)
                     if not self._heap:
-                        self._cv.wait(1.0)
-                        if not self._heap:
-                            self._thread = None
-                            return                          # idle: the next add restarts it
-                        continue
-                    due = self._heap[0][0]
-                    now = time.monotonic()
-                    if due <= now:
-                        _, _, pm = heapq.heappop(self._heap)
-                        self._running = pm
-                        break
+                        self._thread = None
+                        return                              # idle: the next add restarts it
+                    continue
+                due = self._heap[0][0]
+                now = time.monotonic()
+                if due > now:
                     self._cv.wait(due - now)
-            try:
-                alive = pm._beat()
-            except Exception as exc:   # a storage error ends this trial's heartbeat only
-                log.warning("heartbeat of trial %s failed: %s", pm.trial.id, exc)
-                alive = False
+                    continue
+                _, _, pm = heapq.heappop(self._heap)
+                self._running.add(pm)
+                self._ready.append(pm)
+                # one worker per queued beat (an idle worker that has not woken yet counts once)
+                if len(self._ready) > self._idle and self._workers < self.MAX_WORKERS:
+                    self._workers += 1
+                    threading.Thread(target=self._work, name="mopt-heartbeat-worker",
+                                     daemon=True).start()
+                self._cv.notify_all()
+
+    def _work(self):
+        while True:
             with self._cv:
-                self._running = None
+                self._idle += 1
+                deadline = time.monotonic() + self.IDLE_EXIT_S
+                while not self._ready:
+                    left = deadline - time.monotonic()
+                    if left <= 0:
+                        self._idle -= 1
+                        self._workers -= 1
+                        return
+                    self._cv.wait(left)
+                self._idle -= 1
+                pm = self._ready.popleft()
+            alive = False
+            if not pm.stopped.is_set():
+                try:
+                    alive = pm._beat()
+                except Exception as exc:   # a storage error ends this trial's heartbeat only
+                    log.warning("heartbeat of trial %s failed: %s", pm.trial.id, exc)
+            with self._cv:
+                self._running.discard(pm)
                 if alive and not pm.stopped.is_set():
                     heapq.heappush(self._heap, (time.monotonic() + pm.wait_time,
                                                 next(self._seq), pm))

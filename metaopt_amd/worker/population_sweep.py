@@ -74,6 +74,7 @@ class PopulationSweep:
         P = pop.capacity
         self.slot_key = np.full(P, -1, dtype=np.int64)
         self._n_active = 0
+        self._rows_active = 0         # samples per step over the resident members
         self.slot_budget = np.zeros(P, dtype=np.int64)
         # device checkpoints of finished members (ASHA promotion, PBT exploit): trial key ->
         # metadata of a slot in the population's checkpoint pool, evicted FIFO
@@ -107,16 +108,7 @@ class PopulationSweep:
         self.timers: Dict[str, float] = collections.defaultdict(float)  # host seconds per phase
         self._gc_t0 = 0.0
         self.max_write_backlog = 4 * pop.capacity * self.comm.world_size
-        gc.callbacks.append(self._gc_callback)   # host GC pauses show up in the phase timers
-        # Every sync allocates thousands of long-lived objects (trial records, algorithm
-        # entries) and ends with gc.freeze(); with the default gen-0 threshold (700) the young
-        # generations were collected -- and, the frozen objects being out of the heuristics,
-        # fully collected -- several times per sync: 5-13 ms of rank 0's ~30 ms decide at 8
-        # simulated ranks vs 0.5 ms at 20000 (scripts/profile_decide.py, GC_T0).  Restored by
-        # close().
-        self._gc_threshold = gc.get_threshold()
-        if self._gc_threshold[0] < 20000:
-            gc.set_threshold(20000, *self._gc_threshold[1:])
+        self._gc_threshold = None     # set last in __init__ (see there), restored by close()
         self.n_resumed = 0            # members resumed from a device checkpoint (this rank)
         self.n_resume_missing = 0
         self.n_syncs = 0
@@ -206,6 +198,17 @@ class PopulationSweep:
         self.events.emit("sweep_start", world_size=self.comm.world_size, population=P,
                          sync_every=self.sync_every, pipelined=self.pipelined,
                          algorithm=type(getattr(self, "algorithm", None)).__name__)
+        # Process-wide GC settings, changed as the constructor's LAST step (nothing after this can
+        # raise, so a failed construction never leaves them changed) and restored by close():
+        # every sync allocates thousands of long-lived objects (trial records, algorithm
+        # entries) and ends with gc.freeze(); with the default gen-0 threshold (700) the young
+        # generations were collected -- and, the frozen objects being out of the heuristics,
+        # fully collected -- several times per sync: 5-13 ms of rank 0's ~30 ms decide at 8
+        # simulated ranks vs 0.5 ms at 20000 (scripts/profile_decide.py, GC_T0).
+        gc.callbacks.append(self._gc_callback)   # host GC pauses show up in the phase timers
+        self._gc_threshold = gc.get_threshold()
+        if self._gc_threshold[0] < 20000:
+            gc.set_threshold(20000, *self._gc_threshold[1:])
 
     def _make_writer(self, kind: str, sec_name: str):
         """Storage writes off the decision path: in this process (``inline``) or in a child
@@ -239,7 +242,7 @@ class PopulationSweep:
         x, y = self.data.batch(self.global_step)
         self.pop.train_step(x, y)
         self.global_step += 1
-        self.samples += self.pop.batch_size * self._n_active
+        self.samples += self._rows_active
         left = self.sync_every - self.global_step % self.sync_every
         if self.pipelined and left == min(2, self.sync_every - 1):
             # the writes drained at the sync stop once the GPU gets this close to the boundary
@@ -279,7 +282,7 @@ class PopulationSweep:
                 continue
             multi([self.data.batch(self.global_step + i) for i in range(count)])
             self.global_step += count
-            self.samples += self.pop.batch_size * self._n_active * count
+            self.samples += self._rows_active * count
             if count == head and tail:
                 self._busy_marker = self.pop.device_busy()
         self.timers["launch"] += time.perf_counter() - t0
@@ -1019,6 +1022,18 @@ class PopulationSweep:
             self.n_resumed += 1
         self.done = bool(assign[-1, 0])
         self._n_active = int((self.slot_key >= 0).sum())
+        self._rows_active = self._active_rows()
+
+    def _active_rows(self) -> int:
+        """Samples per train step over the resident members: each member's own batch size
+        (a ``/batch_size`` prior trains members on fewer rows than the population's batch)."""
+        pop = self.pop
+        rows_of = getattr(pop, "member_rows", None)
+        members = getattr(pop, "members", None)
+        if rows_of is None or members is None:
+            return pop.batch_size * self._n_active
+        return int(sum(rows_of(members[s]) for s in np.flatnonzero(self.slot_key >= 0)
+                       if members[s] is not None))
 
     def _exchange_checkpoints(self, assign: np.ndarray) -> Dict[int, dict]:
         """C4: checkpoints resumed on another rank travel point-to-point (one batched group of

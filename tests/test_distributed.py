@@ -166,3 +166,37 @@ def test_pbt_sweep_and_c4_copy_gloo_world2():
     n_trials, n_children, n_completed = parents
     assert n_trials == 18 and n_children == 12      # 6 members x 3 generations
     assert n_completed == 18 and fin0 and fin1
+
+
+# ------------------------------------------------------------------ launcher (no HIP before spawn)
+def _fake_kfd(root, simds):
+    for i, s in enumerate(simds):
+        d = root / str(i)
+        d.mkdir(parents=True)
+        (d / "properties").write_text(f"cpu_cores_count {0 if s else 8}\nsimd_count {s}\n"
+                                      f"gfx_target_version {90500 if s else 0}\n")
+    return str(root)
+
+
+def test_visible_gpu_count_from_kfd_topology(tmp_path):
+    from metaopt_amd.parallel.launch import visible_gpu_count
+    root = _fake_kfd(tmp_path / "nodes", [0, 1024, 1024, 1024, 1024])   # one CPU, four GPUs
+    assert visible_gpu_count({}, root) == 4
+    assert visible_gpu_count({"HIP_VISIBLE_DEVICES": "0,2"}, root) == 2
+    assert visible_gpu_count({"ROCR_VISIBLE_DEVICES": "1", "HIP_VISIBLE_DEVICES": "0,1"}, root) == 1
+    assert visible_gpu_count({"CUDA_VISIBLE_DEVICES": "-1"}, root) == 0
+    assert visible_gpu_count({}, str(tmp_path / "absent")) == 0
+
+
+def test_launcher_never_imports_torch_before_spawning():
+    """rank_env (what bench.py / ``mopt sweep --gpus N`` run before starting the ranks) must not
+    initialise HIP: it may not even import torch."""
+    import subprocess
+    import sys
+    code = ("import sys; from metaopt_amd.parallel.launch import rank_env; env = rank_env(2); "
+            "print(int('torch' in sys.modules), env['WORLD_SIZE'])")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                         timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.split() == ["0", "2"]

@@ -130,6 +130,18 @@ def test_prior_arguments_start_the_user_space():
     assert _space_after_options(["sweep", "--", "--lr~u"]) == ["sweep", "--", "--lr~u"]
     assert _space_after_options(["hunt", "-n", "x", "s.py", "--lr~u"]) == \
         ["hunt", "-n", "x", "s.py", "--lr~u"]
+    assert _space_after_options(["-v", "sweep", "--lr~u"]) == ["-v", "sweep", "--", "--lr~u"]
+
+
+@pytest.mark.parametrize("argv", [
+    ["hunt", "-n", "sweep", "./train.py", "--lr~uniform(0,1)"],        # experiment named sweep
+    ["hunt", "-n", "x", "./train.py", "--mode", "sweep", "--lr~u"],    # a user value "sweep"
+    ["-v", "hunt", "-n", "x", "./sweep", "--lr~u"],
+])
+def test_sweep_token_outside_the_subcommand_is_left_alone(argv):
+    """Only the ``sweep`` sub-command is rewritten: a stray ``--`` in a hunt's user arguments
+    would change the CommandLineConflict fingerprint and branch a resumed experiment."""
+    assert _space_after_options(argv) == argv
 
 
 def test_gpus_two_spawns_two_ranks(tmp_path):

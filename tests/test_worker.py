@@ -206,6 +206,48 @@ class TestPacemaker:
         assert pm.stopped.is_set()
         pm.stop()
 
+    def test_stalled_storage_call_does_not_stale_other_heartbeats(self):
+        """One trial's beat blocks inside storage (a contended lock); the other trials held by
+        the same process keep beating (one shared scheduler thread used to serialise
+        every beat behind the stalled one)."""
+        import threading
+        exp = _exp(name="hb_stall")
+        for v in (0.1, 0.2, 0.3):
+            exp.register_trial(Trial(experiment=exp.id,
+                                     params=[dict(name="/x", type="real", value=v)]))
+        trials = [exp.reserve_trial() for _ in range(3)]
+        release = threading.Event()
+
+        class StallingStorage:
+            def __init__(self, inner, stall_id):
+                self.inner, self.stall_id = inner, stall_id
+
+            def get_trial(self, trial):
+                if trial.id == self.stall_id:
+                    release.wait(10)              # blocked until the test releases it
+                return self.inner.get_trial(trial)
+
+            def update_heartbeat(self, trial):
+                return self.inner.update_heartbeat(trial)
+
+        st = StallingStorage(exp.storage, trials[0].id)
+        pms = [TrialPacemaker(t, wait_time=0.05, storage=st) for t in trials]
+        before = [exp.get_trial(t).heartbeat for t in trials]
+        for pm in pms:
+            pm.start()
+        try:
+            time.sleep(0.2)                       # the stalled beat is now in progress
+            mid = [exp.get_trial(t).heartbeat for t in trials[1:]]
+            time.sleep(0.4)
+            after = [exp.get_trial(t).heartbeat for t in trials[1:]]
+            assert all(a > m for a, m in zip(after, mid)), (mid, after)
+            assert all(a > b for a, b in zip(after, before[1:]))
+            assert exp.get_trial(trials[0]).heartbeat == before[0]
+        finally:
+            release.set()
+            for pm in pms:
+                pm.stop()
+
 
 # ------------------------------------------------------------------ study API
 class TestStudy:
