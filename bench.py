@@ -61,6 +61,11 @@ def parse_args(argv=None):
                          "this many sync intervals from the start of the sweep")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--algo", default="asha", choices=["asha", "random", "tpe"])
+    ap.add_argument("--asha-mode", default="async", choices=["async", "bounded"],
+                    help="async: Li et al.'s unbounded asynchronous ASHA; bounded: the "
+                         "reference's bracket semantics repeated (repetitions=inf)")
+    ap.add_argument("--fidelity", default="1,16,4",
+                    help="ASHA fidelity 'min,max,base' in sync intervals (steps = x sync_every)")
     ap.add_argument("--momentum-dtype", default="bf16", choices=["fp32", "bf16"],
                     help="SGD momentum buffer precision (weights: f32 master + bf16 copy)")
     return ap.parse_args(argv)
@@ -96,7 +101,8 @@ def run_rank(args) -> None:
     max_width = args.max_width if on_gpu else min(args.max_width, 256)
     S = args.sync_every
     priors = dict(BENCH_PRIORS)
-    priors["/steps"] = f"fidelity({S}, {16 * S}, 4)"
+    f_min, f_max, f_base = (int(v) for v in args.fidelity.split(","))
+    priors["/steps"] = f"fidelity({f_min * S}, {f_max * S}, {f_base})"
     if not on_gpu:  # CPU smoke configuration (the GPU path is the measured one)
         priors["/width"] = f"loguniform(64, {max_width}, discrete=True)"
     task = MLPSweepTask(priors=priors, max_width=max_width)
@@ -104,7 +110,9 @@ def run_rank(args) -> None:
     experiment = None
     if comm.is_root:
         storage = DocumentStorage(EphemeralDB())
-        algo = {"asha": {"asha": {"seed": args.seed, "repetitions": float("inf")}},
+        asha_cfg = ({"seed": args.seed, "unbounded": True} if args.asha_mode == "async" else
+                    {"seed": args.seed, "repetitions": float("inf")})
+        algo = {"asha": {"asha": asha_cfg},
                 "random": {"random": {"seed": args.seed}},
                 "tpe": {"tpe": {"seed": args.seed, "n_initial_points": P}}}[args.algo]
         experiment = build_experiment("bench-mlp-sweep", priors=priors, algorithms=algo,
@@ -171,7 +179,7 @@ def run_rank(args) -> None:
             "data": "synthetic (teacher-labelled MNIST-shaped 784->10, random-init weights)",
             "config": {
                 "model": "4-layer MLP 784-w-w-w-10, w~loguniform(64,1024), dropout, SGD-momentum",
-                "algorithm": args.algo,
+                "algorithm": args.algo if args.algo != "asha" else f"asha ({args.asha_mode})",
                 "population_per_gpu": P,
                 "global_batch": 128 * P * comm.world_size,
                 "seq_len": None,
@@ -199,6 +207,11 @@ def run_rank(args) -> None:
                        "samples_per_gpu": budget_steps * 128 * P,
                        "trials_finished_within": at_budget[1],
                        "reached": reached},
+            # best-loss at several budgets (sync intervals from the start of the sweep)
+            "best_val_loss_at_intervals": {
+                str(n): (round(sweep.best_within(n * S)[0], 5)
+                         if sweep.global_step >= n * S and math.isfinite(sweep.best_within(n * S)[0])
+                         else None) for n in (12, 24, 48)},
             "samples_per_sec": round(samples / elapsed, 1),
             "host_ms_per_sync": summ["host_ms_per_sync"],
             **({"gpu_timeline": sweep.gpu_timeline()} if os.environ.get("MOPT_GPU_TIMELINE")

@@ -14,6 +14,17 @@ with three changes made for device populations:
 * ``Bracket.is_done`` returns a bool (the reference returns ``len(rung)``, quirk 4);
 * the full rung state round-trips through ``state_dict``/``set_state`` when ``full=True`` is
   requested (device checkpoints resume the search without replaying trials).
+
+``unbounded=True`` selects the asynchronous algorithm of Li et al. (Algorithm 2) instead of the
+reference's bounded brackets: each bracket's rungs grow without limit (a bracket is never
+"filled", its top rung never closes), a configuration is promoted from rung k as soon as it ranks
+in the top ``n_k // eta`` of the rung's *completed* entries (``n_k`` = completed, not pending --
+otherwise the first completions of a rung full of pending work would all qualify), and a new
+configuration is sampled only when nothing is promotable.  With the bounded default every bracket
+promotes exactly one configuration to the top budget and ``repetitions=inf`` turns the search
+into a chain of tiny brackets: at the device sweep's budget that spent the budget on bottom-rung
+runs and lost to random search ("What's weak" 2).  The default stays bounded, the
+reference's semantics (``/root/reference/src/orion/algo/asha.py:156-202,317-361``).
 """
 from __future__ import annotations
 
@@ -44,10 +55,12 @@ class ASHA(BaseAlgorithm):
     trusted_suggestions = True   # space samples and promotions of already-validated points
 
     def __init__(self, space, seed=None, grace_period=None, max_resources=None,
-                 reduction_factor=None, num_rungs=None, num_brackets=1, repetitions=1):
+                 reduction_factor=None, num_rungs=None, num_brackets=1, repetitions=1,
+                 unbounded=False):
         super().__init__(space, seed=seed, max_resources=max_resources,
                          grace_period=grace_period, reduction_factor=reduction_factor,
-                         num_rungs=num_rungs, num_brackets=num_brackets, repetitions=repetitions)
+                         num_rungs=num_rungs, num_brackets=num_brackets, repetitions=repetitions,
+                         unbounded=unbounded)
         self.trial_info = {}  # id (non-fidelity params) -> Bracket
         try:
             fid = self.space.values()[self.fidelity_index]
@@ -65,8 +78,11 @@ class ASHA(BaseAlgorithm):
                                  num_rungs, base=eta).astype(int)
         self.budgets = [int(b) for b in budgets]
         self.eta = eta
-        self.brackets = [Bracket(self, eta, self.budgets[i:]) for i in range(num_brackets)]
+        self.brackets = [self._bracket(self.budgets[i:]) for i in range(num_brackets)]
         self._repetition = 1
+
+    def _bracket(self, budgets):
+        return (AsyncBracket if self.unbounded else Bracket)(self, self.eta, budgets)
 
     def seed_rng(self, seed):
         self.rng = numpy.random.RandomState(seed)
@@ -80,7 +96,7 @@ class ASHA(BaseAlgorithm):
         self.rng.set_state(state_dict["rng_state"])
         if "rungs" in state_dict:
             while len(self.brackets) < len(state_dict["rungs"]):
-                self.brackets.append(Bracket(self, self.eta, self.budgets[:1]))
+                self.brackets.append(self._bracket(self.budgets[:1]))
             self._repetition = state_dict.get("repetition", 1)
             for bracket, rungs in zip(self.brackets, state_dict["rungs"]):
                 bracket.rungs = [(b, {k: (o, tuple(p)) for k, (o, p) in r.items()})
@@ -112,7 +128,12 @@ class ASHA(BaseAlgorithm):
         """Promotions first (one at a time, each registered as pending), then all remaining new
         points drawn in ONE vectorised ``space.sample`` call and spread over the brackets."""
         out = []
-        while len(out) < num:
+        if self.unbounded:       # batched: every eligible promotion of a rung in one query
+            for bracket in self.brackets:
+                out.extend(bracket.promote(num - len(out)))
+                if len(out) >= num:
+                    break
+        while len(out) < num and not self.unbounded:
             cand = None
             for bracket in self.brackets:
                 cand = bracket.update_rungs()
@@ -140,8 +161,7 @@ class ASHA(BaseAlgorithm):
             # ``repetitions > 1``: run another set of brackets (the population keeps sampling
             # instead of idling, as in the original ASHA which never stops adding configs)
             self._repetition += 1
-            self.brackets += [Bracket(self, self.eta, self.budgets[i:])
-                              for i in range(self.num_brackets)]
+            self.brackets += [self._bracket(self.budgets[i:]) for i in range(self.num_brackets)]
             current = self.brackets[-self.num_brackets:]
         return current
 
@@ -216,6 +236,8 @@ class ASHA(BaseAlgorithm):
 
     @property
     def is_done(self):
+        if self.unbounded:        # asynchronous ASHA never runs out of configurations
+            return False
         reps = self.repetitions if self.repetitions is not None else 1
         return self._repetition >= reps and all(b.is_done for b in self.brackets)
 
@@ -303,12 +325,14 @@ class Bracket:
                 self._discard(self._free[i - 1], (below[0], _id))
 
     def get_candidate(self, rung_id):
-        """Best completed entry of the rung's top ``len(rung) // eta`` not promoted yet."""
+        """Best completed entry of the rung's top ``len(rung) // eta`` not promoted yet
+        (unbounded: top ``completed // eta``)."""
         free = self._free[rung_id]
         if not free:
             return None
         _, rung = self.rungs[rung_id]
-        k = min(len(rung) // self.reduction_factor, len(self._sorted[rung_id]))
+        n = len(self._sorted[rung_id]) if self.asha.unbounded else len(rung)
+        k = min(n // self.reduction_factor, len(self._sorted[rung_id]))
         best = free[0]
         if bisect.bisect_left(self._sorted[rung_id], best) < k:
             return rung[best[1]][1]
@@ -321,6 +345,8 @@ class Bracket:
 
     @property
     def is_filled(self) -> bool:
+        if self.asha.unbounded:
+            return False
         return self.has_rung_filled(len(self.rungs) - 2)
 
     def has_rung_filled(self, rung_id) -> bool:
@@ -328,7 +354,8 @@ class Bracket:
         return len(self.rungs[rung_id][1]) >= self.reduction_factor ** (n - rung_id - 1)
 
     def update_rungs(self):
-        if self.rungs[-1][1]:  # the top rung is taken (pending or completed): no more promotions
+        # bounded: the top rung is taken (pending or completed) -> no more promotions
+        if self.rungs[-1][1] and not self.asha.unbounded:
             return None
         for rung_id in range(len(self.rungs) - 2, -1, -1):
             cand = self.get_candidate(rung_id)
@@ -340,3 +367,113 @@ class Bracket:
 
     def __repr__(self):
         return f"Bracket({[b for b, _ in self.rungs]})"
+
+
+class AsyncBracket(Bracket):
+    """The rungs of asynchronous (unbounded) ASHA, with the promotion query over numpy arrays.
+
+    Unbounded rungs grow by every completion of the sweep (about a thousand per sync at 8 GPUs),
+    so the sorted-list index of :class:`Bracket` (``bisect.insort``: O(n) per insert) became the
+    rank-0 decision's largest cost.  Here each rung keeps its objectives in a growable float64
+    array (NaN = pending) with a "promoted" flag per entry; registering a result is O(1), and a
+    promotion query is one ``argpartition`` over the rung's completed objectives -- the top
+    ``completed // eta`` -- recomputed only when the rung received a result since the last query.
+    The eligible, not yet promoted entries are then handed out best first (ties by arrival)."""
+
+    def __init__(self, asha, reduction_factor, budgets):
+        super().__init__(asha, reduction_factor, budgets)
+        self.rebuild_index()
+
+    def rebuild_index(self):
+        R = len(self.rungs)
+        self._pos = [dict() for _ in range(R)]
+        self._obj = [numpy.full(64, numpy.nan) for _ in range(R)]
+        self._prom = [numpy.zeros(64, dtype=bool) for _ in range(R)]
+        self._ids = [[] for _ in range(R)]
+        self._queue = [None] * R          # eligible positions, best first (None = recompute)
+        for i, (_, rung) in enumerate(self.rungs):
+            for _id, (obj, _) in rung.items():
+                self._slot(i, _id, obj)
+        for i in range(1, R):
+            for _id in self.rungs[i][1]:
+                j = self._pos[i - 1].get(_id)
+                if j is not None:
+                    self._prom[i - 1][j] = True
+
+    def _slot(self, i, _id, objective):
+        pos = self._pos[i]
+        j = pos.get(_id)
+        if j is None:
+            j = len(self._ids[i])
+            if j == len(self._obj[i]):
+                self._obj[i] = numpy.concatenate([self._obj[i], numpy.full(j, numpy.nan)])
+                self._prom[i] = numpy.concatenate([self._prom[i], numpy.zeros(j, dtype=bool)])
+            pos[_id] = j
+            self._ids[i].append(_id)
+        if objective is not None:
+            self._obj[i][j] = objective
+            self._queue[i] = None
+        return j
+
+    def _register_at(self, i, point, objective, overwrite, _id=None):
+        rung = self.rungs[i][1]
+        if _id is None:
+            _id = self.asha.get_id(point)
+        if not overwrite and _id in rung:
+            return
+        new = _id not in rung
+        rung[_id] = (objective, tuple(point))
+        self._slot(i, _id, objective)
+        if i > 0 and new:   # entering rung i = promoted out of rung i - 1
+            j = self._pos[i - 1].get(_id)
+            if j is not None:
+                self._prom[i - 1][j] = True
+
+    def _eligible(self, i):
+        q = self._queue[i]
+        if q is None:
+            n = len(self._ids[i])
+            obj = self._obj[i][:n]
+            done = numpy.flatnonzero(~numpy.isnan(obj))
+            k = len(done) // self.reduction_factor
+            if k == 0:
+                q = []
+            else:
+                top = done[numpy.argpartition(obj[done], k - 1)[:k]] if k < len(done) else done
+                top = top[numpy.lexsort((top, obj[top]))]      # best first, ties by arrival
+                q = top[~self._prom[i][top]].tolist()
+            q.reverse()                                         # pop() from the best end
+            self._queue[i] = q
+        return q
+
+    def get_candidate(self, rung_id):
+        q = self._eligible(rung_id)
+        while q and self._prom[rung_id][q[-1]]:
+            q.pop()
+        return self.rungs[rung_id][1][self._ids[rung_id][q[-1]]][1] if q else None
+
+    def promote(self, num):
+        """Up to ``num`` promotions, highest rung first, each registered as pending above."""
+        out = []
+        fi = self.asha.fidelity_index
+        for rung_id in range(len(self.rungs) - 2, -1, -1):
+            q = self._eligible(rung_id)
+            nxt = self.rungs[rung_id + 1][0]
+            while q and len(out) < num:
+                j = q.pop()
+                if self._prom[rung_id][j]:
+                    continue
+                cand = list(self.rungs[rung_id][1][self._ids[rung_id][j]][1])
+                cand[fi] = nxt
+                cand = tuple(cand)
+                self._register_at(rung_id + 1, cand, None, False, self._ids[rung_id][j])
+                out.append(cand)
+            if len(out) >= num:
+                break
+        return out
+
+    def update_rungs(self):
+        out = self.promote(1)
+        if out:   # promote() registered it already; suggest() registers again (no-op)
+            return out[0]
+        return None

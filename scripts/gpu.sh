@@ -7,10 +7,12 @@
 # work after a fault, an abort or a timeout).  Steps:
 #   tests            pytest -m gpu (whole suite)           tests:FILE[,FILE]  a subset
 #   bench            bench.py N=1 (driver shape)           bench_long  60 timed intervals
+#   algos            bench.py per algorithm / ASHA variant over 48 intervals (best loss at 12/24/48)
 #   random           bench.py --algo random (best-loss@budget at the same budget as ASHA)
 #   timeline         bench.py with the GPU-event timeline (MOPT_GPU_TIMELINE=1)
 #   streams          bench.py at MOPT_STREAMS=1,2
 #   kbench           per-kernel MLP microbench             trace_bench  rocprofv3 kernel trace
+#   kbench_ab        the microbench per backward variant (MOPT_BWD_PREFETCH in $PFS, default "1 2")
 #   kbench_rows      the microbench at 128 / 256 / 512 rows per step (multi-row-block kernels)
 #   pmc_kbench       PMC passes of the MLP kernels (fetch/write/MFMA/LDS, one pass each)
 #   lm resnet hyper  bench_configs.py of one config        trace_lm trace_resnet trace_hyper
@@ -44,10 +46,15 @@ for step in "$@"; do
     tests:*)    $T 400 $PYT $(echo "${step#tests:}" | tr ',' ' ') > "$OUT/pytest_sub.log" 2>&1 ;;
     bench)      $T 240 python bench.py --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
     bench_long) $T 240 python bench.py --steps 60 --warmup 5 > "$OUT/bench_long.json" 2> "$OUT/bench_long.err" ;;
+    algos)      # best-loss@budget per search algorithm / ASHA variant (48 intervals each)
+                for v in "random:--algo random" "bounded:--asha-mode bounded" "async:--asha-mode async" \
+                         "async_eta2:--asha-mode async --fidelity 2,16,2" "async_g4:--asha-mode async --fidelity 4,16,4"; do
+                  $T 240 python bench.py --steps 43 --warmup 5 ${v#*:} > "$OUT/algo_${v%%:*}.json" 2> "$OUT/algo_${v%%:*}.err"; done ;;
     random)     $T 240 python bench.py --steps 20 --warmup 5 --algo random > "$OUT/bench_random.json" 2> "$OUT/bench_random.err" ;;
     timeline)   MOPT_GPU_TIMELINE=1 $T 240 python bench.py --steps 20 --warmup 5 > "$OUT/bench_timeline.json" 2> "$OUT/bench_timeline.err" ;;
     streams)    for s in 1 2; do MOPT_STREAMS=$s $T 240 python bench.py --steps 20 --warmup 5 > "$OUT/bench_streams$s.json" 2> "$OUT/bench_streams$s.err"; done ;;
     kbench)     $T 200 python scripts/kernel_bench.py --momentum-dtype bf16 --out "$OUT/kbench.json" > "$OUT/kbench.log" 2>&1 ;;
+    kbench_ab)  for pf in ${PFS:-1 2}; do MOPT_BWD_PREFETCH=$pf $T 200 python scripts/kernel_bench.py --momentum-dtype bf16 --out "$OUT/kbench_pf$pf.json" > "$OUT/kbench_pf$pf.log" 2>&1; done ;;
     kbench_rows) for b in 128 256 512; do $T 200 python scripts/kernel_bench.py --momentum-dtype bf16 --batch $b --iters 20 --out "$OUT/kbench_b$b.json" > "$OUT/kbench_b$b.log" 2>&1; done ;;
     trace_bench) prof trace_bench 300 -- python3 "$ROOT/bench.py" --steps 10 --warmup 3 ;;
     pmc_kbench)

@@ -49,7 +49,9 @@ class _FakeComm:
 def main(n_syncs=40, P=256, world=1, profile=False):
     task = MLPSweepTask(priors=dict(MLP_PRIORS), max_width=1024)
     exp = build_experiment("decide-prof", priors=dict(MLP_PRIORS),
-                           algorithms={"asha": {"seed": 0, "repetitions": float("inf")}},
+                           algorithms={"asha": ({"seed": 0, "unbounded": True}
+                                                if os.environ.get("ASHA", "async") == "async"
+                                                else {"seed": 0, "repetitions": float("inf")})},
                            storage=DocumentStorage(EphemeralDB()), pool_size=P)
     sw = PopulationSweep(_FakePop(P), task, data=None, comm=_FakeComm(world), experiment=exp,
                          sync_every=32, pipelined=False,
