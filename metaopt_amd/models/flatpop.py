@@ -486,6 +486,33 @@ class FlatPopulation:
         self.members[dst] = cfg
         self._write_hp(dst, cfg, int(self.hp[src]["t"]))
 
+    # ---- C4 straight from / into the checkpoint pool (PopulationSweep._exchange_checkpoints)
+    def _c4_header(self) -> torch.Tensor:
+        return torch.empty(2 + self.n_aux, dtype=torch.float32, device=self.device)
+
+    def c4_send_tensors(self, meta: dict) -> list:
+        """The pool entry of a checkpoint as it stands ([state buffers, n_params] f32,
+        contiguous) and a small header: step count, seed, the auxiliary state."""
+        idx = meta["ck"]
+        hdr = self._c4_header()
+        head = torch.tensor([int(meta["t"]), int(meta["config"]["seed"])], dtype=torch.int32)
+        hdr[:2].copy_(head.view(torch.float32))
+        if self.n_aux:
+            hdr[2:].copy_(self._ck_aux[idx, :self.n_aux])
+        return [self._ck[idx], hdr]
+
+    def c4_recv_tensors(self, idx: int) -> list:
+        return [self._ck[idx], self._c4_header()]
+
+    def c4_finish(self, idx: int, tensors: list) -> dict:
+        """Pool meta of a checkpoint received into entry ``idx`` (for :meth:`load_states`)."""
+        hdr = tensors[1]
+        t, seed = (int(v) for v in hdr[:2].view(torch.int32).cpu().tolist())
+        if self.n_aux:
+            self._ck_aux[idx, :self.n_aux].copy_(hdr[2:])
+        return {"config": MemberConfig(width=0, lr=0.0, seed=seed).to_dict(), "t": t,
+                "ck": int(idx), "n": self.n_params}
+
     def _n_packed(self) -> int:
         return 2 + len(self._state_bufs()) * self.n_params + self.n_aux
 

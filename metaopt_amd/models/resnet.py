@@ -67,9 +67,10 @@ class PopulationResNet(FlatPopulation):
         return specs
 
     def direct_grads(self):
-        # conv weights (wgrad kernels) and BatchNorm gamma / beta (BN backward); the classifier
-        # goes through autograd
-        return {f"{name}.{k}" for name, _, _, _ in self.layout for k in ("w", "g", "b")}
+        # conv weights (wgrad kernels), BatchNorm gamma / beta (BN backward) and the classifier
+        # (the fused head kernel): every gradient is written in full by a HIP kernel
+        return {f"{name}.{k}" for name, _, _, _ in self.layout for k in ("w", "g", "b")} | \
+            {"fc.w", "fc.b"}
 
     def aux_specs(self):
         return [(f"{name}.running", 2 * cout) for name, _, cout, _ in self.layout]
@@ -150,13 +151,13 @@ class PopulationResNet(FlatPopulation):
                 r = self._shortcut(h, c2, s1)
                 t = self._conv_bn(n1, h, s1, train, arena=arena)
                 h = self._conv_bn(n2, t, 1, train, res=r, arena=arena)
-        feat = h.view(P, B, -1, h.shape[-1]).float().mean(2)            # [P, B, 64]
-        logits = torch.baddbmm(W["fc.b"].float()[:, None, :], feat,
-                               W["fc.w"].float())[..., :NCLS]           # [P, B, 10]
-        labels = self._expand(y, torch.long)
-        loss = torch.nn.functional.cross_entropy(logits.reshape(-1, NCLS), labels.reshape(-1),
-                                                 reduction="none").view(P, B).sum(1)
-        correct = (logits.argmax(-1) == labels).float().sum(1)
+        labels = self._expand(y, torch.long).reshape(-1)
+        if x.device.type == "cuda":
+            # pool + linear + cross-entropy (+ its backward) in one HIP kernel; the classifier's
+            # dW / db land in the flat gradient buffer (direct gradients), mean-loss scaled
+            return cops.resnet_head(h, W["fc.w"], W["fc.b"], labels, P, NCLS, train,
+                                    scale=1.0 / B)
+        loss, correct, _ = cops.head_ref(h, W["fc.w"], W["fc.b"], labels, P, NCLS)
         if train:
             loss = _GradScale.apply(loss, 1.0 / B)
         return loss, correct

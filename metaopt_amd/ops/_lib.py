@@ -40,7 +40,6 @@ _SIGNATURES = {
     "mopt_mlp_step": ([c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "mopt_mlp_w_layout": ([], c_int),
     "mopt_mlp_steps": ([c_void_p, c_void_p, c_void_p, c_int, c_void_p], c_int),
-    "mopt_mlp_set_bwd_prefetch": ([c_int], c_int),
 }
 
 _OPTIONAL_SIGNATURES: dict = {}
@@ -136,7 +135,7 @@ def _load_checked():
 # and check() synchronises after every launch, reads the per-module violation counters and
 # raises naming the launch.  Implies the synchronous launch checking below.
 CHECKED = os.environ.get("MOPT_KERNEL_CHECKED", "0") not in ("", "0")
-_CHECKED_MODULES = ("lm_ops", "pop_mlp")
+_CHECKED_MODULES = ("lm_ops", "pop_mlp", "resnet_head")
 
 
 class BoundsViolation(RuntimeError):

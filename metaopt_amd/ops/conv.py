@@ -15,7 +15,6 @@ numerics oracle of tests/test_resnet_gpu.py.
 from __future__ import annotations
 
 import ctypes
-import os
 
 import torch
 
@@ -32,13 +31,18 @@ _lib.register_signatures({
     "mopt_dconv": ([c_int] + [c_void_p] * 4 + [c_int] * 7 + [c_void_p], c_int),
     "mopt_dconv_wgrad_splits": ([c_int] * 6, c_int),
     "mopt_dconv_bnin": ([c_int] + [c_void_p] * 4 + [c_int] * 5 + [c_void_p] * 4, c_int),
+    "mopt_resnet_head": ([c_void_p] * 4 + [c_int] * 5 + [c_float, c_int] + [c_void_p] * 7,
+                         c_int),
+    "mopt_resnet_head_part_floats": ([c_int] * 3, c_int),
 })
-# MOPT_BN_INTO_CONV=0: materialise every BatchNorm output (A/B switch of bn_relu_conv3x3)
-_BN_INTO_CONV = os.environ.get("MOPT_BN_INTO_CONV", "1") != "0"
+# BatchNorm 1 + ReLU applied while conv 2 stages its input (6.71 -> 6.55 ms/step, round 3); the
+# materialised path remains for evaluation and shapes the fused kernels do not take
+_BN_INTO_CONV = True
 
 _NOT_SUPPORTED = 801   # hipErrorNotSupported: no direct-conv instantiation for the shape
-# MOPT_CONV_IMPLICIT=1 routes every convolution through the implicit GEMM (A/B and fallback check)
-_DIRECT = os.environ.get("MOPT_CONV_IMPLICIT", "0") != "1"
+# direct convolution kernels for square inputs; the implicit GEMM (pgemm gathers) is the
+# fallback for the rest (scripts/conv_bench.py flips this to compare the two)
+_DIRECT = True
 
 
 def _call(name, *args):
@@ -431,3 +435,77 @@ def conv_bn_act(x, w, gamma, beta, running, P, stride, train, res=None, relu=Tru
     return bn_act(y, gamma, beta, running, P, train, res=res, relu=relu,
                   sums=stats[0] if stats is not None and stats[1] else None,
                   arena=arena if train else None, mailbox=bn_mailbox, res_sub2=res_sub2)
+
+
+# ------------------------------------------------------------------ classifier head
+def head_ref(h, fcw, fcb, labels, P, ncls):
+    """fp32 reference of the head: global average pool -> linear -> softmax cross-entropy.
+    h [P*B, H, W, C] -> (per-trial loss sums [P], #correct [P], logits [P, B, ncls])."""
+    B = h.shape[0] // P
+    feat = h.view(P, B, -1, h.shape[-1]).float().mean(2)                    # [P, B, C]
+    logits = torch.baddbmm(fcb.float()[:, None, :], feat, fcw.float())[..., :ncls]
+    lab = labels.view(P, B).long()
+    loss = torch.nn.functional.cross_entropy(logits.reshape(-1, ncls), lab.reshape(-1),
+                                             reduction="none").view(P, B).sum(1)
+    correct = (logits.argmax(-1) == lab).float().sum(1)
+    return loss, correct, logits
+
+
+class _Head(torch.autograd.Function):
+    """Fused pool + linear + cross-entropy (csrc/resnet_head.hip).  The forward computes the
+    gradients too (``scale`` = d loss_sum / d per-sample loss, e.g. 1 / B): dW and db go straight
+    into the flat gradient buffer (``gw``, ``gb``: direct gradients), dh is kept for backward,
+    which promises that only ``loss.sum()`` is differentiated."""
+
+    @staticmethod
+    def forward(ctx, h, fcw, fcb, labels, P, ncls, scale, gw, gb):
+        N = h.shape[0]
+        B, C = N // P, h.shape[-1]
+        HW = h.numel() // (N * C)
+        dev = h.device
+        loss = torch.empty(P, dtype=torch.float32, device=dev)
+        correct = torch.empty(P, dtype=torch.float32, device=dev)
+        part = torch.empty(_lib.get_lib().mopt_resnet_head_part_floats(P, B, C),
+                           dtype=torch.float32, device=dev)
+        dh = torch.empty_like(h)
+        _call("mopt_resnet_head", h.data_ptr(), fcw.data_ptr(), fcb.data_ptr(), labels.data_ptr(),
+              P, B, HW, C, ncls, float(scale), 1, part.data_ptr(), dh.data_ptr(), gw.data_ptr(),
+              gb.data_ptr(), loss.data_ptr(), correct.data_ptr(), _s(h))
+        ctx.save_for_backward(dh)
+        ctx.mark_non_differentiable(correct)
+        return loss, correct
+
+    @staticmethod
+    def backward(ctx, dloss, dcorrect):
+        (dh,) = ctx.saved_tensors
+        return dh, None, None, None, None, None, None, None, None
+
+
+def resnet_head(h, fcw, fcb, labels, P, ncls, train, scale=1.0):
+    """Per-trial loss sums and #correct of the classifier head over h [P*B, H, W, C] bf16 with
+    fcw [P, C, NP], fcb [P, NP] (NP = 16 padded logits, the first ``ncls`` real) and labels
+    [P*B] int64.  HIP: one fused kernel (+ a per-trial reduction); training writes dW / db
+    straight into ``fcw.grad`` / ``fcb.grad`` (direct gradients) with ``scale`` applied."""
+    if h.device.type != "cuda":
+        loss, correct, _ = head_ref(h, fcw, fcb, labels, P, ncls)
+        return loss, correct
+    N, C = h.shape[0], h.shape[-1]
+    if N % P or (N // P) % 16 or C % 8 or C > 64 or tuple(fcw.shape) != (P, C, 16) or \
+            tuple(fcb.shape) != (P, 16) or labels.dtype != torch.int64 or labels.numel() != N:
+        raise ValueError(f"resnet_head: h {tuple(h.shape)} fcw {tuple(fcw.shape)} fcb "
+                         f"{tuple(fcb.shape)} labels {tuple(labels.shape)} {labels.dtype} P {P}")
+    h = h.contiguous()
+    labels = labels.contiguous()
+    if train:
+        if fcw.grad is None or fcb.grad is None:
+            raise ValueError("resnet_head(train=True) writes into fcw.grad / fcb.grad")
+        return _Head.apply(h, fcw, fcb, labels, P, ncls, scale, fcw.grad, fcb.grad)
+    B, HW = N // P, h.numel() // (N * C)
+    loss = torch.empty(P, dtype=torch.float32, device=h.device)
+    correct = torch.empty(P, dtype=torch.float32, device=h.device)
+    part = torch.empty(_lib.get_lib().mopt_resnet_head_part_floats(P, B, C),
+                       dtype=torch.float32, device=h.device)
+    _call("mopt_resnet_head", h.data_ptr(), fcw.data_ptr(), fcb.data_ptr(), labels.data_ptr(), P,
+          B, HW, C, ncls, 1.0, 0, part.data_ptr(), None, None, None, loss.data_ptr(),
+          correct.data_ptr(), _s(h))
+    return loss, correct

@@ -32,15 +32,7 @@ constexpr int LS = kLdsStride;
 // workgroups share a CU.  dQ at 4 (126 VGPRs, was 104 + 40 AGPRs = 3) and dK/dV at 3 (156, was
 // 154 + 44 = 2) compile without spills and measured 110.9 -> 99.5 / 179.8 -> 157.7 us per call on
 // the 125M LM (profiles/round3.md); the forward spills below its 4 (124 registers), so it is left.
-#ifndef MOPT_ATTN_FWD_WAVES
-#define MOPT_ATTN_FWD_WAVES 0
-#endif
-#ifndef MOPT_ATTN_DQ_WAVES
-#define MOPT_ATTN_DQ_WAVES 4
-#endif
-#ifndef MOPT_ATTN_DKDV_WAVES
-#define MOPT_ATTN_DKDV_WAVES 3
-#endif
+constexpr int kAttnFwdWaves = 0, kAttnDqWaves = 4, kAttnDkdvWaves = 3;
 #define MOPT_WAVES_ATTR(n) __attribute__((amdgpu_waves_per_eu((n) > 0 ? (n) : 1)))
 
 // (position of this workgroup's sequence block within its head, head index bh) for a 1-D grid of
@@ -117,7 +109,7 @@ __device__ __forceinline__ void scores_T(const bf16_t* Ks, const bf16x8 (&qf)[2]
 }
 
 // Forward: O = softmax(QK^T * scale, causal) V.   grid (T/64, BH), 256 threads.
-__global__ __launch_bounds__(256) MOPT_WAVES_ATTR(MOPT_ATTN_FWD_WAVES) void attn_fwd_kernel(const bf16_t* __restrict__ Q,
+__global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnFwdWaves) void attn_fwd_kernel(const bf16_t* __restrict__ Q,
                                                        const bf16_t* __restrict__ K,
                                                        const bf16_t* __restrict__ V,
                                                        bf16_t* __restrict__ O,
@@ -227,7 +219,7 @@ __global__ __launch_bounds__(256) void attn_bwd_prep_kernel(const bf16_t* __rest
 }
 
 // dQ = scale * sum_k dS K, dS = P * (dP - Dsum), dP = dO V^T.   grid (T/64, BH).
-__global__ __launch_bounds__(256) MOPT_WAVES_ATTR(MOPT_ATTN_DQ_WAVES) void attn_bwd_dq_kernel(const bf16_t* __restrict__ Q,
+__global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnDqWaves) void attn_bwd_dq_kernel(const bf16_t* __restrict__ Q,
                                                           const bf16_t* __restrict__ K,
                                                           const bf16_t* __restrict__ V,
                                                           const bf16_t* __restrict__ dO,
@@ -303,7 +295,7 @@ __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(MOPT_ATTN_DQ_WAVES) void attn_
 // dV = sum_q P^T dO,  dK = scale * sum_q dS^T Q.   grid (T/64, BH); one 64-key block per WG.
 // Scores are computed un-transposed here (S = Q K^T, lane = one key) with the Q / dO rows fed in
 // the permuted order, so P^T and dS^T land in A-fragment order for the two accumulating MFMAs.
-__global__ __launch_bounds__(256) MOPT_WAVES_ATTR(MOPT_ATTN_DKDV_WAVES) void attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q,
+__global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnDkdvWaves) void attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q,
                                                             const bf16_t* __restrict__ K,
                                                             const bf16_t* __restrict__ V,
                                                             const bf16_t* __restrict__ dO,

@@ -322,10 +322,7 @@ __global__ __launch_bounds__(256) void pgemm_kernel(const GemmArgs g) {
 // Preconditions (checked on the host): M % BM == 0, N % BN == 0, K % 64 == 0 (per split), row
 // strides multiples of 8 elements, 16-byte aligned bases.
 // ----------------------------------------------------------------------------------------------
-#ifndef MOPT_GEMM_GROUP_M
-#define MOPT_GEMM_GROUP_M 8
-#endif
-constexpr int kGroupM = MOPT_GEMM_GROUP_M;
+constexpr int kGroupM = 8;   // row panels per tile group (4 / 16 measured slower, round 3)
 
 typedef __attribute__((address_space(3))) void lds_void;
 
@@ -537,120 +534,9 @@ __global__ __launch_bounds__(512) void pgemm_big_kernel(const GemmArgs g) {
   }
 }
 
-// Multi-stage variant of pgemm_big_kernel: BK = 32 images in NS LDS stages (NS x 32 KB for
-// 256 x 256), the fills running NS - 1 K-steps ahead of the MFMAs instead of one -- 1.5x (NS = 4)
-// / 2x (NS = 5) the time to cover HBM latency at the same tile and LDS budget.  The fill stream
-// is its own cursor over this workgroup's (tile, K-step) sequence, so it runs ahead across tile
-// boundaries; each K-step waits only for the fill of the NEXT step (vmcnt counts the fill groups
-// issued after it; vector memory operations retire in order, so epilogue stores in between only
-// make that wait stricter).
-template <int NIF>
-__device__ __forceinline__ void wait_fills_newer(int newer) {
-  if (newer >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NIF) : "memory");
-  else if (newer == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NIF) : "memory");
-  else if (newer == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NIF) : "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-template <bool TA, bool TB, int WM, int FM, int FN, int NS>
-__global__ __launch_bounds__(512) void pgemm_pipe_kernel(const GemmArgs g) {
-  constexpr int KD = 32;
-  constexpr int WN = 8 / WM;
-  constexpr int BM = WM * 16 * FM, BN = WN * 16 * FN;
-  static_assert(FN % 2 == 0, "the epilogue pairs n-fragments");
-  static_assert(NS >= 3 && NS <= 5, "wait_fills_newer covers up to 3 newer fill groups");
-  using IA = GImg<BM, !TA, KD>;
-  using IB = GImg<BN, TB, KD>;
-  constexpr int STAGE = IA::ELEMS + IB::ELEMS;
-  constexpr int NIF = IA::NI + IB::NI;               // fill instructions per wave per K-step
-  __shared__ __attribute__((aligned(1024))) bf16_t smem[NS * STAGE];
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int li = lane & 15, gq = lane >> 4, q = li >> 2, pp = li & 3;
-  const int wm = wave / WN, wn = wave % WN;
-  const int nk = g.K / KD;
-
-  auto decode = [&](int v, int& p, int& m0, int& n0) {
-    const int t = xcd_remap(v, g.nwg);
-    const int per = g.tiles_m * g.tiles_n;
-    p = t / per;
-    const int idx = t - p * per, span = kGroupM * g.tiles_n;
-    const int grp = idx / span, in = idx - grp * span;
-    const int gm = min(kGroupM, g.tiles_m - grp * kGroupM);
-    m0 = (grp * kGroupM + in % gm) * BM;
-    n0 = (in / gm) * BN;
-  };
-
-  // fill cursor
-  int fvb = blockIdx.x, fp, fm0, fn0, fkt = 0, nfill = 0;
-  bool fvalid = true;
-  decode(fvb, fp, fm0, fn0);
-  auto fill_next = [&]() {
-    if (!fvalid) return;
-    bf16_t* dst = smem + (nfill % NS) * STAGE;
-    IA::fill(g.a.ptr + fp * g.a.batch, g.a.ld, fm0, fkt * KD, dst, wave, lane);
-    IB::fill(g.b.ptr + fp * g.b.batch, g.b.ld, fn0, fkt * KD, dst + IA::ELEMS, wave, lane);
-    ++nfill;
-    if (++fkt == nk) {
-      fkt = 0;
-      fvb += (int)gridDim.x;
-      if (fvb < g.nwg) decode(fvb, fp, fm0, fn0);
-      else fvalid = false;
-    }
-  };
-#pragma unroll
-  for (int s = 0; s < NS - 1; ++s) fill_next();
-  wait_fills_newer<NIF>(nfill - 1);
-  __syncthreads();
-
-  int vb = blockIdx.x, p, m0, n0, f = 0;
-  decode(vb, p, m0, n0);
-  while (true) {
-    f32x4 acc[FM][FN];
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    for (int kt = 0; kt < nk; ++kt, ++f) {
-      fill_next();                                   // into the stage step f - 1 read
-      const bf16_t* cur = smem + (f % NS) * STAGE;
-      bf16x8 a[FM], b[FN];
-#pragma unroll
-      for (int i = 0; i < FM; ++i) a[i] = IA::frag(cur, wm * 16 * FM + 16 * i, 0, li, gq, q, pp);
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-        b[j] = IB::frag(cur + IA::ELEMS, wn * 16 * FN + 16 * j, 0, li, gq, q, pp);
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(b[j], a[i], acc[i][j]);
-      wait_fills_newer<NIF>(nfill - 2 - f);          // fill f + 1 has landed
-      __syncthreads();
-    }
-
-    // epilogue: as pgemm_big_kernel (transposed accumulators, permlane16 pairing, 64-B rows)
-    bf16_t* C = g.C + p * g.sC + (int64_t)(m0 + wm * 16 * FM + li) * g.ldc + n0 + wn * 16 * FN +
-                16 * (gq & 1) + 8 * (gq >> 1);
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-#pragma unroll
-      for (int j = 0; j < FN; j += 2) {
-        uint32_t x0 = pack2bf(acc[i][j][0], acc[i][j][1]);
-        uint32_t x1 = pack2bf(acc[i][j][2], acc[i][j][3]);
-        uint32_t y0 = pack2bf(acc[i][j + 1][0], acc[i][j + 1][1]);
-        uint32_t y1 = pack2bf(acc[i][j + 1][2], acc[i][j + 1][3]);
-        const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
-        const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
-        *(uint4*)(C + (int64_t)(16 * i) * g.ldc + 16 * j) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
-      }
-    }
-    vb += (int)gridDim.x;
-    if (vb >= g.nwg) break;
-    decode(vb, p, m0, n0);
-  }
-}
+// (A multi-stage variant -- BK = 32 images in 4-5 LDS stages, fills 3-4 K-steps ahead -- was
+// correct on every layout but 5-25 % slower than this 2-stage kernel on every LM shape; it was
+// removed in round 4, the A/B is in profiles/round3.md "LM GEMMs".)
 
 // sum of the split-K partials [splits][P][M][N] -> C[p][m][n * ldc] bf16
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part,
@@ -702,22 +588,6 @@ int launch_big(GemmArgs g, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-template <bool TA, bool TB, int WM, int FM, int FN, int NS>
-int launch_pipe(GemmArgs g, hipStream_t st) {
-  constexpr int BM = WM * 16 * FM, BN = (8 / WM) * 16 * FN;
-  if (g.M % BM || g.N % BN || g.K % 32 || g.K < 32 || g.splits != 1 || g.nin > 1)
-    return (int)hipErrorInvalidValue;
-  g.tiles_m = g.M / BM;
-  g.tiles_n = g.N / BN;
-  const int64_t nwg = (int64_t)g.P * g.tiles_m * g.tiles_n;
-  if (nwg <= 0 || nwg > 0x7FFFFFFF) return (int)hipErrorInvalidValue;
-  g.nwg = (int)nwg;
-  constexpr int kGrid = 256;                 // persistent, one workgroup per CU
-  const int grid = nwg < kGrid ? (int)nwg : kGrid;
-  hipLaunchKernelGGL((pgemm_pipe_kernel<TA, TB, WM, FM, FN, NS>), dim3(grid), dim3(512), 0, st, g);
-  return (int)hipGetLastError();
-}
-
 template <int KA, int KB, bool TA, bool TB>
 int dispatch_tile(const GemmArgs& g, int cfg, hipStream_t st) {
   if constexpr (KA == kDense && KB == kDense) {
@@ -725,9 +595,6 @@ int dispatch_tile(const GemmArgs& g, int cfg, hipStream_t st) {
       case 5: return launch_big<TA, TB, 2, 8, 4>(g, st);  // 256 x 256
       case 6: return launch_big<TA, TB, 4, 4, 4>(g, st);  // 256 x 128
       case 7: return launch_big<TA, TB, 2, 4, 4>(g, st);  // 128 x 256
-      case 8: return launch_pipe<TA, TB, 2, 8, 4, 4>(g, st);  // 256 x 256, BK 32, 4 stages
-      case 9: return launch_pipe<TA, TB, 2, 8, 4, 5>(g, st);  // 256 x 256, BK 32, 5 stages
-      case 10: return launch_pipe<TA, TB, 4, 4, 4, 5>(g, st); // 256 x 128, BK 32, 5 stages
       case 11: return launch_big<TA, TB, 4, 4, 6>(g, st);     // 256 x 192
       default: break;
     }

@@ -25,13 +25,17 @@ using namespace mopt;
 
 extern "C" {
 
+// Work lists are [n][2] int32 (trial-layer, tile), position 8 i + x = the i-th item of XCD x
+// (workgroups are dealt to the XCDs round-robin), built and cost-balanced on the host
+// (metaopt_amd/ops/population.py _xcd_schedule); (-1, *) entries are padding.
+//
 // One (trial, layer) of the population; 64 bytes, mirrored by metaopt_amd/ops/population.py.
 struct MlpTL {
   int32_t K;       // padded input features (multiple of 64)
   int32_t N;       // padded output features (multiple of 64)
   int32_t trial;   // population slot (index into the hyper-parameter table)
   int32_t n_real;  // real outputs (classes of the CE layer)
-  int64_t w_off;   // W [N][K] (layout: MOPT_W_STRIP below): offset into the parameter buffers
+  int64_t w_off;   // W [N][K] (k-strip-major, see w_row_stride): offset into the parameters
   int64_t b_off;   // bias [N]: offset into the f32 master / optimizer buffers
   int64_t x_off;   // layer input  [rows][K] bf16: offset into the x buffer of the launch
   int64_t y_off;   // layer output [rows][N] bf16: offset into act (forward) / grad (backward)
@@ -64,44 +68,26 @@ namespace {
 constexpr int BM = 128;  // rows (batch) per workgroup
 constexpr int BN = 64;   // output features per forward tile / per backward chunk
 constexpr int BK = 64;   // reduction step of the forward, width of a backward k-strip
-// LDS tile layout (A/B switch, -DMOPT_MLP_SWZ=0|1): 1 = 128-B rows with the row-XOR chunk
-// swizzle of common.h (bank-conflict free, scripts/lds_banks.py); 0 = rows padded to 72 bf16.
-#ifndef MOPT_MLP_SWZ
-#define MOPT_MLP_SWZ 0
-#endif
-#if MOPT_MLP_SWZ
-constexpr int TS = 64;
-#define TOFF(r, c) tile_off((r), (c))
-#define FOFF(r, c) ftile_off((r), (c))
-#else
+// LDS tiles: bf16 rows padded to 72 elements (144 B), f32 dW staging rows padded to 68.  (The
+// row-XOR swizzle of common.h, conflict-free by scripts/lds_banks.py, was measured slower in
+// round 3: its address math spilled the backward -- profiles/round3.md "MLP kernels: A/B".)
 constexpr int TS = kLdsStride;
 #define TOFF(r, c) ((r) * TS + (c))
 #define FOFF(r, c) ((r) * (BN + 4) + (c))
-#endif
 
-// Weight layout in HBM (A/B switch, -DMOPT_W_STRIP=0|1).  1 (default): k-strip-major
-// [K/64][N][64] -- W[n][k] at (k / 64) N 64 + n 64 + k % 64, so the backward's k-strip is one
-// contiguous N x 128-B block and every 64 x 64 tile the forward or the backward touches is 8 KB
-// contiguous (a micro-benchmark of the backward's three-array read-modify-write by 64 x 64 tiles
-// measured 5.4 TB/s contiguous vs 4.65 TB/s with 128-B rows K * 2 bytes apart:
-// scripts/dev/tile_layout_bench.*).  0: row-major [N][K].  Same element set, same offsets of
-// the bias and of the optimizer state (which share the layout); metaopt_amd/ops/population.py
-// asks the library (mopt_mlp_w_layout) to view the weights row-major.
-#ifndef MOPT_W_STRIP
-#define MOPT_W_STRIP 1
-#endif
-__device__ __forceinline__ int w_row_stride(int K) { return MOPT_W_STRIP ? BK : K; }
-__device__ __forceinline__ int w_kstep(int N) { return MOPT_W_STRIP ? N : 1; }
+// Weight layout in HBM: k-strip-major [K/64][N][64] -- W[n][k] at (k / 64) N 64 + n 64 + k % 64,
+// so the backward's k-strip is one contiguous N x 128-B block and every 64 x 64 tile the forward
+// or the backward touches is 8 KB contiguous (a micro-benchmark of the backward's three-array
+// read-modify-write by 64 x 64 tiles measured 5.4 TB/s contiguous vs 4.65 TB/s with 128-B rows
+// K * 2 bytes apart: scripts/dev/tile_layout_bench.*).  The bias and the optimizer state share
+// the layout; metaopt_amd/ops/population.py views the weights row-major through it.
+__device__ __forceinline__ int w_row_stride(int) { return BK; }
+__device__ __forceinline__ int w_kstep(int N) { return N; }
 // stored index e -> (n, k)
-__device__ __forceinline__ void w_coords(int64_t e, int N, int K, int& n, int& k) {
-  if (MOPT_W_STRIP) {
-    const int64_t strip = e / ((int64_t)N * BK), r = e - strip * (int64_t)N * BK;
-    n = (int)(r / BK);
-    k = (int)(strip * BK + (r % BK));
-  } else {
-    n = (int)(e / K);
-    k = (int)(e - (int64_t)n * K);
-  }
+__device__ __forceinline__ void w_coords(int64_t e, int N, int, int& n, int& k) {
+  const int64_t strip = e / ((int64_t)N * BK), r = e - strip * (int64_t)N * BK;
+  n = (int)(r / BK);
+  k = (int)(strip * BK + (r % BK));
 }
 
 // kStoreStats: one row block per trial -- store the trial's loss / #correct instead of
@@ -117,10 +103,12 @@ enum Opt { kSGD = 0, kAdamW = 1, kSGD16 = 2 };
 
 // ----------------------------------------------------------------------------------------------
 // Forward GEMM core: acc[i][j] = X[row0 + 32*wave + 16i .., :] . W[n0 + 16j .., :]^T over all K.
-// Register-staged pipelining (T14), two K-steps deep: two register sets alternate (the loop body
-// is one even and one odd K-step, so no register is copied and the counted vmcnt wait at each
-// step leaves the other set's six loads in flight).  With one step of look-ahead a K = 1024
-// strip was a chain of 16 exposed HBM round trips and the whole forward ran at ~2 TB/s.  Loads
+// Register-staged pipelining (T14), NSET (2) K-steps deep: the register sets rotate over an
+// unrolled loop of NSET K-steps (no register is copied; the counted vmcnt wait at each step
+// leaves the other sets' loads in flight).  With one step of look-ahead a K = 1024 strip was a
+// chain of 16 exposed HBM round trips (~2 TB/s); two steps reach ~3 TB/s.  Three sets (3 or 4
+// workgroups per CU) measured no faster (profiles/r4/kbench_fwd_v*.log): the forward is bound by
+// its LDS traffic (6 B of fragment reads per weight byte at 128 rows), not by look-ahead.  Loads
 // past the last K-step re-read the last tile (clamped address) instead of branching, so no
 // control flow sits around a load.
 // ----------------------------------------------------------------------------------------------
@@ -174,7 +162,7 @@ __device__ __forceinline__ void fwd_step(const bf16_t* As, const bf16_t* Bs, int
 }
 
 // W: the tile's first row (w_off + n0 * w_row_stride(K)); N: rows of the layer's weight matrix
-template <int TN>
+template <int TN, int NSET = 2>
 __device__ __forceinline__ void fwd_gemm(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                          int K, int N, bf16_t* As, bf16_t* Bs,
                                          f32x4 (&acc)[2][TN / 16]) {
@@ -201,26 +189,37 @@ __device__ __forceinline__ void fwd_gemm(const bf16_t* __restrict__ X, const bf1
   bf16_t* bs2 = Bs + TOFF(c2 >> 3, (c2 & 7) * 8);
   bf16_t* bs3 = Bs + TOFF(c3 >> 3, (c3 & 7) * 8);
   const int klast = K - BK;
-  uint4 p0, p1, p2, p3, pw0, pw1{}, pw1b{}, pw1c{};  // even K-steps
-  uint4 q0, q1, q2, q3, qw0, qw1{}, qw1b{}, qw1c{};  // odd K-steps
+  uint4 p0, p1, p2, p3, pw0, pw1{}, pw1b{}, pw1c{};  // K-steps 0, 3, 6, ...
+  uint4 q0, q1, q2, q3, qw0, qw1{}, qw1b{}, qw1c{};  // K-steps 1, 4, 7, ...
+  uint4 r0, r1, r2, r3, rw0, rw1{}, rw1b{}, rw1c{};  // K-steps 2, 5, 8, ...
   MOPT_FWD_LOAD(p0, p1, p2, p3, pw0, pw1, 0);
   MOPT_FWD_LOAD(q0, q1, q2, q3, qw0, qw1, min(BK, klast));
-  for (int k0 = 0;; k0 += 2 * BK) {
-    // even K-step: tile k0 from set p, which then fetches tile k0 + 2 BK
-    MOPT_FWD_STORE(p0, p1, p2, p3, pw0, pw1);
-    __syncthreads();
-    MOPT_FWD_LOAD(p0, p1, p2, p3, pw0, pw1, min(k0 + 2 * BK, klast));
-    fwd_step<TN>(As, Bs, wave, li, g, acc);
-    __syncthreads();
-    if (k0 + BK >= K) break;
-    // odd K-step: tile k0 + BK from set q, which then fetches tile k0 + 3 BK
-    MOPT_FWD_STORE(q0, q1, q2, q3, qw0, qw1);
-    __syncthreads();
-    MOPT_FWD_LOAD(q0, q1, q2, q3, qw0, qw1, min(k0 + 3 * BK, klast));
-    fwd_step<TN>(As, Bs, wave, li, g, acc);
-    __syncthreads();
-    if (k0 + 2 * BK >= K) break;
+  if (NSET == 3) MOPT_FWD_LOAD(r0, r1, r2, r3, rw0, rw1, min(2 * BK, klast));
+  // K-step from set S: its tile to LDS, then S fetches the tile NSET steps ahead
+#define MOPT_FWD_KSTEP(S, KNEXT)                                         \
+  MOPT_FWD_STORE(S##0, S##1, S##2, S##3, S##w0, S##w1);                  \
+  __syncthreads();                                                       \
+  MOPT_FWD_LOAD(S##0, S##1, S##2, S##3, S##w0, S##w1, min(KNEXT, klast)); \
+  fwd_step<TN>(As, Bs, wave, li, g, acc);                                \
+  __syncthreads();
+  if (NSET == 3) {
+    for (int k0 = 0;; k0 += 3 * BK) {
+      MOPT_FWD_KSTEP(p, k0 + 3 * BK)
+      if (k0 + BK >= K) break;
+      MOPT_FWD_KSTEP(q, k0 + 4 * BK)
+      if (k0 + 2 * BK >= K) break;
+      MOPT_FWD_KSTEP(r, k0 + 5 * BK)
+      if (k0 + 3 * BK >= K) break;
+    }
+  } else {
+    for (int k0 = 0;; k0 += 2 * BK) {
+      MOPT_FWD_KSTEP(p, k0 + 2 * BK)
+      if (k0 + BK >= K) break;
+      MOPT_FWD_KSTEP(q, k0 + 3 * BK)
+      if (k0 + 2 * BK >= K) break;
+    }
   }
+#undef MOPT_FWD_KSTEP
 }
 #undef MOPT_FWD_LOAD
 #undef MOPT_FWD_STORE
@@ -228,15 +227,16 @@ __device__ __forceinline__ void fwd_gemm(const bf16_t* __restrict__ X, const bf1
 // (Measured and rejected: an LDS-free variant loading every MFMA fragment -- 16 bytes of one
 // row of X or W per lane -- straight from global memory ran the forward 2.5x slower than the
 // LDS-staged tiles above; profiles/README.md.)
-template <int TN>
+template <int TN, int NSET = 2>
 __device__ __forceinline__ void fwd_core(const bf16_t* X, const bf16_t* W, int K, int N,
                                          bf16_t* As, bf16_t* Bs, f32x4 (&acc)[2][TN / 16]) {
-  fwd_gemm<TN>(X, W, K, N, As, Bs, acc);
+  fwd_gemm<TN, NSET>(X, W, K, N, As, Bs, acc);
 }
 
 // Y[rows, n0:n0+TN] = dropout(relu(X W^T + b)) for one (trial-layer, n-tile, 128-row block).
-template <int TN>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TN == 128 ? 3 : 4))) void mlp_fwd_kernel(const MlpTL* __restrict__ tls,
+// NSET register sets of look-ahead, WAVES waves per SIMD (workgroups per CU)
+template <int TN, int NSET, int WAVES>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) void mlp_fwd_kernel(const MlpTL* __restrict__ tls,
                                                       const int2* __restrict__ work, int n_work,
                                                       const bf16_t* __restrict__ xb,
                                                       const bf16_t* __restrict__ plo,
@@ -247,7 +247,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TN == 128 ?
   __shared__ __attribute__((aligned(16))) bf16_t smem[(BM + TN) * TS];
   bf16_t* As = smem;
   bf16_t* Bs = smem + BM * TS;
-  const int2 wi = work[xcd_remap(blockIdx.x, n_work)];
+  const int2 wi = work[blockIdx.x];   // XCD-balanced order built on the host (_xcd_schedule)
+  if (wi.x < 0) return;                // padding: a no-op workgroup
   const MlpTL tl = tls[wi.x];
   const int K = tl.K, N = tl.N, n0 = wi.y * TN, row0 = blockIdx.y * BM;
   if (row0 >= tl.rows) return;           // a smaller batch than the launch's: uniform exit
@@ -255,7 +256,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TN == 128 ?
   const bf16_t* W = p16 + tl.w_off + (size_t)n0 * w_row_stride(K);
 
   f32x4 acc[2][TN / 16];
-  fwd_core<TN>(X, W, K, N, As, Bs, acc);
+  fwd_core<TN, NSET>(X, W, K, N, As, Bs, acc);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, g = lane >> 4;
   const bf16_t* bias_hi = p16 + tl.b_off + n0;
@@ -316,7 +317,8 @@ __global__ __launch_bounds__(256) void mlp_fwd_ce_kernel(const MlpTL* __restrict
   bf16_t* Bs = As + BM * TS;
   float* Ls = (float*)smem_raw;
 
-  const int2 wi = work[xcd_remap(blockIdx.x, n_work)];
+  const int2 wi = work[blockIdx.x];   // XCD-balanced order built on the host (_xcd_schedule)
+  if (wi.x < 0) return;                // padding: a no-op workgroup
   const MlpTL tl = tls[wi.x];
   const int K = tl.K, N = tl.N, row0 = blockIdx.y * BM, C = tl.n_real;
   if (row0 >= tl.rows) return;           // a smaller batch than the launch's: uniform exit
@@ -409,21 +411,14 @@ __global__ __launch_bounds__(256) void mlp_fwd_ce_kernel(const MlpTL* __restrict
 // blocks (the X strip and dZ chunk of blocks 1.. restaged through the same LDS tiles), the
 // update, the bias over all rows.  Trials with fewer rows than the launch skip the extra blocks.
 //
-// LDS (MOPT_BWD_ALIAS=1, default): the f32 dW staging tile aliases the dZ chunk tile (one more
-// barrier per chunk), 47 KB per workgroup instead of 64.5 KB, so three workgroups fit a CU's
-// 160 KB; the variant without the prefetch register set (<= 168 VGPRs) then runs 3 waves per
-// SIMD.  The prefetch variant needs more VGPRs and stays at 2.
-#ifndef MOPT_BWD_ALIAS
-#define MOPT_BWD_ALIAS 1
-#endif
-// 16-byte optimizer-state accesses (2 rows x 8 k per thread) instead of 8-byte ones (4 x 4):
-// A/B switch, -DMOPT_BWD_V16=0|1
-#ifndef MOPT_BWD_V16
-#define MOPT_BWD_V16 1
-#endif
+// LDS: the f32 dW staging tile aliases the dZ chunk tile (one more barrier per chunk), 47 KB per
+// workgroup instead of 64.5 KB, so three workgroups fit a CU's 160 KB; the variant without the
+// prefetch register set (<= 168 VGPRs) then runs 3 waves per SIMD.  The prefetch variant needs
+// more VGPRs and stays at 2.  Optimizer state moves 16 bytes per lane (2 rows x 8 k per thread;
+// -1.7 % step time against 8-byte accesses, profiles/round3.md).
 constexpr int bwd_waves(int opt, bool pf, int mode) {
   // AdamW and the multi-row-block pass spill at 168 VGPRs: they keep 2 waves per SIMD
-  return (MOPT_BWD_ALIAS && !pf && opt != kAdamW && mode != 1) ? 3 : 2;
+  return (!pf && opt != kAdamW && mode != 1) ? 3 : 2;
 }
 template <int OPT, bool PF, int MODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
@@ -439,15 +434,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
   constexpr int DS = BN + 4;  // f32 row stride bound of the dW staging tile (FOFF)
   static_assert(BN * DS * 4 <= BM * TS * 2, "dW staging tile must fit the dZ tile");
   __shared__ __attribute__((aligned(16)))
-      bf16_t smem[(2 * BM + BN) * TS + 2 * 4 * BN + (MOPT_BWD_ALIAS ? 0 : 2 * BN * DS)];
+      bf16_t smem[(2 * BM + BN) * TS + 2 * 4 * BN];
   bf16_t* Xs = smem;
   bf16_t* Zs = smem + BM * TS;
   bf16_t* Ws = smem + 2 * BM * TS;
   float* red = (float*)(smem + (2 * BM + BN) * TS);  // [4][64] bias partial sums
   // [64 n][DS] dW of the current chunk
-  float* Dw = MOPT_BWD_ALIAS ? (float*)Zs : red + 4 * BN;
+  float* Dw = (float*)Zs;
 
-  const int2 wi = work[xcd_remap(blockIdx.x, n_work)];
+  const int2 wi = work[blockIdx.x];   // XCD-balanced order built on the host (_xcd_schedule)
+  if (wi.x < 0) return;                // padding: a no-op workgroup
   const MlpTL tl = tls[wi.x];
   const int K = tl.K, N = tl.N, k0 = wi.y * BK;
   const int R = MODE == 0 ? 1 : (int)(tl.rows / BM);       // the trial's row blocks
@@ -500,7 +496,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
   const int zo2 = ((tid + 512) >> 3) * N + (tid & 7) * 8, zo3 = ((tid + 768) >> 3) * N + (tid & 7) * 8;
   bf16_t* zs0 = Zs + TOFF(tid >> 3, (tid & 7) * 8);     // rows +32 i keep the swizzle
   const int WRS = w_row_stride(K);
-#if MOPT_BWD_V16
   // Optimizer-state layout: thread -> rows 32 i + tid / 8 (i < 2), 8 consecutive k at 8 (tid % 8):
   // every W / M (/ V) access is 16 bytes per lane and a wave-instruction moves 8 rows x 128 B
   // (1 KB) -- half the memory instructions of the 8-byte layout below.
@@ -548,64 +543,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     else { cm0 = nm0; cm1 = nm1; cm2 = nm2; cm3 = nm3; }                                         \
     if (OPT == kAdamW) { cv0 = nv0; cv1 = nv1; cv2 = nv2; cv3 = nv3; }                           \
   }
-#else
-  // Optimizer-state layout: thread -> rows 16i + tid/16 (i < 4), 4 consecutive k at 4 * (tid % 16):
-  // every wave-instruction moves 4 rows x 256 contiguous bytes of W/M (/V), full 128-B lines.
-  // (strip layout: the k-strip is one contiguous [N][64] block, rows 64 apart)
-  const size_t wo = (size_t)k0 * w_kstep(N) + (size_t)(tid >> 4) * WRS + 4 * (tid & 15);
-  // (zero-initialised: MODE 2 loads only the hi halves and dZ; the rest stays unused)
-  uint4 cz0{}, cz1{}, cz2{}, cz3{}, nz0{}, nz1{}, nz2{}, nz3{};
-  f32x4 cm0{}, cm1{}, cm2{}, cm3{}, cv0{}, cv1{}, cv2{}, cv3{};
-  f32x4 nm0{}, nm1{}, nm2{}, nm3{}, nv0{}, nv1{}, nv2{}, nv3{};
-  uint2 cwh0{}, cwh1{}, cwh2{}, cwh3{}, cwl0{}, cwl1{}, cwl2{}, cwl3{};   // master: hi, lo halves
-  uint2 nwh0{}, nwh1{}, nwh2{}, nwh3{}, nwl0{}, nwl1{}, nwl2{}, nwl3{};
-  uint2 ch0{}, ch1{}, ch2{}, ch3{}, nh0{}, nh1{}, nh2{}, nh3{};   // kSGD16 momentum (4 bf16)
-#define MOPT_BWD_LOAD(NC, P)                                                                     \
-  {                                                                                              \
-    const bf16_t* zc_ = dZ + (NC);                                                               \
-    P##z0 = *(const uint4*)(zc_ + zo0);                                                          \
-    P##z1 = *(const uint4*)(zc_ + zo1);                                                          \
-    P##z2 = *(const uint4*)(zc_ + zo2);                                                          \
-    P##z3 = *(const uint4*)(zc_ + zo3);                                                          \
-    const size_t ob = (size_t)(NC) * WRS + wo;                                                   \
-    P##wh0 = *(const uint2*)(W16 + ob);                                                          \
-    P##wh1 = *(const uint2*)(W16 + ob + 16 * WRS);                                                 \
-    P##wh2 = *(const uint2*)(W16 + ob + 32 * WRS);                                                 \
-    P##wh3 = *(const uint2*)(W16 + ob + 48 * WRS);                                                 \
-    if (MODE != 2) {                                                                             \
-    P##wl0 = *(const uint2*)(WLO + ob);                                                          \
-    P##wl1 = *(const uint2*)(WLO + ob + 16 * WRS);                                                 \
-    P##wl2 = *(const uint2*)(WLO + ob + 32 * WRS);                                                 \
-    P##wl3 = *(const uint2*)(WLO + ob + 48 * WRS);                                                 \
-    if (OPT == kSGD16) {                                                                         \
-      P##h0 = *(const uint2*)(M16 + ob);                                                         \
-      P##h1 = *(const uint2*)(M16 + ob + 16 * WRS);                                                \
-      P##h2 = *(const uint2*)(M16 + ob + 32 * WRS);                                                \
-      P##h3 = *(const uint2*)(M16 + ob + 48 * WRS);                                                \
-    } else {                                                                                     \
-      P##m0 = *(const f32x4*)(M32 + ob);                                                         \
-      P##m1 = *(const f32x4*)(M32 + ob + 16 * WRS);                                                \
-      P##m2 = *(const f32x4*)(M32 + ob + 32 * WRS);                                                \
-      P##m3 = *(const f32x4*)(M32 + ob + 48 * WRS);                                                \
-    }                                                                                            \
-    if (OPT == kAdamW) {                                                                         \
-      P##v0 = *(const f32x4*)(V32 + ob);                                                         \
-      P##v1 = *(const f32x4*)(V32 + ob + 16 * WRS);                                                \
-      P##v2 = *(const f32x4*)(V32 + ob + 32 * WRS);                                                \
-      P##v3 = *(const f32x4*)(V32 + ob + 48 * WRS);                                                \
-    }                                                                                            \
-    }                                                                                            \
-  }
-#define MOPT_BWD_ADVANCE()                                                                       \
-  {                                                                                              \
-    cz0 = nz0; cz1 = nz1; cz2 = nz2; cz3 = nz3;                                                  \
-    cwh0 = nwh0; cwh1 = nwh1; cwh2 = nwh2; cwh3 = nwh3;                                          \
-    cwl0 = nwl0; cwl1 = nwl1; cwl2 = nwl2; cwl3 = nwl3;                                          \
-    if (OPT == kSGD16) { ch0 = nh0; ch1 = nh1; ch2 = nh2; ch3 = nh3; }                           \
-    else { cm0 = nm0; cm1 = nm1; cm2 = nm2; cm3 = nm3; }                                         \
-    if (OPT == kAdamW) { cv0 = nv0; cv1 = nv1; cv2 = nv2; cv3 = nv3; }                           \
-  }
-#endif  // MOPT_BWD_V16
   MOPT_BWD_LOAD(0, c)
   for (int nc = 0; nc < N; nc += BN) {
     // ---- this chunk's operands -> LDS (dZ row-major; W^T image as bf16 for the dX MFMAs) ----
@@ -613,7 +550,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     *(uint4*)(zs0 + 32 * TS) = cz1;
     *(uint4*)(zs0 + 64 * TS) = cz2;
     *(uint4*)(zs0 + 96 * TS) = cz3;
-#if MOPT_BWD_V16
     // per thread: 2 rows x 8 k = 4 groups of 4 (row 0 k 0-3, row 0 k 4-7, row 1 k 0-3, 4-7)
     if (OPT == kSGD16) {
       cm0 = bf4_to_f32(make_uint2(ch0.x, ch0.y)); cm1 = bf4_to_f32(make_uint2(ch0.z, ch0.w));
@@ -635,25 +571,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
       for (int i = 0; i < 2; ++i) *(uint4*)(Ws + TOFF(32 * i + (tid >> 3), 8 * (tid & 7))) = wh[i];
     }
-#else
-    if (OPT == kSGD16) {
-      cm0 = bf4_to_f32(ch0); cm1 = bf4_to_f32(ch1); cm2 = bf4_to_f32(ch2); cm3 = bf4_to_f32(ch3);
-    }
-    const f32x4 w[4] = {join4(cwh0, cwl0), join4(cwh1, cwl1), join4(cwh2, cwl2),
-                        join4(cwh3, cwl3)};
-    const f32x4 m[4] = {cm0, cm1, cm2, cm3};
-    f32x4 v[4];
-    if (OPT == kAdamW) {
-      v[0] = cv0; v[1] = cv1; v[2] = cv2; v[3] = cv3;
-    }
-    const uint2 wh[4] = {cwh0, cwh1, cwh2, cwh3};
-    const bool more = nc + BN < N;
-    if (PF && more) MOPT_BWD_LOAD(nc + BN, n)
-    if (has_dx) {   // the bf16 working copy (hi) is the dX operand, as in the forward
-#pragma unroll
-      for (int i = 0; i < 4; ++i) *(uint2*)(Ws + TOFF(16 * i + (tid >> 4), 4 * (tid & 15))) = wh[i];
-    }
-#endif
     __syncthreads();
 
     // ---- dX[:, strip] += dZ[:, chunk] . W[chunk, strip] ----
@@ -738,27 +655,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     // ---- optimizer epilogue: dW^T C-fragments (register r of dw[t][u] = dW[n][k + r]) are
     //      restaged through LDS into the row-contiguous layout of W/M (/V) ----
     if (MODE != 2) {
-    if (MOPT_BWD_ALIAS) __syncthreads();   // every wave is done reading Zs (dX, dW, bias)
+    __syncthreads();   // every wave is done reading Zs (dX, dW, bias): Dw aliases it
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int u = 0; u < 2; ++u)
         *(f32x4*)(Dw + FOFF(32 * wn + 16 * u + li, 32 * wk + 16 * t + 4 * g)) = dw[t][u];
     __syncthreads();
-#if MOPT_BWD_V16
     uint2 ph{}, pl{}, pm{};   // the row's first group, stored with the second
-#endif
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-#if MOPT_BWD_V16
       // group i: row 32 (i / 2) + tid / 8, k 8 (tid % 8) + 4 (i % 2) .. + 3
       const int gr = 32 * (i >> 1) + (tid >> 3), gk = 8 * (tid & 7) + 4 * (i & 1);
       const f32x4 gv = *(const f32x4*)(Dw + FOFF(gr, gk));
       const size_t o = (size_t)nc * WRS + wo + (size_t)(32 * (i >> 1)) * WRS + 4 * (i & 1);
-#else
-      const f32x4 gv = *(const f32x4*)(Dw + FOFF(16 * i + (tid >> 4), 4 * (tid & 15)));
-      const size_t o = (size_t)nc * WRS + wo + (size_t)(16 * i) * WRS;
-#endif
       f32x4 wv = w[i], mv = m[i], vv;
       if (OPT == kAdamW) vv = v[i];
 #pragma unroll
@@ -779,7 +689,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
       }
       uint2 nh, nl;
       split4(wv, nh, nl);
-#if MOPT_BWD_V16
       // the two groups of a row (k 0-3, 4-7) leave as one 16-byte store per array
       if ((i & 1) == 0) {
         ph = nh;
@@ -794,12 +703,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
         }
       }
       if (OPT != kSGD16) *(f32x4*)(M32 + o) = mv;
-#else
-      *(uint2*)(W16 + o) = nh;
-      *(uint2*)(WLO + o) = nl;
-      if (OPT == kSGD16) *(uint2*)(M16 + o) = f32_to_bf4(mv);
-      else *(f32x4*)(M32 + o) = mv;
-#endif
       if (OPT == kAdamW) *(f32x4*)(V32 + o) = vv;
     }
 
@@ -903,9 +806,6 @@ __global__ __launch_bounds__(256) void mlp_init_kernel(const InitDesc* __restric
   }
 }
 
-// Backward chunk prefetch (PF) on/off: A/B switch of the fused backward, on by default
-// (mopt_mlp_set_bwd_prefetch; MOPT_BWD_PREFETCH=0 in metaopt_amd/ops/population.py).
-static int g_bwd_prefetch = 1;
 
 template <int OPT, bool PF, int MODE>
 static void launch_bwd(int n_work, int grid_y, hipStream_t stream, const void* tls,
@@ -926,7 +826,7 @@ static void launch_bwd_rows(int n_work, int n_rowblocks, hipStream_t stream, con
   if (n_rowblocks <= 1) {
     // AdamW's second register set (M and V in f32) does not fit next to the MFMA operands: the
     // prefetch variant spills (256 VGPRs + scratch), so AdamW always runs the plain one
-    if (g_bwd_prefetch && OPT != kAdamW)
+    if (OPT != kAdamW)
       launch_bwd<OPT, true, 0>(n_work, 1, stream, tls, work, xb, grad, plo, p16, m32, v32, hp,
                                flags);
     else
@@ -949,8 +849,8 @@ extern "C" {
 
 int mopt_abi_version() { return 11; }
 
-// weight layout of this build: 1 = k-strip-major [K/64][N][64], 0 = row-major [N][K]
-int mopt_mlp_w_layout() { return MOPT_W_STRIP; }
+// weight layout: 1 = k-strip-major [K/64][N][64] (the only layout)
+int mopt_mlp_w_layout() { return 1; }
 
 // 1 when this library is the bounds-checked variant (-DMOPT_BOUNDS_CHECK)
 int mopt_checked_build() { return MOPT_CHECKED_BUILD; }
@@ -965,27 +865,17 @@ int mopt_mlp_init(const void* descs, int n_desc, void* plo, void* p16, void* m32
   return (int)hipGetLastError();
 }
 
-// tile_n: output features per work item (64 or 32; the work list was built for it)
+// tile_n: output features per work item (64: the work list was built for it; 32 and 128 were
+// measured slower or neutral in round 3, profiles/round3.md "Forward tile width")
 int mopt_mlp_fwd(const void* tls, const void* work, int n_work, int n_rowblocks, const void* xb,
                  const void* plo, const void* p16, void* act, const void* hp, unsigned step,
                  int layer, int flags, int tile_n, void* stream) {
   if (n_work <= 0) return 0;
-  if (tile_n != 32 && tile_n != 64 && tile_n != 128) return (int)hipErrorInvalidValue;
-  if (tile_n == 128)
-    hipLaunchKernelGGL(mlp_fwd_kernel<128>, dim3(n_work, n_rowblocks), dim3(256), 0,
-                       (hipStream_t)stream, (const MlpTL*)tls, (const int2*)work, n_work,
-                       (const bf16_t*)xb, (const bf16_t*)plo, (const bf16_t*)p16, (bf16_t*)act,
-                       (const TrialHP*)hp, step, layer, flags);
-  else if (tile_n == 32)
-    hipLaunchKernelGGL(mlp_fwd_kernel<32>, dim3(n_work, n_rowblocks), dim3(256), 0,
-                       (hipStream_t)stream, (const MlpTL*)tls, (const int2*)work, n_work,
-                       (const bf16_t*)xb, (const bf16_t*)plo, (const bf16_t*)p16, (bf16_t*)act,
-                       (const TrialHP*)hp, step, layer, flags);
-  else
-    hipLaunchKernelGGL(mlp_fwd_kernel<64>, dim3(n_work, n_rowblocks), dim3(256), 0,
-                       (hipStream_t)stream, (const MlpTL*)tls, (const int2*)work, n_work,
-                       (const bf16_t*)xb, (const bf16_t*)plo, (const bf16_t*)p16, (bf16_t*)act,
-                       (const TrialHP*)hp, step, layer, flags);
+  if (tile_n != 64) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL((mlp_fwd_kernel<64, 2, 4>), dim3(n_work, n_rowblocks), dim3(256), 0,
+                     (hipStream_t)stream, (const MlpTL*)tls, (const int2*)work, n_work,
+                     (const bf16_t*)xb, (const bf16_t*)plo, (const bf16_t*)p16, (bf16_t*)act,
+                     (const TrialHP*)hp, step, layer, flags);
   return (int)hipGetLastError();
 }
 
@@ -1002,10 +892,6 @@ int mopt_mlp_fwd_ce(const void* tls, const void* work, int n_work, int n_rowbloc
   return (int)hipGetLastError();
 }
 
-int mopt_mlp_set_bwd_prefetch(int on) {
-  g_bwd_prefetch = on ? 1 : 0;
-  return 0;
-}
 
 int mopt_mlp_bwd(const void* tls, const void* work, int n_work, const void* xb, void* grad,
                  void* plo, void* p16, void* m32, void* v32, const void* hp, int opt, int flags,
@@ -1039,7 +925,7 @@ struct MlpStep {
   void *plo, *p16, *m32, *v32, *act, *grad, *hp, *loss, *correct;
   float inv_b;      // <= 0: each trial's mean over its own rows (MlpTL::rows)
   int32_t n_stats;  // entries of loss / correct (the population's capacity)
-  int32_t fwd_tn;   // hidden-layer forward tile width of the work lists (32 / 64)
+  int32_t fwd_tn;   // hidden-layer forward tile width of the work lists (64)
   int32_t pad;
 };
 

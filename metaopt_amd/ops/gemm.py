@@ -20,7 +20,6 @@ from __future__ import annotations
 
 import ctypes
 import math
-import os
 from typing import Optional
 
 import torch
@@ -44,17 +43,12 @@ _lib.register_signatures({
 # (any shape, ragged edges); 5-7: 8-wave direct-to-LDS kernel, one workgroup per CU, for shapes
 # the tile divides (M % BM == N % BN == K % 64 == 0)
 TILES = {0: (128, 128), 1: (128, 16), 2: (128, 32), 3: (64, 64), 4: (64, 128),
-         5: (256, 256), 6: (256, 128), 7: (128, 256),
-         8: (256, 256), 9: (256, 256), 10: (256, 128), 11: (256, 192)}
+         5: (256, 256), 6: (256, 128), 7: (128, 256), 11: (256, 192)}
 #: 256 x 192 (cfg 11): N = 768 outputs in 4 column panels, so the LM's N = 768 products fill
 #: whole waves of 256 CUs (512 tiles for M = 4096, 256 for M = 2048) where 256 x 256 leaves a
 #: 75 %-full last wave
 BIG_TILES = (5, 6, 7, 11)
-#: the multi-stage big-tile kernel (BK 32, 4 / 5 / 5 LDS stages, fills 3-4 K-steps ahead):
-#: cfg 8 / 9 = 256 x 256, 10 = 256 x 128.  ``MOPT_GEMM_PIPE=<8|9>`` makes the planner use it in
-#: place of cfg 5 (and 10 in place of 6) for A/B
-PIPE_TILES = (8, 9, 10)
-LARGE_TILES = BIG_TILES + PIPE_TILES
+LARGE_TILES = BIG_TILES
 NUM_CU = 256
 #: relative speed of the big tiles at equal occupancy of the chip; the 256 x 128 / 128 x 256 tiles
 #: lose more on long reductions (less reuse per loaded byte): profiles/gemm_r2.md
@@ -128,15 +122,7 @@ def _plan_big(P: int, M: int, N: int, K: int):
     if best is None or best[3] < 0.6:
         return None
     _, cfg, s, _ = best
-    return _PIPE_MAP.get(cfg, cfg) if s == 1 else cfg, s, K // s
-
-
-def _pipe_map():
-    v = os.environ.get("MOPT_GEMM_PIPE", "")
-    return {5: int(v), 6: 10} if v in ("8", "9") else {}
-
-
-_PIPE_MAP = _pipe_map()
+    return cfg, s, K // s
 
 
 def plan(P: int, M: int, N: int, K: int, cfg: Optional[int] = None,
@@ -253,15 +239,9 @@ def pgemm(a: torch.Tensor, b: torch.Tensor, ta: bool = False, tb: bool = False,
     return out
 
 
-#: every product runs on pgemm: the big-tile kernel is at parity with hipBLASLt on the LM's NN
-#: projections (profiles/gemm_r2.md).  ``MOPT_LIBRARY_NN=1`` sends the wide NN forwards
-#: (N >= 256) to ``torch.bmm`` instead, for A/B comparisons.
-LIBRARY_NN_MIN_N = 256 if os.environ.get("MOPT_LIBRARY_NN") == "1" else None
-
-
 def nn_forward(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    if LIBRARY_NN_MIN_N is not None and b.shape[2] >= LIBRARY_NN_MIN_N:
-        return torch.bmm(a, b)
+    """Every product runs on pgemm: the big-tile kernel is at or above hipBLASLt on the LM's NN
+    projections (profiles/gemm_r2.md, profiles/round3.md "LM GEMMs")."""
     return pgemm(a, b)
 
 

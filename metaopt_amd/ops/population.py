@@ -46,7 +46,7 @@ INIT_DTYPE = np.dtype([("w_off", "<i8"), ("b_off", "<i8"), ("K", "<i4"), ("N", "
 assert TL_DTYPE.itemsize == 64 and HP_DTYPE.itemsize == 32 and INIT_DTYPE.itemsize == 48
 
 TILE = 64
-FWD_TN = 64             # default hidden-layer forward tile width (MOPT_FWD_TN)
+FWD_TN = 64             # hidden-layer forward tile width (csrc/pop_mlp.hip mopt_mlp_fwd)
 MAX_ROWS = 64 * 128     # csrc/pop_mlp.hip mopt_mlp_bwd: at most 64 row blocks per launch
 FWD_RELU, FWD_DROPOUT, FWD_WRITE_GRAD, FWD_STORE_STATS, FWD_COUNT_STEP = 1, 2, 4, 8, 16
 BWD_HAS_DX, BWD_IN_DROPOUT, BWD_UPDATE_BIAS = 1, 2, 4
@@ -132,20 +132,76 @@ class StatsSnapshot:
         return self._host.numpy().reshape(4, self.capacity)
 
 
-def _lpt_order(cost: np.ndarray, n_xcd: int = 8) -> np.ndarray:
-    """Work-list permutation: longest-first within each XCD's share.
+N_XCD = 8
 
-    The kernels map block b to work item ``xcd_remap(b)`` (common.h): XCD x processes the
-    contiguous positions [base(x), base(x + 1)) in order, so one trial-layer's tiles share its
-    L2.  Sorting each share by descending cost (stably, so a trial-layer's equal-cost tiles stay
-    adjacent) runs the heavy ragged trials first instead of leaving them as the launch's tail."""
+
+def _xcd_schedule(trial: np.ndarray, cost: np.ndarray, n_xcd: int = N_XCD) -> np.ndarray:
+    """Work-list permutation that balances the launch over the XCDs.
+
+    The MLP kernels run work item ``blockIdx.x`` (csrc/pop_mlp.hip), and workgroups are dealt to
+    the XCDs round-robin (blocks b and b + 8 share one: speed only, never correctness), so
+    position ``8 i + x`` of the list is the ``i``-th item of XCD ``x``.  Items (given grouped by
+    trial) are assigned to XCDs by total cost, longest first: a whole trial to the least-loaded
+    XCD (its tiles share its operands in that XCD's L2), a trial heavier than half an XCD's share
+    in contiguous pieces of about a quarter share.  Each XCD's items then run longest first, and
+    the shorter XCD lists are padded with ``-1`` (a no-op workgroup).  The previous scheme, equal
+    item COUNTS per XCD, left one XCD with up to 1.5x the work of another (bwd0: the slowest
+    XCD at 122 % of the mean, scripts/dev/sched_sim.py).  Returns indices into the items, -1 =
+    padding."""
     n = len(cost)
-    if n <= n_xcd:
-        return np.arange(n)
-    q, r = divmod(n, n_xcd)
-    pos = np.arange(n)
-    share = np.where(pos < r * (q + 1), pos // (q + 1), r + (pos - r * (q + 1)) // max(q, 1))
-    return np.lexsort((-cost, share))
+    if n == 0:
+        return np.zeros(0, np.int64)
+    cost = np.asarray(cost, dtype=np.float64)
+    bounds = np.flatnonzero(np.r_[True, trial[1:] != trial[:-1], True])
+    groups = [(int(bounds[g]), int(bounds[g + 1])) for g in range(len(bounds) - 1)]
+    csum = np.r_[0.0, np.cumsum(cost)]
+    share = csum[-1] / n_xcd
+    pieces = []                      # (cost, start, stop)
+    for a, b in groups:
+        c = csum[b] - csum[a]
+        if c <= share / 2 or b - a == 1:
+            pieces.append((c, a, b))
+            continue
+        k = max(2, int(np.ceil(c / (share / 4))))
+        cuts = np.searchsorted(csum[a:b + 1] - csum[a], np.linspace(0, c, k + 1)[1:-1])
+        edges = [a] + sorted({a + int(x) for x in cuts if 0 < x < b - a}) + [b]
+        pieces += [(csum[e1] - csum[e0], e0, e1) for e0, e1 in zip(edges[:-1], edges[1:])]
+    pieces.sort(key=lambda t: (-t[0], t[1]))
+    load = np.zeros(n_xcd)
+    lists = [[] for _ in range(n_xcd)]
+    for c, a, b in pieces:
+        x = int(np.argmin(load))
+        load[x] += c
+        lists[x].extend(range(a, b))
+    width = max(len(l) for l in lists)
+    out = np.full((width, n_xcd), -1, dtype=np.int64)
+    for x, l in enumerate(lists):
+        if l:
+            idx = np.asarray(l, dtype=np.int64)
+            out[:len(l), x] = idx[np.argsort(-cost[idx], kind="stable")]
+    return out.reshape(-1)
+
+
+def _reschedule(w: np.ndarray, group_of: np.ndarray, g: int, L: int, tl: np.ndarray,
+                field: str) -> np.ndarray:
+    """The real items of work list ``w`` whose slot is in group ``g`` (``group_of[slot]``),
+    rescheduled over the XCDs (a trial's items kept in their order)."""
+    w = w[w[:, 0] >= 0]
+    w = w[group_of[w[:, 0] // L] == g]
+    w = w[np.lexsort((w[:, 1], w[:, 0]))]
+    return _work_list(w[:, 0], w[:, 1], tl[field][w[:, 0]])
+
+
+def _work_list(tl_index: np.ndarray, tile: np.ndarray, cost: np.ndarray) -> np.ndarray:
+    """[n, 2] int32 work list (trial-layer, tile) in :func:`_xcd_schedule` order; padding
+    entries are (-1, 0)."""
+    order = _xcd_schedule(tl_index, cost)
+    w = np.zeros((len(order), 2), np.int32)
+    w[:, 0] = -1
+    real = order >= 0
+    w[real, 0] = tl_index[order[real]]
+    w[real, 1] = tile[order[real]]
+    return w
 
 
 def _lib_sync_check() -> bool:
@@ -197,16 +253,11 @@ class PopulationMLP:
                 raise ValueError("the hip backend needs a GPU device")
             from . import _lib
             self._lib = _lib.get_lib()  # raises loudly: no silent fallback on a GPU box
-            # backward chunk prefetch (csrc/pop_mlp.hip PF): on unless MOPT_BWD_PREFETCH=0
-            self._lib.mopt_mlp_set_bwd_prefetch(int(os.environ.get("MOPT_BWD_PREFETCH", "1")))
         # HIP weight layout: k-strip-major [K/64][N][64] (csrc/pop_mlp.hip MOPT_W_STRIP) -- the
         # optimizer state shares it; layer_views() returns row-major copies
         self.w_strip = backend == "hip" and self._lib.mopt_mlp_w_layout() == 1
-        # output features per hidden-layer forward work item (csrc/pop_mlp.hip mlp_fwd_kernel
-        # TN): 32 gives the launches twice the workgroups (less of a tail at ~1.5 per slot)
-        self.fwd_tn = int(os.environ.get("MOPT_FWD_TN", str(FWD_TN)))
-        if self.fwd_tn not in (32, 64, 128):
-            raise ValueError("MOPT_FWD_TN must be 32, 64 or 128")
+        # output features per hidden-layer forward work item (csrc/pop_mlp.hip mlp_fwd_kernel TN)
+        self.fwd_tn = FWD_TN
         self.backend = backend
         # the population's trials are split into ``n_streams`` groups of equal cost whose train
         # steps run on their own HIP streams, unsynchronised between syncs: one group's
@@ -338,8 +389,6 @@ class PopulationMLP:
         return int(cfg.batch_size) or self.batch_size
 
     def _check_member(self, cfg: MemberConfig) -> None:
-        if self.fwd_tn == 128 and pad64(cfg.width) % 128:
-            raise ValueError("MOPT_FWD_TN=128 (experiment) needs widths padded to 128")
         if cfg.width > self.max_width or cfg.width < 1:
             raise ValueError(f"width {cfg.width} outside [1, {self.max_width}]")
         if not (0.0 <= cfg.dropout < 1.0):
@@ -745,10 +794,9 @@ class PopulationMLP:
                 tl["rows"][i] = used
                 tn = self.fwd_tn if l < L - 1 else TILE   # the loss layer: one 64-wide tile
                 nt, nk = N // tn, K // TILE
-                fo = _lpt_order(np.repeat(K, nt))     # a forward tile costs ~K
-                bo = _lpt_order(np.repeat(N, nk))     # a backward k-strip costs ~N
-                fwd.append(np.stack([np.repeat(i, nt)[fo], _ranges(nt)[fo]], 1).astype(np.int32))
-                bwd.append(np.stack([np.repeat(i, nk)[bo], _ranges(nk)[bo]], 1).astype(np.int32))
+                # a forward tile costs ~K, a backward k-strip ~N
+                fwd.append(_work_list(np.repeat(i, nt), _ranges(nt), np.repeat(K, nt)))
+                bwd.append(_work_list(np.repeat(i, nk), _ranges(nk), np.repeat(N, nk)))
         else:
             fwd = [np.zeros((0, 2), np.int32) for _ in range(L)]
             bwd = [np.zeros((0, 2), np.int32) for _ in range(L)]
@@ -796,6 +844,9 @@ class PopulationMLP:
             bad.append("trial / class fields out of range")
         for name, lists, per in (("fwd", fwd, "N"), ("bwd", bwd, "K")):
             for l, w in enumerate(lists):
+                if not len(w):
+                    continue
+                w = w[w[:, 0] != -1]          # padding entries (no-op workgroups)
                 if not len(w):
                     continue
                 idx = w[:, 0]
@@ -892,8 +943,8 @@ class PopulationMLP:
         parts = []
         keep = []
         for p in range(n):
-            fwd = [w[part_of[w[:, 0] // L] == p] for w in tb["fwd_np"]]
-            bwd = [w[part_of[w[:, 0] // L] == p] for w in tb["bwd_np"]]
+            fwd = [_reschedule(w, part_of, p, L, tb["tl_np"], "K") for w in tb["fwd_np"]]
+            bwd = [_reschedule(w, part_of, p, L, tb["tl_np"], "N") for w in tb["bwd_np"]]
             fwd_t = [upload(w, self.device) for w in fwd]
             bwd_t = [upload(w, self.device) for w in bwd]
             keep += fwd_t + bwd_t
@@ -936,9 +987,15 @@ class PopulationMLP:
             if x.shape != (self.batch_size, self.K0):
                 raise ValueError(f"x must be [{self.batch_size}, {self.K0}] (padded), got "
                                  f"{tuple(x.shape)}")
+            if y.shape != (self.batch_size,) or y.dtype != torch.int32:
+                raise ValueError(f"y must be [{self.batch_size}] int32, got {tuple(y.shape)} "
+                                 f"{y.dtype}")
             if not x.is_contiguous():
                 x = x.contiguous()
                 keep.append(x)
+            if not y.is_contiguous():
+                y = y.contiguous()
+                keep.append(y)
             xs[i], ys[i] = x.data_ptr(), y.data_ptr()
         self.hp["t"][self._active_np] += n
         from ._lib import check
@@ -956,6 +1013,9 @@ class PopulationMLP:
             stream = main if i == 0 else self._side_streams[i - 1]
             check(lib.mopt_mlp_steps(part["step_ptr"], xs.ctypes.data, ys.ctypes.data, n,
                                      stream.cuda_stream), "mlp_steps")
+            if i > 0:   # the temporaries are freed on return: not before the side stream read them
+                for t in keep:
+                    t.record_stream(stream)
 
     def _train_step_hip(self, x, y) -> None:
         from ._lib import check
@@ -1170,7 +1230,8 @@ class PopulationMLP:
         keep = np.zeros(self.capacity, dtype=bool)
         keep[list(subset)] = True
         out = dict(tb)
-        fwd = [w[keep[w[:, 0] // L]] for w in tb["fwd_np"]]
+        fwd = [_reschedule(w, keep.astype(np.int64), 1, L, tb["tl_np"], "K")
+               for w in tb["fwd_np"]]
         from ._lib import upload
         out["fwd"] = [upload(w, self.device) for w in fwd]
         out["n_fwd"] = [len(w) for w in fwd]

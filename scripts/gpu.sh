@@ -12,11 +12,12 @@
 #   timeline         bench.py with the GPU-event timeline (MOPT_GPU_TIMELINE=1)
 #   streams          bench.py at MOPT_STREAMS=1,2
 #   kbench           per-kernel MLP microbench             trace_bench  rocprofv3 kernel trace
-#   kbench_ab        the microbench per backward variant (MOPT_BWD_PREFETCH in $PFS, default "1 2")
+#   kbench_ab        the microbench per kernel variant (MOPT_FWD_VARIANT in $VARIANTS, default "0 1")
 #   kbench_rows      the microbench at 128 / 256 / 512 rows per step (multi-row-block kernels)
 #   pmc_kbench       PMC passes of the MLP kernels (fetch/write/MFMA/LDS, one pass each)
 #   lm resnet hyper  bench_configs.py of one config        trace_lm trace_resnet trace_hyper
 #   gemm conv        pgemm / direct-conv microbenches      gemm32  f32-operand (K11) GEMM plans
+#   c4copy           one config-5 member: slot <-> pool copies, packed C4 path, copy_member
 #   decide           rank-0 decide cost at simulated W=1,8 (host CPU of the box)
 #   rehearsal        bench.py --gpus 2 / 4 / 8 over gloo with ranks sharing the GPU
 set -e
@@ -51,12 +52,12 @@ for step in "$@"; do
                          "async_eta2:--asha-mode async --fidelity 2,16,2" "async_g4:--asha-mode async --fidelity 4,16,4"; do
                   $T 240 python bench.py --steps 43 --warmup 5 ${v#*:} > "$OUT/algo_${v%%:*}.json" 2> "$OUT/algo_${v%%:*}.err"; done ;;
     random)     $T 240 python bench.py --steps 20 --warmup 5 --algo random > "$OUT/bench_random.json" 2> "$OUT/bench_random.err" ;;
-    timeline)   MOPT_GPU_TIMELINE=1 $T 240 python bench.py --steps 20 --warmup 5 > "$OUT/bench_timeline.json" 2> "$OUT/bench_timeline.err" ;;
+    timeline)   MOPT_GPU_TIMELINE=1 $T 240 python bench.py --steps 20 --warmup 5 $BENCH_ARGS > "$OUT/bench_timeline$TAG.json" 2> "$OUT/bench_timeline$TAG.err" ;;
     streams)    for s in 1 2; do MOPT_STREAMS=$s $T 240 python bench.py --steps 20 --warmup 5 > "$OUT/bench_streams$s.json" 2> "$OUT/bench_streams$s.err"; done ;;
     kbench)     $T 200 python scripts/kernel_bench.py --momentum-dtype bf16 --out "$OUT/kbench.json" > "$OUT/kbench.log" 2>&1 ;;
-    kbench_ab)  for pf in ${PFS:-1 2}; do MOPT_BWD_PREFETCH=$pf $T 200 python scripts/kernel_bench.py --momentum-dtype bf16 --out "$OUT/kbench_pf$pf.json" > "$OUT/kbench_pf$pf.log" 2>&1; done ;;
+    kbench_ab)  for v in ${VARIANTS:-0 1}; do MOPT_FWD_VARIANT=$v $T 200 python scripts/kernel_bench.py --momentum-dtype bf16 --out "$OUT/kbench_v$v.json" > "$OUT/kbench_v$v.log" 2>&1; done ;;
     kbench_rows) for b in 128 256 512; do $T 200 python scripts/kernel_bench.py --momentum-dtype bf16 --batch $b --iters 20 --out "$OUT/kbench_b$b.json" > "$OUT/kbench_b$b.log" 2>&1; done ;;
-    trace_bench) prof trace_bench 300 -- python3 "$ROOT/bench.py" --steps 10 --warmup 3 ;;
+    trace_bench) prof trace_bench$TAG 300 -- python3 "$ROOT/bench.py" --steps 10 --warmup 3 $BENCH_ARGS ;;
     pmc_kbench)
       pmc pmc_fetch FETCH_SIZE
       pmc pmc_write WRITE_SIZE
@@ -71,6 +72,7 @@ for step in "$@"; do
     gemm)       $T 300 python scripts/gemm_bench.py --cfgs "${CFGS:-0,5,6,7}" --splits "${SPLITS:-}" --out "$OUT/gemm.json" > "$OUT/gemm.log" 2>&1 ;;
     gemm32)     $T 300 python scripts/gemm_f32_bench.py --out "$OUT/gemm32.json" > "$OUT/gemm32.log" 2>&1 ;;
     conv)       $T 200 python scripts/conv_bench.py --implicit --out "$OUT/conv_bench.json" > "$OUT/conv_bench.log" 2>&1 ;;
+    c4copy)     $T 200 python scripts/c4_copy_bench.py --out "$OUT/c4_copy.json" > "$OUT/c4_copy.log" 2>&1 ;;
     decide)     for w in 1 8; do WORLD=$w $T 300 python scripts/profile_decide.py > "$OUT/decide_world$w.log" 2>&1; done ;;
     rehearsal)  for n in 2 4 8; do $T 400 python bench.py --gpus $n --steps 10 --warmup 3 --population 64 > "$OUT/rehearsal_n$n.json" 2> "$OUT/rehearsal_n$n.err"; done ;;
     *) echo "unknown step $step" >&2; exit 2 ;;

@@ -14,6 +14,8 @@ def _run(*args, timeout=300):
     env = {k: v for k, v in os.environ.items()
            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
     env["OMP_NUM_THREADS"] = "2"
+    # a one-interval bottom rung: trials complete within these few intervals
+    args = (*args, "--fidelity", "1,4,4")
     proc = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args],
                           capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
     assert proc.returncode == 0, proc.stderr[-3000:]

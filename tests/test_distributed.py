@@ -134,7 +134,8 @@ def _pbt_worker(rank, world, port, q):
     sweep.ckpts[999] = pop.save_states([(0, sweep._free_ck.pop())])[0]
     assign = np.zeros((2 * 3 + 1, AS_COLS))
     assign[3 + 2] = (RESUME, 0, 64, 0.1, 0.9, 0, 0, 7, 16, 999, 0, 0)
-    got = sweep._exchange_checkpoints(assign)
+    got, direct = sweep._exchange_checkpoints(assign)
+    assert not direct                         # the MLP population packs its state
     c4 = None
     if rank == 1:
         c4 = (sorted(got), got[2]["t"], got[2]["p32"].shape[0])
@@ -166,6 +167,61 @@ def test_pbt_sweep_and_c4_copy_gloo_world2():
     n_trials, n_children, n_completed = parents
     assert n_trials == 18 and n_children == 12      # 6 members x 3 generations
     assert n_completed == 18 and fin0 and fin1
+
+
+def _c4_flat_worker(rank, world, port, q):
+    """C4 of a flat (CNN / LM) population: pool entry -> pool entry, no pack / unpack."""
+    comm = _init(rank, world, port)
+    import numpy as np
+    from metaopt_amd.io.experiment_builder import build_experiment
+    from metaopt_amd.models.resnet import PopulationResNet
+    from metaopt_amd.ops.population import MemberConfig
+    from metaopt_amd.storage.database import EphemeralDB
+    from metaopt_amd.storage.protocol import DocumentStorage
+    from metaopt_amd.worker.population_sweep import AS_COLS, RESUME, PopulationSweep
+    from metaopt_amd.worker.tasks import get
+    task = get("resnet20")
+    exp = None
+    if rank == 0:
+        exp = build_experiment("dist-c4-flat", priors=dict(task.priors),
+                               algorithms={"random": {"seed": 1}},
+                               storage=DocumentStorage(EphemeralDB()))
+    pop = PopulationResNet(3, batch_size=16, device="cpu", blocks_per_stage=1, image_size=16)
+    pop.set_member(0, MemberConfig(width=0, lr=0.05, momentum=0.9, seed=11 + rank))
+    pop.hp[0]["t"] = 5
+    sweep = PopulationSweep(pop, task, data=None, comm=comm, experiment=exp, sync_every=8,
+                            ckpt_capacity=4, pipelined=False)
+    free0 = len(sweep._free_ck)
+    if rank == 0:
+        sweep.ckpts[999] = pop.save_states([(0, sweep._free_ck.pop())])[0]
+    assign = np.zeros((2 * 3 + 1, AS_COLS))
+    assign[3 + 2] = (RESUME, 0, 0, 0.1, 0.9, 0, 0, 7, 16, 999, 0, 0)
+    states, metas = sweep._exchange_checkpoints(assign)
+    out = None
+    if rank == 1:
+        assert not states and sorted(metas) == [2]
+        pop.load_states([(2, metas[2])])
+        out = (metas[2]["t"], float(pop.slot_state(2)["p32"].double().sum()),
+               len(sweep._free_ck) == free0 - 1)
+    else:
+        out = (5, float(pop.slot_state(0)["p32"].double().sum()), True)
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+def test_c4_flat_population_pool_to_pool_gloo_world2():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_c4_flat_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert res[1][0] == res[0][0] == 5                  # step count travelled in the header
+    assert res[1][1] == res[0][1]                       # the member's weights, bit for bit
+    assert res[1][2]                                    # received into a pool entry
 
 
 # ------------------------------------------------------------------ launcher (no HIP before spawn)

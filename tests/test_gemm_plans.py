@@ -36,9 +36,8 @@ def test_plan_splits_short_grids_and_big_tiles_only_for_a_ragged_last_wave():
     # the other LM projections keep one K pass (the partials would cost more than the fill)
     for M, N, K in [(4096, 2304, 768), (768, 2304, 4096), (2048, 768, 4096), (768, 32000, 4096)]:
         assert plan(8, M, N, K)[1] == 1
-    # an explicit K-split is honoured on the big tiles, not on the pipelined ones
+    # an explicit K-split is honoured on the big tiles
     assert plan(8, 512, 512, 1024, 5, 4) == (5, 4, 256)
-    assert plan(8, 512, 512, 1024, 8, 2)[0] not in (5, 6, 7, 8, 9, 10)
     for c in TILES:
         bm, bn = TILES[c]
         assert bm % 16 == 0 and bn % 16 == 0

@@ -52,7 +52,7 @@ def test_big_tiles_every_layout(cfg, ta, tb):
 def test_big_tiles_persistent_and_strided_output(cfg):
     """More tiles than workgroups (the persistent loop carries the next tile's first K-step
     across the epilogue), a C written into a wider row stride, split-K (f32 partials of the big
-    tiles; the pipelined tiles fall back to a small tile)."""
+    tiles)."""
     A, B, a, b = _operands(2, 256, 256, 2048, True, False, seed=20 + cfg)
     _check(pgemm(a, b, ta=True, cfg=cfg, splits=4), A, B)
     wide = torch.zeros(2, 256, 384, dtype=torch.bfloat16, device=DEV)
@@ -136,15 +136,10 @@ def test_pbmm_autograd_and_grad_out():
     assert w.grad is buf           # written in place, never re-accumulated by autograd
 
 
-@pytest.mark.parametrize("library", [None, 256])
 @pytest.mark.parametrize("K,N", [(768, 2304), (768, 4096), (2048, 768), (768, 32000)])
-def test_nn_forward_lm_shapes(K, N, library, monkeypatch):
-    """The LM's NN projection forwards (``nn_forward``) on the big-tile kernel (default) and on
-    the library (``MOPT_LIBRARY_NN=1``; scripts/check_bmm.py found the library's *transposed*
-    batched GEMM wrong, this guards its NN form on these shapes)."""
-    from metaopt_amd.ops import gemm
+def test_nn_forward_lm_shapes(K, N):
+    """The LM's NN projection forwards (``nn_forward``) on the big-tile kernel."""
     from metaopt_amd.ops.gemm import nn_forward
-    monkeypatch.setattr(gemm, "LIBRARY_NN_MIN_N", library)
     P, M = 2, 1024
     g = torch.Generator(device=DEV).manual_seed(K + N)
     x = (torch.randn(P, M, K, device=DEV, generator=g) * 0.1).to(torch.bfloat16)

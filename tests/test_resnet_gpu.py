@@ -239,3 +239,35 @@ def test_one_launch_member_init():
     assert torch.equal(pop.p32[pop._slices(1)[0]], first)
     pop.set_member(1, MemberConfig(width=0, lr=0.05, momentum=0.9, seed=12))
     assert not torch.equal(pop.p32[pop._slices(1)[0]], first)
+
+
+@pytest.mark.parametrize("P,B,HW,C", [(3, 32, 64, 64), (2, 16, 16, 16), (4, 48, 4, 8)])
+def test_fused_head_matches_fp32_reference(P, B, HW, C):
+    """Pool + linear + cross-entropy fused kernel (csrc/resnet_head.hip) against the fp32
+    PyTorch head: loss sums, #correct, and the gradients of sum(loss) / B -- dh through
+    autograd, dW / db written straight into fc.w.grad / fc.b.grad."""
+    torch.manual_seed(P * 100 + C)
+    S = int(HW ** 0.5)
+    h = torch.relu(torch.randn(P * B, S, S, C, device=DEV)).to(torch.bfloat16)
+    h.requires_grad_(True)
+    fcw = (0.3 * torch.randn(P, C, 16, device=DEV)).to(torch.bfloat16).requires_grad_(True)
+    fcb = (0.1 * torch.randn(P, 16, device=DEV)).to(torch.bfloat16).requires_grad_(True)
+    fcw.grad = torch.full_like(fcw, 7.0)            # direct gradients: overwritten, not added
+    fcb.grad = torch.full_like(fcb, 7.0)
+    labels = torch.randint(0, 10, (P * B,), device=DEV, dtype=torch.int64)
+    loss, correct = cops.resnet_head(h, fcw, fcb, labels, P, 10, train=True, scale=1.0 / B)
+    loss.sum().backward()
+    hr = h.detach().float().requires_grad_(True)
+    wr = fcw.detach().float().requires_grad_(True)
+    br = fcb.detach().float().requires_grad_(True)
+    rl, rc, _ = cops.head_ref(hr, wr, br, labels, P, 10)
+    (rl.sum() / B).backward()
+    _close(loss, rl, 1e-4)
+    assert torch.equal(correct, rc)
+    _close(h.grad, hr.grad, 2e-2)
+    _close(fcw.grad, wr.grad, 2e-2)
+    _close(fcb.grad, br.grad, 2e-2)
+    ev_loss, ev_correct = cops.resnet_head(h.detach(), fcw.detach(), fcb.detach(), labels, P, 10,
+                                           train=False)
+    _close(ev_loss, rl, 1e-4)
+    assert torch.equal(ev_correct, rc)
