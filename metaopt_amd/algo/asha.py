@@ -218,7 +218,11 @@ class ASHA(BaseAlgorithm):
         return _id
 
     def observe(self, points, results):
-        for point, result in zip(points, results):
+        self.observe_objectives(points, [r["objective"] for r in results])
+
+    def observe_objectives(self, points, objectives):
+        """:meth:`observe` with bare objective values (the device sweep's fast path)."""
+        for point, objective in zip(points, objectives):
             _id = self.get_id(point)
             bracket = self.trial_info.get(_id)
             if bracket is None:
@@ -228,7 +232,7 @@ class ASHA(BaseAlgorithm):
                     raise ValueError(f"No bracket found for point {_id} with fidelity {fid}")
                 bracket = cands[0]
             try:
-                bracket.register(point, result["objective"], _id=_id)
+                bracket.register(point, objective, _id=_id)
             except IndexError:
                 log.warning("Point registered to wrong bracket (corrupted timestamps?).")
                 continue

@@ -62,12 +62,25 @@ class PrimaryAlgo(BaseAlgorithm):
         validated them) -- the device sweep observes thousands of points per sync."""
         if len(points) != len(results):
             raise ValueError("points and results differ in length")
+        if not check and self.transformed_space._is_identity():
+            self.algorithm.observe(points, results)
+            return
         tpoints = []
         for p in points:
             if check and p not in self.space:
                 raise ValueError(f"Point {p} is not contained in space {self.space}")
             tpoints.append(self.transformed_space.transform(p))
         self.algorithm.observe(tpoints, results)
+
+    def observe_objectives(self, points, objectives):
+        """:meth:`observe` of suggested points (``check=False``) with bare objective values --
+        the device sweep's path: no result dict per point when the algorithm takes floats."""
+        inner = getattr(self.algorithm, "observe_objectives", None)
+        if inner is None or not self.transformed_space._is_identity():
+            self.observe(points, [{"objective": o, "constraint": [], "gradient": None}
+                                  for o in objectives], check=False)
+            return
+        inner(points, objectives)
 
     def parent_of(self, point):
         """Point whose trained state ``point`` resumes from (PBT exploit, ASHA promotion), if the

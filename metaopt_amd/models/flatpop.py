@@ -6,8 +6,11 @@ parameter tensor is stacked over the population (``[P, ...]``) and lives in flat
 * ``p16`` -- bf16 working weights; the autograd leaves are views of it, and their ``.grad`` is
   pre-bound to views of the flat bf16 gradient ``g16`` (autograd accumulates in place, so the
   whole population's gradient is one contiguous buffer);
-* ``p32`` -- f32 master weights, ``m``/``v`` -- optimizer state; one fused kernel updates every
-  tensor of every trial with per-trial hyper-parameters (AdamW: K6, SGD-momentum: K5);
+* the f32 master weights -- on the GPU split (csrc/common.h): ``p16`` is their high half and
+  ``plo`` (int16) the low half, so the master costs 2 bytes beyond the working copy; on the CPU
+  reference backend a plain f32 ``p32`` -- and ``m``/``v``, the optimizer state; one fused
+  kernel updates every tensor of every trial with per-trial hyper-parameters (AdamW: K6,
+  SGD-momentum: K5; 22 bytes per parameter and step for AdamW with the bf16 first moment);
 * ``aux`` -- per-trial non-parameter state (e.g. BatchNorm running statistics), checkpointed
   with the weights.
 
@@ -33,7 +36,7 @@ from ..ops.population import MemberConfig, device_busy
 
 INIT_SEG_DTYPE = np.dtype([("p32", "<u8"), ("p16", "<u8"), ("m", "<u8"), ("v", "<u8"),
                            ("n", "<i8"), ("kind", "<i4"), ("val", "<f4"), ("seed", "<u4"),
-                           ("tag", "<u4"), ("m16", "<i4"), ("pad", "<i4")])
+                           ("tag", "<u4"), ("m16", "<i4"), ("split", "<i4")])
 assert INIT_SEG_DTYPE.itemsize == 64
 _CHUNK = 4096
 _CHUNK_DTYPE = np.dtype([("desc", "<i4"), ("pad", "<i4"), ("start", "<i8")])
@@ -68,7 +71,10 @@ class FlatPopulation:
             off += P * n
         self.n_flat = off
         dev = self.device
-        self.p32 = torch.zeros(off, dtype=torch.float32, device=dev)
+        # split master on the GPU (the fused optimizer joins / splits it in registers)
+        self.split = self.device.type == "cuda"
+        self.plo = torch.zeros(off, dtype=torch.int16, device=dev) if self.split else None
+        self.p32 = None if self.split else torch.zeros(off, dtype=torch.float32, device=dev)
         self.p16 = torch.zeros(off, dtype=torch.bfloat16, device=dev)
         self.g16 = torch.zeros(off, dtype=torch.bfloat16, device=dev)
         self.m = torch.zeros(off, dtype=self.moment_dtype if self.optimizer == "adamw"
@@ -175,7 +181,8 @@ class FlatPopulation:
         gen = torch.Generator(device=self.device)
         gen.manual_seed(int(cfg.seed) & 0x7FFFFFFF)
         for (name, shape, init_), sl in zip(self.specs, self._slices(slot)):
-            dst = self.p32[sl]
+            dst = self.p32[sl] if not self.split else torch.empty(
+                sl.stop - sl.start, dtype=torch.float32, device=self.device)
             kind = init_[0]
             if kind == "ones":
                 dst.fill_(1.0)
@@ -187,7 +194,7 @@ class FlatPopulation:
                 dst.normal_(0.0, (2.0 / init_[1]) ** 0.5, generator=gen)
             else:
                 raise ValueError(f"unknown init {init_}")
-            self.p16[sl] = dst.to(torch.bfloat16)
+            self._set_master_slice(sl, dst)
             self.m[sl].zero_()
             if self.v.numel():
                 self.v[sl].zero_()
@@ -205,9 +212,10 @@ class FlatPopulation:
         ``mopt_flat_init`` launch (csrc/copy_kernels.hip)."""
         segs = []
         m16 = self.m.dtype == torch.bfloat16
-        p32, p16, mm = self.p32.data_ptr(), self.p16.data_ptr(), self.m.data_ptr()
+        mbuf = self.master_buf
+        p32, p16, mm = mbuf.data_ptr(), self.p16.data_ptr(), self.m.data_ptr()
         v = self.v.data_ptr() if self.v.numel() else 0
-        e32, e16, em = self.p32.element_size(), self.p16.element_size(), self.m.element_size()
+        e32, e16, em = mbuf.element_size(), self.p16.element_size(), self.m.element_size()
         for i, ((name, shape, init_), (o, n)) in enumerate(zip(self.specs, self.segments)):
             start = o + slot * n
             kind = init_[0]
@@ -222,7 +230,8 @@ class FlatPopulation:
             else:
                 raise ValueError(f"unknown init {init_}")
             segs.append((p32 + start * e32, p16 + start * e16, mm + start * em,
-                         v + start * 4 if v else 0, n, k, val, seed, 0x3000 + i, int(m16), 0))
+                         v + start * 4 if v else 0, n, k, val, seed, 0x3000 + i, int(m16),
+                         int(self.split)))
         fills = self.aux_fill_specs()
         if fills is not None:
             a32 = self.aux.data_ptr()
@@ -292,7 +301,7 @@ class FlatPopulation:
         if isinstance(out, tuple):
             self.stats[P:2 * P].copy_(out[1].detach())
         with torch.no_grad():
-            self.opt.step(self.p32, self.p16, self.g16, self.m, self.v, self.opt_hp,
+            self.opt.step(self.master_buf, self.p16, self.g16, self.m, self.v, self.opt_hp,
                           hp_dev=hp_dev)
 
     def _graph_step(self, x, y):
@@ -309,7 +318,7 @@ class FlatPopulation:
         self._gx = x.detach().clone()
         self._gy = y.detach().clone()
         self._hp_dev = upload_bytes(self.opt_hp, self.device)
-        state = [self.p32, self.p16, self.m, self.v, self.aux, self.stats]
+        state = [self.master_buf, self.p16, self.m, self.v, self.aux, self.stats]
         backup = [t.clone() for t in state]
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
@@ -384,8 +393,40 @@ class FlatPopulation:
         return self.eval_result(self.stats_snapshot(), self.evaluate_async(x, y, slots))
 
     # ------------------------------------------------------------------ checkpoints
+    @property
+    def master_buf(self) -> torch.Tensor:
+        """The master weights' own buffer: f32, or the int16 low halves of the split master."""
+        return self.plo if self.split else self.p32
+
+    def _master_slice(self, sl) -> torch.Tensor:
+        """f32 master weights of flat range ``sl`` (a copy when split)."""
+        if self.split:
+            from ..ops.reference import join_f32
+            return join_f32(self.p16[sl], self.plo[sl])
+        return self.p32[sl]
+
+    def _set_master_slice(self, sl, values: torch.Tensor) -> None:
+        """Master weights (and the bf16 working copy) of flat range ``sl`` from f32 values."""
+        if self.split:
+            from ..ops.reference import split_f32
+            hi, lo = split_f32(values.to(self.device, torch.float32))
+            self.p16[sl] = hi
+            self.plo[sl] = lo
+        else:
+            self.p32[sl] = values
+            self.p16[sl] = self.p32[sl].to(torch.bfloat16)
+
+    def master_flat(self) -> torch.Tensor:
+        """Every master weight as one f32 tensor (a copy when split; tests and tools)."""
+        return self._master_slice(slice(0, self.n_flat))
+
+    @torch.no_grad()
+    def load_master_flat(self, values: torch.Tensor) -> None:
+        """Set every master weight (and the working copy) from an f32 tensor."""
+        self._set_master_slice(slice(0, self.n_flat), values)
+
     def _state_bufs(self):
-        return [self.p32, self.m] + ([self.v] if self.v.numel() else [])
+        return [self.master_buf, self.m] + ([self.v] if self.v.numel() else [])
 
     def used_params_for(self, width=None) -> int:
         return self.n_params
@@ -396,13 +437,17 @@ class FlatPopulation:
         self._ck_aux = torch.zeros(n, max(self.n_aux, 4), dtype=torch.float32, device=self.device)
 
     def _copy_items(self, slot, idx, to_pool: bool):
+        from ..ops.ckpt import Split
         items = []
         for j, buf in enumerate(self._state_bufs()):
             o = 0
             for sl in self._slices(slot):
                 n = sl.stop - sl.start
                 pool = self._ck[idx, j, o:o + n]
-                if to_pool:                      # (a bf16 moment widens to the f32 pool)
+                if j == 0 and self.split:        # the pool holds the joined f32 master
+                    part = Split(self.p16[sl], self.plo[sl])
+                    items.append((part, pool, None) if to_pool else (pool, None, part))
+                elif to_pool:                    # (a bf16 moment widens to the f32 pool)
                     items.append((buf[sl], pool, None))
                 elif buf.dtype == torch.bfloat16:   # ... and narrows back on load
                     items.append((pool, None, buf[sl]))
@@ -451,7 +496,8 @@ class FlatPopulation:
     def slot_state(self, slot: int) -> dict:
         cat = lambda buf: torch.cat([buf[sl] for sl in self._slices(slot)])  # noqa: E731
         st = {"config": self.members[slot].to_dict(), "t": int(self.hp[slot]["t"]),
-              "p32": cat(self.p32), "m32": cat(self.m).float(), "aux": self._aux_of(slot),
+              "p32": torch.cat([self._master_slice(sl) for sl in self._slices(slot)]),
+              "m32": cat(self.m).float(), "aux": self._aux_of(slot),
               "optimizer": self.optimizer}
         if self.v.numel():
             st["v32"] = cat(self.v)
@@ -462,11 +508,10 @@ class FlatPopulation:
         o = 0
         for sl in self._slices(slot):
             n = sl.stop - sl.start
-            self.p32[sl] = state["p32"][o:o + n]
+            self._set_master_slice(sl, state["p32"][o:o + n])
             self.m[sl] = state["m32"][o:o + n]
             if self.v.numel():
                 self.v[sl] = state["v32"][o:o + n]
-            self.p16[sl] = self.p32[sl].to(torch.bfloat16)
             o += n
         if "aux" in state and self.n_aux:
             self._set_aux(slot, state["aux"])

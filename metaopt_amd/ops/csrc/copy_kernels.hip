@@ -100,8 +100,8 @@ int mopt_multi_copy(const void* descs, const void* chunks, int n_chunks, void* s
 extern "C" {
 
 struct InitSeg {        // 64 bytes, mirrored by metaopt_amd/models/flatpop.py
-  float* p32;
-  bf16_t* p16;          // nullptr: no bf16 copy
+  float* p32;           // f32 master, or (split) its 16-bit low halves
+  bf16_t* p16;          // nullptr: no bf16 copy; split: the high halves
   void* m;              // nullptr: no first moment
   float* v;             // nullptr: no second moment
   int64_t n;            // multiple of 4
@@ -109,7 +109,7 @@ struct InitSeg {        // 64 bytes, mirrored by metaopt_amd/models/flatpop.py
   float val;
   uint32_t seed, tag;
   int32_t m16;          // m is bf16
-  int32_t pad;
+  int32_t split;        // split master (common.h split4): p16 = hi, p32 = lo
 };
 
 }  // extern "C"
@@ -133,8 +133,15 @@ __global__ __launch_bounds__(256) void flat_init_kernel(const InitSeg* __restric
     f32x4 v;
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] = d.kind == 1 ? d.val * normal_draw(key, e + r) : d.val;
-    *(f32x4*)(d.p32 + e) = v;
-    if (d.p16) *(uint2*)(d.p16 + e) = f32_to_bf4(v);
+    if (d.split) {           // p32 holds the 16-bit low halves of a split master
+      uint2 hi, lo;
+      split4(v, hi, lo);
+      *(uint2*)(d.p16 + e) = hi;
+      *(uint2*)((uint16_t*)d.p32 + e) = lo;
+    } else {
+      *(f32x4*)(d.p32 + e) = v;
+      if (d.p16) *(uint2*)(d.p16 + e) = f32_to_bf4(v);
+    }
     if (d.m) {
       if (d.m16) *(uint2*)((bf16_t*)d.m + e) = make_uint2(0u, 0u);
       else *(f32x4*)((float*)d.m + e) = f32x4{0.f, 0.f, 0.f, 0.f};

@@ -371,6 +371,76 @@ __global__ __launch_bounds__(256) void ce_fwd_bwd_kernel(bf16_t* __restrict__ lo
   }
 }
 
+// Register-resident variant for V <= 256 * 8 * NPT: the row is loaded once into NPT 16-byte
+// registers per thread, the softmax statistics and the gradient are computed from them -- one
+// read and one write of the logits instead of two reads and a write (the second pass of the
+// kernel above re-read a 64 KB row per workgroup with ~128 MB of rows in flight: from HBM).
+template <int NPT>
+__global__ __launch_bounds__(256) void ce_fwd_bwd_reg_kernel(bf16_t* __restrict__ logits,
+                                                             const int32_t* __restrict__ labels,
+                                                             float* __restrict__ loss_sum, int V,
+                                                             int rows_per_trial, float scale,
+                                                             int write_grad) {
+  __shared__ float red[8];
+  const int64_t row = blockIdx.x;
+  bf16_t* z = logits + row * V;
+  const int nc = V >> 3;
+  const int tid = threadIdx.x;
+  uint4 r[NPT];
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    const int c = tid + 256 * k;
+    r[k] = c < nc ? *(const uint4*)(z + 8 * c) : make_uint4(0, 0, 0, 0);
+  }
+  float m = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    if (tid + 256 * k < nc) {
+      float v[8];
+      unpack8(r[k], v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) m = fmaxf(m, v[e]);
+    }
+  }
+  const float wm = wave_max(m);
+  const int wave = tid >> 6, lane = tid & 63;
+  if (lane == 0) red[wave] = wm;
+  __syncthreads();
+  const float M = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    if (tid + 256 * k < nc) {
+      float v[8];
+      unpack8(r[k], v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += __expf(v[e] - M);
+    }
+  }
+  s = wave_sum(s);
+  if (lane == 0) red[4 + wave] = s;
+  __syncthreads();
+  const float S = red[4] + red[5] + red[6] + red[7];
+  int y = labels[row];
+  if (!MOPT_IN_RANGE(y, V, "ce_fwd_bwd label")) y = -1;  // checked build: no loss, no one-hot
+  if (tid == 0 && y >= 0) atomicAdd(loss_sum + row / rows_per_trial, M + __logf(S) - bf2f(z[y]));
+  if (!write_grad) return;
+  __syncthreads();   // z[y] read above before it is overwritten
+  const float inv = 1.f / S;
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    const int c = tid + 256 * k;
+    if (c < nc) {
+      float v[8];
+      unpack8(r[k], v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        v[e] = (__expf(v[e] - M) * inv - ((8 * c + e) == y ? 1.f : 0.f)) * scale;
+      *(uint4*)(z + 8 * c) = pack8(v);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------- embedding
 __global__ __launch_bounds__(256) void embed_fwd_kernel(const int32_t* __restrict__ tok,
                                                         const bf16_t* __restrict__ table,
@@ -531,42 +601,115 @@ __global__ __launch_bounds__(256) void grad_sumsq_kernel(const Segment* __restri
                                                          int n_chunks,
                                                          const bf16_t* __restrict__ g16,
                                                          float* __restrict__ sumsq) {
+  // The block's chunk descriptors are staged in LDS first (one dependent descriptor load per
+  // chunk kept the loop a latency chain: 0.42 ms for 268 MB, ~0.6 TB/s), then the data loads of
+  // four chunks are issued back to back.
   __shared__ float red[4];
+  __shared__ int64_t c_off[kSumChunks];
+  __shared__ int c_len[kSumChunks], c_trial[kSumChunks];
   const int c0 = blockIdx.x * kSumChunks;
-  const int c1 = min(c0 + kSumChunks, n_chunks);
+  const int n = min(kSumChunks, n_chunks - c0);
+  if ((int)threadIdx.x < n) {
+    const SegChunk ch = chunks[c0 + threadIdx.x];
+    const Segment sg = segs[ch.seg];
+    const int64_t end = min(ch.start + (int64_t)kAdamChunk, (int64_t)(ch.trial + 1) * sg.numel);
+    c_off[threadIdx.x] = sg.off + ch.start;
+    c_len[threadIdx.x] = (int)(end - ch.start);
+    c_trial[threadIdx.x] = ch.trial;
+  }
+  __syncthreads();
+  const int e0 = 8 * threadIdx.x;
   float acc = 0.f;
-  int trial = chunks[c0].trial;
-  for (int c = c0; c < c1; ++c) {
-    const SegChunk ch = chunks[c];
-    if (ch.trial != trial) {        // block-uniform: flush the finished trial's run
+  int trial = c_trial[0];
+  int j = 0;
+  while (j < n) {
+    // fast path: four chunks of the current trial, four independent 16-byte loads in flight
+    if (j + 4 <= n && c_trial[j] == trial && c_trial[j + 1] == trial &&
+        c_trial[j + 2] == trial && c_trial[j + 3] == trial) {
+      uint4 u[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        u[k] = e0 < c_len[j + k] ? *(const uint4*)(g16 + c_off[j + k] + e0) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float v[8];
+        unpack8(u[k], v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc += v[e] * v[e];
+      }
+      j += 4;
+      continue;
+    }
+    if (c_trial[j] != trial) {        // block-uniform: flush the finished trial's run
       const float tot = block_sum(acc, red);
       if (threadIdx.x == 0) atomicAdd(sumsq + trial, tot);
       acc = 0.f;
-      trial = ch.trial;
+      trial = c_trial[j];
     }
-    const Segment sg = segs[ch.seg];
-    const int64_t i = ch.start + 8 * threadIdx.x;
-    const int64_t end = min(ch.start + (int64_t)kAdamChunk, (int64_t)(ch.trial + 1) * sg.numel);
-    if (i < end) {
+    if (e0 < c_len[j]) {
       float v[8];
-      unpack8(*(const uint4*)(g16 + sg.off + i), v);
+      unpack8(*(const uint4*)(g16 + c_off[j] + e0), v);
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc += v[e] * v[e];
     }
+    ++j;
   }
   const float tot = block_sum(acc, red);
   if (threadIdx.x == 0) atomicAdd(sumsq + trial, tot);
 }
 
+// 8 consecutive master weights at element o: f32 (p32), or SPLIT, the (hi, lo) halves of
+// common.h -- hi is the bf16 working copy p16 itself, lo a 16-bit residual in ``master`` -- so
+// the master costs 2 bytes beyond the working copy instead of 4, and the update writes no
+// separately rounded copy.
+template <bool SPLIT>
+__device__ __forceinline__ void load_master8(const void* master, const bf16_t* p16, int64_t o,
+                                             float (&w)[8]) {
+  f32x4 a, b;
+  if constexpr (SPLIT) {
+    const uint4 hi = *(const uint4*)(p16 + o);
+    const uint4 lo = *(const uint4*)((const uint16_t*)master + o);
+    a = join4(make_uint2(hi.x, hi.y), make_uint2(lo.x, lo.y));
+    b = join4(make_uint2(hi.z, hi.w), make_uint2(lo.z, lo.w));
+  } else {
+    a = *(const f32x4*)((const float*)master + o);
+    b = *(const f32x4*)((const float*)master + o + 4);
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    w[e] = a[e];
+    w[4 + e] = b[e];
+  }
+}
+
+template <bool SPLIT>
+__device__ __forceinline__ void store_master8(void* master, bf16_t* p16, int64_t o,
+                                              const float (&w)[8]) {
+  const f32x4 a{w[0], w[1], w[2], w[3]}, b{w[4], w[5], w[6], w[7]};
+  if constexpr (SPLIT) {
+    uint2 ha, la, hb, lb;
+    split4(a, ha, la);
+    split4(b, hb, lb);
+    *(uint4*)(p16 + o) = make_uint4(ha.x, ha.y, hb.x, hb.y);
+    *(uint4*)((uint16_t*)master + o) = make_uint4(la.x, la.y, lb.x, lb.y);
+  } else {
+    *(f32x4*)((float*)master + o) = a;
+    *(f32x4*)((float*)master + o + 4) = b;
+    *(uint4*)(p16 + o) = pack8(w);
+  }
+}
+
 // M16: the first moment is kept in bf16 (RNE after each update; the update itself uses the f32
-// value) -- 4 of the 28 bytes per parameter the step moves.  The second moment stays f32: with
-// b2 = 0.999 its per-step change (0.1 %) is below bf16 resolution and would stall.
-template <bool M16>
+// value).  The second moment stays f32: with b2 = 0.999 its per-step change (0.1 %) is below
+// bf16 resolution and would stall.  Bytes per parameter and step: gradient 2, master 4 (SPLIT:
+// hi + lo, of which hi is the working copy) or 4 + the 2 of the rewritten bf16 copy, first
+// moment 2 x 2 (M16), second moment 2 x 4 -- 22 with M16 + SPLIT, 24 with M16 alone.
+template <bool M16, bool SPLIT>
 __global__ __launch_bounds__(256) void adamw_multi_kernel(const Segment* __restrict__ segs,
                                                           const SegChunk* __restrict__ chunks,
                                                           const LmHP* __restrict__ hp,
                                                           const float* __restrict__ sumsq,
-                                                          float* __restrict__ p32,
+                                                          void* __restrict__ master,
                                                           bf16_t* __restrict__ p16,
                                                           const bf16_t* __restrict__ g16,
                                                           void* __restrict__ mbuf,
@@ -587,9 +730,9 @@ __global__ __launch_bounds__(256) void adamw_multi_kernel(const Segment* __restr
   const float bc1 = 1.f - __powf(h.b1, tf), bc2 = 1.f - __powf(h.b2, tf);
   const float step = h.lr / bc1, rbc2 = rsqrtf(bc2);
   const int64_t o = sg.off + i;
-  float gv[8];
+  float gv[8], we[8];
   unpack8(*(const uint4*)(g16 + o), gv);
-  const f32x4 w0 = *(const f32x4*)(p32 + o), w1 = *(const f32x4*)(p32 + o + 4);
+  load_master8<SPLIT>(master, p16, o, we);
   f32x4 m0, m1;
   if constexpr (M16) {
     const uint4 mv = *(const uint4*)((const bf16_t*)mbuf + o);
@@ -600,7 +743,6 @@ __global__ __launch_bounds__(256) void adamw_multi_kernel(const Segment* __restr
     m1 = *(const f32x4*)((const float*)mbuf + o + 4);
   }
   const f32x4 v0 = *(const f32x4*)(v32 + o), v1 = *(const f32x4*)(v32 + o + 4);
-  float we[8] = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
   float me[8] = {m0[0], m0[1], m0[2], m0[3], m1[0], m1[1], m1[2], m1[3]};
   float ve[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
 #pragma unroll
@@ -611,8 +753,7 @@ __global__ __launch_bounds__(256) void adamw_multi_kernel(const Segment* __restr
     ve[e] = h.b2 * ve[e] + (1.f - h.b2) * gr * gr;
     we[e] -= step * me[e] / (sqrtf(ve[e]) * rbc2 + h.eps);
   }
-  *(f32x4*)(p32 + o) = f32x4{we[0], we[1], we[2], we[3]};
-  *(f32x4*)(p32 + o + 4) = f32x4{we[4], we[5], we[6], we[7]};
+  store_master8<SPLIT>(master, p16, o, we);
   if constexpr (M16) {
     *(uint4*)((bf16_t*)mbuf + o) = pack8(me);
   } else {
@@ -621,16 +762,16 @@ __global__ __launch_bounds__(256) void adamw_multi_kernel(const Segment* __restr
   }
   *(f32x4*)(v32 + o) = f32x4{ve[0], ve[1], ve[2], ve[3]};
   *(f32x4*)(v32 + o + 4) = f32x4{ve[4], ve[5], ve[6], ve[7]};
-  *(uint4*)(p16 + o) = pack8(we);
 }
 
 // SGD with momentum (PyTorch convention: m = mu m + (g + wd w); w -= lr m), per-trial lr /
 // momentum (LmHP.b1) / wd, optional per-trial grad-norm clipping (north-star kernel K5).
+template <bool SPLIT>
 __global__ __launch_bounds__(256) void sgd_multi_kernel(const Segment* __restrict__ segs,
                                                         const SegChunk* __restrict__ chunks,
                                                         const LmHP* __restrict__ hp,
                                                         const float* __restrict__ sumsq,
-                                                        float* __restrict__ p32,
+                                                        void* __restrict__ master,
                                                         bf16_t* __restrict__ p16,
                                                         const bf16_t* __restrict__ g16,
                                                         float* __restrict__ m32) {
@@ -646,22 +787,19 @@ __global__ __launch_bounds__(256) void sgd_multi_kernel(const Segment* __restric
     if (nrm > h.max_norm) clip = h.max_norm / (nrm + 1e-6f);
   }
   const int64_t o = sg.off + i;
-  float gv[8];
+  float gv[8], we[8];
   unpack8(*(const uint4*)(g16 + o), gv);
-  const f32x4 w0 = *(const f32x4*)(p32 + o), w1 = *(const f32x4*)(p32 + o + 4);
+  load_master8<SPLIT>(master, p16, o, we);
   const f32x4 m0 = *(const f32x4*)(m32 + o), m1 = *(const f32x4*)(m32 + o + 4);
-  float we[8] = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
   float me[8] = {m0[0], m0[1], m0[2], m0[3], m1[0], m1[1], m1[2], m1[3]};
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     me[e] = h.b1 * me[e] + gv[e] * clip + h.wd * we[e];
     we[e] -= h.lr * me[e];
   }
-  *(f32x4*)(p32 + o) = f32x4{we[0], we[1], we[2], we[3]};
-  *(f32x4*)(p32 + o + 4) = f32x4{we[4], we[5], we[6], we[7]};
+  store_master8<SPLIT>(master, p16, o, we);
   *(f32x4*)(m32 + o) = f32x4{me[0], me[1], me[2], me[3]};
   *(f32x4*)(m32 + o + 4) = f32x4{me[4], me[5], me[6], me[7]};
-  *(uint4*)(p16 + o) = pack8(we);
 }
 
 inline dim3 grid1(int64_t n) { return dim3((unsigned)((n + 255) / 256)); }
@@ -761,9 +899,14 @@ int mopt_swiglu_bwd(const void* gu, const void* dh, void* dgu, int64_t rows, int
 int mopt_ce_fwd_bwd(void* logits, const void* labels, void* loss_sum, int rows, int V,
                     int rows_per_trial, float scale, int write_grad, void* stream) {
   if (V % 8) return 1;
-  hipLaunchKernelGGL(ce_fwd_bwd_kernel, dim3(rows), dim3(256), 0, (hipStream_t)stream,
-                     (bf16_t*)logits, (const int32_t*)labels, (float*)loss_sum, V, rows_per_trial,
-                     scale, write_grad);
+  if (V <= 256 * 8 * 16)    // the row fits 16 registers of 16 bytes per thread
+    hipLaunchKernelGGL(ce_fwd_bwd_reg_kernel<16>, dim3(rows), dim3(256), 0, (hipStream_t)stream,
+                       (bf16_t*)logits, (const int32_t*)labels, (float*)loss_sum, V,
+                       rows_per_trial, scale, write_grad);
+  else
+    hipLaunchKernelGGL(ce_fwd_bwd_kernel, dim3(rows), dim3(256), 0, (hipStream_t)stream,
+                       (bf16_t*)logits, (const int32_t*)labels, (float*)loss_sum, V,
+                       rows_per_trial, scale, write_grad);
   return (int)hipGetLastError();
 }
 
@@ -822,9 +965,10 @@ int mopt_cast_bf16(const void* src, void* dst, int64_t n, void* stream) {
 }
 
 // m16: the first moment buffer is bf16 (else f32)
+// master: f32 master weights, or (split) the 16-bit low halves whose high halves are p16
 int mopt_adamw_multi(const void* segs, const void* chunks, int n_chunks, const void* hp,
-                     void* sumsq, void* p32, void* p16, const void* g16, void* m, void* v32,
-                     int P, int clip, int m16, void* stream) {
+                     void* sumsq, void* master, void* p16, const void* g16, void* m, void* v32,
+                     int P, int clip, int m16, int split, void* stream) {
   if (n_chunks <= 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   if (clip) {
@@ -833,16 +977,17 @@ int mopt_adamw_multi(const void* segs, const void* chunks, int n_chunks, const v
                        dim3(256), 0, st, (const Segment*)segs, (const SegChunk*)chunks, n_chunks,
                        (const bf16_t*)g16, (float*)sumsq);
   }
-  hipLaunchKernelGGL((m16 ? adamw_multi_kernel<true> : adamw_multi_kernel<false>), dim3(n_chunks),
-                     dim3(256), 0, st, (const Segment*)segs, (const SegChunk*)chunks,
-                     (const LmHP*)hp, (const float*)sumsq, (float*)p32, (bf16_t*)p16,
-                     (const bf16_t*)g16, m, (float*)v32);
+  auto kern = m16 ? (split ? adamw_multi_kernel<true, true> : adamw_multi_kernel<true, false>)
+                  : (split ? adamw_multi_kernel<false, true> : adamw_multi_kernel<false, false>);
+  hipLaunchKernelGGL(kern, dim3(n_chunks), dim3(256), 0, st, (const Segment*)segs,
+                     (const SegChunk*)chunks, (const LmHP*)hp, (const float*)sumsq, master,
+                     (bf16_t*)p16, (const bf16_t*)g16, m, (float*)v32);
   return (int)hipGetLastError();
 }
 
 int mopt_sgd_multi(const void* segs, const void* chunks, int n_chunks, const void* hp,
-                   void* sumsq, void* p32, void* p16, const void* g16, void* m32, int P, int clip,
-                   void* stream) {
+                   void* sumsq, void* master, void* p16, const void* g16, void* m32, int P,
+                   int clip, int split, void* stream) {
   if (n_chunks <= 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   if (clip) {
@@ -851,9 +996,10 @@ int mopt_sgd_multi(const void* segs, const void* chunks, int n_chunks, const voi
                        dim3(256), 0, st, (const Segment*)segs, (const SegChunk*)chunks, n_chunks,
                        (const bf16_t*)g16, (float*)sumsq);
   }
-  hipLaunchKernelGGL(sgd_multi_kernel, dim3(n_chunks), dim3(256), 0, st, (const Segment*)segs,
-                     (const SegChunk*)chunks, (const LmHP*)hp, (const float*)sumsq, (float*)p32,
-                     (bf16_t*)p16, (const bf16_t*)g16, (float*)m32);
+  hipLaunchKernelGGL((split ? sgd_multi_kernel<true> : sgd_multi_kernel<false>), dim3(n_chunks),
+                     dim3(256), 0, st, (const Segment*)segs, (const SegChunk*)chunks,
+                     (const LmHP*)hp, (const float*)sumsq, master, (bf16_t*)p16,
+                     (const bf16_t*)g16, (float*)m32);
   return (int)hipGetLastError();
 }
 

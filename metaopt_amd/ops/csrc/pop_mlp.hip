@@ -224,6 +224,10 @@ __device__ __forceinline__ void fwd_gemm(const bf16_t* __restrict__ X, const bf1
 #undef MOPT_FWD_LOAD
 #undef MOPT_FWD_STORE
 
+// (Measured and rejected, round 4: X fragments loaded straight from global memory into the
+// A operands with only W staged through LDS -- 40 instead of 72 KB of LDS traffic per K-step --
+// ran fwd0 at 58.7 vs 48.5 us: each lane's 16-byte row pieces coalesce into 64-byte segments;
+// profiles/round4.md.)
 // (Measured and rejected: an LDS-free variant loading every MFMA fragment -- 16 bytes of one
 // row of X or W per lane -- straight from global memory ran the forward 2.5x slower than the
 // LDS-staged tiles above; profiles/README.md.)
@@ -847,7 +851,7 @@ static void launch_bwd_rows(int n_work, int n_rowblocks, hipStream_t stream, con
 // ------------------------------------------------------------------------------------------------
 extern "C" {
 
-int mopt_abi_version() { return 11; }
+int mopt_abi_version() { return 12; }
 
 // weight layout: 1 = k-strip-major [K/64][N][64] (the only layout)
 int mopt_mlp_w_layout() { return 1; }

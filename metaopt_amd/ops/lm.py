@@ -43,10 +43,9 @@ _lib.register_signatures({
                        c_int),
     "mopt_cast_bf16": ([c_void_p, c_void_p, c_int64, c_void_p], c_int),
     "mopt_embed_bwd_sorted": ([c_void_p] * 4 + [c_int64, c_int, c_void_p], c_int),
-    "mopt_adamw_multi": ([c_void_p, c_void_p, c_int] + [c_void_p] * 7 + [c_int, c_int, c_int,
-                                                                         c_void_p],
+    "mopt_adamw_multi": ([c_void_p, c_void_p, c_int] + [c_void_p] * 7 + [c_int] * 4 + [c_void_p],
                          c_int),
-    "mopt_sgd_multi": ([c_void_p, c_void_p, c_int] + [c_void_p] * 6 + [c_int, c_int, c_void_p],
+    "mopt_sgd_multi": ([c_void_p, c_void_p, c_int] + [c_void_p] * 6 + [c_int] * 3 + [c_void_p],
                        c_int),
 })
 
@@ -477,26 +476,35 @@ class FlatOptimizer:
             self._chunks = _lib.upload_bytes(chunks, self.device)
             self._sumsq = torch.zeros(P, dtype=torch.float32, device=self.device)
 
-    def step(self, p32, p16, g16, m, v, hp: np.ndarray, hp_dev=None):
-        """``hp_dev``: the hyper-parameters already on the device (graph replay); else ``hp`` is
-        uploaded."""
+    def step(self, master, p16, g16, m, v, hp: np.ndarray, hp_dev=None):
+        """``master``: the f32 master weights, or (int16) the low halves of a split master whose
+        high halves are the bf16 working copy ``p16`` (csrc/common.h split4).  ``hp_dev``: the
+        hyper-parameters already on the device (graph replay); else ``hp`` is uploaded."""
         clip = int(bool((hp["max_norm"] > 0).any()))
+        split = master.dtype == torch.int16
         if self.device.type == "cuda":
             if hp_dev is None:
                 hp_dev = _lib.upload_bytes(hp, self.device)
             if self.kind == "adamw":
                 _call("mopt_adamw_multi", _p(self._segs), _p(self._chunks), self.n_chunks,
-                      _p(hp_dev), _p(self._sumsq), _p(p32), _p(p16), _p(g16), _p(m), _p(v),
-                      self.P, clip, int(m.dtype == torch.bfloat16), _lib.stream_ptr(self.device))
+                      _p(hp_dev), _p(self._sumsq), _p(master), _p(p16), _p(g16), _p(m), _p(v),
+                      self.P, clip, int(m.dtype == torch.bfloat16), int(split),
+                      _lib.stream_ptr(self.device))
             else:
                 _call("mopt_sgd_multi", _p(self._segs), _p(self._chunks), self.n_chunks,
-                      _p(hp_dev), _p(self._sumsq), _p(p32), _p(p16), _p(g16), _p(m), self.P,
-                      clip, _lib.stream_ptr(self.device))
+                      _p(hp_dev), _p(self._sumsq), _p(master), _p(p16), _p(g16), _p(m), self.P,
+                      clip, int(split), _lib.stream_ptr(self.device))
             return
+        from .reference import join_f32, split_f32
+        p32 = join_f32(p16, master) if split else master
         if self.kind == "adamw":
             adamw_flat_ref(self.segments, self.P, p32, p16, g16, m, v, hp)
         else:
             sgd_flat_ref(self.segments, self.P, p32, p16, g16, m, hp)
+        if split:
+            hi, lo = split_f32(p32)
+            p16.copy_(hi)
+            master.copy_(lo)
 
 
 FlatAdamW = FlatOptimizer

@@ -253,7 +253,7 @@ class PopulationMLP:
                 raise ValueError("the hip backend needs a GPU device")
             from . import _lib
             self._lib = _lib.get_lib()  # raises loudly: no silent fallback on a GPU box
-        # HIP weight layout: k-strip-major [K/64][N][64] (csrc/pop_mlp.hip MOPT_W_STRIP) -- the
+        # HIP weight layout: k-strip-major [K/64][N][64] (csrc/pop_mlp.hip w_row_stride) -- the
         # optimizer state shares it; layer_views() returns row-major copies
         self.w_strip = backend == "hip" and self._lib.mopt_mlp_w_layout() == 1
         # output features per hidden-layer forward work item (csrc/pop_mlp.hip mlp_fwd_kernel TN)

@@ -140,7 +140,12 @@ def _flatten_query(query: dict, prefix: str = "") -> List[tuple]:
 def match(doc: dict, query: Optional[dict]) -> bool:
     if not query:
         return True
-    for key, op, val in _flatten_query(query):
+    return _match_flat(doc, _flatten_query(query))
+
+
+def _match_flat(doc: dict, flat: List[tuple]) -> bool:
+    """:func:`match` against an already flattened query (scans flatten it once)."""
+    for key, op, val in flat:
         cur = _get_path(doc, key)
         if op == "$eq":
             if cur is _MISSING or cur != val:
@@ -520,8 +525,11 @@ class _Collection:
                                   key=lambda d: self._order(d))
                 else:
                     docs = [d for i, d in self.docs.items() if i in cands]
-                return [d for d in docs if match(d, query)]
-        return [d for d in self.docs.values() if match(d, query)]
+                flat = _flatten_query(query)
+                return [d for d in docs if _match_flat(d, flat)]
+            flat = _flatten_query(query)
+            return [d for d in self.docs.values() if _match_flat(d, flat)]
+        return list(self.docs.values())
 
     def _order(self, doc):
         if not hasattr(self, "_pos") or len(self._pos) != len(self.docs):
@@ -549,14 +557,47 @@ class _Collection:
         del self.docs[_hashable(doc["_id"])]
 
     def insert_owned(self, docs) -> int:
-        """Bulk insert of documents the caller hands over (no defensive copy)."""
+        """Bulk insert of documents the caller hands over (no defensive copy).
+
+        Indexes over top-level fields only (every index the storage creates) are maintained
+        inline -- one dict lookup per indexed field instead of the dotted-path machinery of
+        :meth:`_register`: this is the write path of a device sweep's thousands of trials per
+        second (worker/writer.py)."""
+        uniq = [(fields, values) for fields, unique, values in self.indexes.values() if unique]
+        hashed = list(self.hash_index.items())
+        if any("." in f for fields, _ in uniq for f in fields) or \
+                any("." in f for f, _ in hashed):
+            for d in docs:
+                if "_id" not in d:
+                    self.insert(d)
+                    continue
+                self._check_unique(d)
+                self.docs[_hashable(d["_id"])] = d
+                self._register(d)
+            return len(docs)
+        store, atomic = self.docs, _ATOMIC
         for d in docs:
             if "_id" not in d:
                 self.insert(d)
                 continue
-            self._check_unique(d)
-            self.docs[_hashable(d["_id"])] = d
-            self._register(d)
+            keys = []
+            for fields, values in uniq:
+                k = tuple(v if type(v := d.get(f)) in atomic else _hashable(v) for f in fields)
+                if k in values:
+                    raise DuplicateKeyError(f"Duplicate key error: fields={fields} value={k}")
+                keys.append(k)
+            hid = _hashable(d["_id"])
+            store[hid] = d
+            for (_, values), k in zip(uniq, keys):
+                values.add(k)
+            for f, hidx in hashed:
+                v = d.get(f)
+                hv = v if type(v) in atomic else self._hval(d, f)
+                ids = hidx.get(hv)
+                if ids is None:
+                    hidx[hv] = {hid}
+                else:
+                    ids.add(hid)
         return len(docs)
 
     def set_fields_by_id(self, items, owned: bool = False) -> int:
@@ -640,6 +681,11 @@ class EphemeralDB(AbstractDB):
     def insert_owned(self, collection_name, docs) -> int:
         """Insert documents the caller will never touch again (no copy): bulk writers."""
         return self._col(collection_name).insert_owned(list(docs))
+
+    def read_owned(self, collection_name, query=None) -> List[dict]:
+        """:meth:`read` without the defensive copies: the stored documents themselves, for a
+        caller that only serialises them (the writer child's final hand-back)."""
+        return list(self._col(collection_name).find_iter(query))
 
     def set_fields_by_id(self, collection_name, items, owned: bool = False) -> int:
         """Bulk compare-and-swap field updates by ``_id`` (see ``_Collection``)."""

@@ -452,7 +452,7 @@ class PopulationSweep:
     def _decide(self, gathered: np.ndarray) -> np.ndarray:
         W, P = self.comm.world_size, self.pop.capacity
         assign = np.zeros((W * P + 1, AS_COLS), dtype=np.float64)
-        done_pts, done_res = [], []
+        done_pts = []
         now = datetime.datetime.utcnow()
         max_b = self._max_budget()
         # rows with nothing to report (a member still training, no result) are skipped in
@@ -461,58 +461,70 @@ class PopulationSweep:
         leaving = (cur >= 0) & ((gathered[:, 3] > 0) | (gathered[:, 1] >= gathered[:, 2]))
         free = np.flatnonzero((cur < 0) | leaving).tolist()
         events = np.flatnonzero(leaving | (gathered[:, 4] >= 0))
+        assign[np.flatnonzero(leaving), 0] = CLEAR
         rows = gathered[events].tolist()   # python floats: ~10x cheaper to index than numpy
+        # (hot loop: thousands of rows per sync at 8 ranks -- bound methods and constants local)
+        trials, key_info = self.trials, self.key_info
+        put_result = self._writer.put_update_spec
+        hist_append = self.history.append
+        mirror_save, index_ckpt = self._mirror_save, self._index_ckpt
+        done_obj = []
+        pts_append, obj_append = done_pts.append, done_obj.append
+        wall, rstep, trial_events = time.time(), self._result_step, self.trial_events
+        best = self.best[0]
+        completed = 0
         for row, g, left in zip(events.tolist(), rows, leaving[events].tolist()):
-            rank = row // P
             # 1) the slot's current member: leaves when it reached its budget or diverged; the
             #    owner checkpoints it (below the top budget) -- mirrored here in FIFO order
             if left:
                 key, budget = int(g[0]), int(g[2])
-                bad = g[3] > 0
-                assign[row, 0] = CLEAR
-                if not bad and budget < max_b:
-                    self._mirror_save(rank, key)
-                if bad and key in self.trials:
-                    self.key_info.pop(key, None)
-                    self.broken += 1
-                    self._set_status(self.trials.pop(key), "broken")
+                if g[3] > 0:
+                    if key in trials:
+                        key_info.pop(key, None)
+                        self.broken += 1
+                        self._set_status(trials.pop(key), "broken")
+                elif budget < max_b:
+                    mirror_save(row // P, key)
             # 2) the result of the member that finished in this slot (this sync or, pipelined,
             #    the previous one)
             rkey = int(g[4])
             if rkey < 0:
                 continue
-            doc = self.trials.pop(rkey, None)
-            info = self.key_info.pop(rkey, None)
+            doc = trials.pop(rkey, None)
+            info = key_info.pop(rkey, None)
             if doc is None:
                 continue
             params, pkey, point, budget = info
             if g[8] > 0:
                 self.broken += 1
                 self._set_status(doc, "broken")
-                if self.trial_events:
+                if trial_events:
                     self.events.emit("trial", id=doc[0], status="broken", objective=None,
                                      budget=None)
                 continue
-            vl, va, tl = g[6], g[7], g[5]
-            self._writer.put_update_spec(doc[0], (vl, va, tl, now, doc[1]), was="reserved")
-            self.completed += 1
-            if self.trial_events:
+            vl = g[6]
+            put_result(doc[0], (vl, g[7], g[5], now, doc[1]), "reserved")
+            completed += 1
+            if trial_events:
                 self.events.emit("trial", id=doc[0], status="completed", objective=vl,
                                  budget=budget)
-            self.history.append((time.time(), rkey, vl, budget, self._result_step))
-            if vl < self.best[0]:
+            hist_append((wall, rkey, vl, budget, rstep))
+            if vl < best:
+                best = vl
                 self.best = (vl, dict(params))
-            done_pts.append(point)
-            done_res.append({"objective": vl, "constraint": [], "gradient": None})
+            pts_append(point)
+            obj_append(vl)
             if budget < max_b:
-                self._index_ckpt(pkey, rank, rkey, budget, doc[0])
+                index_ckpt(pkey, row // P, rkey, budget, doc[0])
+        self.completed += completed
         t0 = time.perf_counter()
         if done_pts:
             if isinstance(self.algorithm, PrimaryAlgo):
                 # the points came out of this algorithm's suggest(), validated there
-                self.algorithm.observe(done_pts, done_res, check=False)
+                self.algorithm.observe_objectives(done_pts, done_obj)
             else:
-                self.algorithm.observe(done_pts, done_res)
+                self.algorithm.observe(done_pts, [{"objective": o, "constraint": [],
+                                                   "gradient": None} for o in done_obj])
         t1 = time.perf_counter()
         self._heartbeat()
         self._fill(free, assign)

@@ -18,8 +18,11 @@ Both build documents from specs with one :class:`DocBuilder` (the Trial schema o
 from __future__ import annotations
 
 import collections
+import ctypes
 import logging
+import mmap
 import multiprocessing as mp
+import os
 import threading
 import time
 from typing import Optional
@@ -108,28 +111,52 @@ class WriteBehind:
                 self._apply_batch(self._take())
         self.busy_s += time.perf_counter() - t0
 
-    def _take(self):
-        """Next unit of work: a run of <= 256 registrations (one bulk insert) or of updates
-        (one bulk compare-and-swap)."""
-        first = self._held.popleft()
-        item = [first]
-        while self._held and len(item) < 256 and self._held[0][0] == first[0]:
-            item.append(self._held.popleft())
-        return item
+    def _take(self, limit: int = 256):
+        """Next unit of work: up to ``limit`` queued writes, in order."""
+        held = self._held
+        n = min(limit, len(held))
+        return [held.popleft() for _ in range(n)]
 
     def _apply_batch(self, held):
-        if held[0][0] == "register":
-            docs = [h[1] if type(h[1]) is dict else self.builder.doc(h[1]) for h in held]
-            if not self._call("register_trial_docs", docs, owned=True):
-                for d in docs:            # a bulk insert hit a duplicate: insert one by one
-                    self._call("register_trial_docs", [dict(d)])
+        """Apply a unit: one bulk insert of its registrations and one bulk compare-and-swap of
+        its updates.  An update of a trial registered in the same unit (a result that arrived
+        while the registration still waited, the usual case in a lagging writer child) is merged
+        into the document before it is inserted -- one write instead of two.  The updates of
+        trials registered earlier go first: an update queued before its trial's registration
+        must not see the document (it would not have, applied in order).  A registration that
+        hits the unique index (a replay after a writer failover) is skipped and the updates
+        merged into it are applied to the stored document instead, as they would have been."""
+        b = self.builder
+        docs: dict = {}
+        merged: dict = {}
+        updates = []
+        for kind, x in held:
+            if kind == "register":
+                d = x if type(x) is dict else b.doc(x)
+                if d["_id"] not in docs:
+                    docs[d["_id"]] = d
+                continue
+            uid, f, was = x
+            if type(f) is not dict:
+                f = b.result_fields(f)
+            d = docs.get(uid)
+            if d is None:
+                updates.append((uid, f, was))
+                continue
+            merged.setdefault(uid, []).append((f, was))
+            if was is None or d.get("status") == was:
+                d.update(f)
+        if updates:
+            # the sweep's literals / result_fields are built for this write: the storage may
+            # keep them as they are
+            self._call("update_trial_docs", updates, owned=True)
+        if not docs:
             return
-        fields = self.builder.result_fields if self.builder is not None else None
-        # every queued update carries dicts built for it (the sweep's literals, result_fields):
-        # the storage may keep them as they are
-        self._call("update_trial_docs",
-                   [h[1] if type(h[1][1]) is dict else (h[1][0], fields(h[1][1]), h[1][2])
-                    for h in held], owned=True)
+        if self._call("register_trial_docs", list(docs.values()), owned=True):
+            return
+        for uid, d in docs.items():   # a bulk insert hit a duplicate: insert one by one
+            if not self._call("register_trial_docs", [dict(d)]) and uid in merged:
+                self._call("update_trial_docs", [(uid, f, was) for f, was in merged[uid]])
 
     def _call(self, method, *args, **kwargs) -> bool:
         try:
@@ -146,6 +173,15 @@ class WriteBehind:
     def flush(self):
         """Apply every held write."""
         self.drain_while(lambda: True)
+
+    def drain_all(self, unit: int) -> None:
+        """Apply every held write in units of up to ``unit`` (the writer child's backlog)."""
+        t0 = time.perf_counter()
+        while self._held:
+            with self._lock:
+                if self._held:
+                    self._apply_batch(self._take(unit))
+        self.busy_s += time.perf_counter() - t0
 
     def close(self):
         self.flush()
@@ -176,28 +212,95 @@ def _open(spec):
 
 
 def _child(conn, spec, builder, seed_docs, applied=None):  # pragma: no cover - child process
+    import gc
+    gc.set_threshold(20000, 10, 10)   # as the sweep's rank 0 (PopulationSweep.__init__)
     storage = _open(spec)
     if seed_docs:
         storage.database.write("trials", seed_docs)
     wb = WriteBehind(storage, builder)
     while True:
-        msg = conn.recv()
-        kind = msg[0]
-        if kind == "ops":
-            wb.extend(msg[1])
+        try:
+            msg = conn.recv()
+        except EOFError:                    # the parent is gone
             wb.flush()
+            return
+        if msg[0] == "ops":
+            # everything already waiting is applied as one backlog: a lagging child merges a
+            # trial's registration and its result into one insert (WriteBehind._apply_batch)
+            n = 0
+            while msg is not None and msg[0] == "ops":
+                n += len(msg[1])
+                wb.extend(msg[1])
+                msg = conn.recv() if conn.poll() else None
+            wb.drain_all(4096)
             if applied is not None:         # the parent's view of the child's backlog
-                applied.value += len(msg[1])
-        elif kind == "flush":
-            wb.flush()
+                applied.value += n
+            gc.freeze()                     # the applied documents live on: out of the GC scan
+            if msg is None:
+                continue
+        kind = msg[0]
+        wb.flush()
+        if kind == "flush":
             conn.send(("flushed", wb.errors))
-        elif kind == "dump":
-            wb.flush()
-            conn.send(("docs", storage.database.read("trials", {"experiment": builder.exp_id})))
+        elif kind == "dump":           # pickled straight from the child's store (no copies)
+            db = storage.database
+            read = getattr(db, "read_owned", db.read)
+            conn.send(("docs", read("trials", {"experiment": builder.exp_id})))
         elif kind == "close":
-            wb.flush()
             conn.send(("closed", wb.errors))
             return
+
+
+def _child_main(fd: int, counter_fd: int):  # pragma: no cover - child process
+    """Entry point of the writer child (``python -c``, see :class:`_Child`): the arguments
+    arrive as the first message; ``counter_fd`` is an 8-byte shared mapping that publishes the
+    number of applied writes."""
+    import ctypes
+    import mmap
+    from multiprocessing.connection import Connection
+    conn = Connection(fd)
+    buf = mmap.mmap(counter_fd, 8)
+    spec, builder, seed_docs = conn.recv()
+    _child(conn, spec, builder, seed_docs, ctypes.c_int64.from_buffer(buf))
+
+
+class _Child:
+    """The writer child as a plain ``python -c`` subprocess rather than a ``multiprocessing``
+    spawn: a spawned child re-imports the parent's ``__main__`` (the sweep, bench.py: torch and
+    the whole package, ~2 s and ~300 MB) before it reads its first message, and the sweep's
+    first writes -- the initial fill of every slot -- waited that long in the pipe.  This child
+    imports the storage layer only."""
+
+    def __init__(self, conn_fd: int, counter_fd: int):
+        import os
+        import subprocess
+        import sys
+        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        env = dict(os.environ)
+        env["PYTHONPATH"] = root + (os.pathsep + env["PYTHONPATH"]
+                                    if env.get("PYTHONPATH") else "")
+        code = ("import sys; from metaopt_amd.worker.writer import _child_main; "
+                "_child_main(int(sys.argv[1]), int(sys.argv[2]))")
+        self._p = subprocess.Popen([sys.executable, "-c", code, str(conn_fd), str(counter_fd)],
+                                   pass_fds=(conn_fd, counter_fd), env=env)
+
+    def is_alive(self) -> bool:
+        return self._p.poll() is None
+
+    @property
+    def exitcode(self):
+        return self._p.poll()
+
+    def kill(self) -> None:
+        if self._p.poll() is None:
+            self._p.kill()
+
+    def join(self, timeout=None) -> None:
+        import subprocess
+        try:
+            self._p.wait(timeout)
+        except subprocess.TimeoutExpired:
+            pass
 
 
 class WriterDied(RuntimeError):
@@ -237,17 +340,19 @@ class WriterProcess:
         seed = None
         if spec[0] == "ephemeral":
             seed = storage.database.read("trials", {"experiment": builder.exp_id})
-        ctx = mp.get_context("spawn")
-        self._conn, child = ctx.Pipe()
-        # ops applied by the child (shared counter, no pipe traffic): len(writer) counts the
-        # child's backlog too, so the sweep's backlog bound also holds when the child lags
-        self._applied = ctx.Value("q", 0, lock=False)
+        self._conn, child = mp.Pipe()
+        # ops applied by the child (a shared 8-byte mapping, no pipe traffic): len(writer)
+        # counts the child's backlog too, so the sweep's backlog bound also holds when it lags
+        counter_fd = os.memfd_create("mopt-writer-applied")
+        os.ftruncate(counter_fd, 8)
+        self._counter_map = mmap.mmap(counter_fd, 8)
+        self._applied = ctypes.c_int64.from_buffer(self._counter_map)
         self._handed = 0
-        self._proc = ctx.Process(target=_child, args=(child, spec, builder, seed, self._applied),
-                                 name="mopt-writer", daemon=True)
-        self._proc.start()
+        self._proc = _Child(child.fileno(), counter_fd)
         child.close()
+        os.close(counter_fd)
         self._queue: "queue.SimpleQueue" = queue.SimpleQueue()
+        self._queue.put(("init", (spec, builder, seed)))     # the child's first message
         self._sender = threading.Thread(target=self._send_loop, name="mopt-writer-send",
                                         daemon=True)
         self._sender.start()
@@ -272,6 +377,9 @@ class WriterProcess:
                 item = self._queue.get()
                 if item[0] == "ops":
                     self._conn.send(item)
+                    continue
+                if item[0] == "init":
+                    self._conn.send(item[1])
                     continue
                 # ("sync", request, done event, reply box): a request that waits for the child
                 _, request, done, box = item
@@ -364,8 +472,11 @@ class WriterProcess:
                 _, docs = reply
                 db = self.storage.database
                 db.remove("trials", {"experiment": self.builder.exp_id})
-                if docs:
-                    db.write("trials", docs)
+                if docs:          # unpickled for this call: nobody else holds them
+                    if hasattr(db, "insert_owned"):
+                        db.insert_owned("trials", docs)
+                    else:
+                        db.write("trials", docs)
                 self._unacked = []
         reply = self._request(("close",))
         if reply is not None:

@@ -12,7 +12,7 @@
 #   timeline         bench.py with the GPU-event timeline (MOPT_GPU_TIMELINE=1)
 #   streams          bench.py at MOPT_STREAMS=1,2
 #   kbench           per-kernel MLP microbench             trace_bench  rocprofv3 kernel trace
-#   kbench_ab        the microbench per kernel variant (MOPT_FWD_VARIANT in $VARIANTS, default "0 1")
+#   kbench_ab        the microbench per kernel variant (env $ABVAR set to each of $VARIANTS)
 #   kbench_rows      the microbench at 128 / 256 / 512 rows per step (multi-row-block kernels)
 #   pmc_kbench       PMC passes of the MLP kernels (fetch/write/MFMA/LDS, one pass each)
 #   lm resnet hyper  bench_configs.py of one config        trace_lm trace_resnet trace_hyper
@@ -55,7 +55,7 @@ for step in "$@"; do
     timeline)   MOPT_GPU_TIMELINE=1 $T 240 python bench.py --steps 20 --warmup 5 $BENCH_ARGS > "$OUT/bench_timeline$TAG.json" 2> "$OUT/bench_timeline$TAG.err" ;;
     streams)    for s in 1 2; do MOPT_STREAMS=$s $T 240 python bench.py --steps 20 --warmup 5 > "$OUT/bench_streams$s.json" 2> "$OUT/bench_streams$s.err"; done ;;
     kbench)     $T 200 python scripts/kernel_bench.py --momentum-dtype bf16 --out "$OUT/kbench.json" > "$OUT/kbench.log" 2>&1 ;;
-    kbench_ab)  for v in ${VARIANTS:-0 1}; do MOPT_FWD_VARIANT=$v $T 200 python scripts/kernel_bench.py --momentum-dtype bf16 --out "$OUT/kbench_v$v.json" > "$OUT/kbench_v$v.log" 2>&1; done ;;
+    kbench_ab)  for v in ${VARIANTS:-0 1}; do env ${ABVAR:-MOPT_AB}=$v $T 200 python scripts/kernel_bench.py --momentum-dtype bf16 --out "$OUT/kbench_v$v.json" > "$OUT/kbench_v$v.log" 2>&1; done ;;
     kbench_rows) for b in 128 256 512; do $T 200 python scripts/kernel_bench.py --momentum-dtype bf16 --batch $b --iters 20 --out "$OUT/kbench_b$b.json" > "$OUT/kbench_b$b.log" 2>&1; done ;;
     trace_bench) prof trace_bench$TAG 300 -- python3 "$ROOT/bench.py" --steps 10 --warmup 3 $BENCH_ARGS ;;
     pmc_kbench)

@@ -93,15 +93,27 @@ def main(n_syncs=40, P=256, world=1, profile=False):
             prof.disable()
         t_total += time.perf_counter() - t0
         t1 = time.perf_counter()
-        sw._writer.drain_while(lambda: True)   # rank 0's share of the writes (inline: all)
+        if not os.environ.get("NO_DRAIN"):
+            sw._writer.drain_while(lambda: True)   # rank 0's share (inline: all of them)
         t_rel += time.perf_counter() - t1
         gc.freeze()                     # as PopulationSweep._sync does after every sync
+    if hasattr(sw._writer, "_queue"):
+        w = sw._writer
+        print(f"at loop end: {w._queue.qsize()} messages not sent, "
+              f"{w._handed - w._applied.value} ops not applied")
     t2 = time.perf_counter()
+    if os.environ.get("NO_DRAIN") and profile:
+        prof = cProfile.Profile()
+        prof.enable()
+        sw._writer.drain_all(4096)
+        prof.disable()
     sw._writer.flush()
     t_flush = time.perf_counter() - t2
+    n_ops = getattr(sw._writer, "_handed", None)
+    kind = type(sw._writer).__name__
     sw.close()
-    print(f"writer {type(sw._writer).__name__ if sw._writer else ''}: final flush "
-          f"{1e3 * t_flush:.1f} ms")
+    print(f"writer {kind}: final flush {1e3 * t_flush:.1f} ms"
+          + (f", {n_ops / n_syncs:.0f} ops/sync handed over" if n_ops is not None else ""))
     print("phases ms/sync:", {k: round(1e3 * v / n_syncs, 2) for k, v in sw.timers.items()
                               if k.startswith("decide") or k.startswith("gc")})
     print(f"decide: {1e3 * t_total / n_syncs:.2f} ms/sync, writes {1e3 * t_rel / n_syncs:.2f} ms/sync, "

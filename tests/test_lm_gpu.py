@@ -201,6 +201,40 @@ def test_fused_adamw_matches_reference(m_dtype):
     assert hip["m"].dtype == m_dtype
 
 
+@pytest.mark.parametrize("kind", ["adamw", "sgd"])
+def test_fused_optimizer_split_master_matches_f32_master(kind):
+    """The split master (p16 = high half, int16 low half; 22 B/param AdamW) updates exactly as
+    the f32 master does: the joined result equals the f32 kernel's master bit for bit, and the
+    working copy is the split's high half."""
+    from metaopt_amd.ops.reference import join_f32, split_f32
+    torch.manual_seed(8)
+    P = 2
+    segments, off = [], 0
+    for n in (768, 4096 * 3):
+        segments.append((off, n))
+        off += P * n
+    w = torch.randn(off, device=DEV) * 0.05
+    m = (torch.randn(off, device=DEV) * 0.01).to(torch.bfloat16 if kind == "adamw"
+                                                 else torch.float32)
+    v = (torch.randn(off, device=DEV) * 0.01).abs() if kind == "adamw" else \
+        torch.zeros(0, device=DEV)
+    g16 = torch.randn(off, device=DEV).to(torch.bfloat16)
+    hp = np.zeros(P, dtype=ops.LM_HP_DTYPE)
+    for p in range(P):
+        hp[p] = (1e-3 * (p + 1), 0.9, 0.95, 1e-8, 0.1 * p, 1.0 if p else 0.0, 3 + p, 0)
+    opt = ops.FlatOptimizer(segments, P, DEV, kind=kind)
+    ref = {"p": w.clone(), "m": m.clone(), "v": v.clone()}
+    r16 = torch.empty(off, dtype=torch.bfloat16, device=DEV)
+    opt.step(ref["p"], r16, g16, ref["m"], ref["v"], hp)
+    hi, lo = split_f32(w)
+    sm, sv = m.clone(), v.clone()
+    opt.step(lo, hi, g16, sm, sv, hp)
+    torch.cuda.synchronize()
+    assert torch.equal(join_f32(hi, lo), ref["p"])
+    assert torch.equal(hi, split_f32(ref["p"])[0])
+    assert torch.equal(sm, ref["m"]) and torch.equal(sv, ref["v"])
+
+
 def test_population_lm_step_matches_reference():
     from metaopt_amd.models.llama import PopulationLM, SyntheticLM
     from metaopt_amd.ops.population import MemberConfig
@@ -214,7 +248,7 @@ def test_population_lm_step_matches_reference():
         pops.append(pop)
     # identical starting weights (the generators differ between devices)
     with torch.no_grad():
-        pops[1].p32.copy_(pops[0].p32.cpu())
+        pops[1].p32.copy_(pops[0].master_flat().cpu())
         pops[1].p16.copy_(pops[0].p16.cpu())
     losses = [[], []]
     for step in range(5):

@@ -156,7 +156,7 @@ def test_population_resnet_step_matches_cpu():
             pop.set_member(s, MemberConfig(width=0, lr=0.05 * (s + 1), momentum=0.9, seed=s))
         pops.append(pop)
     with torch.no_grad():
-        pops[1].p32.copy_(pops[0].p32.cpu())
+        pops[1].p32.copy_(pops[0].master_flat().cpu())
         pops[1].p16.copy_(pops[0].p16.cpu())
     data = SyntheticCIFAR(n_train=16 * 8, n_val=32, batch_size=16, image_size=16)
     losses = [[], []]
@@ -207,17 +207,19 @@ def test_one_launch_member_init():
     statistics (0, 1), other slots untouched, same seed -> same weights."""
     from metaopt_amd.models.resnet import PopulationResNet
     from metaopt_amd.ops.population import MemberConfig
+    from metaopt_amd.ops.reference import split_f32
     pop = PopulationResNet(3, batch_size=16, device=DEV, blocks_per_stage=1, image_size=16)
     with torch.no_grad():
-        pop.p32.fill_(7.0)
+        pop.load_master_flat(torch.full((pop.n_flat,), 7.0, device=DEV))
         pop.m.fill_(7.0)
         pop.aux.fill_(7.0)
     cfg = MemberConfig(width=0, lr=0.05, momentum=0.9, seed=11)
     pop.set_member(1, cfg)
     torch.cuda.synchronize()
+    master = pop.master_flat()
     for (name, shape, init), sl in zip(pop.specs, pop._slices(1)):
-        w = pop.p32[sl]
-        assert torch.equal(pop.p16[sl], w.to(torch.bfloat16)), name
+        w = master[sl]
+        assert torch.equal(pop.p16[sl], split_f32(w)[0]), name     # hi half of the split master
         assert torch.all(pop.m[sl] == 0), name
         if init[0] == "ones":
             assert torch.all(w == 1), name
@@ -233,12 +235,12 @@ def test_one_launch_member_init():
         assert torch.all(r[0] == 0) and torch.all(r[1] == 1), name
     for slot in (0, 2):                                   # untouched
         for sl in pop._slices(slot):
-            assert torch.all(pop.p32[sl] == 7.0)
-    first = pop.p32[pop._slices(1)[0]].clone()
+            assert torch.all(master[sl] == 7.0)
+    first = master[pop._slices(1)[0]].clone()
     pop.set_member(1, cfg)
-    assert torch.equal(pop.p32[pop._slices(1)[0]], first)
+    assert torch.equal(pop.master_flat()[pop._slices(1)[0]], first)
     pop.set_member(1, MemberConfig(width=0, lr=0.05, momentum=0.9, seed=12))
-    assert not torch.equal(pop.p32[pop._slices(1)[0]], first)
+    assert not torch.equal(pop.master_flat()[pop._slices(1)[0]], first)
 
 
 @pytest.mark.parametrize("P,B,HW,C", [(3, 32, 64, 64), (2, 16, 16, 16), (4, 48, 4, 8)])

@@ -229,6 +229,46 @@ def test_writer_process_mirrors_ephemeral_db():
     assert docs["t5"]["params"][0] == {"name": "/x", "type": "real", "value": 5.0}
 
 
+def test_write_behind_merges_results_into_pending_registrations():
+    """A unit holding a trial's registration and its later result inserts ONE completed
+    document; the ordering cases keep their applied-in-order meaning: an update queued before
+    its trial's registration finds nothing, a compare-and-swap that does not match is dropped,
+    and a duplicate registration (failover replay) applies its merged updates to the stored
+    document instead."""
+    import datetime
+    from metaopt_amd.storage.protocol import DocumentStorage
+    from metaopt_amd.worker.writer import DocBuilder, WriteBehind
+    storage = DocumentStorage(EphemeralDB())
+    b = DocBuilder(7, ["/x"], ["real"])
+    now = datetime.datetime.utcnow()
+    w = WriteBehind(storage, b)
+    w.put_register_spec(("dup", now, (0.0,), None))
+    w.flush()
+    calls = []
+    real = storage.update_trial_docs
+    storage.update_trial_docs = lambda items, owned=False: (calls.append(len(items)),
+                                                           real(items, owned))[1]
+    w.put_update("early", {"status": "broken"}, was="reserved")     # before its registration
+    for i in range(4):
+        w.put_register_spec((f"t{i}", now, (float(i),), None))
+    w.put_update_spec("t1", (0.5, 0.9, 0.7, now, now), was="reserved")
+    w.put_update("t2", {"status": "broken", "heartbeat": now}, was="reserved")
+    w.put_update_spec("t2", (0.1, 0.9, 0.7, now, now), was="reserved")   # CAS fails: broken
+    w.put_register_spec(("early", now, (9.0,), None))
+    w.flush()
+    # the merged results cost no update: one bulk update, for the trial registered earlier
+    assert calls == [1]
+    w.put_register_spec(("dup", now, (0.0,), None))                       # already stored
+    w.put_update_spec("dup", (0.3, 0.9, 0.7, now, now), was="reserved")
+    w.flush()
+    docs = {d["_id"]: d for d in storage.database.read("trials", {"experiment": 7})}
+    assert len(docs) == 6
+    assert docs["t1"]["status"] == "completed" and docs["t1"]["results"][0]["value"] == 0.5
+    assert docs["t2"]["status"] == "broken" and docs["t2"]["results"] == []
+    assert docs["t0"]["status"] == docs["early"]["status"] == "reserved"
+    assert docs["dup"]["status"] == "completed" and docs["dup"]["results"][0]["value"] == 0.3
+
+
 def test_writer_process_killed_child_falls_back_in_process():
     """A writer child that dies (OOM kill, crash) never hangs flush/close: the writer notices,
     switches to in-process writes and replays what the child had not acknowledged -- for an
