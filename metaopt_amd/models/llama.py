@@ -136,16 +136,16 @@ class PopulationLM(FlatPopulation):
         # every residual add is fused into the pre-norm that follows it (ops.add_rmsnorm)
         h = ops.rmsnorm(x, W["l0.attn_norm"], rpt, c.norm_eps)
         for l in range(c.n_layers):
-            qkv = _lin(h.view(P, rpt, d), W[f"l{l}.wqkv"]).view(R, 3 * d)
-            q, k, v = ops.rope_split(qkv, self.cos, self.sin, T, H)
+            # interleaved-pair RoPE applied by the QKV GEMM's epilogue (ops.qkv_rope)
+            q, k, v = ops.qkv_rope(h.view(P, rpt, d), W[f"l{l}.wqkv"], self.cos, self.sin, T, H)
             o = ops.attention(q, k, v)
             x, h = ops.add_rmsnorm(x, _lin(o.view(P, rpt, d), W[f"l{l}.wo"]).view(R, d),
                                    W[f"l{l}.mlp_norm"], rpt, c.norm_eps)
-            gu = _lin(h.view(P, rpt, d), W[f"l{l}.wgu"])
-            a = ops.swiglu(gu)
+            # gate / up columns interleaved in 16-column groups: the SwiGLU runs in the GEMM
+            # epilogues (ops.swiglu_mlp)
+            y = ops.swiglu_mlp(h.view(P, rpt, d), W[f"l{l}.wgu"], W[f"l{l}.wdown"])
             nxt = W[f"l{l + 1}.attn_norm"] if l + 1 < c.n_layers else W["final_norm"]
-            x, h = ops.add_rmsnorm(x, _lin(a, W[f"l{l}.wdown"]).view(R, d), nxt, rpt,
-                                   c.norm_eps)
+            x, h = ops.add_rmsnorm(x, y.view(R, d), nxt, rpt, c.norm_eps)
         logits = _lin(h.view(P, rpt, d), W["head"]).view(R, c.vocab)
         if train:
             return ops.cross_entropy(logits, labels.reshape(-1), rpt, grad_scale=1.0 / rpt,

@@ -31,6 +31,7 @@ _lib.register_signatures({
     "mopt_dconv": ([c_int] + [c_void_p] * 4 + [c_int] * 7 + [c_void_p], c_int),
     "mopt_dconv_wgrad_splits": ([c_int] * 6, c_int),
     "mopt_dconv_bnin": ([c_int] + [c_void_p] * 4 + [c_int] * 5 + [c_void_p] * 4, c_int),
+    "mopt_dconv_dgrad_bnsums": ([c_void_p] * 4 + [c_int] * 5 + [c_void_p] * 5, c_int),
     "mopt_resnet_head": ([c_void_p] * 4 + [c_int] * 5 + [c_float, c_int] + [c_void_p] * 7,
                          c_int),
     "mopt_resnet_head_part_floats": ([c_int] * 3, c_int),
@@ -306,19 +307,28 @@ class _BNReluConv3x3(torch.autograd.Function):
         N, H, W, _ = x.shape
         Bn = N // P
         dy = dy.contiguous()
-        # data gradient of the convolution = the BatchNorm output's gradient
+        # data gradient of the convolution = the BatchNorm output's gradient; its epilogue also
+        # accumulates the BatchNorm backward's reductions into the zeroed sums (flag 2: the
+        # BatchNorm backward then runs its apply pass only)
         dbn = torch.empty_like(x)
-        _pconv(1, dy, w, dbn, P, Bn, H, W, C, Co, 1)
+        sums = ctx.bwd_sums if ctx.bwd_sums is not None else \
+            torch.zeros(P, 2, C, dtype=torch.float32, device=x.device)
+        rc = _lib.get_lib().mopt_dconv_dgrad_bnsums(
+            dy.data_ptr(), w.data_ptr(), dbn.data_ptr(), sums.data_ptr(), P, Bn, H, C, Co,
+            x.data_ptr(), stat.data_ptr(), gamma.data_ptr(), beta.data_ptr(), _s(x))
+        if rc == _NOT_SUPPORTED:
+            _pconv(1, dy, w, dbn, P, Bn, H, W, C, Co, 1)
+            zeroed = 1
+        else:
+            _lib.check(rc, "mopt_dconv_dgrad_bnsums")
+            zeroed = 2
         dx = torch.empty_like(x)
-        zeroed = ctx.bwd_sums is not None
-        sums = ctx.bwd_sums if zeroed else torch.empty(P, 2, C, dtype=torch.float32,
-                                                       device=x.device)
         gg, gb = ctx.grads
         direct = gg is not None and gb is not None and gg.is_contiguous() and gb.is_contiguous()
         _call("mopt_bn_bwd", x.data_ptr(), 0, dbn.data_ptr(), stat.data_ptr(), gamma.data_ptr(),
               beta.data_ptr(), dx.data_ptr(), 0, sums.data_ptr(),
               gg.data_ptr() if direct else 0, gb.data_ptr() if direct else 0,
-              P, M, C, 2, int(zeroed), _s(x))
+              P, M, C, 2, zeroed, _s(x))
         # weight gradient over relu(BN(x)), applied again while staging
         dw = ctx.grad_w if ctx.grad_w is not None else torch.empty_like(w)
         lib = _lib.get_lib()

@@ -111,6 +111,7 @@ struct BnIn {
   const float* stat;     // [P][2][C] mean, rstd
   const bf16_t* gamma;   // [P][C]
   const bf16_t* beta;    // [P][C]
+  const bf16_t* x;       // BNB data gradients: the BatchNorm's input, shaped like the output
 };
 
 template <int CI>
@@ -142,7 +143,12 @@ __device__ __forceinline__ int tap_off(const Geom& g, int k) {
 // ADD: data-gradient epilogue addend -- 0 none, 1 same layout as the output (identity shortcut),
 // 2 half-resolution option-A shortcut gradient (compile-time: the epilogue code otherwise costs
 // the forward kernels registers and a wave per SIMD)
-template <int CI, int CO, int NPX, int MODE, int S, int ADD, int BNIN = 0>
+// BNB (stride-1 data gradient whose output dy feeds a BatchNorm -> ReLU backward, the first
+// BatchNorm of a basic block under _BNReluConv3x3): the epilogue also accumulates that backward's
+// reductions sums[p][0][c] += dz, sums[p][1][c] += dz xhat (dz = dy relu'(x sc + sh), xhat =
+// (x - mean) rstd, x = bn.x) from the stored bf16 dy -- the BatchNorm backward then skips its
+// reduction pass (bn_reduce_kernel<true>: both tensors read once more).
+template <int CI, int CO, int NPX, int MODE, int S, int ADD, int BNIN = 0, int BNB = 0>
 __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict__ x,
                                                         const bf16_t* __restrict__ w,
                                                         bf16_t* __restrict__ y,
@@ -151,6 +157,7 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
                                                         const Geom g, int addend_c,
                                                         const BnIn bn) {
   static_assert(BNIN == 0 || MODE == kFwd, "the BatchNorm input is applied by forwards only");
+  static_assert(BNB == 0 || (MODE == kDgrad && ADD == 0), "BNB: plain stride-1 data gradients");
   constexpr int mode = MODE;
   constexpr int KS = (9 * CI + 31) / 32;  // 32-wide k steps (k = tap * CI + c)
   constexpr int WN = CO / 16, WM = 4 / WN;
@@ -229,6 +236,23 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
 
   float s1 = 0.f, s2 = 0.f;
   float* bntab = (float*)(smem + g.lds_elems);  // BNIN: [2][CI] past the halo / output tile
+  // output chunks (8 channels) per thread and band; BNB: a thread's chunk is the same in every
+  // band (CO / 8 | 256), so it keeps that chunk's relu' constants and raw sums (sum dz, sum dz
+  // x -- turned into sum dz xhat once, at the end: 32 registers instead of 48)
+  constexpr int CPR = CO / 8;
+  constexpr int XCH = (NPX * CPR + 255) / 256;
+  float bsc[8], bsh[8], ba[8], bb[8];
+  uint4 xpre[BNB != 0 ? XCH : 1];
+  if constexpr (BNB != 0) {
+    const int c0 = 8 * (threadIdx.x % CPR);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float mean = bn.stat[(2 * p) * CO + c0 + e];
+      bsc[e] = bf2f(bn.gamma[(int64_t)p * CO + c0 + e]) * bn.stat[(2 * p + 1) * CO + c0 + e];
+      bsh[e] = bf2f(bn.beta[(int64_t)p * CO + c0 + e]) - mean * bsc[e];
+      ba[e] = bb[e] = 0.f;
+    }
+  }
   if constexpr (BNIN != 0) {
     bnin_table<CI>(bntab, bn, p);
     __syncthreads();
@@ -236,6 +260,16 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
   for (int t = blk; t < g.tiles; t += g.nb) {
     const int b0 = (t / g.tpi) * g.IMGS, oy0 = (t % g.tpi) * g.TR;
     load_halo<CI, S, BNIN>(hs, xp, g, b0, mode == kDgrad2 ? oy0 / 2 - 1 : oy0 * S - 1, bntab);
+    if constexpr (BNB != 0) {   // the band's BatchNorm input, in flight during the MFMAs
+      const int nval = min(NPX, (g.Bn - b0) * ppi) * CPR;
+      const bf16_t* xb = bn.x + p * y_batch + ((int64_t)b0 * g.OH + oy0) * (1 << g.owl) * CO;
+#pragma unroll
+      for (int k = 0; k < XCH; ++k) {
+        const int c = threadIdx.x + 256 * k;
+        xpre[k] = c < nval ? *(const uint4*)(xb + (int64_t)(c / CPR) * CO + 8 * (c % CPR))
+                           : make_uint4(0, 0, 0, 0);
+      }
+    }
     __syncthreads();
 
     f32x4 acc[MFW];
@@ -286,9 +320,11 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
     __syncthreads();
     // the band's output is contiguous: (b0, oy0 .. oy0 + TR) or whole images b0 ..
     bf16_t* yt = yp + ((int64_t)b0 * g.OH + oy0) * (1 << g.owl) * CO;
-    constexpr int CPR = CO / 8;
     const bf16_t* at = ADD == 1 ? addend + (yt - y) : nullptr;
-    for (int c = threadIdx.x; c < valid * CPR; c += 256) {
+#pragma unroll
+    for (int k = 0; k < XCH; ++k) {
+      const int c = threadIdx.x + 256 * k;
+      if (c >= valid * CPR) break;
       const int row = c / CPR, cc = c % CPR;
       uint4 v = *(const uint4*)(cs + row * LSC + 8 * cc);
       const bf16_t* ap = nullptr;
@@ -314,10 +350,51 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
         v = make_uint4(o[0], o[1], o[2], o[3]);
       }
       *(uint4*)(yt + (int64_t)row * CO + 8 * cc) = v;
+      if constexpr (BNB != 0) {
+        const uint4 xr = xpre[k];
+        const uint32_t vw[4] = {v.x, v.y, v.z, v.w}, xw[4] = {xr.x, xr.y, xr.z, xr.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float d = bf2f(e & 1 ? vw[e >> 1] >> 16 : vw[e >> 1] & 0xFFFF);
+          const float xv = bf2f(e & 1 ? xw[e >> 1] >> 16 : xw[e >> 1] & 0xFFFF);
+          // bn_reduce_kernel<true>'s relu mode 2 arithmetic
+          const float dz = xv * bsc[e] + bsh[e] + 0.f <= 0.f ? 0.f : d;
+          ba[e] += dz;
+          bb[e] += dz * xv;
+        }
+      }
     }
     __syncthreads();  // the next band's halo overwrites the output tile
   }
-  if (sums != nullptr) {
+  if constexpr (BNB != 0) {
+    // threads of one chunk: lanes equal mod CPR (xor over the lane bits above log2 CPR), then
+    // the 4 waves through LDS (the tile is free after the last barrier), one atomic per channel
+    for (int off = 32; off >= CPR; off >>= 1) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        ba[e] += __shfl_xor(ba[e], off, 64);
+        bb[e] += __shfl_xor(bb[e], off, 64);
+      }
+    }
+    float* red = (float*)smem;   // [4 waves][2][CO]
+    if (lane < CPR) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[(wave * 2) * CO + 8 * lane + e] = ba[e];
+        red[(wave * 2 + 1) * CO + 8 * lane + e] = bb[e];
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < CO) {     // sum dz xhat = rstd (sum dz x - mean sum dz)
+      const int c = threadIdx.x;
+      const float a = red[c] + red[2 * CO + c] + red[4 * CO + c] + red[6 * CO + c];
+      const float bx = red[CO + c] + red[3 * CO + c] + red[5 * CO + c] + red[7 * CO + c];
+      const float mean = bn.stat[(2 * p) * CO + c], rstd = bn.stat[(2 * p + 1) * CO + c];
+      atomicAdd(sums + (2 * p) * CO + c, a);
+      atomicAdd(sums + (2 * p + 1) * CO + c, rstd * (bx - mean * a));
+    }
+  }
+  if (BNB == 0 && sums != nullptr) {   // (BNB: sums holds the backward reductions above)
     s1 += __shfl_xor(s1, 16, 64);
     s1 += __shfl_xor(s1, 32, 64);
     s2 += __shfl_xor(s2, 16, 64);
@@ -485,7 +562,7 @@ template <int CI, int S>
 size_t halo_bytes(const Geom& g) { return (size_t)g.IMGS * g.TRI * g.WI * pstride<CI, S>() * 2; }
 
 // S: the stride of the halo layout (kDgrad2 reads its half-resolution dy band at layout S = 1)
-template <int CI, int CO, int MODE, int S, int ADD = 0, int BNIN = 0>
+template <int CI, int CO, int MODE, int S, int ADD = 0, int BNIN = 0, int BNB = 0>
 int launch_fwd(const void* x, const void* w, void* y, void* sums, int P, int Bn, int H,
                hipStream_t st, const void* addend = nullptr, int addend_c = 0,
                const BnIn& bn = BnIn{}) {
@@ -498,7 +575,7 @@ int launch_fwd(const void* x, const void* w, void* y, void* sums, int P, int Bn,
   const size_t lds_all = lds + (BNIN ? (size_t)2 * CI * sizeof(float) : 0);
   if (lds_all > 64 * 1024) return (int)hipErrorNotSupported;
   g.lds_elems = (int)(lds / 2);
-  hipLaunchKernelGGL((dconv_fwd_kernel<CI, CO, NPX, MODE, S, ADD, BNIN>), dim3(P * g.nb),
+  hipLaunchKernelGGL((dconv_fwd_kernel<CI, CO, NPX, MODE, S, ADD, BNIN, BNB>), dim3(P * g.nb),
                      dim3(256), lds_all, st,
                      (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)sums,
                      (const bf16_t*)addend, g, addend_c, bn);
@@ -598,12 +675,32 @@ int mopt_dconv_bnin(int kind, const void* a, const void* b, void* out, void* aux
                     void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (stat == nullptr || gamma == nullptr || beta == nullptr) return (int)hipErrorInvalidValue;
-  const BnIn bn{(const float*)stat, (const bf16_t*)gamma, (const bf16_t*)beta};
+  const BnIn bn{(const float*)stat, (const bf16_t*)gamma, (const bf16_t*)beta, nullptr};
 #define X(c) \
   if (Ci == c && Co == c) \
     return kind == 0 ? launch_fwd<c, c, kFwd, 1, 0, 1>(a, b, out, aux, P, Bn, H, st, nullptr, 0, bn) \
          : kind == 2 ? launch_wgrad<c, c, 1, 1>(a, b, out, aux, P, Bn, H, st, nullptr, bn) \
                      : (int)hipErrorInvalidValue;
+  X(16) X(32) X(64)
+#undef X
+  return (int)hipErrorNotSupported;
+}
+
+// Stride-1 data gradient dbn [P*Bn, H, H, Ci] = dgrad(dy [.., Co], w) whose output is the
+// gradient of relu(BatchNorm(x)) (x shaped like dbn; stat / gamma / beta of that BatchNorm):
+// the epilogue also adds the BatchNorm backward's reductions (sum dz, sum dz xhat, relu'
+// recomputed from x) into sums [P][2][Ci] (zeroed by the caller).  Ci == Co in {16, 32, 64}.
+int mopt_dconv_dgrad_bnsums(const void* dy, const void* w, void* dbn, void* sums, int P, int Bn,
+                            int H, int Ci, int Co, const void* x, const void* stat,
+                            const void* gamma, const void* beta, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (sums == nullptr || x == nullptr || stat == nullptr || gamma == nullptr || beta == nullptr)
+    return (int)hipErrorInvalidValue;
+  const BnIn bn{(const float*)stat, (const bf16_t*)gamma, (const bf16_t*)beta, (const bf16_t*)x};
+  // (the data gradient runs the forward kernel with the channel counts swapped: CO = Ci)
+#define X(c) \
+  if (Ci == c && Co == c) \
+    return launch_fwd<c, c, kDgrad, 1, 0, 0, 1>(dy, w, dbn, sums, P, Bn, H, st, nullptr, 0, bn);
   X(16) X(32) X(64)
 #undef X
   return (int)hipErrorNotSupported;

@@ -353,7 +353,9 @@ int mopt_bn_fwd(const void* x, const void* gamma, const void* beta, const void* 
 }
 
 // sums [P][2][C] out: (sum dz, sum dz * xhat) = (dbeta, dgamma) in f32 (zeroed here unless
-// sums_zeroed); dgamma / dbeta (bf16 [P][C], may be null): the gradients written directly.
+// sums_zeroed = 1; sums_zeroed = 2: already accumulated by the producing data gradient's
+// epilogue, mopt_dconv_dgrad_bnsums -- no reduction pass); dgamma / dbeta (bf16 [P][C], may be
+// null): the gradients written directly.
 // relu: 0 none, 1 mask from y, 2 mask recomputed from x with gamma / beta (y may be null)
 int mopt_bn_bwd(const void* x, const void* y, const void* dy, const void* stat, const void* gamma,
                 const void* beta, void* dx, void* dres, void* sums, void* dgamma, void* dbeta,
@@ -364,10 +366,11 @@ int mopt_bn_bwd(const void* x, const void* y, const void* dy, const void* stat, 
   hipStream_t st = (hipStream_t)stream;
   if (!sums_zeroed) (void)hipMemsetAsync(sums, 0, sizeof(float) * 2 * P * C, st);
   const int rpb = reduce_rows(P, M, C);
-  hipLaunchKernelGGL(bn_reduce_kernel<true>, dim3((unsigned)((M + rpb - 1) / rpb), P),
-                     dim3(256), 0, st, (const bf16_t*)x, (const bf16_t*)y, (const bf16_t*)dy,
-                     (const float*)stat, (const bf16_t*)gamma, (const bf16_t*)beta, (float*)sums,
-                     M, C, rpb, relu);
+  if (sums_zeroed != 2)
+    hipLaunchKernelGGL(bn_reduce_kernel<true>, dim3((unsigned)((M + rpb - 1) / rpb), P),
+                       dim3(256), 0, st, (const bf16_t*)x, (const bf16_t*)y, (const bf16_t*)dy,
+                       (const float*)stat, (const bf16_t*)gamma, (const bf16_t*)beta,
+                       (float*)sums, M, C, rpb, relu);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3((unsigned)((M + rpb - 1) / rpb), P), dim3(256), 0,
                      st, (const bf16_t*)x, (const bf16_t*)y, (const bf16_t*)dy, (const float*)stat,
                      (const float*)sums, (const bf16_t*)gamma, (const bf16_t*)beta, (bf16_t*)dx,

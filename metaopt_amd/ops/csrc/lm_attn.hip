@@ -33,6 +33,10 @@ constexpr int LS = kLdsStride;
 // 154 + 44 = 2) compile without spills and measured 110.9 -> 99.5 / 179.8 -> 157.7 us per call on
 // the 125M LM (profiles/round3.md); the forward spills below its 4 (124 registers), so it is left.
 constexpr int kAttnFwdWaves = 0, kAttnDqWaves = 4, kAttnDkdvWaves = 3;
+// (Measured and rejected, round 4: two 16-query / 16-key sets per wave -- 128 queries or keys
+// per workgroup, every LDS fragment feeding two MFMAs -- ran fwd 104 -> 157 us, dQ 98 -> 149,
+// dK/dV 156 -> 250 on the 125M LM: the doubled register state cost the occupancy that hides
+// this loop's latency; profiles/round4.md.)
 #define MOPT_WAVES_ATTR(n) __attribute__((amdgpu_waves_per_eu((n) > 0 ? (n) : 1)))
 
 // (position of this workgroup's sequence block within its head, head index bh) for a 1-D grid of

@@ -192,13 +192,25 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_dw_kernel(const bf16_t* __res
 
 // ---------------------------------------------------------------------------------- RoPE
 // qkv [B' * T][3][H][64] -> Q/K/V [B'][H][T][64]; thread = (row, part, head, 8-pair chunk).
+// 4 interleaved RoPE pairs (x[2j], x[2j+1]) rotated by angle j (cs / sn: the 4 angles' tables),
+// sign -1: the inverse (transposed) rotation of the backward
+__device__ __forceinline__ void rope_pairs8(const float (&x)[8], const float* cs, const float* sn,
+                                            float sign, float (&o)[8]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float c = cs[j], s = sign * sn[j];
+    o[2 * j] = x[2 * j] * c - x[2 * j + 1] * s;
+    o[2 * j + 1] = x[2 * j + 1] * c + x[2 * j] * s;
+  }
+}
+
 __global__ __launch_bounds__(256) void rope_fwd_kernel(const bf16_t* __restrict__ qkv,
                                                        const float* __restrict__ cosv,
                                                        const float* __restrict__ sinv,
                                                        bf16_t* __restrict__ Q,
                                                        bf16_t* __restrict__ K,
                                                        bf16_t* __restrict__ V, int rows, int T,
-                                                       int H) {
+                                                       int H, int il) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t total = (int64_t)rows * 3 * H * 4;
   if (i >= total) return;
@@ -219,12 +231,18 @@ __global__ __launch_bounds__(256) void rope_fwd_kernel(const bf16_t* __restrict_
   float x1[8], x2[8], o1[8], o2[8];
   unpack8(a, x1);
   unpack8(bb, x2);
-  const float* cs = cosv + (size_t)t * 32 + 8 * chunk;
-  const float* sn = sinv + (size_t)t * 32 + 8 * chunk;
+  if (il) {   // interleaved pairs (2j, 2j + 1), angle j: elements 8 chunk .. and 32 + 8 chunk ..
+    rope_pairs8(x1, cosv + (size_t)t * 32 + 4 * chunk, sinv + (size_t)t * 32 + 4 * chunk, 1.f, o1);
+    rope_pairs8(x2, cosv + (size_t)t * 32 + 16 + 4 * chunk, sinv + (size_t)t * 32 + 16 + 4 * chunk,
+                1.f, o2);
+  } else {    // rotate-half pairs (j, j + 32)
+    const float* cs = cosv + (size_t)t * 32 + 8 * chunk;
+    const float* sn = sinv + (size_t)t * 32 + 8 * chunk;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    o1[e] = x1[e] * cs[e] - x2[e] * sn[e];
-    o2[e] = x2[e] * cs[e] + x1[e] * sn[e];
+    for (int e = 0; e < 8; ++e) {
+      o1[e] = x1[e] * cs[e] - x2[e] * sn[e];
+      o2[e] = x2[e] * cs[e] + x1[e] * sn[e];
+    }
   }
   *(uint4*)dst = pack8(o1);
   *(uint4*)(dst + 32) = pack8(o2);
@@ -236,7 +254,7 @@ __global__ __launch_bounds__(256) void rope_bwd_kernel(const bf16_t* __restrict_
                                                        const float* __restrict__ cosv,
                                                        const float* __restrict__ sinv,
                                                        bf16_t* __restrict__ dqkv, int rows, int T,
-                                                       int H) {
+                                                       int H, int il) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t total = (int64_t)rows * 3 * H * 4;
   if (i >= total) return;
@@ -257,29 +275,45 @@ __global__ __launch_bounds__(256) void rope_bwd_kernel(const bf16_t* __restrict_
   float y1[8], y2[8], o1[8], o2[8];
   unpack8(a, y1);
   unpack8(bb, y2);
-  const float* cs = cosv + (size_t)t * 32 + 8 * chunk;
-  const float* sn = sinv + (size_t)t * 32 + 8 * chunk;
+  if (il) {   // the transposed rotation: the angle negated
+    rope_pairs8(y1, cosv + (size_t)t * 32 + 4 * chunk, sinv + (size_t)t * 32 + 4 * chunk, -1.f, o1);
+    rope_pairs8(y2, cosv + (size_t)t * 32 + 16 + 4 * chunk, sinv + (size_t)t * 32 + 16 + 4 * chunk,
+                -1.f, o2);
+  } else {
+    const float* cs = cosv + (size_t)t * 32 + 8 * chunk;
+    const float* sn = sinv + (size_t)t * 32 + 8 * chunk;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    o1[e] = y1[e] * cs[e] + y2[e] * sn[e];
-    o2[e] = y2[e] * cs[e] - y1[e] * sn[e];
+    for (int e = 0; e < 8; ++e) {
+      o1[e] = y1[e] * cs[e] + y2[e] * sn[e];
+      o2[e] = y2[e] * cs[e] - y1[e] * sn[e];
+    }
   }
   *(uint4*)dst = pack8(o1);
   *(uint4*)(dst + 32) = pack8(o2);
 }
 
 // ---------------------------------------------------------------------------------- SwiGLU
+// gate / up columns of activation column c: halves [g | u] (il = 0), or interleaved 16-column
+// groups [g0..g15 u0..u15 g16..] (il = 1: the layout the gate/up GEMM's SwiGLU epilogue writes,
+// csrc/pgemm.hip EPI 1 / 2); c a multiple of 8
+__device__ __forceinline__ int64_t gate_col(int c, int F, int il) {
+  return il ? 32 * (c >> 4) + (c & 15) : c;
+}
+__device__ __forceinline__ int64_t up_col(int c, int F, int il) {
+  return il ? 32 * (c >> 4) + 16 + (c & 15) : F + c;
+}
+
 __global__ __launch_bounds__(256) void swiglu_fwd_kernel(const bf16_t* __restrict__ gu,
                                                          bf16_t* __restrict__ h, int64_t rows,
-                                                         int F) {
+                                                         int F, int il) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;   // 8-element chunk of h
   const int64_t nch = rows * (F >> 3);
   if (i >= nch) return;
   const int64_t r = i / (F >> 3);
   const int c = (int)(i % (F >> 3)) * 8;
   float gv[8], uv[8], o[8];
-  unpack8(*(const uint4*)(gu + r * 2 * F + c), gv);
-  unpack8(*(const uint4*)(gu + r * 2 * F + F + c), uv);
+  unpack8(*(const uint4*)(gu + r * 2 * F + gate_col(c, F, il)), gv);
+  unpack8(*(const uint4*)(gu + r * 2 * F + up_col(c, F, il)), uv);
 #pragma unroll
   for (int e = 0; e < 8; ++e) o[e] = gv[e] / (1.f + __expf(-gv[e])) * uv[e];
   *(uint4*)(h + r * F + c) = pack8(o);
@@ -288,15 +322,16 @@ __global__ __launch_bounds__(256) void swiglu_fwd_kernel(const bf16_t* __restric
 __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const bf16_t* __restrict__ gu,
                                                          const bf16_t* __restrict__ dh,
                                                          bf16_t* __restrict__ dgu, int64_t rows,
-                                                         int F) {
+                                                         int F, int il) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t nch = rows * (F >> 3);
   if (i >= nch) return;
   const int64_t r = i / (F >> 3);
   const int c = (int)(i % (F >> 3)) * 8;
   float gv[8], uv[8], dv[8], dg[8], du[8];
-  unpack8(*(const uint4*)(gu + r * 2 * F + c), gv);
-  unpack8(*(const uint4*)(gu + r * 2 * F + F + c), uv);
+  const int64_t cg = gate_col(c, F, il), cu = up_col(c, F, il);
+  unpack8(*(const uint4*)(gu + r * 2 * F + cg), gv);
+  unpack8(*(const uint4*)(gu + r * 2 * F + cu), uv);
   unpack8(*(const uint4*)(dh + r * F + c), dv);
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -305,8 +340,8 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const bf16_t* __restric
     du[e] = dv[e] * silu;
     dg[e] = dv[e] * uv[e] * sg * (1.f + gv[e] * (1.f - sg));
   }
-  *(uint4*)(dgu + r * 2 * F + c) = pack8(dg);
-  *(uint4*)(dgu + r * 2 * F + F + c) = pack8(du);
+  *(uint4*)(dgu + r * 2 * F + cg) = pack8(dg);
+  *(uint4*)(dgu + r * 2 * F + cu) = pack8(du);
 }
 
 // ---------------------------------------------------------------------------------- loss
@@ -864,35 +899,39 @@ int mopt_rmsnorm_bwd_res(const void* x, const void* w, const void* dy, const voi
   return (int)hipGetLastError();
 }
 
+// il: interleaved pairs (2j, 2j + 1) instead of rotate-half pairs (j, j + 32) -- the layout the
+// QKV GEMM's RoPE epilogue writes (csrc/pgemm.hip EPI 3)
 int mopt_rope_fwd(const void* qkv, const void* cosv, const void* sinv, void* q, void* k, void* v,
-                  int rows, int T, int H, void* stream) {
+                  int rows, int T, int H, int il, void* stream) {
   const int64_t total = (int64_t)rows * 3 * H * 4;
   hipLaunchKernelGGL(rope_fwd_kernel, grid1(total), dim3(256), 0, (hipStream_t)stream,
                      (const bf16_t*)qkv, (const float*)cosv, (const float*)sinv, (bf16_t*)q,
-                     (bf16_t*)k, (bf16_t*)v, rows, T, H);
+                     (bf16_t*)k, (bf16_t*)v, rows, T, H, il);
   return (int)hipGetLastError();
 }
 
 int mopt_rope_bwd(const void* dq, const void* dk, const void* dv, const void* cosv,
-                  const void* sinv, void* dqkv, int rows, int T, int H, void* stream) {
+                  const void* sinv, void* dqkv, int rows, int T, int H, int il, void* stream) {
   const int64_t total = (int64_t)rows * 3 * H * 4;
   hipLaunchKernelGGL(rope_bwd_kernel, grid1(total), dim3(256), 0, (hipStream_t)stream,
                      (const bf16_t*)dq, (const bf16_t*)dk, (const bf16_t*)dv, (const float*)cosv,
-                     (const float*)sinv, (bf16_t*)dqkv, rows, T, H);
+                     (const float*)sinv, (bf16_t*)dqkv, rows, T, H, il);
   return (int)hipGetLastError();
 }
 
-int mopt_swiglu_fwd(const void* gu, void* h, int64_t rows, int F, void* stream) {
-  if (F % 8) return 1;
+// il: gate / up in interleaved 16-column groups (F a multiple of 16) instead of two halves
+int mopt_swiglu_fwd(const void* gu, void* h, int64_t rows, int F, int il, void* stream) {
+  if (F % 8 || (il && F % 16)) return 1;
   hipLaunchKernelGGL(swiglu_fwd_kernel, grid1(rows * (F / 8)), dim3(256), 0, (hipStream_t)stream,
-                     (const bf16_t*)gu, (bf16_t*)h, rows, F);
+                     (const bf16_t*)gu, (bf16_t*)h, rows, F, il);
   return (int)hipGetLastError();
 }
 
-int mopt_swiglu_bwd(const void* gu, const void* dh, void* dgu, int64_t rows, int F, void* stream) {
-  if (F % 8) return 1;
+int mopt_swiglu_bwd(const void* gu, const void* dh, void* dgu, int64_t rows, int F, int il,
+                    void* stream) {
+  if (F % 8 || (il && F % 16)) return 1;
   hipLaunchKernelGGL(swiglu_bwd_kernel, grid1(rows * (F / 8)), dim3(256), 0, (hipStream_t)stream,
-                     (const bf16_t*)gu, (const bf16_t*)dh, (bf16_t*)dgu, rows, F);
+                     (const bf16_t*)gu, (const bf16_t*)dh, (bf16_t*)dgu, rows, F, il);
   return (int)hipGetLastError();
 }
 

@@ -162,6 +162,15 @@ struct GemmArgs {
   int64_t a_in, b_in, c_in;
   int P, M, N, K, ldc;
   int tiles_m, tiles_n, splits, k_per_split, nwg;
+  // SwiGLU epilogue of the big-tile kernel (EPI 1, see pgemm_big_kernel): the activation
+  // h [P][M][N / 2] written next to C
+  bf16_t* H;
+  int64_t sX;
+  int ldx;
+  // RoPE epilogue (EPI 3): cos / sin tables [T][32] f32, sequence length, heads
+  const float* cosT;
+  const float* sinT;
+  int T, nH;
 };
 
 __device__ __forceinline__ int64_t boff(int p, int nin, int64_t so, int64_t si) {
@@ -401,7 +410,16 @@ struct GImg {
   }
 };
 
-template <bool TA, bool TB, int WM, int FM, int FN>
+__device__ __forceinline__ float silu_f(float x) { return x / (1.f + __expf(-x)); }
+
+// EPI 0: C = A B.  EPI 1, the SwiGLU of the LM's MLP (gate / up in interleaved 16-column
+// groups [g0..g15 u0..u15 g16..], so a lane's fragments j (gate) and j + 1 (up) hold the two
+// halves of the same four activation columns -- lm_ops.hip swiglu kernels, il = 1): C = gu = A B
+// as usual, plus h = silu(g) u into g.H (row stride g.ldx = N / 2) from the bf16-rounded g and
+// u -- the separate SwiGLU pass (reads gu, writes h) disappears.  (An EPI 2 writing dgu from the
+// dh = dy wdown^T product, g and u loaded per fragment, doubled that GEMM's time and saved
+// nothing; removed in round 4, profiles/round4.md.)
+template <bool TA, bool TB, int WM, int FM, int FN, int EPI = 0>
 __global__ __launch_bounds__(512) void pgemm_big_kernel(const GemmArgs g) {
   constexpr int WN = 8 / WM;
   constexpr int BM = WM * 16 * FM, BN = WN * 16 * FN;
@@ -509,6 +527,63 @@ __global__ __launch_bounds__(512) void pgemm_big_kernel(const GemmArgs g) {
       p = np; m0 = nm0; n0 = nn0; k0 = nk0;
       continue;
     }
+    if constexpr (EPI == 3) {
+      // lane (li, gq) holds qkv[m][n .. n + 3] of fragment (i, j), n = 16 j + 4 gq (+ origin):
+      // section n / d (q, k, v), head (n % d) / 64, head column c = n % 64; the row is token t =
+      // m % T of sequence m / T.  q and k are rotated by interleaved pairs (c, c+1), (c+2, c+3)
+      // at angles c / 2, c / 2 + 1; out = C + sec (P M d) + ((b' H + head) T + t) 64 + c with
+      // b' = p (M / T) + m / T -- the [3][B'][H][T][64] layout the attention kernels read.
+      const int dm = g.nH * 64;
+      const int64_t sec_stride = (int64_t)g.P * g.M * dm;
+      const int bper = g.M / g.T;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int m = m0 + wm * 16 * FM + 16 * i + li;
+        const int bl = m / g.T, t = m - bl * g.T;
+        const int64_t bq = (int64_t)p * bper + bl;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int n = n0 + wn * 16 * FN + 16 * j + 4 * gq;
+          const int sec = n / dm, hc = n - sec * dm, hh = hc >> 6, c = hc & 63;
+          float x[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) x[r] = bf2f(f2bf(acc[i][j][r]));   // qkv as stored
+          if (sec < 2) {
+            const float* cs = g.cosT + (int64_t)t * 32 + (c >> 1);
+            const float* sn = g.sinT + (int64_t)t * 32 + (c >> 1);
+#pragma unroll
+            for (int q2 = 0; q2 < 2; ++q2) {
+              const float a = x[2 * q2], b = x[2 * q2 + 1], co = cs[q2], si = sn[q2];
+              x[2 * q2] = a * co - b * si;
+              x[2 * q2 + 1] = b * co + a * si;
+            }
+          }
+          bf16_t* o = g.C + sec * sec_stride + ((bq * g.nH + hh) * g.T + t) * 64 + c;
+          *(uint2*)o = make_uint2(pack2bf(x[0], x[1]), pack2bf(x[2], x[3]));
+        }
+      }
+      if (!has_next) break;
+      vb = nvb;
+      p = np; m0 = nm0; n0 = nn0; k0 = nk0;
+      continue;
+    }
+    if constexpr (EPI == 1) {
+      // h[m][(n0 + wn 16 FN) / 2 + 16 (j / 2) + 4 gq + r] from fragments j (gate), j + 1 (up)
+      bf16_t* Hp = g.H + p * g.sX + (int64_t)(m0 + wm * 16 * FM + li) * g.ldx +
+                   (n0 + wn * 16 * FN) / 2 + 4 * gq;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+#pragma unroll
+        for (int j = 0; j < FN; j += 2) {
+          float hv[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            hv[r] = silu_f(bf2f(f2bf(acc[i][j][r]))) * bf2f(f2bf(acc[i][j + 1][r]));
+          *(uint2*)(Hp + (int64_t)(16 * i) * g.ldx + 8 * j) =
+              make_uint2(pack2bf(hv[0], hv[1]), pack2bf(hv[2], hv[3]));
+        }
+      }
+    }
     // Epilogue without LDS: pack 4 columns per fragment to bf16, then exchange between the lane
     // rows gq = 0|1 (and 2|3) with v_permlane16_swap so every lane holds 8 consecutive columns of
     // one row; per fragment pair (j, j+1) each row gets 64 contiguous bytes in one dwordx4 store.
@@ -569,12 +644,13 @@ int launch(GemmArgs g, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-template <bool TA, bool TB, int WM, int FM, int FN>
+template <bool TA, bool TB, int WM, int FM, int FN, int EPI = 0>
 int launch_big(GemmArgs g, hipStream_t st) {
   constexpr int BM = WM * 16 * FM, BN = (8 / WM) * 16 * FN;
   if (g.M % BM || g.N % BN || g.k_per_split % BK || g.k_per_split < BK ||
       (int64_t)g.k_per_split * g.splits != g.K || (g.splits > 1 && g.part == nullptr) ||
-      g.nin > 1)
+      g.nin > 1 || (EPI != 0 && g.splits != 1) || (EPI == 1 && g.H == nullptr) ||
+      (EPI == 3 && (g.cosT == nullptr || g.T <= 0 || g.M % g.T || g.N != 3 * 64 * g.nH)))
     return (int)hipErrorInvalidValue;
   g.tiles_m = g.M / BM;
   g.tiles_n = g.N / BN;
@@ -584,7 +660,7 @@ int launch_big(GemmArgs g, hipStream_t st) {
   // persistent: one workgroup per CU (the LDS stages allow no second one), a multiple of 8
   constexpr int kGrid = 256;
   const int grid = nwg < kGrid ? (int)nwg : kGrid;
-  hipLaunchKernelGGL((pgemm_big_kernel<TA, TB, WM, FM, FN>), dim3(grid), dim3(512), 0, st, g);
+  hipLaunchKernelGGL((pgemm_big_kernel<TA, TB, WM, FM, FN, EPI>), dim3(grid), dim3(512), 0, st, g);
   return (int)hipGetLastError();
 }
 
@@ -687,6 +763,68 @@ int mopt_pgemm(const void* A, const void* B, void* C, void* part, int P, int M, 
   else err = dispatch_tile<kDense, kDense, true, true>(g, cfg, st);
   if (err || splits == 1) return err;
   return finish_splitk(g, st);
+}
+
+// The SwiGLU epilogue of the big-tile kernel (pgemm_big_kernel EPI 1): C = A B (the gate / up
+// product [M][N], interleaved 16-column groups) and X = h [M][N / 2] (row stride ldx, batch
+// stride sX).  Big-tile configurations (5, 6, 7, 11) of an NN product without K splits only --
+// hipErrorNotSupported otherwise (the caller then runs pgemm + the swiglu kernel with il = 1).
+int mopt_pgemm_swiglu(const void* A, const void* B, void* C, void* X, int P, int M, int N, int K,
+                      int lda, int ldb, int ldc, int ldx, int64_t sA, int64_t sB, int64_t sC,
+                      int64_t sX, int cfg, void* stream) {
+  if (P <= 0 || M <= 0 || N <= 0 || K <= 0) return 0;
+  if (N % 32) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  GemmArgs g{};
+  g.a = dense(A, sA, lda, M, K);
+  g.b = dense(B, sB, ldb, K, N);
+  g.C = (bf16_t*)C;
+  g.sC = sC;
+  g.P = P; g.M = M; g.N = N; g.K = K; g.ldc = ldc;
+  g.splits = 1;
+  g.k_per_split = K;
+  g.H = (bf16_t*)X;
+  g.sX = sX;
+  g.ldx = ldx;
+  switch (cfg) {
+    case 5: return launch_big<false, false, 2, 8, 4, 1>(g, st);
+    case 6: return launch_big<false, false, 4, 4, 4, 1>(g, st);
+    case 7: return launch_big<false, false, 2, 4, 4, 1>(g, st);
+    case 11: return launch_big<false, false, 4, 4, 6, 1>(g, st);
+    default: return (int)hipErrorNotSupported;
+  }
+}
+
+// The QKV projection with RoPE in the big-tile GEMM's epilogue (pgemm_big_kernel EPI 3):
+// out [3][P (M / T)][H][T][64] = the q, k, v heads of A [P][M][d] @ B [P][d][3 d] (d = 64 H),
+// q and k rotated by interleaved pairs (cos / sin [T][32]).  NN, big tiles without K splits
+// (M a multiple of T) -- hipErrorNotSupported otherwise (the caller runs pgemm + mopt_rope_fwd
+// with il = 1).
+int mopt_pgemm_qkv_rope(const void* A, const void* B, void* out, const void* cosT,
+                        const void* sinT, int P, int M, int K, int T, int nH, int lda, int ldb,
+                        int64_t sA, int64_t sB, int cfg, void* stream) {
+  const int N = 3 * 64 * nH;
+  if (P <= 0 || M <= 0 || K <= 0) return 0;
+  if (T <= 0 || M % T) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  GemmArgs g{};
+  g.a = dense(A, sA, lda, M, K);
+  g.b = dense(B, sB, ldb, K, N);
+  g.C = (bf16_t*)out;
+  g.P = P; g.M = M; g.N = N; g.K = K; g.ldc = N;
+  g.splits = 1;
+  g.k_per_split = K;
+  g.cosT = (const float*)cosT;
+  g.sinT = (const float*)sinT;
+  g.T = T;
+  g.nH = nH;
+  switch (cfg) {
+    case 5: return launch_big<false, false, 2, 8, 4, 3>(g, st);
+    case 6: return launch_big<false, false, 4, 4, 4, 3>(g, st);
+    case 7: return launch_big<false, false, 2, 4, 4, 3>(g, st);
+    case 11: return launch_big<false, false, 4, 4, 6, 3>(g, st);
+    default: return (int)hipErrorNotSupported;
+  }
 }
 
 // mopt_pgemm with f32 operands and f32 output (a32/b32/c32 all 1; the register-staged tiles

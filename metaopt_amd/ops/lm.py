@@ -31,10 +31,14 @@ _lib.register_signatures({
     "mopt_rmsnorm_bwd_res": ([c_void_p] * 7 + [c_int, c_int, c_int, c_void_p], c_int),
     "mopt_rmsnorm_dw_splits": ([c_int], c_int),
     "mopt_rmsnorm_dw16": ([c_void_p] * 5 + [c_int, c_int, c_int, c_void_p], c_int),
-    "mopt_rope_fwd": ([c_void_p] * 6 + [c_int, c_int, c_int, c_void_p], c_int),
-    "mopt_rope_bwd": ([c_void_p] * 6 + [c_int, c_int, c_int, c_void_p], c_int),
-    "mopt_swiglu_fwd": ([c_void_p, c_void_p, c_int64, c_int, c_void_p], c_int),
-    "mopt_swiglu_bwd": ([c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p], c_int),
+    "mopt_rope_fwd": ([c_void_p] * 6 + [c_int] * 4 + [c_void_p], c_int),
+    "mopt_rope_bwd": ([c_void_p] * 6 + [c_int] * 4 + [c_void_p], c_int),
+    "mopt_pgemm_qkv_rope": ([c_void_p] * 5 + [c_int] * 7 + [c_int64, c_int64, c_int, c_void_p],
+                            c_int),
+    "mopt_swiglu_fwd": ([c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p], c_int),
+    "mopt_swiglu_bwd": ([c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p], c_int),
+    "mopt_pgemm_swiglu": ([c_void_p] * 4 + [c_int] * 8 + [c_int64] * 4 + [c_int, c_void_p],
+                          c_int),
     "mopt_ce_fwd_bwd": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_int,
                          c_void_p], c_int),
     "mopt_embed_fwd": ([c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_void_p],
@@ -95,15 +99,20 @@ def rope_tables(T: int, base: float = 10000.0, device=None):
             torch.sin(ang).float().contiguous().to(device))
 
 
-def rope_split_ref(qkv, cos, sin, T, H):
+def rope_split_ref(qkv, cos, sin, T, H, il=False):
+    """q, k, v heads [B', H, T, 64] of the QKV activation [B' T, 3 H 64], q and k rotated by
+    rotate-half pairs (j, j + 32) or (``il``) interleaved pairs (2j, 2j + 1) at angle j."""
     R = qkv.shape[0]
     Bp = R // T
     x = qkv.float().view(Bp, T, 3, H, 64).permute(2, 0, 3, 1, 4)  # [3, B', H, T, 64]
     q, k, v = x[0], x[1], x[2]
 
     def rot(t):
-        t1, t2 = t[..., :32], t[..., 32:]
         c, s = cos[None, None], sin[None, None]
+        if il:
+            t1, t2 = t[..., 0::2], t[..., 1::2]
+            return torch.stack([t1 * c - t2 * s, t2 * c + t1 * s], -1).flatten(-2)
+        t1, t2 = t[..., :32], t[..., 32:]
         return torch.cat([t1 * c - t2 * s, t2 * c + t1 * s], -1)
     return (rot(q).to(qkv.dtype).contiguous(), rot(k).to(qkv.dtype).contiguous(),
             v.to(qkv.dtype).contiguous())
@@ -119,9 +128,18 @@ def attention_ref(q, k, v, scale):
     return o.permute(0, 2, 1, 3).reshape(Bp * T, H * Dh).to(q.dtype)
 
 
-def swiglu_ref(gu):
+def swiglu_split(gu, il=False):
+    """(gate, up) of a gate/up activation: two halves, or (``il``) interleaved 16-column groups
+    [g0..g15 u0..u15 g16..] -- the layout of the fused gate/up GEMM epilogue (pgemm.hip EPI)."""
     F = gu.shape[-1] // 2
-    g, u = gu.float()[..., :F], gu.float()[..., F:]
+    if not il:
+        return gu[..., :F], gu[..., F:]
+    v = gu.reshape(*gu.shape[:-1], F // 16, 2, 16)
+    return v[..., 0, :].reshape(*gu.shape[:-1], F), v[..., 1, :].reshape(*gu.shape[:-1], F)
+
+
+def swiglu_ref(gu, il=False):
+    g, u = swiglu_split(gu.float(), il)
     return (torch.nn.functional.silu(g) * u).to(gu.dtype)
 
 
@@ -258,7 +276,7 @@ class _RopeSplit(torch.autograd.Function):
         shape = (Bp, H, T, 64)
         q = torch.empty(shape, dtype=qkv.dtype, device=qkv.device)
         k, v = torch.empty_like(q), torch.empty_like(q)
-        _call("mopt_rope_fwd", _p(qkv), _p(cos), _p(sin), _p(q), _p(k), _p(v), R, T, H,
+        _call("mopt_rope_fwd", _p(qkv), _p(cos), _p(sin), _p(q), _p(k), _p(v), R, T, H, 0,
               _stream(qkv))
         ctx.save_for_backward(cos, sin)
         ctx.dims = (R, T, H, qkv.shape)
@@ -270,7 +288,7 @@ class _RopeSplit(torch.autograd.Function):
         R, T, H, shape = ctx.dims
         dqkv = torch.empty(shape, dtype=dq.dtype, device=dq.device)
         _call("mopt_rope_bwd", _p(dq.contiguous()), _p(dk.contiguous()), _p(dv.contiguous()),
-              _p(cos), _p(sin), _p(dqkv), R, T, H, _stream(dq))
+              _p(cos), _p(sin), _p(dqkv), R, T, H, 0, _stream(dq))
         return dqkv, None, None, None, None
 
 
@@ -278,6 +296,60 @@ def rope_split(qkv, cos, sin, T, H):
     if _hip(qkv, "rope"):
         return _RopeSplit.apply(qkv.contiguous(), cos, sin, T, H)
     return rope_split_ref(qkv, cos, sin, T, H)
+
+
+class _QKVRope(torch.autograd.Function):
+    """q, k, v = rope(h @ wqkv) per trial with interleaved RoPE pairs: the big-tile GEMM writes
+    the rotated heads in its epilogue (csrc/pgemm.hip EPI 3; no QKV activation, no RoPE pass).
+    Backward: the inverse rotation back into the [rows, 3 d] gradient, then its two GEMMs."""
+
+    @staticmethod
+    def forward(ctx, h, w, cos, sin, T, H, g_w):
+        from .gemm import LARGE_TILES, pgemm, plan
+        P, R, d = h.shape
+        Bp = P * (R // T)
+        buf = torch.empty(3, Bp, H, T, 64, dtype=h.dtype, device=h.device)
+        cfg, splits, _ = plan(P, R, 3 * d, d)
+        rc = 801
+        if cfg in LARGE_TILES and splits == 1 and R % T == 0:
+            rc = _lib.get_lib().mopt_pgemm_qkv_rope(
+                _p(h), _p(w), _p(buf), _p(cos), _p(sin), P, R, d, T, H, h.stride(1),
+                w.stride(1), h.stride(0), w.stride(0), cfg, _stream(h))
+        if rc == 801:                      # no big tile for this shape: GEMM + RoPE pass
+            qkv = pgemm(h, w)
+            _call("mopt_rope_fwd", _p(qkv), _p(cos), _p(sin), _p(buf[0]), _p(buf[1]),
+                  _p(buf[2]), P * R, T, H, 1, _stream(h))
+        else:
+            _lib.check(rc, "mopt_pgemm_qkv_rope")
+        ctx.save_for_backward(h, w, cos, sin)
+        ctx.dims = (T, H)
+        ctx.g_w = g_w
+        return buf[0], buf[1], buf[2]
+
+    @staticmethod
+    def backward(ctx, dq, dk, dv):
+        from .gemm import pgemm
+        h, w, cos, sin = ctx.saved_tensors
+        T, H = ctx.dims
+        P, R, d = h.shape
+        dqkv = torch.empty(P, R, 3 * d, dtype=h.dtype, device=h.device)
+        _call("mopt_rope_bwd", _p(dq.contiguous()), _p(dk.contiguous()), _p(dv.contiguous()),
+              _p(cos), _p(sin), _p(dqkv), P * R, T, H, 1, _stream(h))
+        dw = None
+        if ctx.g_w is not None:
+            pgemm(h, dqkv, ta=True, out=ctx.g_w)
+        else:
+            dw = pgemm(h, dqkv, ta=True)
+        return pgemm(dqkv, w, tb=True), dw, None, None, None, None, None
+
+
+def qkv_rope(h, w, cos, sin, T, H):
+    """(q, k, v) heads [B', H, T, 64] of ``h [P, R, d] @ w [P, d, 3 d]`` with interleaved-pair
+    RoPE on q and k (the LM's attention input)."""
+    if _hip(h, "rope"):
+        return _QKVRope.apply(h.contiguous(), w.contiguous(), cos, sin, T, H, _grad_view(w))
+    P, R, d = h.shape
+    return rope_split_ref(torch.bmm(h, w).reshape(P * R, 3 * d), cos, sin, T, H, il=True)
 
 
 class _Attention(torch.autograd.Function):
@@ -318,7 +390,7 @@ class _SwiGLU(torch.autograd.Function):
     def forward(ctx, gu):
         rows, F2 = gu.shape[0] * (gu.shape[1] if gu.dim() == 3 else 1), gu.shape[-1]
         h = torch.empty(*gu.shape[:-1], F2 // 2, dtype=gu.dtype, device=gu.device)
-        _call("mopt_swiglu_fwd", _p(gu), _p(h), rows, F2 // 2, _stream(gu))
+        _call("mopt_swiglu_fwd", _p(gu), _p(h), rows, F2 // 2, 0, _stream(gu))
         ctx.save_for_backward(gu)
         return h
 
@@ -327,7 +399,7 @@ class _SwiGLU(torch.autograd.Function):
         (gu,) = ctx.saved_tensors
         rows, F2 = gu.numel() // gu.shape[-1], gu.shape[-1]
         dgu = torch.empty_like(gu)
-        _call("mopt_swiglu_bwd", _p(gu), _p(dh.contiguous()), _p(dgu), rows, F2 // 2,
+        _call("mopt_swiglu_bwd", _p(gu), _p(dh.contiguous()), _p(dgu), rows, F2 // 2, 0,
               _stream(gu))
         return dgu
 
@@ -336,6 +408,79 @@ def swiglu(gu):
     if _hip(gu, "swiglu"):
         return _SwiGLU.apply(gu.contiguous())
     return swiglu_ref(gu)
+
+
+def _swiglu_gemm(a, b, c, x):
+    """``c = a @ b`` (the gate / up product) with the SwiGLU activation ``x`` written by the
+    big-tile GEMM's epilogue (csrc/pgemm.hip EPI 1); False when the shape's plan has no big tile
+    or splits K (the caller runs the GEMM and the swiglu kernel)."""
+    from .gemm import LARGE_TILES, plan
+    P, M, K = a.shape
+    N = b.shape[2]
+    cfg, splits, _ = plan(P, M, N, K)
+    if cfg not in LARGE_TILES or splits != 1 or N % 32:
+        return False
+    rc = _lib.get_lib().mopt_pgemm_swiglu(
+        _p(a), _p(b), _p(c), _p(x), P, M, N, K, a.stride(1), b.stride(1), c.stride(1),
+        x.stride(1), a.stride(0), b.stride(0), c.stride(0), x.stride(0), cfg, _stream(a))
+    if rc == 801:                          # hipErrorNotSupported
+        return False
+    _lib.check(rc, "mopt_pgemm_swiglu")
+    return True
+
+
+class _SwiGLUMLP(torch.autograd.Function):
+    """``swiglu(h @ wgu) @ wdown`` of every trial, gate / up columns interleaved in 16-column
+    groups.  Forward: the gate/up GEMM writes the activation in its epilogue (no SwiGLU pass).
+    The weight gradients go straight into the flat gradient buffer's views when given."""
+
+    @staticmethod
+    def forward(ctx, h, wgu, wdown, g_gu, g_down):
+        from .gemm import pgemm
+        P, R, _ = h.shape
+        F = wdown.shape[1]
+        gu = torch.empty(P, R, 2 * F, dtype=h.dtype, device=h.device)
+        a = torch.empty(P, R, F, dtype=h.dtype, device=h.device)
+        if not _swiglu_gemm(h, wgu, gu, a):
+            pgemm(h, wgu, out=gu)
+            _call("mopt_swiglu_fwd", _p(gu), _p(a), P * R, F, 1, _stream(h))
+        ctx.save_for_backward(h, wgu, wdown, gu, a)
+        ctx.grads = (g_gu, g_down)
+        return pgemm(a, wdown)
+
+    @staticmethod
+    def backward(ctx, dy):
+        from .gemm import pgemm
+        h, wgu, wdown, gu, a = ctx.saved_tensors
+        g_gu, g_down = ctx.grads
+        dy = dy.contiguous()
+        P, R, _ = h.shape
+        F = wdown.shape[1]
+        dwdown = dwgu = None
+        if g_down is not None:
+            pgemm(a, dy, ta=True, out=g_down)
+        else:
+            dwdown = pgemm(a, dy, ta=True)
+        # (a dgu epilogue on the dh GEMM -- g, u loaded per fragment -- doubled that GEMM and
+        # saved nothing: profiles/round4.md; the backward keeps the separate pass)
+        dgu = torch.empty_like(gu)
+        dh = pgemm(dy, wdown, tb=True)
+        _call("mopt_swiglu_bwd", _p(gu), _p(dh), _p(dgu), P * R, F, 1, _stream(dy))
+        if g_gu is not None:
+            pgemm(h, dgu, ta=True, out=g_gu)
+        else:
+            dwgu = pgemm(h, dgu, ta=True)
+        dh_in = pgemm(dgu, wgu, tb=True)
+        return dh_in, dwgu, dwdown, None, None
+
+
+def swiglu_mlp(h, wgu, wdown):
+    """``swiglu(h @ wgu) @ wdown`` per trial: h [P, R, d], wgu [P, d, 2F] (gate / up in
+    interleaved 16-column groups, :func:`swiglu_split`), wdown [P, F, d]."""
+    if _hip(h, "swiglu"):
+        return _SwiGLUMLP.apply(h.contiguous(), wgu.contiguous(), wdown.contiguous(),
+                                _grad_view(wgu), _grad_view(wdown))
+    return torch.bmm(swiglu_ref(torch.bmm(h, wgu), il=True), wdown)
 
 
 class _CrossEntropy(torch.autograd.Function):

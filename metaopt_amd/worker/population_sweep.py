@@ -638,14 +638,14 @@ class PopulationSweep:
         owner = self.ckpt_index.get(ckey)
         src, resume = -1, -1
         if sidecar is not None:
-            rank = max(range(W), key=n_free.__getitem__)
+            rank = n_free.index(max(n_free))        # the least-loaded rank, lowest first
             action, resume = RESUME_FILE, sidecar
         elif owner is not None and n_free[owner[0]]:
             # resume next to the checkpoint (no copy between GPUs)
             rank = owner[0]
             action, resume, src = RESUME, owner[1], owner[0]
         else:
-            rank = max(range(W), key=n_free.__getitem__) if W > 1 else 0
+            rank = n_free.index(max(n_free)) if W > 1 else 0
             side = self._sidecar_index.get(ckey)
             if owner is not None:   # C4: the owner sends the checkpoint to that rank (P2P)
                 action, resume, src = RESUME, owner[1], owner[0]

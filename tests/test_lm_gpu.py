@@ -359,3 +359,59 @@ def test_embedding_backward_into_flat_gradient_sorted():
     ops.embed_ref(tok, tr, rpt).backward(g.float())
     _close(grads[0], tr.grad, 1e-2)
     assert (grads[0][:, 64:] == 0).all()
+
+
+@pytest.mark.parametrize("P,R,d,F,big", [(8, 2048, 256, 512, True), (2, 64, 64, 64, False)])
+def test_swiglu_mlp_epilogues_match_reference(P, R, d, F, big):
+    """swiglu(h @ wgu) @ wdown with the SwiGLU in the gate/up GEMM's epilogue (gate / up
+    interleaved in 16-column groups; pgemm.hip EPI 1) -- or, on shapes without a big tile, the
+    GEMM + interleaved swiglu kernel -- against fp32 autograd: output and the gradients of h,
+    wgu and wdown (backward: GEMMs + the interleaved swiglu backward kernel)."""
+    from metaopt_amd.ops.gemm import LARGE_TILES, plan
+    torch.manual_seed(3)
+    assert (plan(P, R, 2 * F, d)[0] in LARGE_TILES) == big
+    h = (torch.randn(P, R, d, device=DEV) * 0.5).to(torch.bfloat16)
+    wgu = (torch.randn(P, d, 2 * F, device=DEV) / d ** 0.5).to(torch.bfloat16)
+    wdown = (torch.randn(P, F, d, device=DEV) / F ** 0.5).to(torch.bfloat16)
+    dy = torch.randn(P, R, d, device=DEV).to(torch.bfloat16)
+    hs, gs, ds = (t.clone().requires_grad_(True) for t in (h, wgu, wdown))
+    y = ops.swiglu_mlp(hs, gs, ds)
+    y.backward(dy)
+    hr, gr, dr = (t.float().clone().requires_grad_(True) for t in (h, wgu, wdown))
+    yr = torch.bmm(ops.swiglu_ref(torch.bmm(hr, gr), il=True), dr)
+    yr.backward(dy.float())
+    torch.cuda.synchronize()
+
+    def rel(a, b):
+        return float((a.float() - b).norm() / b.norm())
+    assert rel(y, yr) < 2e-2, rel(y, yr)
+    for got, ref in ((hs.grad, hr.grad), (gs.grad, gr.grad), (ds.grad, dr.grad)):
+        assert rel(got, ref) < 3e-2, rel(got, ref)
+
+
+@pytest.mark.parametrize("P,B,T,H,big", [(8, 4, 512, 4, True), (2, 2, 64, 2, False)])
+def test_qkv_rope_epilogue_matches_reference(P, B, T, H, big):
+    """q, k, v = rope(h @ wqkv) with interleaved RoPE pairs applied in the QKV GEMM's epilogue
+    (pgemm.hip EPI 3) -- or, without a big tile, the GEMM + the interleaved RoPE kernel --
+    against fp32 autograd of rope_split_ref(il=True): the three head tensors and the gradients
+    of h and wqkv."""
+    from metaopt_amd.ops.gemm import LARGE_TILES, plan
+    torch.manual_seed(9)
+    d, R = 64 * H, B * T
+    assert (plan(P, R, 3 * d, d)[0] in LARGE_TILES) == big
+    h = (torch.randn(P, R, d, device=DEV) * 0.5).to(torch.bfloat16)
+    w = (torch.randn(P, d, 3 * d, device=DEV) / d ** 0.5).to(torch.bfloat16)
+    cos, sin = ops.rope_tables(T, device=DEV)
+    hs, ws = h.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    outs = ops.qkv_rope(hs, ws, cos, sin, T, H)
+    gs = [torch.randn_like(o) for o in outs]
+    torch.autograd.backward(list(outs), gs)
+    hr, wr = h.float().requires_grad_(True), w.float().requires_grad_(True)
+    refs = ops.rope_split_ref(torch.bmm(hr, wr).reshape(P * R, 3 * d), cos, sin, T, H, il=True)
+    torch.autograd.backward(list(refs), [g.float() for g in gs])
+    torch.cuda.synchronize()
+    for o, r in zip(outs, refs):
+        assert o.shape == r.shape
+        _close(o, r, 2e-2)
+    _close(hs.grad, hr.grad, 3e-2)
+    _close(ws.grad, wr.grad, 3e-2)
