@@ -181,16 +181,17 @@ class ASHA(BaseAlgorithm):
             probs = numpy.array([p * int(not b.is_filled) for p, b in zip(probs, current)])
             if probs.sum() <= 0:
                 break
-            picks = self.rng.choice(len(current), size=len(pts), p=probs / probs.sum())
+            picks = self.rng.choice(len(current), size=len(pts), p=probs / probs.sum()).tolist()
+            info, get_id = self.trial_info, self.get_id
+            rung0 = [b.rungs[0][0] for b in current]
             for point, idx in zip(pts, picks):
-                point = list(point)
-                point[fi] = current[idx].rungs[0][0]
-                point = tuple(point)
-                _id = self.get_id(point)
-                if _id in self.trial_info:
+                point = (*point[:fi], rung0[idx], *point[fi + 1:])
+                _id = get_id(point)
+                if _id in info:
                     continue
-                self.trial_info[_id] = current[idx]
-                current[idx]._register_at(0, point, None, False, _id)   # fidelity = rung 0's
+                b = current[idx]
+                info[_id] = b
+                b._register_at(0, point, None, False, _id)   # fidelity = rung 0's
                 out.append(point)
         else:
             if len(out) < n:
@@ -211,7 +212,8 @@ class ASHA(BaseAlgorithm):
             # python scalars: numpy 2 reprs np.float64 values as 'np.float64(..)', which would
             # give a sampled point and the same point observed back from storage two ids
             p = [v.item() if isinstance(v, numpy.generic) else v for v in key]
-            _id = hashlib.md5(str(p[:fi] + p[fi + 1:]).encode("utf-8")).hexdigest()
+            del p[fi]
+            _id = hashlib.md5(str(p).encode("utf-8")).hexdigest()
             if len(cache) > 1 << 20:
                 cache.clear()
             cache[key] = _id
