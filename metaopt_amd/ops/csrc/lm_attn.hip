@@ -88,6 +88,12 @@ __device__ __forceinline__ bf16x8 pack_frag(const f32x4& a, const f32x4& b) {
   return __builtin_bit_cast(bf16x8, w);
 }
 
+// v_exp_f32 alone: exp2f goes through the library's denormal-safe path (a compare, two selects,
+// an add and a rescale around every v_exp_f32) -- about 5 VALU per score, a third of the
+// backward kernels' VALU issue (round 4 PMC, profiles/round4.md).  Softmax terms below 2^-126
+// flush to zero, which changes no bf16 probability.
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 __device__ __forceinline__ float max4(float v) {
   v = fmaxf(v, __shfl_xor(v, 16, 64));
   return fmaxf(v, __shfl_xor(v, 32, 64));
@@ -168,13 +174,13 @@ __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnFwdWaves) void attn_fwd_k
         mx = fmaxf(mx, v);
       }
     const float m_new = fmaxf(m, max4(mx));
-    const float alpha = exp2f(m - m_new);
+    const float alpha = fast_exp2(m - m_new);
     float ls = 0.f;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = exp2f(st[j][r] - m_new);
+        const float p = fast_exp2(st[j][r] - m_new);
         st[j][r] = p;
         ls += p;
       }
@@ -275,7 +281,7 @@ __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnDqWaves) void attn_bwd_dq
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float p = exp2f(st[j][r] * c - lse);
+        float p = fast_exp2(st[j][r] * c - lse);
         if (kb == qb) {
           const int key = kb * BKV + 32 * (j >> 1) + 8 * g + 4 * (j & 1) + r;
           if (key > qrow) p = 0.f;
@@ -368,7 +374,7 @@ __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnDkdvWaves) void attn_bwd_
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int qi = 32 * (j >> 1) + 8 * g + 4 * (j & 1) + r;
-        float p = exp2f(st[j][r] * c - lse_s[qi]);
+        float p = fast_exp2(st[j][r] * c - lse_s[qi]);
         if (qb == kb && qb * BQ + qi < krow) p = 0.f;
         st[j][r] = p;
         dp[j][r] = p * (dp[j][r] - dsum_s[qi]);
