@@ -26,7 +26,9 @@ namespace {
 constexpr int D = 64;          // head dim
 constexpr int BQ = 64;         // queries per workgroup
 constexpr int BKV = 64;        // keys per block
-constexpr int LS = kLdsStride;
+constexpr int LS = kLdsStride;  // (a conflict-free XOR chunk swizzle of 128-byte rows, per
+                                // scripts/lds_banks.py, measured slower in round 4: dQ 87 -> 138
+                                // us, the per-access address math; profiles/round4.md)
 
 // Occupancy targets (waves per SIMD; 0 = the compiler's choice): the register cap that lets N
 // workgroups share a CU.  dQ at 4 (126 VGPRs, was 104 + 40 AGPRs = 3) and dK/dV at 3 (156, was
