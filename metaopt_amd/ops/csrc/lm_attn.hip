@@ -31,10 +31,17 @@ constexpr int LS = kLdsStride;  // (a conflict-free XOR chunk swizzle of 128-byt
                                 // us, the per-access address math; profiles/round4.md)
 
 // Occupancy targets (waves per SIMD; 0 = the compiler's choice): the register cap that lets N
-// workgroups share a CU.  dQ at 4 (126 VGPRs, was 104 + 40 AGPRs = 3) and dK/dV at 3 (156, was
-// 154 + 44 = 2) compile without spills and measured 110.9 -> 99.5 / 179.8 -> 157.7 us per call on
-// the 125M LM (profiles/round3.md); the forward spills below its 4 (124 registers), so it is left.
-constexpr int kAttnFwdWaves = 0, kAttnDqWaves = 4, kAttnDkdvWaves = 3;
+// workgroups share a CU.  Swept in round 4 on variant builds (scripts/attn_bench.py,
+// profiles/r4/attn_sweep_r4q.log; fwd / dQ+dK/dV us, two runs): 0,4,3 117 / 257; 4,4,3 101 / 263;
+// 3,4,3 109 / 267; 2,4,3 108 / 268; 0,3,3 117 / 261; 0,4,2 123 / 259; 0,5,3 123 / 350; 0,4,4
+// 121 / 386.  The forward at 4 waves (since the native exp2 it compiles without spills) and
+// dQ / dK/dV at 4 / 3 (round 3: 110.9 -> 99.5 / 179.8 -> 157.7 us per call).
+#ifndef MOPT_ATTN_WAVES          // "fwd, dq, dkdv" -- variant builds of scripts/attn_bench.py sweeps
+#define MOPT_ATTN_WAVES 4, 4, 3
+#endif
+constexpr int kAttnWaves[3] = {MOPT_ATTN_WAVES};
+constexpr int kAttnFwdWaves = kAttnWaves[0], kAttnDqWaves = kAttnWaves[1],
+              kAttnDkdvWaves = kAttnWaves[2];
 // (Measured and rejected, round 4: two 16-query / 16-key sets per wave -- 128 queries or keys
 // per workgroup, every LDS fragment feeding two MFMAs -- ran fwd 104 -> 157 us, dQ 98 -> 149,
 // dK/dV 156 -> 250 on the 125M LM: the doubled register state cost the occupancy that hides
