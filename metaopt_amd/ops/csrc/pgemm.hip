@@ -609,6 +609,10 @@ __global__ __launch_bounds__(512) void pgemm_big_kernel(const GemmArgs g) {
   }
 }
 
+// (Round 4: a register-pipelined variant -- the operands of K-step t + 3 loaded into one of two
+// register sets while step t is multiplied, written to the free LDS stage two steps later --
+// was correct but 2.5-4x slower: the two register sets on top of the accumulators exceed the
+// 256 VGPRs of two waves per SIMD and spill; profiles/round4.md.)
 // (A multi-stage variant -- BK = 32 images in 4-5 LDS stages, fills 3-4 K-steps ahead -- was
 // correct on every layout but 5-25 % slower than this 2-stage kernel on every LM shape; it was
 // removed in round 4, the A/B is in profiles/round3.md "LM GEMMs".)
