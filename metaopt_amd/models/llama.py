@@ -136,9 +136,10 @@ class PopulationLM(FlatPopulation):
         # every residual add is fused into the pre-norm that follows it (ops.add_rmsnorm)
         h = ops.rmsnorm(x, W["l0.attn_norm"], rpt, c.norm_eps)
         for l in range(c.n_layers):
-            # interleaved-pair RoPE applied by the QKV GEMM's epilogue (ops.qkv_rope)
-            q, k, v = ops.qkv_rope(h.view(P, rpt, d), W[f"l{l}.wqkv"], self.cos, self.sin, T, H)
-            o = ops.attention(q, k, v)
+            # interleaved-pair RoPE applied by the QKV GEMM's epilogue and, backward, by the
+            # attention kernels' gradient outputs (ops.qkv_rope_attention)
+            o = ops.qkv_rope_attention(h.view(P, rpt, d), W[f"l{l}.wqkv"], self.cos, self.sin,
+                                       T, H)
             x, h = ops.add_rmsnorm(x, _lin(o.view(P, rpt, d), W[f"l{l}.wo"]).view(R, d),
                                    W[f"l{l}.mlp_norm"], rpt, c.norm_eps)
             # gate / up columns interleaved in 16-column groups: the SwiGLU runs in the GEMM

@@ -103,6 +103,38 @@ __device__ __forceinline__ bf16x8 pack_frag(const f32x4& a, const f32x4& b) {
 // flush to zero, which changes no bf16 probability.
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// Gradient outputs of the backward kernels: 4 consecutive head-dim columns col .. col + 3 of row
+// t of head bh, to the head-major buffer `plain` -- or, when dqkv is set (the LM's fused QKV
+// projection + RoPE, ops.qkv_rope_attention), straight into the QKV activation's gradient
+// [B' T][3][H][64] (section sec: q, k, v) with the inverse interleaved-pair RoPE on q and k, so
+// no separate RoPE-backward pass re-reads dQ / dK.
+struct RopeOut {
+  bf16_t* dqkv;
+  const float* cosT;
+  const float* sinT;
+};
+
+__device__ __forceinline__ void put_grad4(bf16_t* plain, const RopeOut& ro, int sec, int bh,
+                                          int H, int T, int t, int col, float (&x)[4]) {
+  if (ro.dqkv == nullptr) {
+    *(uint2*)plain = make_uint2(pack2bf(x[0], x[1]), pack2bf(x[2], x[3]));
+    return;
+  }
+  const int b = bh / H, hh = bh - b * H;
+  if (sec < 2) {
+    const float* cs = ro.cosT + (size_t)t * 32 + (col >> 1);
+    const float* sn = ro.sinT + (size_t)t * 32 + (col >> 1);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float a = x[2 * j], bb = x[2 * j + 1], c = cs[j], sv = sn[j];
+      x[2 * j] = a * c + bb * sv;
+      x[2 * j + 1] = bb * c - a * sv;
+    }
+  }
+  bf16_t* o = ro.dqkv + ((size_t)(b * T + t) * 3 + sec) * H * 64 + hh * 64 + col;
+  *(uint2*)o = make_uint2(pack2bf(x[0], x[1]), pack2bf(x[2], x[3]));
+}
+
 __device__ __forceinline__ float max4(float v) {
   v = fmaxf(v, __shfl_xor(v, 16, 64));
   return fmaxf(v, __shfl_xor(v, 32, 64));
@@ -245,7 +277,8 @@ __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnDqWaves) void attn_bwd_dq
                                                           const float* __restrict__ LSE2,
                                                           const float* __restrict__ Dsum,
                                                           bf16_t* __restrict__ dQ, int T, int H,
-                                                          float c, float scale, int n_bh) {
+                                                          float c, float scale, int n_bh,
+                                                          const RopeOut ro) {
   __shared__ __attribute__((aligned(16))) bf16_t Ks[BKV * LS];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[BKV * LS];
   const int nqb = T / BQ;
@@ -306,9 +339,10 @@ __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnDqWaves) void attn_bwd_dq
   }
   bf16_t* out = dQ + base + (size_t)qrow * D;
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-    *(uint2*)(out + 16 * dt + 4 * g) = make_uint2(pack2bf(acc[dt][0] * scale, acc[dt][1] * scale),
-                                                  pack2bf(acc[dt][2] * scale, acc[dt][3] * scale));
+  for (int dt = 0; dt < 4; ++dt) {
+    float x[4] = {acc[dt][0] * scale, acc[dt][1] * scale, acc[dt][2] * scale, acc[dt][3] * scale};
+    put_grad4(out + 16 * dt + 4 * g, ro, 0, bh, H, T, qrow, 16 * dt + 4 * g, x);
+  }
 }
 
 // dV = sum_q P^T dO,  dK = scale * sum_q dS^T Q.   grid (T/64, BH); one 64-key block per WG.
@@ -322,7 +356,8 @@ __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnDkdvWaves) void attn_bwd_
                                                             const float* __restrict__ Dsum,
                                                             bf16_t* __restrict__ dK,
                                                             bf16_t* __restrict__ dV, int T, int H,
-                                                            float c, float scale, int n_bh) {
+                                                            float c, float scale, int n_bh,
+                                                            const RopeOut ro) {
   __shared__ __attribute__((aligned(16))) bf16_t Qs[BQ * LS];
   __shared__ __attribute__((aligned(16))) bf16_t dOs[BQ * LS];
   __shared__ float lse_s[BQ], dsum_s[BQ];
@@ -405,10 +440,10 @@ __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnDkdvWaves) void attn_bwd_
   bf16_t* ovp = dV + base + (size_t)krow * D;
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) {
-    *(uint2*)(okp + 16 * dt + 4 * g) = make_uint2(pack2bf(dk[dt][0] * scale, dk[dt][1] * scale),
-                                                  pack2bf(dk[dt][2] * scale, dk[dt][3] * scale));
-    *(uint2*)(ovp + 16 * dt + 4 * g) =
-        make_uint2(pack2bf(dv[dt][0], dv[dt][1]), pack2bf(dv[dt][2], dv[dt][3]));
+    float xk[4] = {dk[dt][0] * scale, dk[dt][1] * scale, dk[dt][2] * scale, dk[dt][3] * scale};
+    float xv[4] = {dv[dt][0], dv[dt][1], dv[dt][2], dv[dt][3]};
+    put_grad4(okp + 16 * dt + 4 * g, ro, 1, bh, H, T, krow, 16 * dt + 4 * g, xk);
+    put_grad4(ovp + 16 * dt + 4 * g, ro, 2, bh, H, T, krow, 16 * dt + 4 * g, xv);
   }
 #undef MOPT_DKDV_LOAD
 }
@@ -427,22 +462,26 @@ int mopt_attn_fwd(const void* q, const void* k, const void* v, void* o, void* ls
   return (int)hipGetLastError();
 }
 
+// dqkv (optional): the gradient of the QKV activation [B' T][3][H][64] with the inverse
+// interleaved RoPE applied to its q / k sections (cos / sin [T][32]) -- written instead of dq,
+// dk, dv (which may then be null)
 int mopt_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
                   const void* lse2, void* dsum, void* dq, void* dk, void* dv, int bh, int T, int H,
-                  float scale, void* stream) {
-  if (T % 64 || bh <= 0) return 1;
+                  float scale, void* dqkv, const void* cosT, const void* sinT, void* stream) {
+  if (T % 64 || bh <= 0 || (dqkv != nullptr && (cosT == nullptr || sinT == nullptr))) return 1;
   const float c = scale * 1.4426950408889634f;
   const int rows = bh * T;
+  const RopeOut ro{(bf16_t*)dqkv, (const float*)cosT, (const float*)sinT};
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((rows + 255) / 256), dim3(256), 0, st,
                      (const bf16_t*)o, (const bf16_t*)dout, (float*)dsum, T, H, rows);
   hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((T / 64) * bh), dim3(256), 0, st,
                      (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout,
                      (const float*)lse2, (const float*)dsum, (bf16_t*)dk, (bf16_t*)dv, T, H, c,
-                     scale, bh);
+                     scale, bh, ro);
   hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((T / 64) * bh), dim3(256), 0, st, (const bf16_t*)q,
                      (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, (const float*)lse2,
-                     (const float*)dsum, (bf16_t*)dq, T, H, c, scale, bh);
+                     (const float*)dsum, (bf16_t*)dq, T, H, c, scale, bh, ro);
   return (int)hipGetLastError();
 }
 

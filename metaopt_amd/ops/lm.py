@@ -24,7 +24,7 @@ c_void_p, c_int, c_float, c_int64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_floa
 
 _lib.register_signatures({
     "mopt_attn_fwd": ([c_void_p] * 5 + [c_int, c_int, c_int, c_float, c_void_p], c_int),
-    "mopt_attn_bwd": ([c_void_p] * 10 + [c_int, c_int, c_int, c_float, c_void_p], c_int),
+    "mopt_attn_bwd": ([c_void_p] * 10 + [c_int, c_int, c_int, c_float] + [c_void_p] * 4, c_int),
     "mopt_rmsnorm_fwd": ([c_void_p] * 4 + [c_int, c_int, c_int, c_float, c_void_p], c_int),
     "mopt_rmsnorm_bwd": ([c_void_p] * 6 + [c_int, c_int, c_int, c_void_p], c_int),
     "mopt_add_rmsnorm_fwd": ([c_void_p] * 6 + [c_int, c_int, c_int, c_float, c_void_p], c_int),
@@ -305,22 +305,7 @@ class _QKVRope(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, h, w, cos, sin, T, H, g_w):
-        from .gemm import LARGE_TILES, pgemm, plan
-        P, R, d = h.shape
-        Bp = P * (R // T)
-        buf = torch.empty(3, Bp, H, T, 64, dtype=h.dtype, device=h.device)
-        cfg, splits, _ = plan(P, R, 3 * d, d)
-        rc = 801
-        if cfg in LARGE_TILES and splits == 1 and R % T == 0:
-            rc = _lib.get_lib().mopt_pgemm_qkv_rope(
-                _p(h), _p(w), _p(buf), _p(cos), _p(sin), P, R, d, T, H, h.stride(1),
-                w.stride(1), h.stride(0), w.stride(0), cfg, _stream(h))
-        if rc == 801:                      # no big tile for this shape: GEMM + RoPE pass
-            qkv = pgemm(h, w)
-            _call("mopt_rope_fwd", _p(qkv), _p(cos), _p(sin), _p(buf[0]), _p(buf[1]),
-                  _p(buf[2]), P * R, T, H, 1, _stream(h))
-        else:
-            _lib.check(rc, "mopt_pgemm_qkv_rope")
+        buf = _qkv_heads(h, w, cos, sin, T, H)
         ctx.save_for_backward(h, w, cos, sin)
         ctx.dims = (T, H)
         ctx.g_w = g_w
@@ -341,6 +326,79 @@ class _QKVRope(torch.autograd.Function):
         else:
             dw = pgemm(h, dqkv, ta=True)
         return pgemm(dqkv, w, tb=True), dw, None, None, None, None, None
+
+
+def _qkv_heads(h, w, cos, sin, T, H):
+    """[3, B', H, T, 64] q, k, v heads of h @ w with interleaved RoPE (the EPI 3 GEMM, or the
+    GEMM + the RoPE kernel on shapes without a big tile)."""
+    from .gemm import LARGE_TILES, pgemm, plan
+    P, R, d = h.shape
+    buf = torch.empty(3, P * (R // T), H, T, 64, dtype=h.dtype, device=h.device)
+    cfg, splits, _ = plan(P, R, 3 * d, d)
+    rc = 801
+    if cfg in LARGE_TILES and splits == 1 and R % T == 0:
+        rc = _lib.get_lib().mopt_pgemm_qkv_rope(
+            _p(h), _p(w), _p(buf), _p(cos), _p(sin), P, R, d, T, H, h.stride(1), w.stride(1),
+            h.stride(0), w.stride(0), cfg, _stream(h))
+    if rc == 801:
+        qkv = pgemm(h, w)
+        _call("mopt_rope_fwd", _p(qkv), _p(cos), _p(sin), _p(buf[0]), _p(buf[1]), _p(buf[2]),
+              P * R, T, H, 1, _stream(h))
+    else:
+        _lib.check(rc, "mopt_pgemm_qkv_rope")
+    return buf
+
+
+class _QKVRopeAttention(torch.autograd.Function):
+    """Causal attention over rope(h @ wqkv) in one autograd node: the QKV GEMM writes the rotated
+    heads (EPI 3), and the attention backward writes the QKV activation's gradient with the
+    inverse RoPE applied (no dQ / dK / dV buffers, no RoPE-backward pass), then the projection's
+    two GEMMs."""
+
+    @staticmethod
+    def forward(ctx, h, w, cos, sin, T, H, scale, g_w):
+        P, R, d = h.shape
+        buf = _qkv_heads(h, w, cos, sin, T, H)
+        q, k, v = buf[0], buf[1], buf[2]
+        Bp = P * (R // T)
+        o = torch.empty(Bp * T, H * 64, dtype=h.dtype, device=h.device)
+        lse = torch.empty(Bp * H, T, dtype=torch.float32, device=h.device)
+        _call("mopt_attn_fwd", _p(q), _p(k), _p(v), _p(o), _p(lse), Bp * H, T, H, scale,
+              _stream(h))
+        ctx.save_for_backward(h, w, cos, sin, buf, o, lse)
+        ctx.meta = (T, H, scale)
+        ctx.g_w = g_w
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        from .gemm import pgemm
+        h, w, cos, sin, buf, o, lse = ctx.saved_tensors
+        T, H, scale = ctx.meta
+        P, R, d = h.shape
+        do = do.contiguous()
+        dqkv = torch.empty(P, R, 3 * d, dtype=h.dtype, device=h.device)
+        dsum = torch.empty_like(lse)
+        _call("mopt_attn_bwd", _p(buf[0]), _p(buf[1]), _p(buf[2]), _p(o), _p(do), _p(lse),
+              _p(dsum), None, None, None, P * (R // T) * H, T, H, scale, _p(dqkv), _p(cos),
+              _p(sin), _stream(h))
+        dw = None
+        if ctx.g_w is not None:
+            pgemm(h, dqkv, ta=True, out=ctx.g_w)
+        else:
+            dw = pgemm(h, dqkv, ta=True)
+        return pgemm(dqkv, w, tb=True), dw, None, None, None, None, None, None
+
+
+def qkv_rope_attention(h, w, cos, sin, T, H, scale=None):
+    """Causal self-attention output [B' T, H 64] of the heads rope(h @ w) (interleaved RoPE):
+    h [P, R, d], w [P, d, 3 d]."""
+    scale = 0.125 if scale is None else scale            # head dim 64
+    if _hip(h, "attn") and _hip(h, "rope"):
+        return _QKVRopeAttention.apply(h.contiguous(), w.contiguous(), cos, sin, T, H, scale,
+                                       _grad_view(w))
+    q, k, v = qkv_rope(h, w, cos, sin, T, H)
+    return attention_ref(q, k, v, scale) if not _hip(h, "attn") else attention(q, k, v, scale)
 
 
 def qkv_rope(h, w, cos, sin, T, H):
@@ -374,7 +432,7 @@ class _Attention(torch.autograd.Function):
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         dsum = torch.empty_like(lse)
         _call("mopt_attn_bwd", _p(q), _p(k), _p(v), _p(o), _p(do), _p(lse), _p(dsum), _p(dq),
-              _p(dk), _p(dv), Bp * H, T, H, ctx.scale, _stream(q))
+              _p(dk), _p(dv), Bp * H, T, H, ctx.scale, None, None, None, _stream(q))
         return dq, dk, dv, None
 
 

@@ -415,3 +415,27 @@ def test_qkv_rope_epilogue_matches_reference(P, B, T, H, big):
         _close(o, r, 2e-2)
     _close(hs.grad, hr.grad, 3e-2)
     _close(ws.grad, wr.grad, 3e-2)
+
+
+def test_qkv_rope_attention_matches_reference():
+    """The fused node (QKV GEMM with the RoPE epilogue, attention, and the attention backward
+    writing the QKV gradient with the inverse RoPE) against fp32 autograd of the unfused
+    reference: output and the gradients of h and wqkv."""
+    torch.manual_seed(10)
+    P, B, T, H = 4, 2, 256, 2
+    d, R = 64 * H, B * T
+    h = (torch.randn(P, R, d, device=DEV) * 0.5).to(torch.bfloat16)
+    w = (torch.randn(P, d, 3 * d, device=DEV) / d ** 0.5).to(torch.bfloat16)
+    cos, sin = ops.rope_tables(T, device=DEV)
+    hs, ws = h.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    o = ops.qkv_rope_attention(hs, ws, cos, sin, T, H)
+    g = torch.randn_like(o)
+    o.backward(g)
+    hr, wr = h.float().requires_grad_(True), w.float().requires_grad_(True)
+    q, k, v = ops.rope_split_ref(torch.bmm(hr, wr).reshape(P * R, 3 * d), cos, sin, T, H, il=True)
+    orf = ops.attention_ref(q, k, v, 0.125)
+    orf.backward(g.float())
+    torch.cuda.synchronize()
+    _close(o, orf, 2e-2)
+    _close(hs.grad, hr.grad, 3e-2)
+    _close(ws.grad, wr.grad, 3e-2)
