@@ -73,6 +73,12 @@ constexpr int BK = 64;   // reduction step of the forward, width of a backward k
 // round 3: its address math spilled the backward -- profiles/round3.md "MLP kernels: A/B".)
 constexpr int TS = kLdsStride;
 #define TOFF(r, c) ((r) * TS + (c))
+// Forward tiles: rows of 80 elements (160 B = 10 16-byte slots, 2 mod 4), so the 16 rows of a
+// fragment read (ds_read_b128) hit 16 distinct slots -- conflict-free where 72 costs 4 extra
+// cycles per read (scripts/lds_banks.py "pad80"); the backward keeps 72 (its transposed reads
+// and dZ copy-out conflict more at 80).
+constexpr int TSF = 80;
+#define TOFFF(r, c) ((r) * TSF + (c))
 #define FOFF(r, c) ((r) * (BN + 4) + (c))
 
 // Weight layout in HBM: k-strip-major [K/64][N][64] -- W[n][k] at (k / 64) N 64 + n 64 + k % 64,
@@ -113,19 +119,21 @@ enum Opt { kSGD = 0, kAdamW = 1, kSGD16 = 2 };
 // control flow sits around a load.
 // ----------------------------------------------------------------------------------------------
 // (the two register sets are plain scalars behind a macro: held in a struct passed by reference
-//  they were demoted to scratch)
+//  they were demoted to scratch; 32-bit element offsets keep both sets within the 128 VGPRs of
+//  4 waves per SIMD -- 64-bit ones needed 132.  The pipelined loop below measured 658 -> 650 us
+//  per 256-member step, profiles/round4.md.)
 #define MOPT_FWD_LOAD(x0, x1, x2, x3, w0, w1, k)        \
   do {                                                  \
-    const int kk_ = (k);                                \
-    x0 = *(const uint4*)(X + g0 + kk_);                 \
-    x1 = *(const uint4*)(X + g1 + kk_);                 \
-    x2 = *(const uint4*)(X + g2 + kk_);                 \
-    x3 = *(const uint4*)(X + g3 + kk_);                 \
-    w0 = *(const uint4*)(W + gw0 + (size_t)kk_ * WKS);  \
-    if (TN >= 64) w1 = *(const uint4*)(W + gw1 + (size_t)kk_ * WKS); \
+    const uint32_t kk_ = (uint32_t)(k), kw_ = kk_ * (uint32_t)WKS; \
+    x0 = *(const uint4*)(X + (uint32_t)(g0 + kk_));     \
+    x1 = *(const uint4*)(X + (uint32_t)(g1 + kk_));     \
+    x2 = *(const uint4*)(X + (uint32_t)(g2 + kk_));     \
+    x3 = *(const uint4*)(X + (uint32_t)(g3 + kk_));     \
+    w0 = *(const uint4*)(W + (uint32_t)(gw0 + kw_));    \
+    if (TN >= 64) w1 = *(const uint4*)(W + (uint32_t)(gw1 + kw_)); \
     if (TN >= 128) {                                    \
-      w1##b = *(const uint4*)(W + gw2 + (size_t)kk_ * WKS); \
-      w1##c = *(const uint4*)(W + gw3 + (size_t)kk_ * WKS); \
+      w1##b = *(const uint4*)(W + (uint32_t)(gw2 + kw_)); \
+      w1##c = *(const uint4*)(W + (uint32_t)(gw3 + kw_)); \
     }                                                   \
   } while (0)
 #define MOPT_FWD_STORE(x0, x1, x2, x3, w0, w1) \
@@ -151,9 +159,9 @@ __device__ __forceinline__ void fwd_step(const bf16_t* As, const bf16_t* Bs, int
   for (int ks = 0; ks < BK / 32; ++ks) {
     bf16x8 a[2], b[TN / 16];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) a[i] = lds_frag(As + TOFF(wave * 32 + i * 16 + li, ks * 32 + g * 8));
+    for (int i = 0; i < 2; ++i) a[i] = lds_frag(As + TOFFF(wave * 32 + i * 16 + li, ks * 32 + g * 8));
 #pragma unroll
-    for (int j = 0; j < TN / 16; ++j) b[j] = lds_frag(Bs + TOFF(j * 16 + li, ks * 32 + g * 8));
+    for (int j = 0; j < TN / 16; ++j) b[j] = lds_frag(Bs + TOFFF(j * 16 + li, ks * 32 + g * 8));
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -180,14 +188,14 @@ __device__ __forceinline__ void fwd_gemm(const bf16_t* __restrict__ X, const bf1
   const int WRS = w_row_stride(K), WKS = w_kstep(N);
   const int gw0 = (c0 >> 3) * WRS + (c0 & 7) * 8, gw1 = (c1 >> 3) * WRS + (c1 & 7) * 8;
   const int gw2 = (c2 >> 3) * WRS + (c2 & 7) * 8, gw3 = (c3 >> 3) * WRS + (c3 & 7) * 8;
-  bf16_t* as0 = As + TOFF(c0 >> 3, (c0 & 7) * 8);
-  bf16_t* as1 = As + TOFF(c1 >> 3, (c1 & 7) * 8);
-  bf16_t* as2 = As + TOFF(c2 >> 3, (c2 & 7) * 8);
-  bf16_t* as3 = As + TOFF(c3 >> 3, (c3 & 7) * 8);
-  bf16_t* bs0 = Bs + TOFF(c0 >> 3, (c0 & 7) * 8);
-  bf16_t* bs1 = Bs + TOFF(c1 >> 3, (c1 & 7) * 8);
-  bf16_t* bs2 = Bs + TOFF(c2 >> 3, (c2 & 7) * 8);
-  bf16_t* bs3 = Bs + TOFF(c3 >> 3, (c3 & 7) * 8);
+  bf16_t* as0 = As + TOFFF(c0 >> 3, (c0 & 7) * 8);
+  bf16_t* as1 = As + TOFFF(c1 >> 3, (c1 & 7) * 8);
+  bf16_t* as2 = As + TOFFF(c2 >> 3, (c2 & 7) * 8);
+  bf16_t* as3 = As + TOFFF(c3 >> 3, (c3 & 7) * 8);
+  bf16_t* bs0 = Bs + TOFFF(c0 >> 3, (c0 & 7) * 8);
+  bf16_t* bs1 = Bs + TOFFF(c1 >> 3, (c1 & 7) * 8);
+  bf16_t* bs2 = Bs + TOFFF(c2 >> 3, (c2 & 7) * 8);
+  bf16_t* bs3 = Bs + TOFFF(c3 >> 3, (c3 & 7) * 8);
   const int klast = K - BK;
   uint4 p0, p1, p2, p3, pw0, pw1{}, pw1b{}, pw1c{};  // K-steps 0, 3, 6, ...
   uint4 q0, q1, q2, q3, qw0, qw1{}, qw1b{}, qw1c{};  // K-steps 1, 4, 7, ...
@@ -212,11 +220,17 @@ __device__ __forceinline__ void fwd_gemm(const bf16_t* __restrict__ X, const bf1
       if (k0 + 3 * BK >= K) break;
     }
   } else {
-    for (int k0 = 0;; k0 += 2 * BK) {
+    // whole pairs of K-steps, then the odd last one: no exit between the two steps, so the
+    // loop body is one block -- with a mid-body exit hipcc sank the p refill past the exit
+    // branch (it is dead on that path) into the next iteration, one step before its use
+    // instead of two, and the waits at the q store then drained every load in flight
+    int k0 = 0;
+    for (; k0 + 2 * BK <= K; k0 += 2 * BK) {
       MOPT_FWD_KSTEP(p, k0 + 2 * BK)
-      if (k0 + BK >= K) break;
       MOPT_FWD_KSTEP(q, k0 + 3 * BK)
-      if (k0 + 2 * BK >= K) break;
+    }
+    if (k0 < K) {
+      MOPT_FWD_KSTEP(p, k0 + 2 * BK)
     }
   }
 #undef MOPT_FWD_KSTEP
@@ -248,9 +262,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) vo
                                                       bf16_t* __restrict__ act,
                                                       const TrialHP* __restrict__ hp,
                                                       uint32_t step, int layer, int flags) {
-  __shared__ __attribute__((aligned(16))) bf16_t smem[(BM + TN) * TS];
+  __shared__ __attribute__((aligned(16))) bf16_t smem[(BM + TN) * TSF];
   bf16_t* As = smem;
-  bf16_t* Bs = smem + BM * TS;
+  bf16_t* Bs = smem + BM * TSF;
   const int2 wi = work[blockIdx.x];   // XCD-balanced order built on the host (_xcd_schedule)
   if (wi.x < 0) return;                // padding: a no-op workgroup
   const MlpTL tl = tls[wi.x];
@@ -287,7 +301,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) vo
           const uint32_t idx = (uint32_t)((row0 + row) * N + n0 + col);
           v = rng_uniform(key, idx) >= h.drop ? v * inv_keep : 0.f;
         }
-        Cs[TOFF(row, col)] = f2bf(v);
+        Cs[TOFFF(row, col)] = f2bf(v);
       }
   }
   __syncthreads();
@@ -296,7 +310,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) vo
 #pragma unroll
   for (int i = 0; i < TN / 16; ++i) {
     const int c = tid + 256 * i, r = c / CPR, ch = c % CPR;
-    *(uint4*)(Y + (size_t)r * N + ch * 8) = *(const uint4*)(Cs + TOFF(r, ch * 8));
+    *(uint4*)(Y + (size_t)r * N + ch * 8) = *(const uint4*)(Cs + TOFFF(r, ch * 8));
   }
 }
 
@@ -315,10 +329,10 @@ __global__ __launch_bounds__(256) void mlp_fwd_ce_kernel(const MlpTL* __restrict
                                                          TrialHP* __restrict__ hp, float inv_b,
                                                          int flags) {
   constexpr int CS = BN + 1;  // f32 logits row stride
-  constexpr int kSmemBytes = BM * CS * 4 > (BM + BN) * TS * 2 ? BM * CS * 4 : (BM + BN) * TS * 2;
+  constexpr int kSmemBytes = BM * CS * 4 > (BM + BN) * TSF * 2 ? BM * CS * 4 : (BM + BN) * TSF * 2;
   __shared__ __attribute__((aligned(16))) char smem_raw[kSmemBytes];
   bf16_t* As = (bf16_t*)smem_raw;
-  bf16_t* Bs = As + BM * TS;
+  bf16_t* Bs = As + BM * TSF;
   float* Ls = (float*)smem_raw;
 
   const int2 wi = work[blockIdx.x];   // XCD-balanced order built on the host (_xcd_schedule)

@@ -70,6 +70,8 @@ def xor_rows(fn):
 
 LAYOUTS = {
     "pad72 (current)": padded(72),
+    "pad80": padded(80),
+    "pad88": padded(88),
     "xor (r>>1)&7": xor_rows(lambda r: (r >> 1) & 7),
     "xor swap(r>>1)": xor_rows(lambda r: (((r >> 1) & 4) | (((r >> 1) & 1) << 1)
                                         | ((r >> 2) & 1))),
