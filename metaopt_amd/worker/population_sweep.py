@@ -60,7 +60,17 @@ class PopulationSweep:
                  heartbeat_every: float = 30.0, max_trials: Optional[float] = None,
                  pipelined: Optional[bool] = None, events=None, trial_events: bool = False,
                  watchdog=None, restore_algorithm: bool = False, resume: bool = False,
-                 ckpt_dir: Optional[str] = None, writer: str = "auto"):
+                 ckpt_dir: Optional[str] = None, writer: str = "auto",
+                 stagger: Optional[int] = None):
+        """``stagger``: the first fill of the empty population is spread over this many syncs
+        (None: ceil(W P / 512), at most 4 -- 1 up to 512 slots).  Members that start together
+        finish together, and every completion is rank 0's decision work at the sync it happens:
+        2048 slots starting at once made every rung-0 budget end a burst of ~1800 completions in
+        one sync (25-30 ms of rank-0 host time at 8 ranks against a ~21 ms interval, the GPUs
+        idle for the rest) between syncs with next to none (``scripts/profile_decide.py``
+        PRIORS=headline: per-sync p50 0.1 ms, max 118 ms on the development CPU).  Staggered
+        cohorts keep each sync near the mean; the slots filled late cost W P (s - 1) / 2
+        slot-intervals once, inside any warm-up."""
         self.pop = pop
         self.task = task
         self.data = data
@@ -70,6 +80,10 @@ class PopulationSweep:
             raise ValueError("rank 0 needs the experiment")
         self.sync_every = int(sync_every)
         self.ckpt_capacity = int(ckpt_capacity)
+        total_slots = self.comm.world_size * pop.capacity
+        self.stagger = int(stagger) if stagger is not None else \
+            min(4, max(1, -(-total_slots // 512)))
+        self._fills = 0                 # _fill calls so far (the stagger schedule)
         self.heartbeat_every = heartbeat_every
         P = pop.capacity
         self.slot_key = np.full(P, -1, dtype=np.int64)
@@ -570,6 +584,12 @@ class PopulationSweep:
         in_flight = len(self.trials)
         budget_left = self.max_trials - n_done - in_flight
         n = int(min(len(free_rows), budget_left)) if math.isfinite(budget_left) else len(free_rows)
+        if self._fills < self.stagger - 1:
+            # staggered start: at most (i + 1) / stagger of the slots busy after fill i
+            total = W * P
+            target = -(-total * (self._fills + 1) // self.stagger)
+            n = min(n, max(0, target - (total - len(free_rows))))
+        self._fills += 1
         if n <= 0:
             if not self.trials:
                 self.done = True

@@ -46,9 +46,24 @@ class _FakeComm:
         return [obj]
 
 
+def _priors():
+    """PRIORS=headline: bench.py's space (ASHA rungs 128 / 512 steps = 4 / 16 sync intervals: at
+    8 ranks about 500 completions per sync); default: MLP_PRIORS (rung 0 = 32 steps, ONE sync
+    interval: every rung-0 member finishes at every sync, about 1000 per sync -- the stress case)"""
+    if os.environ.get("PRIORS", "stress") == "headline":
+        sys.argv, argv = sys.argv[:1], sys.argv
+        try:
+            import bench
+            return dict(bench.BENCH_PRIORS)
+        finally:
+            sys.argv = argv
+    return dict(MLP_PRIORS)
+
+
 def main(n_syncs=40, P=256, world=1, profile=False):
-    task = MLPSweepTask(priors=dict(MLP_PRIORS), max_width=1024)
-    exp = build_experiment("decide-prof", priors=dict(MLP_PRIORS),
+    priors = _priors()
+    task = MLPSweepTask(priors=priors, max_width=1024)
+    exp = build_experiment("decide-prof", priors=priors,
                            algorithms={"asha": ({"seed": 0, "unbounded": True}
                                                 if os.environ.get("ASHA", "async") == "async"
                                                 else {"seed": 0, "repetitions": float("inf")})},
@@ -65,6 +80,7 @@ def main(n_syncs=40, P=256, world=1, profile=False):
     assign = sw._decide(gathered)
     prof = cProfile.Profile() if profile else None
     t_total = t_rel = 0.0
+    per_sync = []
     n_done = 0
     for _ in range(n_syncs):
         # apply: new/resumed members start from 0 (resume: from their checkpoint steps)
@@ -91,7 +107,8 @@ def main(n_syncs=40, P=256, world=1, profile=False):
         assign = sw._decide(gathered)
         if prof:
             prof.disable()
-        t_total += time.perf_counter() - t0
+        per_sync.append(time.perf_counter() - t0)
+        t_total += per_sync[-1]
         t1 = time.perf_counter()
         if not os.environ.get("NO_DRAIN"):
             sw._writer.drain_while(lambda: True)   # rank 0's share (inline: all of them)
@@ -117,7 +134,8 @@ def main(n_syncs=40, P=256, world=1, profile=False):
     print("phases ms/sync:", {k: round(1e3 * v / n_syncs, 2) for k, v in sw.timers.items()
                               if k.startswith("decide") or k.startswith("gc")})
     print(f"decide: {1e3 * t_total / n_syncs:.2f} ms/sync, writes {1e3 * t_rel / n_syncs:.2f} ms/sync, "
-          f"{n_done / n_syncs:.1f} completions/sync")
+          f"{n_done / n_syncs:.1f} completions/sync; per sync p50 "
+          f"{1e3 * float(np.median(per_sync)):.2f} ms, max {1e3 * max(per_sync):.2f} ms")
     if prof:
         pstats.Stats(prof).sort_stats(os.environ.get("SORT", "cumulative")).print_stats(30)
 
