@@ -211,13 +211,17 @@ __device__ __forceinline__ void fwd_gemm(const bf16_t* __restrict__ X, const bf1
   fwd_step<TN>(As, Bs, wave, li, g, acc);                                \
   __syncthreads();
   if (NSET == 3) {
-    for (int k0 = 0;; k0 += 3 * BK) {
+    int k0 = 0;
+    for (; k0 + 3 * BK <= K; k0 += 3 * BK) {
       MOPT_FWD_KSTEP(p, k0 + 3 * BK)
-      if (k0 + BK >= K) break;
       MOPT_FWD_KSTEP(q, k0 + 4 * BK)
-      if (k0 + 2 * BK >= K) break;
       MOPT_FWD_KSTEP(r, k0 + 5 * BK)
-      if (k0 + 3 * BK >= K) break;
+    }
+    if (k0 < K) {
+      MOPT_FWD_KSTEP(p, k0 + 3 * BK)
+    }
+    if (k0 + BK < K) {
+      MOPT_FWD_KSTEP(q, k0 + 4 * BK)
     }
   } else {
     // whole pairs of K-steps, then the odd last one: no exit between the two steps, so the
@@ -890,6 +894,8 @@ int mopt_mlp_fwd(const void* tls, const void* work, int n_work, int n_rowblocks,
                  int layer, int flags, int tile_n, void* stream) {
   if (n_work <= 0) return 0;
   if (tile_n != 64) return (int)hipErrorInvalidValue;
+  // (three register sets at 3 waves / SIMD, with the same whole-group loop: step 654-656 vs
+  //  651-654 us, bench 784-787 vs 790-791 trials/s -- profiles/round4.md)
   hipLaunchKernelGGL((mlp_fwd_kernel<64, 2, 4>), dim3(n_work, n_rowblocks), dim3(256), 0,
                      (hipStream_t)stream, (const MlpTL*)tls, (const int2*)work, n_work,
                      (const bf16_t*)xb, (const bf16_t*)plo, (const bf16_t*)p16, (bf16_t*)act,
