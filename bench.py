@@ -195,6 +195,9 @@ def run_rank(args) -> None:
                                    "SGD momentum",
                 "comm_backend": comm.backend or "none",
                 "rehearsal_ranks_share_gpus": rehearsal,
+                # syncs the first fill is spread over (populations over 512 slots: the members'
+                # budgets then end in different syncs, rank 0's decision work stays even)
+                "staggered_start_syncs": sweep.stagger,
             },
             "timed_syncs": n_syncs,
             "trials_completed": completed,
