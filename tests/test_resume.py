@@ -56,7 +56,7 @@ def _make(storage, data, comm=None, cap=4, max_trials=MAX_TRIALS, **kw):
 
 
 def _phase_worker(rank, world, port, db_path, ckpt_dir, max_steps, resume, q, cap=4,
-                  max_trials=MAX_TRIALS):
+                  max_trials=MAX_TRIALS, stagger=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     torch.set_num_threads(1)    # same BLAS reduction order whatever the world size
@@ -64,20 +64,22 @@ def _phase_worker(rank, world, port, db_path, ckpt_dir, max_steps, resume, q, ca
     comm = init_from_env(backend="gloo")
     storage = DocumentStorage(PickledDB(host=db_path)) if comm.is_root else None
     _, sweep = _make(storage, _data(), comm=comm, cap=cap, resume=resume,
-                     restore_algorithm=resume, ckpt_dir=ckpt_dir, max_trials=max_trials)
+                     restore_algorithm=resume, ckpt_dir=ckpt_dir, max_trials=max_trials,
+                     stagger=stagger)
     sweep.run(max_steps)
     sweep.close()
     q.put((rank, sweep.done, sweep.n_resumed, sweep.n_resume_missing))
     shutdown()
 
 
-def _run_phase(db_path, ckpt_dir, max_steps, resume, world=2, cap=4, max_trials=MAX_TRIALS):
+def _run_phase(db_path, ckpt_dir, max_steps, resume, world=2, cap=4, max_trials=MAX_TRIALS,
+               stagger=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_phase_worker,
                          args=(r, world, port, db_path, ckpt_dir, max_steps, resume, q, cap,
-                               max_trials))
+                               max_trials, stagger))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -203,6 +205,24 @@ def test_two_rank_sweep_equals_one_rank_with_the_same_slots(tmp_path):
     two = str(tmp_path / "two.pkl")
     assert all(r[1] for r in _run_phase(one, None, 100000, resume=False, world=1, cap=8))
     assert all(r[1] for r in _run_phase(two, None, 100000, resume=False, world=2, cap=4))
+    done1, _, rungs1 = _outcome(one)
+    done2, _, rungs2 = _outcome(two)
+    assert len(done1) == MAX_TRIALS and set(done1) == set(done2)
+    for tid, obj in done1.items():
+        assert done2[tid] == pytest.approx(obj, rel=1e-6, abs=1e-9), tid
+    assert rungs1 == rungs2
+
+
+def test_staggered_two_rank_sweep_equals_one_rank(tmp_path):
+    """The staggered start (first fill spread over 3 syncs) is decided on rank 0 alone and
+    broadcast like any placement: 2 ranks x 4 slots and 1 rank x 8 slots, both staggered, finish
+    the same trials with the same objectives and ASHA rungs."""
+    one = str(tmp_path / "one.pkl")
+    two = str(tmp_path / "two.pkl")
+    assert all(r[1] for r in _run_phase(one, None, 100000, resume=False, world=1, cap=8,
+                                        stagger=3))
+    assert all(r[1] for r in _run_phase(two, None, 100000, resume=False, world=2, cap=4,
+                                        stagger=3))
     done1, _, rungs1 = _outcome(one)
     done2, _, rungs2 = _outcome(two)
     assert len(done1) == MAX_TRIALS and set(done1) == set(done2)
