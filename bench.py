@@ -124,8 +124,10 @@ def run_rank(args) -> None:
                                  batch_size=128, seed=1234 + args.seed, device=comm.device)
     pop = PopulationMLP(P, max_width=max_width, eval_batch=1024, device=comm.device,
                         momentum_dtype=args.momentum_dtype)
+    # staggered start (populations over 512 slots): finished inside the untimed warm-up
+    stagger = min(4, max(1, -(-comm.world_size * P // 512)), max(1, args.warmup - 1))
     sweep = PopulationSweep(pop, task, data, comm=comm, experiment=experiment,
-                            sync_every=S, ckpt_capacity=4 * P)
+                            sync_every=S, ckpt_capacity=4 * P, stagger=stagger)
 
     def sync():
         if on_gpu:
