@@ -44,7 +44,9 @@ def run_sweep(args, comm):
     exp = None
     if comm.is_root:
         exp = build_experiment(f"bench-{args.config}", priors=dict(task.priors),
-                               algorithms=spec.algorithm(args.seed, P * comm.world_size),
+                               algorithms=(spec.algorithm(args.seed, P * comm.world_size)
+                                           if args.algo is None
+                                           else {args.algo: {"seed": args.seed}}),
                                storage=DocumentStorage(EphemeralDB()),
                                pool_size=P * comm.world_size)
     sweep = PopulationSweep(pop, task, data, comm=comm, experiment=exp, sync_every=sync_every,
@@ -85,6 +87,7 @@ def run_sweep(args, comm):
     if comm.is_root:
         summ = sweep.summary()
         out["best_val_loss"] = summ["best_val_loss"]
+        out["algorithm"] = args.algo or next(iter(spec.algorithm(args.seed, P * comm.world_size)))
     sweep.close()
     return out
 
@@ -135,6 +138,8 @@ def main():
     ap.add_argument("--sync-every", type=int, default=None)
     ap.add_argument("--inner-steps", type=int, default=10)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--algo", default=None,
+                    help="override the config's search algorithm (e.g. random), default seed")
     args = ap.parse_args()
     from metaopt_amd.parallel.comm import init_from_env, shutdown
     comm = init_from_env()
