@@ -66,6 +66,10 @@ class PBT(BaseAlgorithm):
         self.generations: List[Dict[tuple, Optional[float]]] = [{} for _ in self.timeline]
         self._ready: List[tuple] = []      # observed members waiting for their successor
         self._forked = set()               # members whose successor was issued
+        # exploit / explore record: (generation forked from, loser key, winner key), and the
+        # number of perturbed hyper-parameter sets (explore) per generation forked from
+        self.exploit_log: List[tuple] = []
+        self.explores: Dict[int, int] = {}
 
     # ------------------------------------------------------------------ RNG / state
     def seed_rng(self, seed):
@@ -74,7 +78,8 @@ class PBT(BaseAlgorithm):
     @property
     def state_dict(self):
         return {"rng_state": self.rng.get_state(), "nodes": copy.deepcopy(self.nodes),
-                "ready": list(self._ready), "forked": sorted(self._forked, key=repr)}
+                "ready": list(self._ready), "forked": sorted(self._forked, key=repr),
+                "exploit_log": list(self.exploit_log), "explores": dict(self.explores)}
 
     def set_state(self, state_dict):
         self.seed_rng(0)
@@ -86,6 +91,8 @@ class PBT(BaseAlgorithm):
                 self.generations[n["gen"]][k] = n["objective"]
             self._ready = [tuple(k) for k in state_dict["ready"]]
             self._forked = set(tuple(k) for k in state_dict["forked"])
+            self.exploit_log = [tuple(e) for e in state_dict.get("exploit_log", [])]
+            self.explores = {int(g): int(n) for g, n in state_dict.get("explores", {}).items()}
 
     # ------------------------------------------------------------------ study API
     def suggest(self, num=1):
@@ -140,6 +147,16 @@ class PBT(BaseAlgorithm):
             return None
         return self.nodes[node["parent"]]["point"]
 
+    def exploit_counts(self) -> Dict[int, tuple]:
+        """{generation forked from: (#exploits, #explores)} -- an exploit replaces a bottom
+        member by a copy of a top one; an explore perturbs a copy's hyper-parameters."""
+        out: Dict[int, list] = {}
+        for g, _, _ in self.exploit_log:
+            out.setdefault(g, [0, 0])[0] += 1
+        for g, n in self.explores.items():
+            out.setdefault(g, [0, 0])[1] += n
+        return {g: tuple(v) for g, v in sorted(out.items())}
+
     @property
     def is_done(self):
         last = self.generations[-1]
@@ -164,10 +181,12 @@ class PBT(BaseAlgorithm):
         n = len(done)
         source = k
         params = list(node["point"])
+        explored = 0
         if rank >= int(numpy.ceil(self.truncation_quantile * n)):       # bottom fraction: exploit
             pool = max(1, int(numpy.floor(self.candidate_pool_ratio * n)))
             source = done[self.rng.randint(pool)][1]
             params = self._explore(list(self.nodes[source]["point"]))
+            explored = 1
         params[self.fidelity_index] = self.timeline[g + 1]
         succ = tuple(params)
         tries = 0
@@ -176,10 +195,15 @@ class PBT(BaseAlgorithm):
             succ[self.fidelity_index] = self.timeline[g + 1]
             succ = tuple(succ)
             tries += 1
+            explored = 1
         if _key(succ) in self.nodes:
             return None
         self._forked.add(k)
         self._add(succ, g + 1, source)
+        if source != k:
+            self.exploit_log.append((g, k, source))
+        if explored:
+            self.explores[g] = self.explores.get(g, 0) + 1
         return succ
 
     def _explore(self, params):

@@ -29,9 +29,15 @@ KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
 _VISIBLE_VARS = ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")
 
 
-def _kfd_gpu_count(root: str = KFD_NODES) -> int:
-    """GPU agents in the KFD topology: nodes whose ``properties`` report SIMDs (CPU nodes have
-    ``simd_count 0``).  0 when the driver is absent."""
+DRI_DIR = "/dev/dri"
+
+
+def _kfd_gpu_count(root: str = KFD_NODES, dri: str = DRI_DIR) -> int:
+    """GPU agents in the KFD topology that this process can open: nodes whose ``properties``
+    report SIMDs (CPU nodes have ``simd_count 0``) and whose render node
+    ``/dev/dri/renderD<drm_render_minor>`` exists and is read/writable -- sysfs lists every GPU
+    of the host even in a container given only some render nodes.  0 when the driver is
+    absent."""
     try:
         nodes = os.listdir(root)
     except OSError:
@@ -43,17 +49,26 @@ def _kfd_gpu_count(root: str = KFD_NODES) -> int:
                 props = dict(line.split(None, 1) for line in f if line.strip())
         except (OSError, ValueError):
             continue
-        if int(props.get("simd_count", "0")) > 0:
-            n += 1
+        if int(props.get("simd_count", "0")) <= 0:
+            continue
+        minor = props.get("drm_render_minor", "").strip()
+        if minor and int(minor) > 0:
+            dev = os.path.join(dri, f"renderD{int(minor)}")
+            if not os.access(dev, os.R_OK | os.W_OK):
+                continue
+        n += 1
     return n
 
 
-def visible_gpu_count(env: Optional[dict] = None, root: str = KFD_NODES) -> int:
+def visible_gpu_count(env: Optional[dict] = None, root: str = KFD_NODES,
+                      dri: str = DRI_DIR) -> int:
     """GPUs a child process will see, without initialising HIP in this one: the KFD topology's
-    GPU count, narrowed by ``ROCR_VISIBLE_DEVICES`` / ``HIP_VISIBLE_DEVICES`` /
-    ``CUDA_VISIBLE_DEVICES`` (each applied in that order, as the runtime does)."""
+    accessible GPU count, narrowed by ``ROCR_VISIBLE_DEVICES`` / ``HIP_VISIBLE_DEVICES`` /
+    ``CUDA_VISIBLE_DEVICES`` (each applied in that order, as the runtime does).
+    ``MOPT_GPU_COUNT`` overrides the topology count."""
     env = os.environ if env is None else env
-    n = _kfd_gpu_count(root)
+    forced = env.get("MOPT_GPU_COUNT")
+    n = int(forced) if forced not in (None, "") else _kfd_gpu_count(root, dri)
     for var in _VISIBLE_VARS:
         val = env.get(var)
         if val is None:

@@ -48,12 +48,17 @@ class _Scheduler:
 
     def add(self, pm, due):
         with self._cv:
-            heapq.heappush(self._heap, (due, next(self._seq), pm))
-            if self._thread is None or not self._thread.is_alive():
-                self._thread = threading.Thread(target=self._dispatch, name="mopt-heartbeats",
-                                                daemon=True)
-                self._thread.start()
-            self._cv.notify_all()
+            self._push(pm, due)
+
+    def _push(self, pm, due):
+        """Schedule ``pm`` at ``due`` (caller holds the lock); (re)start the dispatcher if it
+        has exited, so a beat re-queued after a long storage call is never orphaned."""
+        heapq.heappush(self._heap, (due, next(self._seq), pm))
+        if self._thread is None or not self._thread.is_alive():
+            self._thread = threading.Thread(target=self._dispatch, name="mopt-heartbeats",
+                                            daemon=True)
+            self._thread.start()
+        self._cv.notify_all()
 
     def wait_idle(self, pm):
         """Block until ``pm`` is not being beaten (its entry may still sit in the heap or the
@@ -69,7 +74,9 @@ class _Scheduler:
                     heapq.heappop(self._heap)              # cancelled entries
                 if not self._heap:
                     self._cv.wait(self.IDLE_EXIT_S)
-                    if not self._heap:
+                    # exit only when nothing can come back: no entry queued and no beat in
+                    # progress (a running beat re-queues itself when it finishes)
+                    if not self._heap and not self._running and not self._ready:
                         self._thread = None
                         return                              # idle: the next add restarts it
                     continue
@@ -111,11 +118,10 @@ class _Scheduler:
             with self._cv:
                 self._running.discard(pm)
                 if alive and not pm.stopped.is_set():
-                    heapq.heappush(self._heap, (time.monotonic() + pm.wait_time,
-                                                next(self._seq), pm))
+                    self._push(pm, time.monotonic() + pm.wait_time)
                 else:
                     pm.stopped.set()
-                self._cv.notify_all()
+                    self._cv.notify_all()
 
 
 _SCHEDULER = _Scheduler()

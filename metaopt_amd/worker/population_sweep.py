@@ -93,8 +93,16 @@ class PopulationSweep:
         # device checkpoints of finished members (ASHA promotion, PBT exploit): trial key ->
         # metadata of a slot in the population's checkpoint pool, evicted FIFO
         self.ckpts: "collections.OrderedDict[int, dict]" = collections.OrderedDict()
-        pop.alloc_ckpt_pool(self.ckpt_capacity)
-        self._free_ck = list(range(self.ckpt_capacity - 1, -1, -1))
+        # direct C4 receives (flat populations, W > 1) land in pool entries of their own that
+        # are never counted in ``ckpts``: taking one by evicting a checkpoint would desync rank
+        # 0's mirror of this rank's FIFO (``ckpt_fifo``), alias an entry being sent in the same
+        # exchange, or silently drop a checkpoint a local RESUME of this sync expects
+        cap = self.ckpt_capacity
+        self._c4_reserve = (pop.capacity if self.comm.world_size > 1
+                            and hasattr(pop, "c4_send_tensors") else 0)
+        pop.alloc_ckpt_pool(cap + self._c4_reserve)
+        self._free_ck = list(range(cap - 1, -1, -1))
+        self._c4_free = list(range(cap + self._c4_reserve - 1, cap - 1, -1))
         self.global_step = 0
         self.samples = 0
         self.done = False
@@ -136,6 +144,7 @@ class PopulationSweep:
         # steps vs the sync work, including any idle the host causes) -- see gpu_timeline()
         self._timeline = [] if (os.environ.get("MOPT_GPU_TIMELINE") == "1"
                                 and pop.device.type == "cuda") else None
+        self._copy_marks: list = []   # (sync number, "save" | "load", event, event)
         # observability / failure detection (utils/events.py, parallel/watchdog.py)
         self.events = events if events is not None else NullEventLog()
         self.trial_events = bool(trial_events) and events is not None
@@ -1064,7 +1073,7 @@ class PopulationSweep:
                             self._free_ck.append(idx_old)
                     to_save.append((s, self._free_ck.pop(), int(self.slot_key[s])))
         if to_save:
-            metas = pop.save_states([(s, idx) for s, idx, _ in to_save])
+            metas = self._timed("save", pop.save_states, [(s, idx) for s, idx, _ in to_save])
             for (_, _, key), meta in zip(to_save, metas):
                 self.ckpts[key] = meta
         for s in leaving:
@@ -1108,10 +1117,10 @@ class PopulationSweep:
             self.slot_key[s] = int(a[1])
             self.slot_budget[s] = int(a[8])
         if loads:
-            pop.load_states(loads)
+            self._timed("load", pop.load_states, loads)
         # pool entries that only carried a C4 transfer are free again (the loads above read them
-        # first: later saves into them are queued behind on the same stream)
-        self._free_ck.extend(m["ck"] for m in received_pool.values())
+        # first: later receives into them are queued behind on the same stream)
+        self._c4_free.extend(m["ck"] for m in received_pool.values())
         for s, cfg in hp_updates:
             extra = {"batch_size": cfg.batch_size} if cfg.batch_size else {}
             pop.update_hparams(s, lr=cfg.lr, momentum=cfg.momentum,
@@ -1175,11 +1184,11 @@ class PopulationSweep:
         return states, metas
 
     def _take_pool_entry(self) -> int:
-        """A free checkpoint-pool entry (the oldest checkpoint is evicted when none is)."""
-        if not self._free_ck:
-            _, old = self.ckpts.popitem(last=False)
-            self._free_ck.append(old["ck"])
-        return self._free_ck.pop()
+        """A pool entry reserved for C4 receives (one per slot: a rank receives at most one
+        transfer per slot and sync) -- never a checkpoint's entry."""
+        if not self._c4_free:
+            raise RuntimeError("C4 receive entries exhausted (more receives than slots)")
+        return self._c4_free.pop()
 
     def _max_budget_local(self) -> int:
         return getattr(self, "_mb", None) or self._compute_mb()
@@ -1195,6 +1204,33 @@ class PopulationSweep:
         ev = torch.cuda.Event(enable_timing=True)
         ev.record(torch.cuda.current_stream(self.pop.device))
         self._timeline.append((kind, ev, time.perf_counter()))
+
+    def _timed(self, kind: str, fn, *args):
+        """``fn(*args)``; with the GPU timeline on, the GPU time of the work it enqueues is
+        recorded per sync (checkpoint saves / loads: the PBT exploit copies)."""
+        if self._timeline is None:
+            return fn(*args)
+        stream = torch.cuda.current_stream(self.pop.device)
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        out = fn(*args)
+        e1.record(stream)
+        self._copy_marks.append((self.n_syncs, kind, e0, e1))
+        return out
+
+    def copy_times(self, clear: bool = True) -> Dict[int, Dict[str, float]]:
+        """{sync number: {"save": ms, "load": ms}} of checkpoint copies (MOPT_GPU_TIMELINE=1)."""
+        if not self._copy_marks:
+            return {}
+        torch.cuda.synchronize()
+        out: Dict[int, Dict[str, float]] = {}
+        for n, kind, e0, e1 in self._copy_marks:
+            d = out.setdefault(n, {})
+            d[kind] = d.get(kind, 0.0) + e0.elapsed_time(e1)
+        if clear:
+            self._copy_marks = []
+        return out
 
     def gpu_timeline(self, clear: bool = True) -> dict:
         """Mean GPU-stream ms of the train steps of an interval and of the sync work between

@@ -228,11 +228,18 @@ def _child(conn, spec, builder, seed_docs, applied=None):  # pragma: no cover - 
             # everything already waiting is applied as one backlog: a lagging child merges a
             # trial's registration and its result into one insert (WriteBehind._apply_batch)
             n = 0
+            gone = False
             while msg is not None and msg[0] == "ops":
                 n += len(msg[1])
                 wb.extend(msg[1])
-                msg = conn.recv() if conn.poll() else None
+                try:
+                    msg = conn.recv() if conn.poll() else None
+                except EOFError:            # the parent died mid-backlog: apply what arrived
+                    msg, gone = None, True
             wb.drain_all(4096)
+            if gone:
+                wb.flush()
+                return
             if applied is not None:         # the parent's view of the child's backlog
                 applied.value += n
             gc.freeze()                     # the applied documents live on: out of the GC scan

@@ -24,7 +24,9 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 DEFAULT_POP = {"logreg": 64, "mlp": 256, "resnet20": 32, "lm-125m": 8, "lm-tiny": 16}
-DEFAULT_SYNC = {"logreg": 32, "mlp": 32, "resnet20": 30, "lm-125m": 50, "lm-tiny": 50}
+# the LM configs sync at the PBT interval (exploit / explore every 200 steps): the syncs between
+# two generation boundaries would only read statistics back
+DEFAULT_SYNC = {"logreg": 32, "mlp": 32, "resnet20": 30, "lm-125m": 200, "lm-tiny": 200}
 
 
 def run_sweep(args, comm):
@@ -51,6 +53,9 @@ def run_sweep(args, comm):
                                pool_size=P * comm.world_size)
     sweep = PopulationSweep(pop, task, data, comm=comm, experiment=exp, sync_every=sync_every,
                             ckpt_capacity=max(4, int(spec.ckpt_factor * P)))
+    on_gpu = comm.device.type == "cuda"
+    if on_gpu and sweep._timeline is None:
+        sweep._timeline = []   # GPU events at interval starts / syncs (per-generation report)
     sweep.start()
     for _ in range(args.warmup):
         sweep.step()
@@ -58,9 +63,17 @@ def run_sweep(args, comm):
     s0, c0 = sweep.samples, sweep.completed
     sweep.timers.clear()
     sweep.n_syncs = 0
+    if on_gpu:
+        sweep._timeline = []
+        sweep.copy_times(clear=True)
+    marks = []                 # (host time after the sync, completed so far, global step)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         sweep.step()
+        if sweep.global_step % sync_every == 0:
+            marks.append((time.perf_counter(), sweep.completed, sweep.global_step))
+    if on_gpu:
+        sweep._mark("interval")   # closes the last sync's GPU span
     sweep.flush()
     sync(comm)
     elapsed = comm.max_float(time.perf_counter() - t0)
@@ -84,12 +97,83 @@ def run_sweep(args, comm):
            else None,
            "host_ms_per_sync": {k: round(1e3 * v / max(sweep.n_syncs, 1), 3)
                                 for k, v in sweep.timers.items()}}
+    if on_gpu:
+        spans = _gpu_spans(sweep._timeline)
+        out["gpu_ms_train_per_interval"] = _mean([a for a, _ in spans])
+        out["gpu_ms_sync_per_interval"] = _mean([b for _, b in spans])
     if comm.is_root:
         summ = sweep.summary()
         out["best_val_loss"] = summ["best_val_loss"]
         out["algorithm"] = args.algo or next(iter(spec.algorithm(args.seed, P * comm.world_size)))
+        inner = getattr(sweep.algorithm, "algorithm", sweep.algorithm)
+        if hasattr(inner, "exploit_counts"):
+            out.update(_pbt_report(sweep, inner, marks, t0, c0,
+                                   spans if on_gpu else None,
+                                   sweep.copy_times() if on_gpu else {}))
     sweep.close()
     return out
+
+
+def _mean(v):
+    return round(sum(v) / len(v), 3) if v else None
+
+
+def _gpu_spans(timeline):
+    """[(GPU ms of an interval's train steps, GPU ms from its sync to the next interval)] from
+    the sweep's alternating interval / sync events (the sync span holds evaluation, checkpoint
+    copies, member initialisation and any idle while the host decides)."""
+    if not timeline:
+        return []
+    torch.cuda.synchronize()
+    ev = [e for _, e, _ in timeline]
+    kinds = [k for k, _, _ in timeline]
+    out = []
+    for i in range(len(kinds) - 2):
+        if kinds[i] == "interval" and kinds[i + 1] == "sync" and kinds[i + 2] == "interval":
+            out.append((ev[i].elapsed_time(ev[i + 1]), ev[i + 1].elapsed_time(ev[i + 2])))
+    return out
+
+
+def _pbt_report(sweep, algo, marks, t0, c0, spans, copies):
+    """Per PBT generation boundary inside the timed window: wall ms of the generation (its
+    training steps plus the boundary's evaluation, decision and exploit copies), the GPU split,
+    the exploits / explores issued there and the generation's best validation loss."""
+    counts = algo.exploit_counts()
+    timeline = list(algo.timeline)
+    best_by_budget = {}
+    for _, _, vl, budget, _ in sweep.history:
+        best_by_budget[budget] = min(vl, best_by_budget.get(budget, float("inf")))
+    gens, prev_t, prev_c = [], t0, c0
+    for i, (t, c, step) in enumerate(marks):
+        row = {"end_step": step, "wall_ms": round(1e3 * (t - prev_t), 2),
+               "completed": c - prev_c}
+        if spans is not None and i < len(spans):
+            row["gpu_train_ms"] = round(spans[i][0], 2)
+            row["gpu_sync_ms"] = round(spans[i][1], 2)
+        cp = copies.get(i, {})
+        row["copy_ms"] = {k: round(v, 3) for k, v in cp.items()}
+        if c - prev_c:
+            # the members finishing here completed generation g; successors fork from it
+            budgets = sorted({h[3] for h in sweep.history[prev_c:c]})   # one per completion
+            g = timeline.index(budgets[-1]) if budgets and budgets[-1] in timeline else None
+            if g is not None:
+                row["generation"] = g
+                row["exploits"], row["explores"] = counts.get(g, (0, 0))
+                row["best_val_loss"] = round(best_by_budget.get(timeline[g], float("nan")), 5)
+        gens.append(row)
+        prev_t, prev_c = t, c
+    bounds = [r for r in gens if "generation" in r]
+    over = [100.0 * (r["wall_ms"] - r["gpu_train_ms"]) / r["wall_ms"]
+            for r in bounds if r.get("gpu_train_ms")]
+    copy_ms = [sum(r["copy_ms"].values()) for r in bounds]
+    return {"pbt_interval": (timeline[1] - timeline[0]) if len(timeline) > 1 else None,
+            "generations": gens,
+            "exploit_rounds": sum(1 for r in bounds if r.get("exploits")),
+            "exploits": sum(r.get("exploits", 0) for r in bounds),
+            "explores": sum(r.get("explores", 0) for r in bounds),
+            "ms_per_generation": _mean([r["wall_ms"] for r in bounds]),
+            "exploit_copy_ms_per_generation": _mean(copy_ms),
+            "generation_overhead_pct": _mean(over)}
 
 
 def run_hyper(args, comm):
@@ -141,6 +225,12 @@ def main():
     ap.add_argument("--algo", default=None,
                     help="override the config's search algorithm (e.g. random), default seed")
     args = ap.parse_args()
+    if args.config != "hyper":
+        every = args.sync_every or DEFAULT_SYNC[args.config]
+        if args.steps % every or args.warmup % every:
+            ap.error(f"--steps ({args.steps}) and --warmup ({args.warmup}) must be multiples of "
+                     f"the sync interval ({every}): the timed window must hold whole intervals, "
+                     "syncs included")
     from metaopt_amd.parallel.comm import init_from_env, shutdown
     comm = init_from_env()
     out = run_hyper(args, comm) if args.config == "hyper" else run_sweep(args, comm)

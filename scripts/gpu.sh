@@ -63,11 +63,11 @@ for step in "$@"; do
       pmc pmc_write WRITE_SIZE
       pmc pmc_mfma SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES
       pmc pmc_lds SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAVE_CYCLES ;;
-    lm)         $T 300 python scripts/bench_configs.py --config lm-125m --steps 20 --warmup 10 > "$OUT/lm.json" 2> "$OUT/lm.err" ;;
+    lm)         $T 300 python scripts/bench_configs.py --config lm-125m --steps 600 --warmup 0 > "$OUT/lm.json" 2> "$OUT/lm.err" ;;
     resnet)     $T 300 python scripts/bench_configs.py --config resnet20 --steps 60 --warmup 30 > "$OUT/resnet20.json" 2> "$OUT/resnet20.err" ;;
     hyper)      $T 300 python scripts/bench_configs.py --config hyper --steps 3 --warmup 1 > "$OUT/hyper.json" 2> "$OUT/hyper.err" ;;
-    trace_lm)   prof trace_lm 300 -- python3 "$ROOT/scripts/bench_configs.py" --config lm-125m --steps 6 --warmup 4 ;;
-    trace_resnet) prof trace_resnet 300 -- python3 "$ROOT/scripts/bench_configs.py" --config resnet20 --steps 20 --warmup 10 ;;
+    trace_lm)   prof trace_lm 300 -- python3 "$ROOT/scripts/bench_configs.py" --config lm-125m --sync-every 2 --steps 6 --warmup 4 ;;
+    trace_resnet) prof trace_resnet 300 -- python3 "$ROOT/scripts/bench_configs.py" --config resnet20 --sync-every 10 --steps 20 --warmup 10 ;;
     trace_hyper) prof trace_hyper 300 -- python3 "$ROOT/scripts/bench_configs.py" --config hyper --steps 1 --warmup 1 ;;
     gemm)       $T 300 python scripts/gemm_bench.py --cfgs "${CFGS:-0,5,6,7}" --splits "${SPLITS:-}" --out "$OUT/gemm.json" > "$OUT/gemm.log" 2>&1 ;;
     gemm32)     $T 300 python scripts/gemm_f32_bench.py --out "$OUT/gemm32.json" > "$OUT/gemm32.log" 2>&1 ;;

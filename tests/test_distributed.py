@@ -191,18 +191,24 @@ def _c4_flat_worker(rank, world, port, q):
     pop.hp[0]["t"] = 5
     sweep = PopulationSweep(pop, task, data=None, comm=comm, experiment=exp, sync_every=8,
                             ckpt_capacity=4, pipelined=False)
-    free0 = len(sweep._free_ck)
-    if rank == 0:
-        sweep.ckpts[999] = pop.save_states([(0, sweep._free_ck.pop())])[0]
+    # both pools full: rank 0 sends its OLDEST checkpoint; the receive must not
+    # evict anything on rank 1 (rank 0 mirrors every rank's FIFO without hearing of receives)
+    keys = [999, 1000, 1001, 1002] if rank == 0 else [2000, 2001, 2002, 2003]
+    for k in keys:
+        sweep.ckpts[k] = pop.save_states([(0, sweep._free_ck.pop())])[0]
+    assert not sweep._free_ck
+    c4_free0 = len(sweep._c4_free)
     assign = np.zeros((2 * 3 + 1, AS_COLS))
     assign[3 + 2] = (RESUME, 0, 0, 0.1, 0.9, 0, 0, 7, 16, 999, 0, 0)
     states, metas = sweep._exchange_checkpoints(assign)
     out = None
+    assert list(sweep.ckpts) == keys                    # nothing evicted on either rank
     if rank == 1:
         assert not states and sorted(metas) == [2]
+        assert metas[2]["ck"] not in [m["ck"] for m in sweep.ckpts.values()]
         pop.load_states([(2, metas[2])])
         out = (metas[2]["t"], float(pop.slot_state(2)["p32"].double().sum()),
-               len(sweep._free_ck) == free0 - 1)
+               len(sweep._c4_free) == c4_free0 - 1)
     else:
         out = (5, float(pop.slot_state(0)["p32"].double().sum()), True)
     q.put((rank, out))
@@ -242,6 +248,22 @@ def test_visible_gpu_count_from_kfd_topology(tmp_path):
     assert visible_gpu_count({"ROCR_VISIBLE_DEVICES": "1", "HIP_VISIBLE_DEVICES": "0,1"}, root) == 1
     assert visible_gpu_count({"CUDA_VISIBLE_DEVICES": "-1"}, root) == 0
     assert visible_gpu_count({}, str(tmp_path / "absent")) == 0
+    assert visible_gpu_count({"MOPT_GPU_COUNT": "2"}, str(tmp_path / "absent")) == 2
+
+
+def test_visible_gpu_count_skips_inaccessible_render_nodes(tmp_path):
+    """a container given some of the host's render nodes still sees every GPU in
+    sysfs; only GPUs whose /dev/dri/renderD<minor> this process can open are counted."""
+    from metaopt_amd.parallel.launch import visible_gpu_count
+    root = _fake_kfd(tmp_path / "nodes", [0, 1024, 1024, 1024])
+    for i, minor in ((1, 128), (2, 136), (3, 144)):
+        with open(tmp_path / "nodes" / str(i) / "properties", "a") as f:
+            f.write(f"drm_render_minor {minor}\n")
+    dri = tmp_path / "dri"
+    dri.mkdir()
+    (dri / "renderD128").write_text("")
+    (dri / "renderD144").write_text("")
+    assert visible_gpu_count({}, root, str(dri)) == 2
 
 
 def test_launcher_never_imports_torch_before_spawning():

@@ -297,6 +297,38 @@ def test_writer_process_killed_child_falls_back_in_process():
     assert docs["late"]["params"][0]["value"] == 99.0
 
 
+def test_writer_child_applies_backlog_when_parent_dies_mid_drain(tmp_path):
+    """the child's backlog drain polled then received; a dead parent makes poll()
+    true and recv() raise EOFError -- the writes already taken from the pipe must still land."""
+    import datetime
+    from metaopt_amd.storage.database import PickledDB
+    from metaopt_amd.storage.protocol import DocumentStorage
+    from metaopt_amd.worker.writer import DocBuilder, _child
+    path = str(tmp_path / "db.pkl")
+    b = DocBuilder(7, ["/x"], ["real"])
+    now = datetime.datetime.utcnow()
+    ops = [("register", (f"t{i}", now, (float(i),), None)) for i in range(6)]
+
+    class DeadParentConn:
+        def __init__(self, msgs):
+            self.msgs = list(msgs)
+
+        def recv(self):
+            if not self.msgs:
+                raise EOFError
+            return self.msgs.pop(0)
+
+        def poll(self):
+            return True          # a closed pipe polls readable
+
+        def send(self, msg):
+            raise AssertionError("nothing is sent to a dead parent")
+
+    _child(DeadParentConn([("ops", ops[:3]), ("ops", ops[3:])]), ("pickleddb", path), b, None)
+    docs = DocumentStorage(PickledDB(host=path)).database.read("trials", {"experiment": 7})
+    assert sorted(d["_id"] for d in docs) == [f"t{i}" for i in range(6)]
+
+
 def test_writer_process_child_that_cannot_open_the_database(tmp_path):
     """A child that fails at start-up (here: a PickledDB path whose parent is a file) is seen
     as dead; the writes land through the parent's own storage."""

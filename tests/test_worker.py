@@ -248,6 +248,37 @@ class TestPacemaker:
             for pm in pms:
                 pm.stop()
 
+    def test_single_slow_beat_keeps_beating(self):
+        """with the only pacemaker's beat running longer than the dispatcher's idle
+        exit, the dispatcher used to exit and the re-queued beat was never served again."""
+        from metaopt_amd.worker.pacemaker import _SCHEDULER
+        exp = _exp(name="hb_slow")
+        exp.register_trial(Trial(experiment=exp.id,
+                                 params=[dict(name="/x", type="real", value=0.5)]))
+        t = exp.reserve_trial()
+        calls = []
+
+        class SlowStorage:
+            def get_trial(self, trial):
+                calls.append(time.monotonic())
+                if len(calls) == 1:
+                    time.sleep(_SCHEDULER.IDLE_EXIT_S * 1.6)   # outlives the idle exit
+                return exp.storage.get_trial(trial)
+
+            def update_heartbeat(self, trial):
+                return exp.storage.update_heartbeat(trial)
+
+        pm = TrialPacemaker(t, wait_time=0.05, storage=SlowStorage())
+        pm.start()
+        try:
+            deadline = time.monotonic() + _SCHEDULER.IDLE_EXIT_S * 1.6 + 2.0
+            while len(calls) < 3 and time.monotonic() < deadline:
+                time.sleep(0.05)
+            assert len(calls) >= 3, calls
+            assert not pm.stopped.is_set()
+        finally:
+            pm.stop()
+
 
 # ------------------------------------------------------------------ study API
 class TestStudy:
