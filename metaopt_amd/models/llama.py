@@ -4,14 +4,16 @@
 is stacked over the population (``[P, ...]``), so a step is a handful of batched launches
 regardless of ``P``:
 
-* GEMMs: ``torch.bmm`` over the population dimension (hipBLASLt strided-batched: plain library
-  GEMMs, the one place we do not hand-write the kernel);
+* GEMMs: ``pbmm`` over the population dimension -- the hand-written gfx950 population GEMM
+  (``ops/gemm.py`` -> ``csrc/pgemm.hip`` ``pgemm_big_kernel``: bf16 MFMA 16x16x32, f32
+  accumulation, the SwiGLU and RoPE epilogues fused); no library GEMM runs in the step;
 * embedding gather/scatter, RMSNorm, RoPE + head split, causal flash attention, SwiGLU, the
   vocabulary cross-entropy and the per-trial fused AdamW: hand-written gfx950 kernels
   (:mod:`metaopt_amd.ops.lm`);
 * parameters live in flat buffers -- bf16 working copy ``p16`` (autograd leaves are views of it,
-  with their ``.grad`` pre-bound to views of the flat bf16 gradient ``g16``), f32 master ``p32``,
-  AdamW moments ``m``/``v`` -- so the optimizer is ONE fused kernel over all tensors and trials,
+  with their ``.grad`` pre-bound to views of the flat bf16 gradient ``g16``), the f32 master
+  (on the GPU split: ``p16`` is its high half, ``plo`` the int16 low half), AdamW moments
+  ``m``/``v`` -- so the optimizer is ONE fused kernel over all tensors and trials,
   and a checkpoint / PBT exploit copy of a trial is a fixed set of contiguous slices.
 
 The member interface (``set_member``, ``update_hparams``, ``save_states``/``load_states``,

@@ -197,7 +197,9 @@ def run_hyper(args, comm):
             "outer_steps_per_sec": round(args.steps / elapsed, 4),
             "inner_steps_per_sec": round(inner / elapsed, 2),
             "tokens_per_sec": round(inner * 4 * 128 / elapsed, 1),
-            "final": hist[-1] if hist else None, "dtype": "fp32 (second-order)",
+            "final": hist[-1] if hist else None,
+            "dtype": "bf16-operand MFMA GEMMs with fp32 accumulation; fp32 activations, "
+                     "weights, tangents and optimizer state",
             "data": "synthetic"}
 
 

@@ -53,7 +53,7 @@ for step in "$@"; do
                   $T 240 python bench.py --steps 43 --warmup 5 ${v#*:} > "$OUT/algo_${v%%:*}.json" 2> "$OUT/algo_${v%%:*}.err"; done ;;
     random)     $T 240 python bench.py --steps 20 --warmup 5 --algo random > "$OUT/bench_random.json" 2> "$OUT/bench_random.err" ;;
     timeline)   MOPT_GPU_TIMELINE=1 $T 240 python bench.py --steps 20 --warmup 5 $BENCH_ARGS > "$OUT/bench_timeline$TAG.json" 2> "$OUT/bench_timeline$TAG.err" ;;
-    streams)    for s in 1 2; do MOPT_STREAMS=$s $T 240 python bench.py --steps 20 --warmup 5 > "$OUT/bench_streams$s.json" 2> "$OUT/bench_streams$s.err"; done ;;
+    streams)    for s in ${STREAM_SET:-1 2}; do MOPT_STREAMS=$s $T 240 python bench.py --steps 20 --warmup 5 > "$OUT/bench_streams$s.json" 2> "$OUT/bench_streams$s.err"; done ;;
     kbench)     $T 200 python scripts/kernel_bench.py --momentum-dtype bf16 --out "$OUT/kbench.json" > "$OUT/kbench.log" 2>&1 ;;
     kbench_ab)  for v in ${VARIANTS:-0 1}; do env ${ABVAR:-MOPT_AB}=$v $T 200 python scripts/kernel_bench.py --momentum-dtype bf16 --out "$OUT/kbench_v$v.json" > "$OUT/kbench_v$v.log" 2>&1; done ;;
     kbench_rows) for b in 128 256 512; do $T 200 python scripts/kernel_bench.py --momentum-dtype bf16 --batch $b --iters 20 --out "$OUT/kbench_b$b.json" > "$OUT/kbench_b$b.log" 2>&1; done ;;
