@@ -609,6 +609,11 @@ __global__ __launch_bounds__(512) void pgemm_big_kernel(const GemmArgs g) {
   }
 }
 
+// (Round 5: a 3-stage LDS-ring variant of this kernel -- 256 x 128 / 128 x 256 tiles, 144 KB of
+// LDS, fills two K-steps ahead behind counted vmcnt waits and one raw s_barrier per K-step, the
+// C stores in inline asm so the counts were exact -- passed every GEMM test but ran 670-860
+// TFLOP/s against 900-1190 for this kernel's best tile on every LM shape; removed,
+// profiles/round5.md "3-stage ring GEMM".)
 // (Round 4: a register-pipelined variant -- the operands of K-step t + 3 loaded into one of two
 // register sets while step t is multiplied, written to the free LDS stage two steps later --
 // was correct but 2.5-4x slower: the two register sets on top of the accumulators exceed the

@@ -101,8 +101,13 @@ __device__ __forceinline__ void w_coords(int64_t e, int N, int, int& n, int& k) 
 // kCountStep: advance the trial's step counter hp.t (the hidden layers of the same step read
 // hp.t + 1; the backward, launched after, reads the new value) -- saves the per-step increment
 // launch.
-enum FwdFlags { kRelu = 1, kDropout = 2, kWriteGrad = 4, kStoreStats = 8, kCountStep = 16 };
-enum BwdFlags { kHasDx = 1, kInDropout = 2, kUpdateBias = 4 };
+// kNarrow (loss layer, <= 16 classes): the layer's N is padded to one 64-wide tile but only its
+// first 16 rows of W (and columns of dZ) can be non-zero -- the kernels skip the other 48 rows'
+// weight / optimizer traffic and MFMAs (the 10-class head moved 4x its real bytes per step).
+enum FwdFlags { kRelu = 1, kDropout = 2, kWriteGrad = 4, kStoreStats = 8, kCountStep = 16,
+                kNarrowCE = 32 };
+enum BwdFlags { kHasDx = 1, kInDropout = 2, kUpdateBias = 4, kNarrow = 8 };
+constexpr int kNarrowRows = 16;
 // kSGD16: SGD with the momentum buffer stored as bf16 (RNE after every update; the update uses
 // the rounded value) -- 4 bytes per parameter and step less HBM traffic than kSGD.
 enum Opt { kSGD = 0, kAdamW = 1, kSGD16 = 2 };
@@ -129,8 +134,8 @@ enum Opt { kSGD = 0, kAdamW = 1, kSGD16 = 2 };
     x1 = *(const uint4*)(X + (uint32_t)(g1 + kk_));     \
     x2 = *(const uint4*)(X + (uint32_t)(g2 + kk_));     \
     x3 = *(const uint4*)(X + (uint32_t)(g3 + kk_));     \
-    w0 = *(const uint4*)(W + (uint32_t)(gw0 + kw_));    \
-    if (TN >= 64) w1 = *(const uint4*)(W + (uint32_t)(gw1 + kw_)); \
+    if (WROWS >= 32 || w_live) w0 = *(const uint4*)(W + (uint32_t)(gw0 + kw_)); \
+    if (TN >= 64 && WROWS >= 64) w1 = *(const uint4*)(W + (uint32_t)(gw1 + kw_)); \
     if (TN >= 128) {                                    \
       w1##b = *(const uint4*)(W + (uint32_t)(gw2 + kw_)); \
       w1##c = *(const uint4*)(W + (uint32_t)(gw3 + kw_)); \
@@ -152,28 +157,32 @@ enum Opt { kSGD = 0, kAdamW = 1, kSGD16 = 2 };
 
 // TN: output features per tile (64, or 32 for twice the workgroups: the hidden layers' launches
 // hold ~1.5 workgroups per slot of the chip at 64, a tail of half-empty CUs)
-template <int TN>
+// WROWS: rows of the W tile that can be non-zero (TN, or kNarrowRows for a narrow loss layer:
+// only those B fragments are read and multiplied)
+template <int TN, int WROWS = TN>
 __device__ __forceinline__ void fwd_step(const bf16_t* As, const bf16_t* Bs, int wave, int li,
                                          int g, f32x4 (&acc)[2][TN / 16]) {
+  constexpr int NJ = (WROWS < TN ? WROWS : TN) / 16;
 #pragma unroll
   for (int ks = 0; ks < BK / 32; ++ks) {
-    bf16x8 a[2], b[TN / 16];
+    bf16x8 a[2], b[NJ];
 #pragma unroll
     for (int i = 0; i < 2; ++i) a[i] = lds_frag(As + TOFFF(wave * 32 + i * 16 + li, ks * 32 + g * 8));
 #pragma unroll
-    for (int j = 0; j < TN / 16; ++j) b[j] = lds_frag(Bs + TOFFF(j * 16 + li, ks * 32 + g * 8));
+    for (int j = 0; j < NJ; ++j) b[j] = lds_frag(Bs + TOFFF(j * 16 + li, ks * 32 + g * 8));
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < TN / 16; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
+      for (int j = 0; j < NJ; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
   }
 }
 
 // W: the tile's first row (w_off + n0 * w_row_stride(K)); N: rows of the layer's weight matrix
-template <int TN, int NSET = 2>
+template <int TN, int NSET = 2, int WROWS = TN>
 __device__ __forceinline__ void fwd_gemm(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                          int K, int N, bf16_t* As, bf16_t* Bs,
                                          f32x4 (&acc)[2][TN / 16]) {
+  static_assert(WROWS == TN || WROWS == kNarrowRows, "narrow tiles keep 16 W rows");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, g = lane >> 4;
 #pragma unroll
@@ -197,9 +206,11 @@ __device__ __forceinline__ void fwd_gemm(const bf16_t* __restrict__ X, const bf1
   bf16_t* bs2 = Bs + TOFFF(c2 >> 3, (c2 & 7) * 8);
   bf16_t* bs3 = Bs + TOFFF(c3 >> 3, (c3 & 7) * 8);
   const int klast = K - BK;
-  uint4 p0, p1, p2, p3, pw0, pw1{}, pw1b{}, pw1c{};  // K-steps 0, 3, 6, ...
-  uint4 q0, q1, q2, q3, qw0, qw1{}, qw1b{}, qw1c{};  // K-steps 1, 4, 7, ...
-  uint4 r0, r1, r2, r3, rw0, rw1{}, rw1b{}, rw1c{};  // K-steps 2, 5, 8, ...
+  // narrow: thread t stages W row t / 8 -- rows >= WROWS stay zero (never loaded)
+  const bool w_live = (c0 >> 3) < WROWS;
+  uint4 p0, p1, p2, p3, pw0{}, pw1{}, pw1b{}, pw1c{};  // K-steps 0, 3, 6, ...
+  uint4 q0, q1, q2, q3, qw0{}, qw1{}, qw1b{}, qw1c{};  // K-steps 1, 4, 7, ...
+  uint4 r0, r1, r2, r3, rw0{}, rw1{}, rw1b{}, rw1c{};  // K-steps 2, 5, 8, ...
   MOPT_FWD_LOAD(p0, p1, p2, p3, pw0, pw1, 0);
   MOPT_FWD_LOAD(q0, q1, q2, q3, qw0, qw1, min(BK, klast));
   if (NSET == 3) MOPT_FWD_LOAD(r0, r1, r2, r3, rw0, rw1, min(2 * BK, klast));
@@ -208,7 +219,7 @@ __device__ __forceinline__ void fwd_gemm(const bf16_t* __restrict__ X, const bf1
   MOPT_FWD_STORE(S##0, S##1, S##2, S##3, S##w0, S##w1);                  \
   __syncthreads();                                                       \
   MOPT_FWD_LOAD(S##0, S##1, S##2, S##3, S##w0, S##w1, min(KNEXT, klast)); \
-  fwd_step<TN>(As, Bs, wave, li, g, acc);                                \
+  fwd_step<TN, WROWS>(As, Bs, wave, li, g, acc);                         \
   __syncthreads();
   if (NSET == 3) {
     int k0 = 0;
@@ -249,10 +260,10 @@ __device__ __forceinline__ void fwd_gemm(const bf16_t* __restrict__ X, const bf1
 // (Measured and rejected: an LDS-free variant loading every MFMA fragment -- 16 bytes of one
 // row of X or W per lane -- straight from global memory ran the forward 2.5x slower than the
 // LDS-staged tiles above; profiles/README.md.)
-template <int TN, int NSET = 2>
+template <int TN, int NSET = 2, int WROWS = TN>
 __device__ __forceinline__ void fwd_core(const bf16_t* X, const bf16_t* W, int K, int N,
                                          bf16_t* As, bf16_t* Bs, f32x4 (&acc)[2][TN / 16]) {
-  fwd_gemm<TN, NSET>(X, W, K, N, As, Bs, acc);
+  fwd_gemm<TN, NSET, WROWS>(X, W, K, N, As, Bs, acc);
 }
 
 // Y[rows, n0:n0+TN] = dropout(relu(X W^T + b)) for one (trial-layer, n-tile, 128-row block).
@@ -318,9 +329,160 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) vo
   }
 }
 
+// ----------------------------------------------------------------------------------------------
+// Hidden-layer forward, W-direct variant (tile_n 128): a 128-row x 128-column tile per workgroup,
+// each wave owning 32 output columns for all 128 rows.  Only X goes through LDS (double-buffered
+// 80-element rows, one barrier per K-step); each wave loads its W B-fragments straight from HBM
+// into registers -- in the k-strip-major layout a fragment (16 rows x 32 k) is 16 x 64-B pieces
+// of one contiguous 2-KB block, the two k-halves of a row land in one 128-B line.  Per weight
+// byte the LDS moves 1 B of staging stores and 4 B of fragment reads (the 64-wide tile: 3 + 6).
+// An odd last tile (N - n0 = 64) leaves waves 2 and 3 without columns: they only stage X.
+// Register sets p / q hold two K-steps of loads in flight (X refilled before the MFMAs of the
+// step, W right after them).
+// ----------------------------------------------------------------------------------------------
+constexpr int TNW = 128;
+#ifndef MOPT_FWDW_WAVES
+#define MOPT_FWDW_WAVES 3   // waves per SIMD of the W-direct forward (variant builds sweep it)
+#endif
+constexpr int CSW = TNW + 8;   // epilogue staging row stride (elements)
+
+template <int WAVES>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) void mlp_fwd_wd_kernel(
+    const MlpTL* __restrict__ tls, const int2* __restrict__ work, int n_work,
+    const bf16_t* __restrict__ xb, const bf16_t* __restrict__ plo, const bf16_t* __restrict__ p16,
+    bf16_t* __restrict__ act, const TrialHP* __restrict__ hp, uint32_t step, int layer,
+    int flags) {
+  static_assert(BM * CSW <= 2 * BM * TSF, "epilogue tile must fit the X buffers");
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * BM * TSF];
+  const int2 wi = work[blockIdx.x];   // XCD-balanced order built on the host (_xcd_schedule)
+  if (wi.x < 0) return;                // padding: a no-op workgroup
+  const MlpTL tl = tls[wi.x];
+  const int K = tl.K, N = tl.N, n0 = wi.y * TNW, row0 = blockIdx.y * BM;
+  if (row0 >= tl.rows) return;         // a smaller batch than the launch's: uniform exit
+  const int tid = threadIdx.x, lane = tid & 63, li = lane & 15, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nw0 = n0 + 32 * wave;      // this wave's first output column
+  const bool wlive = nw0 < N;          // wave-uniform
+  const bf16_t* X = xb + tl.x_off + (size_t)row0 * K;
+  // lane's fragment base: column nw0 + li, k 8 g (fragment j adds 16 rows, k-half s adds 32)
+  const bf16_t* Wl = p16 + tl.w_off + (size_t)(wlive ? nw0 : n0) * BK + li * BK + g * 8;
+
+  f32x4 acc[8][2];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int c0 = tid, c1 = tid + 256, c2 = tid + 512, c3 = tid + 768;
+  const int g0 = (c0 >> 3) * K + (c0 & 7) * 8, g1 = (c1 >> 3) * K + (c1 & 7) * 8;
+  const int g2 = (c2 >> 3) * K + (c2 & 7) * 8, g3 = (c3 >> 3) * K + (c3 & 7) * 8;
+  const int a0 = TOFFF(c0 >> 3, (c0 & 7) * 8), a1 = TOFFF(c1 >> 3, (c1 & 7) * 8);
+  const int a2 = TOFFF(c2 >> 3, (c2 & 7) * 8), a3 = TOFFF(c3 >> 3, (c3 & 7) * 8);
+  const int klast = K - BK;
+  uint4 px0, px1, px2, px3, pw0{}, pw1{}, pw2{}, pw3{};   // even K-steps
+  uint4 qx0, qx1, qx2, qx3, qw0{}, qw1{}, qw2{}, qw3{};   // odd K-steps
+#define MOPT_FWDW_LX(S, k)                                     \
+  do {                                                         \
+    const uint32_t kk_ = (uint32_t)(k);                        \
+    S##x0 = *(const uint4*)(X + (uint32_t)(g0 + kk_));         \
+    S##x1 = *(const uint4*)(X + (uint32_t)(g1 + kk_));         \
+    S##x2 = *(const uint4*)(X + (uint32_t)(g2 + kk_));         \
+    S##x3 = *(const uint4*)(X + (uint32_t)(g3 + kk_));         \
+  } while (0)
+// (unconditional: an idle wave re-reads the live columns -- a load behind a branch made hipcc
+//  count it as possibly absent and wait for every younger load at the next X store)
+#define MOPT_FWDW_LW(S, k)                                     \
+  do {                                                         \
+    const bf16_t* w_ = Wl + (uint32_t)(k) * (uint32_t)N;       \
+    S##w0 = *(const uint4*)(w_);                               \
+    S##w1 = *(const uint4*)(w_ + 32);                          \
+    S##w2 = *(const uint4*)(w_ + 16 * BK);                     \
+    S##w3 = *(const uint4*)(w_ + 16 * BK + 32);                \
+  } while (0)
+  // one K-step from set S through LDS buffer B, refilling S with the step KNEXT
+#define MOPT_FWDW_STEP(S, B, KNEXT)                                                        \
+  {                                                                                        \
+    bf16_t* As_ = smem + (B) * BM * TSF;                                                   \
+    *(uint4*)(As_ + a0) = S##x0;                                                           \
+    *(uint4*)(As_ + a1) = S##x1;                                                           \
+    *(uint4*)(As_ + a2) = S##x2;                                                           \
+    *(uint4*)(As_ + a3) = S##x3;                                                           \
+    __syncthreads();                                                                       \
+    MOPT_FWDW_LX(S, min(KNEXT, klast));                                                    \
+    if (wlive) {                                                                           \
+      _Pragma("unroll") for (int s_ = 0; s_ < 2; ++s_) {                                   \
+        const bf16x8 b0_ = __builtin_bit_cast(bf16x8, s_ ? S##w1 : S##w0);                 \
+        const bf16x8 b1_ = __builtin_bit_cast(bf16x8, s_ ? S##w3 : S##w2);                 \
+        bf16x8 a_[8];                                                                      \
+        _Pragma("unroll") for (int i_ = 0; i_ < 8; ++i_)                                   \
+          a_[i_] = lds_frag(As_ + TOFFF(16 * i_ + li, 32 * s_ + 8 * g));                   \
+        _Pragma("unroll") for (int i_ = 0; i_ < 8; ++i_) {                                 \
+          acc[i_][0] = mfma16(a_[i_], b0_, acc[i_][0]);                                    \
+          acc[i_][1] = mfma16(a_[i_], b1_, acc[i_][1]);                                    \
+        }                                                                                  \
+      }                                                                                    \
+    }                                                                                      \
+    MOPT_FWDW_LW(S, min(KNEXT, klast));                                                    \
+  }
+  MOPT_FWDW_LX(p, 0);
+  MOPT_FWDW_LW(p, 0);
+  MOPT_FWDW_LX(q, min(BK, klast));
+  MOPT_FWDW_LW(q, min(BK, klast));
+  // whole pairs of K-steps (even steps: set p, buffer 0; odd: q, 1), then the odd last one --
+  // the next store into a buffer follows the barrier of the step in between, by which every
+  // wave has finished the MFMAs that read it
+  int k0 = 0;
+  for (; k0 + 2 * BK <= K; k0 += 2 * BK) {
+    MOPT_FWDW_STEP(p, 0, k0 + 2 * BK)
+    MOPT_FWDW_STEP(q, 1, k0 + 3 * BK)
+  }
+  if (k0 < K) {
+    MOPT_FWDW_STEP(p, 0, k0 + 2 * BK)
+  }
+#undef MOPT_FWDW_STEP
+#undef MOPT_FWDW_LX
+#undef MOPT_FWDW_LW
+  __syncthreads();                     // every wave is done reading both X buffers
+
+  const TrialHP h = hp[tl.trial];
+  const bool drop = (flags & kDropout) && h.drop > 0.f;
+  const float inv_keep = drop ? 1.f / (1.f - h.drop) : 1.f;
+  const uint32_t key = rng_key(h.seed, (uint32_t)layer, h.t + step);   // as mlp_fwd_kernel
+  bf16_t* Cs = smem;                   // [128][CSW]
+  if (wlive) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int cl = 32 * wave + 16 * j + li, col = n0 + cl;
+      const float bj = join_hilo(p16[tl.b_off + col], plo[tl.b_off + col]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * i + 4 * g + r;
+          float v = acc[i][j][r] + bj;
+          if (flags & kRelu) v = fmaxf(v, 0.f);
+          if (drop) {
+            const uint32_t idx = (uint32_t)((row0 + row) * N + col);
+            v = rng_uniform(key, idx) >= h.drop ? v * inv_keep : 0.f;
+          }
+          Cs[row * CSW + cl] = f2bf(v);
+        }
+    }
+  }
+  __syncthreads();
+  const int cpr = min(TNW, N - n0) / 8;    // 16-byte chunks per output row (16, or 8)
+  bf16_t* Y = act + tl.y_off + (size_t)row0 * N + n0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = tid + 256 * i, r = c >> 4, ch = c & 15;
+    if (ch < cpr) *(uint4*)(Y + (size_t)r * N + ch * 8) = *(const uint4*)(Cs + r * CSW + ch * 8);
+  }
+}
+
 // Output layer: logits = X W^T + b (N padded to 64 >= classes), fused softmax cross-entropy.
 // Writes dLogits = (softmax - onehot) * inv_b as bf16 (training) and accumulates the per-trial
-// loss sum and #correct (atomic, one add per wave).
+// loss sum and #correct (atomic, one add per wave).  NARROW (<= 16 classes): W rows 16..63 are
+// neither read nor multiplied, and only the first 16 dLogits columns are written (the narrow
+// backward reads no others).
+template <bool NARROW>
 __global__ __launch_bounds__(256) void mlp_fwd_ce_kernel(const MlpTL* __restrict__ tls,
                                                          const int2* __restrict__ work, int n_work,
                                                          const bf16_t* __restrict__ xb,
@@ -350,13 +512,14 @@ __global__ __launch_bounds__(256) void mlp_fwd_ce_kernel(const MlpTL* __restrict
   const bf16_t* W = p16 + tl.w_off;
 
   f32x4 acc[2][4];
-  fwd_core<64>(X, W, K, N, As, Bs, acc);
+  fwd_core<64, 2, NARROW ? kNarrowRows : 64>(X, W, K, N, As, Bs, acc);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, g = lane >> 4;
   const bf16_t* bias_hi = p16 + tl.b_off;
   const bf16_t* bias_lo = plo + tl.b_off;
+  constexpr int NJ = NARROW ? kNarrowRows / 16 : 4;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < NJ; ++j) {
     const int col = j * 16 + li;
     const float bj = join_hilo(bias_hi[col], bias_lo[col]);
 #pragma unroll
@@ -385,7 +548,7 @@ __global__ __launch_bounds__(256) void mlp_fwd_ce_kernel(const MlpTL* __restrict
       const float rs = 1.f / s;
       bf16_t* dz = grad + tl.y_off + (size_t)(row0 + tid) * N;
 #pragma unroll
-      for (int ch = 0; ch < BN / 8; ++ch) {
+      for (int ch = 0; ch < (NARROW ? kNarrowRows : BN) / 8; ++ch) {
         uint32_t w4[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -442,7 +605,7 @@ constexpr int bwd_waves(int opt, bool pf, int mode) {
   // AdamW and the multi-row-block pass spill at 168 VGPRs: they keep 2 waves per SIMD
   return (!pf && opt != kAdamW && mode != 1) ? 3 : 2;
 }
-template <int OPT, bool PF, int MODE>
+template <int OPT, bool PF, int MODE, bool NARROW = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     bwd_waves(OPT, PF, MODE), bwd_waves(OPT, PF, MODE)))) void mlp_bwd_opt_kernel(const MlpTL* __restrict__ tls,
                                                           const int2* __restrict__ work, int n_work,
@@ -485,6 +648,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, g = lane >> 4, q = li >> 2, pp = li & 3;
   const int wk = wave >> 1, wn = wave & 1;
+  // NARROW (the loss layer, N = 64 of which <= 16 rows live): thread t owns W rows t / 8 and
+  // t / 8 + 32 -- only threads < 128 (rows < 16) move weights / optimizer state, and only the
+  // first 16 dZ columns (8-column chunks 0, 1) are read; the rest stay zero in registers
+  const bool st_live = !NARROW || tid < 8 * kNarrowRows;
+  const bool z_live = !NARROW || (tid & 7) < kNarrowRows / 8;
 
   // Optimizer constants (uniform per workgroup).
   float c1 = 1.f, c2 = 1.f;
@@ -530,11 +698,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 #define MOPT_BWD_LOAD(NC, P)                                                                     \
   {                                                                                              \
     const bf16_t* zc_ = dZ + (NC);                                                               \
+    if (z_live) {                                                                                \
     P##z0 = *(const uint4*)(zc_ + zo0);                                                          \
     P##z1 = *(const uint4*)(zc_ + zo1);                                                          \
     P##z2 = *(const uint4*)(zc_ + zo2);                                                          \
     P##z3 = *(const uint4*)(zc_ + zo3);                                                          \
+    }                                                                                            \
     const size_t ob = (size_t)(NC) * WRS + wo;                                                   \
+    if (NARROW) {                                                                                \
+    if (st_live) {                                                                               \
+    P##wh0 = *(const uint4*)(W16 + ob);                                                          \
+    if (MODE != 2) {                                                                             \
+    P##wl0 = *(const uint4*)(WLO + ob);                                                          \
+    if (OPT == kSGD16) {                                                                         \
+      P##h0 = *(const uint4*)(M16 + ob);                                                         \
+    } else {                                                                                     \
+      P##m0 = *(const f32x4*)(M32 + ob);                                                         \
+      P##m1 = *(const f32x4*)(M32 + ob + 4);                                                     \
+    }                                                                                            \
+    if (OPT == kAdamW) {                                                                         \
+      P##v0 = *(const f32x4*)(V32 + ob);                                                         \
+      P##v1 = *(const f32x4*)(V32 + ob + 4);                                                     \
+    }                                                                                            \
+    }                                                                                            \
+    }                                                                                            \
+    } else {                                                                                     \
     P##wh0 = *(const uint4*)(W16 + ob);                                                          \
     P##wh1 = *(const uint4*)(W16 + ob + 32 * WRS);                                               \
     if (MODE != 2) {                                                                             \
@@ -554,6 +742,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
       P##v1 = *(const f32x4*)(V32 + ob + 4);                                                     \
       P##v2 = *(const f32x4*)(V32 + ob + 32 * WRS);                                              \
       P##v3 = *(const f32x4*)(V32 + ob + 32 * WRS + 4);                                          \
+    }                                                                                            \
     }                                                                                            \
     }                                                                                            \
   }
@@ -686,7 +875,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     __syncthreads();
     uint2 ph{}, pl{}, pm{};   // the row's first group, stored with the second
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < (NARROW ? 2 : 4); ++i) {
+      if (NARROW && !st_live) break;   // rows >= 16 of a narrow loss layer: zero, untouched
       // group i: row 32 (i / 2) + tid / 8, k 8 (tid % 8) + 4 (i % 2) .. + 3
       const int gr = 32 * (i >> 1) + (tid >> 3), gk = 8 * (tid & 7) + 4 * (i & 1);
       const f32x4 gv = *(const f32x4*)(Dw + FOFF(gr, gk));
@@ -732,7 +922,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     if (do_bias) {
       red[bpart * 64 + bcol] = bsum;
       __syncthreads();
-      if (tid < 64) {
+      if (tid < (NARROW ? kNarrowRows : 64)) {
         const float gb = red[tid] + red[64 + tid] + red[128 + tid] + red[192 + tid];
         bf16_t* bph = p16 + tl.b_off + nc + tid;
         bf16_t* bpl = plo + tl.b_off + nc + tid;
@@ -833,10 +1023,16 @@ template <int OPT, bool PF, int MODE>
 static void launch_bwd(int n_work, int grid_y, hipStream_t stream, const void* tls,
                        const void* work, const void* xb, void* grad, void* plo, void* p16,
                        void* m32, void* v32, const void* hp, int flags) {
-  hipLaunchKernelGGL((mlp_bwd_opt_kernel<OPT, PF, MODE>), dim3(n_work, grid_y), dim3(256), 0,
-                     stream, (const MlpTL*)tls, (const int2*)work, n_work, (const bf16_t*)xb,
-                     (bf16_t*)grad, (bf16_t*)plo, (bf16_t*)p16, (float*)m32, (float*)v32,
-                     (const TrialHP*)hp, flags);
+  if (flags & kNarrow)
+    hipLaunchKernelGGL((mlp_bwd_opt_kernel<OPT, PF, MODE, true>), dim3(n_work, grid_y), dim3(256),
+                       0, stream, (const MlpTL*)tls, (const int2*)work, n_work, (const bf16_t*)xb,
+                       (bf16_t*)grad, (bf16_t*)plo, (bf16_t*)p16, (float*)m32, (float*)v32,
+                       (const TrialHP*)hp, flags);
+  else
+    hipLaunchKernelGGL((mlp_bwd_opt_kernel<OPT, PF, MODE, false>), dim3(n_work, grid_y), dim3(256),
+                       0, stream, (const MlpTL*)tls, (const int2*)work, n_work, (const bf16_t*)xb,
+                       (bf16_t*)grad, (bf16_t*)plo, (bf16_t*)p16, (float*)m32, (float*)v32,
+                       (const TrialHP*)hp, flags);
 }
 
 // one layer's backward: 128-row batches -> the fused MODE 0 kernel (prefetch per the switch);
@@ -869,7 +1065,7 @@ static void launch_bwd_rows(int n_work, int n_rowblocks, hipStream_t stream, con
 // ------------------------------------------------------------------------------------------------
 extern "C" {
 
-int mopt_abi_version() { return 12; }
+int mopt_abi_version() { return 13; }
 
 // weight layout: 1 = k-strip-major [K/64][N][64] (the only layout)
 int mopt_mlp_w_layout() { return 1; }
@@ -893,6 +1089,13 @@ int mopt_mlp_fwd(const void* tls, const void* work, int n_work, int n_rowblocks,
                  const void* plo, const void* p16, void* act, const void* hp, unsigned step,
                  int layer, int flags, int tile_n, void* stream) {
   if (n_work <= 0) return 0;
+  if (tile_n == TNW) {
+    hipLaunchKernelGGL((mlp_fwd_wd_kernel<MOPT_FWDW_WAVES>), dim3(n_work, n_rowblocks), dim3(256), 0,
+                       (hipStream_t)stream, (const MlpTL*)tls, (const int2*)work, n_work,
+                       (const bf16_t*)xb, (const bf16_t*)plo, (const bf16_t*)p16, (bf16_t*)act,
+                       (const TrialHP*)hp, step, layer, flags);
+    return (int)hipGetLastError();
+  }
   if (tile_n != 64) return (int)hipErrorInvalidValue;
   // (three register sets at 3 waves / SIMD, with the same whole-group loop: step 654-656 vs
   //  651-654 us, bench 784-787 vs 790-791 trials/s -- profiles/round4.md)
@@ -908,11 +1111,18 @@ int mopt_mlp_fwd_ce(const void* tls, const void* work, int n_work, int n_rowbloc
                     void* correct, void* hp, float inv_b, int flags, void* stream) {
   if (n_work <= 0) return 0;
   if ((flags & kStoreStats) && n_rowblocks != 1) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(mlp_fwd_ce_kernel, dim3(n_work, n_rowblocks), dim3(256), 0,
-                     (hipStream_t)stream, (const MlpTL*)tls, (const int2*)work, n_work,
-                     (const bf16_t*)xb, (const bf16_t*)plo, (const bf16_t*)p16,
-                     (const int32_t*)labels, (bf16_t*)grad, (float*)loss, (float*)correct,
-                     (TrialHP*)hp, inv_b, flags);
+  if (flags & kNarrowCE)
+    hipLaunchKernelGGL(mlp_fwd_ce_kernel<true>, dim3(n_work, n_rowblocks), dim3(256), 0,
+                       (hipStream_t)stream, (const MlpTL*)tls, (const int2*)work, n_work,
+                       (const bf16_t*)xb, (const bf16_t*)plo, (const bf16_t*)p16,
+                       (const int32_t*)labels, (bf16_t*)grad, (float*)loss, (float*)correct,
+                       (TrialHP*)hp, inv_b, flags);
+  else
+    hipLaunchKernelGGL(mlp_fwd_ce_kernel<false>, dim3(n_work, n_rowblocks), dim3(256), 0,
+                       (hipStream_t)stream, (const MlpTL*)tls, (const int2*)work, n_work,
+                       (const bf16_t*)xb, (const bf16_t*)plo, (const bf16_t*)p16,
+                       (const int32_t*)labels, (bf16_t*)grad, (float*)loss, (float*)correct,
+                       (TrialHP*)hp, inv_b, flags);
   return (int)hipGetLastError();
 }
 
@@ -950,7 +1160,7 @@ struct MlpStep {
   float inv_b;      // <= 0: each trial's mean over its own rows (MlpTL::rows)
   int32_t n_stats;  // entries of loss / correct (the population's capacity)
   int32_t fwd_tn;   // hidden-layer forward tile width of the work lists (64)
-  int32_t pad;
+  int32_t narrow;   // 1: the loss layer has <= 16 classes (kNarrowCE / kNarrow launches)
 };
 
 int mopt_mlp_step(const MlpStep* s, const void* x, const void* y, void* stream) {
@@ -969,13 +1179,14 @@ int mopt_mlp_step(const MlpStep* s, const void* x, const void* y, void* stream) 
                        stream);
     if (err) return err;
   }
-  const int ce = kWriteGrad | kCountStep | (s->rb == 1 ? kStoreStats : 0);
+  const int ce = kWriteGrad | kCountStep | (s->rb == 1 ? kStoreStats : 0) |
+                 (s->narrow ? kNarrowCE : 0);
   err = mopt_mlp_fwd_ce(s->tls, s->fwd[L - 1], s->n_fwd[L - 1], s->rb, L == 1 ? x : s->act,
                         s->plo, s->p16, y, s->grad, s->loss, s->correct, s->hp, s->inv_b, ce,
                         stream);
   if (err) return err;
   for (int l = L - 1; l >= 0; --l) {
-    int flags = kUpdateBias;
+    int flags = kUpdateBias | ((l == L - 1 && s->narrow) ? kNarrow : 0);
     if (l > 0) flags |= kHasDx | (s->drop ? kInDropout : 0);
     err = mopt_mlp_bwd(s->tls, s->bwd[l], s->n_bwd[l], l == 0 ? x : s->act, s->grad, s->plo,
                        s->p16, s->m32, s->v32, s->hp, s->opt, flags, s->rb, stream);

@@ -49,7 +49,9 @@ TILE = 64
 FWD_TN = 64             # hidden-layer forward tile width (csrc/pop_mlp.hip mopt_mlp_fwd)
 MAX_ROWS = 64 * 128     # csrc/pop_mlp.hip mopt_mlp_bwd: at most 64 row blocks per launch
 FWD_RELU, FWD_DROPOUT, FWD_WRITE_GRAD, FWD_STORE_STATS, FWD_COUNT_STEP = 1, 2, 4, 8, 16
-BWD_HAS_DX, BWD_IN_DROPOUT, BWD_UPDATE_BIAS = 1, 2, 4
+FWD_NARROW_CE = 32      # loss layer with <= NARROW_CLASSES classes: 16 of its 64 W rows live
+BWD_HAS_DX, BWD_IN_DROPOUT, BWD_UPDATE_BIAS, BWD_NARROW = 1, 2, 4, 8
+NARROW_CLASSES = 16
 
 
 class _MlpStep(ctypes.Structure):
@@ -62,7 +64,7 @@ class _MlpStep(ctypes.Structure):
                [(n, ctypes.c_void_p) for n in ("plo", "p16", "m32", "v32", "act", "grad", "hp",
                                                "loss", "correct")] + \
                [("inv_b", ctypes.c_float), ("n_stats", ctypes.c_int32),
-                ("fwd_tn", ctypes.c_int32), ("pad", ctypes.c_int32)]
+                ("fwd_tn", ctypes.c_int32), ("narrow", ctypes.c_int32)]
 OPTIMIZERS = {"sgd": 0, "adamw": 1}
 
 
@@ -257,7 +259,9 @@ class PopulationMLP:
         # optimizer state shares it; layer_views() returns row-major copies
         self.w_strip = backend == "hip" and self._lib.mopt_mlp_w_layout() == 1
         # output features per hidden-layer forward work item (csrc/pop_mlp.hip mlp_fwd_kernel TN)
-        self.fwd_tn = FWD_TN
+        self.fwd_tn = int(os.environ.get("MOPT_FWD_TN", FWD_TN))
+        if self.fwd_tn not in (64, 128):
+            raise ValueError("MOPT_FWD_TN must be 64 or 128")
         self.backend = backend
         # the population's trials are split into ``n_streams`` groups of equal cost whose train
         # steps run on their own HIP streams, unsynchronised between syncs: one group's
@@ -793,7 +797,7 @@ class PopulationMLP:
                 tl["gx_off"][i] = prev if l > 0 else -1
                 tl["rows"][i] = used
                 tn = self.fwd_tn if l < L - 1 else TILE   # the loss layer: one 64-wide tile
-                nt, nk = N // tn, K // TILE
+                nt, nk = -(-N // tn), K // TILE    # a 128-wide tiling ends in a 64-wide tile
                 # a forward tile costs ~K, a backward k-strip ~N
                 fwd.append(_work_list(np.repeat(i, nt), _ranges(nt), np.repeat(K, nt)))
                 bwd.append(_work_list(np.repeat(i, nk), _ranges(nk), np.repeat(N, nk)))
@@ -854,7 +858,7 @@ class PopulationMLP:
                     bad.append(f"{name} work item names a missing trial-layer")
                     break
                 tile = self.fwd_tn if (name == "fwd" and l < L - 1) else TILE
-                if (w[:, 1] < 0).any() or (w[:, 1] >= tl[per][idx] // tile).any():
+                if (w[:, 1] < 0).any() or (w[:, 1] >= -(-tl[per][idx] // tile)).any():
                     bad.append(f"{name} work item tile out of range")
                     break
         if bad:
@@ -900,6 +904,7 @@ class PopulationMLP:
         a.L, a.rb, a.drop = L, self.batch_size // 128, int(self._any_dropout)
         a.n_stats = self.capacity      # > 1 row block: the step zeroes loss/correct first
         a.fwd_tn = self.fwd_tn
+        a.narrow = int(self.num_classes <= NARROW_CLASSES)
         a.opt = 2 if self.momentum_dtype == "bf16" else OPTIMIZERS[self.optimizer]
         for n in ("plo", "p16", "m32", "v32", "act", "grad", "hp", "loss", "correct"):
             setattr(a, n, P[n])
@@ -1049,7 +1054,9 @@ class PopulationMLP:
             check(lib.mopt_mlp_step(part["step_ptr"], xp, yp, stream), "mlp_step")
             return
         L = self.L
-        ce_flags = FWD_WRITE_GRAD | FWD_COUNT_STEP | (FWD_STORE_STATS if rb == 1 else 0)
+        narrow = self.num_classes <= NARROW_CLASSES
+        ce_flags = FWD_WRITE_GRAD | FWD_COUNT_STEP | (FWD_STORE_STATS if rb == 1 else 0) | \
+            (FWD_NARROW_CE if narrow else 0)
         if rb != 1:
             self.stats[:2 * self.capacity].zero_()
         drop = self._any_dropout
@@ -1065,7 +1072,7 @@ class PopulationMLP:
                                   -1.0, ce_flags, stream), "mlp_fwd_ce")
         opt = 2 if self.momentum_dtype == "bf16" else OPTIMIZERS[self.optimizer]
         for l in range(L - 1, -1, -1):
-            flags = BWD_UPDATE_BIAS
+            flags = BWD_UPDATE_BIAS | (BWD_NARROW if (narrow and l == L - 1) else 0)
             if l > 0:
                 flags |= BWD_HAS_DX | (BWD_IN_DROPOUT if drop else 0)
             check(lib.mopt_mlp_bwd(tl, part["bwd"][l], part["n_bwd"][l], xp if l == 0 else act,
@@ -1160,7 +1167,9 @@ class PopulationMLP:
                                       tb["n_fwd"][L - 1], rb, src.data_ptr(), self.plo.data_ptr(),
                                       self.p16.data_ptr(), y.data_ptr(), self.grad.data_ptr(),
                                       self.eval_loss.data_ptr(), self.eval_correct.data_ptr(),
-                                      self.hp_dev.data_ptr(), 1.0, 0, stream), "mlp_fwd_ce(eval)")
+                                      self.hp_dev.data_ptr(), 1.0,
+                                      FWD_NARROW_CE if self.num_classes <= NARROW_CLASSES else 0,
+                                      stream), "mlp_fwd_ce(eval)")
         else:
             self.stats[2 * self.capacity:].zero_()
             xf = x.float()

@@ -15,7 +15,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from metaopt_amd.models.data import TeacherClassification  # noqa: E402
 from metaopt_amd.ops import _lib  # noqa: E402
-from metaopt_amd.ops.population import (BWD_HAS_DX, BWD_IN_DROPOUT, BWD_UPDATE_BIAS,  # noqa: E402
+from metaopt_amd.ops.population import (BWD_HAS_DX, BWD_IN_DROPOUT, BWD_NARROW, BWD_UPDATE_BIAS,  FWD_NARROW_CE, NARROW_CLASSES,  # noqa: E402
                                         FWD_DROPOUT, FWD_RELU, FWD_WRITE_GRAD, MemberConfig,
                                         PopulationMLP)
 
@@ -48,7 +48,9 @@ torch.cuda.synchronize()
 lib, tb, L = pop._lib, pop._tables["train"], pop.L
 stream = _lib.stream_ptr(dev)
 opt = (2 if args.momentum_dtype == "bf16" else 0) if args.optimizer == "sgd" else 1
-BWD_BYTES = {0: 16, 1: 24, 2: 12}[opt]     # split master r+w 8, + momentum (+ AdamW v)
+BWD_BYTES = {0: 16, 1: 24, 2: 12}[opt]
+_narrow = pop.num_classes <= NARROW_CLASSES and os.environ.get("MOPT_NARROW", "1") == "1"
+NARROW_CE, NARROW_BWD = (FWD_NARROW_CE, BWD_NARROW) if _narrow else (0, 0)     # split master r+w 8, + momentum (+ AdamW v)
 
 
 def run_fwd(l):
@@ -62,12 +64,13 @@ def run_fwd(l):
         lib.mopt_mlp_fwd_ce(tb["tl"].data_ptr(), tb["fwd"][l].data_ptr(), tb["n_fwd"][l], RB,
                             src.data_ptr(), pop.plo.data_ptr(), pop.p16.data_ptr(), y.data_ptr(),
                             pop.grad.data_ptr(), pop.loss.data_ptr(), pop.correct.data_ptr(),
-                            pop.hp_dev.data_ptr(), -1.0, FWD_WRITE_GRAD, stream)
+                            pop.hp_dev.data_ptr(), -1.0, FWD_WRITE_GRAD | NARROW_CE, stream)
 
 
 def run_bwd(l):
     src = x if l == 0 else pop.act
-    flags = BWD_UPDATE_BIAS | ((BWD_HAS_DX | BWD_IN_DROPOUT) if l > 0 else 0)
+    flags = BWD_UPDATE_BIAS | ((BWD_HAS_DX | BWD_IN_DROPOUT) if l > 0 else 0) | \
+        (NARROW_BWD if l == L - 1 else 0)
     lib.mopt_mlp_bwd(tb["tl"].data_ptr(), tb["bwd"][l].data_ptr(), tb["n_bwd"][l], src.data_ptr(),
                      pop.grad.data_ptr(), pop.plo.data_ptr(), pop.p16.data_ptr(),
                      pop.m32.data_ptr(), pop.v32.data_ptr(), pop.hp_dev.data_ptr(), opt, flags,

@@ -207,28 +207,32 @@ def test_swiglu_and_rmsnorm_match_reference_second_order():
     assert torch.allclose(h1, h2, rtol=1e-5, atol=1e-5)
 
 
-def _fd_population(dev, eta=0.3, mu=0.5, h=1e-3, steps=3):
+def _fd_population(dev, eta=0.3, mu=0.5, h=1e-3, steps=3, w0=None):
     """Five inner runs from ONE initialisation on the same batches: (eta, mu) and its central
-    finite-difference neighbours in eta and in mu.  Returns the hypergradient of run 0 and the
-    validation losses of all five."""
+    finite-difference neighbours in eta and in mu.  Returns the hypergradient of run 0, the
+    finite differences and the initial weights (``w0``: start from these instead -- the CPU
+    and GPU generators draw different initialisations from one seed)."""
     from metaopt_amd.models.hyper import HypergradLM
     from metaopt_amd.models.llama import SyntheticLM
     data = SyntheticLM(512, 64, 2, n_tokens=1 << 13, seed=0, device=dev)
     m = HypergradLM(5, "micro", batch_size=2, device=dev)
     m.reset([7] * 5, [eta, eta + h, eta - h, eta, eta], [mu, mu, mu, mu + h, mu - h])
+    if w0 is not None:
+        m.w.copy_(w0.to(m.w.device))
+    w_init = m.w.detach().clone().cpu()
     for k in range(steps):
         m.inner_step(*data.batch(k))
     hg, vl = m.hypergradient(*data.validation())
     vl = vl.double().cpu()
     fd = torch.tensor([(vl[1] - vl[2]) / (2 * h), (vl[3] - vl[4]) / (2 * h)])
-    return hg[0].double().cpu(), fd
+    return hg[0].double().cpu(), fd, w_init
 
 
 def test_hypergradient_matches_central_finite_difference_fp32():
     """d L_val / d(lr, momentum) of the forward-mode unrolled hypergradient equals the central
     finite difference of the fp32 validation loss after the same 3 inner steps (CPU, fp32
     throughout: the check of the derivation itself)."""
-    hg, fd = _fd_population("cpu")
+    hg, fd, _ = _fd_population("cpu")
     assert fd.abs().max() > 1e-2                      # a non-trivial derivative
     torch.testing.assert_close(hg, fd, rtol=2e-2, atol=2e-3)
 
@@ -238,6 +242,6 @@ def test_gpu_hypergradient_matches_fp32_finite_difference():
     """The HIP path (bf16-operand MFMA GEMMs, f32 accumulation, f32 activations / state) against
     the central finite difference of the fp32 CPU validation loss: the tolerance is the bf16
     operand rounding of the GEMMs (5 % relative)."""
-    hg, _ = _fd_population("cuda")
-    _, fd = _fd_population("cpu")
+    hg, _, w0 = _fd_population("cuda")
+    _, fd, _ = _fd_population("cpu", w0=w0)
     torch.testing.assert_close(hg, fd, rtol=5e-2, atol=5e-3)
