@@ -193,6 +193,7 @@ def run_rank(args) -> None:
                 "step": f"one sync interval = {S} optimizer steps of every trial + the sync "
                         "(validation, C1 all-gather, decide, C5 broadcast, member init/resume)",
                 "backend": pop.backend,
+                "stream_groups": pop.n_streams,
                 "optimizer_state": f"f32 master weights + bf16 copy, {args.momentum_dtype} "
                                    "SGD momentum",
                 "comm_backend": comm.backend or "none",

@@ -329,153 +329,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) vo
   }
 }
 
-// ----------------------------------------------------------------------------------------------
-// Hidden-layer forward, W-direct variant (tile_n 128): a 128-row x 128-column tile per workgroup,
-// each wave owning 32 output columns for all 128 rows.  Only X goes through LDS (double-buffered
-// 80-element rows, one barrier per K-step); each wave loads its W B-fragments straight from HBM
-// into registers -- in the k-strip-major layout a fragment (16 rows x 32 k) is 16 x 64-B pieces
-// of one contiguous 2-KB block, the two k-halves of a row land in one 128-B line.  Per weight
-// byte the LDS moves 1 B of staging stores and 4 B of fragment reads (the 64-wide tile: 3 + 6).
-// An odd last tile (N - n0 = 64) leaves waves 2 and 3 without columns: they only stage X.
-// Register sets p / q hold two K-steps of loads in flight (X refilled before the MFMAs of the
-// step, W right after them).
-// ----------------------------------------------------------------------------------------------
-constexpr int TNW = 128;
-#ifndef MOPT_FWDW_WAVES
-#define MOPT_FWDW_WAVES 3   // waves per SIMD of the W-direct forward (variant builds sweep it)
-#endif
-constexpr int CSW = TNW + 8;   // epilogue staging row stride (elements)
-
-template <int WAVES>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) void mlp_fwd_wd_kernel(
-    const MlpTL* __restrict__ tls, const int2* __restrict__ work, int n_work,
-    const bf16_t* __restrict__ xb, const bf16_t* __restrict__ plo, const bf16_t* __restrict__ p16,
-    bf16_t* __restrict__ act, const TrialHP* __restrict__ hp, uint32_t step, int layer,
-    int flags) {
-  static_assert(BM * CSW <= 2 * BM * TSF, "epilogue tile must fit the X buffers");
-  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * BM * TSF];
-  const int2 wi = work[blockIdx.x];   // XCD-balanced order built on the host (_xcd_schedule)
-  if (wi.x < 0) return;                // padding: a no-op workgroup
-  const MlpTL tl = tls[wi.x];
-  const int K = tl.K, N = tl.N, n0 = wi.y * TNW, row0 = blockIdx.y * BM;
-  if (row0 >= tl.rows) return;         // a smaller batch than the launch's: uniform exit
-  const int tid = threadIdx.x, lane = tid & 63, li = lane & 15, g = lane >> 4;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int nw0 = n0 + 32 * wave;      // this wave's first output column
-  const bool wlive = nw0 < N;          // wave-uniform
-  const bf16_t* X = xb + tl.x_off + (size_t)row0 * K;
-  // lane's fragment base: column nw0 + li, k 8 g (fragment j adds 16 rows, k-half s adds 32)
-  const bf16_t* Wl = p16 + tl.w_off + (size_t)(wlive ? nw0 : n0) * BK + li * BK + g * 8;
-
-  f32x4 acc[8][2];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int c0 = tid, c1 = tid + 256, c2 = tid + 512, c3 = tid + 768;
-  const int g0 = (c0 >> 3) * K + (c0 & 7) * 8, g1 = (c1 >> 3) * K + (c1 & 7) * 8;
-  const int g2 = (c2 >> 3) * K + (c2 & 7) * 8, g3 = (c3 >> 3) * K + (c3 & 7) * 8;
-  const int a0 = TOFFF(c0 >> 3, (c0 & 7) * 8), a1 = TOFFF(c1 >> 3, (c1 & 7) * 8);
-  const int a2 = TOFFF(c2 >> 3, (c2 & 7) * 8), a3 = TOFFF(c3 >> 3, (c3 & 7) * 8);
-  const int klast = K - BK;
-  uint4 px0, px1, px2, px3, pw0{}, pw1{}, pw2{}, pw3{};   // even K-steps
-  uint4 qx0, qx1, qx2, qx3, qw0{}, qw1{}, qw2{}, qw3{};   // odd K-steps
-#define MOPT_FWDW_LX(S, k)                                     \
-  do {                                                         \
-    const uint32_t kk_ = (uint32_t)(k);                        \
-    S##x0 = *(const uint4*)(X + (uint32_t)(g0 + kk_));         \
-    S##x1 = *(const uint4*)(X + (uint32_t)(g1 + kk_));         \
-    S##x2 = *(const uint4*)(X + (uint32_t)(g2 + kk_));         \
-    S##x3 = *(const uint4*)(X + (uint32_t)(g3 + kk_));         \
-  } while (0)
-// (unconditional: an idle wave re-reads the live columns -- a load behind a branch made hipcc
-//  count it as possibly absent and wait for every younger load at the next X store)
-#define MOPT_FWDW_LW(S, k)                                     \
-  do {                                                         \
-    const bf16_t* w_ = Wl + (uint32_t)(k) * (uint32_t)N;       \
-    S##w0 = *(const uint4*)(w_);                               \
-    S##w1 = *(const uint4*)(w_ + 32);                          \
-    S##w2 = *(const uint4*)(w_ + 16 * BK);                     \
-    S##w3 = *(const uint4*)(w_ + 16 * BK + 32);                \
-  } while (0)
-  // one K-step from set S through LDS buffer B, refilling S with the step KNEXT
-#define MOPT_FWDW_STEP(S, B, KNEXT)                                                        \
-  {                                                                                        \
-    bf16_t* As_ = smem + (B) * BM * TSF;                                                   \
-    *(uint4*)(As_ + a0) = S##x0;                                                           \
-    *(uint4*)(As_ + a1) = S##x1;                                                           \
-    *(uint4*)(As_ + a2) = S##x2;                                                           \
-    *(uint4*)(As_ + a3) = S##x3;                                                           \
-    __syncthreads();                                                                       \
-    MOPT_FWDW_LX(S, min(KNEXT, klast));                                                    \
-    if (wlive) {                                                                           \
-      _Pragma("unroll") for (int s_ = 0; s_ < 2; ++s_) {                                   \
-        const bf16x8 b0_ = __builtin_bit_cast(bf16x8, s_ ? S##w1 : S##w0);                 \
-        const bf16x8 b1_ = __builtin_bit_cast(bf16x8, s_ ? S##w3 : S##w2);                 \
-        bf16x8 a_[8];                                                                      \
-        _Pragma("unroll") for (int i_ = 0; i_ < 8; ++i_)                                   \
-          a_[i_] = lds_frag(As_ + TOFFF(16 * i_ + li, 32 * s_ + 8 * g));                   \
-        _Pragma("unroll") for (int i_ = 0; i_ < 8; ++i_) {                                 \
-          acc[i_][0] = mfma16(a_[i_], b0_, acc[i_][0]);                                    \
-          acc[i_][1] = mfma16(a_[i_], b1_, acc[i_][1]);                                    \
-        }                                                                                  \
-      }                                                                                    \
-    }                                                                                      \
-    MOPT_FWDW_LW(S, min(KNEXT, klast));                                                    \
-  }
-  MOPT_FWDW_LX(p, 0);
-  MOPT_FWDW_LW(p, 0);
-  MOPT_FWDW_LX(q, min(BK, klast));
-  MOPT_FWDW_LW(q, min(BK, klast));
-  // whole pairs of K-steps (even steps: set p, buffer 0; odd: q, 1), then the odd last one --
-  // the next store into a buffer follows the barrier of the step in between, by which every
-  // wave has finished the MFMAs that read it
-  int k0 = 0;
-  for (; k0 + 2 * BK <= K; k0 += 2 * BK) {
-    MOPT_FWDW_STEP(p, 0, k0 + 2 * BK)
-    MOPT_FWDW_STEP(q, 1, k0 + 3 * BK)
-  }
-  if (k0 < K) {
-    MOPT_FWDW_STEP(p, 0, k0 + 2 * BK)
-  }
-#undef MOPT_FWDW_STEP
-#undef MOPT_FWDW_LX
-#undef MOPT_FWDW_LW
-  __syncthreads();                     // every wave is done reading both X buffers
-
-  const TrialHP h = hp[tl.trial];
-  const bool drop = (flags & kDropout) && h.drop > 0.f;
-  const float inv_keep = drop ? 1.f / (1.f - h.drop) : 1.f;
-  const uint32_t key = rng_key(h.seed, (uint32_t)layer, h.t + step);   // as mlp_fwd_kernel
-  bf16_t* Cs = smem;                   // [128][CSW]
-  if (wlive) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int cl = 32 * wave + 16 * j + li, col = n0 + cl;
-      const float bj = join_hilo(p16[tl.b_off + col], plo[tl.b_off + col]);
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = 16 * i + 4 * g + r;
-          float v = acc[i][j][r] + bj;
-          if (flags & kRelu) v = fmaxf(v, 0.f);
-          if (drop) {
-            const uint32_t idx = (uint32_t)((row0 + row) * N + col);
-            v = rng_uniform(key, idx) >= h.drop ? v * inv_keep : 0.f;
-          }
-          Cs[row * CSW + cl] = f2bf(v);
-        }
-    }
-  }
-  __syncthreads();
-  const int cpr = min(TNW, N - n0) / 8;    // 16-byte chunks per output row (16, or 8)
-  bf16_t* Y = act + tl.y_off + (size_t)row0 * N + n0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int c = tid + 256 * i, r = c >> 4, ch = c & 15;
-    if (ch < cpr) *(uint4*)(Y + (size_t)r * N + ch * 8) = *(const uint4*)(Cs + r * CSW + ch * 8);
-  }
-}
+// (Round 5: a W-direct forward -- 128-column tiles, each wave loading its W B-fragments straight
+// from HBM into registers, only X staged through LDS: 1 + 4 instead of 3 + 6 LDS bytes per
+// weight byte -- trained bit for bit like this kernel but ran the headline 781.8 vs 789.6
+// trials/s on one stream and 824 vs 827 on four (800 workgroups against 768 slots: a near-empty
+// second wave); removed, profiles/round5.md.)
 
 // Output layer: logits = X W^T + b (N padded to 64 >= classes), fused softmax cross-entropy.
 // Writes dLogits = (softmax - onehot) * inv_b as bf16 (training) and accumulates the per-trial
@@ -1089,13 +947,6 @@ int mopt_mlp_fwd(const void* tls, const void* work, int n_work, int n_rowblocks,
                  const void* plo, const void* p16, void* act, const void* hp, unsigned step,
                  int layer, int flags, int tile_n, void* stream) {
   if (n_work <= 0) return 0;
-  if (tile_n == TNW) {
-    hipLaunchKernelGGL((mlp_fwd_wd_kernel<MOPT_FWDW_WAVES>), dim3(n_work, n_rowblocks), dim3(256), 0,
-                       (hipStream_t)stream, (const MlpTL*)tls, (const int2*)work, n_work,
-                       (const bf16_t*)xb, (const bf16_t*)plo, (const bf16_t*)p16, (bf16_t*)act,
-                       (const TrialHP*)hp, step, layer, flags);
-    return (int)hipGetLastError();
-  }
   if (tile_n != 64) return (int)hipErrorInvalidValue;
   // (three register sets at 3 waves / SIMD, with the same whole-group loop: step 654-656 vs
   //  651-654 us, bench 784-787 vs 790-791 trials/s -- profiles/round4.md)

@@ -259,19 +259,22 @@ class PopulationMLP:
         # optimizer state shares it; layer_views() returns row-major copies
         self.w_strip = backend == "hip" and self._lib.mopt_mlp_w_layout() == 1
         # output features per hidden-layer forward work item (csrc/pop_mlp.hip mlp_fwd_kernel TN)
-        self.fwd_tn = int(os.environ.get("MOPT_FWD_TN", FWD_TN))
-        if self.fwd_tn not in (64, 128):
-            raise ValueError("MOPT_FWD_TN must be 64 or 128")
+        self.fwd_tn = FWD_TN
         self.backend = backend
         # the population's trials are split into ``n_streams`` groups of equal cost whose train
         # steps run on their own HIP streams, unsynchronised between syncs: one group's
         # latency-bound forward overlaps another's bandwidth-bound backward (measured: two
         # processes sharing the GPU ran 14% more trials/s than one).  Any other operation first
         # joins the side streams into the main one (``_join``); the next train step forks them
-        # again after it.  Default 1: round 3 measured 741.7 / 748.5 trials/s for 1 / 2 streams
-        # (noise) with 2.9 vs 4.0 ms of host launch time per interval (profiles/README.md).
+        # again after it.  Default 3 (round 5, one box, headline bench, two repetitions each:
+        # 1 / 3 / 4 / 6 / 8 streams = 786-790 / 827-831 / 826-827 / 722-737 / 720-724 trials/s --
+        # in situ the forward kernels run at ~2.3 TB/s against ~4.8 for the backward, and the
+        # other groups' kernels fill those latency-bound phases and every kernel's tail; past
+        # the process's 4 hardware queues (GPU_MAX_HW_QUEUES) streams share queues and lose;
+        # profiles/round5.md).  Round 3, before the one-call interval launch, measured 1 vs 2
+        # streams as noise.
         if n_streams is None:
-            n_streams = int(os.environ.get("MOPT_STREAMS", "1")) if backend == "hip" else 1
+            n_streams = int(os.environ.get("MOPT_STREAMS", "3")) if backend == "hip" else 1
         self.n_streams = max(1, int(n_streams))
         self._side_streams: list = []
         self._events: list = []

@@ -353,29 +353,3 @@ def test_per_member_batch_trajectory_and_eval(data384):
     eh, _ = hip.evaluate(*data384.validation())
     er, _ = ref.evaluate(*data384.validation())
     assert np.abs(eh[act] - er[act]).max() < 3e-2
-
-
-def test_wide_forward_tile_trains_bitwise_like_64(data, monkeypatch):
-    """The W-direct 128-column forward (MOPT_FWD_TN=128, mlp_fwd_wd_kernel: odd 64-wide last
-    tiles at widths 64 / 192) runs every output element through the same MFMA chain as the
-    64-column kernel: a few steps train bit for bit alike, dropout included."""
-    pops = []
-    for tn in ("64", "128"):
-        monkeypatch.setenv("MOPT_FWD_TN", tn)
-        p = PopulationMLP(6, max_width=256, eval_batch=256, device="cuda", backend="hip",
-                          momentum_dtype="bf16")
-        assert p.fwd_tn == int(tn)
-        for i, c in enumerate(CONFIGS):
-            p.set_member(i + 1, c)
-        pops.append(p)
-    for step in range(4):
-        for p in pops:
-            p.train_step(*data.batch(step))
-    torch.cuda.synchronize()
-    a, b = pops
-    assert torch.equal(a.p16.view(torch.int16), b.p16.view(torch.int16))
-    assert torch.equal(a.plo, b.plo)
-    assert np.array_equal(a.train_loss(), b.train_loss(), equal_nan=True)   # NaN: empty slots
-    ea, eb = a.evaluate(*data.validation()), b.evaluate(*data.validation())
-    assert np.array_equal(ea[0], eb[0], equal_nan=True)
-    assert np.array_equal(ea[1], eb[1], equal_nan=True)
