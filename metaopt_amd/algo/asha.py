@@ -222,10 +222,12 @@ class ASHA(BaseAlgorithm):
     def observe(self, points, results):
         self.observe_objectives(points, [r["objective"] for r in results])
 
-    def observe_objectives(self, points, objectives):
-        """:meth:`observe` with bare objective values (the device sweep's fast path)."""
-        for point, objective in zip(points, objectives):
-            _id = self.get_id(point)
+    def observe_objectives(self, points, objectives, ids=None):
+        """:meth:`observe` with bare objective values (the device sweep's fast path); ``ids``:
+        the points' :meth:`get_id` values when the caller kept them (no second lookup)."""
+        get_id = self.get_id
+        for j, (point, objective) in enumerate(zip(points, objectives)):
+            _id = ids[j] if ids is not None else get_id(point)
             bracket = self.trial_info.get(_id)
             if bracket is None:
                 fid = point[self.fidelity_index]

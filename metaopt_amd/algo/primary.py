@@ -72,15 +72,19 @@ class PrimaryAlgo(BaseAlgorithm):
             tpoints.append(self.transformed_space.transform(p))
         self.algorithm.observe(tpoints, results)
 
-    def observe_objectives(self, points, objectives):
+    def observe_objectives(self, points, objectives, ids=None):
         """:meth:`observe` of suggested points (``check=False``) with bare objective values --
-        the device sweep's path: no result dict per point when the algorithm takes floats."""
+        the device sweep's path: no result dict per point when the algorithm takes floats.
+        ``ids``: the algorithm's own ids of the points (``get_id``), when the caller has them."""
         inner = getattr(self.algorithm, "observe_objectives", None)
         if inner is None or not self.transformed_space._is_identity():
             self.observe(points, [{"objective": o, "constraint": [], "gradient": None}
                                   for o in objectives], check=False)
             return
-        inner(points, objectives)
+        if ids is not None:
+            inner(points, objectives, ids=ids)
+        else:
+            inner(points, objectives)
 
     def parent_of(self, point):
         """Point whose trained state ``point`` resumes from (PBT exploit, ASHA promotion), if the

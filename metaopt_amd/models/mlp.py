@@ -94,6 +94,38 @@ class MLPSweepTask:
                 float(g("/dropout", 0.0)) if self.n_hidden > 0 else 0.0,
                 int(seed) & 0x7FFFFFFF)
 
+    def point_row_fn(self, names):
+        """``(row, budget, batch)`` functions of a suggested point in ``names`` order: the
+        :meth:`member_row`, :meth:`budget` and :meth:`batch_rows` of ``dict(zip(names, point))``
+        without building the dict (rank 0 places up to thousands of trials per sync); None
+        when a dimension outside this task's hyper-parameters is present."""
+        known = {"/lr", "/width", "/momentum", "/weight_decay", "/dropout", "/batch_size",
+                 self.fidelity}
+        if "/lr" not in names or any(n not in known for n in names):
+            return None
+        ix = {n: i for i, n in enumerate(names)}
+        i_lr = ix["/lr"]
+        i_w, i_m = ix.get("/width"), ix.get("/momentum")
+        i_wd, i_d = ix.get("/weight_decay"), ix.get("/dropout")
+        i_f, i_b = ix.get(self.fidelity), ix.get("/batch_size")
+        width, mom, wd, steps = self.width, self.momentum, self.weight_decay, self.steps
+        hidden = self.n_hidden > 0
+
+        def row(p, seed):
+            return (int(p[i_w]) if i_w is not None else int(width), float(p[i_lr]),
+                    float(p[i_m]) if i_m is not None else float(mom),
+                    float(p[i_wd]) if i_wd is not None else float(wd),
+                    float(p[i_d]) if (i_d is not None and hidden) else 0.0,
+                    int(seed) & 0x7FFFFFFF)
+
+        def budget(p):
+            return int(p[i_f]) if i_f is not None else int(steps)
+
+        def batch(p):
+            return int(p[i_b]) if i_b is not None else 0
+
+        return row, budget, batch
+
     def budget(self, params: Dict) -> int:
         return int(params.get(self.fidelity, self.steps))
 

@@ -192,6 +192,9 @@ class PopulationSweep:
             self._parent_of = getattr(self.algorithm, "parent_of", None)
             self._row_fn = getattr(task, "member_row", None)
             self._batch_fn = getattr(task, "batch_rows", None)
+            # the task's row / budget / batch straight from point tuples (no params dict)
+            prf = getattr(task, "point_row_fn", None)
+            self._point_fns = prf(self._dim_names) if prf is not None else None
             if watchdog is not None:
                 watchdog.on_stall.append(self._interrupt_in_flight)
         # resume bookkeeping (rank 0): stored trials waiting for a slot, device-state sidecars
@@ -491,8 +494,8 @@ class PopulationSweep:
         put_result = self._writer.put_update_spec
         hist_append = self.history.append
         mirror_save, index_ckpt = self._mirror_save, self._index_ckpt
-        done_obj = []
-        pts_append, obj_append = done_pts.append, done_obj.append
+        done_obj, done_ids = [], []
+        pts_append, obj_append, id_append = done_pts.append, done_obj.append, done_ids.append
         wall, rstep, trial_events = time.time(), self._result_step, self.trial_events
         best = self.best[0]
         completed = 0
@@ -534,17 +537,21 @@ class PopulationSweep:
             hist_append((wall, rkey, vl, budget, rstep))
             if vl < best:
                 best = vl
-                self.best = (vl, dict(params))
+                self.best = (vl, dict(params) if params is not None
+                             else dict(zip(self._dim_names, point)))
             pts_append(point)
             obj_append(vl)
+            id_append(pkey)
             if budget < max_b:
                 index_ckpt(pkey, row // P, rkey, budget, doc[0])
         self.completed += completed
         t0 = time.perf_counter()
         if done_pts:
             if isinstance(self.algorithm, PrimaryAlgo):
-                # the points came out of this algorithm's suggest(), validated there
-                self.algorithm.observe_objectives(done_pts, done_obj)
+                # the points came out of this algorithm's suggest(), validated there; with ASHA
+                # the sweep's configuration keys ARE the algorithm's ids (_algo_id)
+                self.algorithm.observe_objectives(
+                    done_pts, done_obj, ids=done_ids if self._algo_id is not None else None)
             else:
                 self.algorithm.observe(done_pts, [{"objective": o, "constraint": [],
                                                    "gradient": None} for o in done_obj])
@@ -659,6 +666,10 @@ class PopulationSweep:
         row_fn, batch_fn, member_config = self._row_fn, self._batch_fn, self.task.member_config
         doc_id = self._doc_id
         key = self.next_key
+        if self._point_fns is not None and algo_id is not None:
+            key = self._fill_points(points, left, key, rows, vals, free_by_rank, n_free, stamp)
+            self.next_key = key
+            return
         for point in points:
             if not left:
                 break
@@ -701,6 +712,54 @@ class PopulationSweep:
                          batch_fn(params) if batch_fn is not None else 0))
             key += 1
         self.next_key = key
+
+    def _fill_points(self, points, left, key, rows, vals, free_by_rank, n_free, stamp) -> int:
+        """:meth:`_fill_new`'s loop for tasks with ``point_row_fn`` and an algorithm id (ASHA):
+        rows, budgets and batch sizes come straight from the point tuples and the params dict
+        is built only if the trial turns out best (``_decide``) -- ~40 % of rank 0's per-trial
+        placement cost at 8 ranks (scripts/profile_decide.py).  Same decisions, same order."""
+        W = len(n_free)
+        row_of, budget_of, batch_of = self._point_fns
+        algo_id, seed_of = self._algo_id, self.task.seed_of
+        ckpt_index, side_index = self.ckpt_index, self._sidecar_index
+        put_register = self._writer.put_register_spec
+        trials, key_info, registered = self.trials, self.key_info, self._registered
+        doc_id = self._doc_id
+        for point in points:
+            if not left:
+                break
+            tid = doc_id(point)
+            if tid in registered:
+                log.debug("duplicate point %s skipped", point)
+                continue
+            registered.add(tid)
+            left -= 1
+            pkey = algo_id(point)
+            owner = ckpt_index.get(pkey)
+            src, resume = -1, -1
+            if owner is not None and n_free[owner[0]]:
+                rank = owner[0]                  # resume next to the checkpoint
+                action, resume, src = RESUME, owner[1], owner[0]
+            else:
+                rank = n_free.index(max(n_free)) if W > 1 else 0
+                if owner is not None:            # C4 from the owner rank
+                    action, resume, src = RESUME, owner[1], owner[0]
+                else:
+                    side = side_index.get(pkey)
+                    if side is not None:
+                        action, resume = RESUME_FILE, side[0]
+                    else:
+                        action = NEW
+            rows.append(free_by_rank[rank].popleft())
+            n_free[rank] -= 1
+            put_register((tid, stamp, point, None))
+            trials[key] = [tid, stamp]           # [trial id, last heartbeat]
+            budget = budget_of(point)
+            key_info[key] = (None, pkey, point, budget)   # params built on demand
+            vals.append((action, key, *row_of(point, seed_of(pkey)), budget, resume, src,
+                         batch_of(point)))
+            key += 1
+        return key
 
     def _place(self, point, tid, rows, vals, free_by_rank, n_free, stamp, was=None,
                sidecar=None):
