@@ -463,19 +463,11 @@ __global__ __launch_bounds__(256) void dconv_wgrad_kernel(const bf16_t* __restri
     }
     __syncthreads();
     // (offsets recomputed per step: hoisting all NKS of them and unrolling fully doubled the
-    //  VGPRs of the 16-channel kernel and cost more in occupancy than the ALU saved.)  With at
-    //  least 32 band pixels per image (OW divides 32), pixel 32 ks + c (c < 32) sits at halo
-    //  offset pix_base(32 ks) + pix_base(c): the first term is uniform (scalar ALU), the second
-    //  a per-lane constant -- the kernel was VALU-issue-bound on this index math
-    //  (profiles/r4/pmc_resnet20_r4am.md).
-    const bool split_pb = g.rpil >= 5;
-    const int rel_a = pix_base<CI, S>(g, 8 * gq + q), rel_b = pix_base<CI, S>(g, 8 * gq + q + 4);
+    //  VGPRs of the 16-channel kernel and cost more in occupancy than the ALU saved)
 #pragma unroll 2
     for (int ks = 0; ks < NKS; ++ks) {
       const int ka = 32 * ks + 8 * gq + q, kb = ka + 4;  // the lane's two pixel rows
-      const int sb = split_pb ? pix_base<CI, S>(g, 32 * ks) : 0;
-      const int pa = split_pb ? sb + rel_a : pix_base<CI, S>(g, ka);
-      const int pb = split_pb ? sb + rel_b : pix_base<CI, S>(g, kb);
+      const int pa = pix_base<CI, S>(g, ka), pb = pix_base<CI, S>(g, kb);
       bf16x8 b[NFT];
 #pragma unroll
       for (int j = 0; j < NFT; ++j)
