@@ -609,222 +609,13 @@ __global__ __launch_bounds__(512) void pgemm_big_kernel(const GemmArgs g) {
   }
 }
 
-// ----------------------------------------------------------------------------------------------
-// pgemm_ring4_kernel: the 256 x 256 big tile with FOUR 32-deep LDS stages (32 KB each, 128 KB)
-// and fills three K-steps ahead.  In the 2-stage kernel above a fill has one K-step of MFMAs
-// (~0.85 us at 2 waves per SIMD) to land, less than a loaded HBM round trip: MFMA busy ~0.41,
-// 44 % of wave time waiting (PMC r4af).  Here each wave waits only for its OWN fills of the step
-// about to be read -- a counted vmcnt that leaves the two younger steps' fills in flight; a
-// __syncthreads() would drain them (an LDS-DMA is a pending LDS write on the VM counter) --
-// then one raw s_barrier publishes every wave's fills and retires the reads of the stage the
-// next fill overwrites.  Per K-step u (32 deep):
-//     wait vmcnt(fills(u+1, u+2) + stores issued since fill(u))  ->  lgkmcnt(0); s_barrier
-//     -> fill step u+3 into stage (u+3) % 4  ->  MFMAs from stage u % 4  [-> epilogue]
-// The K-step stream runs on across the workgroup's persistent tiles.  Every global access of
-// the loop is inline asm (fills, C stores) so the counts are exact: hipcc neither counts nor
-// waits for them.  (A 3-stage 64-deep ring at 256 x 128 / 128 x 256 ran 670-860 TFLOP/s against
-// 900-1190 for the 2-stage kernel, profiles/round5.md.)
-// ----------------------------------------------------------------------------------------------
-__device__ __forceinline__ void glds16r(const bf16_t* src, bf16_t* lds_dst) {
-  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)((lds_void*)lds_dst));
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
-               :
-               : "v"(src), "s"(m0)
-               : "memory", "m0");
-}
-typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void gst16(void* dst, uint4 v) {
-  const u32x4v d{v.x, v.y, v.z, v.w};
-  asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" : : "v"(dst), "v"(d) : "memory");
-}
-__device__ __forceinline__ void gst8(void* dst, uint2 v) {
-  const u32x2v d{v.x, v.y};
-  asm volatile("global_store_dwordx2 %0, %1, off\n\ts_nop 1" : : "v"(dst), "v"(d) : "memory");
-}
-// s_waitcnt vmcnt(n) for n = c F + e S (c <= 2 younger fill steps, e <= 1 epilogue in the
-// window -- K >= 128 keeps tile ends 4+ steps apart); any other n waits for everything
-template <int F, int S0, int S1>
-__device__ __forceinline__ void ring_wait(int n) {
-#define MOPT_RW(N)                                                       \
-  if (n == (N)) {                                                        \
-    asm volatile("s_waitcnt vmcnt(%0)" : : "i"(N) : "memory");           \
-    return;                                                              \
-  }
-  MOPT_RW(2 * F) MOPT_RW(F) MOPT_RW(0)
-  MOPT_RW(2 * F + S0) MOPT_RW(F + S0) MOPT_RW(S0)
-  MOPT_RW(2 * F + S1) MOPT_RW(F + S1) MOPT_RW(S1)
-#undef MOPT_RW
-  asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
-}
-
-template <int ROWS, bool KCONTIG, int KD>
-__device__ __forceinline__ void ring_fill(const bf16_t* __restrict__ base, int ld, int row0, int k0,
-                                          bf16_t* img, int wave, int lane) {
-  using I = GImg<ROWS, KCONTIG, KD>;
-#pragma unroll
-  for (int j = 0; j < I::NI; ++j) {
-    const int blk = wave * I::NI + j;
-    const bf16_t* src;
-    if (KCONTIG) {
-      const int r = blk * (64 / I::KCH) + lane / I::KCH, c = lane % I::KCH;
-      src = base + (int64_t)(row0 + r) * ld + k0 + 8 * (c ^ I::kswz(r));
-    } else {
-      const int lin = blk * 64 + lane, kr = lin / I::CPR, c = lin % I::CPR;
-      src = base + (int64_t)(k0 + kr) * ld + row0 + 8 * (c ^ I::rswz(kr));
-    }
-    glds16r(src, img + blk * 512);
-  }
-}
-
-template <bool TA, bool TB, int WM, int FM, int FN, int EPI = 0>
-__global__ __launch_bounds__(512) void pgemm_ring4_kernel(const GemmArgs g) {
-  constexpr int WN = 8 / WM;
-  constexpr int BM = WM * 16 * FM, BN = WN * 16 * FN;
-  constexpr int KD = 32;                                     // K-step depth
-  static_assert(FN % 2 == 0, "the epilogue pairs n-fragments");
-  static_assert(EPI == 0 || EPI == 1, "the ring kernel has the plain and SwiGLU epilogues");
-  using IA = GImg<BM, !TA, KD>;
-  using IB = GImg<BN, TB, KD>;
-  constexpr int STAGE = IA::ELEMS + IB::ELEMS;
-  constexpr int NST = 4;
-  static_assert(NST * STAGE * 2 <= 160 * 1024, "the stages must fit the LDS");
-  constexpr int F = IA::NI + IB::NI;                        // fills per wave per K-step
-  constexpr int S0 = EPI == 1 ? FM * FN : FM * FN / 2;       // stores of a bf16 epilogue
-  constexpr int S1 = FM * FN;                                // stores of a split-K partial
-  __shared__ __attribute__((aligned(1024))) bf16_t smem[NST * STAGE];  // the only __shared__
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int li = lane & 15, gq = lane >> 4, q = li >> 2, pp = li & 3;
-  const int wm = wave / WN, wn = wave % WN;
-  const int nk = g.k_per_split / KD;
-  const int G = gridDim.x;
-  const int vb0 = blockIdx.x;
-  if (vb0 >= g.nwg) return;
-  const int total = ((g.nwg - vb0 + G - 1) / G) * nk;       // K-steps of this workgroup
-  const int S = g.part != nullptr ? S1 : S0;
-
-  auto decode = [&](int v, int& p, int& m0, int& n0, int& k0) {
-    const int t = xcd_remap(v, g.nwg);
-    const int per = g.tiles_m * g.tiles_n;
-    const int pq = t / per;
-    p = pq / g.splits;
-    k0 = (pq - p * g.splits) * g.k_per_split;
-    const int idx = t - pq * per, span = kGroupM * g.tiles_n;
-    const int grp = idx / span, in = idx - grp * span;
-    const int gm = min(kGroupM, g.tiles_m - grp * kGroupM);
-    m0 = (grp * kGroupM + in % gm) * BM;
-    n0 = (in / gm) * BN;
-  };
-  // fill side: the tile of the K-step being filled (decoded once per tile), its step in it
-  int f_tile = 0, f_kt = 0, fp = 0, fm0 = 0, fn0 = 0, fk0 = 0;
-  decode(vb0, fp, fm0, fn0, fk0);
-  auto fill_next = [&](int u) {   // fill K-step u (the stream advances one step per call)
-    bf16_t* st = smem + (u % NST) * STAGE;
-    const int kk = fk0 + f_kt * KD;
-    ring_fill<BM, !TA, KD>(g.a.ptr + fp * g.a.batch, g.a.ld, fm0, kk, st, wave, lane);
-    ring_fill<BN, TB, KD>(g.b.ptr + fp * g.b.batch, g.b.ld, fn0, kk, st + IA::ELEMS, wave, lane);
-    if (++f_kt == nk) {
-      f_kt = 0;
-      ++f_tile;
-      if ((f_tile * nk) < total) decode(vb0 + f_tile * G, fp, fm0, fn0, fk0);
-    }
-  };
-
-  for (int u = 0; u < 3 && u < total; ++u) fill_next(u);
-  int p, m0, n0, k0;
-  decode(vb0, p, m0, n0, k0);
-  int tile = 0, kt = 0;
-  int end1 = 0, end2 = 0, end3 = 0;    // an epilogue ended step u-1 / u-2 / u-3
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  for (int u = 0; u < total; ++u) {
-    // this wave's fills of step u landed: younger VMEM ops are the fills of steps u+1, u+2 and
-    // the stores of an epilogue at step u-1 .. u-3 (issued after fill(u))
-    const int younger = min(2, total - 1 - u) * F + (end1 + end2 + end3) * S;
-    ring_wait<F, S0, S1>(younger);
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" : : : "memory");
-    if (u + 3 < total) fill_next(u + 3);
-    const bf16_t* cur = smem + (u % NST) * STAGE;
-    {
-      bf16x8 a[FM], b[FN];
-#pragma unroll
-      for (int i = 0; i < FM; ++i) a[i] = IA::frag(cur, wm * 16 * FM + 16 * i, 0, li, gq, q, pp);
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-        b[j] = IB::frag(cur + IA::ELEMS, wn * 16 * FN + 16 * j, 0, li, gq, q, pp);
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(b[j], a[i], acc[i][j]);
-    }
-    end3 = end2;
-    end2 = end1;
-    end1 = 0;
-    if (++kt != nk) continue;
-    kt = 0;
-    end1 = 1;
-    // ---- epilogue of the tile (acc = C^T fragments as in pgemm_big_kernel) ----
-    if (g.part != nullptr) {
-      const int64_t tot = (int64_t)g.P * g.M * g.N;
-      float* part = g.part + (k0 / g.k_per_split) * tot + (int64_t)p * g.M * g.N +
-                    (int64_t)(m0 + wm * 16 * FM + li) * g.N + n0 + wn * 16 * FN + 4 * gq;
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          gst16(part + (int64_t)(16 * i) * g.N + 16 * j, __builtin_bit_cast(uint4, acc[i][j]));
-    } else {
-      if constexpr (EPI == 1) {
-        bf16_t* Hp = g.H + p * g.sX + (int64_t)(m0 + wm * 16 * FM + li) * g.ldx +
-                     (n0 + wn * 16 * FN) / 2 + 4 * gq;
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; j += 2) {
-            float hv[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              hv[r] = silu_f(bf2f(f2bf(acc[i][j][r]))) * bf2f(f2bf(acc[i][j + 1][r]));
-            gst8(Hp + (int64_t)(16 * i) * g.ldx + 8 * j,
-                 make_uint2(pack2bf(hv[0], hv[1]), pack2bf(hv[2], hv[3])));
-          }
-      }
-      bf16_t* C = g.C + p * g.sC + (int64_t)(m0 + wm * 16 * FM + li) * g.ldc + n0 +
-                  wn * 16 * FN + 16 * (gq & 1) + 8 * (gq >> 1);
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; j += 2) {
-          const uint32_t x0 = pack2bf(acc[i][j][0], acc[i][j][1]);
-          const uint32_t x1 = pack2bf(acc[i][j][2], acc[i][j][3]);
-          const uint32_t y0 = pack2bf(acc[i][j + 1][0], acc[i][j + 1][1]);
-          const uint32_t y1 = pack2bf(acc[i][j + 1][2], acc[i][j + 1][3]);
-          const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
-          const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
-          gst16(C + (int64_t)(16 * i) * g.ldc + 16 * j, make_uint4(s0[0], s1[0], s0[1], s1[1]));
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    ++tile;
-    if (u + 1 < total) decode(vb0 + tile * G, p, m0, n0, k0);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" : : : "memory");   // the last tile's stores
-}
-
-// (Round 5: a 3-stage LDS-ring variant of this kernel -- 256 x 128 / 128 x 256 tiles, 144 KB of
-// LDS, fills two K-steps ahead behind counted vmcnt waits and one raw s_barrier per K-step, the
-// C stores in inline asm so the counts were exact -- passed every GEMM test but ran 670-860
-// TFLOP/s against 900-1190 for this kernel's best tile on every LM shape; removed,
-// profiles/round5.md "3-stage ring GEMM".)
+// (Round 5, two deeper-pipelined variants of this kernel, both correct on every GEMM test and
+// both removed (profiles/round5.md): a 3-stage 64-deep LDS ring at 256 x 128 / 128 x 256 (fills
+// two K-steps ahead behind counted vmcnt waits, one raw s_barrier per K-step, C stores in inline
+// asm so the counts were exact) ran 670-860 TFLOP/s, and a 4-stage 32-deep ring at 256 x 256
+// (fills three steps ahead) 610-1009, against 900-1200 for this kernel's best tile on every LM
+// shape.  The fill latency is not what holds this loop back: with 32 MFMAs per wave between
+// barriers the exposed LDS-read latency after each barrier grew instead.)
 // (Round 4: a register-pipelined variant -- the operands of K-step t + 3 loaded into one of two
 // register sets while step t is multiplied, written to the free LDS stage two steps later --
 // was correct but 2.5-4x slower: the two register sets on top of the accumulators exceed the
@@ -884,26 +675,6 @@ int launch_big(GemmArgs g, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-// the 4-stage ring kernel: persistent over the tiles, one workgroup per CU (128 KB of LDS)
-template <bool TA, bool TB, int WM, int FM, int FN, int EPI = 0>
-int launch_ring4(GemmArgs g, hipStream_t st) {
-  constexpr int BM = WM * 16 * FM, BN = (8 / WM) * 16 * FN;
-  if (g.M % BM || g.N % BN || g.k_per_split % 32 || g.k_per_split < 128 ||
-      (int64_t)g.k_per_split * g.splits != g.K || (g.splits > 1 && g.part == nullptr) ||
-      g.nin > 1 || (EPI != 0 && g.splits != 1) || (EPI == 1 && g.H == nullptr))
-    return (int)hipErrorInvalidValue;
-  g.tiles_m = g.M / BM;
-  g.tiles_n = g.N / BN;
-  const int64_t nwg = (int64_t)g.P * g.splits * g.tiles_m * g.tiles_n;
-  if (nwg <= 0 || nwg > 0x7FFFFFFF) return (int)hipErrorInvalidValue;
-  g.nwg = (int)nwg;
-  constexpr int kGrid = 256;
-  const int grid = nwg < kGrid ? (int)nwg : kGrid;
-  hipLaunchKernelGGL((pgemm_ring4_kernel<TA, TB, WM, FM, FN, EPI>), dim3(grid), dim3(512), 0, st,
-                     g);
-  return (int)hipGetLastError();
-}
-
 template <int KA, int KB, bool TA, bool TB>
 int dispatch_tile(const GemmArgs& g, int cfg, hipStream_t st) {
   if constexpr (KA == kDense && KB == kDense) {
@@ -912,7 +683,6 @@ int dispatch_tile(const GemmArgs& g, int cfg, hipStream_t st) {
       case 6: return launch_big<TA, TB, 4, 4, 4>(g, st);  // 256 x 128
       case 7: return launch_big<TA, TB, 2, 4, 4>(g, st);  // 128 x 256
       case 11: return launch_big<TA, TB, 4, 4, 6>(g, st);     // 256 x 192
-      case 12: return launch_ring4<TA, TB, 2, 8, 4>(g, st);   // 256 x 256, 4-stage ring
       default: break;
     }
   }
@@ -968,11 +738,10 @@ extern "C" {
 
 // Tile of configuration ``cfg`` (rows, cols): lets the host size grids and split-K.
 int mopt_pgemm_tile(int cfg, int* bm, int* bn) {
-  static const int t[13][2] = {{128, 128}, {128, 16},  {128, 32},  {64, 64},
+  static const int t[12][2] = {{128, 128}, {128, 16},  {128, 32},  {64, 64},
                                {64, 128},  {256, 256}, {256, 128}, {128, 256},
-                               {256, 256}, {256, 256}, {256, 128}, {256, 192},
-                               {256, 256}};
-  if (cfg < 0 || cfg > 12) return (int)hipErrorInvalidValue;
+                               {256, 256}, {256, 256}, {256, 128}, {256, 192}};
+  if (cfg < 0 || cfg > 11) return (int)hipErrorInvalidValue;
   *bm = t[cfg][0];
   *bn = t[cfg][1];
   return 0;
@@ -1033,7 +802,6 @@ int mopt_pgemm_swiglu(const void* A, const void* B, void* C, void* X, int P, int
     case 6: return launch_big<false, false, 4, 4, 4, 1>(g, st);
     case 7: return launch_big<false, false, 2, 4, 4, 1>(g, st);
     case 11: return launch_big<false, false, 4, 4, 6, 1>(g, st);
-    case 12: return launch_ring4<false, false, 2, 8, 4, 1>(g, st);
     default: return (int)hipErrorNotSupported;
   }
 }
@@ -1061,7 +829,6 @@ int mopt_pgemm_qkv_rope(const void* A, const void* B, void* out, const void* cos
   g.sinT = (const float*)sinT;
   g.T = T;
   g.nH = nH;
-  if (cfg == 12) cfg = 5;    // the ring tile's QKV + RoPE epilogue runs on the 2-stage kernel
   switch (cfg) {
     case 5: return launch_big<false, false, 2, 8, 4, 3>(g, st);
     case 6: return launch_big<false, false, 4, 4, 4, 3>(g, st);

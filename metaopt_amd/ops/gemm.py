@@ -43,20 +43,16 @@ _lib.register_signatures({
 # (any shape, ragged edges); 5-7: 8-wave direct-to-LDS kernel, one workgroup per CU, for shapes
 # the tile divides (M % BM == N % BN == K % 64 == 0)
 TILES = {0: (128, 128), 1: (128, 16), 2: (128, 32), 3: (64, 64), 4: (64, 128),
-         5: (256, 256), 6: (256, 128), 7: (128, 256), 11: (256, 192), 12: (256, 256)}
+         5: (256, 256), 6: (256, 128), 7: (128, 256), 11: (256, 192)}
 #: 256 x 192 (cfg 11): N = 768 outputs in 4 column panels, so the LM's N = 768 products fill
 #: whole waves of 256 CUs (512 tiles for M = 4096, 256 for M = 2048) where 256 x 256 leaves a
 #: 75 %-full last wave
 BIG_TILES = (5, 6, 7, 11)
-#: 12: the 256 x 256 tile on the 4-stage ring kernel (pgemm_ring4_kernel: 32-deep K-steps,
-#: fills three steps ahead behind counted vmcnt waits and one raw barrier per step); the QKV +
-#: RoPE epilogue runs it on the 2-stage kernel (cfg 5).  MOPT_GEMM_RING4=1 lets the planner pick it.
-RING_TILES = (12,)
-LARGE_TILES = BIG_TILES + RING_TILES
+LARGE_TILES = BIG_TILES
 NUM_CU = 256
 #: relative speed of the big tiles at equal occupancy of the chip; the 256 x 128 / 128 x 256 tiles
 #: lose more on long reductions (less reuse per loaded byte): profiles/gemm_r2.md
-BIG_SPEED = {5: 1.0, 6: 0.85, 7: 0.85, 11: 0.95, 12: 1.2}
+BIG_SPEED = {5: 1.0, 6: 0.85, 7: 0.85, 11: 0.95}
 LONG_K = 8192
 
 
@@ -105,9 +101,7 @@ def _plan_big(P: int, M: int, N: int, K: int):
     wave, e.g. the LM head's dX: 384 tiles of K = 32000 on 256 CUs); None when no big tile
     divides the shape or fills the chip well."""
     best = None
-    import os
-    cands = BIG_TILES + (RING_TILES if os.environ.get("MOPT_GEMM_RING4", "0") == "1" else ())
-    for cfg in cands:
+    for cfg in BIG_TILES:
         if not big_fits(M, N, K, cfg):
             continue
         bm, bn = TILES[cfg]
@@ -142,7 +136,7 @@ def plan(P: int, M: int, N: int, K: int, cfg: Optional[int] = None,
             return big
     if cfg in LARGE_TILES:
         sp = splits or 1
-        if big_fits(M, N, K, cfg) and K % (64 * sp) == 0 and (sp == 1 or cfg in LARGE_TILES):
+        if big_fits(M, N, K, cfg) and K % (64 * sp) == 0 and (sp == 1 or cfg in BIG_TILES):
             return cfg, sp, K // sp
         cfg = None                    # the tile does not divide this shape / this K-split
     cfg = pick_tile(M, N) if cfg is None else cfg
