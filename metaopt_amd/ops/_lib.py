@@ -20,7 +20,7 @@ from . import build as _build
 
 _LOCK = threading.Lock()
 _LIB = None
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 c_void_p = ctypes.c_void_p
 c_int = ctypes.c_int

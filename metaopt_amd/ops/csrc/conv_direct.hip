@@ -46,6 +46,7 @@ struct Geom {
   int nb;          // persistent workgroups per trial
   float inv_wi, inv_tri;  // 1 / WI, 1 / TRI: exact quotients of small integers via (t + .5) / d
   int lds_elems;          // bf16 elements of the workgroup's LDS allocation
+  int cs_off;             // forward: element offset of the output tile (0: it aliases the halo)
 };
 
 __device__ __forceinline__ int fdiv(int t, float inv) { return (int)(((float)t + 0.5f) * inv); }
@@ -64,44 +65,122 @@ constexpr int pstride() {
   return CI / 8 % 4 == 2 ? CI : CI + 16;
 }
 
-// halo band: input rows row0 .. row0 + TRI, columns -1 .. WI - 2 of images b0 .. b0 + IMGS.
+// halo band: input rows row0 .. row0 + TRI, columns -1 .. WI - 2 of images b0 .. b0 + IMGS,
+// in 16-byte chunks c = (halo pixel) * CI / 8 + channel chunk.
 // BNIN: x is a BatchNorm's raw input and the convolution's operand is relu(x sc + sh) -- applied
-// here as the band is staged (bn_apply_kernel's arithmetic, rounded to bf16), so the BatchNorm
-// output is never written to HBM; tab = LDS [2][CI] f32 (scale, shift); the zero padding stays 0.
-template <int CI, int S, int BNIN = 0>
-__device__ __forceinline__ void load_halo(bf16_t* hs, const bf16_t* __restrict__ x,
-                                          const Geom& g, int b0, int row0,
-                                          const float* tab = nullptr) {
+// as the band is staged (bn_apply_kernel's arithmetic, rounded to bf16), so the BatchNorm output
+// is never written to HBM; tab = LDS [2][CI] f32 (scale, shift); the zero padding stays 0.
+//
+// Staging is software-pipelined (round 5): the band a workgroup multiplies next is fetched into
+// registers (Halo::fetch, NPF 16-byte chunks per thread, every load unconditional -- padding
+// chunks read the trial's first pixel and are zeroed at the store -- so the compiler's counted
+// waits stay exact) while the current band's MFMAs run, and written to LDS (Halo::put) once the
+// band is done.  Without it a workgroup's band loads were exposed at the top of every band and
+// the 2-4 resident workgroups per CU kept too few bytes in flight (~3.3 TB/s).
+
+// an opaque copy of v: keeps the per-chunk geometry derived from it inside the band loop (hoisted
+// out of it, the chunks' band-invariant index arithmetic held ~60 VGPRs across the MFMAs)
+__device__ __forceinline__ int opaque(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+// global element offset (from the trial's base) of halo chunk c, -1 for zero padding
+template <int CI>
+__device__ __forceinline__ int halo_src(const Geom& g, int b0, int row0, int c) {
   constexpr int CC = CI / 8;
-  const int n = g.IMGS * g.TRI * g.WI * CC;
-  for (int c = threadIdx.x; c < n; c += 256) {
-    const int cc = c % CC;
-    const int t = c / CC;
-    const int t2 = fdiv(t, g.inv_wi);
-    const int hc = t - t2 * g.WI;
-    const int img = fdiv(t2, g.inv_tri);
-    const int hr = t2 - img * g.TRI;
-    const int iy = row0 + hr, ix = hc - 1, b = b0 + img;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (b < g.Bn && iy >= 0 && iy < g.H && ix >= 0 && ix < g.H) {
-      v = *(const uint4*)(x + (((int64_t)b * g.H + iy) * g.H + ix) * CI + 8 * cc);
-      if constexpr (BNIN != 0) {  // the chunk's 8 (scale, shift) pairs: 4 ds_read_b128
-        const f32x4 sa = *(const f32x4*)(tab + 8 * cc), sb = *(const f32x4*)(tab + 8 * cc + 4);
-        const f32x4 ha = *(const f32x4*)(tab + CI + 8 * cc);
-        const f32x4 hb = *(const f32x4*)(tab + CI + 8 * cc + 4);
-        const float sc[8] = {sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3]};
-        const float sh[8] = {ha[0], ha[1], ha[2], ha[3], hb[0], hb[1], hb[2], hb[3]};
-        uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  const int cc = c % CC;
+  const int t = c / CC;
+  const int t2 = fdiv(t, g.inv_wi);
+  const int hc = t - t2 * g.WI;
+  const int img = fdiv(t2, g.inv_tri);
+  const int hr = t2 - img * g.TRI;
+  const int iy = row0 + hr, ix = hc - 1, b = b0 + img;
+  return (b < g.Bn && iy >= 0 && iy < g.H && ix >= 0 && ix < g.H)
+             ? ((b * g.H + iy) * g.H + ix) * CI + 8 * cc
+             : -1;
+}
+
+// relu(x sc + sh) of one chunk (8 channels starting at 8 cc), tab = [2][CI] (scale, shift)
+template <int CI>
+__device__ __forceinline__ uint4 bnin_chunk(uint4 v, const float* tab, int cc) {
+  const f32x4 sa = *(const f32x4*)(tab + 8 * cc), sb = *(const f32x4*)(tab + 8 * cc + 4);
+  const f32x4 ha = *(const f32x4*)(tab + CI + 8 * cc);
+  const f32x4 hb = *(const f32x4*)(tab + CI + 8 * cc + 4);
+  const float sc[8] = {sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3]};
+  const float sh[8] = {ha[0], ha[1], ha[2], ha[3], hb[0], hb[1], hb[2], hb[3]};
+  uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float lo = fmaxf(bf2f(w[e] & 0xFFFF) * sc[2 * e] + sh[2 * e] + 0.f, 0.f);
-          const float hi = fmaxf(bf2f(w[e] >> 16) * sc[2 * e + 1] + sh[2 * e + 1] + 0.f, 0.f);
-          w[e] = pack2bf(lo, hi);
-        }
-        v = make_uint4(w[0], w[1], w[2], w[3]);
-      }
+  for (int e = 0; e < 4; ++e) {
+    const float lo = fmaxf(bf2f(w[e] & 0xFFFF) * sc[2 * e] + sh[2 * e] + 0.f, 0.f);
+    const float hi = fmaxf(bf2f(w[e] >> 16) * sc[2 * e + 1] + sh[2 * e + 1] + 0.f, 0.f);
+    w[e] = pack2bf(lo, hi);
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__device__ __forceinline__ int halo_chunks(const Geom& g, int cc) {
+  return g.IMGS * g.TRI * g.WI * cc;
+}
+
+// NPF: halo chunks per thread held in registers -- enough for a band of the image side this
+// shape has in a CIFAR ResNet (16 channels at 32 x 32, 32 at 16 x 16, 64 at 8 x 8; make_geom's
+// arithmetic); other sides stage the chunks past NPF synchronously.  Capped at 10 (40 VGPRs).
+template <int CI, int CO, int S, int NPX, int MODE>
+constexpr int halo_pf() {
+  // kDgrad2: H is the (full-resolution) output side, the output has CO channels
+  const int c = MODE == 2 ? CO : CI;
+  const int H = c <= 16 ? 32 : 512 / c;
+  const int OH = MODE == 2 ? H : H / S;
+  const int px = OH * OH;
+  const int imgs = px >= NPX ? 1 : NPX / px;
+  const int tr = px >= NPX ? NPX / OH : OH;
+  const int tri = MODE == 2 ? tr / 2 + 2 : (tr - 1) * S + 3;
+  const int wi = MODE == 2 ? OH / 2 + 2 : (OH - 1) * S + 3;
+  const int n = (imgs * tri * wi * (CI / 8) + 255) / 256;
+  const int cap = CI >= 64 || CO >= 64 ? 3 : 10;
+  return n < 1 ? 1 : (n > cap ? cap : n);
+}
+
+// the register half of the pipelined halo staging (plain arrays in the kernel, passed by
+// reference into these force-inlined helpers)
+template <int CI, int NPF>
+__device__ __forceinline__ void halo_fetch(uint4 (&v)[NPF], uint32_t& ok, const bf16_t* x,
+                                           const Geom& g, int b0, int row0) {
+  const int n = halo_chunks(g, CI / 8);
+  ok = 0;
+#pragma unroll
+  for (int i = 0; i < NPF; ++i) {
+    const int c = opaque(threadIdx.x + 256 * i);
+    const int o = halo_src<CI>(g, b0, row0, min(c, n - 1));
+    ok |= (c < n && o >= 0) ? (1u << i) : 0u;
+    v[i] = *(const uint4*)(x + (uint32_t)(o < 0 ? 0 : o));
+  }
+}
+
+template <int CI, int S, int NPF, int BNIN>
+__device__ __forceinline__ void halo_put(bf16_t* hs, const uint4 (&v)[NPF], uint32_t ok,
+                                         const bf16_t* x, const Geom& g, int b0, int row0,
+                                         const float* tab) {
+  constexpr int CC = CI / 8;
+  const int n = halo_chunks(g, CC);
+#pragma unroll
+  for (int i = 0; i < NPF; ++i) {
+    const int c = opaque(threadIdx.x + 256 * i);
+    if (c < n) {
+      uint4 w = make_uint4(0, 0, 0, 0);
+      if ((ok >> i) & 1u) w = BNIN ? bnin_chunk<CI>(v[i], tab, c % CC) : v[i];
+      *(uint4*)(hs + (c / CC) * pstride<CI, S>() + 8 * (c % CC)) = w;
     }
-    *(uint4*)(hs + t * pstride<CI, S>() + 8 * cc) = v;
+  }
+  for (int c = threadIdx.x + 256 * NPF; c < n; c += 256) {   // past the registers: synchronous
+    const int o = halo_src<CI>(g, b0, row0, c);
+    uint4 w = make_uint4(0, 0, 0, 0);
+    if (o >= 0) {
+      w = *(const uint4*)(x + o);
+      if (BNIN) w = bnin_chunk<CI>(w, tab, c % CC);
+    }
+    *(uint4*)(hs + (c / CC) * pstride<CI, S>() + 8 * (c % CC)) = w;
   }
 }
 
@@ -163,10 +242,15 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
   constexpr int WN = CO / 16, WM = 4 / WN;
   constexpr int MFW = NPX / 16 / WM;      // 16-pixel fragments per wave
   constexpr int LSC = CO + 8;
+  // (64-channel data gradients with an addend: one prefetched chunk -- the addend registers on
+  //  top of a full prefetch cost the kernel its second workgroup per CU, 51 -> 72 us in situ)
+  constexpr int NPF = (CO >= 64 && ADD != 0) ? 1 : halo_pf<CI, CO, S, NPX, MODE>();
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
-  const int halo = g.IMGS * g.TRI * g.WI * pstride<CI, S>();
   bf16_t* hs = smem;
-  bf16_t* cs = smem;  // the output tile is restaged over the halo band once the MFMAs are done
+  // the output tile: its own LDS region when the launch found room (cs_off > 0: the band's
+  // copy-out overlaps the next band), else restaged over the halo band once the MFMAs are done
+  bf16_t* cs = smem + g.cs_off;
+  const bool alias = g.cs_off == 0;
 
   const int p = blockIdx.x / g.nb, blk = blockIdx.x % g.nb;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -175,6 +259,17 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
   const int n = 16 * wn + li;
   const int64_t wbatch = (int64_t)9 * CI * CO;
   const bf16_t* wp = w + p * wbatch;
+  const int64_t x_batch = (int64_t)g.Bn * g.H * g.H * CI;
+  const bf16_t* xp = x + p * x_batch;
+  auto band_row0 = [&](int t) {
+    const int oy = (t % g.tpi) * g.TR;
+    return mode == kDgrad2 ? oy / 2 - 1 : oy * S - 1;
+  };
+
+  // the first band's halo is in flight during the weight prologue
+  uint4 hv[NPF];
+  uint32_t hok;
+  halo_fetch<CI, NPF>(hv, hok, xp, g, (blk / g.tpi) * g.IMGS, band_row0(blk));
 
   // this wave's B fragments for every k step
   bf16x8 wr[KS];
@@ -217,9 +312,7 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
     }
   }
 
-  const int64_t x_batch = (int64_t)g.Bn * g.H * g.H * CI;
   const int64_t y_batch = (int64_t)g.Bn * g.OH * (1 << g.owl) * CO;
-  const bf16_t* xp = x + p * x_batch;
   bf16_t* yp = y + p * y_batch;
   const int ppi = 1 << g.rpil;  // band pixels per image
 
@@ -242,7 +335,9 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
   constexpr int CPR = CO / 8;
   constexpr int XCH = (NPX * CPR + 255) / 256;
   float bsc[8], bsh[8], ba[8], bb[8];
-  uint4 xpre[BNB != 0 ? XCH : 1];
+  // BNB: the band's BatchNorm input; ADD: the band's addend -- loaded before the next band's
+  // halo fetch and used by the band's copy-out (one band later)
+  uint4 xr[(BNB != 0 || ADD != 0) ? XCH : 1];
   if constexpr (BNB != 0) {
     const int c0 = 8 * (threadIdx.x % CPR);
 #pragma unroll
@@ -257,20 +352,90 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
     bnin_table<CI>(bntab, bn, p);
     __syncthreads();
   }
-  for (int t = blk; t < g.tiles; t += g.nb) {
+  // Band loop, one band behind on the copy-out: put(t) -> barrier -> copy-out(t - 1) -> loads
+  // of t's addend / BatchNorm input and of band t + nb's halo -> MFMAs(t) -> barrier -> C(t) to
+  // LDS.  Aliased output tile: the copy-out of t - 1 finishes before put(t) overwrites it.
+  int pt = -1;                 // the band whose output tile is in LDS
+  for (int t = blk;; t += g.nb) {
+    const bool have = t < g.tiles;
     const int b0 = (t / g.tpi) * g.IMGS, oy0 = (t % g.tpi) * g.TR;
-    load_halo<CI, S, BNIN>(hs, xp, g, b0, mode == kDgrad2 ? oy0 / 2 - 1 : oy0 * S - 1, bntab);
-    if constexpr (BNB != 0) {   // the band's BatchNorm input, in flight during the MFMAs
-      const int nval = min(NPX, (g.Bn - b0) * ppi) * CPR;
-      const bf16_t* xb = bn.x + p * y_batch + ((int64_t)b0 * g.OH + oy0) * (1 << g.owl) * CO;
+    if (have && !alias) halo_put<CI, S, NPF, BNIN>(hs, hv, hok, xp, g, b0, band_row0(t), bntab);
+    __syncthreads();
+    if (pt >= 0) {
+      // ---- copy-out of band pt: contiguous (b0, oy0 .. oy0 + TR) or whole images b0 .. ----
+      const int pb0 = (pt / g.tpi) * g.IMGS, poy0 = (pt % g.tpi) * g.TR;
+      const int valid = min(NPX, (g.Bn - pb0) * ppi);
+      bf16_t* yt = yp + ((int64_t)pb0 * g.OH + poy0) * (1 << g.owl) * CO;
 #pragma unroll
       for (int k = 0; k < XCH; ++k) {
         const int c = threadIdx.x + 256 * k;
-        xpre[k] = c < nval ? *(const uint4*)(xb + (int64_t)(c / CPR) * CO + 8 * (c % CPR))
-                           : make_uint4(0, 0, 0, 0);
+        if (c >= valid * CPR) break;
+        const int row = c / CPR, cc = c % CPR;
+        uint4 v = *(const uint4*)(cs + row * LSC + 8 * cc);
+        bool add = ADD == 1;
+        if constexpr (ADD == 2) {   // option-A shortcut: its gradient lands on even pixels
+          const int rem = row & ((1 << g.rpil) - 1);
+          const int oy = poy0 + (rem >> g.owl), ox = rem & ((1 << g.owl) - 1);
+          add = ((oy | ox) & 1) == 0;
+        }
+        if (ADD != 0 && add) {  // data gradient + the shortcut branch's gradient
+          const uint4 a = xr[k];
+          const uint32_t vw[4] = {v.x, v.y, v.z, v.w}, aw[4] = {a.x, a.y, a.z, a.w};
+          uint32_t o[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            o[e] = pack2bf(bf2f(vw[e] & 0xFFFF) + bf2f(aw[e] & 0xFFFF),
+                           bf2f(vw[e] >> 16) + bf2f(aw[e] >> 16));
+          v = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+        *(uint4*)(yt + (int64_t)row * CO + 8 * cc) = v;
+        if constexpr (BNB != 0) {
+          const uint4 xq = xr[k];
+          const uint32_t vw[4] = {v.x, v.y, v.z, v.w}, xw[4] = {xq.x, xq.y, xq.z, xq.w};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float d = bf2f(e & 1 ? vw[e >> 1] >> 16 : vw[e >> 1] & 0xFFFF);
+            const float xv = bf2f(e & 1 ? xw[e >> 1] >> 16 : xw[e >> 1] & 0xFFFF);
+            // bn_reduce_kernel<true>'s relu mode 2 arithmetic
+            const float dz = xv * bsc[e] + bsh[e] + 0.f <= 0.f ? 0.f : d;
+            ba[e] += dz;
+            bb[e] += dz * xv;
+          }
+        }
       }
     }
-    __syncthreads();
+    if (alias) {
+      __syncthreads();   // the copy-out is done with the tile the halo overwrites
+      if (have) halo_put<CI, S, NPF, BNIN>(hs, hv, hok, xp, g, b0, band_row0(t), bntab);
+      __syncthreads();
+    }
+    if (!have) break;
+    const int valid = min(NPX, (g.Bn - b0) * ppi);
+    if constexpr (BNB != 0 || ADD != 0) {   // (row clamped: every load unconditional)
+      const bf16_t* yt = yp + ((int64_t)b0 * g.OH + oy0) * (1 << g.owl) * CO;
+#pragma unroll
+      for (int k = 0; k < XCH; ++k) {
+        const int c = min(threadIdx.x + 256 * k, valid * CPR - 1);
+        const int row = c / CPR, cc = c % CPR;
+        const bf16_t* src;
+        if constexpr (BNB != 0) {
+          src = bn.x + (yt - y) + (int64_t)row * CO + 8 * cc;
+        } else if constexpr (ADD == 1) {  // identity shortcut: same layout as the output
+          src = addend + (yt - y) + (int64_t)row * CO + 8 * cc;
+        } else {   // option-A shortcut [P Bn][OH / 2][OH / 2][addend_c], even pixels only
+          const int b = b0 + (row >> g.rpil), rem = row & ((1 << g.rpil) - 1);
+          const int oy = oy0 + (rem >> g.owl), ox = rem & ((1 << g.owl) - 1);
+          const int hs2 = g.OH >> 1;
+          src = addend + ((((int64_t)p * g.Bn + b) * hs2 + (oy >> 1)) * hs2 + (ox >> 1)) *
+                             addend_c + 8 * cc;
+        }
+        xr[k] = *(const uint4*)src;
+      }
+    }
+    {   // the next band's halo (the current one again past the last: loads stay unconditional)
+      const int tn = t + g.nb < g.tiles ? t + g.nb : t;
+      halo_fetch<CI, NPF>(hv, hok, xp, g, (tn / g.tpi) * g.IMGS, band_row0(tn));
+    }
 
     f32x4 acc[MFW];
 #pragma unroll
@@ -302,8 +467,7 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
       }
     }
 
-    const int valid = min(NPX, (g.Bn - b0) * ppi);
-    __syncthreads();  // every wave is done with the halo band
+    __syncthreads();  // every wave is done with the halo band (and with the previous copy-out)
 #pragma unroll
     for (int i = 0; i < MFW; ++i)
 #pragma unroll
@@ -317,54 +481,7 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
           s2 += f * f;
         }
       }
-    __syncthreads();
-    // the band's output is contiguous: (b0, oy0 .. oy0 + TR) or whole images b0 ..
-    bf16_t* yt = yp + ((int64_t)b0 * g.OH + oy0) * (1 << g.owl) * CO;
-    const bf16_t* at = ADD == 1 ? addend + (yt - y) : nullptr;
-#pragma unroll
-    for (int k = 0; k < XCH; ++k) {
-      const int c = threadIdx.x + 256 * k;
-      if (c >= valid * CPR) break;
-      const int row = c / CPR, cc = c % CPR;
-      uint4 v = *(const uint4*)(cs + row * LSC + 8 * cc);
-      const bf16_t* ap = nullptr;
-      if constexpr (ADD == 1) {  // identity shortcut: same layout as the output
-        ap = at + (int64_t)row * CO + 8 * cc;
-      } else if constexpr (ADD == 2) {  // option-A shortcut: its gradient lands on even pixels
-        const int b = b0 + (row >> g.rpil), rem = row & ((1 << g.rpil) - 1);
-        const int oy = oy0 + (rem >> g.owl), ox = rem & ((1 << g.owl) - 1);
-        if (((oy | ox) & 1) == 0) {
-          const int hs2 = g.OH >> 1;
-          ap = addend + ((((int64_t)p * g.Bn + b) * hs2 + (oy >> 1)) * hs2 + (ox >> 1)) *
-                            addend_c + 8 * cc;
-        }
-      }
-      if (ADD != 0 && ap != nullptr) {  // data gradient + the shortcut branch's gradient
-        const uint4 a = *(const uint4*)ap;
-        const uint32_t vw[4] = {v.x, v.y, v.z, v.w}, aw[4] = {a.x, a.y, a.z, a.w};
-        uint32_t o[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          o[e] = pack2bf(bf2f(vw[e] & 0xFFFF) + bf2f(aw[e] & 0xFFFF),
-                         bf2f(vw[e] >> 16) + bf2f(aw[e] >> 16));
-        v = make_uint4(o[0], o[1], o[2], o[3]);
-      }
-      *(uint4*)(yt + (int64_t)row * CO + 8 * cc) = v;
-      if constexpr (BNB != 0) {
-        const uint4 xr = xpre[k];
-        const uint32_t vw[4] = {v.x, v.y, v.z, v.w}, xw[4] = {xr.x, xr.y, xr.z, xr.w};
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float d = bf2f(e & 1 ? vw[e >> 1] >> 16 : vw[e >> 1] & 0xFFFF);
-          const float xv = bf2f(e & 1 ? xw[e >> 1] >> 16 : xw[e >> 1] & 0xFFFF);
-          // bn_reduce_kernel<true>'s relu mode 2 arithmetic
-          const float dz = xv * bsc[e] + bsh[e] + 0.f <= 0.f ? 0.f : d;
-          ba[e] += dz;
-          bb[e] += dz * xv;
-        }
-      }
-    }
-    __syncthreads();  // the next band's halo overwrites the output tile
+    pt = t;
   }
   if constexpr (BNB != 0) {
     // threads of one chunk: lanes equal mod CPR (xor over the lane bits above log2 CPR), then
@@ -417,7 +534,7 @@ __global__ __launch_bounds__(256) void dconv_wgrad_kernel(const bf16_t* __restri
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   const int halo = g.IMGS * g.TRI * g.WI * pstride<CI, S>();
   bf16_t* hs = smem;
-  bf16_t* ds = smem + halo;
+  bf16_t* ds = smem + halo;   // (halo: a multiple of 8 elements)
   bf16_t* zs = ds + NPX * LSD;  // 8 zero bytes: source of the padded rows m >= 9 CI
   float* bntab = (float*)(zs + 8);  // BNIN: [2][CI] (scale, shift)
 
@@ -449,19 +566,44 @@ __global__ __launch_bounds__(256) void dconv_wgrad_kernel(const bf16_t* __restri
   const int ow = 1 << g.owl, ppi = 1 << g.rpil;
   const bf16_t* xp = x + p * ((int64_t)g.Bn * g.H * g.H * CI);
   const bf16_t* dyp = dy + p * ((int64_t)g.Bn * g.OH * ow * CO);
-  for (int t = blk; t < g.tiles; t += g.nb) {
+  // pipelined staging (see Halo): band t + nb's halo and dy tile are loaded into registers while
+  // band t is multiplied (the dy rows past a partial band's end re-read its last row, zeroed at
+  // the store, so every load is unconditional)
+  constexpr int NPF = halo_pf<CI, CO, S, NPX, kFwd>();
+  // 64 output channels: the 144 accumulator registers leave no room for a band in flight (one
+  // workgroup per CU with it, 43 -> 62 us in situ): fetched at the top of the band instead
+  constexpr bool PFW = CO < 64;
+  constexpr int CPR = CO / 8;
+  constexpr int DYC = (NPX * CPR + 255) / 256;
+  uint4 hv[NPF], dv[DYC];
+  uint32_t hok;
+  auto fetch = [&](int t) {
     const int b0 = (t / g.tpi) * g.IMGS, oy0 = (t % g.tpi) * g.TR;
-    load_halo<CI, S, BNIN>(hs, xp, g, b0, oy0 * S - 1, bntab);
+    halo_fetch<CI, NPF>(hv, hok, xp, g, b0, oy0 * S - 1);
     const int valid = min(NPX, (g.Bn - b0) * ppi);
     const bf16_t* dyt = dyp + ((int64_t)b0 * g.OH + oy0) * ow * CO;
-    constexpr int CPR = CO / 8;
-    for (int c = threadIdx.x; c < NPX * CPR; c += 256) {
-      const int row = c / CPR, cc = c % CPR;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (row < valid) v = *(const uint4*)(dyt + (int64_t)row * CO + 8 * cc);
-      *(uint4*)(ds + row * LSD + 8 * cc) = v;
+#pragma unroll
+    for (int k = 0; k < DYC; ++k) {
+      const int c = min(threadIdx.x + 256 * k, valid * CPR - 1);
+      dv[k] = *(const uint4*)(dyt + (int64_t)(c / CPR) * CO + 8 * (c % CPR));
+    }
+  };
+  if (PFW) fetch(blk);
+  for (int t = blk; t < g.tiles; t += g.nb) {
+    const int b0 = (t / g.tpi) * g.IMGS, oy0 = (t % g.tpi) * g.TR;
+    if (!PFW) fetch(t);
+    halo_put<CI, S, NPF, BNIN>(hs, hv, hok, xp, g, b0, oy0 * S - 1, bntab);
+    const int valid = min(NPX, (g.Bn - b0) * ppi);
+#pragma unroll
+    for (int k = 0; k < DYC; ++k) {
+      const int c = threadIdx.x + 256 * k;
+      if (c < NPX * CPR) {
+        const int row = c / CPR, cc = c % CPR;
+        *(uint4*)(ds + row * LSD + 8 * cc) = row < valid ? dv[k] : make_uint4(0, 0, 0, 0);
+      }
     }
     __syncthreads();
+    if (PFW) fetch(t + g.nb < g.tiles ? t + g.nb : t);
     // (offsets recomputed per step: hoisting all NKS of them and unrolling fully doubled the
     //  VGPRs of the 16-channel kernel and cost more in occupancy than the ALU saved)
 #pragma unroll 2
@@ -537,6 +679,8 @@ constexpr int npx_wgrad(int co) { return co >= 32 ? 128 : 256; }
 bool make_geom(Geom& g, int Bn, int H, int S, int npx, int target_blocks, int P, int mode) {
   const int hl = ilog2i(H);
   if (hl < 0 || Bn < 1 || (S != 1 && S != 2) || (S == 2 && H < 2)) return false;
+  // halo offsets are 32-bit element offsets from a trial's base (64 channels at most)
+  if ((int64_t)Bn * H * H * 64 >= ((int64_t)1 << 31)) return false;
   g.Bn = Bn;
   g.H = mode == kDgrad2 ? H / 2 : H;
   g.OH = mode == kDgrad2 ? H : H / S;
@@ -571,10 +715,16 @@ int launch_fwd(const void* x, const void* w, void* y, void* sums, int P, int Bn,
   // (64-wide outputs: half the workgroups, twice the bands each -- their weight prologue is long)
   if (!make_geom(g, Bn, H, MODE == kDgrad2 ? 2 : S, NPX, CO >= 64 ? 512 : 1024, P, MODE))
     return (int)hipErrorInvalidValue;
-  const size_t lds = std::max(halo_bytes<CI, S>(g), (size_t)NPX * (CO + 8) * 2);
-  const size_t lds_all = lds + (BNIN ? (size_t)2 * CI * sizeof(float) : 0);
+  const size_t hb = halo_bytes<CI, S>(g), ob = (size_t)NPX * (CO + 8) * 2;
+  const size_t tab = BNIN ? (size_t)2 * CI * sizeof(float) : 0;
+  // the output tile gets its own region (copy-out overlapped with the next band) when the two
+  // fit the 64 KB per workgroup; else it aliases the halo band
+  const bool sep = hb + ob + tab <= 64 * 1024;
+  const size_t lds = sep ? hb + ob : std::max(hb, ob);
+  const size_t lds_all = lds + tab;
   if (lds_all > 64 * 1024) return (int)hipErrorNotSupported;
   g.lds_elems = (int)(lds / 2);
+  g.cs_off = sep ? (int)(hb / 2) : 0;
   hipLaunchKernelGGL((dconv_fwd_kernel<CI, CO, NPX, MODE, S, ADD, BNIN, BNB>), dim3(P * g.nb),
                      dim3(256), lds_all, st,
                      (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)sums,

@@ -439,6 +439,46 @@ __global__ __launch_bounds__(256) void mlp_fwd_ce_kernel(const MlpTL* __restrict
   }
 }
 
+// The per-parameter optimizer update of four consecutive parameters, shared by every kernel that
+// updates weights (mlp_bwd_opt_kernel, mlp_bwd0_fwd_kernel).  Explicit fmaf: the two kernels
+// must round identically, and hipcc's fp-contraction of the written-out expressions differed
+// between them (1-ulp momentum differences with weight decay, round 5).
+template <int OPT>
+__device__ __forceinline__ void opt_update4(f32x4& wv, f32x4& mv, f32x4& vv, const f32x4& gv,
+                                            const TrialHP& h, float c1, float c2) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float gr = gv[r];
+    if (OPT == kSGD || OPT == kSGD16) {
+      const float gg = fmaf(h.wd, wv[r], gr);
+      float mn = fmaf(h.b1, mv[r], gg);
+      if (OPT == kSGD16) mn = bf2f(f2bf(mn));   // the stored (rounded) momentum drives W
+      mv[r] = mn;
+      wv[r] = fmaf(-h.lr, mn, wv[r]);
+    } else {
+      wv[r] = wv[r] * (1.f - h.lr * h.wd);
+      mv[r] = fmaf(h.b1, mv[r], (1.f - h.b1) * gr);
+      vv[r] = fmaf(h.b2, vv[r], ((1.f - h.b2) * gr) * gr);
+      wv[r] = wv[r] - (c1 * mv[r]) / fmaf(sqrtf(vv[r]), c2, h.eps);
+    }
+  }
+}
+
+// the bias update (no weight decay), shared the same way
+template <int OPT>
+__device__ __forceinline__ void bias_update(float& bw, float& mb, float& vb, float gb,
+                                            const TrialHP& h, float c1, float c2) {
+  if (OPT == kSGD || OPT == kSGD16) {
+    mb = fmaf(h.b1, mb, gb);
+    if (OPT == kSGD16) mb = bf2f(f2bf(mb));
+    bw = fmaf(-h.lr, mb, bw);
+  } else {
+    mb = fmaf(h.b1, mb, (1.f - h.b1) * gb);
+    vb = fmaf(h.b2, vb, ((1.f - h.b2) * gb) * gb);
+    bw = bw - (c1 * mb) / fmaf(sqrtf(vb), c2, h.eps);
+  }
+}
+
 // ----------------------------------------------------------------------------------------------
 // Fused backward + optimizer for one (trial-layer, 64-wide k-strip of W).  The workgroup holds the
 // X strip X[:, k0:k0+64] in LDS for the whole pass and walks W[:, k0:k0+64] in 64-row chunks:
@@ -741,22 +781,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
       const size_t o = (size_t)nc * WRS + wo + (size_t)(32 * (i >> 1)) * WRS + 4 * (i & 1);
       f32x4 wv = w[i], mv = m[i], vv;
       if (OPT == kAdamW) vv = v[i];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float gr = gv[r];
-        if (OPT == kSGD || OPT == kSGD16) {
-          const float gg = gr + h.wd * wv[r];
-          float mn = h.b1 * mv[r] + gg;
-          if (OPT == kSGD16) mn = bf2f(f2bf(mn));   // the stored (rounded) momentum drives W
-          mv[r] = mn;
-          wv[r] = wv[r] - h.lr * mn;
-        } else {
-          wv[r] = wv[r] * (1.f - h.lr * h.wd);
-          mv[r] = h.b1 * mv[r] + (1.f - h.b1) * gr;
-          vv[r] = h.b2 * vv[r] + (1.f - h.b2) * gr * gr;
-          wv[r] = wv[r] - c1 * mv[r] / (sqrtf(vv[r]) * c2 + h.eps);
-        }
-      }
+      opt_update4<OPT>(wv, mv, vv, gv, h, c1, c2);
       uint2 nh, nl;
       split4(wv, nh, nl);
       // the two groups of a row (k 0-3, 4-7) leave as one 16-byte store per array
@@ -787,18 +812,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
         float* bm = m32 + tl.b_off + nc + tid;
         bf16_t* bm16 = (bf16_t*)m32 + tl.b_off + nc + tid;
         float bw = join_hilo(*bph, *bpl), mb = OPT == kSGD16 ? bf2f(*bm16) : *bm;
-        if (OPT == kSGD || OPT == kSGD16) {
-          mb = h.b1 * mb + gb;
-          if (OPT == kSGD16) mb = bf2f(f2bf(mb));
-          bw = bw - h.lr * mb;
-        } else {
-          float* bv = v32 + tl.b_off + nc + tid;
-          float vb = *bv;
-          mb = h.b1 * mb + (1.f - h.b1) * gb;
-          vb = h.b2 * vb + (1.f - h.b2) * gb * gb;
-          bw = bw - c1 * mb / (sqrtf(vb) * c2 + h.eps);
-          *bv = vb;
-        }
+        float* bv = v32 + tl.b_off + nc + tid;
+        float vb = OPT == kAdamW ? *bv : 0.f;
+        bias_update<OPT>(bw, mb, vb, gb, h, c1, c2);
+        if (OPT == kAdamW) *bv = vb;
         const uint32_t ub = __float_as_uint(bw), hb = split_hi(ub) & 0xFFFFu;
         *bph = (bf16_t)hb;
         *bpl = (bf16_t)split_lo(ub, hb);
@@ -835,6 +852,319 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
   for (int i = 0; i < 4; ++i) {
     const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
     *(uint4*)(GX + (size_t)r * K + ch * 8) = *(const uint4*)(Zs + TOFF(r, ch * 8));
+  }
+}
+
+// ----------------------------------------------------------------------------------------------
+// First layer, fused across two steps: the backward + optimizer of step t AND the forward of
+// step t + 1 (round 5).  The first layer has no dX, and its input (the shared minibatch) of the
+// next step is known while step t runs, so one pass over W0 can update it and immediately
+// multiply the NEW weights with the next batch -- the separate forward of layer 0 (a second read
+// of the largest weight matrix, ~10 % of the step) disappears.  A workgroup owns one 64-row
+// output chunk n0 of W0 for ALL of K (the other kernels own a k-strip for all of N), so it holds
+// the complete dot products of the next step's outputs Y'[:, n0:n0+64]:
+//   dZ[:, chunk] staged once; the chunk's bias gradient / update;
+//   for each 64-wide k-strip s:  dW^T = X[:, s]^T dZ[:, chunk]          (as mlp_bwd_opt_kernel)
+//                                W, M <- update(W, M, dW)   in the MFMA C layout (4 consecutive
+//                                          k of one row per lane: no LDS restaging)
+//                                acc += X'[:, s] W_new[chunk, s]^T     (as mlp_fwd_kernel: same
+//                                          fragments, same K order -> bit-identical outputs)
+//   Y' = dropout(relu(acc + b_new)) with the t + 1 dropout key.
+// Every result equals the unfused step pair bit for bit (tests/test_kernels_gpu.py).  Batches of
+// one 128-row block only (MODE 0); the caller keeps the unfused launches otherwise.
+// ----------------------------------------------------------------------------------------------
+// PF: the next strip's state in a second register set (SGD, SGD16; AdamW's f32 moments do not
+// fit twice); two waves per SIMD
+template <int OPT, bool PF, int DIAG = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void mlp_bwd0_fwd_kernel(
+    const MlpTL* __restrict__ tls, const int2* __restrict__ work, int n_work,
+    const bf16_t* __restrict__ xb, const bf16_t* __restrict__ xn, const bf16_t* __restrict__ grad,
+    bf16_t* __restrict__ act, bf16_t* __restrict__ plo, bf16_t* __restrict__ p16,
+    float* __restrict__ m32, float* __restrict__ v32, const TrialHP* __restrict__ hp, int flags) {
+  constexpr int DS = BN + 4;   // f32 row stride of the dW staging tile (FOFF)
+  __shared__ __attribute__((aligned(16)))
+      bf16_t smem[2 * BM * TS + BN * TSF + 2 * BN * DS + 2 * 4 * BN + 2 * BN];
+  bf16_t* Zs = smem;                  // dZ[:, chunk]      [128][TS]  (the whole pass)
+  bf16_t* Xs = smem + BM * TS;        // X[:, strip]       [128][TS]  (then the output tile)
+  bf16_t* Ws = smem + 2 * BM * TS;    // W_new[chunk, strip] hi [64][TSF]
+  float* Dw = (float*)(smem + 2 * BM * TS + BN * TSF);     // dW[chunk, strip] f32 [64][DS]
+  float* red = Dw + BN * DS;                               // [4][64] bias partial sums
+  float* bnew = red + 4 * BN;                              // [64] updated bias (f32)
+
+  const int2 wi = work[blockIdx.x];
+  if (wi.x < 0) return;
+  const MlpTL tl = tls[wi.x];
+  const int K = tl.K, N = tl.N, n0 = wi.y * BN;
+  const bf16_t* X = xb + tl.x_off;
+  const bf16_t* Xn = xn + tl.x_off;
+  const bf16_t* dZ = grad + tl.y_off;
+  bf16_t* WLO = plo + tl.w_off;
+  float* M32 = m32 + tl.w_off;
+  bf16_t* M16 = (bf16_t*)m32 + tl.w_off;
+  float* V32 = v32 + tl.w_off;
+  bf16_t* W16 = p16 + tl.w_off;
+  const TrialHP h = hp[tl.trial];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, g = lane >> 4, q = li >> 2, pp = li & 3;
+  const int wk = wave >> 1, wn = wave & 1;
+  float c1 = 1.f, c2 = 1.f;
+  if (OPT == kAdamW) {
+    const float t = (float)h.t;
+    c1 = h.lr / (1.f - __powf(h.b1, t));
+    c2 = 1.f / sqrtf(1.f - __powf(h.b2, t));
+  }
+
+  // dZ[:, n0:n0+64] -> LDS once; X[:, strip 0] into registers
+  const int xo0 = (tid >> 3) * K + (tid & 7) * 8;       // + 32 K i: rows tid / 8 + 32 i
+  uint4 xr0, xr1, xr2, xr3;
+  xr0 = *(const uint4*)(X + xo0);
+  xr1 = *(const uint4*)(X + xo0 + 32 * K);
+  xr2 = *(const uint4*)(X + xo0 + 64 * K);
+  xr3 = *(const uint4*)(X + xo0 + 96 * K);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
+    *(uint4*)(Zs + TOFF(r, ch * 8)) = *(const uint4*)(dZ + (size_t)r * N + n0 + ch * 8);
+  }
+  __syncthreads();
+
+  // ---- bias of the chunk: db[n] = sum_b dZ[b][n] (mlp_bwd_opt_kernel's order) and its update ----
+  const bool do_bias = flags & kUpdateBias;
+  if (do_bias) {
+    const int bcol = tid & 63, bpart = tid >> 6;
+    float bsum = 0.f;
+    for (int r = bpart * 32; r < bpart * 32 + 32; ++r) bsum += bf2f(Zs[TOFF(r, bcol)]);
+    red[bpart * 64 + bcol] = bsum;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    bf16_t* bph = p16 + tl.b_off + n0 + tid;
+    bf16_t* bpl = plo + tl.b_off + n0 + tid;
+    float bw = join_hilo(*bph, *bpl);
+    if (do_bias) {
+      const float gb = red[tid] + red[64 + tid] + red[128 + tid] + red[192 + tid];
+      float* bm = m32 + tl.b_off + n0 + tid;
+      bf16_t* bm16 = (bf16_t*)m32 + tl.b_off + n0 + tid;
+      float mb = OPT == kSGD16 ? bf2f(*bm16) : *bm;
+      float* bv = v32 + tl.b_off + n0 + tid;
+      float vb = OPT == kAdamW ? *bv : 0.f;
+      bias_update<OPT>(bw, mb, vb, gb, h, c1, c2);
+      if (OPT == kAdamW) *bv = vb;
+      const uint32_t ub = __float_as_uint(bw), hb = split_hi(ub) & 0xFFFFu;
+      *bph = (bf16_t)hb;
+      *bpl = (bf16_t)split_lo(ub, hb);
+      if (OPT == kSGD16) *bm16 = f2bf(mb);
+      else *bm = mb;
+    }
+    bnew[tid] = bw;   // join_hilo of the stored pair is bw exactly
+  }
+
+  // the next batch's A fragments (rows 32 wave + 16 i + li, k 32 ks + 8 g) straight from global
+  // memory (the shared minibatch: L2-resident), 4 per strip
+  const int ao = (32 * wave + li) * K + 8 * g;              // + 16 K i + 32 ks
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / BK;
+  // Weight / optimizer state in mlp_bwd_opt_kernel's thread layout: rows tid / 8 + 32 i (i < 2),
+  // 8 consecutive k at 8 (tid % 8) -- 16 bytes per lane, a wave-instruction moves 8 whole
+  // 128-byte rows.  (The MFMA C layout -- 4 k of one row per lane, 16 rows x 32 bytes per
+  // instruction, no LDS restaging -- ran the pass ~45 % slower.)  The current strip's set (c*)
+  // and, PF, the next strip's (n*), loaded while this strip is multiplied and updated.
+  const int so = (tid >> 3) * BK + 8 * (tid & 7);           // + 32 BK: the second row
+  uint4 cwh0, cwh1, cwl0, cwl1, cmh0, cmh1, nwh0, nwh1, nwl0, nwl1, nmh0, nmh1;
+  f32x4 cm[4], cv[4], nm[4], nv[4];
+#define MOPT_B0F_LOAD(P, S)                                                                      \
+  {                                                                                              \
+    const size_t o_ = (size_t)(S) * BK * N + (size_t)n0 * BK + so;                               \
+    P##wh0 = *(const uint4*)(W16 + o_);                                                          \
+    P##wh1 = *(const uint4*)(W16 + o_ + 32 * BK);                                                \
+    P##wl0 = *(const uint4*)(WLO + o_);                                                          \
+    P##wl1 = *(const uint4*)(WLO + o_ + 32 * BK);                                                \
+    if (OPT == kSGD16) {                                                                         \
+      P##mh0 = *(const uint4*)(M16 + o_);                                                        \
+      P##mh1 = *(const uint4*)(M16 + o_ + 32 * BK);                                              \
+    } else {                                                                                     \
+      _Pragma("unroll") for (int i = 0; i < 4; ++i)                                              \
+        P##m[i] = *(const f32x4*)(M32 + o_ + 32 * BK * (i >> 1) + 4 * (i & 1));                 \
+    }                                                                                            \
+    if (OPT == kAdamW) {                                                                         \
+      _Pragma("unroll") for (int i = 0; i < 4; ++i)                                              \
+        P##v[i] = *(const f32x4*)(V32 + o_ + 32 * BK * (i >> 1) + 4 * (i & 1));                 \
+    }                                                                                            \
+  }
+  MOPT_B0F_LOAD(c, 0)
+  for (int s = 0; s < nk; ++s) {
+    const int k0 = s * BK;
+    const size_t sb = (size_t)k0 * N + (size_t)n0 * BK + so;   // strip s, this thread's rows
+    const int sn = s + 1 < nk ? s + 1 : s;   // the next strip (the last re-reads its own: every
+                                             // load unconditional, the counted waits exact)
+    // X[:, strip s] -> LDS; the next strip's X and state into registers
+    *(uint4*)(Xs + TOFF(tid >> 3, (tid & 7) * 8)) = xr0;
+    *(uint4*)(Xs + TOFF(32 + (tid >> 3), (tid & 7) * 8)) = xr1;
+    *(uint4*)(Xs + TOFF(64 + (tid >> 3), (tid & 7) * 8)) = xr2;
+    *(uint4*)(Xs + TOFF(96 + (tid >> 3), (tid & 7) * 8)) = xr3;
+    {
+      const int kn = sn * BK;
+      xr0 = *(const uint4*)(X + xo0 + kn);
+      xr1 = *(const uint4*)(X + xo0 + 32 * K + kn);
+      xr2 = *(const uint4*)(X + xo0 + 64 * K + kn);
+      xr3 = *(const uint4*)(X + xo0 + 96 * K + kn);
+    }
+    if (PF) MOPT_B0F_LOAD(n, sn)
+    uint4 an[2][2];
+    if (DIAG != 1) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          an[i][ks] = *(const uint4*)(Xn + ao + 16 * K * i + k0 + 32 * ks);
+    }
+    __syncthreads();   // Xs visible; the previous strip's readers of Dw / Ws are done
+
+    // ---- dW^T[strip, chunk] = X^T dZ (mlp_bwd_opt_kernel's fragments and order) -> Dw ----
+    {
+      f32x4 dw[2][2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) dw[t][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        bf16x8 xa[2], bz[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int c0 = 32 * wk + 16 * t + 4 * pp;
+          xa[t] = cat_frag(lds_tr4(Xs + TOFF(32 * s4 + 8 * g + q, c0)),
+                           lds_tr4(Xs + TOFF(32 * s4 + 8 * g + 4 + q, c0)));
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int c0 = 32 * wn + 16 * u + 4 * pp;
+          bz[u] = cat_frag(lds_tr4(Zs + TOFF(32 * s4 + 8 * g + q, c0)),
+                           lds_tr4(Zs + TOFF(32 * s4 + 8 * g + 4 + q, c0)));
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int u = 0; u < 2; ++u) dw[t][u] = mfma16(xa[t], bz[u], dw[t][u]);
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          *(f32x4*)(Dw + FOFF(32 * wn + 16 * u + li, 32 * wk + 16 * t + 4 * g)) = dw[t][u];
+    }
+    __syncthreads();   // Dw visible
+
+    // ---- optimizer (mlp_bwd_opt_kernel's epilogue): group i = row 32 (i / 2) + tid / 8,
+    //      k 8 (tid % 8) + 4 (i % 2) .. + 3 ----
+    {
+      const f32x4 w[4] = {join4(make_uint2(cwh0.x, cwh0.y), make_uint2(cwl0.x, cwl0.y)),
+                          join4(make_uint2(cwh0.z, cwh0.w), make_uint2(cwl0.z, cwl0.w)),
+                          join4(make_uint2(cwh1.x, cwh1.y), make_uint2(cwl1.x, cwl1.y)),
+                          join4(make_uint2(cwh1.z, cwh1.w), make_uint2(cwl1.z, cwl1.w))};
+      f32x4 m[4];
+      if (OPT == kSGD16) {
+        m[0] = bf4_to_f32(make_uint2(cmh0.x, cmh0.y)); m[1] = bf4_to_f32(make_uint2(cmh0.z, cmh0.w));
+        m[2] = bf4_to_f32(make_uint2(cmh1.x, cmh1.y)); m[3] = bf4_to_f32(make_uint2(cmh1.z, cmh1.w));
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) m[i] = cm[i];
+      }
+      uint2 ph{}, pl{}, pm{};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int gr = 32 * (i >> 1) + (tid >> 3), gk = 8 * (tid & 7) + 4 * (i & 1);
+        const f32x4 gv = *(const f32x4*)(Dw + FOFF(gr, gk));
+        const size_t o = sb + (size_t)(32 * (i >> 1)) * BK + 4 * (i & 1);
+        f32x4 wv = w[i], mv = m[i], vv;
+        if (OPT == kAdamW) vv = cv[i];
+        opt_update4<OPT>(wv, mv, vv, gv, h, c1, c2);
+        uint2 nh, nl;
+        split4(wv, nh, nl);
+        if ((i & 1) == 0) {
+          ph = nh;
+          pl = nl;
+          pm = f32_to_bf4(mv);
+        } else {
+          const uint4 hi16 = make_uint4(ph.x, ph.y, nh.x, nh.y);
+          *(uint4*)(W16 + o - 4) = hi16;
+          *(uint4*)(WLO + o - 4) = make_uint4(pl.x, pl.y, nl.x, nl.y);
+          if (OPT == kSGD16) {
+            const uint2 mb = f32_to_bf4(mv);
+            *(uint4*)(M16 + o - 4) = make_uint4(pm.x, pm.y, mb.x, mb.y);
+          }
+          *(uint4*)(Ws + TOFFF(gr, gk - 4)) = hi16;
+        }
+        if (OPT != kSGD16) *(f32x4*)(M32 + o) = mv;
+        if (OPT == kAdamW) *(f32x4*)(V32 + o) = vv;
+      }
+    }
+    __syncthreads();   // W_new of the strip complete in LDS
+
+    // ---- the next step's forward: acc += X'[:, strip] . W_new[chunk, strip]^T ----
+#pragma unroll
+    for (int ks = 0; ks < (DIAG == 1 ? 0 : 2); ++ks) {
+      bf16x8 b[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = lds_frag(Ws + TOFFF(j * 16 + li, ks * 32 + g * 8));
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = mfma16(__builtin_bit_cast(bf16x8, an[i][ks]), b[j], acc[i][j]);
+    }
+    if (PF) {
+      cwh0 = nwh0; cwh1 = nwh1; cwl0 = nwl0; cwl1 = nwl1;
+      if (OPT == kSGD16) { cmh0 = nmh0; cmh1 = nmh1; }
+      else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) cm[i] = nm[i];
+      }
+      if (OPT == kAdamW) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) cv[i] = nv[i];
+      }
+    } else if (s + 1 < nk) {
+      MOPT_B0F_LOAD(c, s + 1)
+    }
+  }
+  __syncthreads();   // every wave is done with Xs (the output tile) and Ws
+#undef MOPT_B0F_LOAD
+
+  // ---- Y'[:, chunk] = dropout(relu(acc + b_new)), keyed by step t + 1 (mlp_fwd_kernel's epilogue) ----
+  const bool drop = (flags & kInDropout) && h.drop > 0.f;   // kInDropout: the forward's dropout
+  const float inv_keep = drop ? 1.f / (1.f - h.drop) : 1.f;
+  const uint32_t key = rng_key(h.seed, 0u, h.t + 1u);
+  bf16_t* Cs = Xs;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = j * 16 + li;
+    const float bj = bnew[col];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wave * 32 + i * 16 + g * 4 + r;
+        float v = fmaxf(acc[i][j][r] + bj, 0.f);
+        if (drop) {
+          const uint32_t idx = (uint32_t)(row * N + n0 + col);
+          v = rng_uniform(key, idx) >= h.drop ? v * inv_keep : 0.f;
+        }
+        Cs[TOFF(row, col)] = f2bf(v);
+      }
+  }
+  __syncthreads();
+  bf16_t* Y = act + tl.y_off + n0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
+    *(uint4*)(Y + (size_t)r * N + ch * 8) = *(const uint4*)(Cs + TOFF(r, ch * 8));
   }
 }
 
@@ -923,7 +1253,7 @@ static void launch_bwd_rows(int n_work, int n_rowblocks, hipStream_t stream, con
 // ------------------------------------------------------------------------------------------------
 extern "C" {
 
-int mopt_abi_version() { return 13; }
+int mopt_abi_version() { return 14; }
 
 // weight layout: 1 = k-strip-major [K/64][N][64] (the only layout)
 int mopt_mlp_w_layout() { return 1; }
@@ -1012,9 +1342,41 @@ struct MlpStep {
   int32_t n_stats;  // entries of loss / correct (the population's capacity)
   int32_t fwd_tn;   // hidden-layer forward tile width of the work lists (64)
   int32_t narrow;   // 1: the loss layer has <= 16 classes (kNarrowCE / kNarrow launches)
+  const void* bwd0f;  // work list of the fused first layer (mlp_bwd0_fwd_kernel): (tl, n-chunk)
+  int32_t n_bwd0f;
+  int32_t fuse0;      // 1: consecutive steps of mopt_mlp_steps run the fused first layer
 };
 
-int mopt_mlp_step(const MlpStep* s, const void* x, const void* y, void* stream) {
+namespace {
+
+int mlp_bwd0_fwd(const MlpStep* s, const void* x, const void* x_next, void* stream) {
+  if (s->n_bwd0f <= 0) return 0;
+  const int flags = kUpdateBias | (s->drop ? kInDropout : 0);
+  const dim3 grid(s->n_bwd0f), block(256);
+#define MOPT_B0F(O, W, ...)                                                                      \
+  hipLaunchKernelGGL((mlp_bwd0_fwd_kernel<O, W, ##__VA_ARGS__>), grid, block, 0, (hipStream_t)stream, \
+                     (const MlpTL*)s->tls, (const int2*)s->bwd0f, s->n_bwd0f, (const bf16_t*)x,  \
+                     (const bf16_t*)x_next, (const bf16_t*)s->grad, (bf16_t*)s->act,            \
+                     (bf16_t*)s->plo, (bf16_t*)s->p16, (float*)s->m32, (float*)s->v32,          \
+                     (const TrialHP*)s->hp, flags)
+  static const int diag = [] {
+    const char* e = getenv("MOPT_B0F_DIAG");
+    return e == nullptr ? 0 : atoi(e);
+  }();
+  if (s->opt == kAdamW) MOPT_B0F(kAdamW, false);
+  else if (s->opt == kSGD16 && diag == 1) MOPT_B0F(kSGD16, true, 1);
+  else if (s->opt == kSGD16 && diag == 2) MOPT_B0F(kSGD16, false);
+  else if (s->opt == kSGD16) MOPT_B0F(kSGD16, true);
+  else MOPT_B0F(kSGD, true);
+#undef MOPT_B0F
+  return (int)hipGetLastError();
+}
+
+// one train step; fwd0_done: layer 0's forward of this step already ran (fused into the previous
+// step's first-layer backward); x_next != nullptr: fuse this step's first-layer backward with the
+// next step's first-layer forward (batch x_next)
+int mlp_step(const MlpStep* s, const void* x, const void* y, bool fwd0_done, const void* x_next,
+             void* stream) {
   if (s == nullptr || s->L < 1 || s->L > 8 || s->rb < 1) return (int)hipErrorInvalidValue;
   const int L = s->L;
   int err;
@@ -1024,7 +1386,7 @@ int mopt_mlp_step(const MlpStep* s, const void* x, const void* y, void* stream) 
     if (!err) err = (int)hipMemsetAsync(s->correct, 0, sizeof(float) * s->n_stats, (hipStream_t)stream);
     if (err) return err;
   }
-  for (int l = 0; l < L - 1; ++l) {
+  for (int l = fwd0_done ? 1 : 0; l < L - 1; ++l) {
     err = mopt_mlp_fwd(s->tls, s->fwd[l], s->n_fwd[l], s->rb, l == 0 ? x : s->act, s->plo,
                        s->p16, s->act, s->hp, 1u, l, kRelu | (s->drop ? kDropout : 0), s->fwd_tn,
                        stream);
@@ -1037,6 +1399,7 @@ int mopt_mlp_step(const MlpStep* s, const void* x, const void* y, void* stream) 
                         stream);
   if (err) return err;
   for (int l = L - 1; l >= 0; --l) {
+    if (l == 0 && x_next != nullptr) return mlp_bwd0_fwd(s, x, x_next, stream);
     int flags = kUpdateBias | ((l == L - 1 && s->narrow) ? kNarrow : 0);
     if (l > 0) flags |= kHasDx | (s->drop ? kInDropout : 0);
     err = mopt_mlp_bwd(s->tls, s->bwd[l], s->n_bwd[l], l == 0 ? x : s->act, s->grad, s->plo,
@@ -1046,13 +1409,23 @@ int mopt_mlp_step(const MlpStep* s, const void* x, const void* y, void* stream) 
   return 0;
 }
 
+}  // namespace
+
+int mopt_mlp_step(const MlpStep* s, const void* x, const void* y, void* stream) {
+  return mlp_step(s, x, y, false, nullptr, stream);
+}
+
 // ``n`` consecutive train steps of a group in ONE host call (step i reads batch xs[i] / ys[i]):
 // the sweep queues a whole sync interval with it, so the per-step host cost is the launches alone.
 int mopt_mlp_steps(const MlpStep* s, const void* const* xs, const void* const* ys, int n,
                    void* stream) {
   if (n < 0 || (n > 0 && (xs == nullptr || ys == nullptr))) return (int)hipErrorInvalidValue;
+  // the fused first layer needs one 128-row block per trial and a hidden layer in front of the
+  // loss layer; the last step of the call keeps the unfused backward (no next batch)
+  const bool fuse = s != nullptr && s->fuse0 && s->rb == 1 && s->L >= 2 && s->n_bwd0f > 0;
   for (int i = 0; i < n; ++i) {
-    const int err = mopt_mlp_step(s, xs[i], ys[i], stream);
+    const void* xn = (fuse && i + 1 < n) ? xs[i + 1] : nullptr;
+    const int err = mlp_step(s, xs[i], ys[i], fuse && i > 0, xn, stream);
     if (err) return err;
   }
   return 0;

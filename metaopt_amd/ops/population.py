@@ -64,7 +64,9 @@ class _MlpStep(ctypes.Structure):
                [(n, ctypes.c_void_p) for n in ("plo", "p16", "m32", "v32", "act", "grad", "hp",
                                                "loss", "correct")] + \
                [("inv_b", ctypes.c_float), ("n_stats", ctypes.c_int32),
-                ("fwd_tn", ctypes.c_int32), ("narrow", ctypes.c_int32)]
+                ("fwd_tn", ctypes.c_int32), ("narrow", ctypes.c_int32),
+                ("bwd0f", ctypes.c_void_p), ("n_bwd0f", ctypes.c_int32),
+                ("fuse0", ctypes.c_int32)]
 OPTIMIZERS = {"sgd": 0, "adamw": 1}
 
 
@@ -276,6 +278,11 @@ class PopulationMLP:
         if n_streams is None:
             n_streams = int(os.environ.get("MOPT_STREAMS", "3")) if backend == "hip" else 1
         self.n_streams = max(1, int(n_streams))
+        # consecutive train steps of one interval fuse the first layer's backward + update with
+        # the next step's first-layer forward (csrc/pop_mlp.hip mlp_bwd0_fwd_kernel: one pass
+        # over W0 instead of two; bit-identical results).  MOPT_FUSE0=0 keeps the separate
+        # launches (the A/B and the equality test).
+        self.fuse_first_layer = os.environ.get("MOPT_FUSE0", "1") != "0"
         self._side_streams: list = []
         self._events: list = []
         self._parts: list = []
@@ -768,6 +775,7 @@ class PopulationMLP:
         slots = np.array(self.active_slots(), dtype=np.int64)
         fwd: List[np.ndarray] = []
         bwd: List[np.ndarray] = []
+        bwd0f = np.zeros((0, 2), np.int32)
         if len(slots):
             widths = np.array([self.members[s].width for s in slots])
             used = (np.array([self.member_rows(self.members[s]) for s in slots], dtype=np.int64)
@@ -804,21 +812,30 @@ class PopulationMLP:
                 # a forward tile costs ~K, a backward k-strip ~N
                 fwd.append(_work_list(np.repeat(i, nt), _ranges(nt), np.repeat(K, nt)))
                 bwd.append(_work_list(np.repeat(i, nk), _ranges(nk), np.repeat(N, nk)))
+                if l == 0 and L >= 2:
+                    # the fused first layer (backward of step t + forward of step t + 1,
+                    # csrc/pop_mlp.hip mlp_bwd0_fwd_kernel): one item per 64-row chunk of W0,
+                    # each walking all of K
+                    nc = N // TILE
+                    bwd0f = _work_list(np.repeat(i, nc), _ranges(nc), np.repeat(K, nc))
         else:
             fwd = [np.zeros((0, 2), np.int32) for _ in range(L)]
             bwd = [np.zeros((0, 2), np.int32) for _ in range(L)]
-        out = {"tl_np": tl, "rows": rows, "fwd_np": fwd, "bwd_np": bwd, "fwd_tn": self.fwd_tn}
-        self._validate_tables(tl, fwd, bwd, rows)
+        out = {"tl_np": tl, "rows": rows, "fwd_np": fwd, "bwd_np": bwd, "fwd_tn": self.fwd_tn,
+               "bwd0f_np": bwd0f}
+        self._validate_tables(tl, fwd, bwd, rows, bwd0f)
         if self.device.type == "cuda":
             from ._lib import upload, upload_bytes
             out["tl"] = upload_bytes(tl, self.device)
             out["fwd"] = [upload(w, self.device) for w in fwd]
             out["bwd"] = [upload(w, self.device) for w in bwd]
+            out["bwd0f"] = upload(bwd0f, self.device) if len(bwd0f) else None
         out["n_fwd"] = [len(w) for w in fwd]
         out["n_bwd"] = [len(w) for w in bwd]
+        out["n_bwd0f"] = len(bwd0f)
         return out
 
-    def _validate_tables(self, tl, fwd, bwd, rows) -> None:
+    def _validate_tables(self, tl, fwd, bwd, rows, bwd0f=None) -> None:
         """Bounds check of every descriptor a launch will read (SURVEY §5 "race detection /
         sanitizers"): the kernels index memory only through these tables, so a table that
         passes here cannot make a kernel read or write outside its buffers.  Vectorised over
@@ -849,7 +866,8 @@ class PopulationMLP:
         if (t["n_real"] > t["N"]).any() or (t["trial"] < 0).any() or \
                 (t["trial"] >= self.capacity).any():
             bad.append("trial / class fields out of range")
-        for name, lists, per in (("fwd", fwd, "N"), ("bwd", bwd, "K")):
+        fused = [("bwd0f", [bwd0f], "N")] if bwd0f is not None and len(bwd0f) else []
+        for name, lists, per in [("fwd", fwd, "N"), ("bwd", bwd, "K")] + fused:
             for l, w in enumerate(lists):
                 if not len(w):
                     continue
@@ -859,6 +877,9 @@ class PopulationMLP:
                 idx = w[:, 0]
                 if (idx < 0).any() or (idx >= n_tl).any() or not live[idx].all():
                     bad.append(f"{name} work item names a missing trial-layer")
+                    break
+                if name == "bwd0f" and (idx % L != 0).any():
+                    bad.append("fused first-layer item names another layer")
                     break
                 tile = self.fwd_tn if (name == "fwd" and l < L - 1) else TILE
                 if (w[:, 1] < 0).any() or (w[:, 1] >= -(-tl[per][idx] // tile)).any():
@@ -892,6 +913,7 @@ class PopulationMLP:
                          "correct": self.correct.data_ptr(), "tl": tb["tl"].data_ptr(),
                          "fwd": [w.data_ptr() for w in tb["fwd"]],
                          "bwd": [w.data_ptr() for w in tb["bwd"]]}
+            # (the fused first layer's work list lives in each part)
             for part in self._parts:
                 part["step"] = self._step_args(part)
         self._dirty = False
@@ -911,6 +933,9 @@ class PopulationMLP:
         a.opt = 2 if self.momentum_dtype == "bf16" else OPTIMIZERS[self.optimizer]
         for n in ("plo", "p16", "m32", "v32", "act", "grad", "hp", "loss", "correct"):
             setattr(a, n, P[n])
+        a.bwd0f = part["bwd0f"] or 0
+        a.n_bwd0f = part["n_bwd0f"]
+        a.fuse0 = int(self.fuse_first_layer)
         a.inv_b = -1.0                 # the mean over each trial's own rows
         part["step_ptr"] = ctypes.addressof(a)
         return a
@@ -936,9 +961,12 @@ class PopulationMLP:
         if self.batch_size > 128:
             n = 1   # the step's stats zeroing covers every trial: one stream orders it
         if n <= 1:
+            b0f = tb.get("bwd0f")
             return [{"fwd": [w.data_ptr() for w in tb["fwd"]],
                      "bwd": [w.data_ptr() for w in tb["bwd"]],
-                     "n_fwd": tb["n_fwd"], "n_bwd": tb["n_bwd"]}]
+                     "n_fwd": tb["n_fwd"], "n_bwd": tb["n_bwd"],
+                     "bwd0f": b0f.data_ptr() if b0f is not None else None,
+                     "n_bwd0f": tb["n_bwd0f"]}]
         from ._lib import upload
         cost = {s: self.padded_params(s) for s in slots}
         load = [0] * n
@@ -956,9 +984,16 @@ class PopulationMLP:
             fwd_t = [upload(w, self.device) for w in fwd]
             bwd_t = [upload(w, self.device) for w in bwd]
             keep += fwd_t + bwd_t
+            b0f = (_reschedule(tb["bwd0f_np"], part_of, p, L, tb["tl_np"], "K")
+                   if len(tb["bwd0f_np"]) else np.zeros((0, 2), np.int32))
+            b0f_t = upload(b0f, self.device) if len(b0f) else None
+            if b0f_t is not None:
+                keep.append(b0f_t)
             parts.append({"fwd": [w.data_ptr() for w in fwd_t],
                           "bwd": [w.data_ptr() for w in bwd_t],
-                          "n_fwd": [len(w) for w in fwd], "n_bwd": [len(w) for w in bwd]})
+                          "n_fwd": [len(w) for w in fwd], "n_bwd": [len(w) for w in bwd],
+                          "bwd0f": b0f_t.data_ptr() if b0f_t is not None else None,
+                          "n_bwd0f": len(b0f)})
         tb["parts_keep"] = keep           # the work lists live as long as the table
         while len(self._side_streams) < n - 1:
             self._side_streams.append(torch.cuda.Stream(device=self.device))

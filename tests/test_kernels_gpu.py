@@ -353,3 +353,36 @@ def test_per_member_batch_trajectory_and_eval(data384):
     eh, _ = hip.evaluate(*data384.validation())
     er, _ = ref.evaluate(*data384.validation())
     assert np.abs(eh[act] - er[act]).max() < 3e-2
+
+
+@pytest.mark.parametrize("optimizer,n_hidden,streams", [
+    ("sgd-bf16m", 3, 3), ("sgd", 3, 1), ("adamw", 1, 1), ("sgd-bf16m", 2, 1)])
+def test_fused_first_layer_equals_separate_launches(data, optimizer, n_hidden, streams):
+    """``train_steps`` fuses each step's first-layer backward + update with the next step's
+    first-layer forward (csrc/pop_mlp.hip mlp_bwd0_fwd_kernel): weights, optimizer state and
+    losses equal the separate launches bit for bit, across two intervals, with dropout members."""
+    kw = {}
+    if optimizer == "sgd-bf16m":
+        optimizer, kw = "sgd", {"momentum_dtype": "bf16"}
+    cfgs = CONFIGS if optimizer == "sgd" else [
+        MemberConfig(width=c.width, lr=c.lr * 0.01, momentum=0.9, weight_decay=c.weight_decay,
+                     dropout=c.dropout, seed=c.seed) for c in CONFIGS]
+    pops = []
+    for fuse in (False, True):
+        p = PopulationMLP(6, max_width=256, n_hidden=n_hidden, eval_batch=256,
+                          optimizer=optimizer, device="cuda", backend="hip", n_streams=streams,
+                          **kw)
+        p.fuse_first_layer = fuse
+        for i, c in enumerate(cfgs):
+            p.set_member(i + 1, c)
+        pops.append(p)
+    for interval in range(2):
+        batches = [data.batch(6 * interval + k) for k in range(6)]
+        for p in pops:
+            p.train_steps(batches)
+        a, b = pops
+        torch.cuda.synchronize()
+        assert np.array_equal(a.train_loss(), b.train_loss(), equal_nan=True)
+        for name in ("p16", "plo", "m32", "v32"):
+            assert torch.equal(getattr(a, name), getattr(b, name)), name
+    assert b._parts[0]["n_bwd0f"] > 0
