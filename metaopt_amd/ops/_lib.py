@@ -40,6 +40,7 @@ _SIGNATURES = {
     "mopt_mlp_step": ([c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "mopt_mlp_w_layout": ([], c_int),
     "mopt_mlp_steps": ([c_void_p, c_void_p, c_void_p, c_int, c_void_p], c_int),
+    "mopt_mlp_bwd0_fwd": ([c_void_p, c_void_p, c_void_p, c_void_p], c_int),
 }
 
 _OPTIONAL_SIGNATURES: dict = {}

@@ -1415,6 +1415,13 @@ int mopt_mlp_step(const MlpStep* s, const void* x, const void* y, void* stream) 
   return mlp_step(s, x, y, false, nullptr, stream);
 }
 
+// the fused first layer of one step alone (its backward + update with batch x, the next step's
+// forward with batch x_next): scripts/kernel_bench.py times it
+int mopt_mlp_bwd0_fwd(const MlpStep* s, const void* x, const void* x_next, void* stream) {
+  if (s == nullptr || s->rb != 1 || s->L < 2) return (int)hipErrorInvalidValue;
+  return mlp_bwd0_fwd(s, x, x_next, stream);
+}
+
 // ``n`` consecutive train steps of a group in ONE host call (step i reads batch xs[i] / ys[i]):
 // the sweep queues a whole sync interval with it, so the per-step host cost is the launches alone.
 int mopt_mlp_steps(const MlpStep* s, const void* const* xs, const void* const* ys, int n,

@@ -100,6 +100,22 @@ for name, fn, byte_per in [("fwd", run_fwd, 2), ("bwd", run_bwd, BWD_BYTES)]:
                                      GBps=round(gbps, 1), TFLOPs=round(flops / ms / 1e9, 1))
         print(f"{name}{l}: {ms*1e3:8.1f} us  WG={n:6d}  params={layer_params[l]/1e6:7.2f}M "
               f"-> {gbps:7.1f} GB/s (param bytes)  {flops/ms/1e9:6.1f} TFLOP/s", flush=True)
+if pop.fuse_first_layer and RB == 1 and L >= 2 and len(pop._parts) == 1:
+    # the fused first layer (backward + update of step t, forward of step t + 1): one pass over W0
+    x2, _ = data.batch(1)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(args.iters):
+        _lib.check(lib.mopt_mlp_bwd0_fwd(pop._parts[0]["step_ptr"], x.data_ptr(), x2.data_ptr(),
+                                         stream), "mlp_bwd0_fwd")
+    ev1.record()
+    torch.cuda.synchronize()
+    ms = ev0.elapsed_time(ev1) / args.iters
+    gbps = layer_params[0] * (BWD_BYTES + 0) / (ms * 1e-3) / 1e9
+    results["bwd0f"] = dict(ms=round(ms, 4), workgroups=pop._parts[0]["n_bwd0f"],
+                            params=layer_params[0], GBps=round(gbps, 1))
+    print(f"bwd0f: {ms*1e3:8.1f} us  WG={pop._parts[0]['n_bwd0f']:6d}  (bwd0 + next fwd0, "
+          f"{gbps:7.1f} GB/s of backward param bytes)", flush=True)
 ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 ev0.record()
 for _ in range(args.iters):
