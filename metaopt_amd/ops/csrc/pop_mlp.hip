@@ -439,6 +439,15 @@ __global__ __launch_bounds__(256) void mlp_fwd_ce_kernel(const MlpTL* __restrict
   }
 }
 
+// Backward tiles (X strip, dZ chunk, W^T image): unpadded 128-byte rows, 16-byte chunk c of row r
+// stored at c ^ bsw(r).  Conflict-free for every per-chunk LDS access of the backward -- the dZ
+// A fragments (ds_read_b128), the three transposed ds_read_b64_tr_b16 reads and the staging
+// stores (scripts/lds_banks.py, searched over all XOR maps of the row bits) -- where the rows
+// padded to 72 elements cost 2 extra cycles per transposed read and 4 per fragment read
+// (1.66 conflict cycles per LDS instruction measured, profiles/r4/pmc_mlp_r4aa.txt).
+__device__ __forceinline__ int bsw(int r) { return (r & 2) | ((r & 8) >> 1); }
+#define BOFF(r, c) ((r) * BK + ((((c) >> 3) ^ bsw(r)) << 3) + ((c) & 7))
+
 // The per-parameter optimizer update of four consecutive parameters, shared by every kernel that
 // updates weights (mlp_bwd_opt_kernel, mlp_bwd0_fwd_kernel).  Explicit fmaf: the two kernels
 // must round identically, and hipcc's fp-contraction of the written-out expressions differed
@@ -515,13 +524,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
                                                           float* __restrict__ v32,
                                                           const TrialHP* __restrict__ hp, int flags) {
   constexpr int DS = BN + 4;  // f32 row stride bound of the dW staging tile (FOFF)
-  static_assert(BN * DS * 4 <= BM * TS * 2, "dW staging tile must fit the dZ tile");
+  // the dZ tile's region also holds the f32 dW staging tile (aliased, one more barrier per chunk)
+  constexpr int ZE = (BM * BK > 2 * BN * DS) ? BM * BK : 2 * BN * DS;
   __shared__ __attribute__((aligned(16)))
-      bf16_t smem[(2 * BM + BN) * TS + 2 * 4 * BN];
+      bf16_t smem[BM * BK + ZE + BN * BK + 2 * 4 * BN];
   bf16_t* Xs = smem;
-  bf16_t* Zs = smem + BM * TS;
-  bf16_t* Ws = smem + 2 * BM * TS;
-  float* red = (float*)(smem + (2 * BM + BN) * TS);  // [4][64] bias partial sums
+  bf16_t* Zs = smem + BM * BK;
+  bf16_t* Ws = smem + BM * BK + ZE;
+  float* red = (float*)(smem + BM * BK + ZE + BN * BK);  // [4][64] bias partial sums
   // [64 n][DS] dW of the current chunk
   float* Dw = (float*)Zs;
 
@@ -564,7 +574,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
-    *(uint4*)(Xs + TOFF(r, ch * 8)) = *(const uint4*)(X + (size_t)r * K + k0 + ch * 8);
+    *(uint4*)(Xs + BOFF(r, ch * 8)) = *(const uint4*)(X + (size_t)r * K + k0 + ch * 8);
   }
   __syncthreads();
 
@@ -582,7 +592,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
   // workgroup per CU hides them).
   const int zo0 = (tid >> 3) * N + (tid & 7) * 8, zo1 = ((tid + 256) >> 3) * N + (tid & 7) * 8;
   const int zo2 = ((tid + 512) >> 3) * N + (tid & 7) * 8, zo3 = ((tid + 768) >> 3) * N + (tid & 7) * 8;
-  bf16_t* zs0 = Zs + TOFF(tid >> 3, (tid & 7) * 8);     // rows +32 i keep the swizzle
+  bf16_t* zs0 = Zs + BOFF(tid >> 3, (tid & 7) * 8);     // rows +32 i keep the swizzle
   const int WRS = w_row_stride(K);
   // Optimizer-state layout: thread -> rows 32 i + tid / 8 (i < 2), 8 consecutive k at 8 (tid % 8):
   // every W / M (/ V) access is 16 bytes per lane and a wave-instruction moves 8 rows x 128 B
@@ -656,9 +666,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
   for (int nc = 0; nc < N; nc += BN) {
     // ---- this chunk's operands -> LDS (dZ row-major; W^T image as bf16 for the dX MFMAs) ----
     *(uint4*)(zs0) = cz0;
-    *(uint4*)(zs0 + 32 * TS) = cz1;
-    *(uint4*)(zs0 + 64 * TS) = cz2;
-    *(uint4*)(zs0 + 96 * TS) = cz3;
+    *(uint4*)(zs0 + 32 * BK) = cz1;
+    *(uint4*)(zs0 + 64 * BK) = cz2;
+    *(uint4*)(zs0 + 96 * BK) = cz3;
     // per thread: 2 rows x 8 k = 4 groups of 4 (row 0 k 0-3, row 0 k 4-7, row 1 k 0-3, 4-7)
     if (OPT == kSGD16) {
       cm0 = bf4_to_f32(make_uint2(ch0.x, ch0.y)); cm1 = bf4_to_f32(make_uint2(ch0.z, ch0.w));
@@ -678,7 +688,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     if (PF && more) MOPT_BWD_LOAD(nc + BN, n)
     if (has_dx) {   // the bf16 working copy (hi) is the dX operand, as in the forward
 #pragma unroll
-      for (int i = 0; i < 2; ++i) *(uint4*)(Ws + TOFF(32 * i + (tid >> 3), 8 * (tid & 7))) = wh[i];
+      for (int i = 0; i < 2; ++i) *(uint4*)(Ws + BOFF(32 * i + (tid >> 3), 8 * (tid & 7))) = wh[i];
     }
     __syncthreads();
 
@@ -688,11 +698,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
       for (int s = 0; s < 2; ++s) {
         bf16x8 a[2], b[4];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) a[i] = lds_frag(Zs + TOFF(32 * wave + 16 * i + li, 32 * s + 8 * g));
+        for (int i = 0; i < 2; ++i) a[i] = lds_frag(Zs + BOFF(32 * wave + 16 * i + li, 32 * s + 8 * g));
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const s16x4 lo = lds_tr4(Ws + TOFF(32 * s + 8 * g + q, 16 * j + 4 * pp));
-          const s16x4 hi = lds_tr4(Ws + TOFF(32 * s + 8 * g + 4 + q, 16 * j + 4 * pp));
+          const s16x4 lo = lds_tr4(Ws + BOFF(32 * s + 8 * g + q, 16 * j + 4 * pp));
+          const s16x4 hi = lds_tr4(Ws + BOFF(32 * s + 8 * g + 4 + q, 16 * j + 4 * pp));
           b[j] = cat_frag(lo, hi);
         }
 #pragma unroll
@@ -713,14 +723,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     bf16x8 xa[2], bz[2];                                                                         \
     _Pragma("unroll") for (int t = 0; t < 2; ++t) {                                              \
       const int c0 = 32 * wk + 16 * t + 4 * pp;                                                  \
-      const s16x4 lo = lds_tr4(Xs + TOFF(32 * s + 8 * g + q, c0));                               \
-      const s16x4 hi = lds_tr4(Xs + TOFF(32 * s + 8 * g + 4 + q, c0));                           \
+      const s16x4 lo = lds_tr4(Xs + BOFF(32 * s + 8 * g + q, c0));                               \
+      const s16x4 hi = lds_tr4(Xs + BOFF(32 * s + 8 * g + 4 + q, c0));                           \
       xa[t] = cat_frag(lo, hi);                                                                  \
     }                                                                                            \
     _Pragma("unroll") for (int u = 0; u < 2; ++u) {                                              \
       const int c0 = 32 * wn + 16 * u + 4 * pp;                                                  \
-      const s16x4 lo = lds_tr4(Zs + TOFF(32 * s + 8 * g + q, c0));                               \
-      const s16x4 hi = lds_tr4(Zs + TOFF(32 * s + 8 * g + 4 + q, c0));                           \
+      const s16x4 lo = lds_tr4(Zs + BOFF(32 * s + 8 * g + q, c0));                               \
+      const s16x4 hi = lds_tr4(Zs + BOFF(32 * s + 8 * g + 4 + q, c0));                           \
       bz[u] = cat_frag(lo, hi);                                                                  \
     }                                                                                            \
     _Pragma("unroll") for (int t = 0; t < 2; ++t)                                                \
@@ -732,7 +742,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     if (MODE != 2) {
       MOPT_BWD_DW()
       if (do_bias)
-        for (int r = bpart * 32; r < bpart * 32 + 32; ++r) bsum += bf2f(Zs[TOFF(r, bcol)]);
+        for (int r = bpart * 32; r < bpart * 32 + 32; ++r) bsum += bf2f(Zs[BOFF(r, bcol)]);
       if (MODE == 1) {
         for (int rb = 1; rb < R; ++rb) {      // R is uniform per workgroup
           __syncthreads();                    // every wave is done with the previous block
@@ -741,20 +751,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
-            *(uint4*)(Xs + TOFF(r, ch * 8)) = *(const uint4*)(Xr + (size_t)r * K + ch * 8);
-            *(uint4*)(Zs + TOFF(r, ch * 8)) = *(const uint4*)(Zr + (size_t)r * N + ch * 8);
+            *(uint4*)(Xs + BOFF(r, ch * 8)) = *(const uint4*)(Xr + (size_t)r * K + ch * 8);
+            *(uint4*)(Zs + BOFF(r, ch * 8)) = *(const uint4*)(Zr + (size_t)r * N + ch * 8);
           }
           __syncthreads();
           MOPT_BWD_DW()
           if (do_bias)
-            for (int r = bpart * 32; r < bpart * 32 + 32; ++r) bsum += bf2f(Zs[TOFF(r, bcol)]);
+            for (int r = bpart * 32; r < bpart * 32 + 32; ++r) bsum += bf2f(Zs[BOFF(r, bcol)]);
         }
         if (R > 1) {                          // row block 0's X strip back (next chunk, dX mask)
           __syncthreads();
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
-            *(uint4*)(Xs + TOFF(r, ch * 8)) = *(const uint4*)(X + (size_t)r * K + k0 + ch * 8);
+            *(uint4*)(Xs + BOFF(r, ch * 8)) = *(const uint4*)(X + (size_t)r * K + k0 + ch * 8);
           }
         }
       }
@@ -843,15 +853,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = 32 * wave + 16 * i + 4 * g + r, col = 16 * j + li;
-        const float xv = bf2f(Xs[TOFF(row, col)]);
-        Zs[TOFF(row, col)] = f2bf(xv > 0.f ? dx[i][j][r] * inv_keep : 0.f);
+        const float xv = bf2f(Xs[BOFF(row, col)]);
+        Zs[BOFF(row, col)] = f2bf(xv > 0.f ? dx[i][j][r] * inv_keep : 0.f);
       }
   __syncthreads();
   bf16_t* GX = grad + tl.gx_off + (size_t)rbx * BM * K + k0;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
-    *(uint4*)(GX + (size_t)r * K + ch * 8) = *(const uint4*)(Zs + TOFF(r, ch * 8));
+    *(uint4*)(GX + (size_t)r * K + ch * 8) = *(const uint4*)(Zs + BOFF(r, ch * 8));
   }
 }
 
