@@ -22,6 +22,18 @@ typedef uint16_t bf16_t;  // storage type of a bf16 element
 
 constexpr int kLdsStride = 72;  // bf16 elements per LDS tile row (64 + 8 pad)
 
+// Unpadded LDS tiles of 64-element (128-byte) rows with the 16-byte chunk c of row r stored at
+// chunk c ^ swz128(r) (row bits 1 and 3 into chunk bits 1 and 2).  Conflict-free for the MFMA
+// fragment reads of these tiles -- ds_read_b128 of 16 rows at one chunk, ds_read_b64_tr_b16 of
+// 4 + 4 rows x 2 lane groups -- and for the 8-lanes-per-row staging stores (scripts/lds_banks.py
+// searched every XOR map of the row bits; padding rows to 72 elements costs 4 extra cycles per
+// fragment read and 2 per transposed read).  Rows r and r + 4 k + 32 m share the map, so a
+// lane's fragment addresses differ by immediate offsets across those rows.
+__device__ __forceinline__ int swz128(int r) { return (r & 2) | ((r & 8) >> 1); }
+__device__ __forceinline__ int soff(int r, int c) {
+  return r * 64 + (((c >> 3) ^ swz128(r)) << 3) + (c & 7);
+}
+
 // 64-column bf16 LDS tiles with 128-B rows whose 16-B chunks are XOR-swizzled by row:
 // chunk' = chunk ^ swz_row(row), swz_row = (r0^r1^r2^r3^r4, r0^r1^r2^r3, r0^r3) over the row's
 // low 5 bits.  Found by scripts/lds_banks.py: conflict-free for every LDS access of the

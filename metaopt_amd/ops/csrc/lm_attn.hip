@@ -26,9 +26,19 @@ namespace {
 constexpr int D = 64;          // head dim
 constexpr int BQ = 64;         // queries per workgroup
 constexpr int BKV = 64;        // keys per block
-constexpr int LS = kLdsStride;  // (a conflict-free XOR chunk swizzle of 128-byte rows, per
-                                // scripts/lds_banks.py, measured slower in round 4: dQ 87 -> 138
-                                // us, the per-access address math; profiles/round4.md)
+constexpr int LS = kLdsStride;
+// LDS tile layouts: SW = common.h's XOR chunk swizzle of 64-element rows (soff; every fragment
+// read conflict-free), else rows padded to LS = 72 elements (4 extra cycles per fragment read, 2
+// per transposed read).  The forward uses SW (round 5: 109-114 -> 96-104 us per call at the same
+// occupancy, bank conflicts 0).  The backward kernels keep the padded rows: swizzled, the extra
+// per-lane addresses spill them at their 4 / 3 waves per SIMD, and at 3 / 2 waves (no spills, no
+// conflicts) dQ + dK/dV ran 324 against 289 us (profiles/r5/attn_swizzle/).  (Round 4 measured
+// another swizzle, chunk ^ (row >> 1) & 7, slower even in the forward: it mixed the rows that
+// otherwise differ by immediate offsets; swz128 leaves row bits 0, 2, 4, 5 out.)
+template <bool SW>
+__device__ __forceinline__ int toff(int r, int c) { return SW ? soff(r, c) : r * LS + c; }
+template <bool SW>
+constexpr int tile_elems() { return SW ? 64 * D : 64 * LS; }
 
 // Occupancy targets (waves per SIMD; 0 = the compiler's choice): the register cap that lets N
 // workgroups share a CU.  Swept in round 4 on variant builds (scripts/attn_bench.py,
@@ -58,12 +68,13 @@ __device__ __forceinline__ int2 head_block(int nblk, int n_bh) {
   return make_int2(t % nblk, t / nblk);
 }
 
-// Load a [64][64] bf16 tile (rows contiguous, row stride 64) into LDS [64][LS].
+// Load a [64][64] bf16 tile (rows contiguous, row stride 64) into a swizzled LDS tile.
+template <bool SW>
 __device__ __forceinline__ void tile_to_lds(const bf16_t* __restrict__ g, bf16_t* s, int tid) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
-    *(uint4*)(s + r * LS + ch * 8) = *(const uint4*)(g + r * D + ch * 8);
+    *(uint4*)(s + toff<SW>(r, ch * 8)) = *(const uint4*)(g + r * D + ch * 8);
   }
 }
 
@@ -74,9 +85,10 @@ __device__ __forceinline__ void tile_load(const bf16_t* __restrict__ g, uint4& r
   r0 = *(const uint4*)(g + (tid >> 3) * D + (tid & 7) * 8);
   r1 = *(const uint4*)(g + ((tid + 256) >> 3) * D + (tid & 7) * 8);
 }
+template <bool SW>
 __device__ __forceinline__ void tile_store(const uint4& r0, const uint4& r1, bf16_t* s, int tid) {
-  *(uint4*)(s + (tid >> 3) * LS + (tid & 7) * 8) = r0;
-  *(uint4*)(s + ((tid + 256) >> 3) * LS + (tid & 7) * 8) = r1;
+  *(uint4*)(s + toff<SW>(tid >> 3, (tid & 7) * 8)) = r0;
+  *(uint4*)(s + toff<SW>((tid + 256) >> 3, (tid & 7) * 8)) = r1;
 }
 
 // Key row of the permuted K/V fragment: tile j = 2s + h, fragment row m.
@@ -85,9 +97,10 @@ __device__ __forceinline__ int perm_row(int s, int h, int m) {
 }
 
 // V^T (or K^T) A-fragment for keys 32s + 8g .. +7, head-dim columns 16 dt .. +15, from LDS [key][dh].
+template <bool SW>
 __device__ __forceinline__ bf16x8 tr_frag(const bf16_t* s, int ks, int g, int q, int pp, int dt) {
-  const s16x4 lo = lds_tr4(s + (32 * ks + 8 * g + q) * LS + 16 * dt + 4 * pp);
-  const s16x4 hi = lds_tr4(s + (32 * ks + 8 * g + 4 + q) * LS + 16 * dt + 4 * pp);
+  const s16x4 lo = lds_tr4(s + toff<SW>(32 * ks + 8 * g + q, 16 * dt + 4 * pp));
+  const s16x4 hi = lds_tr4(s + toff<SW>(32 * ks + 8 * g + 4 + q, 16 * dt + 4 * pp));
   return cat_frag(lo, hi);
 }
 
@@ -135,16 +148,28 @@ __device__ __forceinline__ void put_grad4(bf16_t* plain, const RopeOut& ro, int 
   *(uint2*)o = make_uint2(pack2bf(x[0], x[1]), pack2bf(x[2], x[3]));
 }
 
+// max / sum over the lanes l, l ^ 16, l ^ 32, l ^ 48 with gfx950's v_permlane16_swap /
+// v_permlane32_swap (VALU, a few cycles): with both operands v, the pair the swap returns is
+// {v[l], v[l ^ 16]} (or ^ 32) in some order, and max / + of the pair is order-free.  __shfl_xor
+// compiled to ds_bpermute_b32 -- an LDS round trip on the softmax's critical path, 4 per key block.
+__device__ __forceinline__ float xor16_pair_max(float v) {
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
+}
 __device__ __forceinline__ float max4(float v) {
-  v = fmaxf(v, __shfl_xor(v, 16, 64));
-  return fmaxf(v, __shfl_xor(v, 32, 64));
+  v = xor16_pair_max(v);
+  const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
 }
 __device__ __forceinline__ float sum4(float v) {
-  v += __shfl_xor(v, 16, 64);
-  return v + __shfl_xor(v, 32, 64);
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
 // S^T tiles for one 64-key block: st[j][r] = s(query li, key 32s + 8g + 4h + r), j = 2s + h.
+template <bool SW>
 __device__ __forceinline__ void scores_T(const bf16_t* Ks, const bf16x8 (&qf)[2], int li, int g,
                                          f32x4 (&st)[4]) {
 #pragma unroll
@@ -154,7 +179,7 @@ __device__ __forceinline__ void scores_T(const bf16_t* Ks, const bf16x8 (&qf)[2]
       const int j = 2 * s + h, row = perm_row(s, h, li);
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) acc = mfma16(lds_frag(Ks + row * LS + 32 * ks + 8 * g), qf[ks], acc);
+      for (int ks = 0; ks < 2; ++ks) acc = mfma16(lds_frag(Ks + toff<SW>(row, 32 * ks + 8 * g)), qf[ks], acc);
       st[j] = acc;
     }
 }
@@ -166,8 +191,8 @@ __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnFwdWaves) void attn_fwd_k
                                                        bf16_t* __restrict__ O,
                                                        float* __restrict__ LSE2, int T, int H,
                                                        float c, int n_bh) {
-  __shared__ __attribute__((aligned(16))) bf16_t Ks[BKV * LS];
-  __shared__ __attribute__((aligned(16))) bf16_t Vs[BKV * LS];
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[tile_elems<true>()];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[tile_elems<true>()];
   const int nqb = T / BQ;
   const int2 hb = head_block(nqb, n_bh);
   const int qb = nqb - 1 - hb.x;                      // longest (most key blocks) first
@@ -191,8 +216,8 @@ __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnFwdWaves) void attn_fwd_k
   tile_load(V + base, va, vc, tid);
   for (int kb = 0; kb <= qb; ++kb) {
     __syncthreads();
-    tile_store(ka, kc, Ks, tid);
-    tile_store(va, vc, Vs, tid);
+    tile_store<true>(ka, kc, Ks, tid);
+    tile_store<true>(va, vc, Vs, tid);
     __syncthreads();
     {
       const size_t nb = (size_t)min(kb + 1, qb) * BKV * D;   // clamped: no branch around loads
@@ -200,7 +225,7 @@ __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnFwdWaves) void attn_fwd_k
       tile_load(V + base + nb, va, vc, tid);
     }
     f32x4 st[4];
-    scores_T(Ks, qf, li, g, st);
+    scores_T<true>(Ks, qf, li, g, st);
     float mx = -INFINITY;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
@@ -233,7 +258,7 @@ __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnFwdWaves) void attn_fwd_k
     for (int s = 0; s < 2; ++s) {
       const bf16x8 pb = pack_frag(st[2 * s], st[2 * s + 1]);
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) o[dt] = mfma16(tr_frag(Vs, s, g, q, pp, dt), pb, o[dt]);
+      for (int dt = 0; dt < 4; ++dt) o[dt] = mfma16(tr_frag<true>(Vs, s, g, q, pp, dt), pb, o[dt]);
     }
   }
   // o[dt][r] = O^T[dh 16 dt + 4 g + r][query li]
@@ -279,8 +304,8 @@ __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnDqWaves) void attn_bwd_dq
                                                           bf16_t* __restrict__ dQ, int T, int H,
                                                           float c, float scale, int n_bh,
                                                           const RopeOut ro) {
-  __shared__ __attribute__((aligned(16))) bf16_t Ks[BKV * LS];
-  __shared__ __attribute__((aligned(16))) bf16_t Vs[BKV * LS];
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[tile_elems<false>()];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[tile_elems<false>()];
   const int nqb = T / BQ;
   const int2 hb = head_block(nqb, n_bh);
   const int qb = nqb - 1 - hb.x;
@@ -308,8 +333,8 @@ __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnDqWaves) void attn_bwd_dq
   tile_load(V + base, va, vc, tid);
   for (int kb = 0; kb <= qb; ++kb) {
     __syncthreads();
-    tile_store(ka, kc, Ks, tid);
-    tile_store(va, vc, Vs, tid);
+    tile_store<false>(ka, kc, Ks, tid);
+    tile_store<false>(va, vc, Vs, tid);
     __syncthreads();
     {
       const size_t nb = (size_t)min(kb + 1, qb) * BKV * D;
@@ -317,8 +342,8 @@ __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnDqWaves) void attn_bwd_dq
       tile_load(V + base + nb, va, vc, tid);
     }
     f32x4 st[4], dpt[4];
-    scores_T(Ks, qf, li, g, st);
-    scores_T(Vs, df, li, g, dpt);     // dP^T = V dO^T, same permuted key order
+    scores_T<false>(Ks, qf, li, g, st);
+    scores_T<false>(Vs, df, li, g, dpt);     // dP^T = V dO^T, same permuted key order
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -334,7 +359,7 @@ __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnDqWaves) void attn_bwd_dq
     for (int s = 0; s < 2; ++s) {
       const bf16x8 sb = pack_frag(st[2 * s], st[2 * s + 1]);
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma16(tr_frag(Ks, s, g, q, pp, dt), sb, acc[dt]);
+      for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma16(tr_frag<false>(Ks, s, g, q, pp, dt), sb, acc[dt]);
     }
   }
   bf16_t* out = dQ + base + (size_t)qrow * D;
@@ -358,8 +383,8 @@ __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnDkdvWaves) void attn_bwd_
                                                             bf16_t* __restrict__ dV, int T, int H,
                                                             float c, float scale, int n_bh,
                                                             const RopeOut ro) {
-  __shared__ __attribute__((aligned(16))) bf16_t Qs[BQ * LS];
-  __shared__ __attribute__((aligned(16))) bf16_t dOs[BQ * LS];
+  __shared__ __attribute__((aligned(16))) bf16_t Qs[tile_elems<false>()];
+  __shared__ __attribute__((aligned(16))) bf16_t dOs[tile_elems<false>()];
   __shared__ float lse_s[BQ], dsum_s[BQ];
   const int2 hb = head_block(T / BKV, n_bh);
   const int kb = hb.x;                            // blocks with more query blocks are early ids
@@ -400,9 +425,9 @@ __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnDkdvWaves) void attn_bwd_
   MOPT_DKDV_LOAD(kb)
   for (int qb = kb; qb < nqb; ++qb) {
     __syncthreads();
-    tile_store(qa, qc, Qs, tid);
-    *(uint4*)(dOs + r0 * LS + ch * 8) = da;
-    *(uint4*)(dOs + r1 * LS + ch * 8) = dc;
+    tile_store<false>(qa, qc, Qs, tid);
+    *(uint4*)(dOs + toff<false>(r0, ch * 8)) = da;
+    *(uint4*)(dOs + toff<false>(r1, ch * 8)) = dc;
     if (tid < BQ) {
       lse_s[tid] = lse_r;
       dsum_s[tid] = dsum_r;
@@ -411,8 +436,8 @@ __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnDkdvWaves) void attn_bwd_
     MOPT_DKDV_LOAD(min(qb + 1, nqb - 1))
     // S and dP tiles j = 2s + h: rows = queries 32s + 8g + 4h + r (C layout), column = key li.
     f32x4 st[4], dp[4];
-    scores_T(Qs, kf, li, g, st);
-    scores_T(dOs, vf, li, g, dp);
+    scores_T<false>(Qs, kf, li, g, st);
+    scores_T<false>(dOs, vf, li, g, dp);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -430,8 +455,8 @@ __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnDkdvWaves) void attn_bwd_
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         // dV^T[dh][key] += dO^T P^T : A = dO^T (tr-read), B = P^T fragment (this lane's key)
-        dv[dt] = mfma16(tr_frag(dOs, s, g, q, pp, dt), pa, dv[dt]);
-        dk[dt] = mfma16(tr_frag(Qs, s, g, q, pp, dt), sa, dk[dt]);
+        dv[dt] = mfma16(tr_frag<false>(dOs, s, g, q, pp, dt), pa, dv[dt]);
+        dk[dt] = mfma16(tr_frag<false>(Qs, s, g, q, pp, dt), sa, dk[dt]);
       }
     }
   }

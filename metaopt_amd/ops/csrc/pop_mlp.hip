@@ -440,13 +440,12 @@ __global__ __launch_bounds__(256) void mlp_fwd_ce_kernel(const MlpTL* __restrict
 }
 
 // Backward tiles (X strip, dZ chunk, W^T image): unpadded 128-byte rows, 16-byte chunk c of row r
-// stored at c ^ bsw(r).  Conflict-free for every per-chunk LDS access of the backward -- the dZ
+// stored at c ^ swz128(r) (common.h).  Conflict-free for every per-chunk LDS access of the backward -- the dZ
 // A fragments (ds_read_b128), the three transposed ds_read_b64_tr_b16 reads and the staging
 // stores (scripts/lds_banks.py, searched over all XOR maps of the row bits) -- where the rows
 // padded to 72 elements cost 2 extra cycles per transposed read and 4 per fragment read
 // (1.66 conflict cycles per LDS instruction measured, profiles/r4/pmc_mlp_r4aa.txt).
-__device__ __forceinline__ int bsw(int r) { return (r & 2) | ((r & 8) >> 1); }
-#define BOFF(r, c) ((r) * BK + ((((c) >> 3) ^ bsw(r)) << 3) + ((c) & 7))
+#define BOFF(r, c) soff((r), (c))   // common.h swz128 (BK = 64-element rows)
 
 // The per-parameter optimizer update of four consecutive parameters, shared by every kernel that
 // updates weights (mlp_bwd_opt_kernel, mlp_bwd0_fwd_kernel).  Explicit fmaf: the two kernels
