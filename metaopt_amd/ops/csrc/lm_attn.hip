@@ -385,7 +385,8 @@ __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnDkdvWaves) void attn_bwd_
                                                             const RopeOut ro) {
   __shared__ __attribute__((aligned(16))) bf16_t Qs[tile_elems<false>()];
   __shared__ __attribute__((aligned(16))) bf16_t dOs[tile_elems<false>()];
-  __shared__ float lse_s[BQ], dsum_s[BQ];
+  __shared__ __attribute__((aligned(16))) float lse_s[BQ];
+  __shared__ __attribute__((aligned(16))) float dsum_s[BQ];
   const int2 hb = head_block(T / BKV, n_bh);
   const int kb = hb.x;                            // blocks with more query blocks are early ids
   const int bh = hb.y;
@@ -411,15 +412,24 @@ __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnDkdvWaves) void attn_bwd_
   uint4 qa, qc, da, dc;
   float lse_r = 0.f, dsum_r = 0.f;
   const int r0 = tid >> 3, r1 = (tid + 256) >> 3, ch = tid & 7;
+  // per-thread bases of the query-block loads (block qb_ adds qb_ * BQ rows): 32-bit offsets
+  // from them, no 64-bit index arithmetic inside the loop
+  const bf16_t* qbase = Q + base + (tid >> 3) * D + (tid & 7) * 8;
+  const bf16_t* dob = dO + (((size_t)b * T + r0) * H + hh) * D + ch * 8;
+  const int dorow = 32 * H * D;                                   // rows r1 - r0 = 32
+  const float* lseb = LSE2 + (size_t)bh * T + tid;
+  const float* dsb = Dsum + (size_t)bh * T + tid;
 #define MOPT_DKDV_LOAD(QB)                                                                   \
   {                                                                                          \
     const int qb_ = (QB);                                                                    \
-    tile_load(Q + base + (size_t)qb_ * BQ * D, qa, qc, tid);                                 \
-    da = *(const uint4*)(dO + (((size_t)b * T + qb_ * BQ + r0) * H + hh) * D + ch * 8);      \
-    dc = *(const uint4*)(dO + (((size_t)b * T + qb_ * BQ + r1) * H + hh) * D + ch * 8);      \
+    const uint32_t qo_ = (uint32_t)(qb_ * BQ * D), do_ = (uint32_t)(qb_ * BQ * H * D);       \
+    qa = *(const uint4*)(qbase + qo_);                                                       \
+    qc = *(const uint4*)(qbase + qo_ + 32 * D);                                              \
+    da = *(const uint4*)(dob + do_);                                                         \
+    dc = *(const uint4*)(dob + do_ + dorow);                                                 \
     if (tid < BQ) {                                                                          \
-      lse_r = LSE2[(size_t)bh * T + qb_ * BQ + tid];                                         \
-      dsum_r = Dsum[(size_t)bh * T + qb_ * BQ + tid];                                        \
+      lse_r = lseb[qb_ * BQ];                                                                \
+      dsum_r = dsb[qb_ * BQ];                                                                \
     }                                                                                        \
   }
   MOPT_DKDV_LOAD(kb)
@@ -439,15 +449,19 @@ __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnDkdvWaves) void attn_bwd_
     scores_T<false>(Qs, kf, li, g, st);
     scores_T<false>(dOs, vf, li, g, dp);
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < 4; ++j) {
+      // the 4 queries of register r = 0..3 are consecutive: one 16-byte LDS read each for LSE2
+      // and Dsum (instead of 8 4-byte reads)
+      const int q0 = 32 * (j >> 1) + 8 * g + 4 * (j & 1);
+      const f32x4 l4 = *(const f32x4*)(lse_s + q0), d4 = *(const f32x4*)(dsum_s + q0);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int qi = 32 * (j >> 1) + 8 * g + 4 * (j & 1) + r;
-        float p = fast_exp2(st[j][r] * c - lse_s[qi]);
-        if (qb == kb && qb * BQ + qi < krow) p = 0.f;
+        float p = fast_exp2(st[j][r] * c - l4[r]);
+        if (qb == kb && qb * BQ + q0 + r < krow) p = 0.f;
         st[j][r] = p;
-        dp[j][r] = p * (dp[j][r] - dsum_s[qi]);
+        dp[j][r] = p * (dp[j][r] - d4[r]);
       }
+    }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const bf16x8 pa = pack_frag(st[2 * s], st[2 * s + 1]);
