@@ -14,6 +14,8 @@
 //                        dW = dZ^T X, db = colsum(dZ)
 //                      and applies the per-trial SGD-momentum / AdamW update in the epilogue, so
 //                      dW never touches HBM.  W is read once (f32 master) for both dX and the update.
+//   mlp_bwd0_fwd_kernel the first layer's backward + update of step t fused with its forward of
+//                      step t + 1 (one pass over W0 instead of two; bit-identical results)
 //
 // Memory-bound by design: per parameter and step the population moves 2 B (forward) + 18 B (fused
 // backward + SGD; 14 B with the bf16 momentum buffer of kSGD16) through HBM; the MFMA work
@@ -884,7 +886,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 // ----------------------------------------------------------------------------------------------
 // PF: the next strip's state in a second register set (SGD, SGD16; AdamW's f32 moments do not
 // fit twice); two waves per SIMD
-template <int OPT, bool PF, int DIAG = 0>
+template <int OPT, bool PF>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void mlp_bwd0_fwd_kernel(
     const MlpTL* __restrict__ tls, const int2* __restrict__ work, int n_work,
     const bf16_t* __restrict__ xb, const bf16_t* __restrict__ xn, const bf16_t* __restrict__ grad,
@@ -1026,13 +1028,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
     if (PF) MOPT_B0F_LOAD(n, sn)
     uint4 an[2][2];
-    if (DIAG != 1) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-          an[i][ks] = *(const uint4*)(Xn + ao + 16 * K * i + k0 + 32 * ks);
-    }
+      for (int ks = 0; ks < 2; ++ks)
+        an[i][ks] = *(const uint4*)(Xn + ao + 16 * K * i + k0 + 32 * ks);
     __syncthreads();   // Xs visible; the previous strip's readers of Dw / Ws are done
 
     // ---- dW^T[strip, chunk] = X^T dZ (mlp_bwd_opt_kernel's fragments and order) -> Dw ----
@@ -1118,7 +1118,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
     // ---- the next step's forward: acc += X'[:, strip] . W_new[chunk, strip]^T ----
 #pragma unroll
-    for (int ks = 0; ks < (DIAG == 1 ? 0 : 2); ++ks) {
+    for (int ks = 0; ks < 2; ++ks) {
       bf16x8 b[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) b[j] = lds_frag(Ws + TOFFF(j * 16 + li, ks * 32 + g * 8));
@@ -1362,19 +1362,13 @@ int mlp_bwd0_fwd(const MlpStep* s, const void* x, const void* x_next, void* stre
   if (s->n_bwd0f <= 0) return 0;
   const int flags = kUpdateBias | (s->drop ? kInDropout : 0);
   const dim3 grid(s->n_bwd0f), block(256);
-#define MOPT_B0F(O, W, ...)                                                                      \
-  hipLaunchKernelGGL((mlp_bwd0_fwd_kernel<O, W, ##__VA_ARGS__>), grid, block, 0, (hipStream_t)stream, \
+#define MOPT_B0F(O, W)                                                                           \
+  hipLaunchKernelGGL((mlp_bwd0_fwd_kernel<O, W>), grid, block, 0, (hipStream_t)stream,          \
                      (const MlpTL*)s->tls, (const int2*)s->bwd0f, s->n_bwd0f, (const bf16_t*)x,  \
                      (const bf16_t*)x_next, (const bf16_t*)s->grad, (bf16_t*)s->act,            \
                      (bf16_t*)s->plo, (bf16_t*)s->p16, (float*)s->m32, (float*)s->v32,          \
                      (const TrialHP*)s->hp, flags)
-  static const int diag = [] {
-    const char* e = getenv("MOPT_B0F_DIAG");
-    return e == nullptr ? 0 : atoi(e);
-  }();
   if (s->opt == kAdamW) MOPT_B0F(kAdamW, false);
-  else if (s->opt == kSGD16 && diag == 1) MOPT_B0F(kSGD16, true, 1);
-  else if (s->opt == kSGD16 && diag == 2) MOPT_B0F(kSGD16, false);
   else if (s->opt == kSGD16) MOPT_B0F(kSGD16, true);
   else MOPT_B0F(kSGD, true);
 #undef MOPT_B0F

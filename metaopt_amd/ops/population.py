@@ -16,7 +16,9 @@ A trial with hidden width ``w`` uses padded dims (multiples of 64) inside its re
 zero and stays zero (a zero-padded unit never receives gradient), so ragged widths cost only their
 own padded FLOPs.  Each layer is one launch over a work list of (trial-layer, tile) items: the
 forward (K1, K7), fused softmax-CE (K4) and the fused backward + SGD/AdamW update (K2, K5, K6)
-kernels of ``csrc/pop_mlp.hip``.
+kernels of ``csrc/pop_mlp.hip``.  Inside an interval (``train_steps``) the first layer's
+backward + update of step t and its forward of step t + 1 run as one kernel
+(``mlp_bwd0_fwd_kernel``: one pass over the largest weight matrix instead of two).
 
 Backends: ``"hip"`` (gfx950 kernels, the only GPU path; never falls back silently) and
 ``"torch"`` (the fp32 reference of :mod:`metaopt_amd.ops.reference`, used on CPU-only hosts).
