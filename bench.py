@@ -194,6 +194,9 @@ def run_rank(args) -> None:
                         "(validation, C1 all-gather, decide, C5 broadcast, member init/resume)",
                 "backend": pop.backend,
                 "stream_groups": pop.n_streams,
+                # each step's first-layer backward + update fused with the next step's
+                # first-layer forward (bit-identical to separate launches; MOPT_FUSE0=0 off)
+                "fused_first_layer": bool(getattr(pop, "fuse_first_layer", False)),
                 "optimizer_state": f"f32 master weights + bf16 copy, {args.momentum_dtype} "
                                    "SGD momentum",
                 "comm_backend": comm.backend or "none",
