@@ -710,7 +710,9 @@ template <int CI, int CO, int MODE, int S, int ADD = 0, int BNIN = 0, int BNB = 
 int launch_fwd(const void* x, const void* w, void* y, void* sums, int P, int Bn, int H,
                hipStream_t st, const void* addend = nullptr, int addend_c = 0,
                const BnIn& bn = BnIn{}) {
-  constexpr int NPX = npx_for(CO);
+  // (the stride-2 data gradient of a 64-channel dy: 128-pixel bands -- at 256 its 18 weight
+  //  fragments and 8 accumulator fragments per wave held one workgroup per CU, 0.7 TB/s)
+  constexpr int NPX = (MODE == kDgrad2 && CI >= 32) ? 128 : npx_for(CO);
   Geom g{};
   // (64-wide outputs: half the workgroups, twice the bands each -- their weight prologue is long)
   if (!make_geom(g, Bn, H, MODE == kDgrad2 ? 2 : S, NPX, CO >= 64 ? 512 : 1024, P, MODE))
