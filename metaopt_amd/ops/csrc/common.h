@@ -63,8 +63,13 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return __builtin_bit_cast(bf16_t, b);
 }
 
+// two floats -> packed bf16x2 (RNE) in ONE v_cvt_pk_bf16_f32 with both sources: the scalar form
+// (two converts, a shift and an OR -- hipcc does not merge them) cost 3 extra VALU per pair in
+// every epilogue and softmax pack (round 5)
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pack2bf(float a, float b) {
-  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){a, b}, bf16x2_t));
 }
 
 // Split f32 master weights: hi = the bf16 working copy (round to nearest, ties toward the
