@@ -226,27 +226,30 @@ __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnFwdWaves) void attn_fwd_k
     }
     f32x4 st[4];
     scores_T<true>(Ks, qf, li, g, st);
+    // the row max on the raw scores (c > 0: max(s) c = max(s c)), the scale folded into the
+    // exponent's fma -- 16 multiplies per key block less
     float mx = -INFINITY;
+    if (kb == qb) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kb * BKV + 32 * (j >> 1) + 8 * g + 4 * (j & 1) + r;
+          if (key > qrow) st[j][r] = -INFINITY;
+        }
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float v = st[j][r] * c;
-        if (kb == qb) {
-          const int key = kb * BKV + 32 * (j >> 1) + 8 * g + 4 * (j & 1) + r;
-          if (key > qrow) v = -INFINITY;
-        }
-        st[j][r] = v;
-        mx = fmaxf(mx, v);
-      }
-    const float m_new = fmaxf(m, max4(mx));
+      for (int r = 0; r < 4; ++r) mx = fmaxf(mx, st[j][r]);
+    const float m_new = fmaxf(m, max4(mx) * c);
     const float alpha = fast_exp2(m - m_new);
     float ls = 0.f;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = fast_exp2(st[j][r] - m_new);
+        const float p = fast_exp2(fmaf(st[j][r], c, -m_new));
         st[j][r] = p;
         ls += p;
       }
