@@ -671,6 +671,16 @@ int ilog2i(int v) {
 }
 
 constexpr int npx_for(int co) { return co >= 64 ? 128 : 256; }
+// persistent weight-gradient workgroups in all: ResNet-20 (32 trials) at 512 / 768 / 1024 / 2048
+// / 4096: 5.75 / 5.58 / 5.52 / 5.60 / 5.66 ms per step (fewer workgroups: fewer f32 partials for
+// the reduce to read; too few: bands no longer hide each other's loads); profiles/r5/conv_blocks
+#ifndef MOPT_WGRAD_BLOCKS
+#define MOPT_WGRAD_BLOCKS 1024
+#endif
+// forward / data-gradient workgroups in all (64-wide outputs: half); 512 / 2048: 5.73 / 5.67 ms
+#ifndef MOPT_FWD_BLOCKS
+#define MOPT_FWD_BLOCKS 1024
+#endif
 // weight gradient: halo and dy tile live together, so wide outputs take half bands
 constexpr int npx_wgrad(int co) { return co >= 32 ? 128 : 256; }
 
@@ -715,7 +725,7 @@ int launch_fwd(const void* x, const void* w, void* y, void* sums, int P, int Bn,
   constexpr int NPX = (MODE == kDgrad2 && CI >= 32) ? 128 : npx_for(CO);
   Geom g{};
   // (64-wide outputs: half the workgroups, twice the bands each -- their weight prologue is long)
-  if (!make_geom(g, Bn, H, MODE == kDgrad2 ? 2 : S, NPX, CO >= 64 ? 512 : 1024, P, MODE))
+  if (!make_geom(g, Bn, H, MODE == kDgrad2 ? 2 : S, NPX, CO >= 64 ? MOPT_FWD_BLOCKS / 2 : MOPT_FWD_BLOCKS, P, MODE))
     return (int)hipErrorInvalidValue;
   const size_t hb = halo_bytes<CI, S>(g), ob = (size_t)NPX * (CO + 8) * 2;
   const size_t tab = BNIN ? (size_t)2 * CI * sizeof(float) : 0;
@@ -738,13 +748,13 @@ template <int CI, int CO, int S, int BNIN = 0>
 int launch_wgrad(const void* x, const void* dy, void* dw, void* part, int P, int Bn, int H,
                  hipStream_t st, int* nb_out, const BnIn& bn = BnIn{}) {
   constexpr int NPX = npx_wgrad(CO);
-  // persistent workgroups per trial: ~2048 in all (latency hiding: a workgroup does not overlap
-  // its band loads with its MFMAs), <= 64 MB of f32 partials, >= 4 bands each
+  // persistent workgroups per trial: MOPT_WGRAD_BLOCKS in all, <= 64 MB of f32 partials, >= 4
+  // bands each
   constexpr int64_t kPartBytes = 64 << 20;
   const int64_t per = (int64_t)P * 9 * CI * CO * 4;
   const int by_bytes = (int)(kPartBytes / per > 0 ? kPartBytes / per : 1);
   Geom g{};
-  if (!make_geom(g, Bn, H, S, NPX, 2048, P, kFwd)) return (int)hipErrorInvalidValue;
+  if (!make_geom(g, Bn, H, S, NPX, MOPT_WGRAD_BLOCKS, P, kFwd)) return (int)hipErrorInvalidValue;
   g.nb = min(g.nb, max(1, min(by_bytes, g.tiles / 4)));
   if (nb_out != nullptr) {  // size query
     *nb_out = g.nb;
