@@ -307,11 +307,15 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
   }
 }
 
-// rows per block (per trial): ~2048 blocks over the population, a multiple of the row groups
-// times the unroll
+// rows per block (per trial): ~MOPT_BN_BLOCKS blocks over the population, a multiple of the row
+// groups times the unroll (ResNet-20 at 1024 / 2048 / 4096 / 8192 blocks: 5.56 / 5.49 / 5.46 /
+// 5.46 ms per step, profiles/r5/conv_blocks)
+#ifndef MOPT_BN_BLOCKS
+#define MOPT_BN_BLOCKS 4096
+#endif
 inline int reduce_rows(int P, int64_t M, int C) {
   const int ng = UNROLL * (256 / (C / 8));
-  int64_t rpb = ((int64_t)P * M + 2047) / 2048;
+  int64_t rpb = ((int64_t)P * M + MOPT_BN_BLOCKS - 1) / MOPT_BN_BLOCKS;
   rpb = (rpb + ng - 1) / ng * ng;
   return (int)(rpb > ng ? rpb : ng);
 }
