@@ -184,8 +184,18 @@ __device__ __forceinline__ void scores_T(const bf16_t* Ks, const bf16x8 (&qf)[2]
     }
 }
 
-// Forward: O = softmax(QK^T * scale, causal) V.   grid (T/64, BH), 256 threads.
-__global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnFwdWaves) void attn_fwd_kernel(const bf16_t* __restrict__ Q,
+// Forward: O = softmax(QK^T * scale, causal) V.   1-D grid of (T / 64 / NQB) * BH workgroups of
+// NQB 64-query blocks (256 NQB threads, 16 queries per wave) sharing each staged K / V tile: with
+// NQB = 2 the threads of the first block load the K tile, those of the second the V tile, and the
+// first block's waves skip the multiply of the last key block (past their diagonal).  Measured
+// (round 5, profiles/r5/attn_qb2/, 3 interleaved runs): NQB = 2 95-99 us per call against 90-95
+// for NQB = 1 (LM-125M 38.4-38.9 vs 38.4-38.5 ms) -- half the K / V staging per query does not pay
+// for the 8-wave barriers and the idle diagonal block; NQB = 1 stays the default.
+#ifndef MOPT_ATTN_FWD_QB
+#define MOPT_ATTN_FWD_QB 1
+#endif
+template <int NQB>
+__global__ __launch_bounds__(256 * NQB) MOPT_WAVES_ATTR(kAttnFwdWaves) void attn_fwd_kernel(const bf16_t* __restrict__ Q,
                                                        const bf16_t* __restrict__ K,
                                                        const bf16_t* __restrict__ V,
                                                        bf16_t* __restrict__ O,
@@ -193,14 +203,20 @@ __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnFwdWaves) void attn_fwd_k
                                                        float c, int n_bh) {
   __shared__ __attribute__((aligned(16))) bf16_t Ks[tile_elems<true>()];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[tile_elems<true>()];
-  const int nqb = T / BQ;
-  const int2 hb = head_block(nqb, n_bh);
-  const int qb = nqb - 1 - hb.x;                      // longest (most key blocks) first
+  const int nblk = T / (BQ * NQB);
+  const int2 hb = head_block(nblk, n_bh);
+  const int qb0 = (nblk - 1 - hb.x) * NQB;            // longest (most key blocks) first
+  const int qb_last = qb0 + NQB - 1;
   const int bh = hb.y;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, g = lane >> 4, q = li >> 2, pp = li & 3;
   const size_t base = (size_t)bh * T * D;
-  const int qrow = qb * BQ + wave * 16 + li;            // this lane's query
+  const int qb = qb0 + (wave >> 2);                    // this wave's query block
+  const int qrow = qb * BQ + (wave & 3) * 16 + li;     // this lane's query
+  // NQB = 2: waves 0-3 stage K, waves 4-7 V (wave-uniform pointers)
+  const bf16_t* kvsrc = (NQB == 1 || tid < 256) ? K + base : V + base;
+  bf16_t* kvdst = (NQB == 1 || tid < 256) ? Ks : Vs;
+  const int ltid = tid & 255;
 
   bf16x8 qf[2];
 #pragma unroll
@@ -212,18 +228,19 @@ __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnFwdWaves) void attn_fwd_k
   float m = -INFINITY, l = 0.f;
 
   uint4 ka, kc, va, vc;   // key block kb + 1, fetched while block kb is multiplied
-  tile_load(K + base, ka, kc, tid);
-  tile_load(V + base, va, vc, tid);
-  for (int kb = 0; kb <= qb; ++kb) {
+  tile_load(kvsrc, ka, kc, ltid);
+  if (NQB == 1) tile_load(V + base, va, vc, tid);
+  for (int kb = 0; kb <= qb_last; ++kb) {
     __syncthreads();
-    tile_store<true>(ka, kc, Ks, tid);
-    tile_store<true>(va, vc, Vs, tid);
+    tile_store<true>(ka, kc, kvdst, ltid);
+    if (NQB == 1) tile_store<true>(va, vc, Vs, tid);
     __syncthreads();
     {
-      const size_t nb = (size_t)min(kb + 1, qb) * BKV * D;   // clamped: no branch around loads
-      tile_load(K + base + nb, ka, kc, tid);
-      tile_load(V + base + nb, va, vc, tid);
+      const size_t nb = (size_t)min(kb + 1, qb_last) * BKV * D;   // clamped: no branch around loads
+      tile_load(kvsrc + nb, ka, kc, ltid);
+      if (NQB == 1) tile_load(V + base + nb, va, vc, tid);
     }
+    if (NQB > 1 && kb > qb) continue;                  // wave-uniform: past this wave's diagonal
     f32x4 st[4];
     scores_T<true>(Ks, qf, li, g, st);
     // the row max on the raw scores (c > 0: max(s) c = max(s c)), the scale folded into the
@@ -498,9 +515,15 @@ int mopt_attn_fwd(const void* q, const void* k, const void* v, void* o, void* ls
                   int H, float scale, void* stream) {
   if (T % 64 || bh <= 0) return 1;
   const float c = scale * 1.4426950408889634f;
-  hipLaunchKernelGGL(attn_fwd_kernel, dim3((T / 64) * bh), dim3(256), 0, (hipStream_t)stream,
-                     (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o,
-                     (float*)lse2, T, H, c, bh);
+  constexpr int NQB = MOPT_ATTN_FWD_QB;
+  if (NQB > 1 && T % (64 * NQB) == 0)
+    hipLaunchKernelGGL(attn_fwd_kernel<NQB>, dim3((T / (64 * NQB)) * bh), dim3(256 * NQB), 0,
+                       (hipStream_t)stream, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
+                       (bf16_t*)o, (float*)lse2, T, H, c, bh);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel<1>, dim3((T / 64) * bh), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o,
+                       (float*)lse2, T, H, c, bh);
   return (int)hipGetLastError();
 }
 
