@@ -20,7 +20,7 @@ from . import build as _build
 
 _LOCK = threading.Lock()
 _LIB = None
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 c_void_p = ctypes.c_void_p
 c_int = ctypes.c_int
@@ -41,6 +41,8 @@ _SIGNATURES = {
     "mopt_mlp_w_layout": ([], c_int),
     "mopt_mlp_steps": ([c_void_p, c_void_p, c_void_p, c_int, c_void_p], c_int),
     "mopt_mlp_bwd0_fwd": ([c_void_p, c_void_p, c_void_p, c_void_p], c_int),
+    "mopt_mlp_steps_range": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
+                             c_int),
 }
 
 _OPTIONAL_SIGNATURES: dict = {}

@@ -1262,7 +1262,7 @@ static void launch_bwd_rows(int n_work, int n_rowblocks, hipStream_t stream, con
 // ------------------------------------------------------------------------------------------------
 extern "C" {
 
-int mopt_abi_version() { return 14; }
+int mopt_abi_version() { return 15; }
 
 // weight layout: 1 = k-strip-major [K/64][N][64] (the only layout)
 int mopt_mlp_w_layout() { return 1; }
@@ -1434,6 +1434,25 @@ int mopt_mlp_steps(const MlpStep* s, const void* const* xs, const void* const* y
   // loss layer; the last step of the call keeps the unfused backward (no next batch)
   const bool fuse = s != nullptr && s->fuse0 && s->rb == 1 && s->L >= 2 && s->n_bwd0f > 0;
   for (int i = 0; i < n; ++i) {
+    const void* xn = (fuse && i + 1 < n) ? xs[i + 1] : nullptr;
+    const int err = mlp_step(s, xs[i], ys[i], fuse && i > 0, xn, stream);
+    if (err) return err;
+  }
+  return 0;
+}
+
+// Steps i0 .. i0 + count - 1 of an n-step interval (xs / ys hold all n batches): the sweep queues
+// its trial groups' intervals round-robin in short runs of steps, so every group's stream has
+// work from the interval's first microsecond to its last (one group's whole interval queued
+// before the next group's left the first group running alone at the start and the last one at
+// the end).  The fused first layer spans the runs: step i fuses with batch xs[i + 1] whenever
+// i + 1 < n, exactly as one mopt_mlp_steps call over the n steps.
+int mopt_mlp_steps_range(const MlpStep* s, const void* const* xs, const void* const* ys, int i0,
+                         int n, int count, void* stream) {
+  if (i0 < 0 || count < 0 || i0 + count > n || (count > 0 && (xs == nullptr || ys == nullptr)))
+    return (int)hipErrorInvalidValue;
+  const bool fuse = s != nullptr && s->fuse0 && s->rb == 1 && s->L >= 2 && s->n_bwd0f > 0;
+  for (int i = i0; i < i0 + count; ++i) {
     const void* xn = (fuse && i + 1 < n) ? xs[i + 1] : nullptr;
     const int err = mlp_step(s, xs[i], ys[i], fuse && i > 0, xn, stream);
     if (err) return err;

@@ -285,6 +285,9 @@ class PopulationMLP:
         # over W0 instead of two; bit-identical results).  MOPT_FUSE0=0 keeps the separate
         # launches (the A/B and the equality test).
         self.fuse_first_layer = os.environ.get("MOPT_FUSE0", "1") != "0"
+        # train_steps queues the groups' steps round-robin, this many at a time (0: each group's
+        # whole interval in turn -- the groups then start and finish one after the other)
+        self.step_chunk = int(os.environ.get("MOPT_STEP_CHUNK", "4"))
         self._side_streams: list = []
         self._events: list = []
         self._parts: list = []
@@ -1054,13 +1057,19 @@ class PopulationMLP:
                     side.wait_event(ev)
                 self._fork_needed = False
             self._side_pending = True
-        for i, part in enumerate(parts):
-            stream = main if i == 0 else self._side_streams[i - 1]
-            check(lib.mopt_mlp_steps(part["step_ptr"], xs.ctypes.data, ys.ctypes.data, n,
-                                     stream.cuda_stream), "mlp_steps")
-            if i > 0:   # the temporaries are freed on return: not before the side stream read them
-                for t in keep:
-                    t.record_stream(stream)
+        streams = [main if i == 0 else self._side_streams[i - 1] for i in range(len(parts))]
+        chunk = self.step_chunk if len(parts) > 1 and self.step_chunk > 0 else n
+        # the groups' steps are queued round-robin, ``chunk`` at a time: all streams busy from
+        # the interval's start to its end (mopt_mlp_steps_range keeps the fused first layer
+        # across the runs)
+        for c0 in range(0, n, chunk):
+            cnt = min(chunk, n - c0)
+            for part, stream in zip(parts, streams):
+                check(lib.mopt_mlp_steps_range(part["step_ptr"], xs.ctypes.data, ys.ctypes.data,
+                                               c0, n, cnt, stream.cuda_stream), "mlp_steps")
+        for stream in streams[1:]:  # temporaries are freed on return: not before a side stream
+            for t in keep:          # read them
+                t.record_stream(stream)
 
     def _train_step_hip(self, x, y) -> None:
         from ._lib import check

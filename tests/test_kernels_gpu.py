@@ -360,7 +360,9 @@ def test_per_member_batch_trajectory_and_eval(data384):
 def test_fused_first_layer_equals_separate_launches(data, optimizer, n_hidden, streams):
     """``train_steps`` fuses each step's first-layer backward + update with the next step's
     first-layer forward (csrc/pop_mlp.hip mlp_bwd0_fwd_kernel): weights, optimizer state and
-    losses equal the separate launches bit for bit, across two intervals, with dropout members."""
+    losses equal the separate launches bit for bit, across two intervals, with dropout members.
+    The fused population queues its groups' steps round-robin one at a time (every step a run
+    boundary of mopt_mlp_steps_range), the reference each group's interval in one call."""
     kw = {}
     if optimizer == "sgd-bf16m":
         optimizer, kw = "sgd", {"momentum_dtype": "bf16"}
@@ -373,6 +375,7 @@ def test_fused_first_layer_equals_separate_launches(data, optimizer, n_hidden, s
                           optimizer=optimizer, device="cuda", backend="hip", n_streams=streams,
                           **kw)
         p.fuse_first_layer = fuse
+        p.step_chunk = 1 if fuse else 0
         for i, c in enumerate(cfgs):
             p.set_member(i + 1, c)
         pops.append(p)
