@@ -79,18 +79,24 @@ def test_two_concurrent_workers(db_env):
 
 @pytest.mark.xdist_group("timing")   # `-n N --dist loadgroup`: never beside other timing tests
 def test_thirty_trials_within_ten_seconds(db_env):
-    """The reference's CI bound (10 s for 30 trials on an idle VM).  The bound scales with the
-    machine's load over the run (loadavg / CPUs, at least 1), so a parallel test session that
-    oversubscribes the CPUs does not fail a test that measures wall time."""
+    """The reference's CI bound (10 s for 30 trials on an idle VM).  The bound scales with how
+    busy the machine was during the run, so a parallel test session that oversubscribes the CPUs
+    does not fail a test that measures wall time: by the 1-minute load average (lags a session
+    that just started) and by the mean CPU utilisation over the run itself (psutil; the hunt
+    keeps about one CPU busy, so above half the CPUs busy the others competed with it)."""
+    import psutil
     load0 = os.getloadavg()[0]
+    psutil.cpu_percent(interval=None)          # starts the utilisation window
     t0 = time.perf_counter()
     p = _hunt_process("-n", "quick", "--max-trials", "30", "./black_box.py",
                       "-x~uniform(-50, 50)")
     _, err = p.communicate(timeout=120)
     elapsed = time.perf_counter() - t0
+    util = psutil.cpu_percent(interval=None) / 100.0
     assert p.returncode == 0, err.decode()[-2000:]
     busy = max(load0, os.getloadavg()[0]) / (os.cpu_count() or 1)
-    assert elapsed < 10.0 * max(1.0, busy), (elapsed, busy)
+    scale = max(1.0, busy, 2.0 * util)
+    assert elapsed < 10.0 * scale, (elapsed, busy, util)
     _, trials = _trials("quick")
     assert Counter(t.status for t in trials)["completed"] == 30
 
