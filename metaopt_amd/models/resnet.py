@@ -177,23 +177,42 @@ class _GradScale(torch.autograd.Function):
 
 
 class SyntheticCIFAR:
-    """CIFAR-shaped synthetic classification: N(0, 1) 32x32x3 images (NHWC, padded to 8
-    channels, bf16) labelled by a fixed random two-layer teacher on 4x4-pooled pixels."""
+    """CIFAR-shaped synthetic classification that ResNet-20 can learn: each 32x32x3 image (NHWC,
+    padded to 8 channels, bf16) is a texture -- N(0, 1) noise filtered by its class's fixed
+    random 3x3 colour filter -- mixed with a weaker texture of another class (a distractor)
+    and white noise.  The class is a translation-invariant property of the image (its local
+    colour / spatial correlations), which a conv net with a global average pool reads at every
+    position.  Round 6: the former teacher on position-specific 4x4-pooled pixels was nearly
+    unlearnable through the final global pool (the best of 224 trials reached 2.145 nats against
+    H(y) = 2.286), which left TPE-vs-random comparisons at noise level.  ``mix`` = (class,
+    distractor, white) amplitudes sets the difficulty."""
 
     def __init__(self, n_train: int = 50048, n_val: int = 1024, batch_size: int = 128,
-                 seed: int = 0, device=None, image_size: int = 32):
+                 seed: int = 0, device=None, image_size: int = 32,
+                 mix: tuple = (1.0, 0.7, 0.5)):
         g = torch.Generator().manual_seed(seed)
         S = image_size
-        w1 = torch.randn(3 * (S // 4) ** 2, 256, generator=g) / math.sqrt(3 * (S // 4) ** 2)
-        w2 = torch.randn(256, NCLS, generator=g) / 16.0
+        filt = torch.randn(NCLS, 3, 3, 3, 3, generator=g)          # [class][out][in][3][3]
+        filt = filt / filt.flatten(2).norm(dim=2).view(NCLS, 3, 1, 1, 1)
         dev = torch.device(device) if device is not None else torch.device("cpu")
+        a, b, c = mix
+
+        def texture(cls, n):
+            z = torch.randn(n, 3, S, S, generator=g)
+            out = torch.empty(n, 3, S, S)
+            for k in range(NCLS):   # one grouped conv per class
+                idx = (cls == k).nonzero().flatten()
+                if len(idx):
+                    out[idx] = torch.nn.functional.conv2d(z[idx], filt[k], padding=1)
+            return out
 
         def draw(n):
-            x = torch.randn(n, S, S, 3, generator=g)
-            pooled = x.view(n, S // 4, 4, S // 4, 4, 3).mean((2, 4)).reshape(n, -1)
-            y = (torch.tanh(pooled @ w1 * 4) @ w2).argmax(1)
+            y = torch.randint(0, NCLS, (n,), generator=g)
+            other = (y + torch.randint(1, NCLS, (n,), generator=g)) % NCLS
+            x = a * texture(y, n) + b * texture(other, n) + \
+                c * torch.randn(n, 3, S, S, generator=g)
             xp = torch.zeros(n, S, S, IN_CH)
-            xp[..., :3] = x
+            xp[..., :3] = x.permute(0, 2, 3, 1)
             return xp.to(torch.bfloat16).to(dev), y.to(dev)
 
         self.batch_size = batch_size

@@ -609,6 +609,308 @@ __global__ __launch_bounds__(512) void pgemm_big_kernel(const GemmArgs g) {
   }
 }
 
+// ----------------------------------------------------------------------------------------------
+// Phased 256 x 256 GEMM (cfg 12; round 6).  Same operand images, swizzles, persistent tile walk
+// and epilogues as pgemm_big_kernel, but the K loop is cut into phases whose LDS-DMA fills stay
+// in flight across the barriers (a counted vmcnt, never 0 in the loop) and whose fragment reads
+// are issued before the barrier that precedes their MFMAs:
+//
+//   * the 256 x 64 A and B images of a K-tile are split into half-tiles of 128 rows (A0, A1 =
+//     tile rows 0-127 / 128-255, B0, B1 = tile columns 0-127 / 128-255), 16 KB each, two LDS
+//     buffers of four half-tiles (128 KB);
+//   * wave (wm, wn) of the 2 x 4 waves owns rows {wm 64 + 0..63} of BOTH A halves and columns
+//     {wn 32 + 0..31} of BOTH B halves, so each quarter of its 128 x 64 output (quadrant (mh, nh))
+//     reads exactly one A half and one B half;
+//   * one K-tile = 4 phases, one quadrant (16 MFMAs) each, in the order (A0,B0) (A0,B1) (A1,B1)
+//     (A1,B0); A fragments are read at phases 1 and 3, B fragments at phases 2 and 4 into the
+//     register set the NEXT phase pair uses -- phase 4 reads the next K-tile's B0 -- so two B
+//     register sets alternate and two K-tiles make one loop iteration (8 phases);
+//   * every phase issues one half-tile fill (2 x 1 KB LDS-DMA per lane) into a slot whose last
+//     reads are two phases old -- phase 1: A1 of K-tile g+1, 2: B0 of g+2, 3: A0 of g+2, 4: B1 of
+//     g+2 -- and waits vmcnt(8): the fill of four phases ago has landed (four half-tiles stay in
+//     flight, ~2k SIMD cycles); it is read at the earliest one phase after that wait;
+//   * phase = [fragment reads] [fill] [vmcnt] s_barrier lgkmcnt(0) [16 MFMA] s_barrier, and the
+//     waves of row wm = 1 run one barrier behind those of wm = 0 (one extra barrier at the start,
+//     wm = 0 one at the end): waves w and w + 4 share a SIMD, so one of them multiplies while the
+//     other reads and fills.  With that offset a slot may be refilled two phases after its last
+//     read (both rows' reads retired) and read one phase after its retiring wait -- the schedule
+//     above keeps two phases of slack on the reads.
+// The fills run through the persistent tile walk (the next tile's first K-tiles fill during the
+// current tile's last ones).  Epilogue stores sit in the same vmcnt queue: the four phases after
+// an epilogue wait vmcnt(8 + S) (S = the epilogue's store instructions per lane, a lower bound),
+// and once no fills remain the waits are vmcnt(0).  Preconditions as pgemm_big_kernel, plus
+// k_per_split a multiple of 128 (an even number of K-tiles).
+// ----------------------------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ void ph_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void ph_barrier() { asm volatile("s_barrier" ::: "memory"); }
+__device__ __forceinline__ void ph_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+template <int S>
+__device__ __forceinline__ void ph_wait(int mode) {  // 0 steady, 1 after an epilogue, 2 drain
+  if (mode == 0) ph_vmcnt<8>();
+  else if (mode == 1) ph_vmcnt<8 + S>();
+  else ph_vmcnt<0>();
+}
+
+// Epilogue of one 256 x 256 tile of pgemm_ph_kernel (then the accumulators are zeroed): lane
+// (li, gq) of wave (wm, wn) holds, in acc[mh][nh][i][j], C[m][n .. n + 3] with m = m0 + 128 mh +
+// 64 wm + 16 i + li and n = n0 + 128 nh + 32 wn + 16 j + 4 gq -- pgemm_big_kernel's fragment
+// layout (C^T fragments), so its store paths carry over with these row / column origins.
+template <int EPI>
+__device__ __forceinline__ void pgemm_ph_epilogue(const GemmArgs& g, f32x4 (&acc)[2][2][4][2],
+                                                  int p, int m0, int n0, int k0, int wm, int wn,
+                                                  int li, int gq) {
+  if (g.part != nullptr) {  // K-split partial: f32 [splits][P][M][N]
+    const int64_t total = (int64_t)g.P * g.M * g.N;
+    float* part = g.part + (k0 / g.k_per_split) * total + (int64_t)p * g.M * g.N;
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+      for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int m = m0 + 128 * mh + 64 * wm + 16 * i + li;
+            const int n = n0 + 128 * nh + 32 * wn + 16 * j + 4 * gq;
+            *(f32x4*)(part + (int64_t)m * g.N + n) = acc[mh][nh][i][j];
+          }
+  } else if constexpr (EPI == 3) {  // QKV + RoPE into [3][B'][H][T][64] (pgemm_big_kernel)
+    const int dm = g.nH * 64;
+    const int64_t sec_stride = (int64_t)g.P * g.M * dm;
+    const int bper = g.M / g.T;
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + 128 * mh + 64 * wm + 16 * i + li;
+        const int bl = m / g.T, t = m - bl * g.T;
+        const int64_t bq = (int64_t)p * bper + bl;
+#pragma unroll
+        for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int n = n0 + 128 * nh + 32 * wn + 16 * j + 4 * gq;
+            const int sec = n / dm, hc = n - sec * dm, hh = hc >> 6, c = hc & 63;
+            float x[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) x[r] = bf2f(f2bf(acc[mh][nh][i][j][r]));
+            if (sec < 2) {
+              const float* cs = g.cosT + (int64_t)t * 32 + (c >> 1);
+              const float* sn = g.sinT + (int64_t)t * 32 + (c >> 1);
+#pragma unroll
+              for (int q2 = 0; q2 < 2; ++q2) {
+                const float a = x[2 * q2], b = x[2 * q2 + 1], co = cs[q2], si = sn[q2];
+                x[2 * q2] = a * co - b * si;
+                x[2 * q2 + 1] = b * co + a * si;
+              }
+            }
+            bf16_t* o = g.C + sec * sec_stride + ((bq * g.nH + hh) * g.T + t) * 64 + c;
+            *(uint2*)o = make_uint2(pack2bf(x[0], x[1]), pack2bf(x[2], x[3]));
+          }
+      }
+  } else {
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+      for (int nh = 0; nh < 2; ++nh) {
+        const int mr = m0 + 128 * mh + 64 * wm + li;   // row of fragment i = 0
+        const int nc = n0 + 128 * nh + 32 * wn;        // first column of the j = 0, 1 pair
+        if constexpr (EPI == 1) {  // SwiGLU: j = 0 gate, j = 1 up -> 16 columns of h
+          bf16_t* Hp = g.H + p * g.sX + (int64_t)mr * g.ldx + nc / 2 + 4 * gq;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float hv[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              hv[r] = silu_f(bf2f(f2bf(acc[mh][nh][i][0][r]))) * bf2f(f2bf(acc[mh][nh][i][1][r]));
+            *(uint2*)(Hp + (int64_t)(16 * i) * g.ldx) =
+                make_uint2(pack2bf(hv[0], hv[1]), pack2bf(hv[2], hv[3]));
+          }
+        }
+        // 4 columns per fragment packed, rows gq = 0|1 (2|3) exchanged by v_permlane16_swap:
+        // 8 consecutive columns of one row per lane, one 16-byte store per fragment pair
+        bf16_t* C = g.C + p * g.sC + (int64_t)mr * g.ldc + nc + 16 * (gq & 1) + 8 * (gq >> 1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          uint32_t x0 = pack2bf(acc[mh][nh][i][0][0], acc[mh][nh][i][0][1]);
+          uint32_t x1 = pack2bf(acc[mh][nh][i][0][2], acc[mh][nh][i][0][3]);
+          uint32_t y0 = pack2bf(acc[mh][nh][i][1][0], acc[mh][nh][i][1][1]);
+          uint32_t y1 = pack2bf(acc[mh][nh][i][1][2], acc[mh][nh][i][1][3]);
+          const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+          *(uint4*)(C + (int64_t)(16 * i) * g.ldc) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+        }
+      }
+  }
+#pragma unroll
+  for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+    for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[mh][nh][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+template <bool TA, bool TB, int EPI = 0>
+__global__ __launch_bounds__(512) void pgemm_ph_kernel(const GemmArgs g) {
+  constexpr int H = 128;                          // rows of a half-tile
+  using IA = GImg<H, !TA>;
+  using IB = GImg<H, TB>;
+  constexpr int SL = H * BK;                      // elements of one half-tile image (16 KB)
+  // slot s of buffer b at smem + (2 s + b) SL: s = 0 A0, 1 A1, 2 B0, 3 B1 (both buffers of an
+  // operand within 64 KB of its first slot: every fragment read of the kernel is a base
+  // register + a 16-bit immediate offset)
+  __shared__ __attribute__((aligned(1024))) bf16_t smem[8 * SL];  // the only __shared__ object
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int li = lane & 15, gq = lane >> 4, q = li >> 2, pp = li & 3;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int nk = g.k_per_split / BK;              // >= 2 (host check)
+
+  auto decode = [&](int v, int& p, int& m0, int& n0, int& k0) {
+    const int t = xcd_remap(v, g.nwg);
+    const int per = g.tiles_m * g.tiles_n;
+    const int pq = t / per;
+    p = pq / g.splits;
+    k0 = (pq - p * g.splits) * g.k_per_split;
+    const int idx = t - pq * per, span = kGroupM * g.tiles_n;
+    const int grp = idx / span, in = idx - grp * span;
+    const int gm = min(kGroupM, g.tiles_m - grp * kGroupM);
+    m0 = (grp * kGroupM + in % gm) * 256;
+    n0 = (in / gm) * 256;
+  };
+  int vb = blockIdx.x;
+  int p, m0, n0, k0;
+  decode(vb, p, m0, n0, k0);
+  int vn = vb + (int)gridDim.x;
+  bool has_next = vn < g.nwg;
+  int np = 0, nm0 = 0, nn0 = 0, nk0 = 0;
+  if (has_next) decode(vn, np, nm0, nn0, nk0);
+
+  // fill slot s of buffer b with K-tile kt of the current (nx = false) or next tile
+  auto fill = [&](int s, int b, bool nx, int kt) {
+    const int fp = nx ? np : p, fm = nx ? nm0 : m0, fn = nx ? nn0 : n0;
+    const int fk = (nx ? nk0 : k0) + kt * BK;
+    bf16_t* img = smem + (2 * s + b) * SL;
+    if (s < 2) IA::fill(g.a.ptr + fp * g.a.batch, g.a.ld, fm + s * H, fk, img, wave, lane);
+    else IB::fill(g.b.ptr + fp * g.b.batch, g.b.ld, fn + (s - 2) * H, fk, img, wave, lane);
+  };
+  // the K-tile d ahead of kt: (exists, in the next tile, its k index)
+  auto ahead = [&](int kt, int d, bool& nx, int& kk) {
+    kk = kt + d;
+    nx = kk >= nk;
+    if (nx) kk -= nk;
+    return !nx || has_next;
+  };
+
+  const int S = g.part != nullptr ? 32 : (EPI == 0 ? 16 : 32);  // epilogue stores per lane
+
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int a0 = 0; a0 < 2; ++a0)
+#pragma unroll
+    for (int a1 = 0; a1 < 2; ++a1)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a0][a1][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 fa[2][4], bx[2][2], by[2][2];  // A fragments [k-sub][i], two B sets [k-sub][j]
+
+  // prologue: the fills a steady state would have issued before K-tile 0's first phase --
+  // B0(0) A0(0) B1(0) A1(0) B0(1) A0(1) B1(1) -- the first three retired, B0(0) read into bx
+  fill(2, 0, false, 0);
+  fill(0, 0, false, 0);
+  fill(3, 0, false, 0);
+  fill(1, 0, false, 0);
+  fill(2, 1, false, 1);
+  fill(0, 1, false, 1);
+  fill(3, 1, false, 1);
+  ph_vmcnt<8>();
+  ph_barrier();
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      bx[ks][j] = IB::frag(smem + 4 * SL, wn * 32 + 16 * j, ks, li, gq, q, pp);
+  if (wm == 1) ph_barrier();                     // row 1 runs one barrier behind
+
+  int kt = 0;
+  int post = 0;                                   // phases left that follow an epilogue
+
+#define PH_READ_A(BUF, HALF)                                                                   \
+  _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                             \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i)                                              \
+      fa[ks][i] = IA::frag(smem + (2 * (HALF) + (BUF)) * SL, wm * 64 + 16 * i, ks, li, gq, q, pp);
+#define PH_READ_B(BUF, HALF, BR)                                                               \
+  _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                             \
+    _Pragma("unroll") for (int j = 0; j < 2; ++j)                                              \
+      BR[ks][j] = IB::frag(smem + (2 * (2 + (HALF)) + (BUF)) * SL, wn * 32 + 16 * j, ks, li, gq, q, pp);
+#define PH_MFMA(MH, NH, BR)                                                                    \
+  _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                             \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i)                                              \
+      _Pragma("unroll") for (int j = 0; j < 2; ++j)                                            \
+        acc[MH][NH][i][j] = mfma16(BR[ks][j], fa[ks][i], acc[MH][NH][i][j]);
+  // one phase: FILL is (slot, buffer, K-tiles ahead); the wait mode follows from what is queued
+#define PH_STEP(FSLOT, FBUF, FD, MH, NH, BR)                                                   \
+  {                                                                                            \
+    bool fnx;                                                                                  \
+    int fkk;                                                                                   \
+    const bool fok = ahead(kt, FD, fnx, fkk);                                                  \
+    if (fok) fill(FSLOT, FBUF, fnx, fkk);                                                      \
+    const int mode = !fok ? 2 : (post > 0 ? 1 : 0);                                            \
+    if (S == 16) ph_wait<16>(mode); else ph_wait<32>(mode);                                    \
+    if (post > 0) --post;                                                                      \
+    ph_barrier();                                                                              \
+    ph_lgkm0();                                                                                \
+    PH_MFMA(MH, NH, BR)                                                                        \
+    ph_barrier();                                                                              \
+  }
+  // K-tile in buffer CB (its B0 already in BX): quadrants (0,0) (0,1) (1,1) (1,0); phase 4 reads
+  // the next K-tile's B0 into BY.  nk is even (host check): a tile's K-tiles start in buffer 0
+  // and its last one is an odd instance, after which the epilogue runs (one code copy)
+#define PH_KTILE(CB, BX, BY)                                                                   \
+  {                                                                                            \
+    PH_READ_A(CB, 0)                                                                           \
+    PH_STEP(1, (CB) ^ 1, 1, 0, 0, BX)                                                          \
+    PH_READ_B(CB, 1, BY)                                                                       \
+    PH_STEP(2, CB, 2, 0, 1, BY)                                                                \
+    PH_READ_A(CB, 1)                                                                           \
+    PH_STEP(0, CB, 2, 1, 1, BY)                                                                \
+    {                                                                                          \
+      bool nx1;                                                                                \
+      int kk1;                                                                                 \
+      if (ahead(kt, 1, nx1, kk1)) { PH_READ_B((CB) ^ 1, 0, BY) }                               \
+    }                                                                                          \
+    PH_STEP(3, CB, 2, 1, 0, BX)                                                                \
+  }
+  while (true) {
+    PH_KTILE(0, bx, by)
+    ++kt;
+    PH_KTILE(1, by, bx)
+    if (++kt < nk) continue;
+    pgemm_ph_epilogue<EPI>(g, acc, p, m0, n0, k0, wm, wn, li, gq);
+    if (!has_next) break;
+    vb = vn; p = np; m0 = nm0; n0 = nn0; k0 = nk0;
+    vn = vb + (int)gridDim.x;
+    has_next = vn < g.nwg;
+    if (has_next) decode(vn, np, nm0, nn0, nk0);
+    kt = 0;
+    post = 4;
+  }
+#undef PH_KTILE
+#undef PH_STEP
+#undef PH_MFMA
+#undef PH_READ_B
+#undef PH_READ_A
+  if (wm == 0) ph_barrier();                     // equal barrier counts in both rows
+}
+
 // (Round 5, two deeper-pipelined variants of this kernel, both correct on every GEMM test and
 // both removed (profiles/round5.md): a 3-stage 64-deep LDS ring at 256 x 128 / 128 x 256 (fills
 // two K-steps ahead behind counted vmcnt waits, one raw s_barrier per K-step, C stores in inline
@@ -675,10 +977,29 @@ int launch_big(GemmArgs g, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+template <bool TA, bool TB, int EPI = 0>
+int launch_ph(GemmArgs g, hipStream_t st) {
+  if (g.M % 256 || g.N % 256 || g.k_per_split % (2 * BK) || g.k_per_split < 2 * BK ||
+      (int64_t)g.k_per_split * g.splits != g.K || (g.splits > 1 && g.part == nullptr) ||
+      g.nin > 1 || (EPI != 0 && g.splits != 1) || (EPI == 1 && g.H == nullptr) ||
+      (EPI == 3 && (g.cosT == nullptr || g.T <= 0 || g.M % g.T || g.N != 3 * 64 * g.nH)))
+    return (int)hipErrorInvalidValue;
+  g.tiles_m = g.M / 256;
+  g.tiles_n = g.N / 256;
+  const int64_t nwg = (int64_t)g.P * g.splits * g.tiles_m * g.tiles_n;
+  if (nwg <= 0 || nwg > 0x7FFFFFFF) return (int)hipErrorInvalidValue;
+  g.nwg = (int)nwg;
+  constexpr int kGrid = 256;   // persistent, one workgroup per CU (128 KB of LDS)
+  const int grid = nwg < kGrid ? (int)nwg : kGrid;
+  hipLaunchKernelGGL((pgemm_ph_kernel<TA, TB, EPI>), dim3(grid), dim3(512), 0, st, g);
+  return (int)hipGetLastError();
+}
+
 template <int KA, int KB, bool TA, bool TB>
 int dispatch_tile(const GemmArgs& g, int cfg, hipStream_t st) {
   if constexpr (KA == kDense && KB == kDense) {
     switch (cfg) {
+      case 12: return launch_ph<TA, TB>(g, st);                // 256 x 256, phased
       case 5: return launch_big<TA, TB, 2, 8, 4>(g, st);  // 256 x 256
       case 6: return launch_big<TA, TB, 4, 4, 4>(g, st);  // 256 x 128
       case 7: return launch_big<TA, TB, 2, 4, 4>(g, st);  // 128 x 256
@@ -738,10 +1059,11 @@ extern "C" {
 
 // Tile of configuration ``cfg`` (rows, cols): lets the host size grids and split-K.
 int mopt_pgemm_tile(int cfg, int* bm, int* bn) {
-  static const int t[12][2] = {{128, 128}, {128, 16},  {128, 32},  {64, 64},
+  static const int t[13][2] = {{128, 128}, {128, 16},  {128, 32},  {64, 64},
                                {64, 128},  {256, 256}, {256, 128}, {128, 256},
-                               {256, 256}, {256, 256}, {256, 128}, {256, 192}};
-  if (cfg < 0 || cfg > 11) return (int)hipErrorInvalidValue;
+                               {256, 256}, {256, 256}, {256, 128}, {256, 192},
+                               {256, 256}};
+  if (cfg < 0 || cfg > 12) return (int)hipErrorInvalidValue;
   *bm = t[cfg][0];
   *bn = t[cfg][1];
   return 0;
@@ -802,6 +1124,7 @@ int mopt_pgemm_swiglu(const void* A, const void* B, void* C, void* X, int P, int
     case 6: return launch_big<false, false, 4, 4, 4, 1>(g, st);
     case 7: return launch_big<false, false, 2, 4, 4, 1>(g, st);
     case 11: return launch_big<false, false, 4, 4, 6, 1>(g, st);
+    case 12: return launch_ph<false, false, 1>(g, st);
     default: return (int)hipErrorNotSupported;
   }
 }
@@ -834,6 +1157,7 @@ int mopt_pgemm_qkv_rope(const void* A, const void* B, void* out, const void* cos
     case 6: return launch_big<false, false, 4, 4, 4, 3>(g, st);
     case 7: return launch_big<false, false, 2, 4, 4, 3>(g, st);
     case 11: return launch_big<false, false, 4, 4, 6, 3>(g, st);
+    case 12: return launch_ph<false, false, 3>(g, st);
     default: return (int)hipErrorNotSupported;
   }
 }

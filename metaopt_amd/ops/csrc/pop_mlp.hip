@@ -749,11 +749,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
           __syncthreads();                    // every wave is done with the previous block
           const bf16_t* Xr = X + (size_t)rb * BM * K + k0;
           const bf16_t* Zr = dZ + (size_t)rb * BM * N + nc;
+          // (NARROW: the CE kernel wrote dZ columns < kNarrowRows only -- the dead columns are
+          // zero-filled here, never read: the narrow backward touches no other dZ bytes)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
             *(uint4*)(Xs + BOFF(r, ch * 8)) = *(const uint4*)(Xr + (size_t)r * K + ch * 8);
-            *(uint4*)(Zs + BOFF(r, ch * 8)) = *(const uint4*)(Zr + (size_t)r * N + ch * 8);
+            *(uint4*)(Zs + BOFF(r, ch * 8)) =
+                z_live ? *(const uint4*)(Zr + (size_t)r * N + ch * 8) : make_uint4(0, 0, 0, 0);
           }
           __syncthreads();
           MOPT_BWD_DW()

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 from typing import Optional
 
 import torch
@@ -43,16 +44,24 @@ _lib.register_signatures({
 # (any shape, ragged edges); 5-7: 8-wave direct-to-LDS kernel, one workgroup per CU, for shapes
 # the tile divides (M % BM == N % BN == K % 64 == 0)
 TILES = {0: (128, 128), 1: (128, 16), 2: (128, 32), 3: (64, 64), 4: (64, 128),
-         5: (256, 256), 6: (256, 128), 7: (128, 256), 11: (256, 192)}
+         5: (256, 256), 6: (256, 128), 7: (128, 256), 11: (256, 192), 12: (256, 256)}
 #: 256 x 192 (cfg 11): N = 768 outputs in 4 column panels, so the LM's N = 768 products fill
 #: whole waves of 256 CUs (512 tiles for M = 4096, 256 for M = 2048) where 256 x 256 leaves a
 #: 75 %-full last wave
 BIG_TILES = (5, 6, 7, 11)
-LARGE_TILES = BIG_TILES
+#: 12: the phased 256 x 256 kernel (pgemm_ph_kernel: fills in flight across the barriers, the two
+#: wave rows staggered by a barrier); an even number of 64-deep K-tiles per split
+PH_TILES = (12,)
+LARGE_TILES = BIG_TILES + PH_TILES
+
+
+def _ph_enabled() -> bool:
+    return os.environ.get("MOPT_GEMM_PH", "0") != "0"
+
 NUM_CU = 256
 #: relative speed of the big tiles at equal occupancy of the chip; the 256 x 128 / 128 x 256 tiles
 #: lose more on long reductions (less reuse per loaded byte): profiles/gemm_r2.md
-BIG_SPEED = {5: 1.0, 6: 0.85, 7: 0.85, 11: 0.95}
+BIG_SPEED = {5: 1.0, 6: 0.85, 7: 0.85, 11: 0.95, 12: 1.1}
 LONG_K = 8192
 
 
@@ -83,7 +92,7 @@ def f32_plan(M: int, N: int, ta: bool):
 
 def big_fits(M: int, N: int, K: int, cfg: int) -> bool:
     bm, bn = TILES[cfg]
-    return M % bm == 0 and N % bn == 0 and K % 64 == 0
+    return M % bm == 0 and N % bn == 0 and K % (128 if cfg in PH_TILES else 64) == 0
 
 
 #: model of the big kernel for the planner: sustained MFMA rate (FLOP/s at a full last wave) and
@@ -101,15 +110,16 @@ def _plan_big(P: int, M: int, N: int, K: int):
     wave, e.g. the LM head's dX: 384 tiles of K = 32000 on 256 CUs); None when no big tile
     divides the shape or fills the chip well."""
     best = None
-    for cfg in BIG_TILES:
+    for cfg in BIG_TILES + (PH_TILES if _ph_enabled() else ()):
         if not big_fits(M, N, K, cfg):
             continue
         bm, bn = TILES[cfg]
         tiles = P * (M // bm) * (N // bn)
         speed = BIG_SPEED[cfg] * (0.8 if cfg in (6, 7) and K > LONG_K else 1.0)
         s = 1
+        kq = 128 if cfg in PH_TILES else 64
         while s <= MAX_BIG_SPLITS:
-            if K % (64 * s) or (s > 1 and K // s < MIN_SPLIT_K):
+            if K % (kq * s) or (s > 1 and K // s < MIN_SPLIT_K):
                 break
             n = tiles * s
             fill = n / (math.ceil(n / NUM_CU) * NUM_CU)
@@ -136,7 +146,9 @@ def plan(P: int, M: int, N: int, K: int, cfg: Optional[int] = None,
             return big
     if cfg in LARGE_TILES:
         sp = splits or 1
-        if big_fits(M, N, K, cfg) and K % (64 * sp) == 0 and (sp == 1 or cfg in BIG_TILES):
+        kq = 128 if cfg in PH_TILES else 64
+        if big_fits(M, N, K, cfg) and K % (kq * sp) == 0 and \
+                (sp == 1 or cfg in BIG_TILES + PH_TILES):
             return cfg, sp, K // sp
         cfg = None                    # the tile does not divide this shape / this K-split
     cfg = pick_tile(M, N) if cfg is None else cfg

@@ -61,8 +61,12 @@ class PopulationSweep:
                  pipelined: Optional[bool] = None, events=None, trial_events: bool = False,
                  watchdog=None, restore_algorithm: bool = False, resume: bool = False,
                  ckpt_dir: Optional[str] = None, writer: str = "auto",
-                 stagger: Optional[int] = None):
-        """``stagger``: the first fill of the empty population is spread over this many syncs
+                 stagger: Optional[int] = None, c4_reserve: Optional[int] = None):
+        """``c4_reserve``: checkpoint-pool entries set aside for direct C4 receives on a rank of
+        a multi-rank sweep of flat populations (None: ``MOPT_C4_RESERVE`` or ceil(P / 4)); a
+        sync's receives past that many travel packed instead (one buffer per member).
+
+        ``stagger``: the first fill of the empty population is spread over this many syncs
         (None: ceil(W P / 512), at most 4 -- 1 up to 512 slots).  Members that start together
         finish together, and every completion is rank 0's decision work at the sync it happens:
         2048 slots starting at once made every rung-0 budget end a burst of ~1800 completions in
@@ -97,9 +101,16 @@ class PopulationSweep:
         # are never counted in ``ckpts``: taking one by evicting a checkpoint would desync rank
         # 0's mirror of this rank's FIFO (``ckpt_fifo``), alias an entry being sent in the same
         # exchange, or silently drop a checkpoint a local RESUME of this sync expects
+        # (one entry per slot cost an LM rank 8 x 1.5 GB of idle HBM; a PBT sync
+        # moves about a quarter of the population, so ceil(P / 4) entries by default, and the
+        # receives past them fall back to the packed path -- every rank derives the same split
+        # from the assignment, see _c4_direct_rows)
         cap = self.ckpt_capacity
-        self._c4_reserve = (pop.capacity if self.comm.world_size > 1
-                            and hasattr(pop, "c4_send_tensors") else 0)
+        if c4_reserve is None:
+            c4_reserve = int(os.environ.get("MOPT_C4_RESERVE", -(-pop.capacity // 4)))
+        self._c4_reserve = (max(0, min(pop.capacity, int(c4_reserve)))
+                            if self.comm.world_size > 1 and hasattr(pop, "c4_send_tensors")
+                            else 0)
         pop.alloc_ckpt_pool(cap + self._c4_reserve)
         self._free_ck = list(range(cap - 1, -1, -1))
         self._c4_free = list(range(cap + self._c4_reserve - 1, cap - 1, -1))
@@ -1214,13 +1225,14 @@ class PopulationSweep:
         if W == 1:
             return {}, {}
         pop = self.pop
-        direct = hasattr(pop, "c4_send_tensors")
+        direct_rows = self._c4_direct_rows(assign)
         ops, recv, recv_direct = [], {}, {}
         for row in np.flatnonzero(assign[:W * P, 0] == RESUME).tolist():
             a = assign[row]
             src, dst = int(a[10]), row // P
             if src == dst or src < 0:
                 continue
+            direct = row in direct_rows
             if me == src:
                 meta = self.ckpts.get(int(a[9]))
                 if meta is None:
@@ -1242,11 +1254,31 @@ class PopulationSweep:
         metas = {s: pop.c4_finish(idx, tensors) for s, (idx, tensors) in recv_direct.items()}
         return states, metas
 
+    def _c4_direct_rows(self, assign: np.ndarray) -> set:
+        """Assignment rows whose C4 transfer lands straight in a reserved pool entry of the
+        destination: the first ``c4_reserve`` cross-rank receives of each destination rank, in
+        row order.  Every reserved entry is free again at the end of the sync that used it, so
+        each rank computes the same split from ``assign`` alone; the other receives are packed.
+        (Populations without a flat pool always pack.)"""
+        if not hasattr(self.pop, "c4_send_tensors") or self._c4_reserve <= 0:
+            return set()
+        W, P = self.comm.world_size, self.pop.capacity
+        taken = [0] * W
+        rows = set()
+        for row in np.flatnonzero(assign[:W * P, 0] == RESUME).tolist():
+            src, dst = int(assign[row, 10]), row // P
+            if src == dst or src < 0:
+                continue
+            if taken[dst] < self._c4_reserve:
+                taken[dst] += 1
+                rows.add(row)
+        return rows
+
     def _take_pool_entry(self) -> int:
-        """A pool entry reserved for C4 receives (one per slot: a rank receives at most one
-        transfer per slot and sync) -- never a checkpoint's entry."""
+        """A pool entry reserved for C4 receives -- never a checkpoint's entry
+        (``_c4_direct_rows`` hands out at most ``c4_reserve`` per sync)."""
         if not self._c4_free:
-            raise RuntimeError("C4 receive entries exhausted (more receives than slots)")
+            raise RuntimeError("C4 receive entries exhausted")
         return self._c4_free.pop()
 
     def _max_budget_local(self) -> int:

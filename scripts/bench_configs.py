@@ -14,11 +14,13 @@ one JSON line.
 from __future__ import annotations
 
 import argparse
+import math
 import json
 import os
 import sys
 import time
 
+import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -104,6 +106,15 @@ def run_sweep(args, comm):
     if comm.is_root:
         summ = sweep.summary()
         out["best_val_loss"] = summ["best_val_loss"]
+        # search quality over the run's completed trials, in completion order: the best at
+        # 96 / 224 / all trials and the spread of every trial's validation loss
+        vls = [h[2] for h in sweep.history if math.isfinite(h[2])]
+        if vls:
+            q = np.quantile(vls, [0.0, 0.1, 0.25, 0.5, 0.75, 1.0]).tolist()
+            out["val_loss_quantiles"] = dict(zip(["min", "p10", "p25", "p50", "p75", "max"],
+                                                 [round(v, 5) for v in q]))
+            out["best_val_loss_at_trials"] = {str(n): round(min(vls[:n]), 5)
+                                              for n in (32, 96, 224) if len(vls) >= n}
         out["algorithm"] = args.algo or next(iter(spec.algorithm(args.seed, P * comm.world_size)))
         inner = getattr(sweep.algorithm, "algorithm", sweep.algorithm)
         if hasattr(inner, "exploit_counts"):

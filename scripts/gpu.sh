@@ -20,6 +20,13 @@
 #   c4copy           one config-5 member: slot <-> pool copies, packed C4 path, copy_member
 #   decide           rank-0 decide cost at simulated W=1,8 (host CPU of the box)
 #   rehearsal        bench.py --gpus 2 / 4 / 8 over gloo with ranks sharing the GPU
+#   smoke            __graft_entry__.smoke()
+#   ab               interleaved A/B: for rep in 1..$REPS, for v in $AB_VALUES: run the steps of
+#                    $AB_STEPS with $AB_VAR=v, outputs under $OUT/ab_<v>_<rep>/ (e.g. AB_VAR=
+#                    MOPT_STREAMS AB_VALUES="3 4" AB_STEPS=bench REPS=5).  A value of the form
+#                    lib:<dir> runs with MOPT_KERNEL_LIB=<dir>/libmopt_kernels.so instead (a
+#                    variant library built on the CPU with ops/build.py build_variant)
+#   repeat           the steps of $AB_STEPS $REPS times (run-to-run spread), $OUT/rep_<n>/
 set -e
 OUT=${OUT:-gpurun_out/job}
 mkdir -p "$OUT"
@@ -75,6 +82,15 @@ for step in "$@"; do
     c4copy)     $T 200 python scripts/c4_copy_bench.py --out "$OUT/c4_copy.json" > "$OUT/c4_copy.log" 2>&1 ;;
     decide)     for w in 1 8; do WORLD=$w $T 300 python scripts/profile_decide.py > "$OUT/decide_world$w.log" 2>&1; done ;;
     rehearsal)  for n in 2 4 8; do $T 400 python bench.py --gpus $n --steps 10 --warmup 3 --population 64 > "$OUT/rehearsal_n$n.json" 2> "$OUT/rehearsal_n$n.err"; done ;;
+    smoke)      $T 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
+    ab)         for rep in $(seq 1 "${REPS:-3}"); do
+                  for v in ${AB_VALUES:?AB_VALUES}; do
+                    if [ "${v#lib:}" != "$v" ]; then envset="MOPT_KERNEL_LIB=${v#lib:}/libmopt_kernels.so"; tag=$(basename "${v#lib:}")
+                    else envset="${AB_VAR:?AB_VAR}=$v"; tag=$v; fi
+                    env $envset OUT="$OUT/ab_${tag}_$rep" bash "$0" ${AB_STEPS:?AB_STEPS}
+                  done
+                done ;;
+    repeat)     for rep in $(seq 1 "${REPS:-3}"); do OUT="$OUT/rep_$rep" bash "$0" ${AB_STEPS:?AB_STEPS}; done ;;
     *) echo "unknown step $step" >&2; exit 2 ;;
   esac
 done

@@ -169,8 +169,10 @@ def test_pbt_sweep_and_c4_copy_gloo_world2():
     assert n_completed == 18 and fin0 and fin1
 
 
-def _c4_flat_worker(rank, world, port, q):
-    """C4 of a flat (CNN / LM) population: pool entry -> pool entry, no pack / unpack."""
+def _c4_flat_worker(rank, world, port, q, two=False):
+    """C4 of a flat (CNN / LM) population: pool entry -> pool entry, no pack / unpack.  With
+    ``two``, rank 1 receives two members in one sync with one reserved entry (P = 3 -> ceil(3/4)):
+    the first lands in the pool, the second travels packed."""
     comm = _init(rank, world, port)
     import numpy as np
     from metaopt_amd.io.experiment_builder import build_experiment
@@ -200,9 +202,25 @@ def _c4_flat_worker(rank, world, port, q):
     c4_free0 = len(sweep._c4_free)
     assign = np.zeros((2 * 3 + 1, AS_COLS))
     assign[3 + 2] = (RESUME, 0, 0, 0.1, 0.9, 0, 0, 7, 16, 999, 0, 0)
+    if two:
+        assign[3 + 1] = (RESUME, 0, 0, 0.1, 0.9, 0, 0, 7, 16, 1000, 0, 0)
+    assert sweep._c4_reserve == 1 and len(sweep._c4_free) == 1
     states, metas = sweep._exchange_checkpoints(assign)
     out = None
     assert list(sweep.ckpts) == keys                    # nothing evicted on either rank
+    if two:
+        if rank == 1:
+            assert sorted(metas) == [1] and sorted(states) == [2]
+            pop.load_states([(1, metas[1])])
+            pop.load_slot_state(2, states[2])
+            out = (float(pop.slot_state(1)["p32"].double().sum()),
+                   float(pop.slot_state(2)["p32"].double().sum()))
+        else:
+            s = float(pop.slot_state(0)["p32"].double().sum())
+            out = (s, s)
+        q.put((rank, out))
+        dist.destroy_process_group()
+        return
     if rank == 1:
         assert not states and sorted(metas) == [2]
         assert metas[2]["ck"] not in [m["ck"] for m in sweep.ckpts.values()]
@@ -228,6 +246,20 @@ def test_c4_flat_population_pool_to_pool_gloo_world2():
     assert res[1][0] == res[0][0] == 5                  # step count travelled in the header
     assert res[1][1] == res[0][1]                       # the member's weights, bit for bit
     assert res[1][2]                                    # received into a pool entry
+
+
+def test_c4_receives_past_the_reserve_travel_packed_gloo_world2():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_c4_flat_worker, args=(r, world, port, q, True))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert res[1] == res[0]        # both members arrive bit for bit (direct and packed)
 
 
 # ------------------------------------------------------------------ launcher (no HIP before spawn)

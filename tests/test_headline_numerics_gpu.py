@@ -1,0 +1,115 @@
+"""HIP population MLP vs the fp32 PyTorch reference at the headline benchmark's shapes.
+
+``bench.py`` (BASELINE config 2) trains 256 members of a 784-w-w-w-10 MLP with widths drawn from
+loguniform(64, 1024), dropout in [0, 0.5), SGD with a bf16 momentum buffer, three stream groups,
+the first layer's backward fused with the next step's forward (``mlp_bwd0_fwd_kernel``) and the
+groups' steps queued round-robin in runs of ``step_chunk`` (4) steps.  The small-shape tests in
+``test_kernels_gpu.py`` stop at width 256 (4 k-strips per hidden layer); this one runs that exact
+kernel configuration at widths up to 1024 (16 k-strips, a whole 1024-wide hidden layer) against
+``backend="torch"`` on the same device, over two 32-step sync intervals (SURVEY §4 implication 2:
+kernel-vs-PyTorch numerics at the shapes of §2.3; the reference asserts on its full-size path the
+same way, /root/reference/tests/functional/algos/test_algos.py:60-66).
+"""
+import numpy as np
+import pytest
+import torch
+
+from metaopt_amd.models.data import TeacherClassification
+from metaopt_amd.ops.population import MemberConfig, PopulationMLP
+
+pytestmark = pytest.mark.gpu
+
+CAPACITY = 32
+# the edge widths (one tile, odd, near and at the maximum) plus a loguniform spread; each member
+# has dropout > 0 except one, learning rates over the range where a 64-step trajectory of two
+# correct bf16 implementations stays comparable
+WIDTHS = [64, 449, 960, 1024, 1024, 77, 130, 200, 301, 512, 700, 833, 1000, 96, 257, 640]
+
+
+def _configs():
+    rng = np.random.default_rng(7)
+    cfgs = []
+    for i, w in enumerate(WIDTHS):
+        cfgs.append(MemberConfig(
+            width=int(w), lr=float(np.exp(rng.uniform(np.log(0.01), np.log(0.2)))),
+            momentum=0.9, weight_decay=[0.0, 1e-4][i % 2],
+            dropout=0.0 if i == 4 else float(rng.uniform(0.05, 0.5)), seed=100 + i))
+    return cfgs
+
+
+def _population(backend):
+    p = PopulationMLP(CAPACITY, max_width=1024, n_hidden=3, eval_batch=1024, device="cuda",
+                      backend=backend, momentum_dtype="bf16",
+                      n_streams=3 if backend == "hip" else None)
+    # slots spread over the capacity (sparse work lists, several trials per stream group)
+    for i, c in enumerate(_configs()):
+        p.set_member(2 * i + (i % 2), c)
+    return p
+
+
+@pytest.fixture(scope="module")
+def data():
+    return TeacherClassification(n_train=128 * 64, n_val=1024, batch_size=128, seed=11,
+                                 device="cuda")
+
+
+def _rel(a, b):
+    return float((a - b).abs().max() / (b.abs().max() + 1e-12))
+
+
+def test_headline_config_is_the_benchmarked_one():
+    hip = _population("hip")
+    assert hip.fuse_first_layer and hip.step_chunk == 4 and hip.n_streams == 3
+    hip._refresh()
+    assert len(hip._parts) == 3
+    assert hip.momentum_dtype == "bf16" and hip.max_width == 1024 and hip.n_hidden == 3
+
+
+def test_headline_one_step_weights(data):
+    """After one step every layer of every member (weights, biases, bf16 momentum) agrees."""
+    hip, ref = _population("hip"), _population("torch")
+    x, y = data.batch(0)
+    hip.train_step(x, y)
+    ref.train_step(x, y)
+    torch.cuda.synchronize()
+    lh, lr_ = hip.train_loss(), ref.train_loss()
+    for s in ref.active_slots():
+        assert abs(lh[s] - lr_[s]) < 2e-3 * max(1.0, abs(lr_[s])), (s, lh[s], lr_[s])
+        for li, ((wh, bh), (wr, br)) in enumerate(zip(hip.layer_views(s), ref.layer_views(s))):
+            assert _rel(wh, wr) < 2e-3, (s, li, _rel(wh, wr))
+            assert _rel(bh, br) < 2e-3, (s, li, _rel(bh, br))
+        for (mh, _), (mr, _) in zip(hip.layer_views(s, hip.m32), ref.layer_views(s, ref.m32)):
+            assert mh.dtype == mr.dtype == torch.bfloat16
+            assert _rel(mh.float(), mr.float()) < 3e-2, (s, _rel(mh.float(), mr.float()))
+
+
+def test_headline_two_intervals_trajectory_and_eval(data):
+    """64 steps: the HIP side in ``train_steps`` calls (fused first layer, three stream groups,
+    round-robin runs of 4 steps -- the 6- and 10-step calls end on partial runs), the
+    reference one step at a time; losses after every call, then evaluation, agree."""
+    hip, ref = _population("hip"), _population("torch")
+    calls = [32, 6, 10, 16]            # one whole sync interval, then a split one
+    assert sum(calls) == 64
+    lh, lr_ = [], []
+    step = 0
+    for n in calls:
+        batches = [data.batch(step + k) for k in range(n)]
+        hip.train_steps(batches)
+        for x, y in batches:
+            ref.train_step(x, y)
+        step += n
+        torch.cuda.synchronize()
+        lh.append(hip.train_loss())
+        lr_.append(ref.train_loss())
+    assert hip._parts[0]["n_bwd0f"] > 0          # the fused first layer ran
+    act = ref.active_slots()
+    lh, lr_ = np.array(lh)[:, act], np.array(lr_)[:, act]
+    assert np.isfinite(lh).all() and np.isfinite(lr_).all()
+    err = np.abs(lh - lr_).max()
+    assert err < 3e-2, (err, lh, lr_)
+    # the members learned something (the comparison is not between two stuck trajectories)
+    assert (lr_[-1] < 2.2).mean() > 0.5
+    eh, ah = hip.evaluate(*data.validation())
+    er, ar = ref.evaluate(*data.validation())
+    assert np.abs(eh[act] - er[act]).max() < 3e-2, (eh[act], er[act])
+    assert np.abs(ah[act] - ar[act]).max() < 3e-2, (ah[act], ar[act])

@@ -355,14 +355,16 @@ def test_per_member_batch_trajectory_and_eval(data384):
     assert np.abs(eh[act] - er[act]).max() < 3e-2
 
 
-@pytest.mark.parametrize("optimizer,n_hidden,streams", [
-    ("sgd-bf16m", 3, 3), ("sgd", 3, 1), ("adamw", 1, 1), ("sgd-bf16m", 2, 1)])
-def test_fused_first_layer_equals_separate_launches(data, optimizer, n_hidden, streams):
+@pytest.mark.parametrize("optimizer,n_hidden,streams,chunk", [
+    ("sgd-bf16m", 3, 3, 1), ("sgd", 3, 1, 1), ("adamw", 1, 1, 1), ("sgd-bf16m", 2, 1, 1),
+    ("adamw", 1, 3, 1), ("sgd", 3, 3, 1), ("sgd-bf16m", 3, 3, 4), ("adamw", 2, 3, 4)])
+def test_fused_first_layer_equals_separate_launches(data, optimizer, n_hidden, streams, chunk):
     """``train_steps`` fuses each step's first-layer backward + update with the next step's
     first-layer forward (csrc/pop_mlp.hip mlp_bwd0_fwd_kernel): weights, optimizer state and
     losses equal the separate launches bit for bit, across two intervals, with dropout members.
-    The fused population queues its groups' steps round-robin one at a time (every step a run
-    boundary of mopt_mlp_steps_range), the reference each group's interval in one call."""
+    The fused population queues its groups' steps round-robin ``chunk`` at a time (1: every step
+    a run boundary of mopt_mlp_steps_range; 4, the default: the 6-step interval ends on a
+    2-step run), the reference each group's interval in one call."""
     kw = {}
     if optimizer == "sgd-bf16m":
         optimizer, kw = "sgd", {"momentum_dtype": "bf16"}
@@ -375,7 +377,7 @@ def test_fused_first_layer_equals_separate_launches(data, optimizer, n_hidden, s
                           optimizer=optimizer, device="cuda", backend="hip", n_streams=streams,
                           **kw)
         p.fuse_first_layer = fuse
-        p.step_chunk = 1 if fuse else 0
+        p.step_chunk = chunk if fuse else 0
         for i, c in enumerate(cfgs):
             p.set_member(i + 1, c)
         pops.append(p)

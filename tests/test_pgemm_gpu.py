@@ -44,8 +44,24 @@ def test_every_tile_config(cfg):
 def test_big_tiles_every_layout(cfg, ta, tb):
     """The 8-wave direct-to-LDS kernel (swizzled k-contiguous and row-contiguous images) in
     every operand layout; several K tiles so both LDS stages are used, distinct trials."""
-    A, B, a, b = _operands(3, 512, 512, 320, ta, tb, seed=10 + cfg)
+    A, B, a, b = _operands(3, 512, 512, 384, ta, tb, seed=10 + cfg)
+    assert plan(3, 512, 512, 384, cfg, 1)[0] == cfg
     _check(pgemm(a, b, ta=ta, tb=tb, cfg=cfg), A, B)
+
+
+@pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("P,M,N,K,splits", [(37, 512, 512, 256, 1), (5, 768, 1024, 1536, 1),
+                                            (6, 512, 768, 2048, 2), (4, 256, 512, 1024, 4)])
+def test_phased_tile(ta, tb, P, M, N, K, splits):
+    """cfg 12 (pgemm_ph_kernel): 148 tiles on 148 workgroups, 120 tiles of 24 K-tiles, K-split
+    partials over 4 and 2 splits -- and uneven tile counts per persistent workgroup (300 tiles:
+    44 workgroups walk two)."""
+    A, B, a, b = _operands(P, M, N, K, ta, tb, seed=P + K)
+    assert plan(P, M, N, K, 12, splits)[:2] == (12, splits)
+    _check(pgemm(a, b, ta=ta, tb=tb, cfg=12, splits=splits), A, B)
+    if splits == 1 and P == 37:
+        A, B, a, b = _operands(75, 512, 512, 128, ta, tb, seed=3)       # 300 tiles, 2 K-tiles
+        _check(pgemm(a, b, ta=ta, tb=tb, cfg=12), A, B)
 
 
 @pytest.mark.parametrize("cfg", LARGE_TILES)
