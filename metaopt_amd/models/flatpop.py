@@ -390,7 +390,8 @@ class FlatPopulation:
         return loss, second
 
     def evaluate(self, x, y, slots=None):
-        return self.eval_result(self.stats_snapshot(), self.evaluate_async(x, y, slots))
+        handle = self.evaluate_async(x, y, slots)    # before the snapshot that reads its sums
+        return self.eval_result(self.stats_snapshot(), handle)
 
     # ------------------------------------------------------------------ checkpoints
     @property

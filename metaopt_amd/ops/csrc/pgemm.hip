@@ -851,11 +851,15 @@ __global__ __launch_bounds__(512) void pgemm_ph_kernel(const GemmArgs g) {
   _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                             \
     _Pragma("unroll") for (int j = 0; j < 2; ++j)                                              \
       BR[ks][j] = IB::frag(smem + (2 * (2 + (HALF)) + (BUF)) * SL, wn * 32 + 16 * j, ks, li, gq, q, pp);
+  // s_setprio around the cluster: without it hipcc moves MFMAs across the raw barriers in among
+  // the next phase's reads and fills, which undoes the ping-pong of the two wave rows
 #define PH_MFMA(MH, NH, BR)                                                                    \
+  __builtin_amdgcn_s_setprio(1);                                                               \
   _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                             \
     _Pragma("unroll") for (int i = 0; i < 4; ++i)                                              \
       _Pragma("unroll") for (int j = 0; j < 2; ++j)                                            \
-        acc[MH][NH][i][j] = mfma16(BR[ks][j], fa[ks][i], acc[MH][NH][i][j]);
+        acc[MH][NH][i][j] = mfma16(BR[ks][j], fa[ks][i], acc[MH][NH][i][j]);                   \
+  __builtin_amdgcn_s_setprio(0);
   // one phase: FILL is (slot, buffer, K-tiles ahead); the wait mode follows from what is queued
 #define PH_STEP(FSLOT, FBUF, FD, MH, NH, BR)                                                   \
   {                                                                                            \
@@ -926,6 +930,156 @@ __global__ __launch_bounds__(512) void pgemm_ph_kernel(const GemmArgs g) {
 // correct on every layout but 5-25 % slower than this 2-stage kernel on every LM shape; it was
 // removed in round 4, the A/B is in profiles/round3.md "LM GEMMs".)
 
+// ----------------------------------------------------------------------------------------------
+// The big-tile kernel on v_mfma_f32_32x32x16_bf16 (cfg 13: 256 x 256, cfg 14: 256 x 192; round 6,
+// VERDICT r5 item 1), NT layout (A [M][K], B [N][K]: both images k-contiguous) -- the same LDS-DMA
+// fills, swizzle, 2-stage loop and persistent tile walk as pgemm_big_kernel, each wave a 32 FM x
+// 32 FN sub-tile of 32 x 32 accumulator blocks.  Fragment of a 32-row block for k-sub-step kk
+// (16 deep): lane l reads row (l & 31), k = 16 kk + 8 (l >> 5) .. + 7 -- one ds_read_b128 of
+// chunk 2 kk + (l >> 5); 16 lanes of one read hit 16 rows of one chunk column, which the
+// (r >> 1) & 7 XOR spreads over 16 bank slots, as for the 16x16x32 reads.  The LDS bytes a wave
+// reads per K-step are those of its sub-tile's A and B panels under either MFMA shape (a fragment
+// is reused across the other operand's blocks); what changes is half the MFMA instructions (32
+// cycles each instead of 16) and the C layout: acc (C^T, B the MFMA's A operand) lane l, register
+// 4 q + r = C[m = 32 i + (l & 31)][n = 32 j + 8 q + 4 (l >> 5) + r].
+// ----------------------------------------------------------------------------------------------
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+template <int WM, int FM, int FN>
+__global__ __launch_bounds__(512) void pgemm_big32_kernel(const GemmArgs g) {
+  constexpr int WN = 8 / WM;
+  constexpr int BM = WM * 32 * FM, BN = WN * 32 * FN;
+  static_assert(FN * 4 % 2 == 0, "stores pair the 8-column groups");
+  using IA = GImg<BM, true>;
+  using IB = GImg<BN, true>;
+  constexpr int STAGE = IA::ELEMS + IB::ELEMS;
+  __shared__ __attribute__((aligned(1024))) bf16_t smem[2 * STAGE];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lr = lane & 31, lh = lane >> 5;
+  const int wm = wave / WN, wn = wave % WN;
+  const int nk = g.k_per_split / BK;
+
+  int vb = blockIdx.x;
+  int p = 0, m0 = 0, n0 = 0, k0 = 0;
+  auto decode = [&](int v) {
+    const int t = xcd_remap(v, g.nwg);
+    const int per = g.tiles_m * g.tiles_n;
+    const int pq = t / per;
+    p = pq / g.splits;
+    k0 = (pq - p * g.splits) * g.k_per_split;
+    const int idx = t - pq * per, span = kGroupM * g.tiles_n;
+    const int grp = idx / span, in = idx - grp * span;
+    const int gm = min(kGroupM, g.tiles_m - grp * kGroupM);
+    m0 = (grp * kGroupM + in % gm) * BM;
+    n0 = (in / gm) * BN;
+  };
+  // fragment of the 32-row block starting at row32, k-sub-step kk
+  auto frag = [&](const bf16_t* img, int row32, int kk) {
+    const int r = row32 + lr;
+    return lds_frag(img + r * BK + 8 * ((2 * kk + lh) ^ kc_swz(r)));
+  };
+  decode(vb);
+  IA::fill(g.a.ptr + p * g.a.batch, g.a.ld, m0, k0, smem, wave, lane);
+  IB::fill(g.b.ptr + p * g.b.batch, g.b.ld, n0, k0, smem + IA::ELEMS, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  int stage = 0;
+  while (true) {
+    const int nvb = vb + (int)gridDim.x;
+    const bool has_next = nvb < g.nwg;
+    int np = p, nm0 = m0, nn0 = n0, nk0 = k0;
+    if (has_next) {
+      const int cp = p, cm = m0, cn = n0, ck = k0;
+      decode(nvb);
+      np = p; nm0 = m0; nn0 = n0; nk0 = k0;
+      p = cp; m0 = cm; n0 = cn; k0 = ck;
+    }
+    const bf16_t* A = g.a.ptr + p * g.a.batch;
+    const bf16_t* B = g.b.ptr + p * g.b.batch;
+    f32x16 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    for (int kt = 0; kt < nk; ++kt) {
+      const bf16_t* cur = smem + stage * STAGE;
+      bf16_t* nxt = smem + (stage ^ 1) * STAGE;
+      if (kt + 1 < nk) {
+        IA::fill(A, g.a.ld, m0, k0 + (kt + 1) * BK, nxt, wave, lane);
+        IB::fill(B, g.b.ld, n0, k0 + (kt + 1) * BK, nxt + IA::ELEMS, wave, lane);
+      } else if (has_next) {
+        IA::fill(g.a.ptr + np * g.a.batch, g.a.ld, nm0, nk0, nxt, wave, lane);
+        IB::fill(g.b.ptr + np * g.b.batch, g.b.ld, nn0, nk0, nxt + IA::ELEMS, wave, lane);
+      }
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        bf16x8 a[FM], b[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) a[i] = frag(cur, wm * 32 * FM + 32 * i, kk);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) b[j] = frag(cur + IA::ELEMS, wn * 32 * FN + 32 * j, kk);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = mfma32(b[j], a[i], acc[i][j]);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      stage ^= 1;
+    }
+
+    const int mrow = m0 + wm * 32 * FM + lr;
+    const int ncol = n0 + wn * 32 * FN;
+    if (g.part != nullptr) {
+      const int64_t total = (int64_t)g.P * g.M * g.N;
+      float* part = g.part + (k0 / g.k_per_split) * total + (int64_t)p * g.M * g.N +
+                    (int64_t)mrow * g.N + ncol + 4 * lh;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            *(f32x4*)(part + (int64_t)(32 * i) * g.N + 32 * j + 8 * q) =
+                f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2],
+                      acc[i][j][4 * q + 3]};
+    } else {
+      // groups q (lane half h holds columns 8 q + 4 h .. + 3): v_permlane32_swap of the packed
+      // groups q, q + 1 gives lane l < 32 columns 8 q .. + 7 and lane l + 32 columns 8 (q + 1)
+      // .. + 7 of row l -- one 16-byte store per lane per group pair
+      bf16_t* C = g.C + p * g.sC + (int64_t)mrow * g.ldc + ncol + 8 * lh;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; q += 2) {
+            const uint32_t x0 = pack2bf(acc[i][j][4 * q], acc[i][j][4 * q + 1]);
+            const uint32_t x1 = pack2bf(acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]);
+            const uint32_t y0 = pack2bf(acc[i][j][4 * q + 4], acc[i][j][4 * q + 5]);
+            const uint32_t y1 = pack2bf(acc[i][j][4 * q + 6], acc[i][j][4 * q + 7]);
+            const auto s0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
+            const auto s1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
+            *(uint4*)(C + (int64_t)(32 * i) * g.ldc + 32 * j + 8 * q) =
+                make_uint4(s0[0], s1[0], s0[1], s1[1]);
+          }
+    }
+    if (!has_next) break;
+    vb = nvb;
+    p = np; m0 = nm0; n0 = nn0; k0 = nk0;
+  }
+}
+
 // sum of the split-K partials [splits][P][M][N] -> C[p][m][n * ldc] bf16
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part,
                                                             bf16_t* __restrict__ C,
@@ -977,6 +1131,28 @@ int launch_big(GemmArgs g, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+template <bool TA, bool TB, int WM, int FM, int FN>
+int launch_big32(GemmArgs g, hipStream_t st) {
+  if constexpr (TA || !TB) {
+    return (int)hipErrorNotSupported;          // NT only (both images k-contiguous)
+  } else {
+    constexpr int BM = WM * 32 * FM, BN = (8 / WM) * 32 * FN;
+    if (g.M % BM || g.N % BN || g.k_per_split % BK || g.k_per_split < BK ||
+        (int64_t)g.k_per_split * g.splits != g.K || (g.splits > 1 && g.part == nullptr) ||
+        g.nin > 1)
+      return (int)hipErrorInvalidValue;
+    g.tiles_m = g.M / BM;
+    g.tiles_n = g.N / BN;
+    const int64_t nwg = (int64_t)g.P * g.splits * g.tiles_m * g.tiles_n;
+    if (nwg <= 0 || nwg > 0x7FFFFFFF) return (int)hipErrorInvalidValue;
+    g.nwg = (int)nwg;
+    constexpr int kGrid = 256;
+    const int grid = nwg < kGrid ? (int)nwg : kGrid;
+    hipLaunchKernelGGL((pgemm_big32_kernel<WM, FM, FN>), dim3(grid), dim3(512), 0, st, g);
+    return (int)hipGetLastError();
+  }
+}
+
 template <bool TA, bool TB, int EPI = 0>
 int launch_ph(GemmArgs g, hipStream_t st) {
   if (g.M % 256 || g.N % 256 || g.k_per_split % (2 * BK) || g.k_per_split < 2 * BK ||
@@ -1004,6 +1180,8 @@ int dispatch_tile(const GemmArgs& g, int cfg, hipStream_t st) {
       case 6: return launch_big<TA, TB, 4, 4, 4>(g, st);  // 256 x 128
       case 7: return launch_big<TA, TB, 2, 4, 4>(g, st);  // 128 x 256
       case 11: return launch_big<TA, TB, 4, 4, 6>(g, st);     // 256 x 192
+      case 13: return launch_big32<TA, TB, 2, 4, 2>(g, st);   // 256 x 256, 32x32x16 MFMA
+      case 14: return launch_big32<TA, TB, 4, 2, 3>(g, st);   // 256 x 192, 32x32x16 MFMA
       default: break;
     }
   }
@@ -1059,11 +1237,11 @@ extern "C" {
 
 // Tile of configuration ``cfg`` (rows, cols): lets the host size grids and split-K.
 int mopt_pgemm_tile(int cfg, int* bm, int* bn) {
-  static const int t[13][2] = {{128, 128}, {128, 16},  {128, 32},  {64, 64},
+  static const int t[15][2] = {{128, 128}, {128, 16},  {128, 32},  {64, 64},
                                {64, 128},  {256, 256}, {256, 128}, {128, 256},
                                {256, 256}, {256, 256}, {256, 128}, {256, 192},
-                               {256, 256}};
-  if (cfg < 0 || cfg > 12) return (int)hipErrorInvalidValue;
+                               {256, 256}, {256, 256}, {256, 192}};
+  if (cfg < 0 || cfg > 14) return (int)hipErrorInvalidValue;
   *bm = t[cfg][0];
   *bn = t[cfg][1];
   return 0;

@@ -44,7 +44,8 @@ _lib.register_signatures({
 # (any shape, ragged edges); 5-7: 8-wave direct-to-LDS kernel, one workgroup per CU, for shapes
 # the tile divides (M % BM == N % BN == K % 64 == 0)
 TILES = {0: (128, 128), 1: (128, 16), 2: (128, 32), 3: (64, 64), 4: (64, 128),
-         5: (256, 256), 6: (256, 128), 7: (128, 256), 11: (256, 192), 12: (256, 256)}
+         5: (256, 256), 6: (256, 128), 7: (128, 256), 11: (256, 192), 12: (256, 256),
+         13: (256, 256), 14: (256, 192)}
 #: 256 x 192 (cfg 11): N = 768 outputs in 4 column panels, so the LM's N = 768 products fill
 #: whole waves of 256 CUs (512 tiles for M = 4096, 256 for M = 2048) where 256 x 256 leaves a
 #: 75 %-full last wave
@@ -52,7 +53,10 @@ BIG_TILES = (5, 6, 7, 11)
 #: 12: the phased 256 x 256 kernel (pgemm_ph_kernel: fills in flight across the barriers, the two
 #: wave rows staggered by a barrier); an even number of 64-deep K-tiles per split
 PH_TILES = (12,)
-LARGE_TILES = BIG_TILES + PH_TILES
+#: 13 / 14: the big-tile kernel on the 32x32x16 MFMA (pgemm_big32_kernel), NT layout only (A
+#: [M][K], B [N][K]); explicit requests only -- measured against 5 / 11 in profiles/round6.md
+MF32_TILES = (13, 14)
+LARGE_TILES = BIG_TILES + PH_TILES + MF32_TILES
 
 
 def _ph_enabled() -> bool:
@@ -147,8 +151,7 @@ def plan(P: int, M: int, N: int, K: int, cfg: Optional[int] = None,
     if cfg in LARGE_TILES:
         sp = splits or 1
         kq = 128 if cfg in PH_TILES else 64
-        if big_fits(M, N, K, cfg) and K % (kq * sp) == 0 and \
-                (sp == 1 or cfg in BIG_TILES + PH_TILES):
+        if big_fits(M, N, K, cfg) and K % (kq * sp) == 0:
             return cfg, sp, K // sp
         cfg = None                    # the tile does not divide this shape / this K-split
     cfg = pick_tile(M, N) if cfg is None else cfg

@@ -9,7 +9,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from metaopt_amd.ops.gemm import pgemm, plan  # noqa: E402
+from metaopt_amd.ops.gemm import MF32_TILES, pgemm, plan  # noqa: E402
 
 # (name, P, M, N, K, ta, tb)
 SHAPES = [
@@ -68,6 +68,8 @@ def main():
         row = {"shape": name, "P": P, "M": M, "N": N, "K": K, "plan": plan(P, M, N, K),
                "pgemm_us": round(t_ours, 1), "pgemm_tflops": round(flops / t_ours / 1e6, 1)}
         for c in [int(v) for v in args.cfgs.split(",") if v]:
+            if c in MF32_TILES and (ta or not tb):
+                continue                          # the 32x32x16 kernel is NT only
             t = timeit(lambda: pgemm(a, b, ta=ta, tb=tb, out=out, cfg=c), args.iters)
             row[f"cfg{c}_tflops"] = round(flops / t / 1e6, 1)
         for pair in [v for v in args.splits.split(",") if v]:

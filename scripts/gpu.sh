@@ -15,11 +15,13 @@
 #   kbench_ab        the microbench per kernel variant (env $ABVAR set to each of $VARIANTS)
 #   kbench_rows      the microbench at 128 / 256 / 512 rows per step (multi-row-block kernels)
 #   pmc_kbench       PMC passes of the MLP kernels (fetch/write/MFMA/LDS, one pass each)
+#   pmc_gemm         PMC passes of the GEMM microbench ($SHAPES name prefix, $CFGS tile configs)
 #   lm resnet hyper  bench_configs.py of one config        trace_lm trace_resnet trace_hyper
 #   gemm conv        pgemm / direct-conv microbenches      gemm32  f32-operand (K11) GEMM plans
 #   c4copy           one config-5 member: slot <-> pool copies, packed C4 path, copy_member
 #   decide           rank-0 decide cost at simulated W=1,8 (host CPU of the box)
 #   rehearsal        bench.py --gpus 2 / 4 / 8 over gloo with ranks sharing the GPU
+#   northstar_resnet config 3 search quality: TPE vs random, 224 trials, seeds $SEEDS (0 1 2)
 #   smoke            __graft_entry__.smoke()
 #   ab               interleaved A/B: for rep in 1..$REPS, for v in $AB_VALUES: run the steps of
 #                    $AB_STEPS with $AB_VAR=v, outputs under $OUT/ab_<v>_<rep>/ (e.g. AB_VAR=
@@ -47,6 +49,14 @@ pmc() {    # pmc NAME COUNTERS...: one counter pass over the MLP kernel microben
       > "$ROOT/$OUT/$name.log" 2>&1)
 }
 
+pmcg() {   # pmcg NAME COUNTERS...: one counter pass over the GEMM microbench ($SHAPES, $CFGS)
+  local name=$1; shift
+  (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 150 rocprofv3 --output-format csv \
+      --pmc "$@" -d "$ROOT/$OUT/$name" -o run -- \
+      python3 "$ROOT/scripts/gemm_bench.py" --iters 5 --no-torch --shapes "${SHAPES:-lm}" \
+      --cfgs "${CFGS:-11,12}" > "$ROOT/$OUT/$name.log" 2>&1)
+}
+
 for step in "$@"; do
   echo "[gpu.sh] $step"
   case "$step" in
@@ -70,6 +80,10 @@ for step in "$@"; do
       pmc pmc_write WRITE_SIZE
       pmc pmc_mfma SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES
       pmc pmc_lds SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAVE_CYCLES ;;
+    pmc_gemm)   # PMC passes of the GEMM microbench (SHAPES prefix, CFGS tiles)
+      pmcg pmcg_busy SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE
+      pmcg pmcg_lds SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES
+      pmcg pmcg_fetch FETCH_SIZE ;;
     lm)         $T 300 python scripts/bench_configs.py --config lm-125m --steps 600 --warmup 0 > "$OUT/lm.json" 2> "$OUT/lm.err" ;;
     resnet)     $T 300 python scripts/bench_configs.py --config resnet20 --steps 60 --warmup 30 > "$OUT/resnet20.json" 2> "$OUT/resnet20.err" ;;
     hyper)      $T 300 python scripts/bench_configs.py --config hyper --steps 3 --warmup 1 > "$OUT/hyper.json" 2> "$OUT/hyper.err" ;;
@@ -82,6 +96,11 @@ for step in "$@"; do
     c4copy)     $T 200 python scripts/c4_copy_bench.py --out "$OUT/c4_copy.json" > "$OUT/c4_copy.log" 2>&1 ;;
     decide)     for w in 1 8; do WORLD=$w $T 300 python scripts/profile_decide.py > "$OUT/decide_world$w.log" 2>&1; done ;;
     rehearsal)  for n in 2 4 8; do $T 400 python bench.py --gpus $n --steps 10 --warmup 3 --population 64 > "$OUT/rehearsal_n$n.json" 2> "$OUT/rehearsal_n$n.err"; done ;;
+    northstar_resnet)   # config 3: TPE vs random search, 3120 steps (224 trials) x seeds 0-2
+                for sd in ${SEEDS:-0 1 2}; do
+                  $T 200 python scripts/bench_configs.py --config resnet20 --steps 3120 --warmup 0 --seed $sd > "$OUT/resnet_tpe_s$sd.json" 2> "$OUT/resnet_tpe_s$sd.err"
+                  $T 200 python scripts/bench_configs.py --config resnet20 --steps 3120 --warmup 0 --seed $sd --algo random > "$OUT/resnet_random_s$sd.json" 2> "$OUT/resnet_random_s$sd.err"
+                done ;;
     smoke)      $T 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     ab)         for rep in $(seq 1 "${REPS:-3}"); do
                   for v in ${AB_VALUES:?AB_VALUES}; do

@@ -3,7 +3,7 @@ every tile configuration, ragged edges, split-K, and the autograd wrapper used b
 import pytest
 import torch
 
-from metaopt_amd.ops.gemm import LARGE_TILES, TILES, pbmm, pgemm, plan
+from metaopt_amd.ops.gemm import LARGE_TILES, MF32_TILES, TILES, pbmm, pgemm, plan
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -40,13 +40,32 @@ def test_every_tile_config(cfg):
 
 
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
-@pytest.mark.parametrize("cfg", LARGE_TILES)
+@pytest.mark.parametrize("cfg", [c for c in LARGE_TILES if c not in MF32_TILES])
 def test_big_tiles_every_layout(cfg, ta, tb):
     """The 8-wave direct-to-LDS kernel (swizzled k-contiguous and row-contiguous images) in
     every operand layout; several K tiles so both LDS stages are used, distinct trials."""
-    A, B, a, b = _operands(3, 512, 512, 384, ta, tb, seed=10 + cfg)
-    assert plan(3, 512, 512, 384, cfg, 1)[0] == cfg
+    A, B, a, b = _operands(3, 512, 768, 384, ta, tb, seed=10 + cfg)   # N: 256, 192 and 128 | N
+    assert plan(3, 512, 768, 384, cfg, 1)[0] == cfg
     _check(pgemm(a, b, ta=ta, tb=tb, cfg=cfg), A, B)
+
+
+@pytest.mark.parametrize("cfg", MF32_TILES)
+@pytest.mark.parametrize("P,M,N,K,splits", [(3, 512, 768, 384, 1), (300, 256, 768, 128, 1),
+                                            (4, 256, 768, 2048, 4)])
+def test_mfma32_tiles_nt(cfg, P, M, N, K, splits):
+    """cfg 13 / 14 (pgemm_big32_kernel, v_mfma_f32_32x32x16_bf16, NT only): the 32 x 32 C layout
+    through the permlane32 store and the split-K partial store; persistent walk over more tiles
+    than workgroups (300 trials)."""
+    A, B, a, b = _operands(P, M, N, K, False, True, seed=cfg + K)
+    assert plan(P, M, N, K, cfg, splits)[:2] == (cfg, splits)
+    _check(pgemm(a, b, tb=True, cfg=cfg, splits=splits), A, B)
+
+
+def test_mfma32_tiles_refuse_other_layouts():
+    A, B, a, b = _operands(2, 256, 256, 128, False, False, seed=1)
+    with pytest.raises(RuntimeError):
+        pgemm(a, b, cfg=13)
+        torch.cuda.synchronize()
 
 
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
@@ -64,7 +83,7 @@ def test_phased_tile(ta, tb, P, M, N, K, splits):
         _check(pgemm(a, b, ta=ta, tb=tb, cfg=12), A, B)
 
 
-@pytest.mark.parametrize("cfg", LARGE_TILES)
+@pytest.mark.parametrize("cfg", [c for c in LARGE_TILES if c not in MF32_TILES])
 def test_big_tiles_persistent_and_strided_output(cfg):
     """More tiles than workgroups (the persistent loop carries the next tile's first K-step
     across the epilogue), a C written into a wider row stride, split-K (f32 partials of the big
