@@ -522,12 +522,14 @@ __global__ __launch_bounds__(256) void embed_bwd_sorted_kernel(const int64_t* __
                                                                const int64_t* __restrict__ order,
                                                                const bf16_t* __restrict__ dout,
                                                                bf16_t* __restrict__ dtable,
-                                                               int64_t rows, int d) {
+                                                               int64_t rows, int d,
+                                                               int64_t table_rows) {
   const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (w >= rows) return;
   const int64_t key = keys[w];
   if (w > 0 && keys[w - 1] == key) return;  // not the first of its run
+  if (!MOPT_IN_RANGE(key, table_rows, "embedding backward token")) return;
   const int nc = d >> 3;
   float acc[kMaxChunks][8];
 #pragma unroll
@@ -553,6 +555,64 @@ __global__ __launch_bounds__(256) void embed_bwd_sorted_kernel(const int64_t* __
     const int c = lane + 64 * k;
     if (c < nc) *(uint4*)(dtable + key * (int64_t)d + 8 * c) = pack8(acc[k]);
   }
+}
+
+// The keys of embed_bwd_sorted_kernel without a library sort (round 6; torch.sort was eight
+// rocprim / aten launches per step): one 1024-thread workgroup per trial sorts the trial's (token,
+// row) pairs as 64-bit words token << 32 | row -- the row in the low half makes the order stable
+// -- with a bitonic network in LDS (n = the next power of two >= rows_per_trial, padded with
+// all-ones words), then writes keys = trial V + token and order = the global row.  Rows per trial
+// <= kEmbedSortMax (n 8-byte words of LDS).
+constexpr int kEmbedSortMax = 8192;
+__global__ __launch_bounds__(1024) void embed_sort_kernel(const int32_t* __restrict__ tok,
+                                                          int64_t* __restrict__ keys,
+                                                          int64_t* __restrict__ order, int rpt,
+                                                          int n, int V) {
+  __shared__ uint64_t s[kEmbedSortMax];
+  const int p = blockIdx.x, tid = threadIdx.x;
+  const int32_t* t = tok + (int64_t)p * rpt;
+  for (int i = tid; i < n; i += 1024)
+    s[i] = i < rpt ? ((uint64_t)(uint32_t)t[i] << 32) | (uint32_t)i : ~0ull;
+  __syncthreads();
+  for (int k = 2; k <= n; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < n; i += 1024) {
+        const int ij = i ^ j;
+        if (ij > i) {
+          const uint64_t a = s[i], b = s[ij];
+          if ((a > b) == ((i & k) == 0)) {
+            s[i] = b;
+            s[ij] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = tid; i < rpt; i += 1024) {
+    const uint64_t w = s[i];
+    keys[(int64_t)p * rpt + i] = (int64_t)p * V + (int64_t)(int32_t)(uint32_t)(w >> 32);
+    order[(int64_t)p * rpt + i] = (int64_t)p * rpt + (int64_t)(uint32_t)w;
+  }
+}
+
+// Zero the table-gradient rows of the previous step's sorted keys (one wave per run of equal
+// keys; negative / out-of-range keys -- the initial fill -- are skipped).  With it the table
+// gradient is never cleared whole: every row outside the previous step's keys is already zero
+// (by induction from the zero-initialised buffer), and the rows of this step's keys are fully
+// overwritten by embed_bwd_sorted_kernel -- ~50 MB of row stores instead of a 393 MB fill for
+// the 125M LM (8 trials x 32000 x 768).
+__global__ __launch_bounds__(256) void embed_zero_rows_kernel(const int64_t* __restrict__ keys,
+                                                              bf16_t* __restrict__ dtable,
+                                                              int64_t rows, int d,
+                                                              int64_t table_rows) {
+  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (w >= rows) return;
+  const int64_t key = keys[w];
+  if ((w > 0 && keys[w - 1] == key) || key < 0 || key >= table_rows) return;
+  for (int c = lane; c < (d >> 3); c += 64)
+    *(uint4*)(dtable + key * (int64_t)d + 8 * c) = make_uint4(0, 0, 0, 0);
 }
 
 // RMSNorm weight gradient straight into a bf16 gradient view, two passes without atomics.
@@ -970,11 +1030,32 @@ int mopt_embed_bwd(const void* tok, const void* dout, void* dtable32, int64_t ro
 // keys [rows] = trial * V + token sorted ascending (stably), order [rows] the dout row of each;
 // dtable bf16 [P][V][d] zeroed by the caller.
 int mopt_embed_bwd_sorted(const void* keys, const void* order, const void* dout, void* dtable,
-                          int64_t rows, int d, void* stream) {
+                          int64_t rows, int d, int64_t table_rows, void* stream) {
   if (d % 8 || d > 64 * 8 * kMaxChunks) return 1;
   hipLaunchKernelGGL(embed_bwd_sorted_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0,
                      (hipStream_t)stream, (const int64_t*)keys, (const int64_t*)order,
-                     (const bf16_t*)dout, (bf16_t*)dtable, rows, d);
+                     (const bf16_t*)dout, (bf16_t*)dtable, rows, d, table_rows);
+  return (int)hipGetLastError();
+}
+
+// The in-tree key sort (embed_sort_kernel): tok [P * rpt] int32 -> keys, order [P * rpt] int64.
+int mopt_embed_sort(const void* tok, void* keys, void* order, int P, int rpt, int V,
+                    void* stream) {
+  int n = 1;
+  while (n < rpt) n <<= 1;
+  if (P <= 0 || rpt <= 0 || n > kEmbedSortMax) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(embed_sort_kernel, dim3(P), dim3(1024), 0, (hipStream_t)stream,
+                     (const int32_t*)tok, (int64_t*)keys, (int64_t*)order, rpt, n, V);
+  return (int)hipGetLastError();
+}
+
+// Zero the dtable rows named by the previous step's sorted keys (embed_zero_rows_kernel).
+int mopt_embed_zero_rows(const void* keys, void* dtable, int64_t rows, int d, int64_t table_rows,
+                         void* stream) {
+  if (d % 8) return 1;
+  hipLaunchKernelGGL(embed_zero_rows_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0,
+                     (hipStream_t)stream, (const int64_t*)keys, (bf16_t*)dtable, rows, d,
+                     table_rows);
   return (int)hipGetLastError();
 }
 

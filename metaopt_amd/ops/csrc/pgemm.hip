@@ -536,30 +536,44 @@ __global__ __launch_bounds__(512) void pgemm_big_kernel(const GemmArgs g) {
       const int dm = g.nH * 64;
       const int64_t sec_stride = (int64_t)g.P * g.M * dm;
       const int bper = g.M / g.T;
+      // each lane rotates its own 4 columns, then fragments j, j + 1 are exchanged between the
+      // lane rows gq = 0|1 (2|3) by v_permlane16_swap as in the plain epilogue below: every lane
+      // holds 8 consecutive columns (one head, 8-aligned) of one row -> one 16-byte store per
+      // fragment pair instead of two 8-byte ones (round 6)
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int m = m0 + wm * 16 * FM + 16 * i + li;
         const int bl = m / g.T, t = m - bl * g.T;
         const int64_t bq = (int64_t)p * bper + bl;
 #pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          const int n = n0 + wn * 16 * FN + 16 * j + 4 * gq;
-          const int sec = n / dm, hc = n - sec * dm, hh = hc >> 6, c = hc & 63;
-          float x[4];
+        for (int j = 0; j < FN; j += 2) {
+          uint32_t pk[2][2];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) x[r] = bf2f(f2bf(acc[i][j][r]));   // qkv as stored
-          if (sec < 2) {
-            const float* cs = g.cosT + (int64_t)t * 32 + (c >> 1);
-            const float* sn = g.sinT + (int64_t)t * 32 + (c >> 1);
+          for (int jj = 0; jj < 2; ++jj) {
+            const int n = n0 + wn * 16 * FN + 16 * (j + jj) + 4 * gq;
+            const int sec = n / dm, c = (n - sec * dm) & 63;
+            float x[4];
 #pragma unroll
-            for (int q2 = 0; q2 < 2; ++q2) {
-              const float a = x[2 * q2], b = x[2 * q2 + 1], co = cs[q2], si = sn[q2];
-              x[2 * q2] = a * co - b * si;
-              x[2 * q2 + 1] = b * co + a * si;
+            for (int r = 0; r < 4; ++r) x[r] = bf2f(f2bf(acc[i][j + jj][r]));   // qkv as stored
+            if (sec < 2) {
+              const float* cs = g.cosT + (int64_t)t * 32 + (c >> 1);
+              const float* sn = g.sinT + (int64_t)t * 32 + (c >> 1);
+#pragma unroll
+              for (int q2 = 0; q2 < 2; ++q2) {
+                const float a = x[2 * q2], b = x[2 * q2 + 1], co = cs[q2], si = sn[q2];
+                x[2 * q2] = a * co - b * si;
+                x[2 * q2 + 1] = b * co + a * si;
+              }
             }
+            pk[jj][0] = pack2bf(x[0], x[1]);
+            pk[jj][1] = pack2bf(x[2], x[3]);
           }
+          const auto s0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
+          const int n8 = n0 + wn * 16 * FN + 16 * j + 16 * (gq & 1) + 8 * (gq >> 1);
+          const int sec = n8 / dm, hc = n8 - sec * dm, hh = hc >> 6, c = hc & 63;
           bf16_t* o = g.C + sec * sec_stride + ((bq * g.nH + hh) * g.T + t) * 64 + c;
-          *(uint2*)o = make_uint2(pack2bf(x[0], x[1]), pack2bf(x[2], x[3]));
+          *(uint4*)o = make_uint4(s0[0], s1[0], s0[1], s1[1]);
         }
       }
       if (!has_next) break;

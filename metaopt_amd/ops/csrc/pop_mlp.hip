@@ -36,15 +36,31 @@ struct MlpTL {
   int32_t K;       // padded input features (multiple of 64)
   int32_t N;       // padded output features (multiple of 64)
   int32_t trial;   // population slot (index into the hyper-parameter table)
-  int32_t n_real;  // real outputs (classes of the CE layer)
+  int32_t n_real;  // real outputs (classes of the CE layer, the member's width otherwise)
   int64_t w_off;   // W [N][K] (k-strip-major, see w_row_stride): offset into the parameters
   int64_t b_off;   // bias [N]: offset into the f32 master / optimizer buffers
   int64_t x_off;   // layer input  [rows][K] bf16: offset into the x buffer of the launch
   int64_t y_off;   // layer output [rows][N] bf16: offset into act (forward) / grad (backward)
   int64_t gx_off;  // dZ of the layer below [rows][K] bf16 in grad (backward), -1 if none
-  int64_t rows;    // rows this trial uses in the launch (its batch size; <= the launch's rows):
+  int32_t rows;    // rows this trial uses in the launch (its batch size; <= the launch's rows):
                    // row blocks at or past it are skipped, the loss is normalised by it
+  int32_t k_real;  // real inputs: W[:, k] is zero for k >= k_real (padding to K)
 };
+
+// Dead padding (round 6): K and N are padded to multiples of 64, but W[n][k] (and its optimizer
+// state) is zero forever for n >= n_real or k >= k_real -- its gradient is X[:, k]^T dZ[:, n] with
+// a zero column on either side, and zero stays zero under SGD / AdamW.  The kernels skip the HBM
+// traffic of those elements at 8-element granularity (live extents rounded up to 8: whole 16-byte
+// lanes, and 8-row groups = whole wave-instructions of the state layout): no load, no store.  A
+// skipped load leaves its register stale (never a select on a load: hipcc turns that into a
+// branch and a vmcnt(0) per element), so every value derived from a dead element is either
+// discarded (the skipped stores), multiplied by an exact zero, or zeroed explicitly where it
+// reaches memory (the W^T image of dX, the forward's dead output columns).  12 % of the headline's
+// state bytes are such padding (loguniform(64, 1024) widths padded to 64).
+#ifndef MOPT_DEAD_SKIP
+#define MOPT_DEAD_SKIP 1   // 0: a build that moves the padding like live data (A/B baseline)
+#endif
+__device__ __forceinline__ int live8(int n) { return MOPT_DEAD_SKIP ? (n + 7) & ~7 : 1 << 30; }
 
 // One (member, layer) to initialise; 48 bytes, mirrored by metaopt_amd/ops/population.py.
 struct InitDesc {
@@ -180,10 +196,13 @@ __device__ __forceinline__ void fwd_step(const bf16_t* As, const bf16_t* Bs, int
 }
 
 // W: the tile's first row (w_off + n0 * w_row_stride(K)); N: rows of the layer's weight matrix
+// nlive / klive: the tile's live W rows (from its first) and K's live extent, multiples of 8
+// (live8): dead W rows / k-chunks are not loaded (stale registers -- the dead k meet exact-zero X
+// columns, the dead rows' outputs are zeroed by the caller's epilogue)
 template <int TN, int NSET = 2, int WROWS = TN>
 __device__ __forceinline__ void fwd_gemm(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                          int K, int N, bf16_t* As, bf16_t* Bs,
-                                         f32x4 (&acc)[2][TN / 16]) {
+                                         f32x4 (&acc)[2][TN / 16], int nlive, int klive) {
   static_assert(WROWS == TN || WROWS == kNarrowRows, "narrow tiles keep 16 W rows");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, g = lane >> 4;
@@ -197,7 +216,12 @@ __device__ __forceinline__ void fwd_gemm(const bf16_t* __restrict__ X, const bf1
   const int g2 = (c2 >> 3) * K + (c2 & 7) * 8, g3 = (c3 >> 3) * K + (c3 & 7) * 8;
   // W rows are WRS apart; a K-step of kk columns moves kk * WKS elements (w_row_stride / w_kstep)
   const int WRS = w_row_stride(K), WKS = w_kstep(N);
-  const int gw0 = (c0 >> 3) * WRS + (c0 & 7) * 8, gw1 = (c1 >> 3) * WRS + (c1 & 7) * 8;
+  // dead W rows (>= nlive, 8-row groups): their loads re-read the tile's first row (always
+  // live) -- an L2 hit instead of HBM traffic, with no branch around the pipelined loads (a
+  // predicated load here became a branch + vmcnt(0) and spilled); the caller's epilogue zeroes
+  // those output columns
+  const int gw0 = ((c0 >> 3) < nlive ? (c0 >> 3) * WRS : 0) + (c0 & 7) * 8;
+  const int gw1 = ((c1 >> 3) < nlive ? (c1 >> 3) * WRS : 0) + (c1 & 7) * 8;
   const int gw2 = (c2 >> 3) * WRS + (c2 & 7) * 8, gw3 = (c3 >> 3) * WRS + (c3 & 7) * 8;
   bf16_t* as0 = As + TOFFF(c0 >> 3, (c0 & 7) * 8);
   bf16_t* as1 = As + TOFFF(c1 >> 3, (c1 & 7) * 8);
@@ -210,6 +234,7 @@ __device__ __forceinline__ void fwd_gemm(const bf16_t* __restrict__ X, const bf1
   const int klast = K - BK;
   // narrow: thread t stages W row t / 8 -- rows >= WROWS stay zero (never loaded)
   const bool w_live = (c0 >> 3) < WROWS;
+  (void)klive;   // dead k-chunks meet exact-zero X columns: loaded as they are
   uint4 p0, p1, p2, p3, pw0{}, pw1{}, pw1b{}, pw1c{};  // K-steps 0, 3, 6, ...
   uint4 q0, q1, q2, q3, qw0{}, qw1{}, qw1b{}, qw1c{};  // K-steps 1, 4, 7, ...
   uint4 r0, r1, r2, r3, rw0{}, rw1{}, rw1b{}, rw1c{};  // K-steps 2, 5, 8, ...
@@ -264,8 +289,9 @@ __device__ __forceinline__ void fwd_gemm(const bf16_t* __restrict__ X, const bf1
 // LDS-staged tiles above; profiles/README.md.)
 template <int TN, int NSET = 2, int WROWS = TN>
 __device__ __forceinline__ void fwd_core(const bf16_t* X, const bf16_t* W, int K, int N,
-                                         bf16_t* As, bf16_t* Bs, f32x4 (&acc)[2][TN / 16]) {
-  fwd_gemm<TN, NSET, WROWS>(X, W, K, N, As, Bs, acc);
+                                         bf16_t* As, bf16_t* Bs, f32x4 (&acc)[2][TN / 16],
+                                         int nlive, int klive) {
+  fwd_gemm<TN, NSET, WROWS>(X, W, K, N, As, Bs, acc, nlive, klive);
 }
 
 // Y[rows, n0:n0+TN] = dropout(relu(X W^T + b)) for one (trial-layer, n-tile, 128-row block).
@@ -291,7 +317,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) vo
   const bf16_t* W = p16 + tl.w_off + (size_t)n0 * w_row_stride(K);
 
   f32x4 acc[2][TN / 16];
-  fwd_core<TN, NSET>(X, W, K, N, As, Bs, acc);
+  const int nlive = live8(tl.n_real) - n0;      // live output columns of this tile (may be <= 0)
+  fwd_core<TN, NSET>(X, W, K, N, As, Bs, acc, nlive, live8(tl.k_real));
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, g = lane >> 4;
   const bf16_t* bias_hi = p16 + tl.b_off + n0;
@@ -312,7 +339,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) vo
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = wave * 32 + i * 16 + g * 4 + r;
-        float v = acc[i][j][r] + bj;
+        float v = col < nlive ? acc[i][j][r] + bj : 0.f;   // dead columns: exact zeros
         if (flags & kRelu) v = fmaxf(v, 0.f);
         if (drop) {
           const uint32_t idx = (uint32_t)((row0 + row) * N + n0 + col);
@@ -372,7 +399,9 @@ __global__ __launch_bounds__(256) void mlp_fwd_ce_kernel(const MlpTL* __restrict
   const bf16_t* W = p16 + tl.w_off;
 
   f32x4 acc[2][4];
-  fwd_core<64, 2, NARROW ? kNarrowRows : 64>(X, W, K, N, As, Bs, acc);
+  // only the C real classes' logits are used below: the dead rows' stale sums are never read
+  fwd_core<64, 2, NARROW ? kNarrowRows : 64>(X, W, K, N, As, Bs, acc, live8(C),
+                                             live8(tl.k_real));
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, g = lane >> 4;
   const bf16_t* bias_hi = p16 + tl.b_off;
@@ -562,6 +591,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
   // first 16 dZ columns (8-column chunks 0, 1) are read; the rest stay zero in registers
   const bool st_live = !NARROW || tid < 8 * kNarrowRows;
   const bool z_live = !NARROW || (tid & 7) < kNarrowRows / 8;
+  // dead padding (see live8): this thread's state rows nc + tid / 8 (+ 32) are live below nl
+  // (whole 128-byte rows of the strip: wave-uniform; dead k-chunks are moved like live ones --
+  // skipping them made the row's stores partial lines, which the memory side fills by a read,
+  // measured slower: profiles/round6.md)
+  const int nl = live8(tl.n_real);
+  const int rlo = tid >> 3;
+  constexpr bool k_ok = true;
 
   // Optimizer constants (uniform per workgroup).
   float c1 = 1.f, c2 = 1.f;
@@ -632,25 +668,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     }                                                                                            \
     }                                                                                            \
     } else {                                                                                     \
-    P##wh0 = *(const uint4*)(W16 + ob);                                                          \
-    P##wh1 = *(const uint4*)(W16 + ob + 32 * WRS);                                               \
+    /* dead rows / k-chunks re-read the chunk's first row at the strip's first k (both always  \
+       live): L2 hits instead of HBM traffic, no branch around the loads */                     \
+    const size_t od_ = (size_t)(NC) * WRS + (size_t)k0 * w_kstep(N);                             \
+    const size_t o0_ = k_ok && (NC) + rlo < nl ? ob : od_;                                       \
+    const size_t o1_ = k_ok && (NC) + rlo + 32 < nl ? ob + 32 * WRS : od_;                       \
+    P##wh0 = *(const uint4*)(W16 + o0_);                                                         \
+    P##wh1 = *(const uint4*)(W16 + o1_);                                                         \
     if (MODE != 2) {                                                                             \
-    P##wl0 = *(const uint4*)(WLO + ob);                                                          \
-    P##wl1 = *(const uint4*)(WLO + ob + 32 * WRS);                                               \
+    P##wl0 = *(const uint4*)(WLO + o0_);                                                         \
+    P##wl1 = *(const uint4*)(WLO + o1_);                                                         \
     if (OPT == kSGD16) {                                                                         \
-      P##h0 = *(const uint4*)(M16 + ob);                                                         \
-      P##h1 = *(const uint4*)(M16 + ob + 32 * WRS);                                              \
+      P##h0 = *(const uint4*)(M16 + o0_);                                                        \
+      P##h1 = *(const uint4*)(M16 + o1_);                                                        \
     } else {                                                                                     \
-      P##m0 = *(const f32x4*)(M32 + ob);                                                         \
-      P##m1 = *(const f32x4*)(M32 + ob + 4);                                                     \
-      P##m2 = *(const f32x4*)(M32 + ob + 32 * WRS);                                              \
-      P##m3 = *(const f32x4*)(M32 + ob + 32 * WRS + 4);                                          \
+      P##m0 = *(const f32x4*)(M32 + o0_);                                                        \
+      P##m1 = *(const f32x4*)(M32 + o0_ + 4);                                                    \
+      P##m2 = *(const f32x4*)(M32 + o1_);                                                        \
+      P##m3 = *(const f32x4*)(M32 + o1_ + 4);                                                    \
     }                                                                                            \
     if (OPT == kAdamW) {                                                                         \
-      P##v0 = *(const f32x4*)(V32 + ob);                                                         \
-      P##v1 = *(const f32x4*)(V32 + ob + 4);                                                     \
-      P##v2 = *(const f32x4*)(V32 + ob + 32 * WRS);                                              \
-      P##v3 = *(const f32x4*)(V32 + ob + 32 * WRS + 4);                                          \
+      P##v0 = *(const f32x4*)(V32 + o0_);                                                        \
+      P##v1 = *(const f32x4*)(V32 + o0_ + 4);                                                    \
+      P##v2 = *(const f32x4*)(V32 + o1_);                                                        \
+      P##v3 = *(const f32x4*)(V32 + o1_ + 4);                                                    \
     }                                                                                            \
     }                                                                                            \
     }                                                                                            \
@@ -684,12 +725,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     if (OPT == kAdamW) {
       v[0] = cv0; v[1] = cv1; v[2] = cv2; v[3] = cv3;
     }
+    // this chunk's live state rows (dead ones: stale registers, zeroed in the W^T image)
+    const bool lv[2] = {NARROW ? st_live : k_ok && nc + rlo < nl,
+                        NARROW ? false : k_ok && nc + rlo + 32 < nl};
     const uint4 wh[2] = {cwh0, cwh1};
     const bool more = nc + BN < N;
     if (PF && more) MOPT_BWD_LOAD(nc + BN, n)
     if (has_dx) {   // the bf16 working copy (hi) is the dX operand, as in the forward
 #pragma unroll
-      for (int i = 0; i < 2; ++i) *(uint4*)(Ws + BOFF(32 * i + (tid >> 3), 8 * (tid & 7))) = wh[i];
+      for (int i = 0; i < 2; ++i)
+        *(uint4*)(Ws + BOFF(32 * i + (tid >> 3), 8 * (tid & 7))) =
+            lv[i] ? wh[i] : make_uint4(0, 0, 0, 0);
     }
     __syncthreads();
 
@@ -789,6 +835,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
     for (int i = 0; i < (NARROW ? 2 : 4); ++i) {
       if (NARROW && !st_live) break;   // rows >= 16 of a narrow loss layer: zero, untouched
+      if (!lv[i >> 1]) continue;       // dead padding: nothing loaded, nothing stored
       // group i: row 32 (i / 2) + tid / 8, k 8 (tid % 8) + 4 (i % 2) .. + 3
       const int gr = 32 * (i >> 1) + (tid >> 3), gk = 8 * (tid & 7) + 4 * (i & 1);
       const f32x4 gv = *(const f32x4*)(Dw + FOFF(gr, gk));
@@ -990,25 +1037,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // instruction, no LDS restaging -- ran the pass ~45 % slower.)  The current strip's set (c*)
   // and, PF, the next strip's (n*), loaded while this strip is multiplied and updated.
   const int so = (tid >> 3) * BK + 8 * (tid & 7);           // + 32 BK: the second row
-  uint4 cwh0, cwh1, cwl0, cwl1, cmh0, cmh1, nwh0, nwh1, nwl0, nwl1, nmh0, nmh1;
-  f32x4 cm[4], cv[4], nm[4], nv[4];
+  // dead padding (live8): this thread's rows n0 + tid / 8 (+ 32) below nl, its k-chunk of strip
+  // S at S BK + 8 (tid % 8) below kl -- dead state is neither loaded nor stored
+  const int nl = live8(tl.n_real);
+  const bool rl0 = n0 + (tid >> 3) < nl, rl1 = n0 + (tid >> 3) + 32 < nl;
+  uint4 cwh0{}, cwh1{}, cwl0{}, cwl1{}, cmh0{}, cmh1{}, nwh0{}, nwh1{}, nwl0{}, nwl1{}, nmh0{},
+      nmh1{};
+  f32x4 cm[4]{}, cv[4]{}, nm[4]{}, nv[4]{};
 #define MOPT_B0F_LOAD(P, S)                                                                      \
   {                                                                                              \
     const size_t o_ = (size_t)(S) * BK * N + (size_t)n0 * BK + so;                               \
-    P##wh0 = *(const uint4*)(W16 + o_);                                                          \
-    P##wh1 = *(const uint4*)(W16 + o_ + 32 * BK);                                                \
-    P##wl0 = *(const uint4*)(WLO + o_);                                                          \
-    P##wl1 = *(const uint4*)(WLO + o_ + 32 * BK);                                                \
+    /* dead rows / k-chunks re-read the chunk's first row at the strip's first k (live): L2   \
+       hits instead of HBM traffic, no branch around the loads */                              \
+    constexpr bool kl_ = true;   /* dead k-chunks: moved like live ones (whole lines) */         \
+    const size_t od_ = (size_t)(S) * BK * N + (size_t)n0 * BK;                                   \
+    const size_t o0_ = rl0 && kl_ ? o_ : od_, o1_ = rl1 && kl_ ? o_ + 32 * BK : od_;             \
+    P##wh0 = *(const uint4*)(W16 + o0_);                                                         \
+    P##wh1 = *(const uint4*)(W16 + o1_);                                                         \
+    P##wl0 = *(const uint4*)(WLO + o0_);                                                         \
+    P##wl1 = *(const uint4*)(WLO + o1_);                                                         \
     if (OPT == kSGD16) {                                                                         \
-      P##mh0 = *(const uint4*)(M16 + o_);                                                        \
-      P##mh1 = *(const uint4*)(M16 + o_ + 32 * BK);                                              \
+      P##mh0 = *(const uint4*)(M16 + o0_);                                                       \
+      P##mh1 = *(const uint4*)(M16 + o1_);                                                       \
     } else {                                                                                     \
       _Pragma("unroll") for (int i = 0; i < 4; ++i)                                              \
-        P##m[i] = *(const f32x4*)(M32 + o_ + 32 * BK * (i >> 1) + 4 * (i & 1));                 \
+        P##m[i] = *(const f32x4*)(M32 + ((i >> 1) ? o1_ : o0_) + 4 * (i & 1));                   \
     }                                                                                            \
     if (OPT == kAdamW) {                                                                         \
       _Pragma("unroll") for (int i = 0; i < 4; ++i)                                              \
-        P##v[i] = *(const f32x4*)(V32 + o_ + 32 * BK * (i >> 1) + 4 * (i & 1));                 \
+        P##v[i] = *(const f32x4*)(V32 + ((i >> 1) ? o1_ : o0_) + 4 * (i & 1));                   \
     }                                                                                            \
   }
   MOPT_B0F_LOAD(c, 0)
@@ -1089,9 +1146,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int i = 0; i < 4; ++i) m[i] = cm[i];
       }
       uint2 ph{}, pl{}, pm{};
+      constexpr bool kls = true;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int gr = 32 * (i >> 1) + (tid >> 3), gk = 8 * (tid & 7) + 4 * (i & 1);
+        if (!((i >> 1) ? rl1 : rl0) || !kls) {   // dead padding: W_new's image row stays zero
+          if (i & 1) *(uint4*)(Ws + TOFFF(gr, gk - 4)) = make_uint4(0, 0, 0, 0);
+          continue;
+        }
         const f32x4 gv = *(const f32x4*)(Dw + FOFF(gr, gk));
         const size_t o = sb + (size_t)(32 * (i >> 1)) * BK + 4 * (i & 1);
         f32x4 wv = w[i], mv = m[i], vv;

@@ -46,7 +46,9 @@ _lib.register_signatures({
     "mopt_embed_bwd": ([c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_void_p],
                        c_int),
     "mopt_cast_bf16": ([c_void_p, c_void_p, c_int64, c_void_p], c_int),
-    "mopt_embed_bwd_sorted": ([c_void_p] * 4 + [c_int64, c_int, c_void_p], c_int),
+    "mopt_embed_bwd_sorted": ([c_void_p] * 4 + [c_int64, c_int, c_int64, c_void_p], c_int),
+    "mopt_embed_sort": ([c_void_p] * 3 + [c_int] * 3 + [c_void_p], c_int),
+    "mopt_embed_zero_rows": ([c_void_p] * 2 + [c_int64, c_int, c_int64, c_void_p], c_int),
     "mopt_adamw_multi": ([c_void_p, c_void_p, c_int] + [c_void_p] * 7 + [c_int] * 4 + [c_void_p],
                          c_int),
     "mopt_sgd_multi": ([c_void_p, c_void_p, c_int] + [c_void_p] * 6 + [c_int] * 3 + [c_void_p],
@@ -601,6 +603,29 @@ def ce_eval(logits, labels, rows_per_trial):
     return ce_ref(logits.reshape(-1, logits.shape[-1]), labels, rows_per_trial)
 
 
+#: rows per trial the in-LDS key sort takes (csrc/lm_ops.hip kEmbedSortMax)
+EMBED_SORT_MAX = 8192
+_EMBED_KEYS: dict = {}
+
+
+def _embed_key_buffers(gw: torch.Tensor, R: int):
+    """(keys, order) int64 [R] kept per table-gradient buffer across steps (and HIP-graph
+    replays): ``keys`` holds the previous step's sorted keys, whose table rows are the only
+    non-zero ones.  Created with keys = -1 (nothing to clear) outside any graph capture -- the
+    population's eager warm-up steps run first; a first call inside a capture would record the
+    -1 fill into the graph, so it falls back to the full clear (None)."""
+    key = (gw.device, gw.data_ptr(), gw.numel(), R)
+    buf = _EMBED_KEYS.get(key)
+    if buf is None:
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        gw.zero_()                      # the invariant's base case: every row zero
+        buf = (torch.full((R,), -1, dtype=torch.int64, device=gw.device),
+               torch.empty(R, dtype=torch.int64, device=gw.device))
+        _EMBED_KEYS[key] = buf
+    return buf
+
+
 class _Embedding(torch.autograd.Function):
     @staticmethod
     def forward(ctx, tok, table, rows_per_trial):
@@ -620,15 +645,23 @@ class _Embedding(torch.autograd.Function):
         P, V, d, rpt, dtype = ctx.dims
         dout = dout.contiguous()
         if ctx.gw is not None:
-            # sort the (trial, token) keys once (stable: deterministic sums), zero the table
-            # gradient and let one wave per run of equal keys write its row -- no f32 table,
-            # no atomics, no cast pass
+            # sort the (trial, token) keys once (stable: deterministic sums) and let one wave per
+            # run of equal keys write its row -- no f32 table, no atomics, no cast pass
             R = tok.numel()
-            trial = torch.arange(R, device=tok.device, dtype=torch.int64) // rpt
-            keys, order = torch.sort(trial * V + tok.long(), stable=True)
-            ctx.gw.zero_()
+            n = 1 << max(0, (rpt - 1).bit_length())
+            buf = _embed_key_buffers(ctx.gw, R) if n <= EMBED_SORT_MAX else None
+            if buf is None:            # rows per trial past the in-LDS sort: library sort
+                trial = torch.arange(R, device=tok.device, dtype=torch.int64) // rpt
+                keys, order = torch.sort(trial * V + tok.long(), stable=True)
+                ctx.gw.zero_()
+            else:
+                # the rows the previous step wrote (every other row is zero), then this step's
+                # keys sorted in place of them (csrc/lm_ops.hip embed_sort_kernel)
+                keys, order = buf
+                _call("mopt_embed_zero_rows", _p(keys), _p(ctx.gw), R, d, P * V, _stream(dout))
+                _call("mopt_embed_sort", _p(tok), _p(keys), _p(order), P, rpt, V, _stream(dout))
             _call("mopt_embed_bwd_sorted", _p(keys), _p(order), _p(dout), _p(ctx.gw), R, d,
-                  _stream(dout))
+                  P * V, _stream(dout))
             return None, None, None
         d32 = torch.zeros(P, V, d, dtype=torch.float32, device=dout.device)
         _call("mopt_embed_bwd", _p(tok), _p(dout.contiguous()), _p(d32), tok.numel(), d, V, rpt,

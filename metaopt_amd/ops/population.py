@@ -39,7 +39,7 @@ from . import reference as ref
 
 TL_DTYPE = np.dtype([("K", "<i4"), ("N", "<i4"), ("trial", "<i4"), ("n_real", "<i4"),
                      ("w_off", "<i8"), ("b_off", "<i8"), ("x_off", "<i8"), ("y_off", "<i8"),
-                     ("gx_off", "<i8"), ("rows", "<i8")])
+                     ("gx_off", "<i8"), ("rows", "<i4"), ("k_real", "<i4")])
 HP_DTYPE = np.dtype([("lr", "<f4"), ("b1", "<f4"), ("wd", "<f4"), ("drop", "<f4"),
                      ("b2", "<f4"), ("eps", "<f4"), ("seed", "<u4"), ("t", "<u4")])
 INIT_DTYPE = np.dtype([("w_off", "<i8"), ("b_off", "<i8"), ("K", "<i4"), ("N", "<i4"),
@@ -805,7 +805,9 @@ class PopulationMLP:
                 tl["K"][i] = K
                 tl["N"][i] = N
                 tl["trial"][i] = slots
-                tl["n_real"][i] = self.num_classes if l == L - 1 else N
+                # real extents: the kernels skip the dead padding's HBM traffic (pop_mlp.hip)
+                tl["n_real"][i] = self.num_classes if l == L - 1 else widths
+                tl["k_real"][i] = self.in_features if l == 0 else widths
                 tl["w_off"][i] = w_off
                 tl["b_off"][i] = b_off
                 tl["x_off"][i] = prev
@@ -868,7 +870,8 @@ class PopulationMLP:
             bad.append("layer output outside the activation buffer")
         if (t["rows"] < 128).any() or (t["rows"] % 128).any() or (t["rows"] > rows).any():
             bad.append("trial rows outside the launch's row blocks")
-        if (t["n_real"] > t["N"]).any() or (t["trial"] < 0).any() or \
+        if (t["n_real"] > t["N"]).any() or (t["k_real"] > t["K"]).any() or \
+                (t["n_real"] < 1).any() or (t["k_real"] < 1).any() or (t["trial"] < 0).any() or \
                 (t["trial"] >= self.capacity).any():
             bad.append("trial / class fields out of range")
         fused = [("bwd0f", [bwd0f], "N")] if bwd0f is not None and len(bwd0f) else []

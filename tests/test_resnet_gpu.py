@@ -277,19 +277,25 @@ def test_fused_head_matches_fp32_reference(P, B, HW, C):
 
 def test_config3_task_is_learnable_by_default_member():
     """config 3's synthetic task must be learnable by ResNet-20 within the
-    390-step trial budget, or TPE-vs-random compares noise.  A default member (lr 0.1, momentum
-    0.9, weight decay 5e-4) reaches a validation loss <= 0.7 H(y) after 390 steps of 128 images
-    (the label entropy measured on the validation labels)."""
+    390-step trial budget, or TPE-vs-random compares noise.  Members at lr 0.1 (the default),
+    0.05 and 0.02 (momentum 0.9, weight decay 5e-4) after 390 steps of 128 images: the median
+    validation loss <= 0.7 H(y), the best <= 0.35 H(y) (the label entropy measured on the
+    validation labels), an lr-0 control stays near H(y).  The median, because the validation
+    loss of a single lr-0.1 member spikes between evaluations (BatchNorm running statistics at a
+    high learning rate; scripts/dev/config3_learnability.py on the box: 0.03-0.58 at step 390,
+    up to 3.4 at step 195, training loss 0.002-0.03)."""
     from metaopt_amd.models.resnet import PopulationResNet, SyntheticCIFAR
     from metaopt_amd.ops.population import MemberConfig
     data = SyntheticCIFAR(n_train=390 * 128, n_val=1024, batch_size=128, seed=0, device=DEV)
-    pop = PopulationResNet(2, batch_size=128, device=DEV, blocks_per_stage=3, image_size=32)
-    pop.set_member(0, MemberConfig(width=0, lr=0.1, momentum=0.9, weight_decay=5e-4, seed=1))
-    pop.set_member(1, MemberConfig(width=0, lr=0.0, momentum=0.9, weight_decay=0.0, seed=2))
+    pop = PopulationResNet(4, batch_size=128, device=DEV, blocks_per_stage=3, image_size=32)
+    for s, lr in enumerate((0.1, 0.05, 0.02, 0.0)):
+        pop.set_member(s, MemberConfig(width=0, lr=lr, momentum=0.9, weight_decay=5e-4,
+                                       seed=1 + s))
     for step in range(390):
         pop.train_step(*data.batch(step))
     vl, va = pop.evaluate(*data.validation())
     p = torch.bincount(data.val_y.cpu(), minlength=10).double() / len(data.val_y)
     h = float(-(p[p > 0] * p[p > 0].log()).sum())
-    assert vl[0] <= 0.7 * h, (vl, h)
-    assert vl[1] > 0.9 * h, (vl, h)                  # an untrained member sits near H(y)
+    assert float(np.median(vl[:3])) <= 0.7 * h, (vl, h)
+    assert float(np.min(vl[:3])) <= 0.35 * h, (vl, h)
+    assert vl[3] > 0.9 * h, (vl, h)                  # an untrained member sits near H(y)
