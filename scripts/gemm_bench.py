@@ -17,7 +17,11 @@ SHAPES = [
     ("lm.qkv.dx", 8, 4096, 768, 2304, False, True),
     ("lm.qkv.dw", 8, 768, 2304, 4096, True, False),
     ("lm.wo.fwd", 8, 4096, 768, 768, False, False),
+    ("lm.wo.dx", 8, 4096, 768, 768, False, True),
+    ("lm.wo.dw", 8, 768, 768, 4096, True, False),
     ("lm.gu.fwd", 8, 4096, 4096, 768, False, False),
+    ("lm.gu.dx", 8, 4096, 768, 4096, False, True),
+    ("lm.gu.dw", 8, 768, 4096, 4096, True, False),
     ("lm.down.fwd", 8, 4096, 768, 2048, False, False),
     ("lm.down.dx", 8, 4096, 2048, 768, False, True),
     ("lm.down.dw", 8, 2048, 768, 4096, True, False),
