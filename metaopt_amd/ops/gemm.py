@@ -139,11 +139,24 @@ def _plan_big(P: int, M: int, N: int, K: int):
     return cfg, s, K // s
 
 
+#: measured exceptions to the planner's model, (P, M, N, K) -> (cfg, splits): the LM-125M
+#: weight gradients whose best tile the fill model misjudges -- a persistent 1.5-wave tail runs
+#: faster than its idle fraction suggests (profiles/r6/gemm/lm_tile_split_sweep.json, TFLOP/s):
+#: gate/up dW 768 x 4096 x 4096 cfg 5 981 vs the modelled cfg 6 908; attention-out dW 768 x 768 x
+#: 4096 cfg 7 650 vs cfg 11 split 2 590
+MEASURED_PLANS = {(8, 768, 4096, 4096): (5, 1), (8, 768, 768, 4096): (7, 1)}
+
+
 def plan(P: int, M: int, N: int, K: int, cfg: Optional[int] = None,
          splits: Optional[int] = None):
     """(tile cfg, splits, k_per_split) for a [P] x (M x K) . (K x N) problem: a big tile when it
     divides the shape and fills the chip, else a small one with the K reduction split when the
     output tiles alone give fewer than ~2 workgroups per CU."""
+    if cfg is None and splits is None and (P, M, N, K) in MEASURED_PLANS:
+        cfg, splits = MEASURED_PLANS[(P, M, N, K)]
+        if big_fits(M, N, K, cfg) and K % (64 * splits) == 0:
+            return cfg, splits, K // splits
+        cfg = splits = None
     if cfg is None and splits is None:
         big = _plan_big(P, M, N, K)
         if big is not None:

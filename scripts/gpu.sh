@@ -17,6 +17,7 @@
 #   pmc_kbench       PMC passes of the MLP kernels (fetch/write/MFMA/LDS, one pass each)
 #   pmc_gemm         PMC passes of the GEMM microbench ($SHAPES name prefix, $CFGS tile configs)
 #   lm resnet hyper  bench_configs.py of one config        trace_lm trace_resnet trace_hyper
+#   attn             attention fwd / bwd microbench (LM-125M shape)
 #   gemm conv        pgemm / direct-conv microbenches      gemm32  f32-operand (K11) GEMM plans
 #   c4copy           one config-5 member: slot <-> pool copies, packed C4 path, copy_member
 #   decide           rank-0 decide cost at simulated W=1,8 (host CPU of the box)
@@ -90,6 +91,7 @@ for step in "$@"; do
     trace_lm)   prof trace_lm 300 -- python3 "$ROOT/scripts/bench_configs.py" --config lm-125m --sync-every 2 --steps 6 --warmup 4 ;;
     trace_resnet) prof trace_resnet 300 -- python3 "$ROOT/scripts/bench_configs.py" --config resnet20 --sync-every 10 --steps 20 --warmup 10 ;;
     trace_hyper) prof trace_hyper 300 -- python3 "$ROOT/scripts/bench_configs.py" --config hyper --steps 1 --warmup 1 ;;
+    attn)       $T 200 python scripts/attn_bench.py --out "$OUT/attn.json" > "$OUT/attn.log" 2>&1 ;;
     gemm)       $T 300 python scripts/gemm_bench.py --cfgs "${CFGS:-0,5,6,7}" --splits "${SPLITS:-}" --out "$OUT/gemm.json" > "$OUT/gemm.log" 2>&1 ;;
     gemm32)     $T 300 python scripts/gemm_f32_bench.py --out "$OUT/gemm32.json" > "$OUT/gemm32.log" 2>&1 ;;
     conv)       $T 200 python scripts/conv_bench.py --implicit --out "$OUT/conv_bench.json" > "$OUT/conv_bench.log" 2>&1 ;;

@@ -5,7 +5,7 @@ tests/test_pgemm_gpu.py)."""
 import pytest
 import torch
 
-from metaopt_amd.ops.gemm import BIG_TILES, TILES, f32_plan, pgemm, plan
+from metaopt_amd.ops.gemm import BIG_TILES, TILES, big_fits, f32_plan, pgemm, plan
 
 
 @pytest.mark.parametrize("M,N,ta,want", [(1536, 768, False, 3), (1536, 4096, False, 4),
@@ -75,3 +75,15 @@ def test_cpu_bn_into_conv_is_gpu_only():
     w = torch.zeros(2, 9 * 16, 16)
     arena = object()
     assert not cops.bn_into_conv_ok(x, w, 2, 1, True, arena, True)
+
+
+def test_measured_plans_override_the_model_for_their_shapes_only():
+    """MEASURED_PLANS (profiles/r6/gemm/lm_tile_split_sweep.json) pick the measured-best tile of
+    the LM's gate/up and attention-out weight gradients; other populations keep the model."""
+    from metaopt_amd.ops.gemm import MEASURED_PLANS
+    for (P, M, N, K), (cfg, sp) in MEASURED_PLANS.items():
+        assert plan(P, M, N, K) == (cfg, sp, K // sp)
+        assert big_fits(M, N, K, cfg)
+    from metaopt_amd.ops.gemm import _plan_big
+    assert plan(16, 768, 768, 4096) == _plan_big(16, 768, 768, 4096)    # not in the table
+    assert plan(8, 768, 4096, 4096, cfg=6, splits=1) == (6, 1, 4096)   # explicit requests win
