@@ -402,8 +402,7 @@ __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnDkdvWaves) void attn_bwd_
                                                             bf16_t* __restrict__ dK,
                                                             bf16_t* __restrict__ dV, int T, int H,
                                                             float c, float scale, int n_bh,
-                                                            const RopeOut ro,
-                                                            bf16_t* __restrict__ dST) {
+                                                            const RopeOut ro) {
   __shared__ __attribute__((aligned(16))) bf16_t Qs[tile_elems<false>()];
   __shared__ __attribute__((aligned(16))) bf16_t dOs[tile_elems<false>()];
   __shared__ __attribute__((aligned(16))) float lse_s[BQ];
@@ -487,9 +486,6 @@ __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnDkdvWaves) void attn_bwd_
     for (int s = 0; s < 2; ++s) {
       const bf16x8 pa = pack_frag(st[2 * s], st[2 * s + 1]);
       const bf16x8 sa = pack_frag(dp[2 * s], dp[2 * s + 1]);
-      // dS^T[key][queries 32 s + 8 g .. + 7] for attn_bwd_dq_ds_kernel (16 bytes per lane)
-      if (dST != nullptr)
-        *(bf16x8*)(dST + ((size_t)bh * T + krow) * T + qb * BQ + 32 * s + 8 * g) = sa;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         // dV^T[dh][key] += dO^T P^T : A = dO^T (tr-read), B = P^T fragment (this lane's key)
@@ -509,65 +505,6 @@ __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnDkdvWaves) void attn_bwd_
     put_grad4(ovp + 16 * dt + 4 * g, ro, 2, bh, H, T, krow, 16 * dt + 4 * g, xv);
   }
 #undef MOPT_DKDV_LOAD
-}
-
-// dQ = scale * sum_k dS K from the dS^T tiles attn_bwd_dkdv_kernel stored (round 6): the score,
-// softmax and dP products the dQ kernel above recomputes per key block are gone -- per block only
-// the dS^T and K tiles are staged and dQ^T += K^T dS^T (A = K^T by transposed reads of the K tile,
-// B = dS^T's column of this lane's query by transposed reads of the dS^T tile; the same MFMA
-// operands as attn_bwd_dq_kernel's, with dS in the bf16 the MFMA consumed there).  The causal
-// mask is in dS (zero past the diagonal).  grid (T/64) BH, 4 waves x 16 queries.
-__global__ __launch_bounds__(256) void attn_bwd_dq_ds_kernel(const bf16_t* __restrict__ K,
-                                                             const bf16_t* __restrict__ dST,
-                                                             bf16_t* __restrict__ dQ, int T, int H,
-                                                             float scale, int n_bh,
-                                                             const RopeOut ro) {
-  __shared__ __attribute__((aligned(16))) bf16_t Ks[tile_elems<false>()];
-  __shared__ __attribute__((aligned(16))) bf16_t Ss[tile_elems<false>()];
-  const int nqb = T / BQ;
-  const int2 hb = head_block(nqb, n_bh);
-  const int qb = nqb - 1 - hb.x;
-  const int bh = hb.y;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int li = lane & 15, g = lane >> 4, q = li >> 2, pp = li & 3;
-  const size_t base = (size_t)bh * T * D;
-  const int qrow = qb * BQ + wave * 16 + li;
-  // this thread's two rows of the dS^T tile of key block kb: keys kb 64 + tid / 8 (+ 32),
-  // query columns qb 64 + 8 (tid % 8)
-  const bf16_t* sbase = dST + ((size_t)bh * T + (tid >> 3)) * T + qb * BQ + (tid & 7) * 8;
-  const size_t srow32 = (size_t)32 * T;
-  f32x4 acc[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) acc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  uint4 ka, kc, sa, sc;
-  tile_load(K + base, ka, kc, tid);
-  sa = *(const uint4*)sbase;
-  sc = *(const uint4*)(sbase + srow32);
-  for (int kb = 0; kb <= qb; ++kb) {
-    __syncthreads();
-    tile_store<false>(ka, kc, Ks, tid);
-    tile_store<false>(sa, sc, Ss, tid);
-    __syncthreads();
-    {
-      const int nb = min(kb + 1, qb);                 // clamped: no branch around the loads
-      tile_load(K + base + (size_t)nb * BKV * D, ka, kc, tid);
-      const bf16_t* sp = sbase + (size_t)nb * BKV * T;
-      sa = *(const uint4*)sp;
-      sc = *(const uint4*)(sp + srow32);
-    }
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const bf16x8 sb = tr_frag<false>(Ss, s, g, q, pp, wave);   // dS^T[keys][query qrow]
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma16(tr_frag<false>(Ks, s, g, q, pp, dt), sb, acc[dt]);
-    }
-  }
-  bf16_t* out = dQ + base + (size_t)qrow * D;
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) {
-    float x[4] = {acc[dt][0] * scale, acc[dt][1] * scale, acc[dt][2] * scale, acc[dt][3] * scale};
-    put_grad4(out + 16 * dt + 4 * g, ro, 0, bh, H, T, qrow, 16 * dt + 4 * g, x);
-  }
 }
 
 }  // namespace
@@ -606,35 +543,10 @@ int mopt_attn_bwd(const void* q, const void* k, const void* v, const void* o, co
   hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((T / 64) * bh), dim3(256), 0, st,
                      (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout,
                      (const float*)lse2, (const float*)dsum, (bf16_t*)dk, (bf16_t*)dv, T, H, c,
-                     scale, bh, ro, (bf16_t*)nullptr);
+                     scale, bh, ro);
   hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((T / 64) * bh), dim3(256), 0, st, (const bf16_t*)q,
                      (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, (const float*)lse2,
                      (const float*)dsum, (bf16_t*)dq, T, H, c, scale, bh, ro);
-  return (int)hipGetLastError();
-}
-
-// mopt_attn_bwd with dS materialised: ds_ws is a bf16 [bh][T][T] workspace (only the causal
-// block triangle is written and read): the dK/dV kernel stores dS^T, the dQ kernel multiplies it
-// (attn_bwd_dq_ds_kernel) instead of recomputing scores, softmax and dP.
-int mopt_attn_bwd_ds(const void* q, const void* k, const void* v, const void* o, const void* dout,
-                     const void* lse2, void* dsum, void* dq, void* dk, void* dv, int bh, int T,
-                     int H, float scale, void* dqkv, const void* cosT, const void* sinT,
-                     void* ds_ws, void* stream) {
-  if (T % 64 || bh <= 0 || ds_ws == nullptr ||
-      (dqkv != nullptr && (cosT == nullptr || sinT == nullptr)))
-    return 1;
-  const float c = scale * 1.4426950408889634f;
-  const int rows = bh * T;
-  const RopeOut ro{(bf16_t*)dqkv, (const float*)cosT, (const float*)sinT};
-  hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((rows + 255) / 256), dim3(256), 0, st,
-                     (const bf16_t*)o, (const bf16_t*)dout, (float*)dsum, T, H, rows);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((T / 64) * bh), dim3(256), 0, st,
-                     (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout,
-                     (const float*)lse2, (const float*)dsum, (bf16_t*)dk, (bf16_t*)dv, T, H, c,
-                     scale, bh, ro, (bf16_t*)ds_ws);
-  hipLaunchKernelGGL(attn_bwd_dq_ds_kernel, dim3((T / 64) * bh), dim3(256), 0, st,
-                     (const bf16_t*)k, (const bf16_t*)ds_ws, (bf16_t*)dq, T, H, scale, bh, ro);
   return (int)hipGetLastError();
 }
 

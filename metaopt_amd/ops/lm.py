@@ -25,8 +25,6 @@ c_void_p, c_int, c_float, c_int64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_floa
 _lib.register_signatures({
     "mopt_attn_fwd": ([c_void_p] * 5 + [c_int, c_int, c_int, c_float, c_void_p], c_int),
     "mopt_attn_bwd": ([c_void_p] * 10 + [c_int, c_int, c_int, c_float] + [c_void_p] * 4, c_int),
-    "mopt_attn_bwd_ds": ([c_void_p] * 10 + [c_int, c_int, c_int, c_float] + [c_void_p] * 5,
-                         c_int),
     "mopt_rmsnorm_fwd": ([c_void_p] * 4 + [c_int, c_int, c_int, c_float, c_void_p], c_int),
     "mopt_rmsnorm_bwd": ([c_void_p] * 6 + [c_int, c_int, c_int, c_void_p], c_int),
     "mopt_add_rmsnorm_fwd": ([c_void_p] * 6 + [c_int, c_int, c_int, c_float, c_void_p], c_int),
@@ -383,9 +381,9 @@ class _QKVRopeAttention(torch.autograd.Function):
         do = do.contiguous()
         dqkv = torch.empty(P, R, 3 * d, dtype=h.dtype, device=h.device)
         dsum = torch.empty_like(lse)
-        _attn_bwd(h.device, _p(buf[0]), _p(buf[1]), _p(buf[2]), _p(o), _p(do), _p(lse),
-                  _p(dsum), None, None, None, P * (R // T) * H, T, H, scale, _p(dqkv), _p(cos),
-                  _p(sin), _stream(h))
+        _call("mopt_attn_bwd", _p(buf[0]), _p(buf[1]), _p(buf[2]), _p(o), _p(do), _p(lse),
+              _p(dsum), None, None, None, P * (R // T) * H, T, H, scale, _p(dqkv), _p(cos),
+              _p(sin), _stream(h))
         dw = None
         if ctx.g_w is not None:
             pgemm(h, dqkv, ta=True, out=ctx.g_w)
@@ -414,25 +412,6 @@ def qkv_rope(h, w, cos, sin, T, H):
     return rope_split_ref(torch.bmm(h, w).reshape(P * R, 3 * d), cos, sin, T, H, il=True)
 
 
-#: largest dS workspace (bytes) the attention backward materialises; longer sequences recompute
-#: the scores in the dQ kernel instead (csrc/lm_attn.hip attn_bwd_dq_kernel)
-ATTN_DS_MAX_BYTES = 2 << 30
-
-
-def _attn_bwd(device, q, k, v, o, do, lse, dsum, dq, dk, dv, bh, T, H, scale, dqkv, cos, sin,
-              stream):
-    """The attention backward: with dS materialised (a bf16 [bh, T, T] workspace from the caching
-    allocator, MOPT_ATTN_DS != 0) when it fits ATTN_DS_MAX_BYTES -- the dK/dV kernel writes dS^T
-    and the dQ kernel multiplies it -- else the recomputing dQ kernel."""
-    if os.environ.get("MOPT_ATTN_DS", "1") != "0" and 2 * bh * T * T <= ATTN_DS_MAX_BYTES:
-        ws = torch.empty(bh, T, T, dtype=torch.bfloat16, device=device)
-        _call("mopt_attn_bwd_ds", q, k, v, o, do, lse, dsum, dq, dk, dv, bh, T, H, scale, dqkv,
-              cos, sin, _p(ws), stream)
-        return
-    _call("mopt_attn_bwd", q, k, v, o, do, lse, dsum, dq, dk, dv, bh, T, H, scale, dqkv, cos,
-          sin, stream)
-
-
 class _Attention(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, scale):
@@ -454,8 +433,8 @@ class _Attention(torch.autograd.Function):
         do = do.contiguous()
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         dsum = torch.empty_like(lse)
-        _attn_bwd(q.device, _p(q), _p(k), _p(v), _p(o), _p(do), _p(lse), _p(dsum), _p(dq),
-                  _p(dk), _p(dv), Bp * H, T, H, ctx.scale, None, None, None, _stream(q))
+        _call("mopt_attn_bwd", _p(q), _p(k), _p(v), _p(o), _p(do), _p(lse), _p(dsum), _p(dq),
+              _p(dk), _p(dv), Bp * H, T, H, ctx.scale, None, None, None, _stream(q))
         return dq, dk, dv, None
 
 
