@@ -15,6 +15,7 @@
 #   kbench_ab        the microbench per kernel variant (env $ABVAR set to each of $VARIANTS)
 #   kbench_rows      the microbench at 128 / 256 / 512 rows per step (multi-row-block kernels)
 #   pmc_kbench       PMC passes of the MLP kernels (fetch/write/MFMA/LDS, one pass each)
+#   pmc_attn         PMC passes of the attention microbench (busy / wait / MFMA, LDS / VALU)
 #   pmc_gemm         PMC passes of the GEMM microbench ($SHAPES name prefix, $CFGS tile configs)
 #   lm resnet hyper  bench_configs.py of one config        trace_lm trace_resnet trace_hyper
 #   attn             attention fwd / bwd microbench (LM-125M shape)
@@ -58,6 +59,13 @@ pmcg() {   # pmcg NAME COUNTERS...: one counter pass over the GEMM microbench ($
       --cfgs "${CFGS:-11,12}" > "$ROOT/$OUT/$name.log" 2>&1)
 }
 
+pmca() {   # pmca NAME COUNTERS...: one counter pass over the attention microbench
+  local name=$1; shift
+  (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 150 rocprofv3 --output-format csv \
+      --pmc "$@" -d "$ROOT/$OUT/$name" -o run -- \
+      python3 "$ROOT/scripts/attn_bench.py" --iters 3 > "$ROOT/$OUT/$name.log" 2>&1)
+}
+
 for step in "$@"; do
   echo "[gpu.sh] $step"
   case "$step" in
@@ -85,6 +93,9 @@ for step in "$@"; do
       pmcg pmcg_busy SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE
       pmcg pmcg_lds SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES
       pmcg pmcg_fetch FETCH_SIZE ;;
+    pmc_attn)   # PMC passes of the attention kernels
+      pmca pmca_busy SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE
+      pmca pmca_lds SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES ;;
     lm)         $T 300 python scripts/bench_configs.py --config lm-125m --steps 600 --warmup 0 > "$OUT/lm.json" 2> "$OUT/lm.err" ;;
     resnet)     $T 300 python scripts/bench_configs.py --config resnet20 --steps 60 --warmup 30 > "$OUT/resnet20.json" 2> "$OUT/resnet20.err" ;;
     hyper)      $T 300 python scripts/bench_configs.py --config hyper --steps 3 --warmup 1 > "$OUT/hyper.json" 2> "$OUT/hyper.err" ;;
