@@ -99,17 +99,20 @@ class PopulationResNet(FlatPopulation):
         return cops.conv_bn_act(x, w, W[f"{name}.g"], W[f"{name}.b"], running, P, stride, train,
                                 res=res, relu=relu, arena=arena, **mail)
 
-    def _block_fused(self, n1, n2, h, s1, identity, arena, box):
+    def _block_fused(self, n1, n2, h, s1, identity, arena, box, in_link=None, out_link=None):
         """One training basic block on the HIP path: conv1 (+ its BatchNorm's batch sums),
         BatchNorm 1 + ReLU applied inside conv2 (``bn_relu_conv3x3``: its output never reaches
         HBM) when the shapes allow, BatchNorm 2 + shortcut + ReLU; the shortcut's gradient joins
-        conv1's data gradient in its epilogue (``box``)."""
+        conv1's data gradient in its epilogue (``box``).  ``in_link``: the link of the BatchNorm
+        that produced h (the previous block's BatchNorm 2, or the stem's), whose relu' masking and
+        reductions conv1's data gradient takes over; ``out_link`` is this block's own."""
         P, W = self.capacity, self.W
         w1, w2 = W[f"{n1}.w"], W[f"{n2}.w"]
         c1, c2 = w1.shape[-1], w2.shape[-1]
         run1 = self.A[f"{n1}.running"].view(P, 2, c1)
         run2 = self.A[f"{n2}.running"].view(P, 2, c2)
-        y1, st1 = cops.conv_stats(h, w1, P, s1, True, arena=arena, mailbox=box)
+        y1, st1 = cops.conv_stats(h, w1, P, s1, True, arena=arena, mailbox=box,
+                                  bn_link=in_link)
         if cops.bn_into_conv_ok(y1, w2, P, 1, True, arena, st1 is not None):
             y2, st2 = cops.bn_relu_conv3x3(y1, W[f"{n1}.g"], W[f"{n1}.b"], run1, w2, P, st1,
                                            arena)
@@ -118,7 +121,8 @@ class PopulationResNet(FlatPopulation):
                             arena=arena)
             y2, st2 = cops.conv_stats(t, w2, P, 1, True, arena=arena)
         return cops.bn_act(y2, W[f"{n2}.g"], W[f"{n2}.b"], run2, P, True, res=h.detach(),
-                           sums=st2, arena=arena, mailbox=box, res_sub2=not identity)
+                           sums=st2, arena=arena, mailbox=box, res_sub2=not identity,
+                           link=out_link)
 
     @staticmethod
     def _shortcut(x, cout, stride):
@@ -135,7 +139,10 @@ class PopulationResNet(FlatPopulation):
                  if train and x.device.type == "cuda" else None)
         it = iter(self.layout)
         name, _, cout, stride = next(it)
-        h = self._conv_bn(name, h, stride, train, arena=arena)
+        # each block output's BatchNorm hands its backward's masking and reductions to the next
+        # block's first data gradient (ops/conv.py _bn_res_dgrad): one link dict per BatchNorm
+        link = {} if arena is not None else None
+        h = self._conv_bn(name, h, stride, train, arena=arena, link=link)
         for si in range(len(STAGES)):
             for b in range(self.blocks):
                 n1, _, c1, s1 = next(it)
@@ -146,8 +153,11 @@ class PopulationResNet(FlatPopulation):
                     # kernel's epilogue (no separate add over the block input); an option-A
                     # shortcut is also read in place by the BatchNorm (no padded copy)
                     box = {}
-                    h = self._block_fused(n1, n2, h, s1, identity, arena, box)
+                    out_link = {}
+                    h = self._block_fused(n1, n2, h, s1, identity, arena, box, link, out_link)
+                    link = out_link
                     continue
+                link = None
                 r = self._shortcut(h, c2, s1)
                 t = self._conv_bn(n1, h, s1, train, arena=arena)
                 h = self._conv_bn(n2, t, 1, train, res=r, arena=arena)

@@ -15,6 +15,7 @@ numerics oracle of tests/test_resnet_gpu.py.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -32,6 +33,7 @@ _lib.register_signatures({
     "mopt_dconv_wgrad_splits": ([c_int] * 6, c_int),
     "mopt_dconv_bnin": ([c_int] + [c_void_p] * 4 + [c_int] * 5 + [c_void_p] * 4, c_int),
     "mopt_dconv_dgrad_bnsums": ([c_void_p] * 4 + [c_int] * 5 + [c_void_p] * 5, c_int),
+    "mopt_dconv_dgrad_bnres": ([c_void_p] * 5 + [c_int] * 7 + [c_void_p] * 4, c_int),
     "mopt_resnet_head": ([c_void_p] * 4 + [c_int] * 5 + [c_float, c_int] + [c_void_p] * 7,
                          c_int),
     "mopt_resnet_head_part_floats": ([c_int] * 3, c_int),
@@ -39,6 +41,10 @@ _lib.register_signatures({
 # BatchNorm 1 + ReLU applied while conv 2 stages its input (6.71 -> 6.55 ms/step, round 3); the
 # materialised path remains for evaluation and shapes the fused kernels do not take
 _BN_INTO_CONV = True
+# the backward of a block output's BatchNorm (relu(BN(x) + shortcut)) fused into the data
+# gradient of the next block's first convolution (``_bn_res_dgrad``; MOPT_BN_RES_DGRAD=0: the
+# separate reduce + apply passes, for A/B runs)
+_BN_RES_DGRAD = os.environ.get("MOPT_BN_RES_DGRAD", "1") != "0"
 
 _NOT_SUPPORTED = 801   # hipErrorNotSupported: no direct-conv instantiation for the shape
 # direct convolution kernels for square inputs; the implicit GEMM (pgemm gathers) is the
@@ -151,9 +157,30 @@ def _pconv(kind, a, b, out, P, Bn, H, W, Ci, Co, stride, sums=None, addend=None,
     return out, False
 
 
+def _bn_res_dgrad(dy, w, dx, addend, sub2, link, P, Bn, H, W, Ci, Co, stride) -> bool:
+    """Data gradient of a convolution whose input is the output of a linked BatchNorm (``link``,
+    filled by ``_BNAct.forward``: relu(BN(x) + shortcut) of the previous block, or the stem's
+    relu(BN(x))): dx = (dgrad(dy) + addend) relu'(link y), the gradient behind that ReLU, and the
+    BatchNorm backward's reductions added into its zeroed ``link["sums"]``
+    (csrc/conv_direct.hip ``mopt_dconv_dgrad_bnres``).  False when the shape has no kernel: the
+    caller runs the plain data gradient and the BatchNorm its own reduction."""
+    if not (_BN_RES_DGRAD and _DIRECT and H == W and addend is not None):
+        return False
+    if (stride == 2) != bool(sub2):
+        return False
+    rc = _lib.get_lib().mopt_dconv_dgrad_bnres(
+        dy.data_ptr(), w.data_ptr(), dx.data_ptr(), addend.data_ptr(), link["sums"].data_ptr(),
+        P, Bn, H, Ci, Co, stride, addend.shape[-1] if sub2 else 0, link["x"].data_ptr(),
+        link["y"].data_ptr(), link["stat"].data_ptr(), _s(dx))
+    if rc == _NOT_SUPPORTED:
+        return False
+    _lib.check(rc, "mopt_dconv_dgrad_bnres")
+    return True
+
+
 class _Conv3x3(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, P, stride, grad_out, stats=None, mailbox=None):
+    def forward(ctx, x, w, P, stride, grad_out, stats=None, mailbox=None, bn_link=None):
         N, H, W, Ci = x.shape
         Co = w.shape[-1]
         Bn = N // P
@@ -169,6 +196,7 @@ class _Conv3x3(torch.autograd.Function):
         ctx.meta = (P, Bn, H, W, Ci, Co, stride)
         ctx.grad_out = grad_out
         ctx.mailbox = mailbox
+        ctx.bn_link = bn_link
         return y
 
     @staticmethod
@@ -183,18 +211,23 @@ class _Conv3x3(torch.autograd.Function):
             # in the data-gradient epilogue, instead of in a separate autograd add
             addend = ctx.mailbox.pop("dres", None) if ctx.mailbox is not None else None
             sub2 = addend is not None and ctx.mailbox.pop("sub2", False)
-            _pconv(1, dy, w, dx, P, Bn, H, W, Ci, Co, stride, addend=addend,
-                   addend_c=addend.shape[-1] if sub2 else 0)
+            link = ctx.bn_link
+            if link is not None and _bn_res_dgrad(dy, w, dx, addend, sub2, link, P, Bn, H, W,
+                                                  Ci, Co, stride):
+                link["fused"] = True     # dx is dz, its BatchNorm's reductions are summed
+            else:
+                _pconv(1, dy, w, dx, P, Bn, H, W, Ci, Co, stride, addend=addend,
+                       addend_c=addend.shape[-1] if sub2 else 0)
         if ctx.needs_input_grad[1]:
             if ctx.grad_out is not None:         # straight into the flat gradient buffer
                 _pconv(2, x, dy, ctx.grad_out, P, Bn, H, W, Ci, Co, stride)
             else:
                 dw = torch.empty_like(w)
                 _pconv(2, x, dy, dw, P, Bn, H, W, Ci, Co, stride)
-        return dx, dw, None, None, None, None, None
+        return dx, dw, None, None, None, None, None, None
 
 
-def conv3x3(x, w, P, stride, stats=None, mailbox=None):
+def conv3x3(x, w, P, stride, stats=None, mailbox=None, bn_link=None):
     """Population 3x3 convolution: x [P*B, H, W, Cin] bf16, w [P, 9 Cin, Cout].  ``stats`` (HIP
     only): ``[sums, False]`` with zeroed f32 sums [P, 2, Cout]; when the direct kernel ran, the
     per-trial channel sums of the output and of its square were added and the flag is True."""
@@ -207,13 +240,14 @@ def conv3x3(x, w, P, stride, stats=None, mailbox=None):
         raise ValueError(f"conv3x3: needs power-of-two H, W, channels (>= 8) and w [P, 9C, Co]; "
                          f"got x {tuple(x.shape)} w {tuple(w.shape)} P {P}")
     grad_out = w.grad if (w.requires_grad and w.is_leaf and w.grad is not None) else None
-    return _Conv3x3.apply(x.contiguous(), w.contiguous(), P, stride, grad_out, stats, mailbox)
+    return _Conv3x3.apply(x.contiguous(), w.contiguous(), P, stride, grad_out, stats, mailbox,
+                          bn_link)
 
 
 class _BNAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, res, running, P, train, relu, eps, momentum, sums=None,
-                arena=None, mailbox=None, res_sub2=False):
+                arena=None, mailbox=None, res_sub2=False, link=None):
         C = x.shape[-1]
         M = x.numel() // (P * C)
         y = torch.empty_like(x)
@@ -235,12 +269,20 @@ class _BNAct(torch.autograd.Function):
                           for t in (gamma, beta))
         ctx.mailbox = mailbox
         ctx.res_sub2 = res_sub2
+        # link: the consumer convolution's data gradient may do this backward's masking and
+        # reductions (_bn_res_dgrad) -- it needs the zeroed backward sums, x, y and the statistics
+        ctx.link = None
+        if link is not None and train and relu and ctx.bwd_sums is not None:
+            link.update(x=x, y=y, stat=stat, sums=ctx.bwd_sums, fused=False)
+            ctx.link = link
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, y, stat, gamma, beta = ctx.saved_tensors
         P, M, C, relu, has_res = ctx.meta
+        if ctx.link is not None and ctx.link.pop("fused", False):
+            return _BNAct._fused_backward(ctx, dy, x, stat, gamma, beta, P, M, C, has_res)
         # without a residual relu'(.) is recomputed from x, gamma, beta (y is not read): one
         # activation tensor less through both backward kernels
         mode = 0 if not relu else (1 if has_res else 2)
@@ -262,10 +304,37 @@ class _BNAct(torch.autograd.Function):
             ctx.mailbox["sub2"] = ctx.res_sub2
             dres = None
         if direct:
-            return dx, None, None, dres, None, None, None, None, None, None, None, None, None, None
+            return dx, None, None, dres, None, None, None, None, None, None, None, None, None, \
+                None, None
         dgamma = sums[:, 1].to(gamma.dtype)
         dbeta = sums[:, 0].to(gamma.dtype)
-        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, \
+            None, None
+
+    @staticmethod
+    def _fused_backward(ctx, dz, x, stat, gamma, beta, P, M, C, has_res):
+        """Backward after the consumer's data gradient (``_bn_res_dgrad``) delivered dz (the
+        gradient behind the ReLU) and summed its reductions: the apply pass alone, no mask, and
+        dz itself is the shortcut's gradient (no copy written)."""
+        ctx.link.clear()
+        dz = dz.contiguous()
+        dx = torch.empty_like(x)
+        gg, gb = ctx.grads
+        direct = gg is not None and gb is not None and gg.is_contiguous() and gb.is_contiguous()
+        _call("mopt_bn_bwd", x.data_ptr(), 0, dz.data_ptr(), stat.data_ptr(), gamma.data_ptr(),
+              beta.data_ptr(), dx.data_ptr(), 0, ctx.bwd_sums.data_ptr(),
+              gg.data_ptr() if direct else 0, gb.data_ptr() if direct else 0, P, M, C, 0, 2, _s(x))
+        dres = dz if has_res else None
+        if dres is not None and ctx.mailbox is not None:
+            ctx.mailbox["dres"] = dres
+            ctx.mailbox["sub2"] = ctx.res_sub2
+            dres = None
+        dgamma = dbeta = None
+        if not direct:
+            dgamma = ctx.bwd_sums[:, 1].to(gamma.dtype)
+            dbeta = ctx.bwd_sums[:, 0].to(gamma.dtype)
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None, \
+            None
 
 
 class _BNReluConv3x3(torch.autograd.Function):
@@ -369,16 +438,18 @@ def bn_relu_conv3x3(x, gamma, beta, running, w, P, sums, arena, eps=1e-5, moment
     return y, out_sums
 
 
-def conv_stats(x, w, P, stride, train, arena=None, mailbox=None):
+def conv_stats(x, w, P, stride, train, arena=None, mailbox=None, bn_link=None):
     """``(conv3x3(x, w), batch sums of the output or None)``: the first half of ``conv_bn_act``
-    (HIP path; the sums come from the direct kernel's epilogue when it ran)."""
+    (HIP path; the sums come from the direct kernel's epilogue when it ran).  ``bn_link``: the
+    link dict of the BatchNorm that produced x (``bn_act(link=...)``), whose backward this
+    convolution's data gradient then fuses (``_bn_res_dgrad``)."""
     Co = w.shape[-1]
     stats = None
     if train:
         z = arena.take(P * 2 * Co).view(P, 2, Co) if arena is not None else \
             torch.zeros(P, 2, Co, dtype=torch.float32, device=x.device)
         stats = [z, False]
-    y = conv3x3(x, w, P, stride, stats, mailbox=mailbox)
+    y = conv3x3(x, w, P, stride, stats, mailbox=mailbox, bn_link=bn_link)
     return y, (stats[0] if stats is not None and stats[1] else None)
 
 
@@ -389,9 +460,11 @@ def option_a_shortcut(h, cout):
 
 
 def bn_act(x, gamma, beta, running, P, train, res=None, relu=True, eps=1e-5, momentum=0.1,
-           sums=None, arena=None, mailbox=None, res_sub2=False):
+           sums=None, arena=None, mailbox=None, res_sub2=False, link=None):
     """``res_sub2``: ``res`` is the full-resolution block input and the residual its option-A
-    shortcut, read in place by the kernel (no subsampled / padded copy)."""
+    shortcut, read in place by the kernel (no subsampled / padded copy).  ``link`` (a dict,
+    training with ``arena``): filled for the consumer convolution (``conv_stats(bn_link=...)``),
+    whose data gradient may take over this BatchNorm's relu' masking and reductions."""
     """y = relu?(BN(x) + res?) per trial; ``running`` [P, 2, C] f32 updated when training.
     ``sums``: precomputed f32 [P, 2, C] batch sums of x and x^2 (the producing convolution's
     epilogue) -- the statistics pass is skipped."""
@@ -403,7 +476,7 @@ def bn_act(x, gamma, beta, running, P, train, res=None, relu=True, eps=1e-5, mom
         res_sub2 = False
     return _BNAct.apply(x.contiguous(), gamma.contiguous(), beta.contiguous(),
                         None if res is None else res.contiguous(), running, P, train, relu, eps,
-                        momentum, sums, arena, mailbox, res_sub2)
+                        momentum, sums, arena, mailbox, res_sub2, link)
 
 
 class ZeroArena:
@@ -423,7 +496,7 @@ class ZeroArena:
 
 
 def conv_bn_act(x, w, gamma, beta, running, P, stride, train, res=None, relu=True, arena=None,
-                conv_mailbox=None, bn_mailbox=None, res_sub2=False):
+                conv_mailbox=None, bn_mailbox=None, res_sub2=False, link=None):
     """``bn_mailbox`` / ``conv_mailbox`` (one dict per residual block, HIP path): the block's last
     BatchNorm leaves the identity shortcut's gradient there and the block's first convolution
     adds it in its data-gradient epilogue -- pass ``res`` detached so autograd does not add it
@@ -444,7 +517,8 @@ def conv_bn_act(x, w, gamma, beta, running, P, stride, train, res=None, relu=Tru
     y = conv3x3(x, w, P, stride, stats, mailbox=conv_mailbox)
     return bn_act(y, gamma, beta, running, P, train, res=res, relu=relu,
                   sums=stats[0] if stats is not None and stats[1] else None,
-                  arena=arena if train else None, mailbox=bn_mailbox, res_sub2=res_sub2)
+                  arena=arena if train else None, mailbox=bn_mailbox, res_sub2=res_sub2,
+                  link=link)
 
 
 # ------------------------------------------------------------------ classifier head

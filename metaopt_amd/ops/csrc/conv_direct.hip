@@ -191,6 +191,7 @@ struct BnIn {
   const bf16_t* gamma;   // [P][C]
   const bf16_t* beta;    // [P][C]
   const bf16_t* x;       // BNB data gradients: the BatchNorm's input, shaped like the output
+  const bf16_t* y;       // BNB 2: the BatchNorm's (post-ReLU) output, relu' read off it
 };
 
 template <int CI>
@@ -227,6 +228,13 @@ __device__ __forceinline__ int tap_off(const Geom& g, int k) {
 // reductions sums[p][0][c] += dz, sums[p][1][c] += dz xhat (dz = dy relu'(x sc + sh), xhat =
 // (x - mean) rstd, x = bn.x) from the stored bf16 dy -- the BatchNorm backward then skips its
 // reduction pass (bn_reduce_kernel<true>: both tensors read once more).
+// BNB 2 (data gradient of the conv that consumes a block output relu(BN(x) + shortcut), with the
+// next block's shortcut gradient as ADD 1 / 2): the stored value is dz = (dgrad + addend) *
+// relu'(bn.y) -- the gradient BEHIND that ReLU, which is also the previous block's shortcut
+// gradient -- and the epilogue accumulates sum dz, sum dz xhat (xhat from bn.x) as BNB 1 does.
+// The BatchNorm backward then runs its apply pass alone without a mask and writes no copy of dz:
+// of its reduce (3 tensors), apply (3 read, 2 written) and this epilogue's store, 3 passes and
+// a launch go.
 template <int CI, int CO, int NPX, int MODE, int S, int ADD, int BNIN = 0, int BNB = 0>
 __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict__ x,
                                                         const bf16_t* __restrict__ w,
@@ -236,7 +244,8 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
                                                         const Geom g, int addend_c,
                                                         const BnIn bn) {
   static_assert(BNIN == 0 || MODE == kFwd, "the BatchNorm input is applied by forwards only");
-  static_assert(BNB == 0 || (MODE == kDgrad && ADD == 0), "BNB: plain stride-1 data gradients");
+  static_assert(BNB != 1 || (MODE == kDgrad && ADD == 0), "BNB 1: plain stride-1 data gradients");
+  static_assert(BNB != 2 || (MODE != kFwd && ADD != 0), "BNB 2: data gradients with an addend");
   constexpr int mode = MODE;
   constexpr int KS = (9 * CI + 31) / 32;  // 32-wide k steps (k = tap * CI + c)
   constexpr int WN = CO / 16, WM = 4 / WN;
@@ -338,13 +347,20 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
   // BNB: the band's BatchNorm input; ADD: the band's addend -- loaded before the next band's
   // halo fetch and used by the band's copy-out (one band later)
   uint4 xr[(BNB != 0 || ADD != 0) ? XCH : 1];
+  // BNB 2: the BatchNorm's output (relu' mask) and input (xhat) of the band, loaded beside the
+  // addend -- except at 64 channels, where the 32 more registers cost the second workgroup per
+  // CU: loaded by the copy-out itself
+  constexpr bool BPF = BNB == 2 && CO < 64;
+  uint4 yr[BPF ? XCH : 1], cr[BPF ? XCH : 1];
   if constexpr (BNB != 0) {
     const int c0 = 8 * (threadIdx.x % CPR);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float mean = bn.stat[(2 * p) * CO + c0 + e];
-      bsc[e] = bf2f(bn.gamma[(int64_t)p * CO + c0 + e]) * bn.stat[(2 * p + 1) * CO + c0 + e];
-      bsh[e] = bf2f(bn.beta[(int64_t)p * CO + c0 + e]) - mean * bsc[e];
+      if constexpr (BNB == 1) {
+        const float mean = bn.stat[(2 * p) * CO + c0 + e];
+        bsc[e] = bf2f(bn.gamma[(int64_t)p * CO + c0 + e]) * bn.stat[(2 * p + 1) * CO + c0 + e];
+        bsh[e] = bf2f(bn.beta[(int64_t)p * CO + c0 + e]) - mean * bsc[e];
+      }
       ba[e] = bb[e] = 0.f;
     }
   }
@@ -388,8 +404,33 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
                            bf2f(vw[e] >> 16) + bf2f(aw[e] >> 16));
           v = make_uint4(o[0], o[1], o[2], o[3]);
         }
+        if constexpr (BNB == 2) {  // dz = g relu'(y); sum dz, sum dz x (bn_reduce relu mode 1)
+          uint4 yq, xq;
+          if constexpr (BPF) {
+            yq = yr[k];
+            xq = cr[k];
+          } else {
+            const int64_t o = (yt - y) + (int64_t)row * CO + 8 * cc;
+            yq = *(const uint4*)(bn.y + o);
+            xq = *(const uint4*)(bn.x + o);
+          }
+          const uint32_t yw[4] = {yq.x, yq.y, yq.z, yq.w}, xw[4] = {xq.x, xq.y, xq.z, xq.w};
+          uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float lo = bf2f(yw[e] & 0xFFFF) <= 0.f ? 0.f : bf2f(vw[e] & 0xFFFF);
+            const float hi = bf2f(yw[e] >> 16) <= 0.f ? 0.f : bf2f(vw[e] >> 16);
+            vw[e] = (bf2f(yw[e] & 0xFFFF) <= 0.f ? 0u : (vw[e] & 0xFFFFu)) |
+                    (bf2f(yw[e] >> 16) <= 0.f ? 0u : (vw[e] & 0xFFFF0000u));
+            ba[2 * e] += lo;
+            bb[2 * e] += lo * bf2f(xw[e] & 0xFFFF);
+            ba[2 * e + 1] += hi;
+            bb[2 * e + 1] += hi * bf2f(xw[e] >> 16);
+          }
+          v = make_uint4(vw[0], vw[1], vw[2], vw[3]);
+        }
         *(uint4*)(yt + (int64_t)row * CO + 8 * cc) = v;
-        if constexpr (BNB != 0) {
+        if constexpr (BNB == 1) {
           const uint4 xq = xr[k];
           const uint32_t vw[4] = {v.x, v.y, v.z, v.w}, xw[4] = {xq.x, xq.y, xq.z, xq.w};
 #pragma unroll
@@ -418,7 +459,12 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
         const int c = min(threadIdx.x + 256 * k, valid * CPR - 1);
         const int row = c / CPR, cc = c % CPR;
         const bf16_t* src;
-        if constexpr (BNB != 0) {
+        if constexpr (BPF) {
+          const int64_t o = (yt - y) + (int64_t)row * CO + 8 * cc;
+          yr[k] = *(const uint4*)(bn.y + o);
+          cr[k] = *(const uint4*)(bn.x + o);
+        }
+        if constexpr (BNB == 1) {
           src = bn.x + (yt - y) + (int64_t)row * CO + 8 * cc;
         } else if constexpr (ADD == 1) {  // identity shortcut: same layout as the output
           src = addend + (yt - y) + (int64_t)row * CO + 8 * cc;
@@ -865,6 +911,35 @@ int mopt_dconv_dgrad_bnsums(const void* dy, const void* w, void* dbn, void* sums
     return launch_fwd<c, c, kDgrad, 1, 0, 0, 1>(dy, w, dbn, sums, P, Bn, H, st, nullptr, 0, bn);
   X(16) X(32) X(64)
 #undef X
+  return (int)hipErrorNotSupported;
+}
+
+// Data gradient of a convolution (stride 1: identity shortcut addend shaped like dx; stride 2:
+// option-A addend [P*Bn, H/2, H/2, addend_c] at the even pixels) whose input is a block output
+// bn_y = relu(BatchNorm(bn_x) + shortcut): dz = (dgrad + addend) relu'(bn_y) is stored into dx
+// and the BatchNorm backward's reductions (sum dz, sum dz xhat) are added into sums [P][2][Ci]
+// (zeroed by the caller; stat [P][2][Ci] mean / rstd of that BatchNorm).  Ci == Co at stride 1,
+// Co == 2 Ci at stride 2 (a CIFAR ResNet's block entries).
+int mopt_dconv_dgrad_bnres(const void* dy, const void* w, void* dx, const void* addend,
+                           void* sums, int P, int Bn, int H, int Ci, int Co, int stride,
+                           int addend_c, const void* bn_x, const void* bn_y, const void* stat,
+                           void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (addend == nullptr || sums == nullptr || bn_x == nullptr || bn_y == nullptr ||
+      stat == nullptr || (stride == 2 && addend_c <= 0))
+    return (int)hipErrorInvalidValue;
+  const BnIn bn{(const float*)stat, nullptr, nullptr, (const bf16_t*)bn_x, (const bf16_t*)bn_y};
+  // (the data gradient runs the forward kernel with the channel counts swapped: CI = Co)
+#define X1(c) \
+  if (stride == 1 && Ci == c && Co == c) \
+    return launch_fwd<c, c, kDgrad, 1, 1, 0, 2>(dy, w, dx, sums, P, Bn, H, st, addend, 0, bn);
+#define X2(co, ci) \
+  if (stride == 2 && Co == co && Ci == ci) \
+    return launch_fwd<co, ci, kDgrad2, 1, 2, 0, 2>(dy, w, dx, sums, P, Bn, H, st, addend, \
+                                                   addend_c, bn);
+  X1(16) X1(32) X1(64) X2(32, 16) X2(64, 32)
+#undef X1
+#undef X2
   return (int)hipErrorNotSupported;
 }
 

@@ -15,8 +15,9 @@
 // l^48), and the P.V product reads V through ds_read_b64_tr_b16 (no LDS transpose pass).
 //
 // Kernels: attn_fwd (one 64-query block per workgroup, 16 queries per wave), attn_bwd_dq (same
-// decomposition, loops over key blocks), attn_bwd_dkdv (one 64-key block per workgroup, 16 keys
-// per wave, loops over query blocks) and attn_bwd_prep (Dsum).  No atomics anywhere.
+// decomposition, loops over key blocks; computes Dsum of its own query rows and stores it for
+// attn_bwd_dkdv, launched after it) and attn_bwd_dkdv (one 64-key block per workgroup, 16 keys
+// per wave, loops over query blocks).  No atomics anywhere.
 #include "common.h"
 
 using namespace mopt;
@@ -292,7 +293,9 @@ __global__ __launch_bounds__(256 * NQB) MOPT_WAVES_ATTR(kAttnFwdWaves) void attn
   if (g == 0) LSE2[(size_t)bh * T + qrow] = m + log2f(l);
 }
 
-// Dsum[bh][t] = sum_d dO * O  (one thread per query row).
+// Dsum[bh][t] = sum_d dO * O  (one thread per query row).  (Round 6: no longer launched -- the dQ
+// kernel computes the Dsum of its query rows from the dO fragments it loads anyway; kept as the
+// standalone form for MOPT_ATTN_PREP=1 A/B builds.)
 __global__ __launch_bounds__(256) void attn_bwd_prep_kernel(const bf16_t* __restrict__ O,
                                                             const bf16_t* __restrict__ dO,
                                                             float* __restrict__ Dsum, int T, int H,
@@ -315,15 +318,19 @@ __global__ __launch_bounds__(256) void attn_bwd_prep_kernel(const bf16_t* __rest
 }
 
 // dQ = scale * sum_k dS K, dS = P * (dP - Dsum), dP = dO V^T.   grid (T/64, BH).
+// DSUM: Dsum of the lane's query = sum_d dO O from its two dO fragments and the matching O
+// fragments (16 of the 64 products per lane, summed over the 4 lanes of the query), stored for
+// the dK/dV kernel -- the separate prep pass (O and dO read once more) goes.
 __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnDqWaves) void attn_bwd_dq_kernel(const bf16_t* __restrict__ Q,
                                                           const bf16_t* __restrict__ K,
                                                           const bf16_t* __restrict__ V,
                                                           const bf16_t* __restrict__ dO,
                                                           const float* __restrict__ LSE2,
-                                                          const float* __restrict__ Dsum,
+                                                          float* __restrict__ Dsum,
                                                           bf16_t* __restrict__ dQ, int T, int H,
                                                           float c, float scale, int n_bh,
-                                                          const RopeOut ro) {
+                                                          const RopeOut ro,
+                                                          const bf16_t* __restrict__ O) {
   __shared__ __attribute__((aligned(16))) bf16_t Ks[tile_elems<false>()];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[tile_elems<false>()];
   const int nqb = T / BQ;
@@ -343,7 +350,21 @@ __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnDqWaves) void attn_bwd_dq
     qf[ks] = lds_frag(Q + base + (size_t)qrow * D + 32 * ks + 8 * g);
     df[ks] = lds_frag(dO + orow + 32 * ks + 8 * g);
   }
-  const float lse = LSE2[(size_t)bh * T + qrow], dsum = Dsum[(size_t)bh * T + qrow];
+  const float lse = LSE2[(size_t)bh * T + qrow];
+  float dsum;
+  if (O != nullptr) {
+    float part = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 of = lds_frag(O + orow + 32 * ks + 8 * g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) part = fmaf((float)df[ks][e], (float)of[e], part);
+    }
+    dsum = sum4(part);
+    if (g == 0) Dsum[(size_t)bh * T + qrow] = dsum;
+  } else {
+    dsum = Dsum[(size_t)bh * T + qrow];
+  }
   f32x4 acc[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) acc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -538,15 +559,21 @@ int mopt_attn_bwd(const void* q, const void* k, const void* v, const void* o, co
   const int rows = bh * T;
   const RopeOut ro{(bf16_t*)dqkv, (const float*)cosT, (const float*)sinT};
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((rows + 255) / 256), dim3(256), 0, st,
-                     (const bf16_t*)o, (const bf16_t*)dout, (float*)dsum, T, H, rows);
+  // dQ first: it computes Dsum (MOPT_ATTN_PREP=1: the separate prep pass, for A/B builds)
+#ifndef MOPT_ATTN_PREP
+#define MOPT_ATTN_PREP 0
+#endif
+  if (MOPT_ATTN_PREP)
+    hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((rows + 255) / 256), dim3(256), 0, st,
+                       (const bf16_t*)o, (const bf16_t*)dout, (float*)dsum, T, H, rows);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((T / 64) * bh), dim3(256), 0, st, (const bf16_t*)q,
+                     (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, (const float*)lse2,
+                     (float*)dsum, (bf16_t*)dq, T, H, c, scale, bh, ro,
+                     MOPT_ATTN_PREP ? nullptr : (const bf16_t*)o);
   hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((T / 64) * bh), dim3(256), 0, st,
                      (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout,
                      (const float*)lse2, (const float*)dsum, (bf16_t*)dk, (bf16_t*)dv, T, H, c,
                      scale, bh, ro);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((T / 64) * bh), dim3(256), 0, st, (const bf16_t*)q,
-                     (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, (const float*)lse2,
-                     (const float*)dsum, (bf16_t*)dq, T, H, c, scale, bh, ro);
   return (int)hipGetLastError();
 }
 
