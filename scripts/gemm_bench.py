@@ -33,6 +33,10 @@ SHAPES = [
     ("rn.s1.dw", 32, 144, 16, 131072, True, False),
     ("rn.s3.fwd", 32, 8192, 64, 576, False, False),
     ("rn.s3.dw", 32, 576, 64, 8192, True, False),
+    # square references: the ceiling of this kernel and of the library away from the LM's short
+    # K / narrow N (round 6)
+    ("sq.8192", 1, 8192, 8192, 8192, False, False),
+    ("sq.p8.4096", 8, 4096, 4096, 4096, False, False),
 ]
 
 

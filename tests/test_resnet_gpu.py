@@ -305,14 +305,15 @@ def test_bn_residual_backward_fused_into_next_dgrad(monkeypatch):
     """Each block output's BatchNorm backward (relu(BN(x) + shortcut), and the stem's relu(BN(x)))
     fused into the next block's first data gradient (ops/conv.py _bn_res_dgrad: the kernel stores
     dz = (dgrad + shortcut gradient) relu'(y) and sums the BatchNorm reductions; the BatchNorm then
-    runs its apply pass alone) against the separate reduce + apply passes: the same loss, and the
-    gradients of every parameter within bf16 rounding, at the CIFAR shapes of every kernel
-    instantiation (16 / 32 / 64 channels at stride 1, 32 -> 16 and 64 -> 32 at stride 2)."""
+    runs its apply pass alone) against the separate reduce + apply passes and the fp32 CPU
+    reference: the same loss, and every parameter's gradient as close to the fp32 reference as
+    the unfused path's, at the CIFAR shapes of every kernel instantiation (16 / 32 / 64 channels at
+    stride 1, 32 -> 16 and 64 -> 32 at stride 2)."""
     from metaopt_amd.models.resnet import PopulationResNet, SyntheticCIFAR
     from metaopt_amd.ops.population import MemberConfig
     P, B = 2, 16
     data = SyntheticCIFAR(n_train=4 * B, n_val=32, batch_size=B, image_size=32)
-    x, y = (t.to(DEV) for t in data.batch(1))    # (a host batch takes the unfused path)
+    xh, yh = data.batch(1)
     calls = []
     real = cops._bn_res_dgrad
 
@@ -324,32 +325,42 @@ def test_bn_residual_backward_fused_into_next_dgrad(monkeypatch):
     monkeypatch.setattr(cops, "_bn_res_dgrad", counted)
     out = {}
     ref = None
-    for fused in (True, False):
-        monkeypatch.setattr(cops, "_BN_RES_DGRAD", fused)
-        pop = PopulationResNet(P, batch_size=B, device=DEV, blocks_per_stage=2, image_size=32,
+    for run in ("fused", "unfused", "cpu"):
+        dev = "cpu" if run == "cpu" else DEV
+        monkeypatch.setattr(cops, "_BN_RES_DGRAD", run == "fused")
+        pop = PopulationResNet(P, batch_size=B, device=dev, blocks_per_stage=2, image_size=32,
                                use_graph=False)
         for s in range(P):
             pop.set_member(s, MemberConfig(width=0, lr=0.05, momentum=0.9, seed=s + 3))
         if ref is None:
             ref = pop
+            state = (ref.master_flat().clone(), ref.p16.clone())
         else:
             with torch.no_grad():
-                pop.master_buf.copy_(ref_state[0])
-                pop.p16.copy_(ref_state[1])
-        ref_state = (ref.master_buf.clone(), ref.p16.clone())
+                if pop.split:
+                    pop.master_buf.copy_(ref.master_buf.to(dev))
+                else:
+                    pop.p32.copy_(state[0].to(dev))
+                pop.p16.copy_(state[1].to(dev))
         calls.clear()
-        pop.train_step(x, y)
-        torch.cuda.synchronize()
-        out[fused] = (pop.train_loss(), pop.g16.float().clone(), list(calls))
-    assert out[True][2] == [True] * 6, out[True][2]     # every block entry took the fused kernel
-    assert not any(out[False][2])
+        # (the batch on the device: a host batch takes the unfused path)
+        pop.train_step(xh.to(dev), yh.to(dev))
+        if dev != "cpu":
+            torch.cuda.synchronize()
+        out[run] = (pop.train_loss(), pop.g16.float().cpu().clone(), list(calls))
+    assert out["fused"][2] == [True] * 6, out["fused"][2]   # every block entry fused
+    assert not any(out["unfused"][2])
     # (the BatchNorm statistics are summed with float atomics: the forward is not bitwise
     # reproducible run to run)
-    np.testing.assert_allclose(out[True][0], out[False][0], rtol=2e-3)
-    ga, gb = out[True][1], out[False][1]
-    rel = ((ga - gb).norm() / gb.norm()).item()
-    assert rel < 1e-2, rel
-    # per parameter tensor: no layer's gradient is off by more than bf16 rounding of its scale
+    np.testing.assert_allclose(out["fused"][0], out["unfused"][0], rtol=2e-3)
+    gc = out["cpu"][1]
+    errs = {}
     for name, (o, n) in zip([s[0] for s in ref.specs], ref.segments):
-        a, b = ga[o:o + P * n], gb[o:o + P * n]
-        assert (a - b).abs().max().item() <= 3e-2 * b.abs().max().item() + 1e-6, name
+        b = gc[o:o + P * n]
+        scale = b.norm().item() + 1e-12
+        errs[name] = tuple(round((out[r][1][o:o + P * n] - b).norm().item() / scale, 4)
+                           for r in ("fused", "unfused"))
+    # (measured: both paths 1-14 % from the fp32 reference per conv / BatchNorm tensor at this
+    # 16-image batch -- bf16 activations; the fused path no farther than the unfused one)
+    bad = {k: v for k, v in errs.items() if v[0] > 1.5 * v[1] + 1e-2}
+    assert not bad, (bad, errs)
