@@ -99,20 +99,30 @@ class PopulationResNet(FlatPopulation):
         return cops.conv_bn_act(x, w, W[f"{name}.g"], W[f"{name}.b"], running, P, stride, train,
                                 res=res, relu=relu, arena=arena, **mail)
 
-    def _block_fused(self, n1, n2, h, s1, identity, arena, box, in_link=None, out_link=None):
-        """One training basic block on the HIP path: conv1 (+ its BatchNorm's batch sums),
-        BatchNorm 1 + ReLU applied inside conv2 (``bn_relu_conv3x3``: its output never reaches
-        HBM) when the shapes allow, BatchNorm 2 + shortcut + ReLU; the shortcut's gradient joins
-        conv1's data gradient in its epilogue (``box``).  ``in_link``: the link of the BatchNorm
-        that produced h (the previous block's BatchNorm 2, or the stem's), whose relu' masking and
-        reductions conv1's data gradient takes over; ``out_link`` is this block's own."""
+    def _block_fused(self, n1, n2, h, pend, s1, identity, arena, box):
+        """One training basic block on the HIP path.  Its input is either materialised (``h``)
+        or still ``pend``-ing: the previous block's BatchNorm 2 + shortcut + ReLU (or the stem's
+        BatchNorm + ReLU), which conv 1 then forms while staging its input bands and writes out
+        once (``bn_res_conv3x3``; the materialised fallback runs the apply pass and links that
+        BatchNorm's backward into conv 1's data gradient).  Conv 1 (+ its BatchNorm's batch
+        sums), BatchNorm 1 + ReLU applied inside conv 2 (``bn_relu_conv3x3``) when the shapes
+        allow, and this block's BatchNorm 2 + shortcut + ReLU left pending for the next
+        consumer; the shortcut's gradient joins conv 1's data gradient in its epilogue
+        (``box``).  Returns (the block input h, this block's PendingBN or its output)."""
         P, W = self.capacity, self.W
         w1, w2 = W[f"{n1}.w"], W[f"{n2}.w"]
         c1, c2 = w1.shape[-1], w2.shape[-1]
         run1 = self.A[f"{n1}.running"].view(P, 2, c1)
         run2 = self.A[f"{n2}.running"].view(P, 2, c2)
-        y1, st1 = cops.conv_stats(h, w1, P, s1, True, arena=arena, mailbox=box,
-                                  bn_link=in_link)
+        if pend is not None and cops.bn_res_conv_ok(pend, w1, s1):
+            y1, st1, h = cops.bn_res_conv3x3(pend, w1, P, s1, arena, conv_mailbox=box)
+        else:
+            link = None
+            if pend is not None:
+                link = {}
+                h = pend.materialize(arena, link=link)
+            y1, st1 = cops.conv_stats(h, w1, P, s1, True, arena=arena, mailbox=box,
+                                      bn_link=link)
         if cops.bn_into_conv_ok(y1, w2, P, 1, True, arena, st1 is not None):
             y2, st2 = cops.bn_relu_conv3x3(y1, W[f"{n1}.g"], W[f"{n1}.b"], run1, w2, P, st1,
                                            arena)
@@ -120,9 +130,11 @@ class PopulationResNet(FlatPopulation):
             t = cops.bn_act(y1, W[f"{n1}.g"], W[f"{n1}.b"], run1, P, True, sums=st1,
                             arena=arena)
             y2, st2 = cops.conv_stats(t, w2, P, 1, True, arena=arena)
-        return cops.bn_act(y2, W[f"{n2}.g"], W[f"{n2}.b"], run2, P, True, res=h.detach(),
-                           sums=st2, arena=arena, mailbox=box, res_sub2=not identity,
-                           link=out_link)
+        out = cops.PendingBN(y2, st2, W[f"{n2}.g"], W[f"{n2}.b"], run2, P, res=h.detach(),
+                             res_sub2=not identity, mailbox=box)
+        if st2 is None:       # no batch sums from conv 2: the BatchNorm runs its own reduction
+            return h, out.materialize(arena)
+        return h, out
 
     @staticmethod
     def _shortcut(x, cout, stride):
@@ -139,28 +151,41 @@ class PopulationResNet(FlatPopulation):
                  if train and x.device.type == "cuda" else None)
         it = iter(self.layout)
         name, _, cout, stride = next(it)
-        # each block output's BatchNorm hands its backward's masking and reductions to the next
-        # block's first data gradient (ops/conv.py _bn_res_dgrad): one link dict per BatchNorm
-        link = {} if arena is not None else None
-        h = self._conv_bn(name, h, stride, train, arena=arena, link=link)
+        # training on the HIP path: every BatchNorm whose output feeds a convolution is left
+        # pending (cops.PendingBN) and formed inside that convolution's input staging, its
+        # backward's masking and reductions in that convolution's data gradient
+        pend = None
+        if arena is not None:
+            W0 = self.W[f"{name}.w"]
+            y0, st0 = cops.conv_stats(h, W0, P, stride, True, arena=arena)
+            pend = cops.PendingBN(y0, st0, W[f"{name}.g"], W[f"{name}.b"],
+                                  self.A[f"{name}.running"].view(P, 2, cout), P)
+            if st0 is None:
+                h, pend = pend.materialize(arena), None
+        else:
+            h = self._conv_bn(name, h, stride, train, arena=arena)
         for si in range(len(STAGES)):
             for b in range(self.blocks):
                 n1, _, c1, s1 = next(it)
                 n2, _, c2, _ = next(it)
-                identity = s1 == 1 and h.shape[-1] == c2
+                cin = pend.x.shape[-1] if pend is not None else h.shape[-1]
+                identity = s1 == 1 and cin == c2
                 if train and arena is not None and (identity or s1 == 2):
                     # the shortcut's gradient joins the first conv's data gradient in that
                     # kernel's epilogue (no separate add over the block input); an option-A
-                    # shortcut is also read in place by the BatchNorm (no padded copy)
+                    # shortcut is also read in place (no padded copy)
                     box = {}
-                    out_link = {}
-                    h = self._block_fused(n1, n2, h, s1, identity, arena, box, link, out_link)
-                    link = out_link
+                    h, out = self._block_fused(n1, n2, h if pend is None else None, pend, s1,
+                                               identity, arena, box)
+                    pend, h = (out, None) if isinstance(out, cops.PendingBN) else (None, out)
                     continue
-                link = None
+                if pend is not None:
+                    h, pend = pend.materialize(arena), None
                 r = self._shortcut(h, c2, s1)
                 t = self._conv_bn(n1, h, s1, train, arena=arena)
                 h = self._conv_bn(n2, t, 1, train, res=r, arena=arena)
+        if pend is not None:          # the last block's output feeds the head
+            h = pend.materialize(arena)
         labels = self._expand(y, torch.long).reshape(-1)
         if x.device.type == "cuda":
             # pool + linear + cross-entropy (+ its backward) in one HIP kernel; the classifier's

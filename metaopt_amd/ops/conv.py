@@ -34,6 +34,8 @@ _lib.register_signatures({
     "mopt_dconv_bnin": ([c_int] + [c_void_p] * 4 + [c_int] * 5 + [c_void_p] * 4, c_int),
     "mopt_dconv_dgrad_bnsums": ([c_void_p] * 4 + [c_int] * 5 + [c_void_p] * 5, c_int),
     "mopt_dconv_dgrad_bnres": ([c_void_p] * 5 + [c_int] * 7 + [c_void_p] * 4, c_int),
+    "mopt_dconv_bnres_fwd": ([c_void_p] * 6 + [c_int] + [c_void_p] * 3 + [c_int] * 6 + [c_void_p],
+                             c_int),
     "mopt_resnet_head": ([c_void_p] * 4 + [c_int] * 5 + [c_float, c_int] + [c_void_p] * 7,
                          c_int),
     "mopt_resnet_head_part_floats": ([c_int] * 3, c_int),
@@ -45,6 +47,13 @@ _BN_INTO_CONV = True
 # gradient of the next block's first convolution (``_bn_res_dgrad``; MOPT_BN_RES_DGRAD=0: the
 # separate reduce + apply passes, for A/B runs)
 _BN_RES_DGRAD = os.environ.get("MOPT_BN_RES_DGRAD", "1") != "0"
+# ... and its forward apply pass folded into that convolution's input staging (``PendingBN``,
+# ``bn_res_conv3x3``; MOPT_BN_RES_FWD=0: the separate apply pass)
+_BN_RES_FWD = os.environ.get("MOPT_BN_RES_FWD", "1") != "0"
+# (Ci, Co, stride) of the direct forward with the block output formed in its staging
+# (csrc/conv_direct.hip mopt_dconv_bnres_fwd): shortcut shaped like x or none / option-A
+_BNRES_FWD_SHAPES = {(16, 16, 1), (16, 32, 2), (32, 32, 1), (32, 64, 2), (64, 64, 1)}
+_BNRES_FWD_SHAPES_SUB2 = {(32, 32, 1), (64, 64, 1)}
 
 _NOT_SUPPORTED = 801   # hipErrorNotSupported: no direct-conv instantiation for the shape
 # direct convolution kernels for square inputs; the implicit GEMM (pgemm gathers) is the
@@ -436,6 +445,138 @@ def bn_relu_conv3x3(x, gamma, beta, running, w, P, sums, arena, eps=1e-5, moment
                              w.contiguous(), running, P, eps, momentum, sums, out_sums, arena,
                              grad_w)
     return y, out_sums
+
+
+class PendingBN:
+    """A training ``relu(BN(x) + shortcut?)`` whose apply pass has not run yet: x with its batch
+    sums (from the producing convolution's epilogue), the BatchNorm's parameters, the shortcut
+    (``res``: shaped like x, or with ``res_sub2`` the full-resolution block input of an option-A
+    shortcut; None for the stem) and the block's mailbox (the shortcut gradient goes there).  The
+    consumer convolution forms the output in its input staging (``bn_res_conv3x3``) or calls
+    ``materialize``."""
+
+    __slots__ = ("x", "sums", "gamma", "beta", "running", "res", "res_sub2", "mailbox", "P")
+
+    def __init__(self, x, sums, gamma, beta, running, P, res=None, res_sub2=False, mailbox=None):
+        self.x, self.sums, self.gamma, self.beta, self.running = x, sums, gamma, beta, running
+        self.res, self.res_sub2, self.mailbox, self.P = res, res_sub2, mailbox, P
+
+    def materialize(self, arena, link=None):
+        return bn_act(self.x, self.gamma, self.beta, self.running, self.P, True, res=self.res,
+                      sums=self.sums, arena=arena, mailbox=self.mailbox, res_sub2=self.res_sub2,
+                      link=link)
+
+
+def bn_res_conv_ok(pend: PendingBN, w, stride) -> bool:
+    """Whether ``bn_res_conv3x3`` has a kernel for this block output and convolution."""
+    if not (_BN_RES_FWD and _DIRECT) or pend is None or pend.sums is None:
+        return False
+    x = pend.x
+    if x.device.type != "cuda":
+        return False
+    N, H, W, C = x.shape
+    Co = w.shape[-1]
+    if H != W or not _pow2(H) or N % pend.P or tuple(w.shape) != (pend.P, 9 * C, Co):
+        return False
+    if pend.res is not None and pend.res_sub2:
+        r = pend.res
+        return (C, Co, stride) in _BNRES_FWD_SHAPES_SUB2 and r.shape[0] == N and \
+            tuple(r.shape[1:3]) == (2 * H, 2 * H) and r.shape[-1] % 8 == 0 and r.shape[-1] <= C
+    if pend.res is not None and tuple(pend.res.shape) != tuple(x.shape):
+        return False
+    return (C, Co, stride) in _BNRES_FWD_SHAPES
+
+
+class _BNResConv3x3(torch.autograd.Function):
+    """``conv3x3(relu(BN(x) + shortcut), w)`` and the block output itself, for a training
+    BatchNorm whose output feeds this convolution (the first of the next basic block): the
+    BatchNorm computes its statistics only, the convolution forms the block output while staging
+    its input bands and writes it to HBM once (it is the next shortcut, the relu' mask of the
+    backward and this convolution's weight-gradient operand) -- the separate apply pass is gone.
+    Backward: the data gradient with the BatchNorm's masking and reductions in its epilogue
+    (``_bn_res_dgrad``), the BatchNorm's apply pass, dz as the block's shortcut gradient, the
+    weight gradient over the stored block output."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, w, res, running, P, stride, sums, out_sums, arena,
+                bn_mailbox, res_sub2, conv_mailbox, grad_w, eps, momentum):
+        N, H, W, C = x.shape
+        Co = w.shape[-1]
+        M = x.numel() // (P * C)
+        stat = torch.empty(P, 2, C, dtype=torch.float32, device=x.device)
+        _call("mopt_bn_fwd", x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), 0, 0,
+              stat.data_ptr(), running.data_ptr(), sums.data_ptr(), P, M, C, eps, momentum, 1, 1,
+              1, 0, 0, _s(x))
+        h = torch.empty_like(x)
+        OH = out_hw(H, stride)
+        y = torch.empty(N, OH, OH, Co, dtype=x.dtype, device=x.device)
+        res_c = res.shape[-1] if (res is not None and res_sub2) else 0
+        _call("mopt_dconv_bnres_fwd", x.data_ptr(), w.data_ptr(), y.data_ptr(),
+              out_sums.data_ptr(), h.data_ptr(), 0 if res is None else res.data_ptr(), res_c,
+              stat.data_ptr(), gamma.data_ptr(), beta.data_ptr(), P, N // P, H, C, Co, stride,
+              _s(x))
+        ctx.save_for_backward(x, h, stat, gamma, beta, w)
+        ctx.meta = (P, N // P, H, C, Co, stride, M)
+        ctx.bwd_sums = arena.take(P * 2 * C).view(P, 2, C)
+        ctx.grads = tuple(t.grad if (t.requires_grad and t.is_leaf and t.grad is not None) else None
+                          for t in (gamma, beta))
+        ctx.bn_mailbox, ctx.res_sub2, ctx.has_res = bn_mailbox, res_sub2, res is not None
+        ctx.conv_mailbox, ctx.grad_w = conv_mailbox, grad_w
+        ctx.mark_non_differentiable(h)
+        return y, h
+
+    @staticmethod
+    def backward(ctx, dy, dh):
+        x, h, stat, gamma, beta, w = ctx.saved_tensors
+        P, Bn, H, C, Co, stride, M = ctx.meta
+        dy = dy.contiguous()
+        box = ctx.conv_mailbox
+        addend = box.pop("dres", None) if box is not None else None
+        sub2 = addend is not None and box.pop("sub2", False)
+        g = torch.empty_like(x)
+        link = {"x": x, "y": h, "stat": stat, "sums": ctx.bwd_sums}
+        if _bn_res_dgrad(dy, w, g, addend, sub2, link, P, Bn, H, H, C, Co, stride):
+            mode, zeroed = 0, 2          # g = dz (masked), its reductions summed
+        else:
+            _pconv(1, dy, w, g, P, Bn, H, H, C, Co, stride, addend=addend,
+                   addend_c=addend.shape[-1] if sub2 else 0)
+            mode, zeroed = 1, 1          # g = the block output's gradient: mask from h
+        dx = torch.empty_like(x)
+        dres = torch.empty_like(x) if (mode == 1 and ctx.has_res) else None
+        gg, gb = ctx.grads
+        direct = gg is not None and gb is not None and gg.is_contiguous() and gb.is_contiguous()
+        _call("mopt_bn_bwd", x.data_ptr(), h.data_ptr(), g.data_ptr(), stat.data_ptr(),
+              gamma.data_ptr(), beta.data_ptr(), dx.data_ptr(),
+              0 if dres is None else dres.data_ptr(), ctx.bwd_sums.data_ptr(),
+              gg.data_ptr() if direct else 0, gb.data_ptr() if direct else 0, P, M, C, mode,
+              zeroed, _s(x))
+        if ctx.has_res and ctx.bn_mailbox is not None:
+            ctx.bn_mailbox["dres"] = g if mode == 0 else dres
+            ctx.bn_mailbox["sub2"] = ctx.res_sub2
+        dw = ctx.grad_w if ctx.grad_w is not None else torch.empty_like(w)
+        _pconv(2, h, dy, dw, P, Bn, H, H, C, Co, stride)
+        dgamma = dbeta = None
+        if not direct:
+            dgamma = ctx.bwd_sums[:, 1].to(gamma.dtype)
+            dbeta = ctx.bwd_sums[:, 0].to(gamma.dtype)
+        return (dx, dgamma, dbeta, None if ctx.grad_w is not None else dw) + (None,) * 13
+
+
+def bn_res_conv3x3(pend: PendingBN, w, P, stride, arena, conv_mailbox=None, eps=1e-5,
+                   momentum=0.1):
+    """``(conv3x3(h, w), batch sums of that output, h)`` with h = relu(BN(x) + shortcut) of the
+    pending BatchNorm formed inside the convolution (``_BNResConv3x3``); check
+    ``bn_res_conv_ok`` first.  ``conv_mailbox``: this convolution's block mailbox (the block's
+    shortcut gradient arrives there)."""
+    Co = w.shape[-1]
+    out_sums = arena.take(P * 2 * Co).view(P, 2, Co)
+    grad_w = w.grad if (w.requires_grad and w.is_leaf and w.grad is not None) else None
+    res = None if pend.res is None else pend.res.detach().contiguous()
+    y, h = _BNResConv3x3.apply(pend.x.contiguous(), pend.gamma.contiguous(),
+                               pend.beta.contiguous(), w.contiguous(), res, pend.running, P,
+                               stride, pend.sums, out_sums, arena, pend.mailbox, pend.res_sub2,
+                               conv_mailbox, grad_w, eps, momentum)
+    return y, out_sums, h
 
 
 def conv_stats(x, w, P, stride, train, arena=None, mailbox=None, bn_link=None):

@@ -192,7 +192,125 @@ struct BnIn {
   const bf16_t* beta;    // [P][C]
   const bf16_t* x;       // BNB data gradients: the BatchNorm's input, shaped like the output
   const bf16_t* y;       // BNB 2: the BatchNorm's (post-ReLU) output, relu' read off it
+  // BNIN 2 (a block output relu(BN(x) + shortcut) as the operand): the shortcut -- shaped like x
+  // (res_c = 0) or the option-A shortcut of a block input at twice the side with res_c channels
+  // (res_c > 0: pixel (2i, 2j), channels >= res_c zero); rmul 0: no shortcut (the stem's
+  // relu(BN(x)); res then points at x) -- and the materialised output `out`, shaped like x
+  const bf16_t* res;
+  bf16_t* out;
+  int res_c;
+  float rmul;
 };
+
+// BNIN 2 staging: relu(fma(x, sc, sh) + shortcut) of one chunk (bn_apply_kernel's arithmetic:
+// the materialised block output is bit-identical to the separate pass's)
+template <int CI>
+__device__ __forceinline__ uint4 bnres_chunk(uint4 v, uint4 r, bool rz, float rmul,
+                                             const float* tab, int cc) {
+  const f32x4 sa = *(const f32x4*)(tab + 8 * cc), sb = *(const f32x4*)(tab + 8 * cc + 4);
+  const f32x4 ha = *(const f32x4*)(tab + CI + 8 * cc);
+  const f32x4 hb = *(const f32x4*)(tab + CI + 8 * cc + 4);
+  const float sc[8] = {sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3]};
+  const float sh[8] = {ha[0], ha[1], ha[2], ha[3], hb[0], hb[1], hb[2], hb[3]};
+  const bool use = !rz && rmul != 0.f;   // (a select, not 0 * r: r may be non-finite)
+  uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  const uint32_t rw[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float lo = fmaxf(fmaf(bf2f(w[e] & 0xFFFF), sc[2 * e], sh[2 * e]) +
+                               (use ? bf2f(rw[e] & 0xFFFF) : 0.f), 0.f);
+    const float hi = fmaxf(fmaf(bf2f(w[e] >> 16), sc[2 * e + 1], sh[2 * e + 1]) +
+                               (use ? bf2f(rw[e] >> 16) : 0.f), 0.f);
+    w[e] = pack2bf(lo, hi);
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// element offset of the shortcut chunk matching x's chunk at offset o (trial-relative, x of side
+// 1 << hl with CI channels); rz: the chunk's channels are past an option-A shortcut's res_c
+template <int CI, int RK>
+__device__ __forceinline__ int res_off(int o, int hl, int res_c, bool& rz) {
+  if constexpr (RK == 0) {   // shortcut shaped like x (or none)
+    rz = false;
+    return o;
+  }
+  const int pix = o / CI, c8 = o % CI, side = 1 << hl;
+  const int ix = pix & (side - 1), iy = (pix >> hl) & (side - 1), b = pix >> (2 * hl);
+  rz = c8 >= res_c;
+  return ((b * 2 * side + 2 * iy) * 2 * side + 2 * ix) * res_c + (rz ? 0 : c8);
+}
+
+// BNIN 2 fetch: x and the shortcut of the halo chunks (every load unconditional, as halo_fetch)
+template <int CI, int NPF, int RK>
+__device__ __forceinline__ void halo_fetch_res(uint4 (&v)[NPF], uint4 (&r)[NPF], uint32_t& ok,
+                                               const bf16_t* x, const bf16_t* rp,
+                                               const BnIn& bn, const Geom& g, int b0, int row0,
+                                               int hl) {
+  const int n = halo_chunks(g, CI / 8);
+  ok = 0;
+#pragma unroll
+  for (int i = 0; i < NPF; ++i) {
+    const int c = opaque(threadIdx.x + 256 * i);
+    const int o = halo_src<CI>(g, b0, row0, min(c, n - 1));
+    ok |= (c < n && o >= 0) ? (1u << i) : 0u;
+    const int oo = o < 0 ? 0 : o;
+    bool rz;
+    const int ro = res_off<CI, RK>(oo, hl, bn.res_c, rz);
+    v[i] = *(const uint4*)(x + (uint32_t)oo);
+    r[i] = *(const uint4*)(rp + (uint32_t)ro);
+  }
+}
+
+// is halo chunk c an interior pixel of the band (its own output rows' input pixels -- the bands
+// tile the input exactly) rather than a halo row / column shared with a neighbour
+template <int CI, int S>
+__device__ __forceinline__ bool halo_interior(const Geom& g, int c) {
+  const int t = c / (CI / 8);
+  const int t2 = fdiv(t, g.inv_wi);
+  const int hc = t - t2 * g.WI;
+  const int img = fdiv(t2, g.inv_tri);
+  const int hr = t2 - img * g.TRI;
+  constexpr int E = S == 1 ? 2 : 1;
+  return hr >= 1 && hr <= g.TRI - E && hc >= 1 && hc <= g.WI - E;
+}
+
+// BNIN 2 put: the block output into the LDS band and, for the band's interior pixels, to HBM
+template <int CI, int S, int NPF, int RK>
+__device__ __forceinline__ void halo_put_res(bf16_t* hs, const uint4 (&v)[NPF],
+                                             const uint4 (&r)[NPF], uint32_t ok, const bf16_t* x,
+                                             const bf16_t* rp, bf16_t* op, const BnIn& bn,
+                                             const Geom& g, int b0, int row0, int hl,
+                                             const float* tab) {
+  constexpr int CC = CI / 8;
+  const int n = halo_chunks(g, CC);
+#pragma unroll
+  for (int i = 0; i < NPF; ++i) {
+    const int c = opaque(threadIdx.x + 256 * i);
+    if (c < n) {
+      uint4 w = make_uint4(0, 0, 0, 0);
+      if ((ok >> i) & 1u) {
+        const int o = halo_src<CI>(g, b0, row0, c);
+        bool rz;
+        res_off<CI, RK>(o, hl, bn.res_c, rz);
+        w = bnres_chunk<CI>(v[i], r[i], rz, bn.rmul, tab, c % CC);
+        if (halo_interior<CI, S>(g, c)) *(uint4*)(op + o) = w;
+      }
+      *(uint4*)(hs + (c / CC) * pstride<CI, S>() + 8 * (c % CC)) = w;
+    }
+  }
+  for (int c = threadIdx.x + 256 * NPF; c < n; c += 256) {   // past the registers: synchronous
+    const int o = halo_src<CI>(g, b0, row0, c);
+    uint4 w = make_uint4(0, 0, 0, 0);
+    if (o >= 0) {
+      bool rz;
+      const int ro = res_off<CI, RK>(o, hl, bn.res_c, rz);
+      w = bnres_chunk<CI>(*(const uint4*)(x + o), *(const uint4*)(rp + ro), rz, bn.rmul, tab,
+                          c % CC);
+      if (halo_interior<CI, S>(g, c)) *(uint4*)(op + o) = w;
+    }
+    *(uint4*)(hs + (c / CC) * pstride<CI, S>() + 8 * (c % CC)) = w;
+  }
+}
 
 template <int CI>
 __device__ __forceinline__ void bnin_table(float* tab, const BnIn& bn, int p) {
@@ -235,6 +353,12 @@ __device__ __forceinline__ int tap_off(const Geom& g, int k) {
 // The BatchNorm backward then runs its apply pass alone without a mask and writes no copy of dz:
 // of its reduce (3 tensors), apply (3 read, 2 written) and this epilogue's store, 3 passes and
 // a launch go.
+// BNIN 2 (forward of the conv that consumes a block output): the operand relu(fma(x, sc, sh) +
+// shortcut) is formed while staging (x = the block's last BatchNorm input, bn.res the shortcut),
+// and the band's interior pixels of it are also written to bn.out -- the materialised block
+// output the next shortcut, the relu' mask of the backward and this conv's weight gradient read:
+// bn_apply_kernel's pass (x and shortcut read, output written) is folded into this conv's own
+// operand read.
 template <int CI, int CO, int NPX, int MODE, int S, int ADD, int BNIN = 0, int BNB = 0>
 __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict__ x,
                                                         const bf16_t* __restrict__ w,
@@ -253,7 +377,12 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
   constexpr int LSC = CO + 8;
   // (64-channel data gradients with an addend: one prefetched chunk -- the addend registers on
   //  top of a full prefetch cost the kernel its second workgroup per CU, 51 -> 72 us in situ)
-  constexpr int NPF = (CO >= 64 && ADD != 0) ? 1 : halo_pf<CI, CO, S, NPX, MODE>();
+  // (BNIN 2 / 3: x and the shortcut in flight -- at most 3 chunks of each, the rest of a band
+  //  staged synchronously, so the 16-channel stride-2 and 32-channel kernels keep 2 workgroups
+  //  per CU)
+  constexpr int NPF = (CO >= 64 && ADD != 0) ? 1
+                      : BNIN >= 2 ? (halo_pf<CI, CO, S, NPX, MODE>() < 3 ? halo_pf<CI, CO, S, NPX, MODE>() : 3)
+                                  : halo_pf<CI, CO, S, NPX, MODE>();
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   bf16_t* hs = smem;
   // the output tile: its own LDS region when the launch found room (cs_off > 0: the band's
@@ -278,7 +407,20 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
   // the first band's halo is in flight during the weight prologue
   uint4 hv[NPF];
   uint32_t hok;
-  halo_fetch<CI, NPF>(hv, hok, xp, g, (blk / g.tpi) * g.IMGS, band_row0(blk));
+  // BNIN 2: the shortcut chunks beside x's, the trial's shortcut / output bases
+  constexpr bool BR = BNIN >= 2;
+  constexpr int RK = BNIN == 3 ? 1 : 0;
+  uint4 rv[BR ? NPF : 1];
+  const int hl = 31 - __builtin_clz(g.H);
+  const bf16_t* rp = !BR ? nullptr
+                     : RK ? bn.res + p * ((int64_t)g.Bn * 4 * g.H * g.H * bn.res_c)
+                          : bn.res + p * x_batch;
+  bf16_t* op = BR ? bn.out + p * x_batch : nullptr;
+  if constexpr (BR)
+    halo_fetch_res<CI, NPF, RK>(hv, rv, hok, xp, rp, bn, g, (blk / g.tpi) * g.IMGS, band_row0(blk),
+                            hl);
+  else
+    halo_fetch<CI, NPF>(hv, hok, xp, g, (blk / g.tpi) * g.IMGS, band_row0(blk));
 
   // this wave's B fragments for every k step
   bf16x8 wr[KS];
@@ -375,7 +517,12 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
   for (int t = blk;; t += g.nb) {
     const bool have = t < g.tiles;
     const int b0 = (t / g.tpi) * g.IMGS, oy0 = (t % g.tpi) * g.TR;
-    if (have && !alias) halo_put<CI, S, NPF, BNIN>(hs, hv, hok, xp, g, b0, band_row0(t), bntab);
+    if (have && !alias) {
+      if constexpr (BR)
+        halo_put_res<CI, S, NPF, RK>(hs, hv, rv, hok, xp, rp, op, bn, g, b0, band_row0(t), hl, bntab);
+      else
+        halo_put<CI, S, NPF, BNIN>(hs, hv, hok, xp, g, b0, band_row0(t), bntab);
+    }
     __syncthreads();
     if (pt >= 0) {
       // ---- copy-out of band pt: contiguous (b0, oy0 .. oy0 + TR) or whole images b0 .. ----
@@ -447,7 +594,13 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
     }
     if (alias) {
       __syncthreads();   // the copy-out is done with the tile the halo overwrites
-      if (have) halo_put<CI, S, NPF, BNIN>(hs, hv, hok, xp, g, b0, band_row0(t), bntab);
+      if (have) {
+        if constexpr (BR)
+          halo_put_res<CI, S, NPF, RK>(hs, hv, rv, hok, xp, rp, op, bn, g, b0, band_row0(t), hl,
+                                   bntab);
+        else
+          halo_put<CI, S, NPF, BNIN>(hs, hv, hok, xp, g, b0, band_row0(t), bntab);
+      }
       __syncthreads();
     }
     if (!have) break;
@@ -480,7 +633,11 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
     }
     {   // the next band's halo (the current one again past the last: loads stay unconditional)
       const int tn = t + g.nb < g.tiles ? t + g.nb : t;
-      halo_fetch<CI, NPF>(hv, hok, xp, g, (tn / g.tpi) * g.IMGS, band_row0(tn));
+      if constexpr (BR)
+        halo_fetch_res<CI, NPF, RK>(hv, rv, hok, xp, rp, bn, g, (tn / g.tpi) * g.IMGS,
+                                band_row0(tn), hl);
+      else
+        halo_fetch<CI, NPF>(hv, hok, xp, g, (tn / g.tpi) * g.IMGS, band_row0(tn));
     }
 
     f32x4 acc[MFW];
@@ -771,7 +928,10 @@ int launch_fwd(const void* x, const void* w, void* y, void* sums, int P, int Bn,
   constexpr int NPX = (MODE == kDgrad2 && CI >= 32) ? 128 : npx_for(CO);
   Geom g{};
   // (64-wide outputs: half the workgroups, twice the bands each -- their weight prologue is long)
-  if (!make_geom(g, Bn, H, MODE == kDgrad2 ? 2 : S, NPX, CO >= 64 ? MOPT_FWD_BLOCKS / 2 : MOPT_FWD_BLOCKS, P, MODE))
+  // (the 16-channel BNIN 2 forward holds 3 workgroups per CU, not 4: one wave of them)
+  const int blocks = CO >= 64 ? MOPT_FWD_BLOCKS / 2
+                     : (BNIN >= 2 && CO == 16) ? MOPT_FWD_BLOCKS * 3 / 4 : MOPT_FWD_BLOCKS;
+  if (!make_geom(g, Bn, H, MODE == kDgrad2 ? 2 : S, NPX, blocks, P, MODE))
     return (int)hipErrorInvalidValue;
   const size_t hb = halo_bytes<CI, S>(g), ob = (size_t)NPX * (CO + 8) * 2;
   const size_t tab = BNIN ? (size_t)2 * CI * sizeof(float) : 0;
@@ -910,6 +1070,38 @@ int mopt_dconv_dgrad_bnsums(const void* dy, const void* w, void* dbn, void* sums
   if (Ci == c && Co == c) \
     return launch_fwd<c, c, kDgrad, 1, 0, 0, 1>(dy, w, dbn, sums, P, Bn, H, st, nullptr, 0, bn);
   X(16) X(32) X(64)
+#undef X
+  return (int)hipErrorNotSupported;
+}
+
+// Forward of a convolution whose input is a block output relu(BatchNorm(x) + shortcut), formed
+// while the input bands are staged: y [P*Bn, H/S, H/S, Co] = conv(relu(fma(x, sc, sh) + res), w)
+// with sc = gamma rstd, sh = beta - mean sc (stat [P][2][Ci] mean / rstd, gamma / beta [P][Ci]),
+// res shaped like x (res_c = 0), the option-A shortcut of a [P*Bn, 2H, 2H, res_c] block input
+// (res_c > 0), or none (res null: the stem's relu(BN(x))); the block output itself is written to
+// out (shaped like x) and y's batch sums are added into sums [P][2][Co] (zeroed by the caller).
+int mopt_dconv_bnres_fwd(const void* x, const void* w, void* y, void* sums, void* out,
+                         const void* res, int res_c, const void* stat, const void* gamma,
+                         const void* beta, int P, int Bn, int H, int Ci, int Co, int stride,
+                         void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (out == nullptr || stat == nullptr || gamma == nullptr || beta == nullptr ||
+      sums == nullptr || (res == nullptr && res_c != 0) || (res_c % 8) || res_c > Ci)
+    return (int)hipErrorInvalidValue;
+  BnIn bn{(const float*)stat, (const bf16_t*)gamma, (const bf16_t*)beta, nullptr, nullptr,
+          (const bf16_t*)(res != nullptr ? res : x), (bf16_t*)out, res_c,
+          res != nullptr ? 1.f : 0.f};
+  // (BNIN 2: shortcut shaped like x or none; 3: option-A -- the block outputs whose block
+  //  changed its width, at the two widths a CIFAR ResNet changes to)
+#define X(ci, co, s) \
+  if (Ci == ci && Co == co && stride == s && res_c == 0) \
+    return launch_fwd<ci, co, kFwd, s, 0, 2>(x, w, y, sums, P, Bn, H, st, nullptr, 0, bn);
+  X(16, 16, 1) X(16, 32, 2) X(32, 32, 1) X(32, 64, 2) X(64, 64, 1)
+#undef X
+#define X(c) \
+  if (Ci == c && Co == c && stride == 1 && res_c > 0) \
+    return launch_fwd<c, c, kFwd, 1, 0, 3>(x, w, y, sums, P, Bn, H, st, nullptr, 0, bn);
+  X(32) X(64)
 #undef X
   return (int)hipErrorNotSupported;
 }

@@ -221,7 +221,9 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
       unpack8(rr[u], rv);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float o = v[e] * sc[e] + sh[e] + rv[e];
+        // (explicit fma: conv_direct.hip's bnres_chunk forms the same block output in its
+        //  staging and must round identically)
+        const float o = fmaf(v[e], sc[e], sh[e]) + rv[e];
         v[e] = relu ? fmaxf(o, 0.f) : o;
       }
       *(uint4*)(y + ((int64_t)p * M + ru) * C + 8 * ch) = pack8(v);
