@@ -523,6 +523,9 @@ class _BNResConv3x3(torch.autograd.Function):
         ctx.bn_mailbox, ctx.res_sub2, ctx.has_res = bn_mailbox, res_sub2, res is not None
         ctx.conv_mailbox, ctx.grad_w = conv_mailbox, grad_w
         ctx.mark_non_differentiable(h)
+        # (h has no gradient: without this autograd hands backward a zero-filled dh -- a 134 MB
+        #  fill per stage-1 block, measured +120 us per ResNet-20 step)
+        ctx.set_materialize_grads(False)
         return y, h
 
     @staticmethod
