@@ -701,6 +701,7 @@ class _Head(torch.autograd.Function):
               gb.data_ptr(), loss.data_ptr(), correct.data_ptr(), _s(h))
         ctx.save_for_backward(dh)
         ctx.mark_non_differentiable(correct)
+        ctx.set_materialize_grads(False)     # (no zero-filled gradient of `correct`)
         return loss, correct
 
     @staticmethod
