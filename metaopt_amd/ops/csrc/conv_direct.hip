@@ -726,6 +726,18 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
   }
 }
 
+// weight-gradient dy tile row stride (elements): with 8 consecutive pixel rows per transposed
+// read (below) a row stride of 8 dwords x an odd number spreads them over all 64 banks
+// (MOPT_WGRAD_PERM=0: the direct pixel order and CO + 8 rows, for A/B builds)
+#ifndef MOPT_WGRAD_PERM
+#define MOPT_WGRAD_PERM 1
+#endif
+// (64 channels: 72, 0.2-0.4 modelled extra cycles where 80 has none -- 80 pushes the stride-2
+//  32 -> 64 kernel's halo + tile past the 64 KB per workgroup)
+constexpr int wgrad_lsd(int co) {
+  return !MOPT_WGRAD_PERM ? co + 8 : co == 16 ? 16 : co == 32 ? 48 : co + 8;
+}
+
 template <int CI, int CO, int NPX, int S, int BNIN = 0>
 __global__ __launch_bounds__(256) void dconv_wgrad_kernel(const bf16_t* __restrict__ x,
                                                           const bf16_t* __restrict__ dy,
@@ -733,7 +745,7 @@ __global__ __launch_bounds__(256) void dconv_wgrad_kernel(const bf16_t* __restri
                                                           const Geom g, int P, const BnIn bn) {
   constexpr int M = 9 * CI;
   constexpr int MFT = (M + 15) / 16, NFT = CO / 16, MFW = (MFT + 3) / 4;
-  constexpr int LSD = CO + 8;
+  constexpr int LSD = wgrad_lsd(CO);
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   const int halo = g.IMGS * g.TRI * g.WI * pstride<CI, S>();
   bf16_t* hs = smem;
@@ -811,7 +823,15 @@ __global__ __launch_bounds__(256) void dconv_wgrad_kernel(const bf16_t* __restri
     //  VGPRs of the 16-channel kernel and cost more in occupancy than the ALU saved)
 #pragma unroll 2
     for (int ks = 0; ks < NKS; ++ks) {
-      const int ka = 32 * ks + 8 * gq + q, kb = ka + 4;  // the lane's two pixel rows
+      // the lane's two pixel rows: k = 8 gq + j of the MFMA (j < 4 from the first transposed
+      // read, j >= 4 from the second) is pixel 16 (gq >> 1) + 8 (j >> 2) + 4 (gq & 1) + (j & 3)
+      // of the k-step -- any bijection works (A and B share it); this one gives each 32-lane
+      // half of a transposed read 8 CONSECUTIVE pixels, 8 x 32 B of distinct banks (the direct
+      // order, rows r and r + 8 in one half, conflicted 2-way on every layout: 2.0 extra cycles
+      // per read, scripts/lds_banks.py model; 1.8-2.5 measured, profiles/r6/resnet_pmc/)
+      const int ka = MOPT_WGRAD_PERM ? 32 * ks + 16 * (gq >> 1) + 4 * (gq & 1) + q
+                                     : 32 * ks + 8 * gq + q;
+      const int kb = ka + (MOPT_WGRAD_PERM ? 8 : 4);
       const int pa = pix_base<CI, S>(g, ka), pb = pix_base<CI, S>(g, kb);
       bf16x8 b[NFT];
 #pragma unroll
@@ -966,7 +986,7 @@ int launch_wgrad(const void* x, const void* dy, void* dw, void* part, int P, int
     *nb_out = g.nb;
     return 0;
   }
-  const size_t lds = halo_bytes<CI, S>(g) + (size_t)NPX * (CO + 8) * 2 + 16 +
+  const size_t lds = halo_bytes<CI, S>(g) + (size_t)NPX * wgrad_lsd(CO) * 2 + 16 +
                      (BNIN ? (size_t)2 * CI * sizeof(float) : 0);
   if (lds > 64 * 1024) return (int)hipErrorNotSupported;
   hipLaunchKernelGGL((dconv_wgrad_kernel<CI, CO, NPX, S, BNIN>), dim3(P * g.nb), dim3(256), lds,

@@ -36,10 +36,29 @@ constexpr int LS = kLdsStride;
 // conflicts) dQ + dK/dV ran 324 against 289 us (profiles/r5/attn_swizzle/).  (Round 4 measured
 // another swizzle, chunk ^ (row >> 1) & 7, slower even in the forward: it mixed the rows that
 // otherwise differ by immediate offsets; swz128 leaves row bits 0, 2, 4, 5 out.)
+// The backward kernels' padded tiles (round 6): rows of LSB = 80 elements (40 dwords) and a key /
+// query order within each 32-row step (row_of below) that gives every 32-lane half of a
+// transposed read 8 CONSECUTIVE rows -- 8 x 8 dwords at multiples of 40 mod 64, all 64 banks --
+// and every 16-lane group of a fragment read distinct banks: the scripts/lds_banks.py model goes
+// from 4 / 2 extra cycles per fragment / transposed read (72-element rows, direct order: rows r
+// and r + 8 of one half always share banks) to 0 / 0.
+// (MOPT_ATTN_PERM=0: the direct order and 72-element rows, for A/B builds)
+#ifndef MOPT_ATTN_PERM
+#define MOPT_ATTN_PERM 1
+#endif
+constexpr int LSB = MOPT_ATTN_PERM ? 80 : LS;
 template <bool SW>
-__device__ __forceinline__ int toff(int r, int c) { return SW ? soff(r, c) : r * LS + c; }
+__device__ __forceinline__ int toff(int r, int c) { return SW ? soff(r, c) : r * LSB + c; }
 template <bool SW>
-constexpr int tile_elems() { return SW ? 64 * D : 64 * LS; }
+constexpr int tile_elems() { return SW ? 64 * D : 64 * LSB; }
+
+// Row (key or query) of MFMA k index 8 g + j of 32-row step ks: the direct order (forward,
+// PB = false), or the backward's (PB): 16 (g >> 1) + 8 (j >> 2) + 4 (g & 1) + (j & 3).
+template <bool PB>
+__device__ __forceinline__ int row_of(int ks, int g, int j) {
+  return (PB && MOPT_ATTN_PERM) ? 32 * ks + 16 * (g >> 1) + 8 * (j >> 2) + 4 * (g & 1) + (j & 3)
+                                : 32 * ks + 8 * g + j;
+}
 
 // Occupancy targets (waves per SIMD; 0 = the compiler's choice): the register cap that lets N
 // workgroups share a CU.  Swept in round 4 on variant builds (scripts/attn_bench.py,
@@ -92,16 +111,25 @@ __device__ __forceinline__ void tile_store(const uint4& r0, const uint4& r1, bf1
   *(uint4*)(s + toff<SW>((tid + 256) >> 3, (tid & 7) * 8)) = r1;
 }
 
-// Key row of the permuted K/V fragment: tile j = 2s + h, fragment row m.
+// Key row of the permuted K/V fragment: tile j = 2s + h, fragment row m -- the row whose score
+// lands in accumulator register (j, r) of lane group g where the P.V B operand wants key
+// row_of(s, g, 4 h + r): m = 4 g + r
+template <bool PB>
 __device__ __forceinline__ int perm_row(int s, int h, int m) {
-  return 32 * s + 8 * (m >> 2) + 4 * h + (m & 3);
-}
+  if constexpr (PB) return row_of<true>(s, m >> 2, 4 * h + (m & 3));
+  return 32 * s + 8 * (m >> 2) + 4 * h + (m & 3);   // (the forward's own expression: its code
+}                                                   //  is register-tuned, 88 VGPRs)
 
 // V^T (or K^T) A-fragment for keys 32s + 8g .. +7, head-dim columns 16 dt .. +15, from LDS [key][dh].
 template <bool SW>
 __device__ __forceinline__ bf16x8 tr_frag(const bf16_t* s, int ks, int g, int q, int pp, int dt) {
-  const s16x4 lo = lds_tr4(s + toff<SW>(32 * ks + 8 * g + q, 16 * dt + 4 * pp));
-  const s16x4 hi = lds_tr4(s + toff<SW>(32 * ks + 8 * g + 4 + q, 16 * dt + 4 * pp));
+  if constexpr (SW) {
+    const s16x4 lo = lds_tr4(s + toff<SW>(32 * ks + 8 * g + q, 16 * dt + 4 * pp));
+    const s16x4 hi = lds_tr4(s + toff<SW>(32 * ks + 8 * g + 4 + q, 16 * dt + 4 * pp));
+    return cat_frag(lo, hi);
+  }
+  const s16x4 lo = lds_tr4(s + toff<SW>(row_of<true>(ks, g, q), 16 * dt + 4 * pp));
+  const s16x4 hi = lds_tr4(s + toff<SW>(row_of<true>(ks, g, 4 + q), 16 * dt + 4 * pp));
   return cat_frag(lo, hi);
 }
 
@@ -177,7 +205,7 @@ __device__ __forceinline__ void scores_T(const bf16_t* Ks, const bf16x8 (&qf)[2]
   for (int s = 0; s < 2; ++s)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int j = 2 * s + h, row = perm_row(s, h, li);
+      const int j = 2 * s + h, row = perm_row<!SW>(s, h, li);
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) acc = mfma16(lds_frag(Ks + toff<SW>(row, 32 * ks + 8 * g)), qf[ks], acc);
@@ -391,7 +419,7 @@ __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnDqWaves) void attn_bwd_dq
       for (int r = 0; r < 4; ++r) {
         float p = fast_exp2(st[j][r] * c - lse);
         if (kb == qb) {
-          const int key = kb * BKV + 32 * (j >> 1) + 8 * g + 4 * (j & 1) + r;
+          const int key = kb * BKV + row_of<true>(j >> 1, g, 4 * (j & 1) + r);
           if (key > qrow) p = 0.f;
         }
         st[j][r] = p * (dpt[j][r] - dsum);   // dS (without the scale)
@@ -493,7 +521,7 @@ __global__ __launch_bounds__(256) MOPT_WAVES_ATTR(kAttnDkdvWaves) void attn_bwd_
     for (int j = 0; j < 4; ++j) {
       // the 4 queries of register r = 0..3 are consecutive: one 16-byte LDS read each for LSE2
       // and Dsum (instead of 8 4-byte reads)
-      const int q0 = 32 * (j >> 1) + 8 * g + 4 * (j & 1);
+      const int q0 = row_of<true>(j >> 1, g, 4 * (j & 1));
       const f32x4 l4 = *(const f32x4*)(lse_s + q0), d4 = *(const f32x4*)(dsum_s + q0);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {

@@ -16,6 +16,7 @@
 #   kbench_rows      the microbench at 128 / 256 / 512 rows per step (multi-row-block kernels)
 #   pmc_kbench       PMC passes of the MLP kernels (fetch/write/MFMA/LDS, one pass each)
 #   pmc_attn         PMC passes of the attention microbench (busy / wait / MFMA, LDS / VALU)
+#   pmc_resnet       HBM FETCH / WRITE passes of a short ResNet-20 run (scripts/dev/pmc_bytes.py)
 #   pmc_gemm         PMC passes of the GEMM microbench ($SHAPES name prefix, $CFGS tile configs)
 #   lm resnet hyper  bench_configs.py of one config        trace_lm trace_resnet trace_hyper
 #   attn             attention fwd / bwd microbench (LM-125M shape)
@@ -59,6 +60,14 @@ pmcg() {   # pmcg NAME COUNTERS...: one counter pass over the GEMM microbench ($
       --cfgs "${CFGS:-11,12}" > "$ROOT/$OUT/$name.log" 2>&1)
 }
 
+pmcr() {   # pmcr NAME COUNTERS...: one counter pass over a short ResNet-20 population run
+  local name=$1; shift
+  (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 240 rocprofv3 --output-format csv \
+      --pmc "$@" -d "$ROOT/$OUT/$name" -o run -- \
+      python3 "$ROOT/scripts/bench_configs.py" --config resnet20 --sync-every 4 --steps 4 \
+      --warmup 4 > "$ROOT/$OUT/$name.log" 2>&1)
+}
+
 pmca() {   # pmca NAME COUNTERS...: one counter pass over the attention microbench
   local name=$1; shift
   (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 150 rocprofv3 --output-format csv \
@@ -93,6 +102,12 @@ for step in "$@"; do
       pmcg pmcg_busy SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE
       pmcg pmcg_lds SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES
       pmcg pmcg_fetch FETCH_SIZE ;;
+    pmc_resnet) # HBM bytes per ResNet-20 kernel (scripts/dev/pmc_bytes.py reads the two passes)
+      pmcr pmc_fetch FETCH_SIZE
+      pmcr pmc_write WRITE_SIZE ;;
+    pmc_resnet_busy) # issue / wait / LDS counters per ResNet-20 kernel (scripts/pmc_table.py)
+      pmcr pmcr_busy SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE
+      pmcr pmcr_lds SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES ;;
     pmc_attn)   # PMC passes of the attention kernels
       pmca pmca_busy SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE
       pmca pmca_lds SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES ;;
