@@ -322,6 +322,17 @@ __device__ __forceinline__ void bnin_table(float* tab, const BnIn& bn, int p) {
   }
 }
 
+// The band pixel of MFMA fragment row m (0..15) under PIXP: bits (0, 1, 2, 3) of m move to bits
+// (1, 2, 0, 3) -- the scripts/lds_banks.py search's conflict-free order for 16 pixels spanning two
+// 8-pixel rows of a 80-element-stride halo (MOPT_FWD_PIXP=0: the direct order, A/B builds).
+#ifndef MOPT_FWD_PIXP
+#define MOPT_FWD_PIXP 1
+#endif
+template <bool PIXP>
+__device__ __forceinline__ int frag_pix(int m) {
+  return PIXP ? (((m & 1) << 1) | (((m >> 1) & 1) << 2) | ((m >> 2) & 1) | (m & 8)) : m;
+}
+
 // halo offset of output pixel pl of a band (tap (0, 0), channel 0)
 template <int CI, int S>
 __device__ __forceinline__ int pix_base(const Geom& g, int pl) {
@@ -375,6 +386,11 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
   constexpr int WN = CO / 16, WM = 4 / WN;
   constexpr int MFW = NPX / 16 / WM;      // 16-pixel fragments per wave
   constexpr int LSC = CO + 8;
+  // 64 channels at stride 1 (8 x 8 images: a fragment's 16 pixels are two image rows): fragment
+  // row li multiplies band pixel frag_pix(li) -- with the direct order the two rows' halo pixels
+  // met the same banks (4 extra cycles per A-fragment read on every pixel stride, 2.9 measured);
+  // the epilogue stores C row m at tile row frag_pix(m), so the copy-out is unchanged
+  constexpr bool PIXP = MOPT_FWD_PIXP && CI >= 64 && S == 1 && MODE != kDgrad2;
   // (64-channel data gradients with an addend: one prefetched chunk -- the addend registers on
   //  top of a full prefetch cost the kernel its second workgroup per CU, 51 -> 72 us in situ)
   // (BNIN 2 / 3: x and the shortcut in flight -- at most 3 chunks of each, the rest of a band
@@ -472,7 +488,7 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
 #pragma unroll
   for (int i = 0; i < MFW; ++i) {
     const int pl = (wm * MFW + i) * 16 + li;
-    pb[i] = pix_base<CI, S>(g, pl);
+    pb[i] = pix_base<CI, S>(g, (wm * MFW + i) * 16 + frag_pix<PIXP>(li));
     const int rem = pl & ((1 << g.rpil) - 1);
     ply[i] = ((pl >> g.rpil) * g.TRI) * 2 + (rem >> g.owl);  // kDgrad2: 2 img TRI + ly
     pox[i] = rem & ((1 << g.owl) - 1);
@@ -675,7 +691,7 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
     for (int i = 0; i < MFW; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = (wm * MFW + i) * 16 + 4 * gq + r;
+        const int row = (wm * MFW + i) * 16 + frag_pix<PIXP>(4 * gq + r);
         const bf16_t v = f2bf(acc[i][r]);
         cs[row * LSC + n] = v;
         if (row < valid) {
