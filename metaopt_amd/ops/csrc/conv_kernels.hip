@@ -36,7 +36,10 @@ __device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
 // once into registers and its rows are strided by the 256 / (C / 8) row groups of the block --
 // no 64-bit division per element, and UNROLL independent 16-byte loads in flight per thread
 // (round 2's one-vector-per-thread versions ran at ~1.5 TB/s: 37 % of a ResNet-20 step).
-constexpr int UNROLL = 4;
+#ifndef MOPT_BN_UNROLL
+#define MOPT_BN_UNROLL 4
+#endif
+constexpr int UNROLL = MOPT_BN_UNROLL;
 
 // Per (trial, channel) reductions over the trial's M rows: a wave's lanes with the same ch are
 // summed by xor-shuffles over the lane bits above log2(C/8), then the 4 waves through LDS, then
@@ -234,6 +237,9 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
 // dz = dy * relu'(y); dx = gamma rstd (dz - sum(dz)/M - xhat sum(dz xhat)/M) = k1 dz + k2 x + k3
 // per (trial, channel) constants; dres = dz.  Block (0, 0) also writes (sum dz xhat, sum dz)
 // straight into the bf16 dgamma / dbeta gradients when given.
+// RELU (the relu mode) is a template parameter: with one kernel for all three modes the y stream's
+// registers and the shift constants were allocated for every mode (130 VGPRs, 3 waves per SIMD)
+template <int RELU>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restrict__ x,
                                                            const bf16_t* __restrict__ y,
                                                            const bf16_t* __restrict__ dy,
@@ -246,7 +252,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
                                                            bf16_t* __restrict__ dgamma,
                                                            bf16_t* __restrict__ dbeta, int64_t M,
                                                            int C, int P, int rows_per_block,
-                                                           int relu) {
+                                                           int relu_rt) {
+  const int relu = RELU >= 0 ? RELU : relu_rt;   // (-1: the runtime mode, MOPT_BN_APPLY_RT A/B)
   const int cc = C >> 3, p = blockIdx.y;
   const int tid = threadIdx.x, ch = tid & (cc - 1), rg = tid / cc, ng = 256 / cc;
   if (blockIdx.x == 0 && blockIdx.y == 0 && dgamma != nullptr) {
@@ -377,7 +384,14 @@ int mopt_bn_bwd(const void* x, const void* y, const void* dy, const void* stat, 
                        dim3(256), 0, st, (const bf16_t*)x, (const bf16_t*)y, (const bf16_t*)dy,
                        (const float*)stat, (const bf16_t*)gamma, (const bf16_t*)beta,
                        (float*)sums, M, C, rpb, relu);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3((unsigned)((M + rpb - 1) / rpb), P), dim3(256), 0,
+#ifndef MOPT_BN_APPLY_RT
+#define MOPT_BN_APPLY_RT 0
+#endif
+  auto apply = MOPT_BN_APPLY_RT ? bn_bwd_apply_kernel<-1>
+               : relu == 0      ? bn_bwd_apply_kernel<0>
+               : relu == 1      ? bn_bwd_apply_kernel<1>
+                                : bn_bwd_apply_kernel<2>;
+  hipLaunchKernelGGL(apply, dim3((unsigned)((M + rpb - 1) / rpb), P), dim3(256), 0,
                      st, (const bf16_t*)x, (const bf16_t*)y, (const bf16_t*)dy, (const float*)stat,
                      (const float*)sums, (const bf16_t*)gamma, (const bf16_t*)beta, (bf16_t*)dx,
                      (bf16_t*)dres,
