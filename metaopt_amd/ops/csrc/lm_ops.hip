@@ -172,6 +172,84 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_dx_kernel(const bf16_t* __res
   }
 }
 
+// The same backward with the weight gradient's partial sums fused in: workgroup (s, p) takes
+// split s of trial p's rows (the slices of rmsnorm_dw_partial_kernel), its 4 waves a row each in
+// turn, every lane summing dy * xhat of its columns across the rows; the 4 waves' sums meet in
+// LDS and one f32 partial per (trial, split, column) is stored in rmsnorm_dw_partial_kernel's
+// layout for rmsnorm_dw_reduce_kernel -- the partial kernel's second read of x and dy (a full
+// pass over two activations per norm) goes.  NCH: 8-column chunks per lane (d <= 512 NCH).
+template <bool RES, int NCH>
+__global__ __launch_bounds__(256) void rmsnorm_bwd_dxdw_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, const bf16_t* __restrict__ dy,
+    const bf16_t* __restrict__ dres, const float* __restrict__ rstd, bf16_t* __restrict__ dx,
+    float* __restrict__ part, int d, int rows_per_trial, int S) {
+  extern __shared__ __attribute__((aligned(16))) float red[];   // [4][d]
+  const int s = blockIdx.x, p = blockIdx.y, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nc = d >> 3, G = nc;
+  const int per = (rows_per_trial + S - 1) / S;
+  const int r0 = p * rows_per_trial + s * per;
+  const int r1 = min(r0 + per, (p + 1) * rows_per_trial);
+  float wv[NCH][8], acc[NCH][8];
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = lane + 64 * k;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[k][e] = 0.f;
+    if (c < nc) unpack8(*(const uint4*)(w + (size_t)p * d + 8 * c), wv[k]);
+  }
+  for (int row = r0 + wave; row < r1; row += 4) {
+    const float r = rstd[row];
+    float xh[NCH][8], gv[NCH][8];
+    float dot = 0.f;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int c = lane + 64 * k;
+      if (c < nc) {
+        float dv[8];
+        unpack8(*(const uint4*)(x + (size_t)row * d + 8 * c), xh[k]);
+        unpack8(*(const uint4*)(dy + (size_t)row * d + 8 * c), dv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          xh[k][e] *= r;
+          acc[k][e] += dv[e] * xh[k][e];
+          gv[k][e] = dv[e] * wv[k][e];
+          dot += gv[k][e] * xh[k][e];
+        }
+      }
+    }
+    const float mdot = wave_sum(dot) / d;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int c = lane + 64 * k;
+      if (c < nc) {
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = r * (gv[k][e] - xh[k][e] * mdot);
+        if (RES) {
+          float rv[8];
+          unpack8(*(const uint4*)(dres + (size_t)row * d + 8 * c), rv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] += rv[e];
+        }
+        *(uint4*)(dx + (size_t)row * d + 8 * c) = pack8(o);
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = lane + 64 * k;
+    if (c < nc) {
+      *(f32x4*)(red + wave * d + 8 * c) = f32x4{acc[k][0], acc[k][1], acc[k][2], acc[k][3]};
+      *(f32x4*)(red + wave * d + 8 * c + 4) = f32x4{acc[k][4], acc[k][5], acc[k][6], acc[k][7]};
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < d; i += 256) {
+    const float v = (red[i] + red[d + i]) + (red[2 * d + i] + red[3 * d + i]);
+    part[(((size_t)p * G + i / 8) * S + s) * 8 + i % 8] = v;
+  }
+}
+
 // dw[p][col] += sum over a slice of trial p's rows of dy * x * rstd.  grid (d/256, splits, P).
 __global__ __launch_bounds__(256) void rmsnorm_bwd_dw_kernel(const bf16_t* __restrict__ x,
                                                              const bf16_t* __restrict__ dy,
@@ -1072,6 +1150,34 @@ int mopt_rmsnorm_dw16(const void* x, const void* dy, const void* rstd, void* par
   hipLaunchKernelGGL(rmsnorm_dw_partial_kernel, dim3((G + bx - 1) / bx, S, P), dim3(bx), 0, st,
                      (const bf16_t*)x, (const bf16_t*)dy, (const float*)rstd, (float*)part, d,
                      rows_per_trial);
+  hipLaunchKernelGGL(rmsnorm_dw_reduce_kernel, dim3((P * G + 3) / 4), dim3(256), 0, st,
+                     (const float*)part, (bf16_t*)dw16, P * G, S);
+  return (int)hipGetLastError();
+}
+
+// dx = rmsnorm_bwd(dy) (+ dres when non-null) and the bf16 weight gradient dw16 [P][d] of the same
+// pass (rmsnorm_bwd_dxdw_kernel + rmsnorm_dw_reduce_kernel; part: mopt_rmsnorm_dw_splits(rpt) *
+// P * d f32, fully overwritten)
+int mopt_rmsnorm_bwd_dw16(const void* x, const void* w, const void* dy, const void* dres,
+                          const void* rstd, void* dx, void* part, void* dw16, int rows, int d,
+                          int rows_per_trial, void* stream) {
+  if (d % 8 || d > 64 * 8 * kMaxChunks || rows % rows_per_trial) return 1;
+  hipStream_t st = (hipStream_t)stream;
+  const int P = rows / rows_per_trial, S = mopt_rmsnorm_dw_splits(rows_per_trial), G = d / 8;
+  const int nch = (G + 63) / 64;
+  const size_t lds = (size_t)4 * d * sizeof(float);
+#define L(RES, N)                                                                               \
+  hipLaunchKernelGGL((rmsnorm_bwd_dxdw_kernel<RES, N>), dim3(S, P), dim3(256), lds, st,         \
+                     (const bf16_t*)x, (const bf16_t*)w, (const bf16_t*)dy, (const bf16_t*)dres, \
+                     (const float*)rstd, (bf16_t*)dx, (float*)part, d, rows_per_trial, S)
+  const bool res = dres != nullptr;
+  switch (nch) {
+    case 1: if (res) L(true, 1); else L(false, 1); break;
+    case 2: if (res) L(true, 2); else L(false, 2); break;
+    case 3: if (res) L(true, 3); else L(false, 3); break;
+    default: if (res) L(true, 4); else L(false, 4); break;
+  }
+#undef L
   hipLaunchKernelGGL(rmsnorm_dw_reduce_kernel, dim3((P * G + 3) / 4), dim3(256), 0, st,
                      (const float*)part, (bf16_t*)dw16, P * G, S);
   return (int)hipGetLastError();

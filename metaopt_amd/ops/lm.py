@@ -31,6 +31,7 @@ _lib.register_signatures({
     "mopt_rmsnorm_bwd_res": ([c_void_p] * 7 + [c_int, c_int, c_int, c_void_p], c_int),
     "mopt_rmsnorm_dw_splits": ([c_int], c_int),
     "mopt_rmsnorm_dw16": ([c_void_p] * 5 + [c_int, c_int, c_int, c_void_p], c_int),
+    "mopt_rmsnorm_bwd_dw16": ([c_void_p] * 8 + [c_int, c_int, c_int, c_void_p], c_int),
     "mopt_rope_fwd": ([c_void_p] * 6 + [c_int] * 4 + [c_void_p], c_int),
     "mopt_rope_bwd": ([c_void_p] * 6 + [c_int] * 4 + [c_void_p], c_int),
     "mopt_pgemm_qkv_rope": ([c_void_p] * 5 + [c_int] * 7 + [c_int64, c_int64, c_int, c_void_p],
@@ -175,6 +176,21 @@ def _dw_out(dw32, gw, dtype, stream_of):
     return dw32.to(dtype)
 
 
+# RMSNorm backward with the weight gradient's partial sums in the dx pass (csrc/lm_ops.hip
+# rmsnorm_bwd_dxdw_kernel); MOPT_NORM_DXDW=0: the separate partial pass, for A/B runs
+_NORM_DXDW = os.environ.get("MOPT_NORM_DXDW", "1") != "0"
+
+
+def _norm_bwd_dw(x, w, dy, dres, rstd, dx, gw, rows_per_trial):
+    """dx (+ dres) and the weight gradient into the flat bf16 view ``gw`` in one pass over x and
+    dy (+ the partials' reduce)."""
+    R, d = x.shape
+    S = _lib.get_lib().mopt_rmsnorm_dw_splits(rows_per_trial)
+    part = torch.empty(S * (R // rows_per_trial) * d, dtype=torch.float32, device=x.device)
+    _call("mopt_rmsnorm_bwd_dw16", _p(x), _p(w), _p(dy), _p(dres) if dres is not None else None,
+          _p(rstd), _p(dx), _p(part), _p(gw), R, d, rows_per_trial, _stream(x))
+
+
 def _norm_dw(x, dy, rstd, gw, rows_per_trial):
     """RMSNorm weight gradient written into the flat bf16 gradient view ``gw``: per-slice f32
     partials, then one reduce that writes bf16 (no zero fill, no atomics, no cast kernel).
@@ -206,6 +222,9 @@ class _RMSNorm(torch.autograd.Function):
         dy = dy.contiguous()
         R, d = x.shape
         dx = torch.empty_like(x)
+        if ctx.gw is not None and _NORM_DXDW:
+            _norm_bwd_dw(x, w, dy, None, rstd, dx, ctx.gw, ctx.rpt)
+            return dx, None, None, None
         if ctx.gw is not None:
             _call("mopt_rmsnorm_bwd", _p(x), _p(w), _p(dy), _p(rstd), _p(dx), None, R, d,
                   ctx.rpt, _stream(x))
@@ -251,6 +270,9 @@ class _AddRMSNorm(torch.autograd.Function):
         dy = dy.contiguous()
         dres = dxs.contiguous() if dxs is not None else None
         dx = torch.empty_like(xs)
+        if ctx.gw is not None and _NORM_DXDW:
+            _norm_bwd_dw(xs, w, dy, dres, rstd, dx, ctx.gw, ctx.rpt)
+            return dx, dx, None, None, None
         dw32 = None if ctx.gw is not None else \
             torch.zeros(w.shape, dtype=torch.float32, device=xs.device)
         _call("mopt_rmsnorm_bwd_res", _p(xs), _p(w), _p(dy),
