@@ -31,11 +31,12 @@ _lib.register_signatures({
     "mopt_pconv": ([c_int] + [c_void_p] * 4 + [c_int] * 10 + [c_void_p], c_int),
     "mopt_dconv": ([c_int] + [c_void_p] * 4 + [c_int] * 7 + [c_void_p], c_int),
     "mopt_dconv_wgrad_splits": ([c_int] * 6, c_int),
-    "mopt_dconv_bnin": ([c_int] + [c_void_p] * 4 + [c_int] * 5 + [c_void_p] * 4, c_int),
+    "mopt_dconv_bnin": ([c_int] + [c_void_p] * 4 + [c_int] * 5 + [c_void_p] * 5 +
+                        [c_int64, c_float, c_float, c_void_p], c_int),
     "mopt_dconv_dgrad_bnsums": ([c_void_p] * 4 + [c_int] * 5 + [c_void_p] * 5, c_int),
     "mopt_dconv_dgrad_bnres": ([c_void_p] * 5 + [c_int] * 7 + [c_void_p] * 4, c_int),
-    "mopt_dconv_bnres_fwd": ([c_void_p] * 6 + [c_int] + [c_void_p] * 3 + [c_int] * 6 + [c_void_p],
-                             c_int),
+    "mopt_dconv_bnres_fwd": ([c_void_p] * 6 + [c_int] + [c_void_p] * 3 + [c_int] * 6 +
+                             [c_void_p, c_void_p, c_int64, c_float, c_float, c_void_p], c_int),
     "mopt_resnet_head": ([c_void_p] * 4 + [c_int] * 5 + [c_float, c_int] + [c_void_p] * 7,
                          c_int),
     "mopt_resnet_head_part_floats": ([c_int] * 3, c_int),
@@ -50,6 +51,10 @@ _BN_RES_DGRAD = os.environ.get("MOPT_BN_RES_DGRAD", "1") != "0"
 # ... and its forward apply pass folded into that convolution's input staging (``PendingBN``,
 # ``bn_res_conv3x3``; MOPT_BN_RES_FWD=0: the separate apply pass)
 _BN_RES_FWD = os.environ.get("MOPT_BN_RES_FWD", "1") != "0"
+# the BatchNorms whose apply runs inside a convolution's staging are also finalized there (the
+# kernel derives mean / rstd from the batch sums, its trial's first workgroup stores them and
+# the running update): no bn_finalize launch (MOPT_BN_FIN_IN_CONV=0: the separate launch)
+_BN_FIN_IN_CONV = os.environ.get("MOPT_BN_FIN_IN_CONV", "1") != "0"
 # (Ci, Co, stride) of the direct forward with the block output formed in its staging
 # (csrc/conv_direct.hip mopt_dconv_bnres_fwd): shortcut shaped like x or none / option-A
 _BNRES_FWD_SHAPES = {(16, 16, 1), (16, 32, 2), (32, 32, 1), (32, 64, 2), (64, 64, 1)}
@@ -363,13 +368,16 @@ class _BNReluConv3x3(torch.autograd.Function):
         Co = w.shape[-1]
         M = x.numel() // (P * C)
         stat = torch.empty(P, 2, C, dtype=torch.float32, device=x.device)
-        _call("mopt_bn_fwd", x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), 0, 0,
-              stat.data_ptr(), running.data_ptr(), sums.data_ptr(), P, M, C, eps, momentum, 1, 1,
-              1, 0, 0, _s(x))
+        fin = _BN_FIN_IN_CONV
+        if not fin:
+            _call("mopt_bn_fwd", x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), 0, 0,
+                  stat.data_ptr(), running.data_ptr(), sums.data_ptr(), P, M, C, eps, momentum,
+                  1, 1, 1, 0, 0, _s(x))
         y = torch.empty(N, H, W, Co, dtype=x.dtype, device=x.device)
         _call("mopt_dconv_bnin", 0, x.data_ptr(), w.data_ptr(), y.data_ptr(),
               out_sums.data_ptr(), P, N // P, H, C, Co, stat.data_ptr(), gamma.data_ptr(),
-              beta.data_ptr(), _s(x))
+              beta.data_ptr(), sums.data_ptr() if fin else 0, running.data_ptr() if fin else 0,
+              M, eps, momentum, _s(x))
         ctx.save_for_backward(x, gamma, beta, w, stat)
         ctx.meta = (P, M, C, Co)
         ctx.bwd_sums = arena.take(P * 2 * C).view(P, 2, C) if arena is not None else None
@@ -413,7 +421,8 @@ class _BNReluConv3x3(torch.autograd.Function):
         nb = lib.mopt_dconv_wgrad_splits(P, Bn, H, C, Co, 1)
         part = torch.empty(max(nb, 1) * P * 9 * C * Co, dtype=torch.float32, device=x.device)
         _call("mopt_dconv_bnin", 2, x.data_ptr(), dy.data_ptr(), dw.data_ptr(), part.data_ptr(),
-              P, Bn, H, C, Co, stat.data_ptr(), gamma.data_ptr(), beta.data_ptr(), _s(x))
+              P, Bn, H, C, Co, stat.data_ptr(), gamma.data_ptr(), beta.data_ptr(), 0, 0, 0, 0.0,
+              0.0, _s(x))
         dgamma = dbeta = None
         if not direct:
             dgamma = sums[:, 1].to(gamma.dtype)
@@ -504,9 +513,11 @@ class _BNResConv3x3(torch.autograd.Function):
         Co = w.shape[-1]
         M = x.numel() // (P * C)
         stat = torch.empty(P, 2, C, dtype=torch.float32, device=x.device)
-        _call("mopt_bn_fwd", x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), 0, 0,
-              stat.data_ptr(), running.data_ptr(), sums.data_ptr(), P, M, C, eps, momentum, 1, 1,
-              1, 0, 0, _s(x))
+        fin = _BN_FIN_IN_CONV
+        if not fin:
+            _call("mopt_bn_fwd", x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), 0, 0,
+                  stat.data_ptr(), running.data_ptr(), sums.data_ptr(), P, M, C, eps, momentum,
+                  1, 1, 1, 0, 0, _s(x))
         h = torch.empty_like(x)
         OH = out_hw(H, stride)
         y = torch.empty(N, OH, OH, Co, dtype=x.dtype, device=x.device)
@@ -514,6 +525,7 @@ class _BNResConv3x3(torch.autograd.Function):
         _call("mopt_dconv_bnres_fwd", x.data_ptr(), w.data_ptr(), y.data_ptr(),
               out_sums.data_ptr(), h.data_ptr(), 0 if res is None else res.data_ptr(), res_c,
               stat.data_ptr(), gamma.data_ptr(), beta.data_ptr(), P, N // P, H, C, Co, stride,
+              sums.data_ptr() if fin else 0, running.data_ptr() if fin else 0, M, eps, momentum,
               _s(x))
         ctx.save_for_backward(x, h, stat, gamma, beta, w)
         ctx.meta = (P, N // P, H, C, Co, stride, M)

@@ -200,6 +200,14 @@ struct BnIn {
   bf16_t* out;
   int res_c;
   float rmul;
+  // BNIN forwards that finalize the BatchNorm themselves (round 6: one bn_finalize_kernel launch
+  // less per BatchNorm): xsums [P][2][C] the batch sums of x, from which every workgroup derives
+  // its table; the trial's first workgroup also stores stat (mean, rstd, for the backward) and
+  // the running-statistics update -- bn_finalize_kernel's arithmetic, operation for operation
+  const float* xsums;
+  float* stat_w;
+  float* running;
+  float Mf, Mm1f, eps, momentum;
 };
 
 // BNIN 2 staging: relu(fma(x, sc, sh) + shortcut) of one chunk (bn_apply_kernel's arithmetic:
@@ -313,9 +321,24 @@ __device__ __forceinline__ void halo_put_res(bf16_t* hs, const uint4 (&v)[NPF],
 }
 
 template <int CI>
-__device__ __forceinline__ void bnin_table(float* tab, const BnIn& bn, int p) {
+__device__ __forceinline__ void bnin_table(float* tab, const BnIn& bn, int p, bool first) {
   for (int i = threadIdx.x; i < CI; i += 256) {
-    const float mean = bn.stat[(2 * p) * CI + i], rstd = bn.stat[(2 * p + 1) * CI + i];
+    float mean, rstd;
+    if (bn.xsums != nullptr) {
+      mean = bn.xsums[(2 * p) * CI + i] / bn.Mf;
+      const float var = fmaxf(bn.xsums[(2 * p + 1) * CI + i] / bn.Mf - mean * mean, 0.f);
+      rstd = rsqrtf(var + bn.eps);
+      if (first) {
+        float* rm = bn.running + (int64_t)p * 2 * CI;
+        rm[i] = (1.f - bn.momentum) * rm[i] + bn.momentum * mean;
+        rm[CI + i] = (1.f - bn.momentum) * rm[CI + i] + bn.momentum * var * bn.Mf / bn.Mm1f;
+        bn.stat_w[(2 * p) * CI + i] = mean;
+        bn.stat_w[(2 * p + 1) * CI + i] = rstd;
+      }
+    } else {
+      mean = bn.stat[(2 * p) * CI + i];
+      rstd = bn.stat[(2 * p + 1) * CI + i];
+    }
     const float sc = bf2f(bn.gamma[(int64_t)p * CI + i]) * rstd;
     tab[i] = sc;
     tab[CI + i] = bf2f(bn.beta[(int64_t)p * CI + i]) - mean * sc;
@@ -523,7 +546,7 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
     }
   }
   if constexpr (BNIN != 0) {
-    bnin_table<CI>(bntab, bn, p);
+    bnin_table<CI>(bntab, bn, p, blk == 0);
     __syncthreads();
   }
   // Band loop, one band behind on the copy-out: put(t) -> barrier -> copy-out(t - 1) -> loads
@@ -774,7 +797,7 @@ __global__ __launch_bounds__(256) void dconv_wgrad_kernel(const bf16_t* __restri
   const int li = lane & 15, gq = lane >> 4, q = li >> 2, pp = li & 3;
   if (threadIdx.x == 0) *(uint2*)zs = make_uint2(0, 0);
   if constexpr (BNIN != 0) {
-    bnin_table<CI>(bntab, bn, p);
+    bnin_table<CI>(bntab, bn, p, false);   // (stat read: finalized by the forward)
     __syncthreads();
   }
 
@@ -1074,12 +1097,26 @@ int mopt_dconv(int kind, const void* a, const void* b, void* out, void* aux, int
 // is relu(BatchNorm(x)) of the raw BatchNorm input x, applied while the halo bands are staged
 // (stat [P][2][Ci] mean / rstd, gamma / beta [P][Ci] bf16): the BatchNorm output is never
 // materialised.  Ci == Co in {16, 32, 64} (the second convolution of a ResNet basic block).
+// fin (kind 0): xsums [P][2][Ci] the batch sums of x, running [P][2][Ci]; the forward finalizes
+// the statistics itself -- stat is written (and the running statistics updated) by the kernel,
+// no bn_finalize launch (null: stat holds them already).
 int mopt_dconv_bnin(int kind, const void* a, const void* b, void* out, void* aux, int P, int Bn,
                     int H, int Ci, int Co, const void* stat, const void* gamma, const void* beta,
+                    const void* xsums, void* running, int64_t M, float eps, float momentum,
                     void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (stat == nullptr || gamma == nullptr || beta == nullptr) return (int)hipErrorInvalidValue;
-  const BnIn bn{(const float*)stat, (const bf16_t*)gamma, (const bf16_t*)beta, nullptr};
+  if (stat == nullptr || gamma == nullptr || beta == nullptr || (xsums && (kind != 0 || !running)))
+    return (int)hipErrorInvalidValue;
+  BnIn bn{(const float*)stat, (const bf16_t*)gamma, (const bf16_t*)beta, nullptr};
+  if (xsums != nullptr) {
+    bn.xsums = (const float*)xsums;
+    bn.stat_w = (float*)stat;
+    bn.running = (float*)running;
+    bn.Mf = (float)M;
+    bn.Mm1f = (float)(M - 1 > 1 ? M - 1 : 1);
+    bn.eps = eps;
+    bn.momentum = momentum;
+  }
 #define X(c) \
   if (Ci == c && Co == c) \
     return kind == 0 ? launch_fwd<c, c, kFwd, 1, 0, 1>(a, b, out, aux, P, Bn, H, st, nullptr, 0, bn) \
@@ -1116,17 +1153,29 @@ int mopt_dconv_dgrad_bnsums(const void* dy, const void* w, void* dbn, void* sums
 // res shaped like x (res_c = 0), the option-A shortcut of a [P*Bn, 2H, 2H, res_c] block input
 // (res_c > 0), or none (res null: the stem's relu(BN(x))); the block output itself is written to
 // out (shaped like x) and y's batch sums are added into sums [P][2][Co] (zeroed by the caller).
+// xsums / running / M / eps / momentum: as mopt_dconv_bnin's (the statistics finalized here).
 int mopt_dconv_bnres_fwd(const void* x, const void* w, void* y, void* sums, void* out,
                          const void* res, int res_c, const void* stat, const void* gamma,
                          const void* beta, int P, int Bn, int H, int Ci, int Co, int stride,
+                         const void* xsums, void* running, int64_t M, float eps, float momentum,
                          void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (out == nullptr || stat == nullptr || gamma == nullptr || beta == nullptr ||
-      sums == nullptr || (res == nullptr && res_c != 0) || (res_c % 8) || res_c > Ci)
+      sums == nullptr || (res == nullptr && res_c != 0) || (res_c % 8) || res_c > Ci ||
+      (xsums != nullptr && running == nullptr))
     return (int)hipErrorInvalidValue;
   BnIn bn{(const float*)stat, (const bf16_t*)gamma, (const bf16_t*)beta, nullptr, nullptr,
           (const bf16_t*)(res != nullptr ? res : x), (bf16_t*)out, res_c,
           res != nullptr ? 1.f : 0.f};
+  if (xsums != nullptr) {
+    bn.xsums = (const float*)xsums;
+    bn.stat_w = (float*)stat;
+    bn.running = (float*)running;
+    bn.Mf = (float)M;
+    bn.Mm1f = (float)(M - 1 > 1 ? M - 1 : 1);
+    bn.eps = eps;
+    bn.momentum = momentum;
+  }
   // (BNIN 2: shortcut shaped like x or none; 3: option-A -- the block outputs whose block
   //  changed its width, at the two widths a CIFAR ResNet changes to)
 #define X(ci, co, s) \
