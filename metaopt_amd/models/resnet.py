@@ -144,7 +144,10 @@ class PopulationResNet(FlatPopulation):
 
     def _loss(self, x, y, train: bool):
         P, W = self.capacity, self.W
-        h = self._expand(x, torch.bfloat16).view(-1, *x.shape[1:])     # [P*B, H, W, 8]
+        # [P*B, H, W, 8]: the evaluation / CPU path's input (training on the HIP path reads the
+        # shared batch in place, cops.shared_conv_stats)
+        h = self._expand(x, torch.bfloat16).view(-1, *x.shape[1:]) \
+            if not (train and x.device.type == "cuda") else None
         B = x.shape[0]
         # one zero fill per step for every layer's BatchNorm sums (forward and backward)
         arena = (cops.ZeroArena(sum(4 * P * c for _, _, c, _ in self.layout), x.device)
@@ -157,7 +160,13 @@ class PopulationResNet(FlatPopulation):
         pend = None
         if arena is not None:
             W0 = self.W[f"{name}.w"]
-            y0, st0 = cops.conv_stats(h, W0, P, stride, True, arena=arena)
+            # the stem reads the shared minibatch itself, not the P-fold expanded copy
+            shared = cops.shared_conv_stats(x.to(self.device, torch.bfloat16), W0, P, arena) \
+                if stride == 1 else None
+            if shared is None:
+                h = self._expand(x, torch.bfloat16).view(-1, *x.shape[1:])
+                shared = cops.conv_stats(h, W0, P, stride, True, arena=arena)
+            y0, st0 = shared
             pend = cops.PendingBN(y0, st0, W[f"{name}.g"], W[f"{name}.b"],
                                   self.A[f"{name}.running"].view(P, 2, cout), P)
             if st0 is None:

@@ -31,6 +31,7 @@ _lib.register_signatures({
     "mopt_pconv": ([c_int] + [c_void_p] * 4 + [c_int] * 10 + [c_void_p], c_int),
     "mopt_dconv": ([c_int] + [c_void_p] * 4 + [c_int] * 7 + [c_void_p], c_int),
     "mopt_dconv_wgrad_splits": ([c_int] * 6, c_int),
+    "mopt_dconv_shared_x": ([c_int] + [c_void_p] * 4 + [c_int] * 6 + [c_void_p], c_int),
     "mopt_dconv_bnin": ([c_int] + [c_void_p] * 4 + [c_int] * 5 + [c_void_p] * 5 +
                         [c_int64, c_float, c_float, c_void_p], c_int),
     "mopt_dconv_dgrad_bnsums": ([c_void_p] * 4 + [c_int] * 5 + [c_void_p] * 5, c_int),
@@ -592,6 +593,56 @@ def bn_res_conv3x3(pend: PendingBN, w, P, stride, arena, conv_mailbox=None, eps=
                                stride, pend.sums, out_sums, arena, pend.mailbox, pend.res_sub2,
                                conv_mailbox, grad_w, eps, momentum)
     return y, out_sums, h
+
+
+class _SharedInputConv3x3(torch.autograd.Function):
+    """The stem: a stride-1 convolution of the minibatch every trial shares, x [Bn, H, W, Ci]
+    (no P-fold copy), with the output's BatchNorm batch sums; backward: the weight gradient only
+    (the input needs none)."""
+
+    @staticmethod
+    def forward(ctx, x, w, P, sums, grad_out):
+        Bn, H, W, Ci = x.shape
+        Co = w.shape[-1]
+        y = torch.empty(P * Bn, H, W, Co, dtype=x.dtype, device=x.device)
+        _call("mopt_dconv_shared_x", 0, x.data_ptr(), w.data_ptr(), y.data_ptr(), sums.data_ptr(),
+              P, Bn, H, Ci, Co, 1, _s(x))
+        ctx.save_for_backward(x, w)
+        ctx.meta = (P, Bn, H, Ci, Co)
+        ctx.grad_out = grad_out
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        P, Bn, H, Ci, Co = ctx.meta
+        dy = dy.contiguous()
+        lib = _lib.get_lib()
+        nb = lib.mopt_dconv_wgrad_splits(P, Bn, H, Ci, Co, 1)
+        part = torch.empty(max(nb, 1) * P * 9 * Ci * Co, dtype=torch.float32, device=dy.device)
+        dw = ctx.grad_out if ctx.grad_out is not None else torch.empty_like(w)
+        _call("mopt_dconv_shared_x", 2, x.data_ptr(), dy.data_ptr(), dw.data_ptr(),
+              part.data_ptr(), P, Bn, H, Ci, Co, 1, _s(dy))
+        return None, (None if ctx.grad_out is not None else dw), None, None, None
+
+
+# the stem reads the shared minibatch in place (MOPT_SHARED_STEM=0: a P-fold expanded copy)
+_SHARED_STEM = os.environ.get("MOPT_SHARED_STEM", "1") != "0"
+
+
+def shared_conv_stats(x, w, P, arena):
+    """``(conv3x3 of the shared batch x [Bn, H, W, Ci] for every trial, batch sums)`` on the HIP
+    path (``_SharedInputConv3x3``), or None when the shape has no kernel / it is switched off."""
+    Bn, H, W, Ci = x.shape
+    Co = w.shape[-1]
+    if not (_SHARED_STEM and _DIRECT) or H != W or (Ci, Co) not in ((8, 16), (16, 16)) or \
+            tuple(w.shape) != (P, 9 * Ci, Co) or \
+            _lib.get_lib().mopt_dconv_wgrad_splits(P, Bn, H, Ci, Co, 1) <= 0:
+        return None
+    sums = arena.take(P * 2 * Co).view(P, 2, Co)
+    grad_out = w.grad if (w.requires_grad and w.is_leaf and w.grad is not None) else None
+    y = _SharedInputConv3x3.apply(x.contiguous(), w.contiguous(), P, sums, grad_out)
+    return y, sums
 
 
 def conv_stats(x, w, P, stride, train, arena=None, mailbox=None, bn_link=None):

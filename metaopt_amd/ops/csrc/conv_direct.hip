@@ -47,6 +47,7 @@ struct Geom {
   float inv_wi, inv_tri;  // 1 / WI, 1 / TRI: exact quotients of small integers via (t + .5) / d
   int lds_elems;          // bf16 elements of the workgroup's LDS allocation
   int cs_off;             // forward: element offset of the output tile (0: it aliases the halo)
+  int x_shared;           // every trial reads the same input x (the stem over the shared batch)
 };
 
 __device__ __forceinline__ int fdiv(int t, float inv) { return (int)(((float)t + 0.5f) * inv); }
@@ -437,7 +438,7 @@ __global__ __launch_bounds__(256) void dconv_fwd_kernel(const bf16_t* __restrict
   const int64_t wbatch = (int64_t)9 * CI * CO;
   const bf16_t* wp = w + p * wbatch;
   const int64_t x_batch = (int64_t)g.Bn * g.H * g.H * CI;
-  const bf16_t* xp = x + p * x_batch;
+  const bf16_t* xp = x + (g.x_shared ? 0 : p * x_batch);
   auto band_row0 = [&](int t) {
     const int oy = (t % g.tpi) * g.TR;
     return mode == kDgrad2 ? oy / 2 - 1 : oy * S - 1;
@@ -818,7 +819,7 @@ __global__ __launch_bounds__(256) void dconv_wgrad_kernel(const bf16_t* __restri
 
   constexpr int NKS = NPX / 32;
   const int ow = 1 << g.owl, ppi = 1 << g.rpil;
-  const bf16_t* xp = x + p * ((int64_t)g.Bn * g.H * g.H * CI);
+  const bf16_t* xp = x + (g.x_shared ? 0 : p * ((int64_t)g.Bn * g.H * g.H * CI));
   const bf16_t* dyp = dy + p * ((int64_t)g.Bn * g.OH * ow * CO);
   // pipelined staging (see Halo): band t + nb's halo and dy tile are loaded into registers while
   // band t is multiplied (the dy rows past a partial band's end re-read its last row, zeroed at
@@ -981,7 +982,7 @@ size_t halo_bytes(const Geom& g) { return (size_t)g.IMGS * g.TRI * g.WI * pstrid
 template <int CI, int CO, int MODE, int S, int ADD = 0, int BNIN = 0, int BNB = 0>
 int launch_fwd(const void* x, const void* w, void* y, void* sums, int P, int Bn, int H,
                hipStream_t st, const void* addend = nullptr, int addend_c = 0,
-               const BnIn& bn = BnIn{}) {
+               const BnIn& bn = BnIn{}, int x_shared = 0) {
   // (the stride-2 data gradient of a 64-channel dy: 128-pixel bands -- at 256 its 18 weight
   //  fragments and 8 accumulator fragments per wave held one workgroup per CU, 0.7 TB/s)
   constexpr int NPX = (MODE == kDgrad2 && CI >= 32) ? 128 : npx_for(CO);
@@ -1002,6 +1003,7 @@ int launch_fwd(const void* x, const void* w, void* y, void* sums, int P, int Bn,
   if (lds_all > 64 * 1024) return (int)hipErrorNotSupported;
   g.lds_elems = (int)(lds / 2);
   g.cs_off = sep ? (int)(hb / 2) : 0;
+  g.x_shared = x_shared;
   hipLaunchKernelGGL((dconv_fwd_kernel<CI, CO, NPX, MODE, S, ADD, BNIN, BNB>), dim3(P * g.nb),
                      dim3(256), lds_all, st,
                      (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, (float*)sums,
@@ -1011,7 +1013,7 @@ int launch_fwd(const void* x, const void* w, void* y, void* sums, int P, int Bn,
 
 template <int CI, int CO, int S, int BNIN = 0>
 int launch_wgrad(const void* x, const void* dy, void* dw, void* part, int P, int Bn, int H,
-                 hipStream_t st, int* nb_out, const BnIn& bn = BnIn{}) {
+                 hipStream_t st, int* nb_out, const BnIn& bn = BnIn{}, int x_shared = 0) {
   constexpr int NPX = npx_wgrad(CO);
   // persistent workgroups per trial: MOPT_WGRAD_BLOCKS in all, <= 64 MB of f32 partials, >= 4
   // bands each
@@ -1020,6 +1022,7 @@ int launch_wgrad(const void* x, const void* dy, void* dw, void* part, int P, int
   const int by_bytes = (int)(kPartBytes / per > 0 ? kPartBytes / per : 1);
   Geom g{};
   if (!make_geom(g, Bn, H, S, NPX, MOPT_WGRAD_BLOCKS, P, kFwd)) return (int)hipErrorInvalidValue;
+  g.x_shared = x_shared;
   g.nb = min(g.nb, max(1, min(by_bytes, g.tiles / 4)));
   if (nb_out != nullptr) {  // size query
     *nb_out = g.nb;
@@ -1217,6 +1220,24 @@ int mopt_dconv_dgrad_bnres(const void* dy, const void* w, void* dx, const void* 
   X1(16) X1(32) X1(64) X2(32, 16) X2(64, 32)
 #undef X1
 #undef X2
+  return (int)hipErrorNotSupported;
+}
+
+// mopt_dconv kinds 0 (forward, with the output's batch sums) and 2 (weight gradient) of a
+// convolution whose input is the SAME for every trial: x [Bn, H, H, Ci] (the stem over the shared
+// minibatch -- no P-fold copy of the batch, and its reads are L2 hits after the first trials).
+int mopt_dconv_shared_x(int kind, const void* a, const void* b, void* out, void* aux, int P,
+                        int Bn, int H, int Ci, int Co, int stride, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (stride != 1) return (int)hipErrorNotSupported;
+#define X(ci, co) \
+  if (Ci == ci && Co == co) \
+    return kind == 0 ? launch_fwd<ci, co, kFwd, 1>(a, b, out, aux, P, Bn, H, st, nullptr, 0, \
+                                                   BnIn{}, 1) \
+         : kind == 2 ? launch_wgrad<ci, co, 1>(a, b, out, aux, P, Bn, H, st, nullptr, BnIn{}, 1) \
+                     : (int)hipErrorInvalidValue;
+  X(8, 16) X(16, 16)
+#undef X
   return (int)hipErrorNotSupported;
 }
 

@@ -420,3 +420,29 @@ def test_bn_res_conv_fused_matches_materialised(C, Co, H, stride, kind):
             assert u is None
             continue
         _close(u, v, 2e-2)
+
+
+@pytest.mark.parametrize("Ci,Co,H", [(8, 16, 32), (16, 16, 16)])
+def test_shared_input_stem_matches_expanded(Ci, Co, H):
+    """The stem over the shared minibatch (cops.shared_conv_stats: every trial's convolution reads
+    the same x [B, H, W, Ci], no P-fold copy) equals the convolution of the expanded copy: output
+    bit for bit, its batch sums and the weight gradient within rounding."""
+    torch.manual_seed(9)
+    P, B = 3, 4
+    x = torch.randn(B, H, H, Ci, device=DEV).to(torch.bfloat16)
+    w0 = (0.1 * torch.randn(P, 9 * Ci, Co, device=DEV)).to(torch.bfloat16)
+    out = {}
+    for shared in (True, False):
+        w = w0.clone().requires_grad_(True)
+        arena = cops.ZeroArena(8 * P * Co, DEV)
+        if shared:
+            y, st = cops.shared_conv_stats(x, w, P, arena)
+        else:
+            xe = x.unsqueeze(0).expand(P, *x.shape).reshape(P * B, H, H, Ci).contiguous()
+            y, st = cops.conv_stats(xe, w, P, 1, True, arena=arena)
+        wt = torch.linspace(-1, 1, y.numel(), device=DEV).view(y.shape)
+        (y.float() * wt).sum().backward()
+        out[shared] = (y.detach(), st.clone(), w.grad)
+    assert torch.equal(out[True][0], out[False][0])
+    _close(out[True][1], out[False][1], 1e-3)
+    _close(out[True][2], out[False][2], 2e-2)
