@@ -135,8 +135,9 @@ class PopulationLM(FlatPopulation):
         R = tok.numel()
         W = self.W
         x = ops.embedding(tok.reshape(-1), W["embed"], rpt)
-        # every residual add is fused into the pre-norm that follows it (ops.add_rmsnorm)
-        h = ops.rmsnorm(x, W["l0.attn_norm"], rpt, c.norm_eps)
+        # every residual add is fused into the pre-norm that follows it (ops.add_rmsnorm); the
+        # embedding's two gradients (residual stream, first norm) meet in that norm's backward
+        x, h = ops.rmsnorm_pass(x, W["l0.attn_norm"], rpt, c.norm_eps)
         for l in range(c.n_layers):
             # interleaved-pair RoPE applied by the QKV GEMM's epilogue and, backward, by the
             # attention kernels' gradient outputs (ops.qkv_rope_attention)

@@ -248,11 +248,19 @@ class _AddRMSNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, delta, w, rows_per_trial, eps):
         R, d = x.shape
-        xs = torch.empty_like(x)
         y = torch.empty_like(x)
         rstd = torch.empty(R, dtype=torch.float32, device=x.device)
-        _call("mopt_add_rmsnorm_fwd", _p(x), _p(delta), _p(xs), _p(w), _p(y), _p(rstd), R, d,
-              rows_per_trial, eps, _stream(x))
+        if delta is None:              # rmsnorm_pass: x itself is the sum
+            xs = x
+            _call("mopt_rmsnorm_fwd", _p(x), _p(w), _p(y), _p(rstd), R, d, rows_per_trial, eps,
+                  _stream(x))
+        else:
+            xs = torch.empty_like(x)
+            _call("mopt_add_rmsnorm_fwd", _p(x), _p(delta), _p(xs), _p(w), _p(y), _p(rstd), R, d,
+                  rows_per_trial, eps, _stream(x))
+        ctx.has_delta = delta is not None
+        # an unused sum (the last norm's) reaches the backward as None, not a zero-filled [R, d]
+        ctx.set_materialize_grads(False)
         ctx.save_for_backward(xs, w, rstd)
         ctx.rpt = rows_per_trial
         ctx.gw = _grad_view(w)
@@ -263,24 +271,26 @@ class _AddRMSNorm(torch.autograd.Function):
         xs, w, rstd = ctx.saved_tensors
         R, d = xs.shape
         if dy is None:
+            dd = dxs if ctx.has_delta else None
             if ctx.gw is not None:
                 ctx.gw.zero_()
-                return dxs, dxs, None, None, None
-            return dxs, dxs, torch.zeros_like(w), None, None
+                return dxs, dd, None, None, None
+            return dxs, dd, torch.zeros_like(w), None, None
         dy = dy.contiguous()
         dres = dxs.contiguous() if dxs is not None else None
         dx = torch.empty_like(xs)
+        dd = dx if ctx.has_delta else None
         if ctx.gw is not None and _NORM_DXDW:
             _norm_bwd_dw(xs, w, dy, dres, rstd, dx, ctx.gw, ctx.rpt)
-            return dx, dx, None, None, None
+            return dx, dd, None, None, None
         dw32 = None if ctx.gw is not None else \
             torch.zeros(w.shape, dtype=torch.float32, device=xs.device)
         _call("mopt_rmsnorm_bwd_res", _p(xs), _p(w), _p(dy),
               _p(dres) if dres is not None else None, _p(rstd), _p(dx),
               _p(dw32) if dw32 is not None else None, R, d, ctx.rpt, _stream(xs))
         if ctx.gw is not None:
-            return dx, dx, _norm_dw(xs, dy, rstd, ctx.gw, ctx.rpt), None, None
-        return dx, dx, dw32.to(w.dtype), None, None
+            return dx, dd, _norm_dw(xs, dy, rstd, ctx.gw, ctx.rpt), None, None
+        return dx, dd, dw32.to(w.dtype), None, None
 
 
 def add_rmsnorm(x, delta, w, rows_per_trial, eps=1e-5):
@@ -290,6 +300,15 @@ def add_rmsnorm(x, delta, w, rows_per_trial, eps=1e-5):
                                  rows_per_trial, eps)
     xs = x + delta
     return xs, rmsnorm_ref(xs, w, rows_per_trial, eps)
+
+
+def rmsnorm_pass(x, w, rows_per_trial, eps=1e-5):
+    """``(x, rmsnorm(x))``: the norm's input passed through, so a gradient that reaches ``x``
+    through its other uses joins the norm's backward pass (the ``dres`` addend of
+    :class:`_AddRMSNorm`) instead of an autograd accumulation kernel."""
+    if _hip(x, "rmsnorm"):
+        return _AddRMSNorm.apply(x.contiguous(), None, w.contiguous(), rows_per_trial, eps)
+    return x, rmsnorm_ref(x, w, rows_per_trial, eps)
 
 
 class _RopeSplit(torch.autograd.Function):

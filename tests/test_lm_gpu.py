@@ -77,6 +77,28 @@ def test_add_rmsnorm_fwd_bwd(use_xs):
     _close(w.grad, wr.grad, 2e-2)
 
 
+@pytest.mark.parametrize("use_xs", [True, False])
+def test_rmsnorm_pass_joins_input_gradient(use_xs):
+    """(x, rmsnorm(x)) with x also used downstream: the downstream gradient is added inside the
+    norm's backward (dres) -- x.grad equals the fp32 sum of both paths."""
+    torch.manual_seed(6)
+    P, rpt, d = 2, 128, 768
+    x = torch.randn(P * rpt, d, device=DEV).to(torch.bfloat16).requires_grad_(True)
+    w = (1 + 0.1 * torch.randn(P, d, device=DEV)).to(torch.bfloat16).requires_grad_(True)
+    dy = torch.randn(P * rpt, d, device=DEV).to(torch.bfloat16)
+    dxs = torch.randn(P * rpt, d, device=DEV).to(torch.bfloat16)
+    xo, y = ops.rmsnorm_pass(x, w, rpt)
+    torch.autograd.backward([y, xo * 1] if use_xs else [y], [dy, dxs] if use_xs else [dy])
+    xr, wr = (t.detach().float().requires_grad_(True) for t in (x, w))
+    yr = ops.rmsnorm_ref(xr, wr, rpt)
+    torch.autograd.backward([yr, xr * 1] if use_xs else [yr],
+                            [dy.float(), dxs.float()] if use_xs else [dy.float()])
+    assert torch.equal(xo, x)
+    _close(y, yr, 1e-2)
+    _close(x.grad, xr.grad, 2e-2)
+    _close(w.grad, wr.grad, 2e-2)
+
+
 @pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("P,rpt,d", [(3, 1000, 768), (2, 48, 200)])
 def test_rmsnorm_weight_grad_into_flat_view(fused, P, rpt, d):
