@@ -193,9 +193,13 @@ class PopulationResNet(FlatPopulation):
                 r = self._shortcut(h, c2, s1)
                 t = self._conv_bn(n1, h, s1, train, arena=arena)
                 h = self._conv_bn(n2, t, 1, train, res=r, arena=arena)
+        labels = self._expand(y, torch.long).reshape(-1)
+        if pend is not None and cops.bn_head_ok(pend, W["fc.w"], W["fc.b"], labels):
+            # the last block's output is formed inside the head, never written
+            return cops.bn_resnet_head(pend, W["fc.w"], W["fc.b"], labels, NCLS, arena,
+                                       scale=1.0 / B)
         if pend is not None:          # the last block's output feeds the head
             h = pend.materialize(arena)
-        labels = self._expand(y, torch.long).reshape(-1)
         if x.device.type == "cuda":
             # pool + linear + cross-entropy (+ its backward) in one HIP kernel; the classifier's
             # dW / db land in the flat gradient buffer (direct gradients), mean-loss scaled

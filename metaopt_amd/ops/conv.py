@@ -38,6 +38,7 @@ _lib.register_signatures({
     "mopt_dconv_dgrad_bnres": ([c_void_p] * 5 + [c_int] * 7 + [c_void_p] * 4, c_int),
     "mopt_dconv_bnres_fwd": ([c_void_p] * 6 + [c_int] + [c_void_p] * 3 + [c_int] * 6 +
                              [c_void_p, c_void_p, c_int64, c_float, c_float, c_void_p], c_int),
+    "mopt_resnet_head_bn": ([c_void_p] * 8 + [c_int] * 5 + [c_float] + [c_void_p] * 8, c_int),
     "mopt_resnet_head": ([c_void_p] * 4 + [c_int] * 5 + [c_float, c_int] + [c_void_p] * 7,
                          c_int),
     "mopt_resnet_head_part_floats": ([c_int] * 3, c_int),
@@ -771,6 +772,96 @@ class _Head(torch.autograd.Function):
     def backward(ctx, dloss, dcorrect):
         (dh,) = ctx.saved_tensors
         return dh, None, None, None, None, None, None, None, None
+
+
+# the last block's BatchNorm 2 + shortcut + ReLU formed inside the classifier head
+# (MOPT_BN_HEAD=0: the apply pass materialises the block output first)
+_BN_HEAD = os.environ.get("MOPT_BN_HEAD", "1") != "0"
+
+
+def bn_head_ok(pend: "PendingBN", fcw, fcb, labels) -> bool:
+    """Whether ``bn_resnet_head`` has a kernel for this pending block output."""
+    if not (_BN_HEAD and pend is not None and pend.sums is not None and pend.res is not None) \
+            or pend.res_sub2 or pend.x.device.type != "cuda":
+        return False
+    x, P = pend.x, pend.P
+    N, H, W, C = x.shape
+    if tuple(pend.res.shape) != tuple(x.shape) or N % P or (N // P) % 16 or C % 8 or C > 64 or \
+            16 % (C // 8) or tuple(fcw.shape) != (P, C, 16) or tuple(fcb.shape) != (P, 16) or \
+            labels.dtype != torch.int64 or labels.numel() != N:
+        return False
+    nph = 16 // (C // 8)
+    return (H * W) % (4 * nph) == 0 and (H * W) // (4 * nph) <= 8
+
+
+class _BNHead(torch.autograd.Function):
+    """The classifier head over relu(BN(x) + shortcut) of the last block, formed while pooling
+    (csrc/resnet_head.hip ``head_kernel<true>``): the block output is never written.  The head
+    writes dz -- the gradient behind the ReLU, which is also the block's shortcut gradient (to
+    the mailbox) -- and the BatchNorm's reductions; backward is the BatchNorm's apply pass."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, res, running, fcw, fcb, labels, P, ncls, scale, gw, gb,
+                sums, arena, bn_mailbox, eps, momentum):
+        N, H, W, C = x.shape
+        B, HW, M = N // P, H * W, x.numel() // (P * C)
+        dev = x.device
+        stat = torch.empty(P, 2, C, dtype=torch.float32, device=dev)
+        _call("mopt_bn_fwd", x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), 0, 0,
+              stat.data_ptr(), running.data_ptr(), sums.data_ptr(), P, M, C, eps, momentum,
+              1, 1, 1, 0, 0, _s(x))
+        loss = torch.empty(P, dtype=torch.float32, device=dev)
+        correct = torch.empty(P, dtype=torch.float32, device=dev)
+        part = torch.empty(_lib.get_lib().mopt_resnet_head_part_floats(P, B, C),
+                           dtype=torch.float32, device=dev)
+        dz = torch.empty_like(x)
+        bwd_sums = arena.take(P * 2 * C).view(P, 2, C)
+        _call("mopt_resnet_head_bn", x.data_ptr(), res.data_ptr(), stat.data_ptr(),
+              gamma.data_ptr(), beta.data_ptr(), fcw.data_ptr(), fcb.data_ptr(),
+              labels.data_ptr(), P, B, HW, C, ncls, float(scale), part.data_ptr(), dz.data_ptr(),
+              gw.data_ptr(), gb.data_ptr(), loss.data_ptr(), correct.data_ptr(),
+              bwd_sums.data_ptr(), _s(x))
+        ctx.save_for_backward(x, dz, stat, gamma, beta)
+        ctx.bwd_sums, ctx.P, ctx.bn_mailbox = bwd_sums, P, bn_mailbox
+        ctx.grads = tuple(t.grad if (t.requires_grad and t.is_leaf and t.grad is not None) else None
+                          for t in (gamma, beta))
+        ctx.mark_non_differentiable(correct)
+        ctx.set_materialize_grads(False)
+        return loss, correct
+
+    @staticmethod
+    def backward(ctx, dloss, dcorrect):
+        x, dz, stat, gamma, beta = ctx.saved_tensors
+        P = ctx.P
+        C = x.shape[-1]
+        M = x.numel() // (P * C)
+        dx = torch.empty_like(x)
+        gg, gb = ctx.grads
+        direct = gg is not None and gb is not None and gg.is_contiguous() and gb.is_contiguous()
+        _call("mopt_bn_bwd", x.data_ptr(), 0, dz.data_ptr(), stat.data_ptr(), gamma.data_ptr(),
+              beta.data_ptr(), dx.data_ptr(), 0, ctx.bwd_sums.data_ptr(),
+              gg.data_ptr() if direct else 0, gb.data_ptr() if direct else 0, P, M, C, 0, 2,
+              _s(x))
+        if ctx.bn_mailbox is not None:
+            ctx.bn_mailbox["dres"] = dz
+            ctx.bn_mailbox["sub2"] = False
+        dgamma = dbeta = None
+        if not direct:
+            dgamma = ctx.bwd_sums[:, 1].to(gamma.dtype)
+            dbeta = ctx.bwd_sums[:, 0].to(gamma.dtype)
+        return (dx, dgamma, dbeta) + (None,) * 15
+
+
+def bn_resnet_head(pend: "PendingBN", fcw, fcb, labels, ncls, arena, scale=1.0, eps=1e-5,
+                   momentum=0.1):
+    """Training ``resnet_head(pend.materialize(arena), ...)`` with the pending block output
+    formed inside the head (``_BNHead``); check ``bn_head_ok`` first."""
+    if fcw.grad is None or fcb.grad is None:
+        raise ValueError("bn_resnet_head writes into fcw.grad / fcb.grad")
+    return _BNHead.apply(pend.x.contiguous(), pend.gamma.contiguous(), pend.beta.contiguous(),
+                         pend.res.detach().contiguous(), pend.running, fcw, fcb,
+                         labels.contiguous(), pend.P, ncls, scale, fcw.grad, fcb.grad, pend.sums,
+                         arena, pend.mailbox, eps, momentum)
 
 
 def resnet_head(h, fcw, fcb, labels, P, ncls, train, scale=1.0):

@@ -49,14 +49,33 @@ __device__ __forceinline__ float sum16(float v) {
 // partial record per (trial, image block): dW [C][NP], db [NP], loss, correct
 __host__ __device__ constexpr int rec_floats(int C) { return C * NP + NP + 2; }
 
+// BN: x is the last block's pre-BatchNorm conv output and the features are formed on the fly,
+// h = relu(BN(x) + res) rounded to bf16 exactly as bn_apply_kernel / the conv staging round it;
+// the backward writes dz = dh relu'(h) (the BatchNorm's input gradient before its apply pass and
+// the block's shortcut gradient) and adds the BatchNorm's reductions (sum dz, sum dz xhat) into
+// bsums [P][2][C] -- the block output is never written.  dz is constant over an image's pixels
+// up to the mask, so those sums are g * count and g * rstd * sum(x - mean) over the pixels the
+// mask keeps, gathered while pooling (the mask bits wait in LDS for the dz stores).
+struct HeadBN {
+  const bf16_t* res;
+  const float* stat;     // [P][2][C] mean, rstd
+  const bf16_t* gamma;
+  const bf16_t* beta;
+  float* bsums;          // [P][2][C], accumulated
+};
+
+template <bool BN>
 __global__ __launch_bounds__(256) void head_kernel(const bf16_t* __restrict__ x,
                                                    const bf16_t* __restrict__ W,
                                                    const bf16_t* __restrict__ bias,
                                                    const int64_t* __restrict__ labels, int B,
                                                    int HW, int C, int ncls, float scale,
                                                    int train, float* __restrict__ part,
-                                                   bf16_t* __restrict__ dx) {
+                                                   bf16_t* __restrict__ dx, HeadBN bn) {
   __shared__ float Ws[CMAX][NP + 1];
+  // BN: one mask word per 4 pixels of a thread (host: HW / nph <= 32, HW % (4 nph) == 0)
+  __shared__ uint32_t mbits[BN ? 8 * 256 : 1];
+  __shared__ float bred[BN ? 2 : 1][CMAX];
   __shared__ float bs[NP];
   __shared__ float feat[IMG][CMAX + 1];
   __shared__ float dl[IMG][NP + 1];
@@ -76,7 +95,52 @@ __global__ __launch_bounds__(256) void head_kernel(const bf16_t* __restrict__ x,
   const int64_t row = (int64_t)p * B + (int64_t)blk * IMG + i;
   const bf16_t* xi = x + row * HW * C;
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (ph < nph) {
+  float cnt[8], sxm[8];   // BN: pixels the mask keeps, sum of (x - mean) over them
+  if constexpr (BN) {
+    float sc[8], sh[8], mu[8];
+    {
+      float gm[8], bt[8];
+      unpack8h(*(const uint4*)(bn.gamma + (int64_t)p * C + 8 * ch), gm);
+      unpack8h(*(const uint4*)(bn.beta + (int64_t)p * C + 8 * ch), bt);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        mu[e] = bn.stat[(2 * p) * C + 8 * ch + e];
+        sc[e] = gm[e] * bn.stat[(2 * p + 1) * C + 8 * ch + e];
+        sh[e] = bt[e] - mu[e] * sc[e];
+        cnt[e] = 0.f;
+        sxm[e] = 0.f;
+      }
+    }
+    for (int e = tid; e < 2 * CMAX; e += 256) bred[e / CMAX][e % CMAX] = 0.f;
+    const bf16_t* ri = bn.res + row * HW * C;
+    int j = 0;
+    for (int px = ph; px < HW; px += 4 * nph, ++j) {
+      uint4 u[4], r[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        u[k] = *(const uint4*)(xi + (int64_t)(px + k * nph) * C + 8 * ch);
+        r[k] = *(const uint4*)(ri + (int64_t)(px + k * nph) * C + 8 * ch);
+      }
+      uint32_t mw = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float f[8], rv[8];
+        unpack8h(u[k], f);
+        unpack8h(r[k], rv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float hb = bf2f(f2bf(fmaxf(fmaf(f[e], sc[e], sh[e]) + rv[e], 0.f)));
+          acc[e] += hb;
+          if (hb > 0.f) {
+            mw |= 1u << (8 * k + e);
+            cnt[e] += 1.f;
+            sxm[e] += f[e] - mu[e];
+          }
+        }
+      }
+      mbits[j * 256 + tid] = mw;
+    }
+  } else if (ph < nph) {
     int px = ph;
     for (; px + 3 * nph < HW; px += 4 * nph) {        // four 16-byte loads in flight
       uint4 u[4];
@@ -181,7 +245,39 @@ __global__ __launch_bounds__(256) void head_kernel(const bf16_t* __restrict__ x,
     const uint4 v = make_uint4(pack2bf(g[0], g[1]), pack2bf(g[2], g[3]), pack2bf(g[4], g[5]),
                                pack2bf(g[6], g[7]));
     bf16_t* di = dx + row * HW * C + 8 * ch;
-    for (int px = ph; px < HW; px += nph) *(uint4*)(di + (int64_t)px * C) = v;
+    if constexpr (BN) {
+      // dz = the stored (bf16) gradient where the mask keeps the pixel; the BatchNorm sums
+      float gb[8];
+      unpack8h(v, gb);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        atomicAdd(&bred[0][8 * ch + e], gb[e] * cnt[e]);
+        atomicAdd(&bred[1][8 * ch + e],
+                  gb[e] * bn.stat[(2 * p + 1) * C + 8 * ch + e] * sxm[e]);
+      }
+      const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+      int j = 0;
+      for (int px = ph; px < HW; px += 4 * nph, ++j) {
+        const uint32_t mw = mbits[j * 256 + tid];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t m = mw >> (8 * k);
+          uint32_t o[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            o[q] = (vw[q] & ((m >> (2 * q)) & 1u ? 0xFFFFu : 0u)) |
+                   (vw[q] & ((m >> (2 * q + 1)) & 1u ? 0xFFFF0000u : 0u));
+          *(uint4*)(di + (int64_t)(px + k * nph) * C) = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+      }
+    } else {
+      for (int px = ph; px < HW; px += nph) *(uint4*)(di + (int64_t)px * C) = v;
+    }
+  }
+  if constexpr (BN) {
+    __syncthreads();
+    for (int e = tid; e < 2 * C; e += 256)
+      atomicAdd(bn.bsums + (int64_t)p * 2 * C + e, bred[e / C][e % C]);
   }
 }
 
@@ -221,11 +317,36 @@ int mopt_resnet_head(const void* x, const void* W, const void* b, const void* la
       HW < 1 || (train && (dx == nullptr || dW == nullptr || db == nullptr)))
     return (int)hipErrorInvalidValue;
   const hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(head_kernel, dim3(B / IMG, P), dim3(256), 0, st, (const bf16_t*)x,
+  hipLaunchKernelGGL(head_kernel<false>, dim3(B / IMG, P), dim3(256), 0, st, (const bf16_t*)x,
                      (const bf16_t*)W, (const bf16_t*)b, (const int64_t*)labels, B, HW, C, ncls,
-                     scale, train, (float*)part, (bf16_t*)dx);
+                     scale, train, (float*)part, (bf16_t*)dx, HeadBN{});
   hipLaunchKernelGGL(head_reduce_kernel, dim3(P), dim3(256), 0, st, (const float*)part, B / IMG,
                      C, train, (bf16_t*)dW, (bf16_t*)db, (float*)loss, (float*)correct);
+  return (int)hipGetLastError();
+}
+
+// Training head over the last block's output relu(BN(x) + res) formed on the fly (x, res
+// [P*B][HW][C] bf16; stat [P][2][C] mean / rstd; gamma / beta bf16 [P][C]): dz (the BatchNorm's
+// masked input gradient, [P*B][HW][C] bf16) instead of dh, and (sum dz, sum dz xhat) added into
+// bsums [P][2][C] (zeroed by the caller).  hipErrorNotSupported (801) for shapes it does not take.
+int mopt_resnet_head_bn(const void* x, const void* res, const void* stat, const void* gamma,
+                        const void* beta, const void* W, const void* b, const void* labels, int P,
+                        int B, int HW, int C, int ncls, float scale, void* part, void* dz,
+                        void* dW, void* db, void* loss, void* correct, void* bsums,
+                        void* stream) {
+  if (P <= 0 || B <= 0 || B % IMG || C % 8 || C < 8 || C > CMAX || ncls < 1 || ncls > NP ||
+      HW < 1 || !x || !res || !stat || !gamma || !beta || !dz || !dW || !db || !bsums)
+    return (int)hipErrorInvalidValue;
+  const int cc = C / 8, nph = 16 / cc;
+  if (16 % cc || HW % (4 * nph) || HW / (4 * nph) > 8) return (int)hipErrorNotSupported;
+  const hipStream_t st = (hipStream_t)stream;
+  const HeadBN bn{(const bf16_t*)res, (const float*)stat, (const bf16_t*)gamma,
+                  (const bf16_t*)beta, (float*)bsums};
+  hipLaunchKernelGGL(head_kernel<true>, dim3(B / IMG, P), dim3(256), 0, st, (const bf16_t*)x,
+                     (const bf16_t*)W, (const bf16_t*)b, (const int64_t*)labels, B, HW, C, ncls,
+                     scale, 1, (float*)part, (bf16_t*)dz, bn);
+  hipLaunchKernelGGL(head_reduce_kernel, dim3(P), dim3(256), 0, st, (const float*)part, B / IMG,
+                     C, 1, (bf16_t*)dW, (bf16_t*)db, (float*)loss, (float*)correct);
   return (int)hipGetLastError();
 }
 

@@ -422,6 +422,49 @@ def test_bn_res_conv_fused_matches_materialised(C, Co, H, stride, kind):
         _close(u, v, 2e-2)
 
 
+@pytest.mark.parametrize("C", [64, 16])
+def test_bn_head_fused_matches_materialised(C):
+    """bn_resnet_head (the last block's relu(BN(x) + shortcut) formed while the classifier head
+    pools it; the head writes the masked gradient dz and the BatchNorm's reductions) equals the
+    apply pass followed by the head: losses, #correct and the classifier gradients bit for bit
+    (the same bf16 block output), the running statistics, the shortcut gradient (dz) bit for bit,
+    and the gradients of x, gamma, beta within rounding."""
+    torch.manual_seed(8)
+    P, B, H, ncls = 2, 32, 8, 10
+    x0 = (0.3 + torch.randn(P * B, H, H, C, device=DEV)).to(torch.bfloat16)
+    r0 = torch.randn(P * B, H, H, C, device=DEV).to(torch.bfloat16)
+    g0 = (1 + 0.1 * torch.randn(P, C, device=DEV)).to(torch.bfloat16)
+    b0 = (0.1 * torch.randn(P, C, device=DEV)).to(torch.bfloat16)
+    fw0 = (0.3 * torch.randn(P, C, 16, device=DEV)).to(torch.bfloat16)
+    fb0 = (0.1 * torch.randn(P, 16, device=DEV)).to(torch.bfloat16)
+    labels = torch.randint(0, ncls, (P * B,), device=DEV)
+    xf = x0.float().view(P, -1, C)
+    sums = torch.stack([xf.sum(1), (xf * xf).sum(1)], 1).contiguous()
+    out = {}
+    for fused in (True, False):
+        x, g, b = (t.clone().requires_grad_(True) for t in (x0, g0, b0))
+        fw, fb = (t.clone().requires_grad_(True) for t in (fw0, fb0))
+        fw.grad, fb.grad = torch.zeros_like(fw), torch.zeros_like(fb)
+        run = torch.stack([torch.zeros(P, C), torch.ones(P, C)], 1).to(DEV).contiguous()
+        arena = cops.ZeroArena(16 * P * C, DEV)
+        box = {}
+        pend = cops.PendingBN(x, sums.clone(), g, b, run, P, res=r0, mailbox=box)
+        if fused:
+            assert cops.bn_head_ok(pend, fw, fb, labels)
+            loss, correct = cops.bn_resnet_head(pend, fw, fb, labels, ncls, arena, scale=1 / B)
+        else:
+            h = pend.materialize(arena)
+            loss, correct = cops.resnet_head(h, fw, fb, labels, P, ncls, True, scale=1 / B)
+        loss.sum().backward()
+        out[fused] = (loss.detach(), correct, fw.grad, fb.grad, box.get("dres"), run, x.grad,
+                      g.grad, b.grad)
+    a, r = out[True], out[False]
+    for u, v in zip(a[:5], r[:5]):
+        assert torch.equal(u, v)
+    for u, v in zip(a[5:], r[5:]):
+        _close(u, v, 2e-2)
+
+
 @pytest.mark.parametrize("Ci,Co,H", [(8, 16, 32), (16, 16, 16)])
 def test_shared_input_stem_matches_expanded(Ci, Co, H):
     """The stem over the shared minibatch (cops.shared_conv_stats: every trial's convolution reads
