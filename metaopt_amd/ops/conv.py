@@ -38,7 +38,8 @@ _lib.register_signatures({
     "mopt_dconv_dgrad_bnres": ([c_void_p] * 5 + [c_int] * 7 + [c_void_p] * 4, c_int),
     "mopt_dconv_bnres_fwd": ([c_void_p] * 6 + [c_int] + [c_void_p] * 3 + [c_int] * 6 +
                              [c_void_p, c_void_p, c_int64, c_float, c_float, c_void_p], c_int),
-    "mopt_resnet_head_bn": ([c_void_p] * 8 + [c_int] * 5 + [c_float] + [c_void_p] * 8, c_int),
+    "mopt_resnet_head_bn": ([c_void_p] * 8 + [c_int] * 5 + [c_float] + [c_void_p] * 9 +
+                            [c_int64, c_float, c_float, c_void_p], c_int),
     "mopt_resnet_head": ([c_void_p] * 4 + [c_int] * 5 + [c_float, c_int] + [c_void_p] * 7,
                          c_int),
     "mopt_resnet_head_part_floats": ([c_int] * 3, c_int),
@@ -807,9 +808,11 @@ class _BNHead(torch.autograd.Function):
         B, HW, M = N // P, H * W, x.numel() // (P * C)
         dev = x.device
         stat = torch.empty(P, 2, C, dtype=torch.float32, device=dev)
-        _call("mopt_bn_fwd", x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), 0, 0,
-              stat.data_ptr(), running.data_ptr(), sums.data_ptr(), P, M, C, eps, momentum,
-              1, 1, 1, 0, 0, _s(x))
+        fin = _BN_FIN_IN_CONV        # mean / rstd and the running update inside the head
+        if not fin:
+            _call("mopt_bn_fwd", x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), 0, 0,
+                  stat.data_ptr(), running.data_ptr(), sums.data_ptr(), P, M, C, eps, momentum,
+                  1, 1, 1, 0, 0, _s(x))
         loss = torch.empty(P, dtype=torch.float32, device=dev)
         correct = torch.empty(P, dtype=torch.float32, device=dev)
         part = torch.empty(_lib.get_lib().mopt_resnet_head_part_floats(P, B, C),
@@ -820,7 +823,8 @@ class _BNHead(torch.autograd.Function):
               gamma.data_ptr(), beta.data_ptr(), fcw.data_ptr(), fcb.data_ptr(),
               labels.data_ptr(), P, B, HW, C, ncls, float(scale), part.data_ptr(), dz.data_ptr(),
               gw.data_ptr(), gb.data_ptr(), loss.data_ptr(), correct.data_ptr(),
-              bwd_sums.data_ptr(), _s(x))
+              bwd_sums.data_ptr(), sums.data_ptr() if fin else 0,
+              running.data_ptr() if fin else 0, M, eps, momentum, _s(x))
         ctx.save_for_backward(x, dz, stat, gamma, beta)
         ctx.bwd_sums, ctx.P, ctx.bn_mailbox = bwd_sums, P, bn_mailbox
         ctx.grads = tuple(t.grad if (t.requires_grad and t.is_leaf and t.grad is not None) else None

@@ -58,11 +58,23 @@ __host__ __device__ constexpr int rec_floats(int C) { return C * NP + NP + 2; }
 // mask keeps, gathered while pooling (the mask bits wait in LDS for the dz stores).
 struct HeadBN {
   const bf16_t* res;
-  const float* stat;     // [P][2][C] mean, rstd
+  float* stat;           // [P][2][C] mean, rstd (written here when xsums is given)
   const bf16_t* gamma;
   const bf16_t* beta;
   float* bsums;          // [P][2][C], accumulated
+  // finalize in the head (bn_finalize_kernel's arithmetic): the forward batch sums of x, the
+  // running statistics the trial's first workgroup updates; xsums == nullptr: stat is given
+  const float* xsums;
+  float* running;
+  float Mf, Mm1f, eps, momentum;
 };
+
+// pixels per iteration of a thread's BatchNorm pooling loop (loads in flight: 2 x HEAD_PX)
+#ifndef MOPT_HEAD_PX
+#define MOPT_HEAD_PX 8
+#endif
+constexpr int HEAD_PX = MOPT_HEAD_PX;
+static_assert(HEAD_PX == 4 || HEAD_PX == 8, "mask words hold 4 pixels");
 
 template <bool BN>
 __global__ __launch_bounds__(256) void head_kernel(const bf16_t* __restrict__ x,
@@ -73,7 +85,7 @@ __global__ __launch_bounds__(256) void head_kernel(const bf16_t* __restrict__ x,
                                                    int train, float* __restrict__ part,
                                                    bf16_t* __restrict__ dx, HeadBN bn) {
   __shared__ float Ws[CMAX][NP + 1];
-  // BN: one mask word per 4 pixels of a thread (host: HW / nph <= 32, HW % (4 nph) == 0)
+  // BN: one mask word per 4 pixels of a thread (host: HW / nph <= 32, HW % (HEAD_PX nph) == 0)
   __shared__ uint32_t mbits[BN ? 8 * 256 : 1];
   __shared__ float bred[BN ? 2 : 1][CMAX];
   __shared__ float bs[NP];
@@ -95,17 +107,33 @@ __global__ __launch_bounds__(256) void head_kernel(const bf16_t* __restrict__ x,
   const int64_t row = (int64_t)p * B + (int64_t)blk * IMG + i;
   const bf16_t* xi = x + row * HW * C;
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  float cnt[8], sxm[8];   // BN: pixels the mask keeps, sum of (x - mean) over them
+  float cnt[8], sxm[8], rs[8];   // BN: pixels the mask keeps, sum of (x - mean) over them, rstd
   if constexpr (BN) {
     float sc[8], sh[8], mu[8];
     {
       float gm[8], bt[8];
       unpack8h(*(const uint4*)(bn.gamma + (int64_t)p * C + 8 * ch), gm);
       unpack8h(*(const uint4*)(bn.beta + (int64_t)p * C + 8 * ch), bt);
+      const bool fin_w = bn.xsums != nullptr && blk == 0 && i == 0 && ph == 0;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        mu[e] = bn.stat[(2 * p) * C + 8 * ch + e];
-        sc[e] = gm[e] * bn.stat[(2 * p + 1) * C + 8 * ch + e];
+        const int c = 8 * ch + e;
+        if (bn.xsums != nullptr) {
+          mu[e] = bn.xsums[(2 * p) * C + c] / bn.Mf;
+          const float var = fmaxf(bn.xsums[(2 * p + 1) * C + c] / bn.Mf - mu[e] * mu[e], 0.f);
+          rs[e] = rsqrtf(var + bn.eps);
+          if (fin_w) {
+            float* rm = bn.running + (int64_t)p * 2 * C;
+            rm[c] = (1.f - bn.momentum) * rm[c] + bn.momentum * mu[e];
+            rm[C + c] = (1.f - bn.momentum) * rm[C + c] + bn.momentum * var * bn.Mf / bn.Mm1f;
+            bn.stat[(2 * p) * C + c] = mu[e];
+            bn.stat[(2 * p + 1) * C + c] = rs[e];
+          }
+        } else {
+          mu[e] = bn.stat[(2 * p) * C + c];
+          rs[e] = bn.stat[(2 * p + 1) * C + c];
+        }
+        sc[e] = gm[e] * rs[e];
         sh[e] = bt[e] - mu[e] * sc[e];
         cnt[e] = 0.f;
         sxm[e] = 0.f;
@@ -114,31 +142,34 @@ __global__ __launch_bounds__(256) void head_kernel(const bf16_t* __restrict__ x,
     for (int e = tid; e < 2 * CMAX; e += 256) bred[e / CMAX][e % CMAX] = 0.f;
     const bf16_t* ri = bn.res + row * HW * C;
     int j = 0;
-    for (int px = ph; px < HW; px += 4 * nph, ++j) {
-      uint4 u[4], r[4];
+    for (int px = ph; px < HW; px += HEAD_PX * nph) {
+      uint4 u[HEAD_PX], r[HEAD_PX];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < HEAD_PX; ++k) {
         u[k] = *(const uint4*)(xi + (int64_t)(px + k * nph) * C + 8 * ch);
         r[k] = *(const uint4*)(ri + (int64_t)(px + k * nph) * C + 8 * ch);
       }
-      uint32_t mw = 0;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        float f[8], rv[8];
-        unpack8h(u[k], f);
-        unpack8h(r[k], rv);
+      for (int w = 0; w < HEAD_PX / 4; ++w, ++j) {
+        uint32_t mw = 0;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float hb = bf2f(f2bf(fmaxf(fmaf(f[e], sc[e], sh[e]) + rv[e], 0.f)));
-          acc[e] += hb;
-          if (hb > 0.f) {
-            mw |= 1u << (8 * k + e);
-            cnt[e] += 1.f;
-            sxm[e] += f[e] - mu[e];
+        for (int k = 0; k < 4; ++k) {
+          float f[8], rv[8];
+          unpack8h(u[4 * w + k], f);
+          unpack8h(r[4 * w + k], rv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float hb = bf2f(f2bf(fmaxf(fmaf(f[e], sc[e], sh[e]) + rv[e], 0.f)));
+            acc[e] += hb;
+            if (hb > 0.f) {
+              mw |= 1u << (8 * k + e);
+              cnt[e] += 1.f;
+              sxm[e] += f[e] - mu[e];
+            }
           }
         }
+        mbits[j * 256 + tid] = mw;
       }
-      mbits[j * 256 + tid] = mw;
     }
   } else if (ph < nph) {
     int px = ph;
@@ -252,8 +283,7 @@ __global__ __launch_bounds__(256) void head_kernel(const bf16_t* __restrict__ x,
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         atomicAdd(&bred[0][8 * ch + e], gb[e] * cnt[e]);
-        atomicAdd(&bred[1][8 * ch + e],
-                  gb[e] * bn.stat[(2 * p + 1) * C + 8 * ch + e] * sxm[e]);
+        atomicAdd(&bred[1][8 * ch + e], gb[e] * rs[e] * sxm[e]);
       }
       const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
       int j = 0;
@@ -329,19 +359,22 @@ int mopt_resnet_head(const void* x, const void* W, const void* b, const void* la
 // [P*B][HW][C] bf16; stat [P][2][C] mean / rstd; gamma / beta bf16 [P][C]): dz (the BatchNorm's
 // masked input gradient, [P*B][HW][C] bf16) instead of dh, and (sum dz, sum dz xhat) added into
 // bsums [P][2][C] (zeroed by the caller).  hipErrorNotSupported (801) for shapes it does not take.
-int mopt_resnet_head_bn(const void* x, const void* res, const void* stat, const void* gamma,
+int mopt_resnet_head_bn(const void* x, const void* res, void* stat, const void* gamma,
                         const void* beta, const void* W, const void* b, const void* labels, int P,
                         int B, int HW, int C, int ncls, float scale, void* part, void* dz,
                         void* dW, void* db, void* loss, void* correct, void* bsums,
+                        const void* xsums, void* running, int64_t M, float eps, float momentum,
                         void* stream) {
   if (P <= 0 || B <= 0 || B % IMG || C % 8 || C < 8 || C > CMAX || ncls < 1 || ncls > NP ||
-      HW < 1 || !x || !res || !stat || !gamma || !beta || !dz || !dW || !db || !bsums)
+      HW < 1 || !x || !res || !stat || !gamma || !beta || !dz || !dW || !db || !bsums ||
+      (xsums && !running))
     return (int)hipErrorInvalidValue;
   const int cc = C / 8, nph = 16 / cc;
-  if (16 % cc || HW % (4 * nph) || HW / (4 * nph) > 8) return (int)hipErrorNotSupported;
+  if (16 % cc || HW % (HEAD_PX * nph) || HW / (4 * nph) > 8) return (int)hipErrorNotSupported;
   const hipStream_t st = (hipStream_t)stream;
-  const HeadBN bn{(const bf16_t*)res, (const float*)stat, (const bf16_t*)gamma,
-                  (const bf16_t*)beta, (float*)bsums};
+  const HeadBN bn{(const bf16_t*)res, (float*)stat, (const bf16_t*)gamma, (const bf16_t*)beta,
+                  (float*)bsums, (const float*)xsums, (float*)running, (float)M,
+                  (float)(M > 1 ? M - 1 : 1), eps, momentum};
   hipLaunchKernelGGL(head_kernel<true>, dim3(B / IMG, P), dim3(256), 0, st, (const bf16_t*)x,
                      (const bf16_t*)W, (const bf16_t*)b, (const int64_t*)labels, B, HW, C, ncls,
                      scale, 1, (float*)part, (bf16_t*)dz, bn);
