@@ -305,12 +305,12 @@ class FlatPopulation:
                           hp_dev=hp_dev)
 
     def _graph_step(self, x, y):
-        from ..ops._lib import upload_bytes
+        from ..ops._lib import upload_bytes_into
         if self._graph is None or self._gx.shape != x.shape or self._gy.shape != y.shape:
             self._capture(x, y)
         self._gx.copy_(x)
         self._gy.copy_(y)
-        self._hp_dev.copy_(upload_bytes(self.opt_hp, self.device))
+        upload_bytes_into(self._hp_dev, self.opt_hp)
         self._graph.replay()
 
     def _capture(self, x, y):

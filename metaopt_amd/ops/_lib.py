@@ -209,6 +209,18 @@ def upload_bytes(arr, device) -> torch.Tensor:
     return upload(np.ascontiguousarray(arr).view(np.uint8), device)
 
 
+def upload_bytes_into(dst: torch.Tensor, arr) -> None:
+    """``upload_bytes`` straight into the existing device buffer ``dst`` (one host -> device
+    copy, no device-side copy of a fresh tensor)."""
+    t = torch.from_numpy(np.ascontiguousarray(arr).view(np.uint8))
+    if dst.device.type != "cuda":
+        dst.copy_(t)
+        return
+    staged = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    staged.copy_(t)
+    dst.copy_(staged, non_blocking=True)
+
+
 def available() -> bool:
     """True when a GPU is visible and the kernel library loads."""
     if not torch.cuda.is_available():

@@ -428,8 +428,8 @@ class PopulationMLP:
                          cfg.seed & 0xFFFFFFFF, t)
 
     def _upload_hp(self) -> None:
-        from ._lib import upload_bytes
-        self.hp_dev.copy_(upload_bytes(self.hp, self.device))
+        from ._lib import upload_bytes_into
+        upload_bytes_into(self.hp_dev, self.hp)
 
     def set_member(self, slot: int, cfg: MemberConfig, init: bool = True) -> None:
         """Place ``cfg`` in ``slot``; with ``init`` draw fresh weights (torch.nn.Linear-style
