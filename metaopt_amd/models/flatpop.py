@@ -295,7 +295,12 @@ class FlatPopulation:
             self.g16[a:b].zero_()
         out = self._loss(x, y, train=True)
         loss = out[0] if isinstance(out, tuple) else out
-        loss.sum().backward()
+        # d(sum loss) / d loss_p = 1: a persistent ones vector (created in the eager warm-up
+        # before any graph capture) instead of loss.sum() -- no reduction and no fill per step
+        ones = getattr(self, "_loss_ones", None)
+        if ones is None or ones.shape != loss.shape or ones.device != loss.device:
+            ones = self._loss_ones = torch.ones_like(loss)
+        loss.backward(ones)
         P = self.capacity
         self.stats[:P].copy_(loss.detach())
         if isinstance(out, tuple):
